@@ -1,0 +1,195 @@
+/*
+ * lhpc.h — C ABI of the MI355X-native libHPC hot path (CSR SpMV + ghost-cell
+ * stencils).  Every entry point is `extern "C"`, takes plain pointers and
+ * sizes, and returns an `int` status:
+ *
+ *     0              success (LHPC_OK)
+ *     < 0            lhpc error (see lhpc_status below)
+ *     > 0            a wrapped hipError_t value
+ *
+ * No exception crosses this boundary.  The C++ drop-in headers
+ * (include/hpc/ and include/sparse/ headers) map a non-zero status to
+ * std::system_error, mirroring the reference's cudahelper::throwCudaError
+ * convention (reference lib/gpu/util/include/cudaHelper.cuh:10-27).
+ *
+ * What each entry point replaces in the reference
+ * ------------------------------------------------
+ * The reference (Liupeter01/libHPC) has NO CSR SpMV anywhere:
+ * the SpMV entry points below are a new operator in the reference's
+ * `sparse` namespace idiom (lib/sparse/include/RootGrid.hpp:10-22 is the
+ * existing `sparse::` API), fed by the reference's host layout contract
+ * hpc::HPCHighDimensionFlatArray<1,T> (lib/hpc/include/HPCHighDimensionFlatArray.hpp:54-57).
+ *
+ * The stencil entry points replace the 17-tap box blurs of
+ * tests/test_hpc_benchmark/test_hpc_benchmark.cpp:354-368 (x) and :444-457 (y)
+ * and their SSE twins :425-441 / :575-601, operating on the same padded
+ * row-major buffers hpc::HPCHighDimensionFlatArray<2,float,nblur> (input, `a`
+ * at :32) and <2,float> (output, `b` at :33).
+ *
+ * Threading: a plan is not thread-safe; drive it from one host thread.
+ * All compute calls are asynchronous on the given stream (`void*` is a
+ * hipStream_t; NULL = the null stream) unless a host pointer is passed, in
+ * which case the call synchronises that stream before returning.
+ */
+#ifndef LHPC_H_
+#define LHPC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LHPC_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- status */
+enum lhpc_status {
+  LHPC_OK = 0,
+  LHPC_ERR_INVALID_ARG = -1,   /* null pointer, negative size, bad enum     */
+  LHPC_ERR_BAD_CSR = -2,       /* row_ptr not monotone / col out of range   */
+  LHPC_ERR_ALLOC = -3,         /* device or host allocation failed          */
+  LHPC_ERR_NO_DEVICE = -4,     /* no usable gfx950 device                   */
+  LHPC_ERR_UNSUPPORTED = -5,   /* valid request the build does not support  */
+  LHPC_ERR_INTERNAL = -6
+};
+
+/* ----------------------------------------------------------------- dtype */
+enum lhpc_dtype { LHPC_F32 = 0, LHPC_F64 = 1 };
+
+/* --------------------------------------------------------- plan flags   */
+enum lhpc_plan_flags {
+  LHPC_PLAN_DEFAULT = 0,
+  LHPC_PLAN_VALIDATE = 1u << 0,     /* check row_ptr monotone, cols in range  */
+  LHPC_PLAN_DEVICE_INPUT = 1u << 1, /* row_ptr/col_idx/val are device ptrs    */
+  /* force a kernel family instead of the heuristic (testing / benchmarks)   */
+  LHPC_PLAN_FORCE_ROWGROUP = 1u << 4,
+  LHPC_PLAN_FORCE_ADAPTIVE = 1u << 5
+};
+
+/* kernel families a plan can select (lhpc_spmv_plan_info.kernel)          */
+enum lhpc_spmv_kernel {
+  LHPC_KERNEL_ROWGROUP = 0, /* L lanes per row, wave64 DPP reduction        */
+  LHPC_KERNEL_ADAPTIVE = 1  /* nnz-balanced row blocks + long-row split     */
+};
+
+typedef struct lhpc_spmv_plan lhpc_spmv_plan;
+
+typedef struct lhpc_spmv_plan_info {
+  int dtype;
+  int kernel;          /* enum lhpc_spmv_kernel                             */
+  int lanes_per_row;   /* ROWGROUP: L in {4,8,16,32,64}                     */
+  int rows_per_group;  /* ROWGROUP: rows per lane group per launch step     */
+  int64_t n_rows, n_cols, nnz;
+  int64_t n_blocks;    /* ADAPTIVE: row blocks                              */
+  int64_t n_long_rows; /* ADAPTIVE: rows split across workgroups            */
+  int64_t device_bytes;/* HBM held by the plan                              */
+  int device;          /* HIP device ordinal                                */
+  int launches;        /* kernel launches per lhpc_spmv call                */
+} lhpc_spmv_plan_info;
+
+/* ------------------------------------------------------------- runtime   */
+const char *lhpc_strerror(int status);
+int lhpc_abi_version(void);
+/* number of visible gfx950 devices (0 when none; never an error)          */
+int lhpc_device_count(void);
+
+/* ------------------------------------------------------------ CSR SpMV   */
+/*
+ * Create a plan for y = A·x with A an n_rows × n_cols CSR matrix.
+ *   dtype        LHPC_F32 or LHPC_F64 (type of val, x, y)
+ *   row_ptr      n_rows+1 offsets, int32 (row_ptr_bits = 32) or int64 (64)
+ *   col_idx      nnz int32 column indices in [0, n_cols)
+ *   val          nnz values of dtype
+ *   device_ids   HIP device ordinals; NULL = current device
+ *   n_devices    1 (one process drives one GPU; multi-GPU = one process
+ *                per GPU, see lhpc_csr_partition_rows)
+ * The plan COPIES A into HBM (and may re-encode it); it never retains the
+ * caller's pointers after returning.
+ */
+int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
+                          int64_t n_cols, int64_t nnz, const void *row_ptr,
+                          int row_ptr_bits, const int32_t *col_idx,
+                          const void *val, const int *device_ids,
+                          int n_devices, unsigned flags);
+/*
+ * y = A·x.  With buffers_on_device != 0, x (n_cols) and y (n_rows) are HBM
+ * pointers and the call is fully asynchronous on `stream`.  Otherwise they
+ * are host pointers: x is staged through a plan-owned HBM buffer, y copied
+ * back, and the stream synchronised before return.
+ */
+int lhpc_spmv(lhpc_spmv_plan *plan, const void *x, void *y,
+              int buffers_on_device, void *stream);
+int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *plan,
+                            lhpc_spmv_plan_info *info);
+int lhpc_spmv_plan_destroy(lhpc_spmv_plan *plan);
+
+/*
+ * nnz-balanced contiguous row split for one-process-per-GPU SpMV:
+ * cuts[0] = 0, cuts[parts] = n_rows, and cuts[p] is the smallest row r with
+ * row_ptr[r] >= ceil(p·nnz/parts) (binary search on row_ptr).  Host only.
+ */
+int lhpc_csr_partition_rows(const void *row_ptr, int row_ptr_bits,
+                            int64_t n_rows, int parts, int64_t *cuts);
+
+/* -------------------------------------------------------- stencils      */
+/*
+ * 17-tap (2·nblur+1) box blur along x of a ghost-padded 2-D grid, the
+ * reference's BM_x_blur (test_hpc_benchmark.cpp:354-368):
+ *     b(y,x) = Σ_{k=-nblur..nblur} a(y, x+k), ascending k, from 0.0f.
+ * `a` has layout HPCHighDimensionFlatArray<2,float,ghost>: physical row
+ * length nx + 2·ghost, ny + 2·ghost rows; logical (y,x) lives at
+ * (y+ghost)·(nx+2·ghost) + (x+ghost).  `b` is HPCHighDimensionFlatArray<2,float,0>
+ * (ny × nx, row-major).  Requires ghost >= nblur.
+ */
+int lhpc_blur_x_f32(const float *a, float *b, int64_t ny, int64_t nx,
+                    int64_t ghost, int nblur, int buffers_on_device,
+                    void *stream);
+/* y-direction twin: b(y,x) = Σ_k a(y+k, x) (test_hpc_benchmark.cpp:444-457) */
+int lhpc_blur_y_f32(const float *a, float *b, int64_t ny, int64_t nx,
+                    int64_t ghost, int nblur, int buffers_on_device,
+                    void *stream);
+/*
+ * 7-point 3-D stencil on HPCHighDimensionFlatArray<3,float,ghost> buffers
+ * (ghost >= 1), both u and out with the same padded layout:
+ *   out(z,y,x) = c0·u + c1·(((((u(z-1)+u(z+1)) + u(y-1)) + u(y+1)) + u(x-1)) + u(x+1))
+ * evaluated exactly in that order with c0·u and c1·(…) rounded separately
+ * (no contraction).  Only logical cells of `out` are written.
+ */
+int lhpc_stencil7_f32(const float *u, float *out, int64_t nz, int64_t ny,
+                      int64_t nx, int64_t ghost, float c0, float c1,
+                      int buffers_on_device, void *stream);
+/* same, over z-planes [z_begin, z_end) only (halo-overlap scheduling)     */
+int lhpc_stencil7_f32_planes(const float *u, float *out, int64_t nz,
+                             int64_t ny, int64_t nx, int64_t ghost, float c0,
+                             float c1, int64_t z_begin, int64_t z_end,
+                             void *stream);
+
+/* ------------------------------------------- synthetic workloads (host) */
+/*
+ * Deterministic, thread-count-independent CSR generators (splitmix64 keyed
+ * by (seed, row)), OpenMP-parallel.  See DESIGN.md §"Synthetic inputs".
+ *   uniform:   every row has exactly `per_row` distinct sorted columns.
+ *   powerlaw:  row lengths from a truncated discrete power law
+ *              P(l) ∝ l^-alpha on [lmin, lmax]; rows 0, n/2, n-1 forced to
+ *              lmax; then a seeded row shuffle.
+ *   values:    U[-1,1) (dist 0) or dyadic {k/8 : k∈[-8,8]} (dist 1).
+ * Two-phase: *_lengths fills row_ptr (n_rows+1, int64) and returns nnz in
+ * *nnz_out; *_fill then fills col_idx (and val).
+ */
+int lhpc_gen_uniform_row_ptr(int64_t n_rows, int per_row, int64_t *row_ptr);
+int lhpc_gen_powerlaw_row_ptr(int64_t n_rows, int64_t n_cols, double alpha,
+                              int64_t lmin, int64_t lmax, uint64_t seed,
+                              int64_t *row_ptr, int64_t *nnz_out);
+int lhpc_gen_fill_cols(int64_t n_rows, int64_t n_cols, const int64_t *row_ptr,
+                       uint64_t seed, int32_t *col_idx);
+int lhpc_gen_fill_values(int dtype, int dist, int64_t count, uint64_t seed,
+                         void *out);
+/* int64 → int32 row_ptr narrowing (fails with LHPC_ERR_UNSUPPORTED if nnz
+ * does not fit int32)                                                       */
+int lhpc_row_ptr_narrow(const int64_t *in, int64_t n, int32_t *out);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+#endif /* LHPC_H_ */

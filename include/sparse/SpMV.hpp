@@ -1,0 +1,90 @@
+// sparse/SpMV.hpp — y = A·x on MI355X behind the reference's host types.
+//
+//   sparse::SpMVPlan<T>  RAII owner of the HBM copy of A (one per GPU)
+//   sparse::spmv(plan, x, y)  with x, y hpc::HPCHighDimensionFlatArray<1,T,...>
+//                             (host, synchronous) or raw HBM pointers (async)
+// Forwards to the C ABI (include/lhpc.h); non-zero status → std::system_error
+// (include/lhpc_error.hpp).  The reference has no SpMV; the
+// operator and its numerics are defined in DESIGN.md.
+#pragma once
+#ifndef LHPC_SPARSE_SPMV_HPP_
+#define LHPC_SPARSE_SPMV_HPP_
+
+#include <cstdint>
+#include <type_traits>
+#include <utility>
+
+#include "../hpc/HPCHighDimensionFlatArray.hpp"
+#include "../lhpc.h"
+#include "../lhpc_error.hpp"
+#include "CSRMatrix.hpp"
+
+namespace sparse {
+
+template <typename T>
+class SpMVPlan {
+  static_assert(std::is_same_v<T, float> || std::is_same_v<T, double>, "SpMV is fp32 or fp64");
+
+ public:
+  template <typename OffsetT>
+  explicit SpMVPlan(const CSRMatrix<T, std::int32_t, OffsetT> &A, int device = -1,
+                    unsigned flags = LHPC_PLAN_DEFAULT)
+      : n_rows_(A.n_rows), n_cols_(A.n_cols) {
+    const int dev[1] = {device};
+    lhpc::checkLhpc(lhpc_spmv_plan_create(&plan_, std::is_same_v<T, float> ? LHPC_F32 : LHPC_F64,
+                                          A.n_rows, A.n_cols, A.nnz(), A.row_ptr.data(),
+                                          sizeof(OffsetT) * 8, A.col_idx.data(), A.val.data(),
+                                          device >= 0 ? dev : nullptr, device >= 0 ? 1 : 0, flags));
+  }
+  SpMVPlan(const SpMVPlan &) = delete;
+  SpMVPlan &operator=(const SpMVPlan &) = delete;
+  SpMVPlan(SpMVPlan &&o) noexcept : plan_(std::exchange(o.plan_, nullptr)), n_rows_(o.n_rows_), n_cols_(o.n_cols_) {}
+  SpMVPlan &operator=(SpMVPlan &&o) noexcept {
+    if (this != &o) {
+      reset();
+      plan_ = std::exchange(o.plan_, nullptr);
+      n_rows_ = o.n_rows_;
+      n_cols_ = o.n_cols_;
+    }
+    return *this;
+  }
+  ~SpMVPlan() { reset(); }
+
+  lhpc_spmv_plan_info info() const {
+    lhpc_spmv_plan_info i{};
+    lhpc::checkLhpc(lhpc_spmv_plan_info_get(plan_, &i));
+    return i;
+  }
+  std::int64_t rows() const noexcept { return n_rows_; }
+  std::int64_t cols() const noexcept { return n_cols_; }
+  lhpc_spmv_plan *native() noexcept { return plan_; }
+
+ private:
+  void reset() noexcept {
+    if (plan_) lhpc_spmv_plan_destroy(plan_);
+    plan_ = nullptr;
+  }
+  lhpc_spmv_plan *plan_ = nullptr;
+  std::int64_t n_rows_ = 0, n_cols_ = 0;
+};
+
+// Host vectors: the logical cells [0, n) of 1-D flat arrays (ghost cells, if
+// any, are skipped and left untouched).  Synchronous.
+template <typename T, std::size_t LX, std::size_t HX, std::size_t AX, class AlX, std::size_t LY,
+          std::size_t HY, std::size_t AY, class AlY>
+void spmv(SpMVPlan<T> &plan, const hpc::HPCHighDimensionFlatArray<1, T, LX, HX, AX, AlX> &x,
+          hpc::HPCHighDimensionFlatArray<1, T, LY, HY, AY, AlY> &y) {
+  if (static_cast<std::int64_t>(x.dims()[0]) < plan.cols() ||
+      static_cast<std::int64_t>(y.dims()[0]) < plan.rows())
+    lhpc::throwLhpcError(LHPC_ERR_INVALID_ARG, __FILE__, __LINE__);
+  lhpc::checkLhpc(lhpc_spmv(plan.native(), x.data() + LX, y.data() + LY, 0, nullptr));
+}
+
+// Device vectors (HBM pointers), asynchronous on `stream` (a hipStream_t).
+template <typename T>
+void spmv(SpMVPlan<T> &plan, const T *d_x, T *d_y, void *stream = nullptr) {
+  lhpc::checkLhpc(lhpc_spmv(plan.native(), d_x, d_y, 1, stream));
+}
+
+}  // namespace sparse
+#endif  // LHPC_SPARSE_SPMV_HPP_

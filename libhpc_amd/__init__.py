@@ -1,0 +1,336 @@
+"""libhpc_amd — MI355X-native libHPC hot path (CSR SpMV + ghost-cell stencils).
+
+Python mirror of the C ABI in ``include/lhpc.h`` (ctypes over the in-tree
+``libhpc_amd/_lib/liblhpc.so``).  The C++ drop-in surface lives in
+``include/hpc/*.hpp`` and ``include/sparse/*.hpp``; this module exists so the
+tests and ``bench.py`` drive exactly the same entry points a C++ caller would.
+
+There is deliberately no CPU fallback: if the shared library is missing this
+module raises at import, and every compute call raises ``LhpcError`` when no
+gfx950 device is present.  (The CPU restatement used as the checker lives in
+``oracle/`` and is imported only by tests and bench's ``cpu_baseline`` leg.)
+
+Reference anchors (read-only, /root/reference):
+  * layout contract: lib/hpc/include/HPCHighDimensionFlatArray.hpp:54-57, 161-187
+  * blur semantics:  tests/test_hpc_benchmark/test_hpc_benchmark.cpp:354-368, 444-457
+  * error idiom:     lib/gpu/util/include/cudaHelper.cuh:10-27 (std::system_error)
+  * SpMV: absent from the reference; defined in DESIGN.md.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+__all__ = [
+    "LhpcError", "lib", "F32", "F64", "device_count", "SpMVPlan",
+    "csr_partition_rows", "blur_x", "blur_y", "stencil7", "stencil7_planes",
+    "gen_uniform_csr", "gen_powerlaw_csr", "gen_values", "padded_shape",
+    "PLAN_VALIDATE", "PLAN_FORCE_ROWGROUP", "PLAN_FORCE_ADAPTIVE",
+    "KERNEL_ROWGROUP", "KERNEL_ADAPTIVE",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "liblhpc.so")
+
+F32, F64 = 0, 1
+PLAN_VALIDATE = 1 << 0
+PLAN_FORCE_ROWGROUP = 1 << 4
+PLAN_FORCE_ADAPTIVE = 1 << 5
+KERNEL_ROWGROUP, KERNEL_ADAPTIVE = 0, 1
+
+# every symbol include/lhpc.h declares (checked by tests/test_abi.py)
+ABI_SYMBOLS = (
+    "lhpc_strerror", "lhpc_abi_version", "lhpc_device_count",
+    "lhpc_spmv_plan_create", "lhpc_spmv", "lhpc_spmv_plan_info_get",
+    "lhpc_spmv_plan_destroy", "lhpc_csr_partition_rows",
+    "lhpc_blur_x_f32", "lhpc_blur_y_f32", "lhpc_stencil7_f32",
+    "lhpc_stencil7_f32_planes", "lhpc_gen_uniform_row_ptr",
+    "lhpc_gen_powerlaw_row_ptr", "lhpc_gen_fill_cols", "lhpc_gen_fill_values",
+    "lhpc_row_ptr_narrow",
+)
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"libhpc_amd: native library {LIB_PATH} is missing; build it with "
+        "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+
+lib = C.CDLL(LIB_PATH)
+_p, _i, _i64, _u, _u64, _f, _d = (C.c_void_p, C.c_int, C.c_int64, C.c_uint,
+                                  C.c_uint64, C.c_float, C.c_double)
+
+
+class PlanInfo(C.Structure):
+    _fields_ = [("dtype", _i), ("kernel", _i), ("lanes_per_row", _i),
+                ("rows_per_group", _i), ("n_rows", _i64), ("n_cols", _i64),
+                ("nnz", _i64), ("n_blocks", _i64), ("n_long_rows", _i64),
+                ("device_bytes", _i64), ("device", _i), ("launches", _i)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def _sig(name, res, *args):
+    fn = getattr(lib, name)
+    fn.restype = res
+    fn.argtypes = list(args)
+    return fn
+
+
+_sig("lhpc_strerror", C.c_char_p, _i)
+_sig("lhpc_abi_version", _i)
+_sig("lhpc_device_count", _i)
+_sig("lhpc_spmv_plan_create", _i, C.POINTER(_p), _i, _i64, _i64, _i64, _p, _i, _p,
+     _p, _p, _i, _u)
+_sig("lhpc_spmv", _i, _p, _p, _p, _i, _p)
+_sig("lhpc_spmv_plan_info_get", _i, _p, C.POINTER(PlanInfo))
+_sig("lhpc_spmv_plan_destroy", _i, _p)
+_sig("lhpc_csr_partition_rows", _i, _p, _i, _i64, _i, _p)
+for _n in ("lhpc_blur_x_f32", "lhpc_blur_y_f32"):
+    _sig(_n, _i, _p, _p, _i64, _i64, _i64, _i, _i, _p)
+_sig("lhpc_stencil7_f32", _i, _p, _p, _i64, _i64, _i64, _i64, _f, _f, _i, _p)
+_sig("lhpc_stencil7_f32_planes", _i, _p, _p, _i64, _i64, _i64, _i64, _f, _f, _i64,
+     _i64, _p)
+_sig("lhpc_gen_uniform_row_ptr", _i, _i64, _i, _p)
+_sig("lhpc_gen_powerlaw_row_ptr", _i, _i64, _i64, _d, _i64, _i64, _u64, _p, _p)
+_sig("lhpc_gen_fill_cols", _i, _i64, _i64, _p, _u64, _p)
+_sig("lhpc_gen_fill_values", _i, _i, _i, _i64, _u64, _p)
+_sig("lhpc_row_ptr_narrow", _i, _p, _i64, _p)
+
+
+class LhpcError(RuntimeError):
+    """Non-zero status from the C ABI (negative: lhpc, positive: hipError_t)."""
+
+    def __init__(self, status: int, where: str = ""):
+        self.status = status
+        msg = lib.lhpc_strerror(status).decode()
+        super().__init__(f"{where}: {msg} (status {status})" if where else msg)
+
+
+def _check(st: int, where: str):
+    if st != 0:
+        raise LhpcError(st, where)
+
+
+def device_count() -> int:
+    return lib.lhpc_device_count()
+
+
+# ------------------------------------------------------------ buffers
+def _is_torch(t) -> bool:
+    return type(t).__module__.startswith("torch") and hasattr(t, "data_ptr")
+
+
+def _buf(a, dtype=None, writable=False):
+    """(pointer, on_device) for a numpy array or a torch tensor."""
+    if _is_torch(a):
+        if not a.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return a.data_ptr(), bool(a.is_cuda)
+    if not isinstance(a, np.ndarray):
+        raise TypeError(f"expected numpy array or torch tensor, got {type(a)}")
+    if dtype is not None and a.dtype != dtype:
+        raise TypeError(f"expected dtype {dtype}, got {a.dtype}")
+    if not a.flags.c_contiguous or (writable and not a.flags.writeable):
+        raise ValueError("array must be C-contiguous (and writable for outputs)")
+    return a.ctypes.data, False
+
+
+def _stream_ptr(stream) -> Optional[int]:
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)  # torch.cuda.Stream
+
+
+# ------------------------------------------------------------ SpMV
+class SpMVPlan:
+    """RAII plan for y = A·x (mirrors sparse::SpMVPlan<T> in include/sparse/SpMV.hpp).
+
+    ``row_ptr`` int32/int64 (n_rows+1), ``col_idx`` int32 (nnz), ``val``
+    float32/float64 (nnz), all host numpy arrays; A is copied to HBM once.
+    """
+
+    def __init__(self, row_ptr, col_idx, val, n_cols: int, flags: int = 0,
+                 device: Optional[int] = None):
+        row_ptr = np.ascontiguousarray(row_ptr)
+        col_idx = np.ascontiguousarray(col_idx, dtype=np.int32)
+        val = np.ascontiguousarray(val)
+        if row_ptr.dtype not in (np.int32, np.int64):
+            raise TypeError("row_ptr must be int32 or int64")
+        if val.dtype == np.float32:
+            self.dtype = F32
+        elif val.dtype == np.float64:
+            self.dtype = F64
+        else:
+            raise TypeError("val must be float32 or float64")
+        self.np_dtype = val.dtype
+        self.n_rows = int(row_ptr.shape[0] - 1)
+        self.n_cols = int(n_cols)
+        self.nnz = int(col_idx.shape[0])
+        self._h = _p()
+        dev = (_i * 1)(device) if device is not None else None
+        _check(lib.lhpc_spmv_plan_create(
+            C.byref(self._h), self.dtype, self.n_rows, self.n_cols, self.nnz,
+            row_ptr.ctypes.data, 64 if row_ptr.dtype == np.int64 else 32,
+            col_idx.ctypes.data, val.ctypes.data, dev, 1 if device is not None else 0,
+            flags), "lhpc_spmv_plan_create")
+
+    def info(self) -> dict:
+        inf = PlanInfo()
+        _check(lib.lhpc_spmv_plan_info_get(self._h, C.byref(inf)), "lhpc_spmv_plan_info_get")
+        return inf.as_dict()
+
+    def __call__(self, x, y=None, stream=None):
+        """y = A·x.  numpy in → numpy out (synchronous); torch CUDA tensors →
+        asynchronous on ``stream`` (default: torch's current stream)."""
+        if y is None:
+            if _is_torch(x):
+                import torch
+                y = torch.empty(self.n_rows, dtype=x.dtype, device=x.device)
+            else:
+                y = np.empty(self.n_rows, dtype=self.np_dtype)
+        if x.shape[0] < self.n_cols or y.shape[0] < self.n_rows:
+            raise ValueError("x/y too short for the plan")
+        xp, xd = _buf(x, None if _is_torch(x) else self.np_dtype)
+        yp, yd = _buf(y, None if _is_torch(y) else self.np_dtype, writable=True)
+        if xd != yd:
+            raise ValueError("x and y must both be host or both be device buffers")
+        if xd and stream is None:
+            import torch
+            stream = torch.cuda.current_stream(y.device)
+        _check(lib.lhpc_spmv(self._h, xp, yp, int(xd), _stream_ptr(stream)), "lhpc_spmv")
+        return y
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib.lhpc_spmv_plan_destroy(self._h)
+            self._h = _p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def csr_partition_rows(row_ptr: np.ndarray, parts: int) -> np.ndarray:
+    row_ptr = np.ascontiguousarray(row_ptr)
+    cuts = np.empty(parts + 1, dtype=np.int64)
+    _check(lib.lhpc_csr_partition_rows(row_ptr.ctypes.data,
+                                       64 if row_ptr.dtype == np.int64 else 32,
+                                       row_ptr.shape[0] - 1, parts, cuts.ctypes.data),
+           "lhpc_csr_partition_rows")
+    return cuts
+
+
+# ------------------------------------------------------------ stencils
+def padded_shape(dims, ghost):
+    """Physical shape of HPCHighDimensionFlatArray<D,T,ghost> with logical dims."""
+    return tuple(int(d) + 2 * int(ghost) for d in dims)
+
+
+def _blur(fn, name, a, b, ny, nx, ghost, nblur, stream):
+    ap, ad = _buf(a, None if _is_torch(a) else np.float32)
+    bp, bd = _buf(b, None if _is_torch(b) else np.float32, writable=True)
+    if ad != bd:
+        raise ValueError("a and b must both be host or both be device buffers")
+    if ad and stream is None:
+        import torch
+        stream = torch.cuda.current_stream(b.device)
+    _check(fn(ap, bp, ny, nx, ghost, nblur, int(ad), _stream_ptr(stream)), name)
+    return b
+
+
+def blur_x(a, b, ny: int, nx: int, ghost: int, nblur: int = 8, stream=None):
+    """b(y,x) = Σ_{k=-nblur..nblur} a(y,x+k) (test_hpc_benchmark.cpp:354-368)."""
+    return _blur(lib.lhpc_blur_x_f32, "lhpc_blur_x_f32", a, b, ny, nx, ghost, nblur, stream)
+
+
+def blur_y(a, b, ny: int, nx: int, ghost: int, nblur: int = 8, stream=None):
+    """b(y,x) = Σ_{k=-nblur..nblur} a(y+k,x) (test_hpc_benchmark.cpp:444-457)."""
+    return _blur(lib.lhpc_blur_y_f32, "lhpc_blur_y_f32", a, b, ny, nx, ghost, nblur, stream)
+
+
+def stencil7(u, out, nz: int, ny: int, nx: int, ghost: int = 1, c0: float = -6.0,
+             c1: float = 1.0, stream=None):
+    up, ud = _buf(u, None if _is_torch(u) else np.float32)
+    op, od = _buf(out, None if _is_torch(out) else np.float32, writable=True)
+    if ud != od:
+        raise ValueError("u and out must both be host or both be device buffers")
+    if ud and stream is None:
+        import torch
+        stream = torch.cuda.current_stream(out.device)
+    _check(lib.lhpc_stencil7_f32(up, op, nz, ny, nx, ghost, c0, c1, int(ud),
+                                 _stream_ptr(stream)), "lhpc_stencil7_f32")
+    return out
+
+
+def stencil7_planes(u, out, nz, ny, nx, ghost, c0, c1, z_begin, z_end, stream=None):
+    up, ud = _buf(u)
+    op, od = _buf(out, writable=True)
+    if not (ud and od):
+        raise ValueError("stencil7_planes takes device tensors")
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream(out.device)
+    _check(lib.lhpc_stencil7_f32_planes(up, op, nz, ny, nx, ghost, c0, c1, z_begin, z_end,
+                                        _stream_ptr(stream)), "lhpc_stencil7_f32_planes")
+    return out
+
+
+# ------------------------------------------------------------ workloads
+SEED_A = 0x5EED0001   # matrix columns / values
+SEED_X = 0x5EED0002   # x vector
+
+
+def gen_values(dtype, dist: int, count: int, seed: int) -> np.ndarray:
+    npd = np.float32 if dtype in (F32, np.float32) else np.float64
+    out = np.empty(count, dtype=npd)
+    _check(lib.lhpc_gen_fill_values(F32 if npd == np.float32 else F64, dist, count, seed,
+                                    out.ctypes.data), "lhpc_gen_fill_values")
+    return out
+
+
+def _finish_csr(row_ptr64, n_rows, n_cols, seed, dtype, dist, narrow):
+    nnz = int(row_ptr64[-1])
+    col = np.empty(nnz, dtype=np.int32)
+    _check(lib.lhpc_gen_fill_cols(n_rows, n_cols, row_ptr64.ctypes.data, seed,
+                                  col.ctypes.data), "lhpc_gen_fill_cols")
+    val = gen_values(dtype, dist, nnz, seed ^ 0xA5A5)
+    rp = row_ptr64
+    if narrow and nnz <= np.iinfo(np.int32).max:
+        rp = np.empty(n_rows + 1, dtype=np.int32)
+        _check(lib.lhpc_row_ptr_narrow(row_ptr64.ctypes.data, n_rows + 1, rp.ctypes.data),
+               "lhpc_row_ptr_narrow")
+    return rp, col, val
+
+
+def gen_uniform_csr(n_rows: int, n_cols: int, per_row: int, dtype=F32, dist: int = 0,
+                    seed: int = SEED_A, narrow: bool = True):
+    """Every row: exactly ``per_row`` distinct uniform sorted columns."""
+    rp = np.empty(n_rows + 1, dtype=np.int64)
+    _check(lib.lhpc_gen_uniform_row_ptr(n_rows, per_row, rp.ctypes.data),
+           "lhpc_gen_uniform_row_ptr")
+    return _finish_csr(rp, n_rows, n_cols, seed, dtype, dist, narrow)
+
+
+def gen_powerlaw_csr(n_rows: int, n_cols: int, alpha: float = 1.792, lmin: int = 1,
+                     lmax: int = 10_000, dtype=F32, dist: int = 0, seed: int = SEED_A,
+                     narrow: bool = True):
+    """Row lengths ~ l^-alpha on [lmin,lmax]; rows 0, n/2, n-1 forced to lmax."""
+    rp = np.empty(n_rows + 1, dtype=np.int64)
+    nnz = C.c_int64()
+    _check(lib.lhpc_gen_powerlaw_row_ptr(n_rows, n_cols, alpha, lmin, lmax, seed ^ 0x1111,
+                                         rp.ctypes.data, C.byref(nnz)),
+           "lhpc_gen_powerlaw_row_ptr")
+    return _finish_csr(rp, n_rows, n_cols, seed, dtype, dist, narrow)

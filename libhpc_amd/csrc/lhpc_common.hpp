@@ -1,0 +1,109 @@
+// lhpc_common.hpp — shared HIP helpers for the gfx950 kernels and the C ABI.
+//
+// Error convention (include/lhpc.h): 0 ok, < 0 lhpc error, > 0 hipError_t.
+// The reference checks every CUDA call with cudahelper::checkCuda and throws
+// (lib/gpu/util/include/cudaHelper.cuh:96-101); across a C ABI we return the
+// code instead and let the C++ wrapper throw.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/lhpc.h"
+
+#define LHPC_HIP_TRY(expr)                                                     \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) return static_cast<int>(_e);                         \
+  } while (0)
+
+#define LHPC_TRY(expr)                                                         \
+  do {                                                                         \
+    int _s = (expr);                                                           \
+    if (_s != LHPC_OK) return _s;                                              \
+  } while (0)
+
+namespace lhpc {
+
+constexpr int kWave = 64;  // CDNA wavefront; never 32
+
+// Native clang vector types: the nontemporal builtins (global_load ... nt)
+// accept these, not HIP_vector_type.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Debug builds check every launch synchronously, the way the reference does
+// under #ifndef NDEBUG (lib/gpu/radix_gpu/src/cuda_radix_sort_v4.cu:104-107).
+inline int check_launch(hipStream_t s) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return static_cast<int>(e);
+#ifdef LHPC_DEBUG_SYNC
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return static_cast<int>(e);
+#else
+  (void)s;
+#endif
+  return LHPC_OK;
+}
+
+// ------------------------------------------------------------ DPP helpers
+// DPP control words (GFX9 encoding).  quad_perm[a,b,c,d] = a|b<<2|c<<4|d<<6.
+enum : int {
+  kDppQuadXor1 = 0xB1,     // quad_perm [1,0,3,2]
+  kDppQuadXor2 = 0x4E,     // quad_perm [2,3,0,1]
+  kDppRowHalfMirror = 0x141,
+  kDppRowMirror = 0x140,
+};
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                         0xF, 0xF, false));
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(u), CTRL, 0xF,
+                                             0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(
+      0, static_cast<int>(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(
+      double, (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) |
+                  static_cast<uint32_t>(lo));
+}
+
+template <typename A, int CTRL>
+__device__ __forceinline__ A dpp(A v) {
+  if constexpr (sizeof(A) == 8)
+    return dpp_f64<CTRL>(v);
+  else
+    return dpp_f32<CTRL>(v);
+}
+
+// Butterfly sum over aligned groups of L lanes; every lane of the group ends
+// with the same, order-fixed sum (fp add is commutative, so a+b == b+a
+// bit-for-bit and the tree is identical in every lane).  L <= 16 stays inside
+// one DPP row (no LDS traffic); 32 and 64 add ds_swizzle-free bpermutes.
+template <int L, typename A>
+__device__ __forceinline__ A group_sum(A v) {
+  static_assert(L == 1 || L == 2 || L == 4 || L == 8 || L == 16 || L == 32 ||
+                    L == 64,
+                "lanes per row must be a power of two <= 64");
+  if constexpr (L >= 2) v += dpp<A, kDppQuadXor1>(v);
+  if constexpr (L >= 4) v += dpp<A, kDppQuadXor2>(v);
+  if constexpr (L >= 8) v += dpp<A, kDppRowHalfMirror>(v);
+  if constexpr (L >= 16) v += dpp<A, kDppRowMirror>(v);
+  if constexpr (L >= 32) v += __shfl_xor(v, 16, 64);
+  if constexpr (L >= 64) v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T *p) {
+  return __builtin_nontemporal_load(p);
+}
+
+}  // namespace lhpc

@@ -1,0 +1,121 @@
+// lhpc_probe.hip — attainable-rate probes used by bench.py / DESIGN.md to
+// place the SpMV and stencil kernels against measured ceilings (not part of
+// the include/lhpc.h ABI).  The reference's own probe of this kind is the
+// coalescing micro-benchmark lib/gpu/stall_lg_testsuite/src/cuda_tut_stall_lg.cu:63-71
+// (int4-wide copy); these are written for wave64 / gfx950.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+__global__ __launch_bounds__(256) void k_copy16(const f32x4 *__restrict__ s, f32x4 *__restrict__ d,
+                                               int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+}
+
+__global__ __launch_bounds__(256) void k_read16(const f32x4 *__restrict__ s, float *__restrict__ sink,
+                                               int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  float acc = 0.f;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride) {
+    const f32x4 v = __builtin_nontemporal_load(s + i);
+    acc += v[0] + v[1] + v[2] + v[3];
+  }
+  if (acc == 12345.678f) sink[0] = acc;  // keep the loads alive
+}
+
+// out[i] = table[idx[i]]: a 4-byte random gather per lane with the index
+// stream read non-temporally (the SpMV x-gather in isolation).
+template <int U>
+__global__ __launch_bounds__(256) void k_gather(const int32_t *__restrict__ idx,
+                                               const float *__restrict__ table,
+                                               float *__restrict__ out, int64_t n) {
+  const int64_t base = (static_cast<int64_t>(blockIdx.x) * 256 * U) + threadIdx.x;
+  int32_t c[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    c[u] = i < n ? __builtin_nontemporal_load(idx + i) : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    if (c[u] >= 0) __builtin_nontemporal_store(table[c[u]], out + i);
+  }
+}
+
+// Column-sliced variant: block b gathers only from slice sl(b) of the table,
+// idx holds offsets within a slice.  S <= 8: sl = b % S (one slice per XCD
+// group).  S = 16: XCD group k = b % 8 does slice k for its first half of
+// blocks, then slice k + 8.
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_gather_sliced(const int32_t *__restrict__ idx,
+                                                      const float *__restrict__ table,
+                                                      float *__restrict__ out, int64_t n,
+                                                      int S, int64_t slice_len) {
+  const int64_t b = blockIdx.x;
+  int sl;
+  if (S <= 8) {
+    sl = static_cast<int>(b % S);
+  } else {
+    const int64_t per = (static_cast<int64_t>(gridDim.x) + 7) / 8;
+    sl = static_cast<int>(b % 8) + 8 * static_cast<int>((b / 8) * 2 / per);
+  }
+  const float *tb = table + sl * slice_len;
+  const int64_t base = (b * 256 * U) + threadIdx.x;
+  int32_t c[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    c[u] = i < n ? __builtin_nontemporal_load(idx + i) : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    if (c[u] >= 0) {
+      const float v = NT ? __builtin_nontemporal_load(tb + c[u]) : tb[c[u]];
+      __builtin_nontemporal_store(v, out + i);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int lhpc_probe_gather_sliced(const int32_t *idx, const float *table, float *out,
+                                        int64_t n, int S, int64_t slice_len, int nt, void *stream) {
+  constexpr int U = 8;
+  const int64_t blocks = (n + 256 * U - 1) / (256 * U);
+  if (nt)
+    hipLaunchKernelGGL((k_gather_sliced<U, true>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), idx, table, out, n, S, slice_len);
+  else
+    hipLaunchKernelGGL((k_gather_sliced<U, false>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), idx, table, out, n, S, slice_len);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int lhpc_probe_copy(const void *src, void *dst, int64_t bytes, int grid, void *stream) {
+  hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const f32x4 *>(src), static_cast<f32x4 *>(dst), bytes / 16);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int lhpc_probe_read(const void *src, void *sink, int64_t bytes, int grid, void *stream) {
+  hipLaunchKernelGGL(k_read16, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const f32x4 *>(src), static_cast<float *>(sink), bytes / 16);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int lhpc_probe_gather(const int32_t *idx, const float *table, float *out, int64_t n,
+                                 void *stream) {
+  constexpr int U = 8;
+  const int64_t blocks = (n + 256 * U - 1) / (256 * U);
+  hipLaunchKernelGGL((k_gather<U>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), idx, table, out, n);
+  return static_cast<int>(hipGetLastError());
+}

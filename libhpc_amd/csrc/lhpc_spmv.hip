@@ -1,0 +1,475 @@
+// lhpc_spmv.hip — CSR SpMV y = A·x for gfx950 (MI355X), behind include/lhpc.h.
+//
+// The reference has no SpMV; the operator is defined
+// here as y[i] = Σ_{k=row_ptr[i]}^{row_ptr[i+1]-1} val[k]·x[col_idx[k]].
+// Numerics: every dtype accumulates in fp64 registers and rounds once at the
+// store (SURVEY §8c "binding recommendation"), so fp32 results are within
+// 2^-24·|y| + ~1e-16·Σ|a·x| of the exact sum for any row length.
+//
+// Kernel families:
+//   ROWGROUP  L lanes per row (L | 64), R rows per lane group per wave, all
+//             loads hoisted so a wave keeps R gathers + R val/col loads in
+//             flight; the row sum is a DPP butterfly inside one 16-lane DPP
+//             row for L <= 16 (no LDS), then one coalesced y store per wave.
+//   ADAPTIVE  nnz-balanced row blocks: a 256-thread workgroup streams up to
+//             kBlockNnz contiguous nonzeros (coalesced), stages fp64 products
+//             in LDS, and reduces each row with L = 256/rows lanes; a row
+//             longer than kBlockNnz gets a workgroup to itself.  For skewed
+//             (power-law) row lengths.  Deterministic: fixed trees only.
+// Both read val/col_idx with non-temporal loads (streamed once) so the
+// gathered x keeps its place in L2 / Infinity Cache.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "lhpc_common.hpp"
+
+namespace lhpc {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kBlockNnz = 2048;  // ADAPTIVE: nonzeros per stream block
+
+// ------------------------------------------------------------- ROWGROUP
+template <typename T, typename I, int L, int R>
+__global__ __launch_bounds__(kBlock) void k_spmv_rowgroup(
+    const I *__restrict__ row_ptr, const int32_t *__restrict__ col,
+    const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y,
+    int64_t n_rows) {
+  constexpr int G = kWave / L;     // lane groups (rows) per wave per step
+  constexpr int WR = G * R;        // rows per wave
+  static_assert(WR <= kWave, "one y store per wave");
+  const int lane = threadIdx.x & (kWave - 1);
+  const int sub = lane & (L - 1);  // lane within its group
+  const int grp = lane / L;        // group within the wave
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t row0 = wave * WR;
+  if (row0 >= n_rows) return;  // wave-uniform
+
+  int64_t s[R], e[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = row0 + r * G + grp;
+    if (row < n_rows) {
+      s[r] = row_ptr[row];
+      e[r] = row_ptr[row + 1];
+    } else {
+      s[r] = e[r] = 0;
+    }
+  }
+  // first L-wide chunk of every row, loads hoisted for memory-level parallelism
+  int32_t c[R];
+  T v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t k = s[r] + sub;
+    c[r] = -1;
+    v[r] = T(0);
+    if (k < e[r]) {
+      c[r] = ld_stream(col + k);
+      v[r] = ld_stream(val + k);
+    }
+  }
+  double acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    acc[r] = 0.0;
+    if (c[r] >= 0) acc[r] = static_cast<double>(v[r]) * static_cast<double>(x[c[r]]);
+  }
+  // rows longer than L (rare for the uniform workload)
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    for (int64_t k = s[r] + sub + L; k < e[r]; k += L)
+      acc[r] += static_cast<double>(ld_stream(val + k)) *
+                static_cast<double>(x[ld_stream(col + k)]);
+  }
+  // all 64 lanes active here: DPP reads never see a disabled source lane
+  T out = T(0);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const T tot = static_cast<T>(group_sum<L>(acc[r]));
+    // lane l (< WR) stores row row0 + l = row0 + (l/G)*G + l%G: take the
+    // sum of step r = l/G from group g = l%G
+    const T mine = __shfl(tot, (lane % G) * L, kWave);
+    if (lane / G == r) out = mine;
+  }
+  if (lane < WR && row0 + lane < n_rows) __builtin_nontemporal_store(out, y + row0 + lane);
+}
+
+// ------------------------------------------------------------- ADAPTIVE
+// blocks[b] = first row of block b; blocks[n_blocks] = n_rows.
+template <typename T, typename I>
+__global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
+    const I *__restrict__ row_ptr, const int32_t *__restrict__ col,
+    const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y,
+    const int64_t *__restrict__ blocks) {
+  __shared__ double prod[kBlockNnz];
+  __shared__ double wsum[kBlock / kWave];
+  const int tid = threadIdx.x;
+  const int64_t r0 = blocks[blockIdx.x];
+  const int64_t r1 = blocks[blockIdx.x + 1];
+  const int64_t base = row_ptr[r0];
+  const int64_t cnt = static_cast<int64_t>(row_ptr[r1]) - base;
+  const int64_t nrows = r1 - r0;
+
+  if (cnt > kBlockNnz) {
+    // one long row: strided per-thread sums, then a fixed block tree
+    double a = 0.0;
+    for (int64_t k = tid; k < cnt; k += kBlock)
+      a += static_cast<double>(ld_stream(val + base + k)) *
+           static_cast<double>(x[ld_stream(col + base + k)]);
+    a = group_sum<kWave>(a);
+    if ((tid & (kWave - 1)) == 0) wsum[tid / kWave] = a;
+    __syncthreads();
+    if (tid == 0) {
+      double t = wsum[0];
+#pragma unroll
+      for (int w = 1; w < kBlock / kWave; ++w) t += wsum[w];
+      y[r0] = static_cast<T>(t);
+    }
+    return;
+  }
+  // stream phase: every thread products kBlockNnz/kBlock nonzeros
+  constexpr int PER = kBlockNnz / kBlock;
+  int32_t c[PER];
+  T v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int64_t k = i * kBlock + tid;
+    c[i] = -1;
+    v[i] = T(0);
+    if (k < cnt) {
+      c[i] = ld_stream(col + base + k);
+      v[i] = ld_stream(val + base + k);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = i * kBlock + tid;
+    if (c[i] >= 0) prod[k] = static_cast<double>(v[i]) * static_cast<double>(x[c[i]]);
+  }
+  __syncthreads();
+  // reduce: L lanes per row, L = largest power of two with nrows*L <= 256
+  int L = kWave;
+  while (L > 1 && nrows * L > kBlock) L >>= 1;
+  const int grp = tid / L, sub = tid & (L - 1);
+  double a = 0.0;
+  int64_t rs = 0, re = 0;
+  if (grp < nrows) {
+    rs = static_cast<int64_t>(row_ptr[r0 + grp]) - base;
+    re = static_cast<int64_t>(row_ptr[r0 + grp + 1]) - base;
+    for (int64_t k = rs + sub; k < re; k += L) a += prod[k];
+  }
+  switch (L) {  // block-uniform
+    case 64: a = group_sum<64>(a); break;
+    case 32: a = group_sum<32>(a); break;
+    case 16: a = group_sum<16>(a); break;
+    case 8: a = group_sum<8>(a); break;
+    case 4: a = group_sum<4>(a); break;
+    case 2: a = group_sum<2>(a); break;
+    default: break;
+  }
+  if (grp < nrows && sub == 0) y[r0 + grp] = static_cast<T>(a);
+}
+
+// ------------------------------------------------------------- host side
+bool is_gfx950(int dev) {
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, dev) != hipSuccess) return false;
+  return std::strncmp(p.gcnArchName, "gfx950", 6) == 0;
+}
+
+}  // namespace
+}  // namespace lhpc
+
+using namespace lhpc;
+
+struct lhpc_spmv_plan {
+  int dtype = LHPC_F32;
+  int device = 0;
+  int rp64 = 0;  // device row_ptr is int64
+  int64_t n_rows = 0, n_cols = 0, nnz = 0;
+  void *d_row_ptr = nullptr;
+  int32_t *d_col = nullptr;
+  void *d_val = nullptr;
+  int64_t *d_blocks = nullptr;
+  int64_t n_blocks = 0, n_long = 0;
+  void *d_xstage = nullptr, *d_ystage = nullptr;
+  int kernel = LHPC_KERNEL_ROWGROUP;
+  int L = 16, R = 4;
+  int64_t bytes = 0;
+};
+
+namespace {
+
+int dmalloc(void **p, size_t n, int64_t &acct) {
+  if (n == 0) n = 16;
+  hipError_t e = hipMalloc(p, n);
+  if (e == hipErrorOutOfMemory) return LHPC_ERR_ALLOC;
+  if (e != hipSuccess) return static_cast<int>(e);
+  acct += static_cast<int64_t>(n);
+  return LHPC_OK;
+}
+
+template <typename T, typename I, int L, int R>
+int launch_rowgroup_t(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  constexpr int WR = (kWave / L) * R;
+  const int64_t waves = (p->n_rows + WR - 1) / WR;
+  const int64_t blocks = (waves * kWave + kBlock - 1) / kBlock;
+  if (blocks == 0) return LHPC_OK;
+  hipLaunchKernelGGL((k_spmv_rowgroup<T, I, L, R>), dim3(static_cast<unsigned>(blocks)),
+                     dim3(kBlock), 0, s, static_cast<const I *>(p->d_row_ptr), p->d_col,
+                     static_cast<const T *>(p->d_val), static_cast<const T *>(x),
+                     static_cast<T *>(y), p->n_rows);
+  return check_launch(s);
+}
+
+template <typename T, typename I>
+int launch_rowgroup(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  switch (p->L * 100 + p->R) {
+    case 401: return launch_rowgroup_t<T, I, 4, 1>(p, x, y, s);
+    case 802: return launch_rowgroup_t<T, I, 8, 2>(p, x, y, s);
+    case 804: return launch_rowgroup_t<T, I, 8, 4>(p, x, y, s);
+    case 1601: return launch_rowgroup_t<T, I, 16, 1>(p, x, y, s);
+    case 1602: return launch_rowgroup_t<T, I, 16, 2>(p, x, y, s);
+    case 1604: return launch_rowgroup_t<T, I, 16, 4>(p, x, y, s);
+    case 1608: return launch_rowgroup_t<T, I, 16, 8>(p, x, y, s);
+    case 3201: return launch_rowgroup_t<T, I, 32, 1>(p, x, y, s);
+    case 3202: return launch_rowgroup_t<T, I, 32, 2>(p, x, y, s);
+    case 6401: return launch_rowgroup_t<T, I, 64, 1>(p, x, y, s);
+    default: return LHPC_ERR_UNSUPPORTED;
+  }
+}
+
+template <typename T, typename I>
+int launch_adaptive(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  if (p->n_blocks == 0) return LHPC_OK;
+  hipLaunchKernelGGL((k_spmv_adaptive<T, I>), dim3(static_cast<unsigned>(p->n_blocks)),
+                     dim3(kBlock), 0, s, static_cast<const I *>(p->d_row_ptr), p->d_col,
+                     static_cast<const T *>(p->d_val), static_cast<const T *>(x),
+                     static_cast<T *>(y), p->d_blocks);
+  return check_launch(s);
+}
+
+template <typename T>
+int launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  if (p->kernel == LHPC_KERNEL_ADAPTIVE)
+    return p->rp64 ? launch_adaptive<T, int64_t>(p, x, y, s)
+                   : launch_adaptive<T, int32_t>(p, x, y, s);
+  return p->rp64 ? launch_rowgroup<T, int64_t>(p, x, y, s)
+                 : launch_rowgroup<T, int32_t>(p, x, y, s);
+}
+
+// Host view of row_ptr regardless of width.
+struct RowPtrView {
+  const void *p;
+  int bits;
+  int64_t operator[](int64_t i) const {
+    return bits == 64 ? static_cast<const int64_t *>(p)[i]
+                      : static_cast<const int32_t *>(p)[i];
+  }
+};
+
+// Row blocks for ADAPTIVE: greedy, each block <= kBlockNnz nonzeros and
+// <= kBlock rows, or a single row of any length.
+std::vector<int64_t> build_blocks(RowPtrView rp, int64_t n_rows, int64_t &n_long) {
+  std::vector<int64_t> b;
+  b.reserve(static_cast<size_t>(n_rows / 64 + 2));
+  n_long = 0;
+  int64_t r = 0;
+  while (r < n_rows) {
+    b.push_back(r);
+    const int64_t start = rp[r];
+    if (rp[r + 1] - start > kBlockNnz) {
+      ++n_long;
+      ++r;
+      continue;
+    }
+    int64_t end = r + 1;
+    while (end < n_rows && end - r < kBlock && rp[end + 1] - start <= kBlockNnz) ++end;
+    r = end;
+  }
+  b.push_back(n_rows);
+  return b;
+}
+
+}  // namespace
+
+extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
+                                     int64_t n_cols, int64_t nnz, const void *row_ptr,
+                                     int row_ptr_bits, const int32_t *col_idx,
+                                     const void *val, const int *device_ids,
+                                     int n_devices, unsigned flags) {
+  if (!out) return LHPC_ERR_INVALID_ARG;
+  *out = nullptr;
+  if ((dtype != LHPC_F32 && dtype != LHPC_F64) || n_rows < 0 || n_cols < 0 || nnz < 0 ||
+      !row_ptr || (row_ptr_bits != 32 && row_ptr_bits != 64) || n_cols > INT32_MAX ||
+      (nnz > 0 && (!col_idx || !val)))
+    return LHPC_ERR_INVALID_ARG;
+  if (n_devices > 1) return LHPC_ERR_UNSUPPORTED;  // one process per GPU
+  if (flags & LHPC_PLAN_DEVICE_INPUT) return LHPC_ERR_UNSUPPORTED;
+  if (row_ptr_bits == 32 && nnz > INT32_MAX) return LHPC_ERR_INVALID_ARG;
+
+  const RowPtrView rp{row_ptr, row_ptr_bits};
+  if (rp[0] != 0 || rp[n_rows] != nnz) return LHPC_ERR_BAD_CSR;
+  if (flags & LHPC_PLAN_VALIDATE) {
+    for (int64_t i = 0; i < n_rows; ++i)
+      if (rp[i + 1] < rp[i]) return LHPC_ERR_BAD_CSR;
+    for (int64_t k = 0; k < nnz; ++k)
+      if (col_idx[k] < 0 || col_idx[k] >= n_cols) return LHPC_ERR_BAD_CSR;
+  }
+
+  int dev = 0;
+  if (device_ids && n_devices == 1) {
+    dev = device_ids[0];
+    LHPC_HIP_TRY(hipSetDevice(dev));
+  } else {
+    LHPC_HIP_TRY(hipGetDevice(&dev));
+  }
+  if (!is_gfx950(dev)) return LHPC_ERR_NO_DEVICE;
+
+  auto *p = new (std::nothrow) lhpc_spmv_plan();
+  if (!p) return LHPC_ERR_ALLOC;
+  p->dtype = dtype;
+  p->device = dev;
+  p->n_rows = n_rows;
+  p->n_cols = n_cols;
+  p->nnz = nnz;
+  // int32 offsets whenever they fit: 4 B/row less HBM traffic
+  p->rp64 = nnz > INT32_MAX ? 1 : 0;
+  const size_t tsz = dtype == LHPC_F32 ? 4 : 8;
+
+  // ---- kernel selection from row-length statistics
+  int64_t maxlen = 0;
+  double sum2 = 0;
+  for (int64_t i = 0; i < n_rows; ++i) {
+    const int64_t l = rp[i + 1] - rp[i];
+    maxlen = std::max(maxlen, l);
+    sum2 += static_cast<double>(l) * static_cast<double>(l);
+  }
+  const double mean = n_rows ? static_cast<double>(nnz) / static_cast<double>(n_rows) : 0;
+  const double var = n_rows ? sum2 / static_cast<double>(n_rows) - mean * mean : 0;
+  const double cv = mean > 0 ? std::sqrt(std::max(var, 0.0)) / mean : 0;
+  bool adaptive = (cv > 1.0 && maxlen > 256) || maxlen > 4096;
+  if (flags & LHPC_PLAN_FORCE_ROWGROUP) adaptive = false;
+  if (flags & LHPC_PLAN_FORCE_ADAPTIVE) adaptive = true;
+  if (adaptive) {
+    p->kernel = LHPC_KERNEL_ADAPTIVE;
+  } else {
+    p->kernel = LHPC_KERNEL_ROWGROUP;
+    int L = 4;
+    while (L < 64 && L < mean) L <<= 1;
+    p->L = L;
+    p->R = L <= 16 ? 4 : (L == 32 ? 2 : 1);
+    if (L == 4) p->R = 1;
+  }
+  if (const char *env = std::getenv("LHPC_SPMV_ROWGROUP")) {  // "L,R" bench knob
+    int L = 0, R = 0;
+    if (std::sscanf(env, "%d,%d", &L, &R) == 2 && p->kernel == LHPC_KERNEL_ROWGROUP) {
+      p->L = L;
+      p->R = R;
+    }
+  }
+
+  int st = LHPC_OK;
+  do {
+    const size_t rp_bytes = static_cast<size_t>(n_rows + 1) * (p->rp64 ? 8 : 4);
+    if ((st = dmalloc(&p->d_row_ptr, rp_bytes, p->bytes))) break;
+    if ((st = dmalloc(reinterpret_cast<void **>(&p->d_col), static_cast<size_t>(nnz) * 4,
+                      p->bytes)))
+      break;
+    if ((st = dmalloc(&p->d_val, static_cast<size_t>(nnz) * tsz, p->bytes))) break;
+    // row_ptr in the device width
+    if (p->rp64 == (row_ptr_bits == 64 ? 1 : 0)) {
+      if ((st = static_cast<int>(hipMemcpy(p->d_row_ptr, row_ptr, rp_bytes, hipMemcpyHostToDevice))))
+        break;
+    } else {
+      std::vector<int32_t> tmp(static_cast<size_t>(n_rows + 1));
+      for (int64_t i = 0; i <= n_rows; ++i) tmp[static_cast<size_t>(i)] = static_cast<int32_t>(rp[i]);
+      if ((st = static_cast<int>(hipMemcpy(p->d_row_ptr, tmp.data(), rp_bytes, hipMemcpyHostToDevice))))
+        break;
+    }
+    if (nnz) {
+      if ((st = static_cast<int>(hipMemcpy(p->d_col, col_idx, static_cast<size_t>(nnz) * 4,
+                                           hipMemcpyHostToDevice))))
+        break;
+      if ((st = static_cast<int>(hipMemcpy(p->d_val, val, static_cast<size_t>(nnz) * tsz,
+                                           hipMemcpyHostToDevice))))
+        break;
+    }
+    if (p->kernel == LHPC_KERNEL_ADAPTIVE) {
+      std::vector<int64_t> b = build_blocks(rp, n_rows, p->n_long);
+      p->n_blocks = static_cast<int64_t>(b.size()) - 1;
+      if ((st = dmalloc(reinterpret_cast<void **>(&p->d_blocks), b.size() * 8, p->bytes))) break;
+      if ((st = static_cast<int>(hipMemcpy(p->d_blocks, b.data(), b.size() * 8, hipMemcpyHostToDevice))))
+        break;
+    }
+  } while (false);
+  if (st != LHPC_OK) {
+    lhpc_spmv_plan_destroy(p);
+    return st;
+  }
+  *out = p;
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_spmv(lhpc_spmv_plan *p, const void *x, void *y, int on_device,
+                         void *stream) {
+  if (!p || (p->n_cols > 0 && !x) || (p->n_rows > 0 && !y)) return LHPC_ERR_INVALID_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  LHPC_HIP_TRY(hipSetDevice(p->device));
+  const size_t tsz = p->dtype == LHPC_F32 ? 4 : 8;
+  const void *dx = x;
+  void *dy = y;
+  if (!on_device) {
+    if (!p->d_xstage) {
+      LHPC_TRY(dmalloc(&p->d_xstage, static_cast<size_t>(p->n_cols) * tsz, p->bytes));
+      LHPC_TRY(dmalloc(&p->d_ystage, static_cast<size_t>(p->n_rows) * tsz, p->bytes));
+    }
+    LHPC_HIP_TRY(hipMemcpyAsync(p->d_xstage, x, static_cast<size_t>(p->n_cols) * tsz,
+                                hipMemcpyHostToDevice, s));
+    dx = p->d_xstage;
+    dy = p->d_ystage;
+  }
+  const int st = p->dtype == LHPC_F32 ? launch<float>(p, dx, dy, s) : launch<double>(p, dx, dy, s);
+  if (st != LHPC_OK) return st;
+  if (!on_device) {
+    LHPC_HIP_TRY(hipMemcpyAsync(y, p->d_ystage, static_cast<size_t>(p->n_rows) * tsz,
+                                hipMemcpyDeviceToHost, s));
+    LHPC_HIP_TRY(hipStreamSynchronize(s));
+  }
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *p, lhpc_spmv_plan_info *info) {
+  if (!p || !info) return LHPC_ERR_INVALID_ARG;
+  info->dtype = p->dtype;
+  info->kernel = p->kernel;
+  info->lanes_per_row = p->kernel == LHPC_KERNEL_ROWGROUP ? p->L : 0;
+  info->rows_per_group = p->kernel == LHPC_KERNEL_ROWGROUP ? p->R : 0;
+  info->n_rows = p->n_rows;
+  info->n_cols = p->n_cols;
+  info->nnz = p->nnz;
+  info->n_blocks = p->n_blocks;
+  info->n_long_rows = p->n_long;
+  info->device_bytes = p->bytes;
+  info->device = p->device;
+  info->launches = 1;
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
+  if (!p) return LHPC_OK;
+  (void)hipSetDevice(p->device);
+  for (void *q : {p->d_row_ptr, static_cast<void *>(p->d_col), p->d_val,
+                  static_cast<void *>(p->d_blocks), p->d_xstage, p->d_ystage})
+    if (q) (void)hipFree(q);
+  delete p;
+  return LHPC_OK;
+}

@@ -1,0 +1,119 @@
+"""Test helpers: the oracle (CPU restatement, oracle/oracle.c) via ctypes and
+numpy-facing wrappers.  Test infrastructure only."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+REF_PROBE = os.path.join(ROOT, "oracle", "_ref", "ref_probe")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+_p, _i, _i64, _f = C.c_void_p, C.c_int, C.c_int64, C.c_float
+_lib = None
+
+
+def load_oracle():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "_build/liboracle.so"],
+                           check=True, capture_output=True)
+        lib = C.CDLL(ORACLE_SO)
+        lib.oracle_spmv_f32.argtypes = [_i64, _p, _i, _p, _p, _p, _p, _p, _p]
+        lib.oracle_spmv_f64.argtypes = [_i64, _p, _i, _p, _p, _p, _p, _p]
+        lib.cpu_spmv_simd.argtypes = [_i, _i64, _p, _i, _p, _p, _p, _p, _i]
+        lib.cpu_spmv_simd.restype = _i
+        lib.oracle_blur_x.argtypes = [_p, _p, _i64, _i64, _i64, _i]
+        lib.oracle_blur_y.argtypes = [_p, _p, _i64, _i64, _i64, _i]
+        lib.cpu_blur_x_sse.argtypes = [_p, _p, _i64, _i64, _i64, _i]
+        lib.cpu_blur_y_sse.argtypes = [_p, _p, _i64, _i64, _i64, _i]
+        lib.cpu_blur_x_sse.restype = _i
+        lib.cpu_blur_y_sse.restype = _i
+        lib.oracle_stencil7.argtypes = [_p, _p, _i64, _i64, _i64, _i64, _f, _f, _i]
+        _lib = lib
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data if a is not None else None
+
+
+def _bits(rp):
+    return 64 if rp.dtype == np.int64 else 32
+
+
+def spmv_oracle(rp, col, val, x):
+    """(y64, y_rounded, abs_sum): fp64 sequential ascending-k sums."""
+    lib = load_oracle()
+    n = rp.shape[0] - 1
+    y64 = np.empty(n, dtype=np.float64)
+    asum = np.empty(n, dtype=np.float64)
+    if val.dtype == np.float32:
+        y32 = np.empty(n, dtype=np.float32)
+        lib.oracle_spmv_f32(n, _ptr(rp), _bits(rp), _ptr(col), _ptr(val), _ptr(x), _ptr(y64),
+                            _ptr(y32), _ptr(asum))
+        return y64, y32, asum
+    lib.oracle_spmv_f64(n, _ptr(rp), _bits(rp), _ptr(col), _ptr(val), _ptr(x), _ptr(y64), _ptr(asum))
+    return y64, y64.copy(), asum
+
+
+def spmv_cpu_simd(rp, col, val, x, threads=0):
+    lib = load_oracle()
+    n = rp.shape[0] - 1
+    y = np.empty(n, dtype=val.dtype)
+    used = lib.cpu_spmv_simd(0 if val.dtype == np.float32 else 1, n, _ptr(rp), _bits(rp), _ptr(col),
+                             _ptr(val), _ptr(x), _ptr(y), threads)
+    return y, used
+
+
+# Parity bound for fp SpMV (north_star: "fp within 1e-6 relative"): per row
+# |y - y_exact| <= 1e-6 * sum_k |a_k x_k| (+ a denormal floor), and norm-wise
+# ||dy||_inf <= 1e-6 * ||y||_inf when y is not all-cancellation.
+SPMV_RTOL = 1e-6
+
+
+def assert_spmv_close(y, y64, asum, rtol=SPMV_RTOL):
+    y = np.asarray(y, dtype=np.float64)
+    err = np.abs(y - y64)
+    bound = rtol * asum + 1e-30
+    bad = np.nonzero(err > bound)[0]
+    assert bad.size == 0, (
+        f"{bad.size} rows exceed |dy| <= {rtol}*sum|a*x|; first row {bad[0]}: "
+        f"got {y[bad[0]]!r} want {y64[bad[0]]!r} bound {bound[bad[0]]!r}")
+    ninf = np.max(np.abs(y64)) if y64.size else 0.0
+    if ninf > 0:
+        assert np.max(err) <= rtol * max(ninf, np.max(asum) * 1e-3), "norm-wise error above 1e-6"
+
+
+def blur_oracle(a, ny, nx, ghost, nblur, ydir):
+    lib = load_oracle()
+    b = np.empty(ny * nx, dtype=np.float32)
+    (lib.oracle_blur_y if ydir else lib.oracle_blur_x)(_ptr(a), _ptr(b), ny, nx, ghost, nblur)
+    return b
+
+
+def stencil7_oracle(u, nz, ny, nx, g, c0, c1, out=None):
+    lib = load_oracle()
+    if out is None:
+        out = np.zeros_like(u)
+    lib.oracle_stencil7(_ptr(u), _ptr(out), nz, ny, nx, g, c0, c1, 0)
+    return out
+
+
+def load_golden(name):
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def random_padded(shape, seed, zero_ghost=False, ghost=0):
+    rng = np.random.default_rng(seed)
+    a = rng.uniform(-1, 1, size=shape).astype(np.float32)
+    if zero_ghost and ghost:
+        m = np.zeros(shape, dtype=bool)
+        sl = tuple(slice(ghost, s - ghost) for s in shape)
+        m[sl] = True
+        a[~m] = 0
+    return a
