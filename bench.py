@@ -1,0 +1,278 @@
+"""bench.py — CSR SpMV throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5|blur_x|blur_y]
+
+N=1: BASELINE configs[1] — CSR SpMV, n=10M, nnz=150M (exactly 15 uniform
+distinct sorted columns per row), fp32 values/x/y, A and x resident in HBM.
+N>1 (launched by torch.distributed.run, one rank per GPU): the SAME matrix is
+split into N nnz-balanced contiguous row blocks (strong scaling); a step is
+the local SpMV plus the RCCL all-gather of y over xGMI (torch.distributed
+backend "nccl" = RCCL), i.e. the exchange that makes y the next x.
+
+One step = one y = A·x over the whole matrix.  W untimed warmup steps, then
+exactly K timed steps between barrier + device synchronize; the max over ranks
+is reported.  value = 2·nnz·K / time (GFLOP/s, whole job).
+
+Extra objects on the JSON line:
+  roofline      the SpMV call on rank 0 (XSLICE = k_spmv_xslice + k_xslice_reduce,
+                see DESIGN.md): achieved = algorithmic bytes per call
+                (nnz·(4+4) + (n+1)·4 + 2·n·4, x counted once) ÷ average call
+                time from HIP events on the launch stream; peak 8.0 TB/s;
+                traffic = PMC HBM bytes per call from profiles/ (or null).
+  cpu_baseline  rank 0, N=1 only: the AVX2 + OpenMP CSR SpMV of oracle/ (the
+                reference has no CPU SpMV) on the same matrix, timed
+                for ~10 s on the box's host cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "CSR SpMV GFLOP/s + achieved HBM GB/s, n=10M nnz=150M, at 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "blur_x", "blur_y"])
+    ap.add_argument("--n", type=int, default=10_000_000)
+    ap.add_argument("--per-row", type=int, default=15)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_threads():
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def load_traffic(kernel_tag):
+    """PMC-measured HBM bytes per call, committed under profiles/ by
+    tools/pmc_traffic.py (FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected)."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        return d.get(kernel_tag, {}).get("bytes_per_call")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import libhpc_amd as L
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream(dev)
+    wl = args.workload
+    result = {}
+    if wl in ("c2", "c3", "c4"):
+        dt = L.F64 if wl == "c3" else L.F32
+        tsz = 8 if dt == L.F64 else 4
+        n = args.n
+        t0 = time.time()
+        if wl == "c4":
+            rp, col, val = L.gen_powerlaw_csr(n, n, dtype=dt)
+        else:
+            rp, col, val = L.gen_uniform_csr(n, n, args.per_row, dtype=dt)
+        x = L.gen_values(dt, 0, n, L.SEED_X)
+        nnz = int(col.shape[0])
+        t_gen = time.time() - t0
+        from libhpc_amd.dist import DistSpMV, row_block
+        blk = row_block(rp, col, val, rank, world)
+        k0, k1 = int(rp[blk.r0]), int(rp[blk.r1])
+        t0 = time.time()
+        plan = L.SpMVPlan(blk.row_ptr, blk.col_idx, blk.val, n)
+        t_plan = time.time() - t0
+        info = plan.info()
+        xd = torch.from_numpy(x).to(dev)
+        local_rows = blk.rows
+        dsp = DistSpMV(blk, lambda xv, yv: plan(xv, yv, stream=stream), like=xd)
+        y_local = dsp.y_local
+
+        def step():
+            if world > 1:
+                dsp.step(xd)
+            else:
+                plan(xd, y_local[:local_rows], stream=stream)
+
+        for _ in range(args.warmup):
+            step()
+        barrier()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        t_wall0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(args.steps):
+            step()
+        ev1.record(stream)
+        barrier()
+        t_wall = time.perf_counter() - t_wall0
+        t_ev = ev0.elapsed_time(ev1) * 1e-3
+        elapsed = max(t_wall, t_ev)
+        if world > 1:
+            tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+        per_step = elapsed / args.steps
+        gflops = 2.0 * nnz / per_step / 1e9
+        alg_bytes = nnz * (tsz + 4) + (n + 1) * 4 + 2 * n * tsz
+        # live SpMV-call timing on rank 0's launch stream (kernel-only, no collective)
+        kev0 = torch.cuda.Event(enable_timing=True)
+        kev1 = torch.cuda.Event(enable_timing=True)
+        reps = max(args.steps, 10)
+        barrier()
+        kev0.record(stream)
+        for _ in range(reps):
+            plan(xd, y_local[:local_rows], stream=stream)
+        kev1.record(stream)
+        torch.cuda.synchronize()
+        call_s = kev0.elapsed_time(kev1) * 1e-3 / reps
+        local_alg = (k1 - k0) * (tsz + 4) + (local_rows + 1) * 4 + (n + local_rows) * tsz
+        achieved = local_alg / call_s / 1e9
+        kname = {L.KERNEL_XSLICE: "xslice", L.KERNEL_ROWGROUP: "rowgroup",
+                 L.KERNEL_ADAPTIVE: "adaptive"}[info["kernel"]]
+        kernels = {"xslice": "k_spmv_xslice+k_xslice_reduce", "rowgroup": "k_spmv_rowgroup",
+                   "adaptive": "k_spmv_adaptive"}[kname]
+        traffic = load_traffic(f"{wl}_{kname}") if world == 1 else None
+        result.update(
+            metric=METRIC, value=gflops, unit="GFLOP/s", n_gpus=world, steps=args.steps,
+            warmup=args.warmup, ms_per_step=per_step * 1e3, higher_is_better=True,
+            scaling="strong", vs_baseline=None, dtype="f64" if dt == L.F64 else "f32",
+            data="synthetic: deterministic splitmix64 CSR (SURVEY §8d seeds), A/x resident in HBM",
+            config={"workload": {"c2": "BASELINE configs[1]: CSR SpMV n=10M nnz=150M fp32 uniform 15/row",
+                                 "c3": "BASELINE configs[2] matrix: CSR SpMV n=10M nnz=150M fp64 uniform 15/row",
+                                 "c4": "BASELINE configs[3]: power-law CSR (1..1e4 nnz/row) fp32"}[wl],
+                    "n_rows": n, "n_cols": n, "nnz": nnz, "kernel": kname, "slices": info["slices"],
+                    "parallelism": f"row-block x{world}" + (" + RCCL all_gather(y)" if world > 1 else "")},
+            achieved_GBps=alg_bytes / per_step / 1e9,
+            roofline={"bound": "hbm", "kernel": kernels, "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                      "alg_bytes_per_call": local_alg, "call_us": call_s * 1e6},
+            setup_s={"generate": t_gen, "plan": t_plan},
+        )
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_spmv_baseline(rp, col, val, x, nnz, args.cpu_seconds)
+        plan.close()
+    else:
+        result.update(stencil_bench(args, L, torch, dev, stream, barrier))
+        if rank == 0 and world == 1 and not args.no_cpu_baseline and wl in ("blur_x", "blur_y"):
+            result["cpu_baseline"] = result.pop("_cpu", None)
+        result.pop("_cpu", None)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_spmv_baseline(rp, col, val, x, nnz, seconds):
+    from tests import _support as S  # oracle/ is test infrastructure: baseline leg only
+    threads = cpu_threads()
+    y, used = S.spmv_cpu_simd(rp, col, val, x, threads=threads)  # warm
+    times = []
+    t_end = time.perf_counter() + seconds
+    while len(times) < 3 or (time.perf_counter() < t_end and len(times) < 400):
+        t0 = time.perf_counter()
+        S.spmv_cpu_simd(rp, col, val, x, threads=threads)
+        times.append(time.perf_counter() - t0)
+    best = min(times)
+    return {"value": 2.0 * nnz / best / 1e9, "unit": "GFLOP/s", "cores": used, "kind": "port",
+            "sample": f"full matrix (nnz={nnz}), best of {len(times)} passes "
+                      f"({sum(times):.1f} s), AVX2 gather + OpenMP, oracle/oracle.c cpu_spmv_simd"}
+
+
+def stencil_bench(args, L, torch, dev, stream, barrier):
+    wl = args.workload
+    if wl == "c5":
+        n = 512
+        g = 1
+        P = n + 2
+        u = torch.zeros(P ** 3, device=dev)
+        u.view(P, P, P)[1:-1, 1:-1, 1:-1] = torch.rand(n, n, n, device=dev) * 2 - 1
+        o = torch.zeros_like(u)
+        fn = lambda: L.stencil7(u, o, n, n, n, g, -6.0, 1.0, stream=stream)  # noqa: E731
+        cells = n ** 3
+        name = "k_stencil7"
+        workload = "BASELINE configs[4] grid: 7-point 3-D stencil 512^3 fp32, 1 GPU"
+    else:
+        n, g = 8192, 8
+        a = torch.rand((n + 2 * g) ** 2, device=dev) * 2 - 1
+        b = torch.empty(n * n, device=dev)
+        f = L.blur_x if wl == "blur_x" else L.blur_y
+        fn = lambda: f(a, b, n, n, g, 8, stream=stream)  # noqa: E731
+        cells = n * n
+        name = "k_blur_x" if wl == "blur_x" else "k_blur_y"
+        workload = f"reference BM_{wl} grid: 8192^2 fp32, ghost 8, 17 taps"
+    for _ in range(args.warmup):
+        fn()
+    barrier()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        fn()
+    e1.record(stream)
+    barrier()
+    per = e0.elapsed_time(e1) * 1e-3 / args.steps
+    ach = 8.0 * cells / per / 1e9
+    out = dict(metric=f"{wl} Gcell/s (8 B/cell algorithmic)", value=cells / per / 1e9, unit="Gcell/s",
+               n_gpus=1, steps=args.steps, warmup=args.warmup, ms_per_step=per * 1e3,
+               higher_is_better=True, scaling="weak", vs_baseline=None, dtype="f32",
+               data="synthetic U[-1,1)", config={"workload": workload},
+               roofline={"bound": "hbm", "kernel": name, "achieved": ach, "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": None})
+    if wl in ("blur_x", "blur_y") and not args.no_cpu_baseline:
+        from tests import _support as S
+        lib = S.load_oracle()
+        ah = a.cpu().numpy()
+        bh = np.empty(n * n, dtype=np.float32)
+        fnc = lib.cpu_blur_x_sse if wl == "blur_x" else lib.cpu_blur_y_sse
+        th = cpu_threads()
+        fnc(ah.ctypes.data, bh.ctypes.data, n, n, g, th)
+        ts = []
+        t_end = time.perf_counter() + args.cpu_seconds
+        while len(ts) < 3 or (time.perf_counter() < t_end and len(ts) < 400):
+            t0 = time.perf_counter()
+            fnc(ah.ctypes.data, bh.ctypes.data, n, n, g, th)
+            ts.append(time.perf_counter() - t0)
+        out["_cpu"] = {"value": cells / min(ts) / 1e9, "unit": "Gcell/s", "cores": th, "kind": "port",
+                       "sample": f"full 8192^2 grid, best of {len(ts)} passes, reference SSE loop restated"}
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -64,13 +64,15 @@ enum lhpc_plan_flags {
   LHPC_PLAN_DEVICE_INPUT = 1u << 1, /* row_ptr/col_idx/val are device ptrs    */
   /* force a kernel family instead of the heuristic (testing / benchmarks)   */
   LHPC_PLAN_FORCE_ROWGROUP = 1u << 4,
-  LHPC_PLAN_FORCE_ADAPTIVE = 1u << 5
+  LHPC_PLAN_FORCE_ADAPTIVE = 1u << 5,
+  LHPC_PLAN_FORCE_XSLICE = 1u << 6
 };
 
 /* kernel families a plan can select (lhpc_spmv_plan_info.kernel)          */
 enum lhpc_spmv_kernel {
   LHPC_KERNEL_ROWGROUP = 0, /* L lanes per row, wave64 DPP reduction        */
-  LHPC_KERNEL_ADAPTIVE = 1  /* nnz-balanced row blocks + long-row split     */
+  LHPC_KERNEL_ADAPTIVE = 1, /* nnz-balanced row blocks + long-row split     */
+  LHPC_KERNEL_XSLICE = 2    /* XCD-local column slices + partial reduce     */
 };
 
 typedef struct lhpc_spmv_plan lhpc_spmv_plan;
@@ -86,6 +88,8 @@ typedef struct lhpc_spmv_plan_info {
   int64_t device_bytes;/* HBM held by the plan                              */
   int device;          /* HIP device ordinal                                */
   int launches;        /* kernel launches per lhpc_spmv call                */
+  int slices;          /* XSLICE: column slices S (8 per XCD phase)         */
+  int64_t slice_width; /* XSLICE: columns per slice                         */
 } lhpc_spmv_plan_info;
 
 /* ------------------------------------------------------------- runtime   */

@@ -28,8 +28,8 @@ __all__ = [
     "LhpcError", "lib", "F32", "F64", "device_count", "SpMVPlan",
     "csr_partition_rows", "blur_x", "blur_y", "stencil7", "stencil7_planes",
     "gen_uniform_csr", "gen_powerlaw_csr", "gen_values", "padded_shape",
-    "PLAN_VALIDATE", "PLAN_FORCE_ROWGROUP", "PLAN_FORCE_ADAPTIVE",
-    "KERNEL_ROWGROUP", "KERNEL_ADAPTIVE",
+    "PLAN_VALIDATE", "PLAN_FORCE_ROWGROUP", "PLAN_FORCE_ADAPTIVE", "PLAN_FORCE_XSLICE",
+    "KERNEL_ROWGROUP", "KERNEL_ADAPTIVE", "KERNEL_XSLICE",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -39,7 +39,8 @@ F32, F64 = 0, 1
 PLAN_VALIDATE = 1 << 0
 PLAN_FORCE_ROWGROUP = 1 << 4
 PLAN_FORCE_ADAPTIVE = 1 << 5
-KERNEL_ROWGROUP, KERNEL_ADAPTIVE = 0, 1
+PLAN_FORCE_XSLICE = 1 << 6
+KERNEL_ROWGROUP, KERNEL_ADAPTIVE, KERNEL_XSLICE = 0, 1, 2
 
 # every symbol include/lhpc.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = (
@@ -57,6 +58,23 @@ if not os.path.exists(LIB_PATH):
         f"libhpc_amd: native library {LIB_PATH} is missing; build it with "
         "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
 
+def _bind_single_hip_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm bundles its own
+    libamdhip64 (SONAME libamdhip64.so.7, like /opt/rocm's); if ours were
+    loaded first, torch would later load its copy as a second runtime and see
+    no GPU.  Loading torch's copy first makes liblhpc.so bind to it."""
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec and spec.origin:
+        cand = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+        if os.path.exists(cand):
+            C.CDLL(cand, mode=C.RTLD_GLOBAL)
+
+
+_bind_single_hip_runtime()
 lib = C.CDLL(LIB_PATH)
 _p, _i, _i64, _u, _u64, _f, _d = (C.c_void_p, C.c_int, C.c_int64, C.c_uint,
                                   C.c_uint64, C.c_float, C.c_double)
@@ -66,7 +84,8 @@ class PlanInfo(C.Structure):
     _fields_ = [("dtype", _i), ("kernel", _i), ("lanes_per_row", _i),
                 ("rows_per_group", _i), ("n_rows", _i64), ("n_cols", _i64),
                 ("nnz", _i64), ("n_blocks", _i64), ("n_long_rows", _i64),
-                ("device_bytes", _i64), ("device", _i), ("launches", _i)]
+                ("device_bytes", _i64), ("device", _i), ("launches", _i),
+                ("slices", _i), ("slice_width", _i64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

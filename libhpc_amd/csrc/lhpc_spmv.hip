@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "lhpc_common.hpp"
+#include "lhpc_plan.hpp"
 
 namespace lhpc {
 namespace {
@@ -178,6 +179,170 @@ __global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
   if (grp < nrows && sub == 0) y[r0 + grp] = static_cast<T>(a);
 }
 
+// --------------------------------------------------------------- XSLICE
+// Column-sliced SpMV.  Slice s = g + 8·phase is processed
+// by the blocks with blockIdx % 8 == g (the blocks the dispatcher deals to one
+// XCD), phase after phase, so each XCD's L2 holds one x slice (≈ 2.5–5 MB)
+// and the random x-gathers hit L2 instead of Infinity Cache / HBM (measured:
+// 151–168 G gathers/s vs 59 unsliced, tools/probe_slices.py).  Placement is a
+// speed heuristic only: any block→XCD mapping gives the same result.
+// One lane per row, one wave per 64-row chunk; the chunk's in-slice
+// nonzeros are jagged-diagonal, so iteration j reads the active lanes'
+// elements contiguously (ballot + mbcnt addressing, no padding).  Each row
+// accumulates its in-slice products in fp64 in CSR order and stores one
+// partial per (slice, row); k_xslice_reduce adds the S partials in slice
+// order.  Loads are unconditional (clamped index) so hipcc keeps U
+// iterations of loads in flight instead of branching around each one.
+template <typename T, int U>
+__global__ __launch_bounds__(kBlock) void k_spmv_xslice(
+    const uint8_t *__restrict__ lens, const int64_t *__restrict__ cbase,
+    const int32_t *__restrict__ col, const T *__restrict__ val, const T *__restrict__ x,
+    T *__restrict__ partial, int64_t n_rows, int64_t n_rows_pad, int64_t n_chunks,
+    int64_t blocks_per_slice, int S, int64_t nnz_last) {
+  const int64_t b = blockIdx.x;
+  int s;
+  int64_t wb;
+  if (S >= 8) {
+    const int64_t g = b % 8, idx = b / 8;
+    s = static_cast<int>(g + 8 * (idx / blocks_per_slice));
+    wb = idx % blocks_per_slice;
+  } else {
+    s = static_cast<int>(b % S);
+    wb = b / S;
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t chunk = wb * (kBlock / kWave) + threadIdx.x / kWave;
+  if (s >= S || chunk >= n_chunks) return;  // wave-uniform
+  const int64_t row = chunk * kWave + lane;
+  const int len = lens[static_cast<int64_t>(s) * n_rows_pad + row];
+  int64_t pos = cbase[static_cast<int64_t>(s) * n_chunks + chunk];
+  double acc = 0.0;
+  for (int j = 0;; j += U) {
+    if (__ballot(j < len) == 0) break;  // wave-uniform exit
+    int64_t k[U];
+    bool act[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      act[u] = (j + u) < len;
+      const uint64_t m = __ballot(act[u]);
+      const int rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0));
+      k[u] = act[u] ? pos + rank : (pos < nnz_last ? pos : nnz_last);
+      pos += __popcll(m);
+    }
+    int32_t c[U];
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      c[u] = ld_stream(col + k[u]);
+      v[u] = ld_stream(val + k[u]);
+    }
+    T xv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xv[u] = x[c[u]];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (act[u]) acc += static_cast<double>(v[u]) * static_cast<double>(xv[u]);
+  }
+  if (row < n_rows) __builtin_nontemporal_store(static_cast<T>(acc), partial + static_cast<int64_t>(s) * n_rows_pad + row);
+}
+
+// XSLICE "stream" form (default): same slicing and XCD grouping, but the
+// chunk's in-slice nonzeros are in CSR order and the whole wave streams
+// them NB·64 at a time — every lane loads / gathers (full lane utilisation,
+// NB gathers in flight per lane) — staging exact fp64 products in a
+// wave-private LDS window; lane r then adds its row's products in CSR order.
+// Row offsets inside the chunk come from a wave prefix sum of the uint8
+// lengths.  A chunk with more than NB·64 nonzeros loops over windows (rows
+// spanning windows keep accumulating in order, so the result is unchanged).
+template <typename T, int NB>
+__global__ __launch_bounds__(kBlock) void k_spmv_xslice_stream(
+    const uint8_t *__restrict__ lens, const int64_t *__restrict__ cbase,
+    const int32_t *__restrict__ col, const T *__restrict__ val, const T *__restrict__ x,
+    T *__restrict__ partial, int64_t n_rows, int64_t n_rows_pad, int64_t n_chunks,
+    int64_t blocks_per_slice, int S) {
+  constexpr int CAP = NB * kWave;
+  __shared__ double prod[kBlock / kWave][CAP];
+  const int64_t b = blockIdx.x;
+  int s;
+  int64_t wb;
+  if (S >= 8) {
+    const int64_t g = b % 8, idx = b / 8;
+    s = static_cast<int>(g + 8 * (idx / blocks_per_slice));
+    wb = idx % blocks_per_slice;
+  } else {
+    s = static_cast<int>(b % S);
+    wb = b / S;
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = threadIdx.x / kWave;
+  const int64_t chunk = wb * (kBlock / kWave) + wv;
+  if (s >= S || chunk >= n_chunks) return;  // wave-uniform
+  const int64_t row = chunk * kWave + lane;
+  const int len = lens[static_cast<int64_t>(s) * n_rows_pad + row];
+  const int64_t base = cbase[static_cast<int64_t>(s) * n_chunks + chunk];
+  // inclusive wave scan of len → this lane's row offset inside the chunk
+  int inc = len;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int t = __shfl_up(inc, d, kWave);
+    if (lane >= d) inc += t;
+  }
+  const int off = inc - len;
+  const int cnt = __shfl(inc, kWave - 1, kWave);
+  double acc = 0.0;
+  double *wp = prod[wv];
+  for (int w0 = 0; w0 < cnt; w0 += CAP) {  // wave-uniform
+    int32_t c[NB];
+    T v[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      int k = w0 + i * kWave + lane;
+      k = k < cnt ? k : cnt - 1;  // clamped: loads stay unconditional
+      c[i] = ld_stream(col + base + k);
+      v[i] = ld_stream(val + base + k);
+    }
+    T xv[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) xv[i] = x[c[i]];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      wp[i * kWave + lane] = static_cast<double>(v[i]) * static_cast<double>(xv[i]);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int lo = off > w0 ? off : w0;
+    const int hi = (off + len) < (w0 + CAP) ? (off + len) : (w0 + CAP);
+    for (int k = lo; k < hi; ++k) acc += wp[k - w0];
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (row < n_rows)
+    __builtin_nontemporal_store(static_cast<T>(acc), partial + static_cast<int64_t>(s) * n_rows_pad + row);
+}
+
+// y[i] = Σ_{s=0}^{S-1} partial[s][i], fp64, fixed slice order; 4 rows/thread.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_xslice_reduce(const T *__restrict__ partial,
+                                                          T *__restrict__ y, int64_t n_rows,
+                                                          int64_t n_rows_pad, int S) {
+  const int64_t i0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 4;
+  if (i0 >= n_rows) return;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int s = 0; s < S; ++s) {
+    const T *p = partial + static_cast<int64_t>(s) * n_rows_pad + i0;
+    if constexpr (sizeof(T) == 4) {
+      const f32x4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
+      a[0] += q[0]; a[1] += q[1]; a[2] += q[2]; a[3] += q[3];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] += __builtin_nontemporal_load(p + j);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (i0 + j < n_rows) y[i0 + j] = static_cast<T>(a[j]);
+}
+
 // ------------------------------------------------------------- host side
 bool is_gfx950(int dev) {
   hipDeviceProp_t p;
@@ -204,6 +369,13 @@ struct lhpc_spmv_plan {
   int kernel = LHPC_KERNEL_ROWGROUP;
   int L = 16, R = 4;
   int64_t bytes = 0;
+  // XSLICE
+  int S = 0;
+  int xs_jagged = 0, xs_nb = 2;
+  int64_t xs_width = 0, xs_chunks = 0, xs_rows_pad = 0, xs_bps = 0;
+  uint8_t *d_lens = nullptr;
+  int64_t *d_cbase = nullptr;
+  void *d_partial = nullptr;
 };
 
 namespace {
@@ -258,7 +430,40 @@ int launch_adaptive(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t
 }
 
 template <typename T>
+int launch_xslice(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  if (p->n_rows == 0) return LHPC_OK;
+  const int64_t grid = p->S >= 8 ? 8 * (p->S / 8) * p->xs_bps : p->S * p->xs_bps;
+  const int64_t nnz_last = p->nnz > 0 ? p->nnz - 1 : 0;
+  const dim3 g(static_cast<unsigned>(grid)), blk(kBlock);
+  const T *xv = static_cast<const T *>(x);
+  const T *vv = static_cast<const T *>(p->d_val);
+  T *pp = static_cast<T *>(p->d_partial);
+  if (p->xs_jagged) {
+    hipLaunchKernelGGL((k_spmv_xslice<T, 4>), g, blk, 0, s, p->d_lens, p->d_cbase, p->d_col, vv, xv, pp,
+                       p->n_rows, p->xs_rows_pad, p->xs_chunks, p->xs_bps, p->S, nnz_last);
+  } else {
+#define LHPC_XS_STREAM(NB)                                                                          \
+  hipLaunchKernelGGL((k_spmv_xslice_stream<T, NB>), g, blk, 0, s, p->d_lens, p->d_cbase, p->d_col, vv, \
+                     xv, pp, p->n_rows, p->xs_rows_pad, p->xs_chunks, p->xs_bps, p->S)
+    switch (p->xs_nb) {
+      case 1: LHPC_XS_STREAM(1); break;
+      case 2: LHPC_XS_STREAM(2); break;
+      case 3: LHPC_XS_STREAM(3); break;
+      default: LHPC_XS_STREAM(4); break;
+    }
+#undef LHPC_XS_STREAM
+  }
+  LHPC_TRY(check_launch(s));
+  const int64_t rgrid = (p->n_rows + 4 * kBlock - 1) / (4 * kBlock);
+  hipLaunchKernelGGL((k_xslice_reduce<T>), dim3(static_cast<unsigned>(rgrid)), dim3(kBlock), 0, s,
+                     static_cast<const T *>(p->d_partial), static_cast<T *>(y), p->n_rows,
+                     p->xs_rows_pad, p->S);
+  return check_launch(s);
+}
+
+template <typename T>
 int launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  if (p->kernel == LHPC_KERNEL_XSLICE) return launch_xslice<T>(p, x, y, s);
   if (p->kernel == LHPC_KERNEL_ADAPTIVE)
     return p->rp64 ? launch_adaptive<T, int64_t>(p, x, y, s)
                    : launch_adaptive<T, int32_t>(p, x, y, s);
@@ -359,6 +564,65 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
   bool adaptive = (cv > 1.0 && maxlen > 256) || maxlen > 4096;
   if (flags & LHPC_PLAN_FORCE_ROWGROUP) adaptive = false;
   if (flags & LHPC_PLAN_FORCE_ADAPTIVE) adaptive = true;
+  // XSLICE when x outgrows one XCD's 4 MB L2 and rows are short enough for
+  // the uint8 in-slice lengths (the builder re-checks per slice).
+  const double x_bytes = static_cast<double>(n_cols) * static_cast<double>(tsz);
+  double slice_mb = 5.0;
+  if (const char *env = std::getenv("LHPC_XSLICE_MB")) slice_mb = std::max(0.25, std::atof(env));
+  const bool want_xslice = (flags & LHPC_PLAN_FORCE_XSLICE) ||
+                           (!(flags & (LHPC_PLAN_FORCE_ROWGROUP | LHPC_PLAN_FORCE_ADAPTIVE)) && !adaptive &&
+                            x_bytes > 8.0e6 && maxlen <= 255);
+  if (want_xslice && nnz > 0) {
+    int P = static_cast<int>(std::ceil(x_bytes / (8.0 * slice_mb * 1.0e6)));
+    P = std::max(1, std::min(P, 32));
+    int S = 8 * P;
+    if (const char *env = std::getenv("LHPC_XSLICE_S")) S = std::max(1, std::min(256, std::atoi(env)));
+    if (S > 8) S = (S + 7) / 8 * 8;
+    XsliceHost xs;
+    bool jagged = false;
+    if (const char *env = std::getenv("LHPC_XSLICE_LAYOUT")) jagged = std::strcmp(env, "jagged") == 0;
+    const int bst = build_xslice(row_ptr, row_ptr_bits, col_idx, val, tsz, n_rows, n_cols, S, jagged, xs);
+    if (bst == LHPC_OK) {
+      p->kernel = LHPC_KERNEL_XSLICE;
+      p->S = S;
+      p->xs_jagged = jagged ? 1 : 0;
+      {  // window = NB·64 nonzeros: cover a typical chunk in one window
+        const double mean_chunk = xs.n_chunks ? static_cast<double>(nnz) / (static_cast<double>(S) * xs.n_chunks) : 0;
+        int nb = static_cast<int>(std::ceil(mean_chunk * 1.2 / kWave));
+        if (const char *env = std::getenv("LHPC_XSLICE_NB")) nb = std::atoi(env);
+        p->xs_nb = std::max(1, std::min(nb, 4));
+      }
+      p->xs_width = xs.width;
+      p->xs_chunks = xs.n_chunks;
+      p->xs_rows_pad = xs.n_rows_pad;
+      p->xs_bps = (xs.n_chunks + (kBlock / kWave) - 1) / (kBlock / kWave);
+      int st = LHPC_OK;
+      do {
+        const size_t lb = static_cast<size_t>(S) * xs.n_rows_pad;
+        const size_t cb = (static_cast<size_t>(S) * xs.n_chunks + 1) * 8;
+        if ((st = dmalloc(reinterpret_cast<void **>(&p->d_lens), lb, p->bytes))) break;
+        if ((st = dmalloc(reinterpret_cast<void **>(&p->d_cbase), cb, p->bytes))) break;
+        if ((st = dmalloc(reinterpret_cast<void **>(&p->d_col), static_cast<size_t>(nnz) * 4, p->bytes))) break;
+        if ((st = dmalloc(&p->d_val, static_cast<size_t>(nnz) * tsz, p->bytes))) break;
+        if ((st = dmalloc(&p->d_partial, lb * tsz, p->bytes))) break;
+        if ((st = static_cast<int>(hipMemcpy(p->d_lens, xs.lens.get(), lb, hipMemcpyHostToDevice)))) break;
+        if ((st = static_cast<int>(hipMemcpy(p->d_cbase, xs.cbase.get(), cb, hipMemcpyHostToDevice)))) break;
+        if ((st = static_cast<int>(hipMemcpy(p->d_col, xs.col.get(), static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice)))) break;
+        if ((st = static_cast<int>(hipMemcpy(p->d_val, xs.val.get(), static_cast<size_t>(nnz) * tsz, hipMemcpyHostToDevice)))) break;
+      } while (false);
+      if (st != LHPC_OK) {
+        lhpc_spmv_plan_destroy(p);
+        return st;
+      }
+      *out = p;
+      return LHPC_OK;
+    }
+    if (bst != LHPC_ERR_UNSUPPORTED) {
+      lhpc_spmv_plan_destroy(p);
+      return bst;
+    }
+    // some row too long for one slice: fall through to a CSR kernel
+  }
   if (adaptive) {
     p->kernel = LHPC_KERNEL_ADAPTIVE;
   } else {
@@ -460,7 +724,9 @@ extern "C" int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *p, lhpc_spmv_plan_i
   info->n_long_rows = p->n_long;
   info->device_bytes = p->bytes;
   info->device = p->device;
-  info->launches = 1;
+  info->launches = p->kernel == LHPC_KERNEL_XSLICE ? 2 : 1;
+  info->slices = p->S;
+  info->slice_width = p->xs_width;
   return LHPC_OK;
 }
 
@@ -468,7 +734,8 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
   if (!p) return LHPC_OK;
   (void)hipSetDevice(p->device);
   for (void *q : {p->d_row_ptr, static_cast<void *>(p->d_col), p->d_val,
-                  static_cast<void *>(p->d_blocks), p->d_xstage, p->d_ystage})
+                  static_cast<void *>(p->d_blocks), p->d_xstage, p->d_ystage,
+                  static_cast<void *>(p->d_lens), static_cast<void *>(p->d_cbase), p->d_partial})
     if (q) (void)hipFree(q);
   delete p;
   return LHPC_OK;

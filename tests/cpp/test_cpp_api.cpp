@@ -1,0 +1,149 @@
+// test_cpp_api.cpp — exercises the C++ drop-in surface exactly as a reference
+// user would: hpc::HPCHighDimensionFlatArray / hpc::AlignedAllocator (same
+// names and layout as lib/hpc/include), sparse::CSRMatrix + sparse::spmv, and
+// hpc::blur_x / blur_y / stencil7, all forwarding to liblhpc.so.
+//   test_cpp_api layout   — no GPU: layout offsets (JSON) + at() bounds
+//   test_cpp_api gpu      — SpMV / blur / stencil7 on the device vs plain loops
+// Linked with second_tu.cpp, which includes the same headers: the reference's
+// AlignedAlloc.hpp fails to link this way; ours must not.
+#include <HPCHighDimensionFlatArray.hpp>
+#include <Stencil.hpp>
+#include <sparse/SpMV.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <system_error>
+
+int second_tu_sum(int n);  // second_tu.cpp
+
+namespace {
+
+int fail(const char *what) {
+  std::fprintf(stderr, "FAIL: %s\n", what);
+  return 1;
+}
+
+template <std::size_t G>
+void print_layout2(long ny, long nx, bool first) {
+  hpc::HPCHighDimensionFlatArray<2, float, G> a(ny, nx);
+  const long g = static_cast<long>(G);
+  const long pts[][2] = {{-g, -g}, {0, 0}, {0, 1}, {1, 0}, {ny - 1, nx - 1}, {ny + g - 1, nx + g - 1}};
+  std::printf("%s{\"dims\":[%ld,%ld],\"ghost\":%ld,\"offsets\":[", first ? "" : ",", ny, nx, g);
+  for (size_t i = 0; i < 6; ++i)
+    std::printf("%s[%ld,%ld,%td]", i ? "," : "", pts[i][0], pts[i][1], &a.at({pts[i][0], pts[i][1]}) - a.data());
+  bool threw = false;
+  try {
+    a.at({ny + g, 0});
+  } catch (const std::out_of_range &) {
+    threw = true;
+  }
+  std::printf("],\"at_out_of_range_throws\":%s}", threw ? "true" : "false");
+}
+
+void print_layout3(long nz, long ny, long nx) {
+  hpc::HPCHighDimensionFlatArray<3, float, 1> a(nz, ny, nx);
+  const long pts[][3] = {{-1, -1, -1}, {0, 0, 0}, {0, 0, 1}, {0, 1, 0}, {1, 0, 0}, {nz - 1, ny - 1, nx - 1}, {nz, ny, nx}};
+  std::printf(",{\"dims\":[%ld,%ld,%ld],\"ghost\":1,\"offsets\":[", nz, ny, nx);
+  for (size_t i = 0; i < 7; ++i)
+    std::printf("%s[%ld,%ld,%ld,%td]", i ? "," : "", pts[i][0], pts[i][1], pts[i][2],
+                &a.at({pts[i][0], pts[i][1], pts[i][2]}) - a.data());
+  std::printf("]}");
+}
+
+int layout_mode() {
+  std::printf("[");
+  print_layout2<8>(5, 7, true);
+  print_layout2<0>(3, 4, false);
+  print_layout2<1>(9, 2, false);
+  print_layout3(4, 5, 6);
+  print_layout3(1, 1, 1);
+  std::printf("]\n");
+  // zero-initialised, aligned, usable from a second TU
+  hpc::HPCHighDimensionFlatArray<2, double, 2, 2, 64> z(3, 3);
+  for (std::size_t i = 0; i < z.size(); ++i)
+    if (z.data()[i] != 0.0) return fail("not zero-initialised");
+  if (reinterpret_cast<std::uintptr_t>(z.data()) % 64) return fail("alignment");
+  if (second_tu_sum(10) != 45) return fail("second TU");
+  return 0;
+}
+
+float dyadic(unsigned i) { return static_cast<float>(static_cast<int>((i * 2654435761u) >> 28) % 17 - 8) * 0.125f; }
+
+int gpu_mode() {
+  // ---- SpMV through sparse::SpMVPlan / sparse::spmv with flat-array vectors
+  const std::int64_t n = 5000, m = 4001;
+  sparse::CSRMatrix<float> A(n, m);
+  for (std::int64_t i = 0; i < n; ++i) {
+    const int len = static_cast<int>(i % 23);
+    for (int j = 0; j < len; ++j) {
+      A.col_idx.push_back(static_cast<std::int32_t>((i * 37 + j * 151) % m));
+      A.val.push_back(dyadic(static_cast<unsigned>(i * 31 + j)));
+    }
+    std::sort(A.col_idx.end() - len, A.col_idx.end());
+    // distinct columns: (i*37 + j*151) % m is injective in j for len < 23
+    A.row_ptr[static_cast<std::size_t>(i + 1)] = static_cast<std::int32_t>(A.col_idx.size());
+  }
+  A.validate();
+  hpc::HPCHighDimensionFlatArray<1, float> x(m), y(n);
+  for (std::int64_t c = 0; c < m; ++c) x(c) = dyadic(static_cast<unsigned>(c + 7));
+  sparse::SpMVPlan<float> plan(A);
+  sparse::spmv(plan, x, y);
+  for (std::int64_t i = 0; i < n; ++i) {
+    double s = 0;
+    for (auto k = A.row_ptr[i]; k < A.row_ptr[i + 1]; ++k) s += double(A.val[k]) * double(x(A.col_idx[k]));
+    if (static_cast<float>(s) != y(i)) return fail("spmv mismatch (dyadic inputs must be exact)");
+  }
+  // wrong-size vector → std::system_error in the lhpc category
+  try {
+    hpc::HPCHighDimensionFlatArray<1, float> shortx(10);
+    sparse::spmv(plan, shortx, y);
+    return fail("expected std::system_error");
+  } catch (const std::system_error &e) {
+    if (std::strcmp(e.code().category().name(), "lhpc") != 0) return fail("error category");
+  }
+  // ---- blur_x / blur_y on the reference container types
+  const long ny = 37, nx = 70;
+  hpc::HPCHighDimensionFlatArray<2, float, 8> a(ny, nx);
+  hpc::HPCHighDimensionFlatArray<2, float> b(ny, nx);
+  for (long yy = -8; yy < ny + 8; ++yy)
+    for (long xx = -8; xx < nx + 8; ++xx) a.at({yy, xx}) = std::sin(0.37f * yy + 0.11f * xx);
+  for (int dir = 0; dir < 2; ++dir) {
+    if (dir == 0) hpc::blur_x<8>(a, b); else hpc::blur_y<8>(a, b);
+    for (long yy = 0; yy < ny; ++yy)
+      for (long xx = 0; xx < nx; ++xx) {
+        float res = 0.f;
+        for (int k = -8; k <= 8; ++k) res += dir == 0 ? a(yy, xx + k) : a(yy + k, xx);
+        if (res != b(yy, xx)) return fail(dir == 0 ? "blur_x mismatch" : "blur_y mismatch");
+      }
+  }
+  // ---- stencil7
+  hpc::HPCHighDimensionFlatArray<3, float, 1> u(9, 10, 11), o(9, 10, 11);
+  for (long z = 0; z < 9; ++z)
+    for (long yy = 0; yy < 10; ++yy)
+      for (long xx = 0; xx < 11; ++xx) u(z, yy, xx) = std::cos(0.3f * z + 0.7f * yy - 0.2f * xx);
+  hpc::stencil7(u, o, -6.f, 1.f);
+  for (long z = 0; z < 9; ++z)
+    for (long yy = 0; yy < 10; ++yy)
+      for (long xx = 0; xx < 11; ++xx) {
+        float s = u(z - 1, yy, xx) + u(z + 1, yy, xx);
+        s = s + u(z, yy - 1, xx);
+        s = s + u(z, yy + 1, xx);
+        s = s + u(z, yy, xx - 1);
+        s = s + u(z, yy, xx + 1);
+        const float t0 = -6.f * u(z, yy, xx), t1 = 1.f * s;
+        if (t0 + t1 != o(z, yy, xx)) return fail("stencil7 mismatch");
+      }
+  std::printf("cpp api gpu: ok (spmv kernel %d)\n", plan.info().kernel);
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  if (argc > 1 && !std::strcmp(argv[1], "gpu")) return gpu_mode();
+  return layout_mode();
+}

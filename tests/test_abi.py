@@ -1,0 +1,102 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every
+function include/lhpc.h declares, and rejects bad arguments with the
+documented status codes before touching a device."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tests._support import ROOT
+
+HEADER = os.path.join(ROOT, "include", "lhpc.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(lhpc_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_every_declared_symbol_is_exported(lhpc):
+    names = declared_functions()
+    assert len(names) >= 17
+    for n in names:
+        assert hasattr(lhpc.lib, n), f"{n} declared in lhpc.h but not exported"
+    assert set(names) == set(lhpc.ABI_SYMBOLS), "python mirror's symbol list drifted from lhpc.h"
+
+
+def test_nm_exports_match_header():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(ROOT, "libhpc_amd", "_lib", "liblhpc.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l and l.split()[-1].startswith("lhpc_")}
+    assert set(declared_functions()) <= exported
+
+
+def test_abi_version_and_strerror(lhpc):
+    assert lhpc.lib.lhpc_abi_version() == 1
+    for st in (0, -1, -2, -3, -4, -5, -6):
+        assert lhpc.lib.lhpc_strerror(st)
+    assert b"invalid" in lhpc.lib.lhpc_strerror(-1)
+
+
+def _create(lhpc, **kw):
+    args = dict(dtype=0, n_rows=2, n_cols=2, nnz=2, row_ptr=np.array([0, 1, 2], np.int32), bits=32,
+                col=np.array([0, 1], np.int32), val=np.ones(2, np.float32), flags=0)
+    args.update(kw)
+    h = C.c_void_p()
+    st = lhpc.lib.lhpc_spmv_plan_create(
+        C.byref(h), args["dtype"], args["n_rows"], args["n_cols"], args["nnz"],
+        args["row_ptr"].ctypes.data if args["row_ptr"] is not None else None, args["bits"],
+        args["col"].ctypes.data if args["col"] is not None else None,
+        args["val"].ctypes.data if args["val"] is not None else None, None, 0, args["flags"])
+    return st, h
+
+
+@pytest.mark.parametrize("bad", [dict(dtype=7), dict(n_rows=-1), dict(bits=16), dict(row_ptr=None),
+                                 dict(col=None), dict(nnz=-3)])
+def test_plan_create_invalid_args(lhpc, bad):
+    st, h = _create(lhpc, **bad)
+    assert st == -1 and not h.value
+
+
+def test_plan_create_bad_csr(lhpc):
+    st, _ = _create(lhpc, row_ptr=np.array([0, 2, 1], np.int32))  # row_ptr[n] != nnz
+    assert st == -2
+    st, _ = _create(lhpc, row_ptr=np.array([1, 1, 2], np.int32))
+    assert st == -2
+    st, _ = _create(lhpc, col=np.array([0, 5], np.int32), flags=1)  # validate: col out of range
+    assert st == -2
+
+
+def test_plan_create_without_device_fails_loudly(lhpc):
+    if lhpc.device_count() > 0:
+        pytest.skip("a GPU is present")
+    st, h = _create(lhpc)
+    assert st != 0 and not h.value  # no silent CPU fallback
+
+
+def test_null_plan_calls(lhpc):
+    assert lhpc.lib.lhpc_spmv(None, None, None, 1, None) == -1
+    assert lhpc.lib.lhpc_spmv_plan_destroy(None) == 0
+    assert lhpc.lib.lhpc_blur_x_f32(None, None, 1, 1, 8, 8, 1, None) == -1
+    assert lhpc.lib.lhpc_stencil7_f32(None, None, 1, 1, 1, 1, 1.0, 1.0, 1, None) == -1
+
+
+def test_python_mirror_raises(lhpc):
+    with pytest.raises(TypeError):
+        lhpc.SpMVPlan(np.array([0, 1], np.int16), np.array([0], np.int32), np.ones(1, np.float32), 1)
+    with pytest.raises(lhpc.LhpcError):
+        lhpc.SpMVPlan(np.array([0, 1], np.int32), np.array([0], np.int32), np.ones(1, np.float32), -5)
+
+
+def test_single_hip_runtime_with_torch():
+    """liblhpc.so must share torch's HIP runtime (never two in one process)."""
+    import subprocess, sys
+    code = ("import sys; sys.path.insert(0, %r); import libhpc_amd, torch; "
+            "m = open('/proc/self/maps').read(); "
+            "print(len({l.split()[-1] for l in m.splitlines() if 'libamdhip64' in l}))" % ROOT)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == "1"

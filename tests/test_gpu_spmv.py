@@ -1,0 +1,167 @@
+"""GPU parity for CSR SpMV through the C ABI (include/lhpc.h) — every kernel
+family against the exact-arithmetic golden fixtures and the CPU oracle.
+
+Bars (north_star): index handling bit-exact — dyadic-valued inputs make every
+summation order exact, so y must equal the reference bit-for-bit; random
+fp inputs within |dy| <= 1e-6 * sum|a*x| per row (tests/_support.py).
+SpMV parity is "unpinned by the reference" (the reference has no SpMV, SURVEY
+§0): the anchor is exact arithmetic (Fractions) and the fp64 oracle.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from tests import _support as S
+
+pytestmark = pytest.mark.gpu
+
+FAMILIES = {
+    "auto": 0,
+    "rowgroup": 1 << 4,
+    "adaptive": 1 << 5,
+    "xslice": 1 << 6,
+}
+GOLDEN_SPMV = sorted(glob.glob(os.path.join(S.GOLDEN, "spmv_*.npz")))
+
+
+def _run(lhpc, gpu, rp, col, val, x, n_cols, flags, device_buffers=True):
+    import torch
+    with lhpc.SpMVPlan(rp, col, val, n_cols, flags=flags) as plan:
+        if device_buffers:
+            xd = torch.from_numpy(x).to(gpu)
+            y = plan(xd).cpu().numpy()
+        else:
+            y = plan(x)
+        info = plan.info()
+    return y, info
+
+
+@pytest.mark.parametrize("family", list(FAMILIES))
+@pytest.mark.parametrize("path", GOLDEN_SPMV, ids=lambda p: os.path.basename(p)[5:-4])
+def test_golden(lhpc, gpu, path, family):
+    g = S.load_golden(os.path.basename(path))
+    rp, col, val, x = g["row_ptr"], g["col_idx"], g["val"], g["x"]
+    n_cols = int(g["n_cols"])
+    y, info = _run(lhpc, gpu, rp, col, val, x, n_cols, FAMILIES[family])
+    if family == "xslice" and np.max(np.diff(rp.astype(np.int64)), initial=0) > 255 * 8:
+        assert info["kernel"] != lhpc.KERNEL_XSLICE  # > 255 per slice: CSR fallback
+    exact = g["y_exact"]
+    if "dyadic" in path:
+        assert np.array_equal(y, exact.astype(val.dtype)), "dyadic SpMV must be bit-exact"
+    else:
+        _, _, asum = S.spmv_oracle(rp, col, val, x)
+        S.assert_spmv_close(y, exact, asum)
+
+
+@pytest.mark.parametrize("family", ["auto", "xslice"])
+def test_host_buffers_match_device(lhpc, gpu, family):
+    g = S.load_golden("spmv_dyadic_f32_n1000.npz")
+    args = (g["row_ptr"], g["col_idx"], g["val"], g["x"], int(g["n_cols"]), FAMILIES[family])
+    yd, _ = _run(lhpc, gpu, *args, device_buffers=True)
+    yh, _ = _run(lhpc, gpu, *args, device_buffers=False)
+    assert np.array_equal(yd, yh)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 4099])
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+@pytest.mark.parametrize("family", list(FAMILIES))
+def test_edge_sizes_vs_oracle(lhpc, gpu, n, dtype, family):
+    dt = lhpc.F32 if dtype == "f32" else lhpc.F64
+    per = min(n, 15)
+    for dist in (0, 1):
+        rp, col, val = lhpc.gen_uniform_csr(n, n, per, dtype=dt, dist=dist, seed=0xE000 + n)
+        x = lhpc.gen_values(dt, dist, n, 0xE100 + n)
+        y, _ = _run(lhpc, gpu, rp, col, val, x, n, FAMILIES[family])
+        y64, yr, asum = S.spmv_oracle(rp, col, val, x)
+        if dist == 1:
+            assert np.array_equal(y, yr)
+        else:
+            S.assert_spmv_close(y, y64, asum)
+
+
+def test_empty_matrix_and_zero_rows(lhpc, gpu):
+    import torch
+    rp = np.zeros(11, dtype=np.int32)
+    col = np.zeros(0, dtype=np.int32)
+    val = np.zeros(0, dtype=np.float32)
+    x = np.ones(7, dtype=np.float32)
+    for flags in FAMILIES.values():
+        y, _ = _run(lhpc, gpu, rp, col, val, x, 7, flags)
+        assert np.array_equal(y, np.zeros(10, dtype=np.float32))
+    with lhpc.SpMVPlan(np.zeros(1, dtype=np.int32), col, val, 7) as plan:
+        out = plan(torch.ones(7, device=gpu))
+        assert out.numel() == 0
+
+
+@pytest.mark.parametrize("family", list(FAMILIES))
+def test_powerlaw_vs_oracle(lhpc, gpu, family):
+    n = 200_000
+    rp, col, val = lhpc.gen_powerlaw_csr(n, n, lmax=10_000, dtype=lhpc.F32, seed=0xE200)
+    x = lhpc.gen_values(lhpc.F32, 0, n, 0xE201)
+    y, info = _run(lhpc, gpu, rp, col, val, x, n, FAMILIES[family])
+    y64, _, asum = S.spmv_oracle(rp, col, val, x)
+    S.assert_spmv_close(y, y64, asum)
+
+
+def test_c1_config_vs_oracle(lhpc, gpu):
+    """BASELINE configs[0] shape (n=1e5, nnz=1e6, fp64) on the GPU."""
+    n = 100_000
+    rp, col, val = lhpc.gen_uniform_csr(n, n, 10, dtype=lhpc.F64)
+    x = lhpc.gen_values(lhpc.F64, 0, n, lhpc.SEED_X)
+    y, _ = _run(lhpc, gpu, rp, col, val, x, n, 0)
+    y64, _, asum = S.spmv_oracle(rp, col, val, x)
+    S.assert_spmv_close(y, y64, asum)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_full_size_c2_c3(lhpc, gpu, dtype):
+    """BASELINE configs[1]/[2] shape: n=10M, 15/row (nnz=150M) against the
+    oracle on every row, plus the dyadic twin bit-exact, plus exact
+    linearity A(2x) = 2·A(x) and run-to-run determinism."""
+    import torch
+    dt = lhpc.F32 if dtype == "f32" else lhpc.F64
+    n = 10_000_000
+    for dist in (0, 1):
+        rp, col, val = lhpc.gen_uniform_csr(n, n, 15, dtype=dt, dist=dist)
+        x = lhpc.gen_values(dt, dist, n, lhpc.SEED_X)
+        with lhpc.SpMVPlan(rp, col, val, n) as plan:
+            if dt == lhpc.F32:
+                assert plan.info()["kernel"] == lhpc.KERNEL_XSLICE
+            xd = torch.from_numpy(x).to(gpu)
+            y1 = plan(xd).clone()
+            y2 = plan(xd).clone()
+            y2x = plan(xd * 2)
+            torch.cuda.synchronize()
+            assert torch.equal(y1, y2), "SpMV must be deterministic run to run"
+            assert torch.equal(y2x, y1 * 2), "A(2x) must equal 2·A(x) exactly"
+            y = y1.cpu().numpy()
+        y64, yr, asum = S.spmv_oracle(rp, col, val, x)
+        if dist == 1:
+            assert np.array_equal(y, yr)
+        else:
+            S.assert_spmv_close(y, y64, asum)
+        del rp, col, val
+
+
+def test_partitioned_blocks_concatenate_bit_exact(lhpc, gpu):
+    """Row-block split used by multi-GPU runs: per-block plans (rebased row_ptr,
+    global columns) concatenate to exactly the unpartitioned y."""
+    import torch
+    n = 300_000
+    rp, col, val = lhpc.gen_uniform_csr(n, n, 15, dtype=lhpc.F32)
+    x = lhpc.gen_values(lhpc.F32, 0, n, lhpc.SEED_X)
+    xd = torch.from_numpy(x).to(gpu)
+    with lhpc.SpMVPlan(rp, col, val, n, flags=FAMILIES["rowgroup"]) as plan:
+        y_full = plan(xd).cpu().numpy()
+    cuts = lhpc.csr_partition_rows(rp, 4)
+    parts = []
+    for p in range(4):
+        r0, r1 = int(cuts[p]), int(cuts[p + 1])
+        lrp = (rp[r0:r1 + 1] - rp[r0]).astype(np.int32)
+        with lhpc.SpMVPlan(lrp, col[rp[r0]:rp[r1]], val[rp[r0]:rp[r1]], n,
+                           flags=FAMILIES["rowgroup"]) as plan:
+            parts.append(plan(xd).cpu().numpy())
+    assert np.array_equal(np.concatenate(parts), y_full)

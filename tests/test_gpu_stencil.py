@@ -1,0 +1,114 @@
+"""GPU parity for the ghost-cell stencils through the C ABI.
+
+blur_x / blur_y must be BIT-EXACT against (a) the golden fixtures produced by
+the reference's own HPCHighDimensionFlatArray + BM_x_blur/BM_y_blur loop
+(oracle/_ref/ref_probe, tests/golden/make_golden.py) and (b) the C oracle at
+other shapes, up to the reference's 8192² grid.  stencil7 is bit-exact
+against the oracle (both evaluate the same order without contraction).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from tests import _support as S
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN_BLUR = sorted(glob.glob(os.path.join(S.GOLDEN, "blur_*.npz")))
+
+
+def _dev(gpu, a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+
+
+@pytest.mark.parametrize("buffers", ["device", "host"])
+@pytest.mark.parametrize("path", GOLDEN_BLUR, ids=lambda p: os.path.basename(p)[:-4])
+def test_blur_golden_bit_exact(lhpc, gpu, path, buffers):
+    g = S.load_golden(os.path.basename(path))
+    ny, nx, ghost, nb = (int(g[k]) for k in ("ny", "nx", "ghost", "nblur"))
+    fn = lhpc.blur_y if os.path.basename(path).startswith("blur_y") else lhpc.blur_x
+    if buffers == "device":
+        import torch
+        b = torch.empty(ny * nx, dtype=torch.float32, device=gpu)
+        out = fn(_dev(gpu, g["a"]), b, ny, nx, ghost, nb).cpu().numpy()
+    else:
+        out = fn(g["a"].copy(), np.empty(ny * nx, dtype=np.float32), ny, nx, ghost, nb)
+    assert np.array_equal(out, g["b"])
+
+
+SHAPES = [(1, 1, 8), (3, 5, 8), (17, 33, 8), (64, 1000, 8), (257, 131, 12), (100, 96, 8),
+          (33, 64, 3), (512, 1024, 8)]
+
+
+@pytest.mark.parametrize("ny,nx,ghost", SHAPES)
+@pytest.mark.parametrize("ydir", [False, True])
+def test_blur_shapes_vs_oracle(lhpc, gpu, ny, nx, ghost, ydir):
+    import torch
+    nb = min(8, ghost)
+    a = S.random_padded(((ny + 2 * ghost) * (nx + 2 * ghost),), seed=ny * 7919 + nx)
+    want = S.blur_oracle(a, ny, nx, ghost, nb, ydir)
+    b = torch.empty(ny * nx, dtype=torch.float32, device=gpu)
+    fn = lhpc.blur_y if ydir else lhpc.blur_x
+    got = fn(_dev(gpu, a), b, ny, nx, ghost, nb).cpu().numpy()
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("ydir", [False, True])
+def test_blur_reference_grid_8192(lhpc, gpu, ydir):
+    """The reference benchmark's own size: 8192², ghost 8, nblur 8."""
+    import torch
+    n, g = 8192, 8
+    a = S.random_padded(((n + 2 * g) ** 2,), seed=8192 + ydir)
+    want = S.blur_oracle(a, n, n, g, 8, ydir)
+    b = torch.empty(n * n, dtype=torch.float32, device=gpu)
+    got = (lhpc.blur_y if ydir else lhpc.blur_x)(_dev(gpu, a), b, n, n, g, 8).cpu().numpy()
+    assert np.array_equal(got, want)
+
+
+def test_blur_rejects_narrow_ghost(lhpc):
+    a = np.zeros((4 + 4) * (4 + 4), dtype=np.float32)
+    with pytest.raises(lhpc.LhpcError):
+        lhpc.blur_x(a, np.zeros(16, dtype=np.float32), 4, 4, 2, 8)
+
+
+@pytest.mark.parametrize("nz,ny,nx", [(1, 1, 1), (2, 3, 5), (16, 17, 65), (33, 64, 64), (64, 96, 130)])
+def test_stencil7_vs_oracle(lhpc, gpu, nz, ny, nx):
+    g = 1
+    shape = (nz + 2, ny + 2, nx + 2)
+    u = S.random_padded(shape, seed=nz * 131 + nx, zero_ghost=False).reshape(-1)
+    out0 = S.random_padded(shape, seed=99).reshape(-1)  # ghosts of `out` must survive
+    want = S.stencil7_oracle(u, nz, ny, nx, g, -6.0, 1.0, out=out0.copy())
+    got = lhpc.stencil7(_dev(gpu, u), _dev(gpu, out0), nz, ny, nx, g, -6.0, 1.0).cpu().numpy()
+    assert np.array_equal(got, want)
+    # host-buffer path
+    got_h = lhpc.stencil7(u.copy(), out0.copy(), nz, ny, nx, g, -6.0, 1.0)
+    assert np.array_equal(got_h, want)
+
+
+def test_stencil7_planes_compose(lhpc, gpu):
+    """Computing z-plane ranges separately (the halo-overlap schedule) gives
+    exactly the full sweep."""
+    nz, ny, nx = 40, 30, 70
+    shape = (nz + 2, ny + 2, nx + 2)
+    u = _dev(gpu, S.random_padded(shape, seed=5).reshape(-1))
+    full = lhpc.stencil7(u, _dev(gpu, np.zeros(np.prod(shape), np.float32)), nz, ny, nx, 1, -6.0, 1.0)
+    part = _dev(gpu, np.zeros(np.prod(shape), np.float32))
+    for z0, z1 in ((0, 1), (1, 17), (17, 39), (39, 40)):
+        lhpc.stencil7_planes(u, part, nz, ny, nx, 1, -6.0, 1.0, z0, z1)
+    import torch
+    assert torch.equal(full, part)
+
+
+@pytest.mark.slow
+def test_stencil7_c5_size(lhpc, gpu):
+    """BASELINE configs[4] grid (512³, Dirichlet-0 ghosts, c0=-6, c1=1)."""
+    n, g = 512, 1
+    shape = (n + 2,) * 3
+    u = S.random_padded(shape, seed=0x5EED0005, zero_ghost=True, ghost=1).reshape(-1)
+    want = S.stencil7_oracle(u, n, n, n, g, -6.0, 1.0)
+    got = lhpc.stencil7(_dev(gpu, u), _dev(gpu, np.zeros_like(u)), n, n, n, g, -6.0, 1.0).cpu().numpy()
+    assert np.array_equal(got, want)

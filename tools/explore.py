@@ -91,14 +91,31 @@ def main():
             samp = np.random.default_rng(0).integers(0, n, 2000)
             ref = np.array([np.dot(val[rp[i]:rp[i + 1]].astype(np.float64),
                                    x[col[rp[i]:rp[i + 1]]].astype(np.float64)) for i in samp])
-            configs = ["16,1", "16,2", "16,4", "16,8", "8,2", "8,4", "32,1", "adaptive"]
+            configs = ["auto", "jag:5", "nb:1", "nb:2", "nb:3", "nb:4", "xs:2.5"]
             if dt == L.F64:
-                configs = ["16,2", "16,4", "adaptive"]
+                configs = ["auto", "jag:10", "xs:10", "xs:5", "nb:1", "nb:2"]
             for cfg in configs:
                 flags = 0
+                for k in ("LHPC_XSLICE_MB", "LHPC_XSLICE_LAYOUT", "LHPC_XSLICE_NB"):
+                    os.environ.pop(k, None)
                 if cfg == "adaptive":
                     flags = L.PLAN_FORCE_ADAPTIVE
                     os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                elif cfg == "auto":
+                    os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                elif cfg.startswith("jag:"):
+                    os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                    os.environ["LHPC_XSLICE_MB"] = cfg[4:]
+                    os.environ["LHPC_XSLICE_LAYOUT"] = "jagged"
+                    flags = L.PLAN_FORCE_XSLICE
+                elif cfg.startswith("nb:"):
+                    os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                    os.environ["LHPC_XSLICE_NB"] = cfg[3:]
+                    flags = L.PLAN_FORCE_XSLICE
+                elif cfg.startswith("xs:"):
+                    os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                    os.environ["LHPC_XSLICE_MB"] = cfg[3:]
+                    flags = L.PLAN_FORCE_XSLICE
                 else:
                     os.environ["LHPC_SPMV_ROWGROUP"] = cfg
                     flags = L.PLAN_FORCE_ROWGROUP
