@@ -65,7 +65,11 @@ enum lhpc_plan_flags {
   /* force a kernel family instead of the heuristic (testing / benchmarks)   */
   LHPC_PLAN_FORCE_ROWGROUP = 1u << 4,
   LHPC_PLAN_FORCE_ADAPTIVE = 1u << 5,
-  LHPC_PLAN_FORCE_XSLICE = 1u << 6
+  LHPC_PLAN_FORCE_XSLICE = 1u << 6,
+  /* XSLICE: keep per-slice partial sums in the value type instead of fp64
+   * (~10% faster for fp32; error bound then 2^-23·Σ|a·x| instead of
+   * 2^-24·|y| + O(2^-53)·Σ|a·x|).                                          */
+  LHPC_PLAN_FAST_PARTIALS = 1u << 7
 };
 
 /* kernel families a plan can select (lhpc_spmv_plan_info.kernel)          */

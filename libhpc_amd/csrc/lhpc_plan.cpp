@@ -30,14 +30,15 @@ int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, 
   if (o.width == 0) o.width = 64;
   const int64_t nnz = rp_at(rp, bits, n_rows) - rp_at(rp, bits, 0);
   o.nnz = nnz;
-  o.lens.reset(new uint8_t[static_cast<size_t>(S) * o.n_rows_pad]);
   o.cbase.reset(new int64_t[static_cast<size_t>(S) * o.n_chunks + 1]);
   o.col.reset(new int32_t[nnz > 0 ? nnz : 1]);
   o.val.reset(new unsigned char[(nnz > 0 ? nnz : 1) * tsz]);
   const int64_t W = o.width;
-  int bad = 0;
+  const size_t nl = static_cast<size_t>(S) * o.n_rows_pad;
+  std::unique_ptr<uint16_t[]> l16(new uint16_t[nl]);
+  int bad = 0, maxc = 0;
   // pass 1: in-slice lengths
-#pragma omp parallel for schedule(static) reduction(| : bad)
+#pragma omp parallel for schedule(static) reduction(| : bad) reduction(max : maxc)
   for (int64_t r = 0; r < o.n_rows_pad; ++r) {
     int cnt[256];
     std::memset(cnt, 0, sizeof(int) * static_cast<size_t>(S));
@@ -45,16 +46,25 @@ int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, 
       for (int64_t k = rp_at(rp, bits, r); k < rp_at(rp, bits, r + 1); ++k) ++cnt[col[k] / W];
     }
     for (int s = 0; s < S; ++s) {
-      if (cnt[s] > 255) bad = 1;
-      o.lens[static_cast<size_t>(s) * o.n_rows_pad + r] = static_cast<uint8_t>(std::min(cnt[s], 255));
+      if (cnt[s] > 65535) bad = 1;
+      maxc = std::max(maxc, cnt[s]);
+      l16[static_cast<size_t>(s) * o.n_rows_pad + r] = static_cast<uint16_t>(std::min(cnt[s], 65535));
     }
   }
-  if (bad) return LHPC_ERR_UNSUPPORTED;
+  if (bad || (jagged && maxc > 255)) return LHPC_ERR_UNSUPPORTED;
+  o.lens_bytes = maxc > 255 ? 2 : 1;
+  o.lens.reset(new uint8_t[nl * o.lens_bytes]);
+  if (o.lens_bytes == 2) {
+    std::memcpy(o.lens.get(), l16.get(), nl * 2);
+  } else {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < static_cast<int64_t>(nl); ++i) o.lens[i] = static_cast<uint8_t>(l16[i]);
+  }
   // chunk sizes → offsets, slice-major
   std::vector<int64_t> csz(static_cast<size_t>(S) * o.n_chunks);
 #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < S * o.n_chunks; ++i) {
-    const uint8_t *l = o.lens.get() + (i / o.n_chunks) * o.n_rows_pad + (i % o.n_chunks) * 64;
+    const uint16_t *l = l16.get() + (i / o.n_chunks) * o.n_rows_pad + (i % o.n_chunks) * 64;
     int64_t t = 0;
     for (int r = 0; r < 64; ++r) t += l[r];
     csz[static_cast<size_t>(i)] = t;
@@ -84,14 +94,14 @@ int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, 
         const int64_t s0 = rp_at(rp, bits, r0 + r), s1 = rp_at(rp, bits, r0 + r + 1);
         int64_t *st = start.data() + static_cast<size_t>(r) * (S + 1);
         st[0] = s0 - e0;
-        for (int s = 0; s < S; ++s) st[s + 1] = st[s] + o.lens[static_cast<size_t>(s) * o.n_rows_pad + r0 + r];
+        for (int s = 0; s < S; ++s) st[s + 1] = st[s] + l16[static_cast<size_t>(s) * o.n_rows_pad + r0 + r];
         int64_t fill[256];  // stable counting sort by slice
         for (int s = 0; s < S; ++s) fill[s] = st[s];
         for (int64_t k = s0; k < s1; ++k) order[static_cast<size_t>(fill[col[k] / W]++)] = k;
       }
       for (int s = 0; s < S; ++s) {
         int64_t pos = o.cbase[s * o.n_chunks + c];
-        const uint8_t *l = o.lens.get() + static_cast<size_t>(s) * o.n_rows_pad + r0;
+        const uint16_t *l = l16.get() + static_cast<size_t>(s) * o.n_rows_pad + r0;
         auto emit = [&](int64_t e) {
           o.col[pos] = col[e];
           std::memcpy(o.val.get() + pos * tsz, static_cast<const unsigned char *>(val) + e * tsz, tsz);

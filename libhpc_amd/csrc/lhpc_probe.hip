@@ -29,6 +29,16 @@ __global__ __launch_bounds__(256) void k_read16(const f32x4 *__restrict__ s, flo
   if (acc == 12345.678f) sink[0] = acc;  // keep the loads alive
 }
 
+// dword-per-lane streaming read (FETCH_SIZE calibration for 4-byte loads)
+__global__ __launch_bounds__(256) void k_read4(const float *__restrict__ s, float *__restrict__ sink,
+                                              int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  float acc = 0.f;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride)
+    acc += __builtin_nontemporal_load(s + i);
+  if (acc == 12345.678f) sink[0] = acc;
+}
+
 // out[i] = table[idx[i]]: a 4-byte random gather per lane with the index
 // stream read non-temporally (the SpMV x-gather in isolation).
 template <int U>
@@ -108,6 +118,12 @@ extern "C" int lhpc_probe_copy(const void *src, void *dst, int64_t bytes, int gr
 extern "C" int lhpc_probe_read(const void *src, void *sink, int64_t bytes, int grid, void *stream) {
   hipLaunchKernelGGL(k_read16, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
                      static_cast<const f32x4 *>(src), static_cast<float *>(sink), bytes / 16);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int lhpc_probe_read4(const void *src, void *sink, int64_t bytes, int grid, void *stream) {
+  hipLaunchKernelGGL(k_read4, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const float *>(src), static_cast<float *>(sink), bytes / 4);
   return static_cast<int>(hipGetLastError());
 }
 

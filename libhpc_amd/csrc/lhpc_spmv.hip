@@ -36,6 +36,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kBlockNnz = 2048;  // ADAPTIVE: nonzeros per stream block
+constexpr int kLongRow = 48;     // XSLICE: in-slice rows longer than this are wave-reduced
 
 // ------------------------------------------------------------- ROWGROUP
 template <typename T, typename I, int L, int R>
@@ -255,11 +256,11 @@ __global__ __launch_bounds__(kBlock) void k_spmv_xslice(
 // Row offsets inside the chunk come from a wave prefix sum of the uint8
 // lengths.  A chunk with more than NB·64 nonzeros loops over windows (rows
 // spanning windows keep accumulating in order, so the result is unchanged).
-template <typename T, int NB>
+template <typename T, typename P, typename LT, int NB>
 __global__ __launch_bounds__(kBlock) void k_spmv_xslice_stream(
-    const uint8_t *__restrict__ lens, const int64_t *__restrict__ cbase,
+    const LT *__restrict__ lens, const int64_t *__restrict__ cbase,
     const int32_t *__restrict__ col, const T *__restrict__ val, const T *__restrict__ x,
-    T *__restrict__ partial, int64_t n_rows, int64_t n_rows_pad, int64_t n_chunks,
+    P *__restrict__ partial, int64_t n_rows, int64_t n_rows_pad, int64_t n_chunks,
     int64_t blocks_per_slice, int S) {
   constexpr int CAP = NB * kWave;
   __shared__ double prod[kBlock / kWave][CAP];
@@ -312,25 +313,39 @@ __global__ __launch_bounds__(kBlock) void k_spmv_xslice_stream(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const int lo = off > w0 ? off : w0;
     const int hi = (off + len) < (w0 + CAP) ? (off + len) : (w0 + CAP);
-    for (int k = lo; k < hi; ++k) acc += wp[k - w0];
+    // short rows: the owning lane adds its products in CSR order
+    if (len <= kLongRow)
+      for (int k = lo; k < hi; ++k) acc += wp[k - w0];
+    // long rows (skewed matrices): the whole wave sums the row's part of the
+    // window — strided lane sums, then a fixed DPP/shuffle tree
+    uint64_t m = __ballot(len > kLongRow && lo < hi);
+    while (m) {  // wave-uniform
+      const int r = __builtin_ctzll(m);
+      m &= m - 1;
+      const int rlo = __shfl(lo, r, kWave), rhi = __shfl(hi, r, kWave);
+      double t = 0.0;
+      for (int k = rlo + lane; k < rhi; k += kWave) t += wp[k - w0];
+      t = group_sum<kWave>(t);
+      if (lane == r) acc += t;
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
   if (row < n_rows)
-    __builtin_nontemporal_store(static_cast<T>(acc), partial + static_cast<int64_t>(s) * n_rows_pad + row);
+    __builtin_nontemporal_store(static_cast<P>(acc), partial + static_cast<int64_t>(s) * n_rows_pad + row);
 }
 
 // y[i] = Σ_{s=0}^{S-1} partial[s][i], fp64, fixed slice order; 4 rows/thread.
-template <typename T>
-__global__ __launch_bounds__(kBlock) void k_xslice_reduce(const T *__restrict__ partial,
+template <typename T, typename P>
+__global__ __launch_bounds__(kBlock) void k_xslice_reduce(const P *__restrict__ partial,
                                                           T *__restrict__ y, int64_t n_rows,
                                                           int64_t n_rows_pad, int S) {
   const int64_t i0 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 4;
   if (i0 >= n_rows) return;
   double a[4] = {0.0, 0.0, 0.0, 0.0};
   for (int s = 0; s < S; ++s) {
-    const T *p = partial + static_cast<int64_t>(s) * n_rows_pad + i0;
-    if constexpr (sizeof(T) == 4) {
+    const P *p = partial + static_cast<int64_t>(s) * n_rows_pad + i0;
+    if constexpr (sizeof(P) == 4) {
       const f32x4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
       a[0] += q[0]; a[1] += q[1]; a[2] += q[2]; a[3] += q[3];
     } else {
@@ -371,9 +386,9 @@ struct lhpc_spmv_plan {
   int64_t bytes = 0;
   // XSLICE
   int S = 0;
-  int xs_jagged = 0, xs_nb = 2;
+  int xs_jagged = 0, xs_nb = 2, xs_p64 = 0, xs_lens16 = 0;
   int64_t xs_width = 0, xs_chunks = 0, xs_rows_pad = 0, xs_bps = 0;
-  uint8_t *d_lens = nullptr;
+  void *d_lens = nullptr;
   int64_t *d_cbase = nullptr;
   void *d_partial = nullptr;
 };
@@ -437,27 +452,46 @@ int launch_xslice(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s
   const dim3 g(static_cast<unsigned>(grid)), blk(kBlock);
   const T *xv = static_cast<const T *>(x);
   const T *vv = static_cast<const T *>(p->d_val);
-  T *pp = static_cast<T *>(p->d_partial);
   if (p->xs_jagged) {
-    hipLaunchKernelGGL((k_spmv_xslice<T, 4>), g, blk, 0, s, p->d_lens, p->d_cbase, p->d_col, vv, xv, pp,
-                       p->n_rows, p->xs_rows_pad, p->xs_chunks, p->xs_bps, p->S, nnz_last);
+    hipLaunchKernelGGL((k_spmv_xslice<T, 4>), g, blk, 0, s, static_cast<const uint8_t *>(p->d_lens), p->d_cbase, p->d_col, vv, xv,
+                       static_cast<T *>(p->d_partial), p->n_rows, p->xs_rows_pad, p->xs_chunks,
+                       p->xs_bps, p->S, nnz_last);
   } else {
-#define LHPC_XS_STREAM(NB)                                                                          \
-  hipLaunchKernelGGL((k_spmv_xslice_stream<T, NB>), g, blk, 0, s, p->d_lens, p->d_cbase, p->d_col, vv, \
-                     xv, pp, p->n_rows, p->xs_rows_pad, p->xs_chunks, p->xs_bps, p->S)
-    switch (p->xs_nb) {
-      case 1: LHPC_XS_STREAM(1); break;
-      case 2: LHPC_XS_STREAM(2); break;
-      case 3: LHPC_XS_STREAM(3); break;
-      default: LHPC_XS_STREAM(4); break;
+#define LHPC_XS_STREAM(P, NB)                                                                        \
+  if (p->xs_lens16)                                                                                  \
+    hipLaunchKernelGGL((k_spmv_xslice_stream<T, P, uint16_t, NB>), g, blk, 0, s,                      \
+                       static_cast<const uint16_t *>(p->d_lens), p->d_cbase, p->d_col, vv, xv,         \
+                       static_cast<P *>(p->d_partial), p->n_rows, p->xs_rows_pad, p->xs_chunks,        \
+                       p->xs_bps, p->S);                                                              \
+  else                                                                                               \
+    hipLaunchKernelGGL((k_spmv_xslice_stream<T, P, uint8_t, NB>), g, blk, 0, s,                       \
+                       static_cast<const uint8_t *>(p->d_lens), p->d_cbase, p->d_col, vv, xv,          \
+                       static_cast<P *>(p->d_partial), p->n_rows, p->xs_rows_pad, p->xs_chunks,        \
+                       p->xs_bps, p->S)
+#define LHPC_XS_NB(P)                     \
+  switch (p->xs_nb) {                     \
+    case 1: LHPC_XS_STREAM(P, 1); break;  \
+    case 2: LHPC_XS_STREAM(P, 2); break;  \
+    case 3: LHPC_XS_STREAM(P, 3); break;  \
+    default: LHPC_XS_STREAM(P, 4); break; \
+  }
+    if (p->xs_p64) {
+      LHPC_XS_NB(double)
+    } else {
+      LHPC_XS_NB(T)
     }
+#undef LHPC_XS_NB
 #undef LHPC_XS_STREAM
   }
   LHPC_TRY(check_launch(s));
   const int64_t rgrid = (p->n_rows + 4 * kBlock - 1) / (4 * kBlock);
-  hipLaunchKernelGGL((k_xslice_reduce<T>), dim3(static_cast<unsigned>(rgrid)), dim3(kBlock), 0, s,
-                     static_cast<const T *>(p->d_partial), static_cast<T *>(y), p->n_rows,
-                     p->xs_rows_pad, p->S);
+  const dim3 rg(static_cast<unsigned>(rgrid));
+  if (p->xs_p64 && !p->xs_jagged)
+    hipLaunchKernelGGL((k_xslice_reduce<T, double>), rg, blk, 0, s, static_cast<const double *>(p->d_partial),
+                       static_cast<T *>(y), p->n_rows, p->xs_rows_pad, p->S);
+  else
+    hipLaunchKernelGGL((k_xslice_reduce<T, T>), rg, blk, 0, s, static_cast<const T *>(p->d_partial),
+                       static_cast<T *>(y), p->n_rows, p->xs_rows_pad, p->S);
   return check_launch(s);
 }
 
@@ -570,8 +604,8 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
   double slice_mb = 5.0;
   if (const char *env = std::getenv("LHPC_XSLICE_MB")) slice_mb = std::max(0.25, std::atof(env));
   const bool want_xslice = (flags & LHPC_PLAN_FORCE_XSLICE) ||
-                           (!(flags & (LHPC_PLAN_FORCE_ROWGROUP | LHPC_PLAN_FORCE_ADAPTIVE)) && !adaptive &&
-                            x_bytes > 8.0e6 && maxlen <= 255);
+                           (!(flags & (LHPC_PLAN_FORCE_ROWGROUP | LHPC_PLAN_FORCE_ADAPTIVE)) &&
+                            x_bytes > 8.0e6);
   if (want_xslice && nnz > 0) {
     int P = static_cast<int>(std::ceil(x_bytes / (8.0 * slice_mb * 1.0e6)));
     P = std::max(1, std::min(P, 32));
@@ -586,6 +620,10 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
       p->kernel = LHPC_KERNEL_XSLICE;
       p->S = S;
       p->xs_jagged = jagged ? 1 : 0;
+      // fp64 partials (exact-ish: one rounding per row overall) vs partials in
+      // the value type (less traffic).  fp64 values always use fp64.
+      p->xs_p64 = (tsz == 8 || !(flags & LHPC_PLAN_FAST_PARTIALS)) && !jagged ? 1 : 0;
+      if (const char *env = std::getenv("LHPC_XSLICE_PARTIAL")) p->xs_p64 = (tsz == 8 || !std::strcmp(env, "f64")) && !jagged;
       {  // window = NB·64 nonzeros: cover a typical chunk in one window
         const double mean_chunk = xs.n_chunks ? static_cast<double>(nnz) / (static_cast<double>(S) * xs.n_chunks) : 0;
         int nb = static_cast<int>(std::ceil(mean_chunk * 1.2 / kWave));
@@ -600,12 +638,13 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
       do {
         const size_t lb = static_cast<size_t>(S) * xs.n_rows_pad;
         const size_t cb = (static_cast<size_t>(S) * xs.n_chunks + 1) * 8;
-        if ((st = dmalloc(reinterpret_cast<void **>(&p->d_lens), lb, p->bytes))) break;
+        p->xs_lens16 = xs.lens_bytes == 2 ? 1 : 0;
+        if ((st = dmalloc(&p->d_lens, lb * xs.lens_bytes, p->bytes))) break;
         if ((st = dmalloc(reinterpret_cast<void **>(&p->d_cbase), cb, p->bytes))) break;
         if ((st = dmalloc(reinterpret_cast<void **>(&p->d_col), static_cast<size_t>(nnz) * 4, p->bytes))) break;
         if ((st = dmalloc(&p->d_val, static_cast<size_t>(nnz) * tsz, p->bytes))) break;
-        if ((st = dmalloc(&p->d_partial, lb * tsz, p->bytes))) break;
-        if ((st = static_cast<int>(hipMemcpy(p->d_lens, xs.lens.get(), lb, hipMemcpyHostToDevice)))) break;
+        if ((st = dmalloc(&p->d_partial, lb * (p->xs_p64 ? 8 : tsz), p->bytes))) break;
+        if ((st = static_cast<int>(hipMemcpy(p->d_lens, xs.lens.get(), lb * xs.lens_bytes, hipMemcpyHostToDevice)))) break;
         if ((st = static_cast<int>(hipMemcpy(p->d_cbase, xs.cbase.get(), cb, hipMemcpyHostToDevice)))) break;
         if ((st = static_cast<int>(hipMemcpy(p->d_col, xs.col.get(), static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice)))) break;
         if ((st = static_cast<int>(hipMemcpy(p->d_val, xs.val.get(), static_cast<size_t>(nnz) * tsz, hipMemcpyHostToDevice)))) break;
@@ -735,7 +774,7 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
   (void)hipSetDevice(p->device);
   for (void *q : {p->d_row_ptr, static_cast<void *>(p->d_col), p->d_val,
                   static_cast<void *>(p->d_blocks), p->d_xstage, p->d_ystage,
-                  static_cast<void *>(p->d_lens), static_cast<void *>(p->d_cbase), p->d_partial})
+                  p->d_lens, static_cast<void *>(p->d_cbase), p->d_partial})
     if (q) (void)hipFree(q);
   delete p;
   return LHPC_OK;

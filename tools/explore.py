@@ -91,16 +91,19 @@ def main():
             samp = np.random.default_rng(0).integers(0, n, 2000)
             ref = np.array([np.dot(val[rp[i]:rp[i + 1]].astype(np.float64),
                                    x[col[rp[i]:rp[i + 1]]].astype(np.float64)) for i in samp])
-            configs = ["auto", "jag:5", "nb:1", "nb:2", "nb:3", "nb:4", "xs:2.5"]
+            configs = ["auto", "p64", "nb:2", "xs:2.5"]
             if dt == L.F64:
-                configs = ["auto", "jag:10", "xs:10", "xs:5", "nb:1", "nb:2"]
+                configs = ["auto", "xs:2.5"]
             for cfg in configs:
                 flags = 0
-                for k in ("LHPC_XSLICE_MB", "LHPC_XSLICE_LAYOUT", "LHPC_XSLICE_NB"):
+                for k in ("LHPC_XSLICE_MB", "LHPC_XSLICE_LAYOUT", "LHPC_XSLICE_NB", "LHPC_XSLICE_PARTIAL"):
                     os.environ.pop(k, None)
                 if cfg == "adaptive":
                     flags = L.PLAN_FORCE_ADAPTIVE
                     os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                elif cfg == "p64":
+                    os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                    os.environ["LHPC_XSLICE_PARTIAL"] = "f64"
                 elif cfg == "auto":
                     os.environ.pop("LHPC_SPMV_ROWGROUP", None)
                 elif cfg.startswith("jag:"):
