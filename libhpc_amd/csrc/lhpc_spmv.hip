@@ -335,6 +335,118 @@ __global__ __launch_bounds__(kBlock) void k_spmv_xslice_stream(
     __builtin_nontemporal_store(static_cast<P>(acc), partial + static_cast<int64_t>(s) * n_rows_pad + row);
 }
 
+// XSLICE, fused reduction.  Same per-slice work as k_spmv_xslice_stream, but
+// instead of a second kernel, the LAST of the S slice-blocks that cover a
+// 256-row block adds the S fp64 partial slabs (slice order, identical to
+// k_xslice_reduce) and writes y.  Hand-off per cdna_hip_programming.md §6
+// Guideline 16 R1: partials stored write-through (8-B agent-scope relaxed
+// atomic stores = global_store sc1), every storing wave drains vmcnt, block
+// barrier, one lane adds to the block's arrival counter (agent scope); the
+// block whose add returns S-1 takes one agent acquire (buffer_inv sc1),
+// drains, barriers, and reads the slabs with sc1 loads.  Counters are zeroed
+// by a hipMemsetAsync on the same stream before every launch.  Correct for
+// any block→XCD placement; placement only changes speed.
+template <typename T, typename LT, int NB>
+__global__ __launch_bounds__(kBlock) void k_spmv_xslice_fused(
+    const LT *__restrict__ lens, const int64_t *__restrict__ cbase,
+    const int32_t *__restrict__ col, const T *__restrict__ val, const T *__restrict__ x,
+    double *__restrict__ partial, unsigned *__restrict__ arrive, T *__restrict__ y,
+    int64_t n_rows, int64_t n_rows_pad, int64_t n_chunks, int64_t blocks_per_slice, int S) {
+  constexpr int CAP = NB * kWave;
+  __shared__ double prod[kBlock / kWave][CAP];
+  __shared__ int last_flag;
+  const int64_t b = blockIdx.x;
+  int s;
+  int64_t wb;
+  if (S >= 8) {
+    const int64_t g = b % 8, idx = b / 8;
+    s = static_cast<int>(g + 8 * (idx / blocks_per_slice));
+    wb = idx % blocks_per_slice;
+  } else {
+    s = static_cast<int>(b % S);
+    wb = b / S;
+  }
+  if (s >= S) return;  // block-uniform (only for grids rounded past S)
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = threadIdx.x / kWave;
+  const int64_t chunk = wb * (kBlock / kWave) + wv;
+  const bool live = chunk < n_chunks;  // wave-uniform; dead waves still join the barriers
+  const int64_t row = chunk * kWave + lane;
+  double acc = 0.0;
+  if (live) {
+    const int len = lens[static_cast<int64_t>(s) * n_rows_pad + row];
+    const int64_t base = cbase[static_cast<int64_t>(s) * n_chunks + chunk];
+    int inc = len;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const int t = __shfl_up(inc, d, kWave);
+      if (lane >= d) inc += t;
+    }
+    const int off = inc - len;
+    const int cnt = __shfl(inc, kWave - 1, kWave);
+    double *wp = prod[wv];
+    for (int w0 = 0; w0 < cnt; w0 += CAP) {
+      int32_t c[NB];
+      T v[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        int k = w0 + i * kWave + lane;
+        k = k < cnt ? k : cnt - 1;
+        c[i] = ld_stream(col + base + k);
+        v[i] = ld_stream(val + base + k);
+      }
+      T xv[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) xv[i] = x[c[i]];
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        wp[i * kWave + lane] = static_cast<double>(v[i]) * static_cast<double>(xv[i]);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      const int lo = off > w0 ? off : w0;
+      const int hi = (off + len) < (w0 + CAP) ? (off + len) : (w0 + CAP);
+      if (len <= kLongRow)
+        for (int k = lo; k < hi; ++k) acc += wp[k - w0];
+      uint64_t m = __ballot(len > kLongRow && lo < hi);
+      while (m) {
+        const int r = __builtin_ctzll(m);
+        m &= m - 1;
+        const int rlo = __shfl(lo, r, kWave), rhi = __shfl(hi, r, kWave);
+        double t = 0.0;
+        for (int k = rlo + lane; k < rhi; k += kWave) t += wp[k - w0];
+        t = group_sum<kWave>(t);
+        if (lane == r) acc += t;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    // R1 payload: write-through 8-byte store of this row's slice partial
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(partial + static_cast<int64_t>(s) * n_rows_pad + row),
+                       __builtin_bit_cast(unsigned long long, acc), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(arrive + wb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_flag = (old == static_cast<unsigned>(S - 1));
+    if (last_flag) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last_flag) return;  // block-uniform
+  const int64_t r = wb * kBlock + threadIdx.x;
+  if (r >= n_rows) return;
+  double a = 0.0;
+  for (int q = 0; q < S; ++q)
+    a += __builtin_bit_cast(double, __hip_atomic_load(
+                                        reinterpret_cast<unsigned long long *>(partial + static_cast<int64_t>(q) * n_rows_pad + r),
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  y[r] = static_cast<T>(a);
+}
+
 // y[i] = Σ_{s=0}^{S-1} partial[s][i], fp64, fixed slice order; 4 rows/thread.
 template <typename T, typename P>
 __global__ __launch_bounds__(kBlock) void k_xslice_reduce(const P *__restrict__ partial,
@@ -386,7 +498,8 @@ struct lhpc_spmv_plan {
   int64_t bytes = 0;
   // XSLICE
   int S = 0;
-  int xs_jagged = 0, xs_nb = 2, xs_p64 = 0, xs_lens16 = 0;
+  int xs_jagged = 0, xs_nb = 2, xs_p64 = 0, xs_lens16 = 0, xs_fused = 0;
+  unsigned *d_arrive = nullptr;  // XSLICE fused: arrival counter per 256-row block
   int64_t xs_width = 0, xs_chunks = 0, xs_rows_pad = 0, xs_bps = 0;
   void *d_lens = nullptr;
   int64_t *d_cbase = nullptr;
@@ -452,6 +565,29 @@ int launch_xslice(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s
   const dim3 g(static_cast<unsigned>(grid)), blk(kBlock);
   const T *xv = static_cast<const T *>(x);
   const T *vv = static_cast<const T *>(p->d_val);
+  if (p->xs_fused) {
+    // counters zeroed on the stream before every launch (Guideline 16: re-initialise every call)
+    LHPC_HIP_TRY(hipMemsetAsync(p->d_arrive, 0, static_cast<size_t>((p->xs_bps + 3) / 4 * 16), s));
+#define LHPC_XS_FUSED(LT, NB)                                                                      \
+  hipLaunchKernelGGL((k_spmv_xslice_fused<T, LT, NB>), g, blk, 0, s, static_cast<const LT *>(p->d_lens), \
+                     p->d_cbase, p->d_col, vv, xv, static_cast<double *>(p->d_partial), p->d_arrive,   \
+                     static_cast<T *>(y), p->n_rows, p->xs_rows_pad, p->xs_chunks, p->xs_bps, p->S)
+#define LHPC_XS_FUSED_NB(LT)                 \
+  switch (p->xs_nb) {                        \
+    case 1: LHPC_XS_FUSED(LT, 1); break;     \
+    case 2: LHPC_XS_FUSED(LT, 2); break;     \
+    case 3: LHPC_XS_FUSED(LT, 3); break;     \
+    default: LHPC_XS_FUSED(LT, 4); break;    \
+  }
+    if (p->xs_lens16) {
+      LHPC_XS_FUSED_NB(uint16_t)
+    } else {
+      LHPC_XS_FUSED_NB(uint8_t)
+    }
+#undef LHPC_XS_FUSED_NB
+#undef LHPC_XS_FUSED
+    return check_launch(s);
+  }
   if (p->xs_jagged) {
     hipLaunchKernelGGL((k_spmv_xslice<T, 4>), g, blk, 0, s, static_cast<const uint8_t *>(p->d_lens), p->d_cbase, p->d_col, vv, xv,
                        static_cast<T *>(p->d_partial), p->n_rows, p->xs_rows_pad, p->xs_chunks,
@@ -624,6 +760,12 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
       // the value type (less traffic).  fp64 values always use fp64.
       p->xs_p64 = (tsz == 8 || !(flags & LHPC_PLAN_FAST_PARTIALS)) && !jagged ? 1 : 0;
       if (const char *env = std::getenv("LHPC_XSLICE_PARTIAL")) p->xs_p64 = (tsz == 8 || !std::strcmp(env, "f64")) && !jagged;
+      // fused slice reduction (fp64 partials only): opt-in.  Measured 2.5×
+      // SLOWER than the separate reduce on C2 (3.07 vs 1.23 ms): every block
+      // waits out its store drain + arrival atomic, which costs more than the
+      // 123 µs reduce pass it removes.
+      p->xs_fused = 0;
+      if (const char *env = std::getenv("LHPC_XSLICE_FUSE")) p->xs_fused = p->xs_p64 && !jagged && std::atoi(env) != 0;
       {  // window = NB·64 nonzeros: cover a typical chunk in one window
         const double mean_chunk = xs.n_chunks ? static_cast<double>(nnz) / (static_cast<double>(S) * xs.n_chunks) : 0;
         int nb = static_cast<int>(std::ceil(mean_chunk * 1.2 / kWave));
@@ -644,6 +786,11 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
         if ((st = dmalloc(reinterpret_cast<void **>(&p->d_col), static_cast<size_t>(nnz) * 4, p->bytes))) break;
         if ((st = dmalloc(&p->d_val, static_cast<size_t>(nnz) * tsz, p->bytes))) break;
         if ((st = dmalloc(&p->d_partial, lb * (p->xs_p64 ? 8 : tsz), p->bytes))) break;
+        if (p->xs_fused) {
+          const size_t ab = static_cast<size_t>((p->xs_bps + 3) / 4 * 16);  // 16-B multiple, from the allocation start
+          if ((st = dmalloc(reinterpret_cast<void **>(&p->d_arrive), ab, p->bytes))) break;
+          if ((st = static_cast<int>(hipMemset(p->d_arrive, 0, ab)))) break;
+        }
         if ((st = static_cast<int>(hipMemcpy(p->d_lens, xs.lens.get(), lb * xs.lens_bytes, hipMemcpyHostToDevice)))) break;
         if ((st = static_cast<int>(hipMemcpy(p->d_cbase, xs.cbase.get(), cb, hipMemcpyHostToDevice)))) break;
         if ((st = static_cast<int>(hipMemcpy(p->d_col, xs.col.get(), static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice)))) break;
@@ -763,7 +910,7 @@ extern "C" int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *p, lhpc_spmv_plan_i
   info->n_long_rows = p->n_long;
   info->device_bytes = p->bytes;
   info->device = p->device;
-  info->launches = p->kernel == LHPC_KERNEL_XSLICE ? 2 : 1;
+  info->launches = p->kernel == LHPC_KERNEL_XSLICE && !p->xs_fused ? 2 : 1;
   info->slices = p->S;
   info->slice_width = p->xs_width;
   return LHPC_OK;
@@ -774,7 +921,8 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
   (void)hipSetDevice(p->device);
   for (void *q : {p->d_row_ptr, static_cast<void *>(p->d_col), p->d_val,
                   static_cast<void *>(p->d_blocks), p->d_xstage, p->d_ystage,
-                  p->d_lens, static_cast<void *>(p->d_cbase), p->d_partial})
+                  p->d_lens, static_cast<void *>(p->d_cbase), p->d_partial,
+                  static_cast<void *>(p->d_arrive)})
     if (q) (void)hipFree(q);
   delete p;
   return LHPC_OK;

@@ -22,6 +22,7 @@ FAMILIES = {
     "rowgroup": 1 << 4,
     "adaptive": 1 << 5,
     "xslice": 1 << 6,
+    "xslice_fast": (1 << 6) | (1 << 7),  # fp32 partials, separate reduce kernel
 }
 GOLDEN_SPMV = sorted(glob.glob(os.path.join(S.GOLDEN, "spmv_*.npz")))
 
@@ -45,7 +46,7 @@ def test_golden(lhpc, gpu, path, family):
     rp, col, val, x = g["row_ptr"], g["col_idx"], g["val"], g["x"]
     n_cols = int(g["n_cols"])
     y, info = _run(lhpc, gpu, rp, col, val, x, n_cols, FAMILIES[family])
-    if family == "xslice" and rp[-1] > 0:
+    if family.startswith("xslice") and rp[-1] > 0:
         assert info["kernel"] == lhpc.KERNEL_XSLICE  # long rows: uint16 lens + wave-reduced rows
     exact = g["y_exact"]
     if "dyadic" in path:
@@ -165,3 +166,15 @@ def test_partitioned_blocks_concatenate_bit_exact(lhpc, gpu):
                            flags=FAMILIES["rowgroup"]) as plan:
             parts.append(plan(xd).cpu().numpy())
     assert np.array_equal(np.concatenate(parts), y_full)
+
+
+@pytest.mark.parametrize("path", [p for p in GOLDEN_SPMV if "dyadic" in p or "powerlaw" in p],
+                         ids=lambda p: os.path.basename(p)[5:-4])
+def test_golden_xslice_fused_reduction(lhpc, gpu, path, monkeypatch):
+    """Opt-in fused slice reduction (last-arriver hand-off) gives the same bits."""
+    monkeypatch.setenv("LHPC_XSLICE_FUSE", "1")
+    g = S.load_golden(os.path.basename(path))
+    y, info = _run(lhpc, gpu, g["row_ptr"], g["col_idx"], g["val"], g["x"], int(g["n_cols"]),
+                   FAMILIES["xslice"])
+    assert info["launches"] == 1
+    assert np.array_equal(y, g["y_exact"].astype(g["val"].dtype))

@@ -91,16 +91,23 @@ def main():
             samp = np.random.default_rng(0).integers(0, n, 2000)
             ref = np.array([np.dot(val[rp[i]:rp[i + 1]].astype(np.float64),
                                    x[col[rp[i]:rp[i + 1]]].astype(np.float64)) for i in samp])
-            configs = ["auto", "p64", "nb:2", "xs:2.5"]
+            configs = ["auto", "nofuse", "fast", "xs:2.5", "nb:2", "nb:4"]
             if dt == L.F64:
-                configs = ["auto", "xs:2.5"]
+                configs = ["auto", "nofuse", "xs:2.5", "xs:10"]
             for cfg in configs:
                 flags = 0
-                for k in ("LHPC_XSLICE_MB", "LHPC_XSLICE_LAYOUT", "LHPC_XSLICE_NB", "LHPC_XSLICE_PARTIAL"):
+                for k in ("LHPC_XSLICE_MB", "LHPC_XSLICE_LAYOUT", "LHPC_XSLICE_NB", "LHPC_XSLICE_PARTIAL",
+                          "LHPC_XSLICE_FUSE"):
                     os.environ.pop(k, None)
                 if cfg == "adaptive":
                     flags = L.PLAN_FORCE_ADAPTIVE
                     os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                elif cfg == "nofuse":
+                    os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                    os.environ["LHPC_XSLICE_FUSE"] = "0"
+                elif cfg == "fast":
+                    os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                    flags = L.PLAN_FAST_PARTIALS
                 elif cfg == "p64":
                     os.environ.pop("LHPC_SPMV_ROWGROUP", None)
                     os.environ["LHPC_XSLICE_PARTIAL"] = "f64"
@@ -147,7 +154,7 @@ def main():
                 yd = torch.empty(n, dtype=xd.dtype, device=dev)
                 ref = np.array([np.dot(val[rp[i]:rp[i + 1]].astype(np.float64),
                                        x[col[rp[i]:rp[i + 1]]].astype(np.float64)) for i in samp])
-                for cfg, flags in (("auto", 0), ("rowgroup", L.PLAN_FORCE_ROWGROUP),
+                for cfg, flags in (("auto", 0), ("fast", L.PLAN_FAST_PARTIALS),
                                    ("adaptive", L.PLAN_FORCE_ADAPTIVE)):
                     plan = L.SpMVPlan(rp, col, val, n, flags=flags)
                     t = timeit(lambda: plan(xd, yd, stream=s), iters=10)
