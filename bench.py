@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--n", type=int, default=10_000_000)
     ap.add_argument("--per-row", type=int, default=15)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--chunks", type=int, default=4, help="N>1: row chunks per rank (all-gather overlap)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -111,23 +112,33 @@ def main():
         x = L.gen_values(dt, 0, n, L.SEED_X)
         nnz = int(col.shape[0])
         t_gen = time.time() - t0
-        from libhpc_amd.dist import DistSpMV, row_block
-        blk = row_block(rp, col, val, rank, world)
-        k0, k1 = int(rp[blk.r0]), int(rp[blk.r1])
-        t0 = time.time()
-        plan = L.SpMVPlan(blk.row_ptr, blk.col_idx, blk.val, n)
-        t_plan = time.time() - t0
-        info = plan.info()
+        from libhpc_amd.dist import DistSpMVOverlap, InterleavedBlocks
         xd = torch.from_numpy(x).to(dev)
-        local_rows = blk.rows
-        dsp = DistSpMV(blk, lambda xv, yv: plan(xv, yv, stream=stream), like=xd)
-        y_local = dsp.y_local
+        t0 = time.time()
+        if world == 1:
+            plans = [L.SpMVPlan(rp, col, val, n)]
+            local_nnz, local_rows = nnz, n
+            y_local = torch.empty(n, dtype=xd.dtype, device=dev)
 
-        def step():
-            if world > 1:
+            def step():
+                plans[0](xd, y_local, stream=stream)
+        else:
+            # interleaved row blocks, K chunks per rank: chunk k's RCCL
+            # all-gather overlaps the SpMV of chunk k+1 (libhpc_amd/dist.py)
+            ib = InterleavedBlocks(n, world, args.chunks)
+            plans, local_nnz = [], 0
+            for k in range(args.chunks):
+                lrp, lc, lv = ib.local_csr(rp, col, val, rank, k)
+                plans.append(L.SpMVPlan(lrp, lc, lv, n))
+                local_nnz += int(lc.shape[0])
+            local_rows = ib.B * args.chunks
+            dsp = DistSpMVOverlap(ib, [lambda xv, yv, pl=pl: pl(xv, yv, stream=stream) for pl in plans],
+                                  like=xd)
+
+            def step():
                 dsp.step(xd)
-            else:
-                plan(xd, y_local[:local_rows], stream=stream)
+        t_plan = time.time() - t0
+        info = plans[0].info()
 
         for _ in range(args.warmup):
             step()
@@ -155,13 +166,15 @@ def main():
         kev1 = torch.cuda.Event(enable_timing=True)
         reps = max(args.steps, 10)
         barrier()
+        ysc = torch.empty(max(pl.n_rows for pl in plans), dtype=xd.dtype, device=dev)
         kev0.record(stream)
         for _ in range(reps):
-            plan(xd, y_local[:local_rows], stream=stream)
+            for pl in plans:
+                pl(xd, ysc[:pl.n_rows], stream=stream)
         kev1.record(stream)
         torch.cuda.synchronize()
         call_s = kev0.elapsed_time(kev1) * 1e-3 / reps
-        local_alg = (k1 - k0) * (tsz + 4) + (local_rows + 1) * 4 + (n + local_rows) * tsz
+        local_alg = local_nnz * (tsz + 4) + (local_rows + len(plans)) * 4 + (n + local_rows) * tsz
         achieved = local_alg / call_s / 1e9
         kname = {L.KERNEL_XSLICE: "xslice", L.KERNEL_ROWGROUP: "rowgroup",
                  L.KERNEL_ADAPTIVE: "adaptive"}[info["kernel"]]
@@ -177,7 +190,7 @@ def main():
                                  "c3": "BASELINE configs[2] matrix: CSR SpMV n=10M nnz=150M fp64 uniform 15/row",
                                  "c4": "BASELINE configs[3]: power-law CSR (1..1e4 nnz/row) fp32"}[wl],
                     "n_rows": n, "n_cols": n, "nnz": nnz, "kernel": kname, "slices": info["slices"],
-                    "parallelism": f"row-block x{world}" + (" + RCCL all_gather(y)" if world > 1 else "")},
+                    "parallelism": f"row-block x{world}" + (f" (interleaved, {args.chunks} chunks/rank) + RCCL all_gather(y) overlapped" if world > 1 else "")},
             achieved_GBps=alg_bytes / per_step / 1e9,
             roofline={"bound": "hbm", "kernel": kernels, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                       "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
@@ -186,7 +199,8 @@ def main():
         )
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_spmv_baseline(rp, col, val, x, nnz, args.cpu_seconds)
-        plan.close()
+        for pl in plans:
+            pl.close()
     else:
         result.update(stencil_bench(args, L, torch, dev, stream, barrier))
         if rank == 0 and world == 1 and not args.no_cpu_baseline and wl in ("blur_x", "blur_y"):
@@ -217,17 +231,31 @@ def cpu_spmv_baseline(rp, col, val, x, nnz, seconds):
 
 def stencil_bench(args, L, torch, dev, stream, barrier):
     wl = args.workload
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
     if wl == "c5":
         n = 512
         g = 1
         P = n + 2
-        u = torch.zeros(P ** 3, device=dev)
-        u.view(P, P, P)[1:-1, 1:-1, 1:-1] = torch.rand(n, n, n, device=dev) * 2 - 1
-        o = torch.zeros_like(u)
-        fn = lambda: L.stencil7(u, o, n, n, n, g, -6.0, 1.0, stream=stream)  # noqa: E731
         cells = n ** 3
-        name = "k_stencil7"
-        workload = "BASELINE configs[4] grid: 7-point 3-D stencil 512^3 fp32, 1 GPU"
+        name = "k_stencil7_lds"
+        if world == 1:
+            u = torch.zeros(P ** 3, device=dev)
+            u.view(P, P, P)[1:-1, 1:-1, 1:-1] = torch.rand(n, n, n, device=dev) * 2 - 1
+            o = torch.zeros_like(u)
+            fn = lambda: L.stencil7(u, o, n, n, n, g, -6.0, 1.0, stream=stream)  # noqa: E731
+            workload = "BASELINE configs[4] grid: 7-point 3-D stencil 512^3 fp32, 1 GPU"
+        else:
+            from libhpc_amd.dist import DistStencil7, slab_bounds
+            z0, z1 = slab_bounds(n, rank, world)
+            nzl = z1 - z0
+            u = torch.zeros((nzl + 2) * P * P, device=dev)
+            u.view(nzl + 2, P, P)[1:-1, 1:-1, 1:-1] = torch.rand(nzl, n, n, device=dev) * 2 - 1
+            o = torch.zeros_like(u)
+            ds = DistStencil7(nzl, n, n, rank, world, lambda ut, ot, zb, ze: L.stencil7_planes(
+                ut, ot, nzl, n, n, 1, -6.0, 1.0, zb, ze, stream=stream))
+            fn = lambda: ds.step(u, o)  # noqa: E731
+            workload = f"BASELINE configs[4]: 7-point 3-D stencil 512^3 fp32, z-slabs x{world} + RCCL halo"
     else:
         n, g = 8192, 8
         a = torch.rand((n + 2 * g) ** 2, device=dev) * 2 - 1
@@ -248,10 +276,15 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
     e1.record(stream)
     barrier()
     per = e0.elapsed_time(e1) * 1e-3 / args.steps
-    ach = 8.0 * cells / per / 1e9
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([per], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        per = float(tt.item())
+    ach = 8.0 * cells / per / 1e9 / world
     out = dict(metric=f"{wl} Gcell/s (8 B/cell algorithmic)", value=cells / per / 1e9, unit="Gcell/s",
-               n_gpus=1, steps=args.steps, warmup=args.warmup, ms_per_step=per * 1e3,
-               higher_is_better=True, scaling="weak", vs_baseline=None, dtype="f32",
+               n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=per * 1e3,
+               higher_is_better=True, scaling="strong" if wl == "c5" else "weak", vs_baseline=None, dtype="f32",
                data="synthetic U[-1,1)", config={"workload": workload},
                roofline={"bound": "hbm", "kernel": name, "achieved": ach, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": None})

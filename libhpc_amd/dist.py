@@ -84,3 +84,120 @@ class DistSpMV:
         m = b.max_rows
         parts = [self.y_gather[p * m: p * m + int(b.cuts[p + 1] - b.cuts[p])] for p in range(b.world)]
         return torch.cat(parts) if out is None else torch.cat(parts, out=out)
+
+
+# --------------------------------------------------------------- stencil7
+def slab_bounds(nz: int, rank: int, world: int):
+    """Even z-slab split: rank r owns global planes [z0, z1)."""
+    base, rem = divmod(nz, world)
+    z0 = rank * base + min(rank, rem)
+    return z0, z0 + base + (1 if rank < rem else 0)
+
+
+class DistStencil7:
+    """7-point stencil on a z-slab decomposition (BASELINE config C5).
+
+    Every rank holds its slab as HPCHighDimensionFlatArray<3,float,1> of
+    logical (nzl, ny, nx): the z ghost planes are halos filled from the
+    neighbouring ranks each step (global boundary ranks keep the Dirichlet
+    ghost planes they were given).  ``step`` posts the halo send/recv
+    (torch.distributed batched P2P — RCCL over xGMI on MI355X), computes the
+    interior planes [1, nzl-1) meanwhile, then the two boundary planes.
+    ``compute(u, out, z_begin, z_end)`` is the local kernel
+    (libhpc_amd.stencil7_planes on the GPU; the oracle in CPU tests).
+    """
+
+    def __init__(self, nzl: int, ny: int, nx: int, rank: int, world: int, compute: Callable,
+                 group=None):
+        self.nzl, self.ny, self.nx = nzl, ny, nx
+        self.rank, self.world = rank, world
+        self.compute = compute
+        self.group = group
+        self.plane = (ny + 2) * (nx + 2)
+
+    def _plane(self, t, z):  # padded plane index z in [-1, nzl]
+        p = self.plane
+        return t[(z + 1) * p:(z + 2) * p]
+
+    def halo_ops(self, u):
+        import torch.distributed as dist
+        ops = []
+        if self.rank > 0:
+            ops.append(dist.P2POp(dist.isend, self._plane(u, 0), self.rank - 1, self.group))
+            ops.append(dist.P2POp(dist.irecv, self._plane(u, -1), self.rank - 1, self.group))
+        if self.rank < self.world - 1:
+            ops.append(dist.P2POp(dist.isend, self._plane(u, self.nzl - 1), self.rank + 1, self.group))
+            ops.append(dist.P2POp(dist.irecv, self._plane(u, self.nzl), self.rank + 1, self.group))
+        return ops
+
+    def step(self, u, out):
+        import torch.distributed as dist
+        ops = self.halo_ops(u) if self.world > 1 else []
+        reqs = dist.batch_isend_irecv(ops) if ops else []
+        if self.nzl > 2:
+            self.compute(u, out, 1, self.nzl - 1)          # interior: no halo needed
+        for r in reqs:
+            r.wait()
+        self.compute(u, out, 0, min(1, self.nzl))          # boundary planes
+        if self.nzl > 1:
+            self.compute(u, out, self.nzl - 1, self.nzl)
+        return out
+
+
+# ---------------------------------------------- SpMV with overlapped all-gather
+class InterleavedBlocks:
+    """Row ownership for overlapped all-gather: the rows are cut into
+    world·K blocks of B = ceil(n/(world·K)) rows; global block b = k·world + r
+    belongs to rank r as its chunk k.  The all-gather of chunk k from every
+    rank is then exactly rows [k·world·B, (k+1)·world·B) of y, so each chunk's
+    collective can run while the next chunk computes."""
+
+    def __init__(self, n_rows: int, world: int, K: int):
+        self.n, self.world, self.K = n_rows, world, K
+        self.B = -(-n_rows // (world * K)) if n_rows else 0
+
+    def rows(self, rank: int, k: int):
+        b = k * self.world + rank
+        r0 = min(b * self.B, self.n)
+        return r0, min(r0 + self.B, self.n)
+
+    def local_csr(self, row_ptr, col_idx, val, rank: int, k: int):
+        r0, r1 = self.rows(rank, k)
+        lrp = np.zeros(self.B + 1, dtype=row_ptr.dtype)  # padded to B rows (empty tail rows)
+        seg = (row_ptr[r0:r1 + 1] - row_ptr[r0]).astype(row_ptr.dtype)
+        lrp[:seg.shape[0]] = seg
+        lrp[seg.shape[0]:] = seg[-1]
+        k0, k1 = int(row_ptr[r0]), int(row_ptr[r1])
+        return lrp, col_idx[k0:k1], val[k0:k1]
+
+
+class DistSpMVOverlap:
+    """y = A·x on `world` ranks, K chunks per rank, all-gather of chunk k
+    (async, RCCL stream) overlapped with the SpMV of chunk k+1.
+
+    ``local_spmvs[k](x, y_out)`` computes the rank's chunk k (B rows)."""
+
+    def __init__(self, blocks: InterleavedBlocks, local_spmvs, like, group=None):
+        import torch
+        self.blocks = blocks
+        self.fns = local_spmvs
+        self.group = group
+        B, W, K = blocks.B, blocks.world, blocks.K
+        self.y_local = torch.zeros(K, B, dtype=like.dtype, device=like.device)
+        self.y_full = torch.empty(K * W * B, dtype=like.dtype, device=like.device)
+
+    def step(self, x):
+        import torch.distributed as dist
+        B, W, K = self.blocks.B, self.blocks.world, self.blocks.K
+        works = []
+        for k in range(K):
+            self.fns[k](x, self.y_local[k])
+            out = self.y_full[k * W * B:(k + 1) * W * B]
+            if W > 1:
+                works.append(dist.all_gather_into_tensor(out, self.y_local[k], group=self.group,
+                                                         async_op=True))
+            else:
+                out.copy_(self.y_local[k])
+        for w in works:
+            w.wait()
+        return self.y_full[:self.blocks.n]

@@ -75,3 +75,49 @@ def test_distributed_spmv_gloo(world, kind):
     assert sum(r[2] for r in res) == total
     # nnz balance: each block within one max-row of total/world
     assert max(r[2] for r in res) - min(r[2] for r in res) <= 10_000
+
+
+def _worker_overlap(rank, world, port, K, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import libhpc_amd as L
+        from libhpc_amd.dist import DistSpMVOverlap, InterleavedBlocks
+        from tests import _support as S
+        n = 10_007
+        rp, col, val = L.gen_powerlaw_csr(n, n, lmax=500, dtype=L.F32, seed=0xD160)
+        x = L.gen_values(L.F32, 0, n, 0xD161)
+        ib = InterleavedBlocks(n, world, K)
+        fns = []
+        for k in range(K):
+            lrp, lc, lv = ib.local_csr(rp, col, val, rank, k)
+
+            def f(xt, yt, lrp=lrp, lc=lc, lv=lv):  # oracle as the local product (CPU test only)
+                _, yr, _ = S.spmv_oracle(lrp, lc, lv, xt.numpy())
+                yt.copy_(torch.from_numpy(yr))
+            fns.append(f)
+        d = DistSpMVOverlap(ib, fns, like=torch.from_numpy(x))
+        y = d.step(torch.from_numpy(x)).numpy()
+        _, want, _ = S.spmv_oracle(rp, col, val, x)
+        dist.destroy_process_group()
+        q.put((rank, bool(np.array_equal(y, want))))
+    except Exception as e:
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.parametrize("world,K", [(2, 3), (3, 4), (4, 1)])
+def test_overlapped_allgather_gloo(world, K):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_overlap, args=(r, world, port, K, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    for rank, ok in res:
+        assert ok is True, f"rank {rank}: {ok}"

@@ -1,0 +1,45 @@
+"""A/B of stencil kernel variants (env knobs read per launch)."""
+import json, os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import libhpc_amd as L
+dev = torch.device("cuda:0"); st = torch.cuda.current_stream()
+def timeit(fn, iters=30):
+    for _ in range(5): fn()
+    torch.cuda.synchronize()
+    a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters): fn()
+    b.record(); torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters * 1e-3
+n, g = 8192, 8
+a = torch.rand((n + 2 * g) ** 2, device=dev) * 2 - 1
+bb = torch.empty(n * n, device=dev)
+ref = None
+for rows in ("2",):
+    os.environ["LHPC_BLUR_X_ROWS"] = rows
+    t = timeit(lambda: L.blur_x(a, bb, n, n, g, 8, stream=st))
+    out = bb.clone()
+    if ref is None: ref = out
+    print(json.dumps(dict(k="blur_x", rows=rows, us=t * 1e6, frac=8 * n * n / t / 8e12, same=bool(torch.equal(out, ref)))), flush=True)
+ref = None
+for cfg in ("4,16",):
+    os.environ["LHPC_BLUR_Y_CFG"] = cfg
+    t = timeit(lambda: L.blur_y(a, bb, n, n, g, 8, stream=st))
+    out = bb.clone()
+    if ref is None: ref = out
+    print(json.dumps(dict(k="blur_y", cfg=cfg, us=t * 1e6, frac=8 * n * n / t / 8e12, same=bool(torch.equal(out, ref)))), flush=True)
+del a, bb
+m = 512; P = m + 2
+u = torch.zeros(P ** 3, device=dev); u.view(P, P, P)[1:-1, 1:-1, 1:-1] = torch.rand(m, m, m, device=dev) * 2 - 1
+o = torch.zeros_like(u)
+ref = None
+for simple in ("ring", "wide:2,4", "wide:1,8", "wide:2,8", "wide:4,2", "wide:1,4"):
+    os.environ["LHPC_STENCIL7_IMPL"] = simple.split(":")[0]
+    if ":" in simple:
+        os.environ["LHPC_STENCIL7_WIDE"] = simple.split(":")[1]
+    t = timeit(lambda: L.stencil7(u, o, m, m, m, 1, -6.0, 1.0, stream=st))
+    out = o.clone()
+    if ref is None: ref = out
+    o.zero_()
+    print(json.dumps(dict(k="stencil7", simple=simple, us=t * 1e6, frac=8 * m ** 3 / t / 8e12, same=bool(torch.equal(out, ref)))), flush=True)

@@ -1,0 +1,4 @@
+#!/bin/bash
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
+timeout -k 10 600 python tools/explore_stencil.py > gpurun_out/explore_stencil.log 2>&1
