@@ -447,6 +447,103 @@ __global__ __launch_bounds__(kBlock) void k_spmv_xslice_fused(
   y[r] = static_cast<T>(a);
 }
 
+// XSLICE, persistent and partial-free (default for XSLICE plans).  A
+// resident grid of waves; in each pass wave w owns G consecutive 64-row
+// chunks (one row per lane per chunk, G fp64 accumulators per lane in
+// registers) and walks ALL slices in order.  Every wave moves through the
+// slices in step, so at any time the chip's L2s hold (about) one x slice —
+// no XCD mapping and no per-slice partial sums in HBM.  The G chunks of one
+// slice are contiguous (slice-major layout), so a wave streams them as one
+// range in windows of NB·64 nonzeros: col/val loads and x gathers at full
+// lane utilisation, exact fp64 products staged in a wave-private LDS window,
+// then each lane adds its rows' products in CSR order (rows longer than
+// kLongRow in one slice are summed by the whole wave).  Row sums therefore
+// accumulate slice by slice in fixed order: deterministic.
+template <typename T, typename LT, int NB, int G>
+__global__ __launch_bounds__(kBlock) void k_spmv_xslice_persist(
+    const LT *__restrict__ lens, const int64_t *__restrict__ cbase,
+    const int32_t *__restrict__ col, const T *__restrict__ val, const T *__restrict__ x,
+    T *__restrict__ y, int64_t n_rows, int64_t n_rows_pad, int64_t n_chunks, int S) {
+  constexpr int CAP = NB * kWave;
+  __shared__ double prod[kBlock / kWave][CAP];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = threadIdx.x / kWave;
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + wv;
+  const int64_t waves = static_cast<int64_t>(gridDim.x) * (kBlock / kWave);
+  const int64_t per_pass = waves * G;
+  double *wp = prod[wv];
+  for (int64_t pass = 0; pass * per_pass < n_chunks; ++pass) {
+    const int64_t c0 = pass * per_pass + w * G;
+    if (c0 >= n_chunks) break;  // wave-uniform
+    const int nc = static_cast<int>((n_chunks - c0) < G ? (n_chunks - c0) : G);
+    double acc[G];
+#pragma unroll
+    for (int c = 0; c < G; ++c) acc[c] = 0.0;
+    for (int sl = 0; sl < S; ++sl) {
+      int len[G], off[G];
+#pragma unroll
+      for (int c = 0; c < G; ++c)
+        len[c] = c < nc ? static_cast<int>(lens[static_cast<int64_t>(sl) * n_rows_pad + (c0 + c) * kWave + lane]) : 0;
+      const int64_t cb = cbase[static_cast<int64_t>(sl) * n_chunks + c0 + (lane <= nc ? lane : nc)];
+      const int64_t base = __shfl(cb, 0, kWave);
+      const int total = static_cast<int>(__shfl(cb, nc, kWave) - base);
+#pragma unroll
+      for (int c = 0; c < G; ++c) {
+        int inc = len[c];
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+          const int t = __shfl_up(inc, d, kWave);
+          if (lane >= d) inc += t;
+        }
+        off[c] = static_cast<int>(__shfl(cb, c < nc ? c : nc, kWave) - base) + inc - len[c];
+      }
+      for (int w0 = 0; w0 < total; w0 += CAP) {  // wave-uniform
+        int32_t cc[NB];
+        T vv[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          int k = w0 + i * kWave + lane;
+          k = k < total ? k : total - 1;  // clamped: loads stay unconditional
+          cc[i] = ld_stream(col + base + k);
+          vv[i] = ld_stream(val + base + k);
+        }
+        T xv[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) xv[i] = x[cc[i]];
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+          wp[i * kWave + lane] = static_cast<double>(vv[i]) * static_cast<double>(xv[i]);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+        for (int c = 0; c < G; ++c) {
+          const int lo = off[c] > w0 ? off[c] : w0;
+          const int hi = (off[c] + len[c]) < (w0 + CAP) ? (off[c] + len[c]) : (w0 + CAP);
+          if (len[c] <= kLongRow)
+            for (int k = lo; k < hi; ++k) acc[c] += wp[k - w0];
+          uint64_t m = __ballot(len[c] > kLongRow && lo < hi);
+          while (m) {  // wave-uniform
+            const int r = __builtin_ctzll(m);
+            m &= m - 1;
+            const int rlo = __shfl(lo, r, kWave), rhi = __shfl(hi, r, kWave);
+            double t = 0.0;
+            for (int k = rlo + lane; k < rhi; k += kWave) t += wp[k - w0];
+            t = group_sum<kWave>(t);
+            if (lane == r) acc[c] += t;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+      const int64_t row = (c0 + c) * kWave + lane;
+      if (c < nc && row < n_rows) __builtin_nontemporal_store(static_cast<T>(acc[c]), y + row);
+    }
+  }
+}
+
 // y[i] = Σ_{s=0}^{S-1} partial[s][i], fp64, fixed slice order; 4 rows/thread.
 template <typename T, typename P>
 __global__ __launch_bounds__(kBlock) void k_xslice_reduce(const P *__restrict__ partial,
@@ -499,6 +596,7 @@ struct lhpc_spmv_plan {
   // XSLICE
   int S = 0;
   int xs_jagged = 0, xs_nb = 2, xs_p64 = 0, xs_lens16 = 0, xs_fused = 0;
+  int xs_persist = 0, xs_grid = 0, xs_g = 8;  // persistent partial-free kernel: grid, chunks/wave/pass
   unsigned *d_arrive = nullptr;  // XSLICE fused: arrival counter per 256-row block
   int64_t xs_width = 0, xs_chunks = 0, xs_rows_pad = 0, xs_bps = 0;
   void *d_lens = nullptr;
@@ -565,6 +663,26 @@ int launch_xslice(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s
   const dim3 g(static_cast<unsigned>(grid)), blk(kBlock);
   const T *xv = static_cast<const T *>(x);
   const T *vv = static_cast<const T *>(p->d_val);
+  if (p->xs_persist) {
+#define LHPC_XS_P(LT, NB, GG)                                                                      \
+  hipLaunchKernelGGL((k_spmv_xslice_persist<T, LT, NB, GG>), dim3(static_cast<unsigned>(p->xs_grid)), blk, \
+                     0, s, static_cast<const LT *>(p->d_lens), p->d_cbase, p->d_col, vv, xv,           \
+                     static_cast<T *>(y), p->n_rows, p->xs_rows_pad, p->xs_chunks, p->S)
+#define LHPC_XS_PG(LT, NB)                    \
+  do {                                        \
+    if (p->xs_g == 16) LHPC_XS_P(LT, NB, 16); \
+    else if (p->xs_g == 4) LHPC_XS_P(LT, NB, 4); \
+    else LHPC_XS_P(LT, NB, 8);                \
+  } while (0)
+    if (p->xs_lens16) {
+      if (p->xs_nb <= 2) LHPC_XS_PG(uint16_t, 2); else LHPC_XS_PG(uint16_t, 4);
+    } else {
+      if (p->xs_nb <= 2) LHPC_XS_PG(uint8_t, 2); else LHPC_XS_PG(uint8_t, 4);
+    }
+#undef LHPC_XS_PG
+#undef LHPC_XS_P
+    return check_launch(s);
+  }
   if (p->xs_fused) {
     // counters zeroed on the stream before every launch (Guideline 16: re-initialise every call)
     LHPC_HIP_TRY(hipMemsetAsync(p->d_arrive, 0, static_cast<size_t>((p->xs_bps + 3) / 4 * 16), s));
@@ -766,6 +884,38 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
       // 123 µs reduce pass it removes.
       p->xs_fused = 0;
       if (const char *env = std::getenv("LHPC_XSLICE_FUSE")) p->xs_fused = p->xs_p64 && !jagged && std::atoi(env) != 0;
+      // persistent partial-free kernel: opt-in.  Measured slower on C2/C3/C4
+      // (1.65-2.3 ms vs 1.24 ms): each wave walks the S slices serially and
+      // its dependent window round trips are not hidden at 4-5 waves/SIMD
+      // (DESIGN.md §4).
+      p->xs_persist = 0;
+      if (const char *env = std::getenv("LHPC_XSLICE_PERSIST"))
+        p->xs_persist = !jagged && !p->xs_fused && !(flags & LHPC_PLAN_FAST_PARTIALS) && std::atoi(env) != 0;
+      if (p->xs_persist) {
+        // G chunks per wave and pass (G fp64 accumulators per lane); window NB·64
+        p->xs_g = 8;
+        if (const char *env = std::getenv("LHPC_XSLICE_G")) p->xs_g = std::atoi(env);
+        if (p->xs_g != 4 && p->xs_g != 16) p->xs_g = 8;
+        p->xs_nb = 4;
+        if (const char *env = std::getenv("LHPC_XSLICE_NB")) p->xs_nb = std::atoi(env) <= 2 ? 2 : 4;
+        int cus = 256, per_cu = 4;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+        int occ = 0;
+        const void *kfn = nullptr;
+        if (tsz == 4)
+          kfn = p->xs_g == 16 ? reinterpret_cast<const void *>(k_spmv_xslice_persist<float, uint8_t, 4, 16>)
+                : p->xs_g == 4 ? reinterpret_cast<const void *>(k_spmv_xslice_persist<float, uint8_t, 4, 4>)
+                               : reinterpret_cast<const void *>(k_spmv_xslice_persist<float, uint8_t, 4, 8>);
+        else
+          kfn = p->xs_g == 16 ? reinterpret_cast<const void *>(k_spmv_xslice_persist<double, uint8_t, 4, 16>)
+                : p->xs_g == 4 ? reinterpret_cast<const void *>(k_spmv_xslice_persist<double, uint8_t, 4, 4>)
+                               : reinterpret_cast<const void *>(k_spmv_xslice_persist<double, uint8_t, 4, 8>);
+        const hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, kBlock, 0);
+        if (oe == hipSuccess && occ > 0) per_cu = std::min(occ, 8);
+        if (const char *env = std::getenv("LHPC_XSLICE_BPC")) per_cu = std::max(1, std::atoi(env));
+        p->xs_grid = cus * per_cu;
+      }
       {  // window = NB·64 nonzeros: cover a typical chunk in one window
         const double mean_chunk = xs.n_chunks ? static_cast<double>(nnz) / (static_cast<double>(S) * xs.n_chunks) : 0;
         int nb = static_cast<int>(std::ceil(mean_chunk * 1.2 / kWave));
@@ -785,7 +935,7 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
         if ((st = dmalloc(reinterpret_cast<void **>(&p->d_cbase), cb, p->bytes))) break;
         if ((st = dmalloc(reinterpret_cast<void **>(&p->d_col), static_cast<size_t>(nnz) * 4, p->bytes))) break;
         if ((st = dmalloc(&p->d_val, static_cast<size_t>(nnz) * tsz, p->bytes))) break;
-        if ((st = dmalloc(&p->d_partial, lb * (p->xs_p64 ? 8 : tsz), p->bytes))) break;
+        if (!p->xs_persist && (st = dmalloc(&p->d_partial, lb * (p->xs_p64 ? 8 : tsz), p->bytes))) break;
         if (p->xs_fused) {
           const size_t ab = static_cast<size_t>((p->xs_bps + 3) / 4 * 16);  // 16-B multiple, from the allocation start
           if ((st = dmalloc(reinterpret_cast<void **>(&p->d_arrive), ab, p->bytes))) break;
@@ -910,7 +1060,7 @@ extern "C" int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *p, lhpc_spmv_plan_i
   info->n_long_rows = p->n_long;
   info->device_bytes = p->bytes;
   info->device = p->device;
-  info->launches = p->kernel == LHPC_KERNEL_XSLICE && !p->xs_fused ? 2 : 1;
+  info->launches = p->kernel == LHPC_KERNEL_XSLICE && !p->xs_fused && !p->xs_persist ? 2 : 1;
   info->slices = p->S;
   info->slice_width = p->xs_width;
   return LHPC_OK;

@@ -178,3 +178,36 @@ def test_golden_xslice_fused_reduction(lhpc, gpu, path, monkeypatch):
                    FAMILIES["xslice"])
     assert info["launches"] == 1
     assert np.array_equal(y, g["y_exact"].astype(g["val"].dtype))
+
+
+def test_interleaved_chunk_plans_on_gpu(lhpc, gpu):
+    """The multi-GPU data path at world=1: K interleaved chunk plans (padded
+    local CSR blocks, as bench.py --gpus N builds them) assemble to exactly
+    the single-plan y."""
+    import torch
+    from libhpc_amd.dist import DistSpMVOverlap, InterleavedBlocks
+    n = 250_003
+    rp, col, val = lhpc.gen_powerlaw_csr(n, n, lmax=3000, dtype=lhpc.F32, seed=0xE300)
+    x = lhpc.gen_values(lhpc.F32, 1, n, 0xE301)
+    xd = torch.from_numpy(x).to(gpu)
+    with lhpc.SpMVPlan(rp, col, val, n) as plan:
+        y_ref = plan(xd).cpu().numpy()
+    ib = InterleavedBlocks(n, 1, 3)
+    plans = [lhpc.SpMVPlan(*ib.local_csr(rp, col, val, 0, k), n) for k in range(3)]
+    d = DistSpMVOverlap(ib, [lambda xv, yv, p=p: p(xv, yv) for p in plans], like=xd)
+    y = d.step(xd).cpu().numpy()
+    for p in plans:
+        p.close()
+    assert np.array_equal(y, y_ref)
+
+
+@pytest.mark.parametrize("path", [p for p in GOLDEN_SPMV if "dyadic" in p or "powerlaw" in p],
+                         ids=lambda p: os.path.basename(p)[5:-4])
+def test_golden_xslice_persistent(lhpc, gpu, path, monkeypatch):
+    """Opt-in persistent partial-free XSLICE gives the same bits on dyadic data."""
+    monkeypatch.setenv("LHPC_XSLICE_PERSIST", "1")
+    g = S.load_golden(os.path.basename(path))
+    y, info = _run(lhpc, gpu, g["row_ptr"], g["col_idx"], g["val"], g["x"], int(g["n_cols"]),
+                   FAMILIES["xslice"])
+    assert info["launches"] == 1
+    assert np.array_equal(y, g["y_exact"].astype(g["val"].dtype))

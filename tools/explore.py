@@ -91,17 +91,23 @@ def main():
             samp = np.random.default_rng(0).integers(0, n, 2000)
             ref = np.array([np.dot(val[rp[i]:rp[i + 1]].astype(np.float64),
                                    x[col[rp[i]:rp[i + 1]]].astype(np.float64)) for i in samp])
-            configs = ["auto", "nofuse", "fast", "xs:2.5", "nb:2", "nb:4"]
+            configs = ["auto", "g:4", "g:16", "xs:2.5", "xs:1.25", "nb:2", "nopersist", "fast"]
             if dt == L.F64:
-                configs = ["auto", "nofuse", "xs:2.5", "xs:10"]
+                configs = ["auto", "g:4", "xs:2.5", "xs:10", "nopersist"]
             for cfg in configs:
                 flags = 0
                 for k in ("LHPC_XSLICE_MB", "LHPC_XSLICE_LAYOUT", "LHPC_XSLICE_NB", "LHPC_XSLICE_PARTIAL",
-                          "LHPC_XSLICE_FUSE"):
+                          "LHPC_XSLICE_FUSE", "LHPC_XSLICE_PERSIST", "LHPC_XSLICE_G"):
                     os.environ.pop(k, None)
                 if cfg == "adaptive":
                     flags = L.PLAN_FORCE_ADAPTIVE
                     os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                elif cfg.startswith("g:"):
+                    os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                    os.environ["LHPC_XSLICE_G"] = cfg[2:]
+                elif cfg == "nopersist":
+                    os.environ.pop("LHPC_SPMV_ROWGROUP", None)
+                    os.environ["LHPC_XSLICE_PERSIST"] = "0"
                 elif cfg == "nofuse":
                     os.environ.pop("LHPC_SPMV_ROWGROUP", None)
                     os.environ["LHPC_XSLICE_FUSE"] = "0"
@@ -125,7 +131,6 @@ def main():
                 elif cfg.startswith("xs:"):
                     os.environ.pop("LHPC_SPMV_ROWGROUP", None)
                     os.environ["LHPC_XSLICE_MB"] = cfg[3:]
-                    flags = L.PLAN_FORCE_XSLICE
                 else:
                     os.environ["LHPC_SPMV_ROWGROUP"] = cfg
                     flags = L.PLAN_FORCE_ROWGROUP
@@ -154,8 +159,15 @@ def main():
                 yd = torch.empty(n, dtype=xd.dtype, device=dev)
                 ref = np.array([np.dot(val[rp[i]:rp[i + 1]].astype(np.float64),
                                        x[col[rp[i]:rp[i + 1]]].astype(np.float64)) for i in samp])
-                for cfg, flags in (("auto", 0), ("fast", L.PLAN_FAST_PARTIALS),
-                                   ("adaptive", L.PLAN_FORCE_ADAPTIVE)):
+                for k in ("LHPC_XSLICE_MB", "LHPC_XSLICE_G", "LHPC_XSLICE_PERSIST"):
+                    os.environ.pop(k, None)
+                for cfg, flags in (("auto", 0), ("fast", L.PLAN_FAST_PARTIALS), ("g4", 0), ("xs2.5", 0)):
+                    os.environ.pop("LHPC_XSLICE_G", None)
+                    os.environ.pop("LHPC_XSLICE_MB", None)
+                    if cfg == "g4":
+                        os.environ["LHPC_XSLICE_G"] = "4"
+                    if cfg == "xs2.5":
+                        os.environ["LHPC_XSLICE_MB"] = "2.5"
                     plan = L.SpMVPlan(rp, col, val, n, flags=flags)
                     t = timeit(lambda: plan(xd, yd, stream=s), iters=10)
                     y = yd.cpu().numpy()
