@@ -203,7 +203,7 @@ def main():
             pl.close()
     else:
         result.update(stencil_bench(args, L, torch, dev, stream, barrier))
-        if rank == 0 and world == 1 and not args.no_cpu_baseline and wl in ("blur_x", "blur_y"):
+        if rank == 0 and world == 1 and not args.no_cpu_baseline and wl in ("blur_x", "blur_y", "c5"):
             result["cpu_baseline"] = result.pop("_cpu", None)
         result.pop("_cpu", None)
     if rank == 0:
@@ -238,7 +238,7 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
         g = 1
         P = n + 2
         cells = n ** 3
-        name = "k_stencil7_lds"
+        name = "k_stencil7_buf"
         if world == 1:
             u = torch.zeros(P ** 3, device=dev)
             u.view(P, P, P)[1:-1, 1:-1, 1:-1] = torch.rand(n, n, n, device=dev) * 2 - 1
@@ -287,7 +287,22 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
                higher_is_better=True, scaling="strong" if wl == "c5" else "weak", vs_baseline=None, dtype="f32",
                data="synthetic U[-1,1)", config={"workload": workload},
                roofline={"bound": "hbm", "kernel": name, "achieved": ach, "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": None})
+                         "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,
+                         "traffic": load_traffic(wl) if world == 1 else None})
+    if wl == "c5" and world == 1 and not args.no_cpu_baseline:
+        from tests import _support as S
+        lib = S.load_oracle()
+        uh = u.cpu().numpy()
+        oh = np.zeros_like(uh)
+        th = cpu_threads()
+        ts = []
+        t_end = time.perf_counter() + args.cpu_seconds
+        while len(ts) < 2 or (time.perf_counter() < t_end and len(ts) < 5000):
+            t0 = time.perf_counter()
+            lib.oracle_stencil7(uh.ctypes.data, oh.ctypes.data, n, n, n, g, -6.0, 1.0, th)
+            ts.append(time.perf_counter() - t0)
+        out["_cpu"] = {"value": cells / min(ts) / 1e9, "unit": "Gcell/s", "cores": th, "kind": "port",
+                       "sample": f"full 512^3 grid, best of {len(ts)} passes, OpenMP oracle_stencil7"}
     if wl in ("blur_x", "blur_y") and not args.no_cpu_baseline:
         from tests import _support as S
         lib = S.load_oracle()

@@ -8,6 +8,7 @@
 #include <cstdint>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 namespace {
 
@@ -16,6 +17,28 @@ __global__ __launch_bounds__(256) void k_copy16(const f32x4 *__restrict__ s, f32
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride)
     __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+}
+
+// width / cache-policy / access-order copy probes (stencil write-path study):
+// CHUNKED = false: grid-stride (the whole grid sweeps one front through memory);
+// CHUNKED = true: block b copies its own contiguous 1/grid of the buffer (grid fronts).
+template <typename T, bool NT, bool CHUNKED>
+__global__ __launch_bounds__(256) void k_copyw(const T *__restrict__ s, T *__restrict__ d, int64_t n) {
+  if constexpr (CHUNKED) {
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t b0 = static_cast<int64_t>(blockIdx.x) * per;
+    const int64_t b1 = b0 + per < n ? b0 + per : n;
+    for (int64_t i = b0 + threadIdx.x; i < b1; i += 256) {
+      if constexpr (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+      else d[i] = s[i];
+    }
+  } else {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride) {
+      if constexpr (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+      else d[i] = s[i];
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_read16(const f32x4 *__restrict__ s, float *__restrict__ sink,
@@ -133,5 +156,28 @@ extern "C" int lhpc_probe_gather(const int32_t *idx, const float *table, float *
   const int64_t blocks = (n + 256 * U - 1) / (256 * U);
   hipLaunchKernelGGL((k_gather<U>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), idx, table, out, n);
+  return static_cast<int>(hipGetLastError());
+}
+
+// width ∈ {4, 8, 16} bytes per lane; mode bit 0 = non-temporal, bit 1 = chunked (see k_copyw)
+extern "C" int lhpc_probe_copy_w(const void *src, void *dst, int64_t bytes, int grid, int width, int mode,
+                                 void *stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+#define LHPC_CW(T, W)                                                                                     \
+  do {                                                                                                    \
+    const T *sp = static_cast<const T *>(src);                                                           \
+    T *dp = static_cast<T *>(dst);                                                                        \
+    const int64_t n = bytes / W;                                                                          \
+    switch (mode & 3) {                                                                                   \
+      case 0: hipLaunchKernelGGL((k_copyw<T, false, false>), dim3(grid), dim3(256), 0, st, sp, dp, n); break; \
+      case 1: hipLaunchKernelGGL((k_copyw<T, true, false>), dim3(grid), dim3(256), 0, st, sp, dp, n); break;  \
+      case 2: hipLaunchKernelGGL((k_copyw<T, false, true>), dim3(grid), dim3(256), 0, st, sp, dp, n); break;  \
+      default: hipLaunchKernelGGL((k_copyw<T, true, true>), dim3(grid), dim3(256), 0, st, sp, dp, n); break;  \
+    }                                                                                                     \
+  } while (0)
+  if (width == 4) LHPC_CW(float, 4);
+  else if (width == 8) LHPC_CW(f32x2, 8);
+  else LHPC_CW(f32x4, 16);
+#undef LHPC_CW
   return static_cast<int>(hipGetLastError());
 }

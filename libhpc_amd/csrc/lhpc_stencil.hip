@@ -16,6 +16,7 @@
 // All three are HBM-bound (8 B/cell algorithmic: read once, write once).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -602,7 +603,7 @@ __global__ __launch_bounds__(256) void k_stencil7_ring(const float *__restrict__
 // 116 µs without stores vs 296 µs with them on the 64-wide ring).  x±1 inside
 // the tile come from shuffles / readlanes of the neighbouring block; the two
 // tile-edge values are loaded by lanes 0 and 63 as part of the plane ring.
-template <int RY, int NJ, int ZC>
+template <int RY, int NJ, int ZC, int STORE = 0>  // STORE: 0 plain, 1 non-temporal, 2 none (diagnostic)
 __global__ __launch_bounds__(256) void k_stencil7_wide(const float *__restrict__ u, float *__restrict__ out,
                                                        int64_t nz, int64_t ny, int64_t nx, int64_t g,
                                                        float c0, float c1, int64_t z_begin, int64_t z_end,
@@ -650,6 +651,7 @@ __global__ __launch_bounds__(256) void k_stencil7_wide(const float *__restrict__
 #pragma unroll
     for (int r = 0; r < RY; ++r) S.e[r] = pl[ro[r + 1] + ex];
   };
+  float diag = 0.f;
   auto step = [&](const Slot &M, const Slot &Cc, const Slot &Pp, int64_t z) {
     if (z >= ze) return;
     float *po = out + (z + g) * Pyx;
@@ -671,7 +673,14 @@ __global__ __launch_bounds__(256) void k_stencil7_wide(const float *__restrict__
         sum = __fadd_rn(sum, xm);
         sum = __fadd_rn(sum, xp);
         const float res = __fadd_rn(__fmul_rn(c0, cz), __fmul_rn(c1, sum));
-        if (x0 + kWave * j + lane < nx) po[ro[r + 1] + xo[j]] = res;
+        if constexpr (STORE == 2) {
+          diag += res;
+        } else if (x0 + kWave * j + lane < nx) {
+          if constexpr (STORE == 1)
+            __builtin_nontemporal_store(res, po + ro[r + 1] + xo[j]);
+          else
+            po[ro[r + 1] + xo[j]] = res;
+        }
       }
     }
   };
@@ -688,6 +697,130 @@ __global__ __launch_bounds__(256) void k_stencil7_wide(const float *__restrict__
     load(C, z + 5);
     step(D, A, B, z + 3);
   }
+  if constexpr (STORE == 2)
+    if (diag == 1234.5f) out[0] = diag;
+}
+
+// Buffer-addressed wide ring (default).  Same tiling and summation order as
+// k_stencil7_wide, re-addressed so the ring costs registers only for data:
+//  * loads/stores are raw buffer ops on per-row descriptors (scalar base =
+//    plane + row), voffset = one per-lane VGPR (x), the 64-float block step an
+//    immediate — no 64-bit VGPR address per load (the flat version spent ~200
+//    VGPRs on them: 340 → 1 wave/SIMD);
+//  * x±1 are DPP wave_shr:1 / wave_shl:1 moves whose lane-0 / lane-63 inputs
+//    (the neighbouring block's edge value) are readlane broadcasts, instead of
+//    ds_bpermute shuffles;
+//  * the z chunk is a runtime argument so the grid can be sized to occupancy.
+// Lanes of the last x tile may read past their row (x ≥ nx + g): those values
+// feed only lanes that are never stored; past the array end the descriptor's
+// range check returns 0.
+__device__ __forceinline__ int fbits(float v) { return __builtin_bit_cast(int, v); }
+__device__ __forceinline__ float bitsf(int v) { return __builtin_bit_cast(float, v); }
+constexpr int kDppWaveShl1 = 0x130;  // lane i ← lane i+1 (lane 63 keeps `old`)
+constexpr int kDppWaveShr1 = 0x138;  // lane i ← lane i-1 (lane 0 keeps `old`)
+
+// PF = prefetch distance in planes: the ring holds PF + 3 slots (planes z-1, z, z+1 being used,
+// PF planes in flight); its rotation is unrolled so every slot index is a compile-time constant.
+template <int RY, int NJ, int STORE, int PF = 1>  // STORE: 0 plain, 1 non-temporal, 2 none, 3 line-aligned (2, 3: diagnostics)
+__global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ u, float *__restrict__ out,
+                                                      int64_t nz, int64_t ny, int64_t nx, int64_t g,
+                                                      float c0, float c1, int64_t z_begin, int64_t z_end,
+                                                      int64_t ntx, int64_t nty, int64_t ntz, int64_t zc) {
+  constexpr int TW = NJ * kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
+  const int64_t t = xcd_tile(blockIdx.x, ntx * nty * ntz);
+  const int64_t x0 = (t % ntx) * TW;
+  const int64_t y0 = (((t / ntx) % nty) * 4 + w) * RY;
+  const int64_t zs = z_begin + (t / (ntx * nty)) * zc;
+  if (zs >= z_end || y0 >= ny) return;  // wave-uniform
+  const int64_t ze = zs + zc < z_end ? zs + zc : z_end;
+  const int64_t Px = nx + 2 * g;
+  const int64_t Pyx = (ny + 2 * g) * Px;
+  const int vx = static_cast<int>((x0 + lane + g) * 4);
+  const int ve = static_cast<int>((lane == 0 ? x0 - 1 + g : x0 + TW + g) * 4);
+  // Element offsets of rows y0-1 .. y0+RY (wave-uniform).  Every row gets its own
+  // descriptor (scalar base = plane + row, num_records = bytes left to the end
+  // of the padded array), so voffset is only x and the range check still stops
+  // the x-tile lanes past the last ghost row of the last plane.
+  int64_t rowo[RY + 2];
+#pragma unroll
+  for (int r = 0; r < RY + 2; ++r) {
+    int64_t yy = y0 - 1 + r;
+    yy = yy < ny ? yy : ny;
+    rowo[r] = (yy + g) * Px;
+  }
+  const int64_t total = (nz + 2 * g) * Pyx;  // padded array elements (u and out alike)
+  auto rsrc = [&](const float *base, int64_t z, int r) {
+    const int64_t off = ((z < nz ? z : nz) + g) * Pyx + rowo[r];
+    const int64_t left = (total - off) * 4;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base + off), 0,
+                                             static_cast<int>(left < 0x7fffffff ? left : 0x7fffffff), 0x00020000);
+  };
+  struct Slot {
+    float v[RY + 2][NJ];
+    float e[RY];
+  };
+  constexpr int NS = PF + 3;
+  Slot R[NS];
+  auto load = [&](Slot &S, int64_t z) {
+#pragma unroll
+    for (int r = 0; r < RY + 2; ++r) {
+      const auto rs = rsrc(u, z, r);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) S.v[r][j] = bitsf(__builtin_amdgcn_raw_buffer_load_b32(rs, vx + 256 * j, 0, 0));
+      if (r >= 1 && r <= RY) S.e[r - 1] = bitsf(__builtin_amdgcn_raw_buffer_load_b32(rs, ve, 0, 0));
+    }
+  };
+  float diag = 0.f;
+  auto step = [&](const Slot &M, const Slot &Cc, const Slot &Pp, int64_t z) {
+    if (z >= ze) return;
+#pragma unroll
+    for (int r = 0; r < RY; ++r) {
+      if (y0 + r >= ny) break;
+      auto ws = rsrc(out, z, r + 1);
+      if constexpr (STORE == 3) {  // diagnostic: same stores, row start rounded down to a 128-B line
+        const int64_t off = ((z < nz ? z : nz) + g) * Pyx + rowo[r + 1];
+        ws = __builtin_amdgcn_make_buffer_rsrc(out + (off & ~int64_t{31}), 0, 0x7fffffff, 0x00020000);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float cz = Cc.v[r + 1][j];
+        // bit patterns throughout: readlane/update_dpp and the b32 buffer builtins take/return
+        // integers (a float would convert by value)
+        const int lft = j > 0 ? __builtin_amdgcn_readlane(fbits(Cc.v[r + 1][j > 0 ? j - 1 : 0]), kWave - 1)
+                              : __builtin_amdgcn_readlane(fbits(Cc.e[r]), 0);
+        const int rgt = j < NJ - 1 ? __builtin_amdgcn_readlane(fbits(Cc.v[r + 1][j < NJ - 1 ? j + 1 : 0]), 0)
+                                   : __builtin_amdgcn_readlane(fbits(Cc.e[r]), kWave - 1);
+        const float xm = bitsf(__builtin_amdgcn_update_dpp(lft, fbits(cz), kDppWaveShr1, 0xF, 0xF, false));
+        const float xp = bitsf(__builtin_amdgcn_update_dpp(rgt, fbits(cz), kDppWaveShl1, 0xF, 0xF, false));
+        float sum = __fadd_rn(M.v[r + 1][j], Pp.v[r + 1][j]);
+        sum = __fadd_rn(sum, Cc.v[r][j]);
+        sum = __fadd_rn(sum, Cc.v[r + 2][j]);
+        sum = __fadd_rn(sum, xm);
+        sum = __fadd_rn(sum, xp);
+        const float res = __fadd_rn(__fmul_rn(c0, cz), __fmul_rn(c1, sum));
+        if constexpr (STORE == 2) {
+          diag += res;
+        } else if (x0 + kWave * j + lane < nx) {
+          __builtin_amdgcn_raw_buffer_store_b32(fbits(res), ws, (STORE == 3 ? vx - 4 * g : vx) + 256 * j, 0,
+                                                STORE == 1 ? 2 : 0);
+        }
+      }
+    }
+  };
+  // plane p lives in slot (p - zs + 1) mod NS
+#pragma unroll
+  for (int k = 0; k < PF + 2; ++k) load(R[k], zs - 1 + k);
+  for (int64_t z = zs; z < ze; z += NS) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      load(R[(k + PF + 2) % NS], z + k + PF + 1);
+      step(R[k % NS], R[(k + 1) % NS], R[(k + 2) % NS], z + k);
+    }
+  }
+  if constexpr (STORE == 2)
+    if (diag == 1234.5f) out[0] = diag;
 }
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -791,7 +924,8 @@ int blur_entry(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int6
 int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, int64_t g, float c0,
               float c1, int64_t zb, int64_t ze, hipStream_t s) {
   if (zb >= ze || ny == 0 || nx == 0) return LHPC_OK;
-  // implementation: ring (default); "simple", "pf", "reg", "lds" are measured alternatives
+  // implementation: buf (default); "wide", "ring", "simple", "pf", "reg", "lds" are measured
+  // alternatives
   const char *impl = std::getenv("LHPC_STENCIL7_IMPL");
   const bool use_lds = impl && !std::strcmp(impl, "lds");
   const bool simple = impl && !std::strcmp(impl, "simple");
@@ -799,17 +933,81 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
   const bool use_pf = impl && !std::strcmp(impl, "pf");
   const bool use_ring = impl && !std::strcmp(impl, "ring");
   const bool plane32 = (ny + 2 * g) * (nx + 2 * g) < (int64_t{1} << 31);
-  if (!simple && !use_pf && !use_reg && !use_lds && !use_ring && plane32) {
+  const bool use_wide = impl && !std::strcmp(impl, "wide");
+  // Store policy: "plain" | "nt" | "none" / "aligned" (timing diagnostics).  Default: plain for
+  // the buffer ring (measured 220 vs 224-272 us nt), non-temporal for the flat wide ring
+  // (234-238 vs 234-255 us).
+  const char *stm = std::getenv("LHPC_STENCIL7_STORE");
+  const bool buf_impl = !impl || !std::strcmp(impl, "buf");
+  const int store_mode = stm ? (!std::strcmp(stm, "plain") ? 0 : !std::strcmp(stm, "none") ? 2
+                                : !std::strcmp(stm, "aligned") ? 3 : 1)
+                             : (buf_impl ? 0 : 1);
+  // buffer-addressed ring: the in-row byte offset (voffset) must fit 31 bits
+  const bool row_b31 = (nx + 2 * g + 1024) * 4 < (int64_t{1} << 31);
+  if (buf_impl && row_b31) {
+    // Tiling RY×(64·NJ) per wave, 4 waves per block.  The z chunk is sized so the grid is about
+    // one block per CU (256): measured on 512^3, fewer concurrent z fronts beat
+    // more waves — 2,8 at zc 128 (256 blocks) 209-220 us vs 250 us at zc 32 (1024 blocks);
+    // prefetch depth (PF) and store policy (plain vs nt) are secondary.
+    const char *cfg = std::getenv("LHPC_STENCIL7_BUF");  // "RY,NJ,ZC[,PF]"
+    int ry = 2, nj = 8, zc = 0, pf = 1;
+    if (cfg) std::sscanf(cfg, "%d,%d,%d,%d", &ry, &nj, &zc, &pf);
+    if (zc < 1) {
+      const char *bt = std::getenv("LHPC_STENCIL7_BLOCKS");
+      const int64_t target = bt ? std::max<int64_t>(1, std::atoll(bt)) : 256;
+      const int64_t tw = int64_t{nj} * kWave, th = 4 * int64_t{ry};
+      const int64_t xy = ((nx + tw - 1) / tw) * ((ny + th - 1) / th);
+      const int64_t nchunks = std::max<int64_t>(1, (target + xy - 1) / xy);
+      zc = static_cast<int>(std::max<int64_t>(4, (ze - zb + nchunks - 1) / nchunks));
+    }
+#define LHPC_S7B_M(RY, NJ, M)                                                                         \
+  do {                                                                                                \
+    const int64_t ntx = (nx + NJ * kWave - 1) / (NJ * kWave), nty = (ny + 4 * RY - 1) / (4 * RY),        \
+                  ntz = (ze - zb + zc - 1) / zc;                                                      \
+    if (pf == 2)                                                                                      \
+      hipLaunchKernelGGL((k_stencil7_buf<RY, NJ, M, 2>), dim3(static_cast<unsigned>(ntx * nty * ntz)),  \
+                         dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
+    else if (pf == 3)                                                                                 \
+      hipLaunchKernelGGL((k_stencil7_buf<RY, NJ, M, 3>), dim3(static_cast<unsigned>(ntx * nty * ntz)),  \
+                         dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
+    else                                                                                              \
+    hipLaunchKernelGGL((k_stencil7_buf<RY, NJ, M>), dim3(static_cast<unsigned>(ntx * nty * ntz)),       \
+                       dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
+  } while (0)
+#define LHPC_S7B(RY, NJ)                                 \
+  do {                                                   \
+    if (store_mode == 1) LHPC_S7B_M(RY, NJ, 1);          \
+    else if (store_mode == 2) LHPC_S7B_M(RY, NJ, 2);     \
+    else if (store_mode == 3) LHPC_S7B_M(RY, NJ, 3);     \
+    else LHPC_S7B_M(RY, NJ, 0);                          \
+  } while (0)
+    if (ry == 1 && nj == 8) LHPC_S7B(1, 8);
+    else if (ry == 4 && nj == 8) LHPC_S7B(4, 8);
+    else if (ry == 1 && nj == 4) LHPC_S7B(1, 4);
+    else if (ry == 2 && nj == 4) LHPC_S7B(2, 4);
+    else if (ry == 4 && nj == 4) LHPC_S7B(4, 4);
+    else LHPC_S7B(2, 8);
+#undef LHPC_S7B
+#undef LHPC_S7B_M
+    return check_launch(s);
+  }
+  if ((use_wide || !impl) && plane32) {
     const char *cfg = std::getenv("LHPC_STENCIL7_WIDE");  // "RY,NJ"
     int ry = 2, nj = 8;  // measured best on 512^3
     if (cfg) std::sscanf(cfg, "%d,%d", &ry, &nj);
     constexpr int ZC = 32;
-#define LHPC_S7W(RY, NJ)                                                                             \
+#define LHPC_S7W_M(RY, NJ, M)                                                                        \
   do {                                                                                               \
     const int64_t ntx = (nx + NJ * kWave - 1) / (NJ * kWave), nty = (ny + 4 * RY - 1) / (4 * RY),       \
                   ntz = (ze - zb + ZC - 1) / ZC;                                                     \
-    hipLaunchKernelGGL((k_stencil7_wide<RY, NJ, ZC>), dim3(static_cast<unsigned>(ntx * nty * ntz)),    \
+    hipLaunchKernelGGL((k_stencil7_wide<RY, NJ, ZC, M>), dim3(static_cast<unsigned>(ntx * nty * ntz)), \
                        dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz);         \
+  } while (0)
+#define LHPC_S7W(RY, NJ)                       \
+  do {                                         \
+    if (store_mode == 1) LHPC_S7W_M(RY, NJ, 1); \
+    else if (store_mode == 2) LHPC_S7W_M(RY, NJ, 2); \
+    else LHPC_S7W_M(RY, NJ, 0);                \
   } while (0)
     if (ry == 1 && nj == 8) LHPC_S7W(1, 8);
     else if (ry == 4 && nj == 2) LHPC_S7W(4, 2);
@@ -817,6 +1015,7 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
     else if (ry == 2 && nj == 4) LHPC_S7W(2, 4);
     else LHPC_S7W(2, 8);
 #undef LHPC_S7W
+#undef LHPC_S7W_M
     return check_launch(s);
   }
   if (use_ring) {

@@ -112,3 +112,28 @@ def test_stencil7_c5_size(lhpc, gpu):
     want = S.stencil7_oracle(u, n, n, n, g, -6.0, 1.0)
     got = lhpc.stencil7(_dev(gpu, u), _dev(gpu, np.zeros_like(u)), n, n, n, g, -6.0, 1.0).cpu().numpy()
     assert np.array_equal(got, want)
+
+
+S7_IMPLS = ["buf", "buf:2,8,0,2", "buf:4,4,128,3", "buf:2,8,5,3", "buf:2,8,32", "buf:1,8,16", "buf:1,8,32", "buf:2,4,32", "buf:4,4,32", "buf:1,4,32", "buf:4,8,32",
+            "buf:2,8,4", "wide:2,8", "wide:1,8", "wide:2,4", "ring", "simple", "pf", "reg", "lds"]
+
+
+@pytest.mark.parametrize("impl", S7_IMPLS)
+@pytest.mark.parametrize("store", ["nt", "plain"])
+def test_stencil7_every_impl(lhpc, gpu, impl, store, monkeypatch):
+    """Every stencil7 implementation / tiling / store mode selectable through
+    LHPC_STENCIL7_* is bit-exact against the oracle on ragged shapes: nx
+    spanning several 512-wide x tiles with a partial last one, ny and nz not
+    multiples of the row / z-chunk tiles, ghost widths 1 and 2."""
+    name, _, cfg = impl.partition(":")
+    monkeypatch.setenv("LHPC_STENCIL7_IMPL", name)
+    if cfg:
+        monkeypatch.setenv("LHPC_STENCIL7_BUF" if name == "buf" else "LHPC_STENCIL7_WIDE", cfg)
+    monkeypatch.setenv("LHPC_STENCIL7_STORE", store)
+    for (nz, ny, nx, g) in ((37, 45, 1100, 1), (9, 19, 130, 2), (3, 2, 1, 1)):
+        shape = (nz + 2 * g, ny + 2 * g, nx + 2 * g)
+        u = S.random_padded(shape, seed=nz * 7 + nx + g, zero_ghost=False).reshape(-1)
+        out0 = S.random_padded(shape, seed=1234 + g).reshape(-1)
+        want = S.stencil7_oracle(u, nz, ny, nx, g, -6.0, 1.0, out=out0.copy())
+        got = lhpc.stencil7(_dev(gpu, u), _dev(gpu, out0), nz, ny, nx, g, -6.0, 1.0).cpu().numpy()
+        assert np.array_equal(got, want), (impl, store, nz, ny, nx, g)

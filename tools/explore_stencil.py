@@ -34,10 +34,21 @@ m = 512; P = m + 2
 u = torch.zeros(P ** 3, device=dev); u.view(P, P, P)[1:-1, 1:-1, 1:-1] = torch.rand(m, m, m, device=dev) * 2 - 1
 o = torch.zeros_like(u)
 ref = None
-for simple in ("ring", "wide:2,4", "wide:1,8", "wide:2,8", "wide:4,2", "wide:1,4"):
-    os.environ["LHPC_STENCIL7_IMPL"] = simple.split(":")[0]
-    if ":" in simple:
-        os.environ["LHPC_STENCIL7_WIDE"] = simple.split(":")[1]
+CFGS = os.environ.get("S7_CFGS", "default wide:2,8:nt buf:2,8,128:plain buf:4,4,128:plain buf:2,8,32:plain "
+                                  "buf:2,8,128:none").split()
+for simple in CFGS:
+    parts = simple.split(":")
+    if parts[0] == "default":
+        for k in ("LHPC_STENCIL7_IMPL", "LHPC_STENCIL7_BUF", "LHPC_STENCIL7_WIDE", "LHPC_STENCIL7_STORE"):
+            os.environ.pop(k, None)
+        t = timeit(lambda: L.stencil7(u, o, m, m, m, 1, -6.0, 1.0, stream=st))
+        ref = o.clone()
+        o.zero_()
+        print(json.dumps(dict(k="stencil7", simple="default", us=t * 1e6, frac=8 * m ** 3 / t / 8e12, same=True)), flush=True)
+        continue
+    os.environ["LHPC_STENCIL7_IMPL"] = parts[0]
+    os.environ["LHPC_STENCIL7_WIDE" if parts[0] == "wide" else "LHPC_STENCIL7_BUF"] = parts[1]
+    os.environ["LHPC_STENCIL7_STORE"] = parts[2] if len(parts) > 2 else "plain"
     t = timeit(lambda: L.stencil7(u, o, m, m, m, 1, -6.0, 1.0, stream=st))
     out = o.clone()
     if ref is None: ref = out
