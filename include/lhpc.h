@@ -197,6 +197,46 @@ int lhpc_gen_fill_values(int dtype, int dist, int64_t count, uint64_t seed,
  * does not fit int32)                                                       */
 int lhpc_row_ptr_narrow(const int64_t *in, int64_t n, int32_t *out);
 
+/* ------------------------------------------------------------------ sort
+ * LSD radix sort on the GPU, ascending, 8-bit digits over bits
+ * [begin_bit, end_bit) of the key (bits outside are ignored for ordering and
+ * preserved in the output).  Stable: equal keys keep their input order, so the
+ * pairs variants carry values exactly like a stable CPU sort.  n < 2^32.
+ * on_device = 1: keys/vals are HBM pointers and the call is asynchronous on
+ * `stream` (scratch: one key + value copy, stream-ordered hipMallocAsync);
+ * on_device = 0: host arrays, staged through HBM, synchronous.
+ *
+ * Replaces sort::gpu::radix::radix_sort(std::vector<uint32_t,…>&)
+ * (reference lib/gpu/radix_gpu/src/radix_sort_gpu.cpp:24-29, the 4-pass v4
+ * kernel chain lib/gpu/radix_gpu/src/cuda_radix_sort_v4.cu:17-242) — the
+ * uint32 case with begin_bit = 0, end_bit = 32 — and, on the CPU side,
+ * sort::radix::radix_sort (lib/sort/radix_cpu/include/radix_sort_cpu.hpp:326-331).
+ */
+int lhpc_radix_sort_u32(uint32_t *keys, int64_t n, int begin_bit, int end_bit,
+                        int on_device, void *stream);
+int lhpc_radix_sort_pairs_u32(uint32_t *keys, uint32_t *vals, int64_t n,
+                              int begin_bit, int end_bit, int on_device,
+                              void *stream);
+int lhpc_radix_sort_pairs_u64(uint64_t *keys, uint32_t *vals, int64_t n,
+                              int begin_bit, int end_bit, int on_device,
+                              void *stream);
+
+/* ------------------------------------------------------------ COO → CSR
+ * Builds CSR from coordinate triples (the assembly step
+ * behind sparse::to_csr(RootGrid), reference lib/sparse/include/RootGrid.hpp:20-22).
+ * Entries are ordered by (row, col) with the GPU radix sort; duplicate
+ * coordinates are merged by summing their values in input order (left to
+ * right, in the value type).  Outputs: row_ptr (n_rows+1, int32 or int64 per
+ * row_ptr_bits), col_out / val_out (capacity nnz; the first *nnz_out entries
+ * are written).  Rows/cols outside [0,n_rows)/[0,n_cols) → LHPC_ERR_INVALID_ARG.
+ * Synchronous (it returns the merged count).  on_device as for the sort.
+ */
+int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
+                    const int32_t *rows, const int32_t *cols, const void *vals,
+                    void *row_ptr, int row_ptr_bits, int32_t *col_out,
+                    void *val_out, int64_t *nnz_out, int on_device,
+                    void *stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -51,7 +51,8 @@ ABI_SYMBOLS = (
     "lhpc_blur_x_f32", "lhpc_blur_y_f32", "lhpc_stencil7_f32",
     "lhpc_stencil7_f32_planes", "lhpc_gen_uniform_row_ptr",
     "lhpc_gen_powerlaw_row_ptr", "lhpc_gen_fill_cols", "lhpc_gen_fill_values",
-    "lhpc_row_ptr_narrow",
+    "lhpc_row_ptr_narrow", "lhpc_radix_sort_u32", "lhpc_radix_sort_pairs_u32",
+    "lhpc_radix_sort_pairs_u64", "lhpc_coo_to_csr",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -118,6 +119,10 @@ _sig("lhpc_gen_powerlaw_row_ptr", _i, _i64, _i64, _d, _i64, _i64, _u64, _p, _p)
 _sig("lhpc_gen_fill_cols", _i, _i64, _i64, _p, _u64, _p)
 _sig("lhpc_gen_fill_values", _i, _i, _i, _i64, _u64, _p)
 _sig("lhpc_row_ptr_narrow", _i, _p, _i64, _p)
+_sig("lhpc_radix_sort_u32", _i, _p, _i64, _i, _i, _i, _p)
+_sig("lhpc_radix_sort_pairs_u32", _i, _p, _p, _i64, _i, _i, _i, _p)
+_sig("lhpc_radix_sort_pairs_u64", _i, _p, _p, _i64, _i, _i, _i, _p)
+_sig("lhpc_coo_to_csr", _i, _i, _i64, _i64, _i64, _p, _p, _p, _p, _i, _p, _p, C.POINTER(_i64), _i, _p)
 
 
 class LhpcError(RuntimeError):
@@ -354,3 +359,90 @@ def gen_powerlaw_csr(n_rows: int, n_cols: int, alpha: float = 1.792, lmin: int =
                                          rp.ctypes.data, C.byref(nnz)),
            "lhpc_gen_powerlaw_row_ptr")
     return _finish_csr(rp, n_rows, n_cols, seed, dtype, dist, narrow)
+
+
+# ------------------------------------------------------------ radix sort / COO→CSR
+def _elem_bytes(a) -> int:
+    return a.element_size() if _is_torch(a) else a.dtype.itemsize
+
+
+def _numel(a) -> int:
+    return a.numel() if _is_torch(a) else a.size
+
+
+def _dev_stream(a, stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream(a.device)
+    return stream
+
+
+def radix_sort(keys, begin_bit: int = 0, end_bit: Optional[int] = None, stream=None):
+    """Sort 32-bit unsigned keys in place, ascending (LSD, 8-bit digits over
+    bits [begin_bit, end_bit)).  Mirrors sort::gpu::radix::radix_sort
+    (reference lib/gpu/radix_gpu/src/radix_sort_gpu.cpp:24-29), which sorts a
+    uint32 vector in place.  ``keys``: numpy uint32 array or a contiguous
+    4-byte torch tensor on the GPU (int32 tensors are sorted as their uint32
+    bit patterns).  Returns ``keys``."""
+    if _elem_bytes(keys) != 4 or (not _is_torch(keys) and keys.dtype != np.uint32):
+        raise TypeError("radix_sort: keys must be uint32 (numpy) or a 4-byte tensor")
+    kp, kd = _buf(keys, writable=True)
+    eb = 32 if end_bit is None else end_bit
+    st = _dev_stream(keys, stream) if kd else None
+    _check(lib.lhpc_radix_sort_u32(kp, _numel(keys), begin_bit, eb, int(kd), _stream_ptr(st)),
+           "lhpc_radix_sort_u32")
+    return keys
+
+
+def radix_sort_pairs(keys, vals, begin_bit: int = 0, end_bit: Optional[int] = None, stream=None):
+    """Stable in-place sort of (key, value) pairs: keys uint32 or uint64
+    (numpy) / 4- or 8-byte tensors, values 4-byte.  Equal keys keep their
+    input order."""
+    kb = _elem_bytes(keys)
+    if kb not in (4, 8) or _elem_bytes(vals) != 4 or _numel(keys) != _numel(vals):
+        raise TypeError("radix_sort_pairs: keys 4/8-byte, values 4-byte, same length")
+    if not _is_torch(keys) and keys.dtype not in (np.uint32, np.uint64):
+        raise TypeError("radix_sort_pairs: numpy keys must be uint32 or uint64")
+    kp, kd = _buf(keys, writable=True)
+    vp, vd = _buf(vals, writable=True)
+    if kd != vd:
+        raise ValueError("keys and vals must both be host or both be device buffers")
+    eb = kb * 8 if end_bit is None else end_bit
+    st = _dev_stream(keys, stream) if kd else None
+    fn = lib.lhpc_radix_sort_pairs_u64 if kb == 8 else lib.lhpc_radix_sort_pairs_u32
+    _check(fn(kp, vp, _numel(keys), begin_bit, eb, int(kd), _stream_ptr(st)), fn.__name__)
+    return keys, vals
+
+
+def coo_to_csr(n_rows: int, n_cols: int, rows, cols, vals, row_ptr_bits: int = 64, stream=None):
+    """CSR from coordinate triples on the GPU (sort by (row, col), duplicates
+    summed in input order).  Host numpy inputs → numpy (row_ptr, col_idx, val);
+    device tensors → device tensors.  See include/lhpc.h lhpc_coo_to_csr."""
+    nnz = _numel(rows)
+    if _numel(cols) != nnz or _numel(vals) != nnz:
+        raise ValueError("rows, cols and vals must have the same length")
+    vb = _elem_bytes(vals)
+    dtype = F32 if vb == 4 else F64
+    rp_, rd = _buf(rows, None if _is_torch(rows) else np.int32)
+    cp_, cd = _buf(cols, None if _is_torch(cols) else np.int32)
+    vp_, vd = _buf(vals, None if _is_torch(vals) else (np.float32 if vb == 4 else np.float64))
+    if not (rd == cd == vd):
+        raise ValueError("inputs must all be host or all be device buffers")
+    out_n = C.c_int64(0)
+    if rd:
+        import torch
+        dev = rows.device
+        row_ptr = torch.empty(n_rows + 1, dtype=torch.int64 if row_ptr_bits == 64 else torch.int32, device=dev)
+        col = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+        val = torch.empty(max(nnz, 1), dtype=vals.dtype, device=dev)
+        st = _dev_stream(rows, stream)
+        _check(lib.lhpc_coo_to_csr(dtype, n_rows, n_cols, nnz, rp_, cp_, vp_, row_ptr.data_ptr(), row_ptr_bits,
+                                   col.data_ptr(), val.data_ptr(), C.byref(out_n), 1, _stream_ptr(st)),
+               "lhpc_coo_to_csr")
+        return row_ptr, col[:out_n.value], val[:out_n.value]
+    row_ptr = np.empty(n_rows + 1, dtype=np.int64 if row_ptr_bits == 64 else np.int32)
+    col = np.empty(max(nnz, 1), dtype=np.int32)
+    val = np.empty(max(nnz, 1), dtype=np.float32 if vb == 4 else np.float64)
+    _check(lib.lhpc_coo_to_csr(dtype, n_rows, n_cols, nnz, rp_, cp_, vp_, row_ptr.ctypes.data, row_ptr_bits,
+                               col.ctypes.data, val.ctypes.data, C.byref(out_n), 0, None), "lhpc_coo_to_csr")
+    return row_ptr, col[:out_n.value].copy(), val[:out_n.value].copy()

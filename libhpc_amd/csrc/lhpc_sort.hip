@@ -1,0 +1,567 @@
+// lhpc_sort.hip — LSD radix sort (uint32 keys; uint64 keys + uint32 values) and
+// COO→CSR assembly for gfx950.
+//
+// Reference behaviour: sort::gpu::radix::radix_sort
+// (lib/gpu/radix_gpu/src/radix_sort_gpu.cpp:24-29 → cuda_radix_sort_v4.cu:17-242)
+// sorts a uint32 vector in place with four 8-bit LSD passes; the CPU twin
+// sort::radix::radix_sort (lib/sort/radix_cpu/include/radix_sort_cpu.hpp:320-331)
+// is the same LSD counting sort.  Sorted output is unique for keys, and for
+// (key, value) pairs this sort is stable, so every result is bit-exact
+// against a stable CPU sort.
+//
+// MI355X design (not a port of the reference's hierarchical 1024-tile scan):
+//  * per 8-bit pass: upsweep (per-block digit histogram, block-major counts),
+//    scan (one workgroup per digit: per-block exclusive prefixes + digit
+//    totals), downsweep;
+//  * even-share grid sized to the resident downsweep blocks (CUs × blocks per
+//    CU, ≤ 2048): each block walks its own run of TILE-key sub-tiles in order
+//    (the next sub-tile's keys load under the current one's work), so the
+//    per-block histogram table stays ≤ 2 MB;
+//  * downsweep ranks stably inside a sub-tile with a wave64 match-any
+//    (8 ballots per key → peer mask; rank = popcount(peers & lanes below)),
+//    per-wave running digit counters in LDS, then reorders the sub-tile in
+//    LDS by digit so the global scatter writes contiguous digit runs;
+//  * only bits [begin_bit, end_bit) are used (partial last digit masked).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "lhpc_common.hpp"
+
+namespace lhpc {
+namespace {
+
+constexpr int kSortThreads = 256;
+constexpr int kSortMaxBlocks = 2048;
+
+template <typename K>
+__device__ __forceinline__ uint32_t digit_of(K k, int shift, uint32_t mask) {
+  return static_cast<uint32_t>(k >> shift) & mask;
+}
+
+// Upsweep: digit histogram of the block's sub-tiles → counts[b·256 + d].
+template <typename K, int TILE>
+__global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const K *__restrict__ keys, int64_t n,
+                                                                int shift, uint32_t mask, int64_t per_block,
+                                                                uint32_t *__restrict__ counts) {
+  __shared__ uint32_t hist[4][256];
+  const int t = threadIdx.x, w = t / kWave;
+  for (int i = t; i < 4 * 256; i += kSortThreads) (&hist[0][0])[i] = 0;
+  __syncthreads();
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * per_block * TILE;
+  const int64_t b1 = std::min<int64_t>(n, b0 + per_block * TILE);
+  int64_t i = b0 + t;
+  for (; i + 3 * kSortThreads < b1; i += 4 * kSortThreads) {
+    const K k0 = keys[i], k1 = keys[i + kSortThreads], k2 = keys[i + 2 * kSortThreads],
+            k3 = keys[i + 3 * kSortThreads];
+    atomicAdd(&hist[w][digit_of(k0, shift, mask)], 1u);
+    atomicAdd(&hist[w][digit_of(k1, shift, mask)], 1u);
+    atomicAdd(&hist[w][digit_of(k2, shift, mask)], 1u);
+    atomicAdd(&hist[w][digit_of(k3, shift, mask)], 1u);
+  }
+  for (; i < b1; i += kSortThreads) atomicAdd(&hist[w][digit_of(keys[i], shift, mask)], 1u);
+  __syncthreads();
+  counts[static_cast<int64_t>(blockIdx.x) * 256 + t] = hist[0][t] + hist[1][t] + hist[2][t] + hist[3][t];
+}
+
+// Block-wide exclusive scan of one value per thread (256 threads); returns the total.
+__device__ __forceinline__ uint32_t block_exscan256(uint32_t v, uint32_t *tmp /*[256]*/, uint32_t &total) {
+  const int t = threadIdx.x;
+  tmp[t] = v;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const uint32_t add = t >= off ? tmp[t - off] : 0u;
+    __syncthreads();
+    tmp[t] += add;
+    __syncthreads();
+  }
+  total = tmp[255];
+  const uint32_t incl = tmp[t];
+  __syncthreads();
+  return incl - v;
+}
+
+// Scan: one workgroup per digit d.  counts[b][d] → exclusive prefix over
+// blocks (in place); totals[d] = Σ_b counts[b][d].  (The digit bases — the
+// exclusive prefix of totals over digits — are formed by every downsweep block
+// from the 256 totals.)
+__global__ __launch_bounds__(kSortThreads) void k_radix_scan(uint32_t *__restrict__ counts, int nblocks,
+                                                             uint32_t *__restrict__ totals) {
+  __shared__ uint32_t tmp[256];
+  const int d = blockIdx.x, t = threadIdx.x;
+  uint32_t carry = 0;
+  for (int b0 = 0; b0 < nblocks; b0 += kSortThreads * 4) {
+    uint32_t c[4], s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int b = b0 + t * 4 + j;
+      c[j] = b < nblocks ? counts[static_cast<int64_t>(b) * 256 + d] : 0u;
+      s += c[j];
+    }
+    uint32_t total;
+    uint32_t run = carry + block_exscan256(s, tmp, total);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int b = b0 + t * 4 + j;
+      if (b < nblocks) counts[static_cast<int64_t>(b) * 256 + d] = run;
+      run += c[j];
+    }
+    carry += total;
+  }
+  if (t == 0) totals[d] = carry;
+}
+
+// Downsweep: stable rank within each sub-tile, LDS reorder, coalesced scatter.
+// Sub-tile layout: wave w owns keys [w·IPT·64, (w+1)·IPT·64) of the sub-tile,
+// visited as IPT rounds of 64 consecutive keys — so (wave, round, lane)
+// order is the input order, which makes the rank stable.
+template <typename K, bool HAS_V, int IPT>
+__global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
+    const K *__restrict__ kin, K *__restrict__ kout, const uint32_t *__restrict__ vin, uint32_t *__restrict__ vout,
+    int64_t n, int shift, uint32_t mask, int64_t per_block, const uint32_t *__restrict__ counts,
+    const uint32_t *__restrict__ totals) {
+  constexpr int TILE = IPT * kSortThreads;
+  constexpr int WSEG = IPT * kWave;
+  __shared__ K sk[TILE];
+  __shared__ uint32_t sv[HAS_V ? TILE : 1];
+  __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t tstart[256];
+  __shared__ uint32_t gbase[256];
+  __shared__ uint32_t tmp[256];
+  const int t = threadIdx.x, w = t / kWave, lane = t & (kWave - 1);
+  const uint64_t lt_mask = (uint64_t{1} << lane) - 1;
+  {
+    uint32_t all;
+    const uint32_t db = block_exscan256(totals[t], tmp, all);
+    gbase[t] = db + counts[static_cast<int64_t>(blockIdx.x) * 256 + t];
+  }
+  const int64_t first = static_cast<int64_t>(blockIdx.x) * per_block;
+  const int64_t ntiles = (n + TILE - 1) / TILE;
+  const int64_t last = std::min<int64_t>(ntiles, first + per_block);
+  K key[IPT];
+  uint32_t val[IPT];
+  auto load_tile = [&](int64_t tile, K(&kr)[IPT], uint32_t(&vr)[IPT]) {
+    const int64_t base = tile * TILE;
+    const int valid = static_cast<int>(std::min<int64_t>(TILE, n - base));
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const int p = w * WSEG + i * kWave + lane;
+      kr[i] = p < valid ? kin[base + p] : ~K(0);  // pad: max digit, ranked after every real key
+      if constexpr (HAS_V) vr[i] = p < valid ? vin[base + p] : 0u;
+    }
+  };
+  if (first < last) load_tile(first, key, val);
+  for (int64_t tile = first; tile < last; ++tile) {
+    const int64_t base = tile * TILE;
+    const int valid = static_cast<int>(std::min<int64_t>(TILE, n - base));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wcnt[w][lane + kWave * k] = 0;
+    // next sub-tile in flight under this one's rank / reorder / scatter
+    K nkey[IPT];
+    uint32_t nval[IPT];
+    if (tile + 1 < last) load_tile(tile + 1, nkey, nval);
+    uint32_t loc[IPT];
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const uint32_t d = digit_of(key[i], shift, mask);
+      uint64_t peers = ~uint64_t{0};
+#pragma unroll
+      for (int bit = 0; bit < 8; ++bit) {
+        const uint64_t bal = __ballot((d >> bit) & 1u);
+        peers &= ((d >> bit) & 1u) ? bal : ~bal;
+      }
+      const uint64_t below = peers & lt_mask;
+      const uint32_t before = wcnt[w][d];
+      loc[i] = before + static_cast<uint32_t>(__popcll(below));
+      if (below == 0) wcnt[w][d] = before + static_cast<uint32_t>(__popcll(peers));
+    }
+    __syncthreads();
+    // per digit t: exclusive prefix over waves, tile total, tile start
+    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
+    wcnt[0][t] = 0;
+    wcnt[1][t] = c0;
+    wcnt[2][t] = c0 + c1;
+    wcnt[3][t] = c0 + c1 + c2;
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    uint32_t all;
+    tstart[t] = block_exscan256(tot, tmp, all);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const uint32_t d = digit_of(key[i], shift, mask);
+      const uint32_t p = tstart[d] + wcnt[w][d] + loc[i];
+      sk[p] = key[i];
+      if constexpr (HAS_V) sv[p] = val[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int p = t + kSortThreads * k;
+      if (p < valid) {
+        const K kk = sk[p];
+        const uint32_t d = digit_of(kk, shift, mask);
+        const uint32_t g = gbase[d] + (static_cast<uint32_t>(p) - tstart[d]);
+        kout[g] = kk;
+        if constexpr (HAS_V) vout[g] = sv[p];
+      }
+    }
+    __syncthreads();
+    gbase[t] += tot;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      key[i] = nkey[i];
+      if constexpr (HAS_V) val[i] = nval[i];
+    }
+  }
+}
+
+struct DevBuf {
+  void *p = nullptr;
+  hipStream_t s = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFreeAsync(p, s);
+  }
+  hipError_t alloc(size_t bytes, hipStream_t st) {
+    s = st;
+    return hipMallocAsync(&p, bytes ? bytes : 16, st);
+  }
+};
+
+// resident downsweep blocks on this device (CUs × blocks per CU), cached per kernel
+template <typename K, bool HAS_V, int IPT>
+int64_t sort_grid_cap() {
+  static int64_t cap = 0;
+  if (!cap) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT>, kSortThreads, 0) !=
+            hipSuccess ||
+        cus <= 0 || per_cu <= 0)
+      return kSortMaxBlocks;
+    cap = std::min<int64_t>(kSortMaxBlocks, int64_t{cus} * per_cu);
+  }
+  return cap;
+}
+
+template <typename K, bool HAS_V, int IPT>
+int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, hipStream_t s) {
+  if (n <= 1 || begin_bit >= end_bit) return LHPC_OK;
+  constexpr int TILE = IPT * kSortThreads;
+  const int64_t ntiles = (n + TILE - 1) / TILE;
+  int64_t nb = std::min<int64_t>(sort_grid_cap<K, HAS_V, IPT>(), ntiles);
+  const int64_t per = (ntiles + nb - 1) / nb;
+  nb = (ntiles + per - 1) / per;
+  DevBuf k2, v2, counts, dbase;
+  LHPC_HIP_TRY(k2.alloc(static_cast<size_t>(n) * sizeof(K), s));
+  if (HAS_V) LHPC_HIP_TRY(v2.alloc(static_cast<size_t>(n) * 4, s));
+  LHPC_HIP_TRY(counts.alloc(static_cast<size_t>(nb) * 256 * 4, s));
+  LHPC_HIP_TRY(dbase.alloc(256 * 4, s));
+  K *kin = keys, *kout = static_cast<K *>(k2.p);
+  uint32_t *vin = vals, *vout = static_cast<uint32_t *>(v2.p);
+  uint32_t *cnt = static_cast<uint32_t *>(counts.p), *db = static_cast<uint32_t *>(dbase.p);
+  int passes = 0;
+  for (int shift = begin_bit; shift < end_bit; shift += 8, ++passes) {
+    const int bits = std::min(8, end_bit - shift);
+    const uint32_t mask = (1u << bits) - 1u;
+    hipLaunchKernelGGL((k_radix_upsweep<K, TILE>), dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0, s, kin,
+                       n, shift, mask, per, cnt);
+    hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(kSortThreads), 0, s, cnt, static_cast<int>(nb), db);
+    hipLaunchKernelGGL((k_radix_downsweep<K, HAS_V, IPT>), dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0,
+                       s, kin, kout, vin, vout, n, shift, mask, per, cnt, db);
+    std::swap(kin, kout);
+    if (HAS_V) std::swap(vin, vout);
+  }
+  if (passes & 1) {  // result sits in the scratch buffers
+    LHPC_HIP_TRY(hipMemcpyAsync(keys, kin, static_cast<size_t>(n) * sizeof(K), hipMemcpyDeviceToDevice, s));
+    if (HAS_V) LHPC_HIP_TRY(hipMemcpyAsync(vals, vin, static_cast<size_t>(n) * 4, hipMemcpyDeviceToDevice, s));
+  }
+  return check_launch(s);
+}
+
+// ---------------------------------------------------------------- scan (uint32 → uint32 exclusive)
+constexpr int kScanTile = 4096;  // 256 threads × 16
+
+__global__ __launch_bounds__(kSortThreads) void k_scan_reduce(const uint32_t *__restrict__ in, int64_t n,
+                                                              uint32_t *__restrict__ sums) {
+  __shared__ uint32_t tmp[256];
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kScanTile;
+  uint32_t s = 0;
+  for (int k = 0; k < kScanTile / kSortThreads; ++k) {
+    const int64_t i = b0 + k * kSortThreads + threadIdx.x;
+    if (i < n) s += in[i];
+  }
+  uint32_t total;
+  (void)block_exscan256(s, tmp, total);
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kSortThreads) void k_scan_sums(uint32_t *__restrict__ sums, int64_t nb,
+                                                            uint32_t *__restrict__ grand) {
+  __shared__ uint32_t tmp[256];
+  uint32_t carry = 0;
+  for (int64_t b0 = 0; b0 < nb; b0 += kSortThreads) {
+    const int64_t i = b0 + threadIdx.x;
+    const uint32_t v = i < nb ? sums[i] : 0u;
+    uint32_t total;
+    const uint32_t ex = block_exscan256(v, tmp, total);
+    if (i < nb) sums[i] = carry + ex;
+    carry += total;
+  }
+  if (threadIdx.x == 0 && grand) *grand = carry;
+}
+
+__global__ __launch_bounds__(kSortThreads) void k_scan_apply(const uint32_t *__restrict__ in, int64_t n,
+                                                             const uint32_t *__restrict__ sums,
+                                                             uint32_t *__restrict__ out) {
+  __shared__ uint32_t tmp[256];
+  __shared__ uint32_t tile[kScanTile + kScanTile / 32];  // +1 word per 32: conflict-free row reads
+  constexpr int E = kScanTile / kSortThreads;            // each thread scans 16 consecutive elements
+  const int t = threadIdx.x;
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kScanTile;
+  auto at = [](int i) { return i + (i >> 5); };
+#pragma unroll
+  for (int k = 0; k < E; ++k) {  // coalesced load
+    const int i = k * kSortThreads + t;
+    tile[at(i)] = b0 + i < n ? in[b0 + i] : 0u;
+  }
+  __syncthreads();
+  uint32_t v[E], s = 0;
+#pragma unroll
+  for (int k = 0; k < E; ++k) {
+    v[k] = tile[at(t * E + k)];
+    s += v[k];
+  }
+  uint32_t total;
+  uint32_t run = sums[blockIdx.x] + block_exscan256(s, tmp, total);
+#pragma unroll
+  for (int k = 0; k < E; ++k) {
+    tile[at(t * E + k)] = run;
+    run += v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < E; ++k) {  // coalesced store
+    const int i = k * kSortThreads + t;
+    if (b0 + i < n) out[b0 + i] = tile[at(i)];
+  }
+}
+
+// exclusive scan in → out (may alias), grand total to *grand (device) if non-null
+int exclusive_scan_u32(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *grand, hipStream_t s) {
+  if (n <= 0) return LHPC_OK;
+  const int64_t nb = (n + kScanTile - 1) / kScanTile;
+  DevBuf sums;
+  LHPC_HIP_TRY(sums.alloc(static_cast<size_t>(nb) * 4, s));
+  uint32_t *sp = static_cast<uint32_t *>(sums.p);
+  hipLaunchKernelGGL(k_scan_reduce, dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0, s, in, n, sp);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kSortThreads), 0, s, sp, nb, grand);
+  hipLaunchKernelGGL(k_scan_apply, dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0, s, in, n, sp, out);
+  return check_launch(s);
+}
+
+// ---------------------------------------------------------------- COO → CSR
+// key = row << col_bits | col; payload = the f32 value's bits (carried through the sort, so no
+// permutation gather) or, for f64 values, the input index.
+template <bool PAY_BITS>
+__global__ void k_coo_keys(const int32_t *__restrict__ rows, const int32_t *__restrict__ cols,
+                           const uint32_t *__restrict__ vbits, int64_t nnz, int64_t n_rows, int64_t n_cols,
+                           int col_bits, uint64_t *__restrict__ keys, uint32_t *__restrict__ pay,
+                           int *__restrict__ bad) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= nnz) return;
+  const int32_t r = rows[i], c = cols[i];
+  if (r < 0 || r >= n_rows || c < 0 || c >= n_cols) {
+    atomicOr(bad, 1);
+    keys[i] = 0;
+  } else {
+    keys[i] = (static_cast<uint64_t>(r) << col_bits) | static_cast<uint64_t>(c);
+  }
+  pay[i] = PAY_BITS ? vbits[i] : static_cast<uint32_t>(i);
+}
+
+__global__ void k_coo_heads(const uint64_t *__restrict__ keys, int64_t nnz, uint32_t *__restrict__ head) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < nnz) head[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+
+// one thread per run head: col, and the run's values summed in input order
+template <typename T, bool PAY_BITS>
+__global__ void k_coo_emit(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ pay,
+                           const uint32_t *__restrict__ head, const uint32_t *__restrict__ pos, int64_t nnz,
+                           int col_bits, const T *__restrict__ vals, int32_t *__restrict__ col_out,
+                           T *__restrict__ val_out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= nnz || !head[i]) return;
+  auto value = [&](int64_t j) -> T {
+    if constexpr (PAY_BITS) return __builtin_bit_cast(T, pay[j]);
+    else return vals[pay[j]];
+  };
+  const uint64_t k = keys[i];
+  T s = value(i);
+  for (int64_t j = i + 1; j < nnz && keys[j] == k; ++j) s = s + value(j);
+  const uint32_t p = pos[i];
+  col_out[p] = static_cast<int32_t>(k & ((uint64_t{1} << col_bits) - 1));
+  val_out[p] = s;
+}
+
+// row_ptr from the merged entries: thread per sorted index i that starts a new
+// row (a run head whose row differs from the previous entry's) fills
+// row_ptr[prev_row+1 .. row] = pos[i]; the last one also fills the tail.
+template <typename O>
+__global__ void k_coo_rowptr(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ pos,
+                             const uint32_t *__restrict__ grand, int64_t nnz, int64_t n_rows, int col_bits,
+                             O *__restrict__ row_ptr) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i > nnz) return;
+  const int64_t row = i < nnz ? static_cast<int64_t>(keys[i] >> col_bits) : n_rows;
+  const int64_t prev = i > 0 ? static_cast<int64_t>(keys[i - 1] >> col_bits) : -1;
+  if (row == prev) return;
+  const O p = static_cast<O>(i < nnz ? pos[i] : *grand);
+  for (int64_t r = prev + 1; r <= row; ++r) row_ptr[r] = p;
+}
+
+int bits_for(int64_t v) {  // bits to hold values in [0, v)
+  int b = 0;
+  while (b < 62 && (int64_t{1} << b) < v) ++b;
+  return b;
+}
+
+template <typename T>
+int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *rows, const int32_t *cols,
+                   const T *vals, void *row_ptr, int row_ptr_bits, int32_t *col_out, T *val_out,
+                   int64_t *nnz_out, hipStream_t s) {
+  const int cb = std::max(1, bits_for(n_cols)), rb = std::max(1, bits_for(n_rows));
+  if (cb + rb > 64) return LHPC_ERR_UNSUPPORTED;
+  DevBuf keys, idx, head, pos, flag, grand;
+  LHPC_HIP_TRY(keys.alloc(static_cast<size_t>(nnz) * 8, s));
+  LHPC_HIP_TRY(idx.alloc(static_cast<size_t>(nnz) * 4, s));
+  LHPC_HIP_TRY(head.alloc(static_cast<size_t>(nnz) * 4, s));
+  LHPC_HIP_TRY(pos.alloc(static_cast<size_t>(nnz) * 4, s));
+  LHPC_HIP_TRY(flag.alloc(8, s));
+  LHPC_HIP_TRY(grand.alloc(8, s));
+  uint64_t *kp = static_cast<uint64_t *>(keys.p);
+  uint32_t *ip = static_cast<uint32_t *>(idx.p), *hp = static_cast<uint32_t *>(head.p),
+           *pp = static_cast<uint32_t *>(pos.p);
+  int *bad = static_cast<int *>(flag.p);
+  uint32_t *gp = static_cast<uint32_t *>(grand.p);
+  LHPC_HIP_TRY(hipMemsetAsync(bad, 0, 8, s));
+  LHPC_HIP_TRY(hipMemsetAsync(gp, 0, 8, s));
+  const unsigned g = static_cast<unsigned>((std::max<int64_t>(nnz, 1) + 255) / 256);
+  constexpr bool kBits = sizeof(T) == 4;
+  if (nnz > 0) {
+    hipLaunchKernelGGL((k_coo_keys<kBits>), dim3(g), dim3(256), 0, s, rows, cols,
+                       reinterpret_cast<const uint32_t *>(vals), nnz, n_rows, n_cols, cb, kp, ip, bad);
+    LHPC_TRY((radix_sort_dev<uint64_t, true, 16>(kp, ip, nnz, 0, cb + rb, s)));
+    hipLaunchKernelGGL(k_coo_heads, dim3(g), dim3(256), 0, s, kp, nnz, hp);
+    LHPC_TRY(exclusive_scan_u32(hp, pp, nnz, gp, s));
+    hipLaunchKernelGGL((k_coo_emit<T, kBits>), dim3(g), dim3(256), 0, s, kp, ip, hp, pp, nnz, cb, vals, col_out,
+                       val_out);
+  }
+  const unsigned gr = static_cast<unsigned>((nnz + 1 + 255) / 256);
+  if (row_ptr_bits == 64)
+    hipLaunchKernelGGL((k_coo_rowptr<int64_t>), dim3(gr), dim3(256), 0, s, kp, pp, gp, nnz, n_rows, cb,
+                       static_cast<int64_t *>(row_ptr));
+  else
+    hipLaunchKernelGGL((k_coo_rowptr<int32_t>), dim3(gr), dim3(256), 0, s, kp, pp, gp, nnz, n_rows, cb,
+                       static_cast<int32_t *>(row_ptr));
+  LHPC_TRY(check_launch(s));
+  int hbad = 0;
+  uint32_t hnnz = 0;
+  LHPC_HIP_TRY(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
+  LHPC_HIP_TRY(hipMemcpyAsync(&hnnz, gp, 4, hipMemcpyDeviceToHost, s));
+  LHPC_HIP_TRY(hipStreamSynchronize(s));
+  if (hbad) return LHPC_ERR_INVALID_ARG;
+  if (nnz_out) *nnz_out = hnnz;
+  return LHPC_OK;
+}
+
+}  // namespace
+}  // namespace lhpc
+
+using namespace lhpc;
+
+namespace {
+template <typename K, bool HAS_V, int IPT>
+int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, int on_device, void *stream) {
+  constexpr int KB = static_cast<int>(sizeof(K) * 8);
+  if (n < 0 || (!keys && n > 0) || (HAS_V && !vals && n > 0) || begin_bit < 0 || end_bit > KB ||
+      begin_bit > end_bit)
+    return LHPC_ERR_INVALID_ARG;
+  if (n >= (int64_t{1} << 32)) return LHPC_ERR_UNSUPPORTED;  // 32-bit ranks
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (on_device) return radix_sort_dev<K, HAS_V, IPT>(keys, vals, n, begin_bit, end_bit, s);
+  DevBuf dk, dv;
+  LHPC_HIP_TRY(dk.alloc(static_cast<size_t>(n) * sizeof(K), s));
+  if (HAS_V) LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(n) * 4, s));
+  LHPC_HIP_TRY(hipMemcpyAsync(dk.p, keys, static_cast<size_t>(n) * sizeof(K), hipMemcpyHostToDevice, s));
+  if (HAS_V) LHPC_HIP_TRY(hipMemcpyAsync(dv.p, vals, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice, s));
+  LHPC_TRY((radix_sort_dev<K, HAS_V, IPT>(static_cast<K *>(dk.p), static_cast<uint32_t *>(dv.p), n, begin_bit,
+                                          end_bit, s)));
+  LHPC_HIP_TRY(hipMemcpyAsync(keys, dk.p, static_cast<size_t>(n) * sizeof(K), hipMemcpyDeviceToHost, s));
+  if (HAS_V) LHPC_HIP_TRY(hipMemcpyAsync(vals, dv.p, static_cast<size_t>(n) * 4, hipMemcpyDeviceToHost, s));
+  LHPC_HIP_TRY(hipStreamSynchronize(s));
+  return LHPC_OK;
+}
+}  // namespace
+
+extern "C" int lhpc_radix_sort_u32(uint32_t *keys, int64_t n, int begin_bit, int end_bit, int on_device,
+                                   void *stream) {
+  return sort_entry<uint32_t, false, 16>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
+}
+
+extern "C" int lhpc_radix_sort_pairs_u32(uint32_t *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit,
+                                         int on_device, void *stream) {
+  return sort_entry<uint32_t, true, 16>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+}
+
+extern "C" int lhpc_radix_sort_pairs_u64(uint64_t *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit,
+                                         int on_device, void *stream) {
+  return sort_entry<uint64_t, true, 16>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+}
+
+extern "C" int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *rows,
+                               const int32_t *cols, const void *vals, void *row_ptr, int row_ptr_bits,
+                               int32_t *col_out, void *val_out, int64_t *nnz_out, int on_device, void *stream) {
+  if (n_rows < 0 || n_cols < 0 || nnz < 0 || !row_ptr || (row_ptr_bits != 32 && row_ptr_bits != 64) ||
+      (nnz > 0 && (!rows || !cols || !vals || !col_out || !val_out)) || (dtype != LHPC_F32 && dtype != LHPC_F64))
+    return LHPC_ERR_INVALID_ARG;
+  if (nnz >= (int64_t{1} << 32) || (row_ptr_bits == 32 && nnz >= (int64_t{1} << 31))) return LHPC_ERR_UNSUPPORTED;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t vb = dtype == LHPC_F32 ? 4 : 8;
+  auto run = [&](const int32_t *r, const int32_t *c, const void *v, void *rp, int32_t *co, void *vo,
+                 int64_t *un) -> int {
+    if (dtype == LHPC_F32)
+      return coo_to_csr_dev<float>(n_rows, n_cols, nnz, r, c, static_cast<const float *>(v), rp, row_ptr_bits, co,
+                                   static_cast<float *>(vo), un, s);
+    return coo_to_csr_dev<double>(n_rows, n_cols, nnz, r, c, static_cast<const double *>(v), rp, row_ptr_bits, co,
+                                  static_cast<double *>(vo), un, s);
+  };
+  if (on_device) return run(rows, cols, vals, row_ptr, col_out, val_out, nnz_out);
+  const size_t rpb = static_cast<size_t>(n_rows + 1) * (row_ptr_bits / 8);
+  DevBuf dr, dc, dv, drp, dco, dvo;
+  LHPC_HIP_TRY(dr.alloc(static_cast<size_t>(nnz) * 4, s));
+  LHPC_HIP_TRY(dc.alloc(static_cast<size_t>(nnz) * 4, s));
+  LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(nnz) * vb, s));
+  LHPC_HIP_TRY(drp.alloc(rpb, s));
+  LHPC_HIP_TRY(dco.alloc(static_cast<size_t>(nnz) * 4, s));
+  LHPC_HIP_TRY(dvo.alloc(static_cast<size_t>(nnz) * vb, s));
+  if (nnz > 0) {
+    LHPC_HIP_TRY(hipMemcpyAsync(dr.p, rows, static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice, s));
+    LHPC_HIP_TRY(hipMemcpyAsync(dc.p, cols, static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice, s));
+    LHPC_HIP_TRY(hipMemcpyAsync(dv.p, vals, static_cast<size_t>(nnz) * vb, hipMemcpyHostToDevice, s));
+  }
+  int64_t un = 0;
+  LHPC_TRY(run(static_cast<int32_t *>(dr.p), static_cast<int32_t *>(dc.p), dv.p, drp.p,
+               static_cast<int32_t *>(dco.p), dvo.p, &un));
+  LHPC_HIP_TRY(hipMemcpyAsync(row_ptr, drp.p, rpb, hipMemcpyDeviceToHost, s));
+  if (un > 0) {
+    LHPC_HIP_TRY(hipMemcpyAsync(col_out, dco.p, static_cast<size_t>(un) * 4, hipMemcpyDeviceToHost, s));
+    LHPC_HIP_TRY(hipMemcpyAsync(val_out, dvo.p, static_cast<size_t>(un) * vb, hipMemcpyDeviceToHost, s));
+  }
+  LHPC_HIP_TRY(hipStreamSynchronize(s));
+  if (nnz_out) *nnz_out = un;
+  return LHPC_OK;
+}

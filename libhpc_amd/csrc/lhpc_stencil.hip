@@ -928,7 +928,6 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
   // alternatives
   const char *impl = std::getenv("LHPC_STENCIL7_IMPL");
   const bool use_lds = impl && !std::strcmp(impl, "lds");
-  const bool simple = impl && !std::strcmp(impl, "simple");
   const bool use_reg = impl && !std::strcmp(impl, "reg");
   const bool use_pf = impl && !std::strcmp(impl, "pf");
   const bool use_ring = impl && !std::strcmp(impl, "ring");

@@ -31,6 +31,7 @@
 #include <math.h>
 #include <omp.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #define ORACLE_API __attribute__((visibility("default")))
@@ -249,3 +250,95 @@ ORACLE_API void oracle_stencil7(const float *u, float *out, int64_t nz, int64_t 
       }
     }
 }
+
+/* ------------------------------------------------------------ radix sort
+ * LSD counting sort, 8-bit digits, ascending, stable — the algorithm of the
+ * reference's sort::radix::details::radix_sort_v4 / _cache_v1
+ * (lib/sort/radix_cpu/include/radix_sort_cpu.hpp:125-166, :168-203): per
+ * pass, histogram the digit, exclusive-scan the 256 counts, scatter in input
+ * order into the other buffer, swap.  Restricted to bits [begin, end) (the
+ * GPU ABI's contract); the last digit is masked to the remaining bits.
+ * Pinned by tests/test_oracle.py against numpy's stable sort and against the
+ * reference's own CPU sort compiled from its sources (oracle/_ref).        */
+#define ORACLE_SORT_BODY(KT)                                                         \
+  KT *tk = (KT *)malloc((size_t)(n > 0 ? n : 1) * sizeof(KT));                      \
+  uint32_t *tv = vals ? (uint32_t *)malloc((size_t)(n > 0 ? n : 1) * 4) : NULL;     \
+  KT *ka = keys, *kb = tk;                                                           \
+  uint32_t *va = vals, *vb = tv;                                                     \
+  int passes = 0;                                                                    \
+  for (int shift = begin; shift < end; shift += 8, ++passes) {                       \
+    const int bits = end - shift < 8 ? end - shift : 8;                              \
+    const uint64_t mask = (1ull << bits) - 1;                                        \
+    int64_t cnt[256] = {0};                                                          \
+    for (int64_t i = 0; i < n; ++i) cnt[(ka[i] >> shift) & mask]++;                 \
+    int64_t sum = 0;                                                                 \
+    for (int d = 0; d < 256; ++d) {                                                  \
+      const int64_t c = cnt[d];                                                      \
+      cnt[d] = sum;                                                                  \
+      sum += c;                                                                      \
+    }                                                                                \
+    for (int64_t i = 0; i < n; ++i) {                                                \
+      const int64_t p = cnt[(ka[i] >> shift) & mask]++;                              \
+      kb[p] = ka[i];                                                                 \
+      if (va) vb[p] = va[i];                                                         \
+    }                                                                                \
+    KT *tt = ka; ka = kb; kb = tt;                                                   \
+    uint32_t *vt = va; va = vb; vb = vt;                                             \
+  }                                                                                  \
+  if (passes & 1) {                                                                  \
+    memcpy(keys, ka, (size_t)n * sizeof(KT));                                        \
+    if (vals) memcpy(vals, va, (size_t)n * 4);                                       \
+  }                                                                                  \
+  free(tk);                                                                          \
+  free(tv);
+
+ORACLE_API void oracle_radix_sort_u32(uint32_t *keys, uint32_t *vals, int64_t n, int begin, int end) {
+  ORACLE_SORT_BODY(uint32_t)
+}
+
+ORACLE_API void oracle_radix_sort_u64(uint64_t *keys, uint32_t *vals, int64_t n, int begin, int end) {
+  ORACLE_SORT_BODY(uint64_t)
+}
+
+/* COO → CSR: order by (row, col) with the stable sort
+ * above on key = row << col_bits | col, then merge equal coordinates by
+ * summing their values left to right in input order (the ABI's contract).
+ * Returns the merged nnz, or -1 for an out-of-range coordinate.            */
+#define ORACLE_COO(NAME, VT)                                                                          \
+ORACLE_API int64_t NAME(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *rows,               \
+                        const int32_t *cols, const VT *vals, int64_t *row_ptr, int32_t *col_out,        \
+                        VT *val_out) {                                                                  \
+  int cb = 1, rb = 1;                                                                               \
+  while ((1ll << cb) < n_cols) ++cb;                                                                \
+  while ((1ll << rb) < n_rows) ++rb;                                                                \
+  uint64_t *k = (uint64_t *)malloc((size_t)(nnz > 0 ? nnz : 1) * 8);                                \
+  uint32_t *ix = (uint32_t *)malloc((size_t)(nnz > 0 ? nnz : 1) * 4);                               \
+  for (int64_t i = 0; i < nnz; ++i) {                                                               \
+    if (rows[i] < 0 || rows[i] >= n_rows || cols[i] < 0 || cols[i] >= n_cols) {                     \
+      free(k);                                                                                      \
+      free(ix);                                                                                     \
+      return -1;                                                                                    \
+    }                                                                                               \
+    k[i] = ((uint64_t)rows[i] << cb) | (uint64_t)cols[i];                                           \
+    ix[i] = (uint32_t)i;                                                                            \
+  }                                                                                                 \
+  oracle_radix_sort_u64(k, ix, nnz, 0, cb + rb);                                                    \
+  int64_t u = 0;                                                                                    \
+  for (int64_t r = 0; r <= n_rows; ++r) row_ptr[r] = 0;                                             \
+  for (int64_t i = 0; i < nnz;) {                                                                   \
+    VT s = vals[ix[i]];                                                                             \
+    int64_t j = i + 1;                                                                              \
+    while (j < nnz && k[j] == k[i]) s = s + vals[ix[j++]];                                          \
+    col_out[u] = (int32_t)(k[i] & ((1ull << cb) - 1));                                              \
+    val_out[u] = s;                                                                                 \
+    row_ptr[(int64_t)(k[i] >> cb) + 1]++;                                                           \
+    ++u;                                                                                            \
+    i = j;                                                                                          \
+  }                                                                                                 \
+  for (int64_t r = 0; r < n_rows; ++r) row_ptr[r + 1] += row_ptr[r];                                \
+  free(k);                                                                                          \
+  free(ix);                                                                                         \
+  return u;                                                                                         \
+}
+ORACLE_COO(oracle_coo_to_csr_f64, double)
+ORACLE_COO(oracle_coo_to_csr_f32, float)

@@ -9,6 +9,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
 REF_PROBE = os.path.join(ROOT, "oracle", "_ref", "ref_probe")
+REF_SORT_SO = os.path.join(ROOT, "oracle", "_ref", "libref_sort.so")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 _p, _i, _i64, _f = C.c_void_p, C.c_int, C.c_int64, C.c_float
@@ -33,6 +34,11 @@ def load_oracle():
         lib.cpu_blur_x_sse.restype = _i
         lib.cpu_blur_y_sse.restype = _i
         lib.oracle_stencil7.argtypes = [_p, _p, _i64, _i64, _i64, _i64, _f, _f, _i]
+        lib.oracle_radix_sort_u32.argtypes = [_p, _p, _i64, _i, _i]
+        lib.oracle_radix_sort_u64.argtypes = [_p, _p, _i64, _i, _i]
+        for f in (lib.oracle_coo_to_csr_f32, lib.oracle_coo_to_csr_f64):
+            f.argtypes = [_i64, _i64, _i64, _p, _p, _p, _p, _p, _p]
+            f.restype = _i64
         _lib = lib
     return _lib
 
@@ -116,4 +122,56 @@ def random_padded(shape, seed, zero_ghost=False, ghost=0):
         sl = tuple(slice(ghost, s - ghost) for s in shape)
         m[sl] = True
         a[~m] = 0
+    return a
+
+
+# ------------------------------------------------------------ sort / COO→CSR
+def sort_oracle(keys, vals=None, begin=0, end=None):
+    """Stable LSD restatement (oracle.c); returns sorted copies."""
+    lib = load_oracle()
+    k = np.ascontiguousarray(keys).copy()
+    v = None if vals is None else np.ascontiguousarray(vals, dtype=np.uint32).copy()
+    end = k.dtype.itemsize * 8 if end is None else end
+    fn = lib.oracle_radix_sort_u64 if k.dtype == np.uint64 else lib.oracle_radix_sort_u32
+    fn(_ptr(k), _ptr(v), k.size, begin, end)
+    return k if v is None else (k, v)
+
+
+def coo_oracle(n_rows, n_cols, rows, cols, vals):
+    """(row_ptr int64, col int32, val) or None for out-of-range input."""
+    lib = load_oracle()
+    nnz = rows.size
+    rp = np.zeros(n_rows + 1, dtype=np.int64)
+    col = np.empty(max(nnz, 1), dtype=np.int32)
+    val = np.empty(max(nnz, 1), dtype=vals.dtype)
+    fn = lib.oracle_coo_to_csr_f32 if vals.dtype == np.float32 else lib.oracle_coo_to_csr_f64
+    u = fn(n_rows, n_cols, nnz, _ptr(rows), _ptr(cols), _ptr(vals), _ptr(rp), _ptr(col), _ptr(val))
+    if u < 0:
+        return None
+    return rp, col[:u].copy(), val[:u].copy()
+
+
+_ref_sort = None
+
+
+def load_ref_sort():
+    """The reference's own CPU radix sort (oracle/_ref/libref_sort.so), or None
+    when it was not built (reference absent and no prebuilt copy)."""
+    global _ref_sort
+    if _ref_sort is None and os.path.exists(REF_SORT_SO):
+        lib = C.CDLL(REF_SORT_SO)
+        for f in ("ref_radix_sort_u32", "ref_radix_sort_v4_u32", "ref_generate_random", "ref_gpu_test_keys"):
+            getattr(lib, f).argtypes = [_p, C.c_size_t]
+        _ref_sort = lib
+    return _ref_sort
+
+
+def ref_gpu_test_keys(n):
+    """The reference GPU test's keys (mt19937 default seed, U[100, 2^32-101]),
+    from oracle/_ref, or None."""
+    lib = load_ref_sort()
+    if lib is None:
+        return None
+    a = np.empty(n, dtype=np.uint32)
+    lib.ref_gpu_test_keys(_ptr(a), n)
     return a

@@ -14,6 +14,11 @@ Provenance of every fixture:
                  edge shapes); y_exact is the EXACT row sum computed with
                  Python Fractions and rounded once to float64 — independent
                  of both the oracle and the GPU kernels.
+  sort_ref_*.npz keys from the reference's own input generators and their
+                 order as produced by the REFERENCE's CPU radix sort
+                 (oracle/_ref/libref_sort.so, compiled from
+                 lib/sort/radix_cpu/include/radix_sort_cpu.hpp + src/helper.cpp):
+                 sort::radix::radix_sort (radix_sort_cache_thread_v2<256>).
   gen_checksums.json  sha256 of generator outputs for the BASELINE configs,
                  so a generator change cannot silently change the workload.
 
@@ -143,7 +148,27 @@ def gen_checksums():
     print("wrote gen_checksums.json")
 
 
+def sort_fixtures():
+    import ctypes as C
+    so = os.path.join(ROOT, "oracle", "_ref", "libref_sort.so")
+    if not os.path.exists(so):
+        print("oracle/_ref/libref_sort.so missing: run `make -C oracle` where /root/reference exists")
+        return
+    lib = C.CDLL(so)
+    for f in ("ref_radix_sort_u32", "ref_generate_random", "ref_gpu_test_keys"):
+        getattr(lib, f).argtypes = [C.c_void_p, C.c_size_t]
+    for name, gen, n in (("sort_ref_gpu_keys_5000.npz", lib.ref_gpu_test_keys, 5000),
+                         ("sort_ref_cpu_keys_4097.npz", lib.ref_generate_random, 4097)):
+        keys = np.empty(n, dtype=np.uint32)
+        gen(keys.ctypes.data, n)
+        out = keys.copy()
+        lib.ref_radix_sort_u32(out.ctypes.data, n)
+        np.savez_compressed(os.path.join(HERE, name), keys=keys, sorted=out)
+        print("wrote", name)
+
+
 if __name__ == "__main__":
+    sort_fixtures()
     spmv_fixtures()
     blur_fixtures()
     layout_fixture()

