@@ -1,6 +1,6 @@
 """bench.py — CSR SpMV throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5|blur_x|blur_y]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5|blur_x|blur_y|sort]
 
 N=1: BASELINE configs[1] — CSR SpMV, n=10M, nnz=150M (exactly 15 uniform
 distinct sorted columns per row), fp32 values/x/y, A and x resident in HBM.
@@ -22,6 +22,13 @@ Extra objects on the JSON line:
   cpu_baseline  rank 0, N=1 only: the AVX2 + OpenMP CSR SpMV of oracle/ (the
                 reference has no CPU SpMV) on the same matrix, timed
                 for ~10 s on the box's host cores.
+
+--workload sort (not the headline): the reference's only
+published GPU number — radix sort of 500M uint32 keys (README.md:52, ~360 ms
+on an RTX 3080 Ti Laptop = 1.39 G keys/s) — on lhpc_radix_sort_u32; each step
+sorts a fresh copy of the same random keys (the restore copy is outside the
+timed events); cpu_baseline = the reference's own CPU radix sort
+(oracle/_ref/libref_sort.so, kind "reference").
 """
 import argparse
 import json
@@ -43,7 +50,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "blur_x", "blur_y"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "blur_x", "blur_y", "sort"])
     ap.add_argument("--n", type=int, default=10_000_000)
     ap.add_argument("--per-row", type=int, default=15)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -201,6 +208,8 @@ def main():
             result["cpu_baseline"] = cpu_spmv_baseline(rp, col, val, x, nnz, args.cpu_seconds)
         for pl in plans:
             pl.close()
+    elif wl == "sort":
+        result.update(sort_bench(args, L, torch, dev, stream, barrier, world, rank))
     else:
         result.update(stencil_bench(args, L, torch, dev, stream, barrier))
         if rank == 0 and world == 1 and not args.no_cpu_baseline and wl in ("blur_x", "blur_y", "c5"):
@@ -320,6 +329,80 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
         out["_cpu"] = {"value": cells / min(ts) / 1e9, "unit": "Gcell/s", "cores": th, "kind": "port",
                        "sample": f"full 8192^2 grid, best of {len(ts)} passes, reference SSE loop restated"}
     return out
+
+
+SORT_N = 500_000_000
+SORT_REF_GKEYS = 500e6 / 0.360 / 1e9  # reference README.md:52: 500M keys in ~360 ms
+
+
+def sort_bench(args, L, torch, dev, stream, barrier, world, rank):
+    n = SORT_N
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED0006 + rank)
+    src = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device=dev, generator=g)
+    keys = torch.empty_like(src)
+    for _ in range(args.warmup):
+        keys.copy_(src)
+        L.radix_sort(keys, stream=stream)
+    barrier()
+    total = 0.0
+    for _ in range(args.steps):
+        keys.copy_(src)  # restore the unsorted batch (outside the timed events)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        L.radix_sort(keys, stream=stream)
+        e1.record(stream)
+        e1.synchronize()
+        total += e0.elapsed_time(e1) * 1e-3
+    barrier()
+    per = total / args.steps
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([per], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        per = float(tt.item())
+    ok = bool((keys[1:].to(torch.int64) & 0xFFFFFFFF).ge(keys[:-1].to(torch.int64) & 0xFFFFFFFF).all())
+    value = world * n / per / 1e9
+    alg = 32.0 * n  # 4 passes x (read + write) x 4 B per key
+    out = dict(metric="radix sort G keys/s, 500M uint32 keys (reference README.md:52)", value=value,
+               unit="Gkeys/s", n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=per * 1e3,
+               higher_is_better=True, scaling="weak", vs_baseline=value / world / SORT_REF_GKEYS, dtype="u32",
+               data="synthetic uniform uint32 (torch generator)",
+               config={"workload": "reference README radix-sort config: 500M uint32 keys, 1 GPU"
+                       + (f" x{world} replicas" if world > 1 else ""), "sorted": ok},
+               roofline={"bound": "hbm", "kernel": "k_radix_upsweep+k_radix_scan+k_radix_downsweep x4",
+                         "achieved": alg / per / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": alg / per / 1e9 / HBM_PEAK_GBPS,
+                         "traffic": load_traffic("sort") if world == 1 else None})
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_sort_baseline(keys, src, args.cpu_seconds)
+    return out
+
+
+def cpu_sort_baseline(keys, src, seconds):
+    """The reference's own CPU radix sort (radix_sort_cache_thread_v2<256>, OpenMP) on a
+    bounded 50M-key sample of the same keys; the C restatement if the reference build is absent."""
+    from tests import _support as S
+    m = 50_000_000
+    base = src[:m].cpu().numpy().view(np.uint32).copy()
+    ref = S.load_ref_sort()
+    if ref is not None:
+        fn, kind = (lambda a: ref.ref_radix_sort_u32(a.ctypes.data, a.size)), "reference"
+    else:
+        lib = S.load_oracle()
+        fn, kind = (lambda a: lib.oracle_radix_sort_u32(a.ctypes.data, None, a.size, 0, 32)), "port"
+    ts = []
+    t_end = time.perf_counter() + seconds
+    while len(ts) < 2 or (time.perf_counter() < t_end and len(ts) < 50):
+        a = base.copy()
+        t0 = time.perf_counter()
+        fn(a)
+        ts.append(time.perf_counter() - t0)
+    assert np.all(a[1:] >= a[:-1])
+    return {"value": m / min(ts) / 1e9, "unit": "Gkeys/s", "cores": cpu_threads(), "kind": kind,
+            "sample": f"50M of the same keys, best of {len(ts)} sorts"
+                      + (" (reference radix_sort, OpenMP)" if kind == "reference" else " (C LSD restatement)")}
 
 
 if __name__ == "__main__":
