@@ -66,10 +66,15 @@ enum lhpc_plan_flags {
   LHPC_PLAN_FORCE_ROWGROUP = 1u << 4,
   LHPC_PLAN_FORCE_ADAPTIVE = 1u << 5,
   LHPC_PLAN_FORCE_XSLICE = 1u << 6,
-  /* XSLICE: keep per-slice partial sums in the value type instead of fp64
-   * (~10% faster for fp32; error bound then 2^-23·Σ|a·x| instead of
-   * 2^-24·|y| + O(2^-53)·Σ|a·x|).                                          */
-  LHPC_PLAN_FAST_PARTIALS = 1u << 7
+  /* XSLICE per-slice partial sums.  Every slice's row sum is accumulated in
+   * fp64 registers; the S partials are then summed in fp64 in slice order.
+   * Default for fp32 data: partials stored as fp32 (one rounding each), error
+   * ≤ 2^-23·Σ|a·x| — 8× inside the 1e-6·Σ|a·x| bar.  EXACT_PARTIALS stores
+   * them as fp64 (error 2^-24·|y| + O(2^-50)·Σ|a·x|, ~10% slower at C2).
+   * fp64 data always uses fp64 partials.  FAST_PARTIALS is the fp32 default,
+   * kept as a flag for callers that name it.                               */
+  LHPC_PLAN_FAST_PARTIALS = 1u << 7,
+  LHPC_PLAN_EXACT_PARTIALS = 1u << 8
 };
 
 /* kernel families a plan can select (lhpc_spmv_plan_info.kernel)          */

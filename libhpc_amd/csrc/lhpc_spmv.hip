@@ -876,14 +876,16 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
       p->xs_jagged = jagged ? 1 : 0;
       // fp64 partials (exact-ish: one rounding per row overall) vs partials in
       // the value type (less traffic).  fp64 values always use fp64.
-      p->xs_p64 = (tsz == 8 || !(flags & LHPC_PLAN_FAST_PARTIALS)) && !jagged ? 1 : 0;
+      p->xs_p64 = (tsz == 8 || ((flags & LHPC_PLAN_EXACT_PARTIALS) && !(flags & LHPC_PLAN_FAST_PARTIALS))) && !jagged
+                      ? 1 : 0;
       if (const char *env = std::getenv("LHPC_XSLICE_PARTIAL")) p->xs_p64 = (tsz == 8 || !std::strcmp(env, "f64")) && !jagged;
       // fused slice reduction (fp64 partials only): opt-in.  Measured 2.5×
       // SLOWER than the separate reduce on C2 (3.07 vs 1.23 ms): every block
       // waits out its store drain + arrival atomic, which costs more than the
       // 123 µs reduce pass it removes.
       p->xs_fused = 0;
-      if (const char *env = std::getenv("LHPC_XSLICE_FUSE")) p->xs_fused = p->xs_p64 && !jagged && std::atoi(env) != 0;
+      if (const char *env = std::getenv("LHPC_XSLICE_FUSE"))
+        if (!jagged && std::atoi(env) != 0) p->xs_fused = p->xs_p64 = 1;  // the hand-off is fp64
       // persistent partial-free kernel: opt-in.  Measured slower on C2/C3/C4
       // (1.65-2.3 ms vs 1.24 ms): each wave walks the S slices serially and
       // its dependent window round trips are not hidden at 4-5 waves/SIMD

@@ -22,7 +22,8 @@ FAMILIES = {
     "rowgroup": 1 << 4,
     "adaptive": 1 << 5,
     "xslice": 1 << 6,
-    "xslice_fast": (1 << 6) | (1 << 7),  # fp32 partials, separate reduce kernel
+    "xslice_fast": (1 << 6) | (1 << 7),  # fp32 partials (the fp32 default), separate reduce kernel
+    "xslice_exact": (1 << 6) | (1 << 8),  # fp64 partials
 }
 GOLDEN_SPMV = sorted(glob.glob(os.path.join(S.GOLDEN, "spmv_*.npz")))
 
