@@ -242,6 +242,31 @@ int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
                     void *val_out, int64_t *nnz_out, int on_device,
                     void *stream);
 
+/* ------------------------------------------------------------------- I/O
+ * SURVEY §8f rank 4 (the reference has no file formats).  Host-only.
+ * .lcsr: 64-byte header {"LHPCCSR1", version 1, dtype, n_rows, n_cols, nnz,
+ * row_ptr_bits, index_bits = 32}, then row_ptr, col_idx, val, each section
+ * 64-byte aligned, little-endian.  load_header → allocate → load.
+ */
+int lhpc_csr_save(const char *path, int dtype, int64_t n_rows, int64_t n_cols,
+                  int64_t nnz, const void *row_ptr, int row_ptr_bits,
+                  const int32_t *col_idx, const void *val);
+int lhpc_csr_load_header(const char *path, int *dtype, int64_t *n_rows,
+                         int64_t *n_cols, int64_t *nnz, int *row_ptr_bits);
+int lhpc_csr_load(const char *path, void *row_ptr, int32_t *col_idx, void *val);
+/* Matrix Market "matrix coordinate {real|integer|pattern}
+ * {general|symmetric|skew-symmetric}": the header gives the shape and an
+ * upper bound on the expanded entry count (2× the listed entries for
+ * symmetric files); read_coo fills 0-based (row, col, value-as-double)
+ * triples — symmetric/skew entries expanded to both triangles, pattern
+ * values 1.0 — and the count written.  Build CSR with lhpc_coo_to_csr.
+ * symmetry: 0 general, 1 symmetric, 2 skew; field: 0 real, 1 integer,
+ * 2 pattern.  Dense "array" and complex/hermitian files: LHPC_ERR_UNSUPPORTED. */
+int lhpc_mm_read_header(const char *path, int64_t *n_rows, int64_t *n_cols,
+                        int64_t *nnz_max, int *symmetry, int *field);
+int lhpc_mm_read_coo(const char *path, int32_t *rows, int32_t *cols,
+                     double *vals, int64_t *count);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -53,7 +53,8 @@ ABI_SYMBOLS = (
     "lhpc_stencil7_f32_planes", "lhpc_gen_uniform_row_ptr",
     "lhpc_gen_powerlaw_row_ptr", "lhpc_gen_fill_cols", "lhpc_gen_fill_values",
     "lhpc_row_ptr_narrow", "lhpc_radix_sort_u32", "lhpc_radix_sort_pairs_u32",
-    "lhpc_radix_sort_pairs_u64", "lhpc_coo_to_csr",
+    "lhpc_radix_sort_pairs_u64", "lhpc_coo_to_csr", "lhpc_csr_save", "lhpc_csr_load_header",
+    "lhpc_csr_load", "lhpc_mm_read_header", "lhpc_mm_read_coo",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -124,6 +125,13 @@ _sig("lhpc_radix_sort_u32", _i, _p, _i64, _i, _i, _i, _p)
 _sig("lhpc_radix_sort_pairs_u32", _i, _p, _p, _i64, _i, _i, _i, _p)
 _sig("lhpc_radix_sort_pairs_u64", _i, _p, _p, _i64, _i, _i, _i, _p)
 _sig("lhpc_coo_to_csr", _i, _i, _i64, _i64, _i64, _p, _p, _p, _p, _i, _p, _p, C.POINTER(_i64), _i, _p)
+_sig("lhpc_csr_save", _i, C.c_char_p, _i, _i64, _i64, _i64, _p, _i, _p, _p)
+_sig("lhpc_csr_load_header", _i, C.c_char_p, C.POINTER(_i), C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64),
+     C.POINTER(_i))
+_sig("lhpc_csr_load", _i, C.c_char_p, _p, _p, _p)
+_sig("lhpc_mm_read_header", _i, C.c_char_p, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i),
+     C.POINTER(_i))
+_sig("lhpc_mm_read_coo", _i, C.c_char_p, _p, _p, _p, C.POINTER(_i64))
 
 
 class LhpcError(RuntimeError):
@@ -447,3 +455,56 @@ def coo_to_csr(n_rows: int, n_cols: int, rows, cols, vals, row_ptr_bits: int = 6
     _check(lib.lhpc_coo_to_csr(dtype, n_rows, n_cols, nnz, rp_, cp_, vp_, row_ptr.ctypes.data, row_ptr_bits,
                                col.ctypes.data, val.ctypes.data, C.byref(out_n), 0, None), "lhpc_coo_to_csr")
     return row_ptr, col[:out_n.value].copy(), val[:out_n.value].copy()
+
+
+# ------------------------------------------------------------ files (.lcsr, Matrix Market)
+def save_csr(path: str, row_ptr, col_idx, val, n_cols: int):
+    """Write a host CSR (row_ptr int32/int64, col_idx int32, val f32/f64) as .lcsr."""
+    rp = np.ascontiguousarray(row_ptr)
+    col = np.ascontiguousarray(col_idx, dtype=np.int32)
+    v = np.ascontiguousarray(val)
+    dt = F32 if v.dtype == np.float32 else F64
+    if v.dtype not in (np.float32, np.float64) or rp.dtype not in (np.int32, np.int64):
+        raise TypeError("save_csr: row_ptr int32/int64, val float32/float64")
+    _check(lib.lhpc_csr_save(os.fsencode(path), dt, rp.size - 1, n_cols, col.size, rp.ctypes.data,
+                             64 if rp.dtype == np.int64 else 32, col.ctypes.data, v.ctypes.data), "lhpc_csr_save")
+
+
+def load_csr(path: str):
+    """(row_ptr, col_idx, val, n_cols) from an .lcsr file."""
+    dt, rpb = C.c_int(0), C.c_int(0)
+    nr, nc, nz = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+    _check(lib.lhpc_csr_load_header(os.fsencode(path), C.byref(dt), C.byref(nr), C.byref(nc), C.byref(nz),
+                                    C.byref(rpb)), "lhpc_csr_load_header")
+    rp = np.empty(nr.value + 1, dtype=np.int64 if rpb.value == 64 else np.int32)
+    col = np.empty(nz.value, dtype=np.int32)
+    val = np.empty(nz.value, dtype=np.float32 if dt.value == F32 else np.float64)
+    _check(lib.lhpc_csr_load(os.fsencode(path), rp.ctypes.data, col.ctypes.data, val.ctypes.data), "lhpc_csr_load")
+    return rp, col, val, nc.value
+
+
+def read_matrix_market_coo(path: str):
+    """(rows int32, cols int32, vals float64, n_rows, n_cols): 0-based triples,
+    symmetric / skew-symmetric files expanded to both triangles."""
+    nr, nc, zmax = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+    sym, fld = C.c_int(0), C.c_int(0)
+    p = os.fsencode(path)
+    _check(lib.lhpc_mm_read_header(p, C.byref(nr), C.byref(nc), C.byref(zmax), C.byref(sym), C.byref(fld)),
+           "lhpc_mm_read_header")
+    rows = np.empty(max(zmax.value, 1), dtype=np.int32)
+    cols = np.empty(max(zmax.value, 1), dtype=np.int32)
+    vals = np.empty(max(zmax.value, 1), dtype=np.float64)
+    cnt = C.c_int64(0)
+    _check(lib.lhpc_mm_read_coo(p, rows.ctypes.data, cols.ctypes.data, vals.ctypes.data, C.byref(cnt)),
+           "lhpc_mm_read_coo")
+    k = cnt.value
+    return rows[:k].copy(), cols[:k].copy(), vals[:k].copy(), nr.value, nc.value
+
+
+def read_matrix_market(path: str, dtype=F64, row_ptr_bits: int = 64):
+    """CSR (row_ptr, col_idx, val, n_cols) from a Matrix Market file: parsed on
+    the host, assembled on the GPU (lhpc_coo_to_csr; duplicates summed)."""
+    rows, cols, vals, n_rows, n_cols = read_matrix_market_coo(path)
+    v = vals.astype(np.float32) if dtype == F32 else vals
+    rp, col, val = coo_to_csr(n_rows, n_cols, rows, cols, v, row_ptr_bits=row_ptr_bits)
+    return rp, col, val, n_cols

@@ -7,9 +7,12 @@
 //                            §2c-5 cells (-5,7), (1000,-2000)), PointerBlock
 //                            wrap, concurrent OpenMP writes, copies
 //   test_sparse_grid gpu   — sparse::to_csr (GPU COO→CSR) vs a std::map build,
-//                            then SpMV on the assembled matrix
+//                            then SpMV on the assembled matrix; sparse::save_csr /
+//                            load_csr / read_matrix_market (include/sparse/IO.hpp)
+#include <sparse/IO.hpp>
 #include <sparse/SparseDS.hpp>
 #include <sparse/SpMV.hpp>
+#include <unistd.h>
 
 #include <cmath>
 #include <cstdint>
@@ -192,6 +195,37 @@ int gpu_tests() {
   CHECK(err <= 1e-12 * (1.0 + mag));
   std::printf("to_csr: %lld x %lld, nnz %lld ok; spmv max err %.3g\n", static_cast<long long>(A.n_rows),
               static_cast<long long>(A.n_cols), static_cast<long long>(A.nnz()), err);
+  {  // file round trips
+    char tmpl[] = "/tmp/lhpc_io_XXXXXX";
+    const int fd = mkstemp(tmpl);
+    CHECK(fd >= 0);
+    close(fd);
+    save_csr(tmpl, A);
+    auto B = load_csr<double, std::int64_t>(tmpl);
+    CHECK(B.n_rows == A.n_rows && B.n_cols == A.n_cols && B.row_ptr == A.row_ptr && B.col_idx == A.col_idx &&
+          B.val == A.val);
+    bool threw_type = false;
+    try {
+      (void)load_csr<float, std::int64_t>(tmpl);
+    } catch (const std::invalid_argument &) {
+      threw_type = true;
+    }
+    CHECK(threw_type);
+    const std::string mtx = std::string(tmpl) + ".mtx";
+    FILE *f = std::fopen(mtx.c_str(), "w");
+    std::fprintf(f, "%%%%MatrixMarket matrix coordinate real symmetric\n%% comment\n3 3 3\n1 1 2.0\n2 1 -1.5\n3 3 4e0\n");
+    std::fclose(f);
+    auto M = read_matrix_market<double>(mtx);
+    CHECK(M.n_rows == 3 && M.n_cols == 3 && M.nnz() == 4);
+    const std::int32_t rp_want[] = {0, 2, 3, 4};
+    const std::int32_t col_want[] = {0, 1, 0, 2};
+    const double val_want[] = {2.0, -1.5, -1.5, 4.0};
+    for (int i = 0; i < 4; ++i) CHECK(M.row_ptr[i] == rp_want[i]);
+    for (int i = 0; i < 4; ++i) CHECK(M.col_idx[i] == col_want[i] && M.val[i] == val_want[i]);
+    std::remove(tmpl);
+    std::remove(mtx.c_str());
+    std::printf("io: lcsr round trip + matrix market ok\n");
+  }
   return failures;
 }
 
