@@ -1,6 +1,6 @@
 """bench.py — CSR SpMV throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5|blur_x|blur_y|sort]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5|blur_x|blur_y|sort|cg]
 
 N=1: BASELINE configs[1] — CSR SpMV, n=10M, nnz=150M (exactly 15 uniform
 distinct sorted columns per row), fp32 values/x/y, A and x resident in HBM.
@@ -29,6 +29,11 @@ on an RTX 3080 Ti Laptop = 1.39 G keys/s) — on lhpc_radix_sort_u32; each step
 sorts a fresh copy of the same random keys (the restore copy is outside the
 timed events); cpu_baseline = the reference's own CPU radix sort
 (oracle/_ref/libref_sort.so, kind "reference").
+
+--workload cg: conjugate gradient on the 4096² 2-D
+Laplacian in fp64 (16.8M rows, 83.9M nnz); a step = one CG iteration
+(SpMV + 2 all-reduced dots + the fused vector updates); N>1 runs DistCG
+(row blocks, RCCL all-reduce of the dots, all-gather of p).
 """
 import argparse
 import json
@@ -50,7 +55,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "blur_x", "blur_y", "sort"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "blur_x", "blur_y", "sort", "cg"])
     ap.add_argument("--n", type=int, default=10_000_000)
     ap.add_argument("--per-row", type=int, default=15)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -210,6 +215,8 @@ def main():
             pl.close()
     elif wl == "sort":
         result.update(sort_bench(args, L, torch, dev, stream, barrier, world, rank))
+    elif wl == "cg":
+        result.update(cg_bench(args, L, torch, dev, stream, barrier, world, rank))
     else:
         result.update(stencil_bench(args, L, torch, dev, stream, barrier))
         if rank == 0 and world == 1 and not args.no_cpu_baseline and wl in ("blur_x", "blur_y", "c5"):
@@ -328,6 +335,67 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
             ts.append(time.perf_counter() - t0)
         out["_cpu"] = {"value": cells / min(ts) / 1e9, "unit": "Gcell/s", "cores": th, "kind": "port",
                        "sample": f"full 8192^2 grid, best of {len(ts)} passes, reference SSE loop restated"}
+    return out
+
+
+def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
+    from libhpc_amd.dist import DistCG, HipOps, InterleavedBlocks
+    nx = 4096
+    rp, col, val = L.gen_laplacian_2d(nx, nx, L.F64)
+    n, nnz = nx * nx, int(col.size)
+    b = L.gen_values(L.F64, 0, n, L.SEED_X)
+    ib = InterleavedBlocks(n, world, 1)
+    r0, r1 = ib.rows(rank, 0)
+    plan = L.SpMVPlan(*ib.local_csr(rp, col, val, rank, 0), n)
+    bd = torch.zeros(ib.B, dtype=torch.float64, device=dev)
+    bd[:r1 - r0] = torch.from_numpy(b[r0:r1]).to(dev)
+    solver = DistCG(ib, rank, lambda pf, qb: plan(pf, qb, stream=stream), HipOps(stream), like=bd)
+
+    def run(iters):
+        x = torch.zeros_like(bd)
+        return solver.solve(bd, x, tol=0.0, max_iter=iters, check_every=iters)  # tol 0: exactly `iters` iterations
+
+    run(max(1, args.warmup))
+    barrier()
+    t0 = time.perf_counter()
+    _, it, res = run(args.steps)
+    barrier()
+    per = (time.perf_counter() - t0) / args.steps
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([per], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        per = float(tt.item())
+    spmv_b = nnz * (8 + 4) + (n + 1) * 4 + 2 * n * 8
+    vec_b = 11 * n * 8  # p·q (2n), x/r update (read 4n, write 2n), p update (read 2n, write n)
+    alg = (spmv_b + vec_b) / world
+    out = dict(metric="CG iterations/s, 2-D Laplacian 4096^2 fp64 (SURVEY 8f rank 3)", value=1.0 / per,
+               unit="iter/s", n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=per * 1e3,
+               higher_is_better=True, scaling="strong", vs_baseline=None, dtype="f64",
+               data="synthetic: 5-point Laplacian, b = U[-1,1) (SEED_X)",
+               config={"workload": f"CG, 2-D Laplacian {nx}^2 fp64, n={n}, nnz={nnz}, {world} GPU(s)",
+                       "iterations": it, "relres": res, "kernel": plan.info()["kernel"]},
+               roofline={"bound": "hbm", "kernel": "spmv + k_dot_partial/k_cg_xr/k_cg_p",
+                         "achieved": alg / per / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": alg / per / 1e9 / HBM_PEAK_GBPS, "traffic": None,
+                         "alg_bytes_per_iter": alg})
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from tests import _support as S
+        lib = S.load_oracle()
+        import ctypes as C
+        k = 0
+        ts = []
+        t_end = time.perf_counter() + args.cpu_seconds
+        while len(ts) < 1 or (time.perf_counter() < t_end and len(ts) < 5):
+            x = np.zeros(n)
+            res_c = C.c_double(0.0)
+            t0 = time.perf_counter()
+            k = lib.oracle_cg_f64(n, rp.ctypes.data, 64, col.ctypes.data, val.ctypes.data, b.ctypes.data,
+                                  x.ctypes.data, 0.0, 5, C.byref(res_c))
+            ts.append((time.perf_counter() - t0) / max(k, 1))
+        out["cpu_baseline"] = {"value": 1.0 / min(ts), "unit": "iter/s", "cores": 1, "kind": "port",
+                               "sample": f"{k} iterations of the fp64 CG restatement (oracle.c), best of {len(ts)}"}
+    plan.close()
     return out
 
 

@@ -242,6 +242,32 @@ int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
                     void *val_out, int64_t *nnz_out, int on_device,
                     void *stream);
 
+/* ------------------------------------------------------------------- CG
+ * Conjugate gradient on an SpMV plan (no reference
+ * counterpart).  lhpc_cg_solve: b and x are HBM pointers of the plan's dtype
+ * (x = initial guess in, solution out); stops when ‖r‖₂ ≤ tol·‖b‖₂ (tested
+ * every `check_every` iterations, the only host synchronisations) or after
+ * max_iter iterations; reports the iterations run and ‖r‖/‖b‖ of the
+ * recursively updated residual.  LHPC_ERR_INTERNAL on breakdown (non-finite
+ * residual: the matrix is not SPD).  Dots are fp64, deterministic.
+ * Building blocks for multi-GPU composition (all asynchronous on `stream`,
+ * scalars are fp64 HBM pointers, read on the device):
+ *   lhpc_vec_dot     *out = a·b
+ *   lhpc_cg_step_xr  α = *alpha_num / *alpha_den; x += α·p; r -= α·q; *rr_out = r·r
+ *   lhpc_cg_step_p   β = *beta_num / *beta_den; p = r + β·p
+ */
+int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, double tol,
+                  int max_iter, int check_every, int *iters_out,
+                  double *resid_out, void *stream);
+int lhpc_vec_dot(int dtype, int64_t n, const void *a, const void *b,
+                 double *out, void *stream);
+int lhpc_cg_step_xr(int dtype, int64_t n, const double *alpha_num,
+                    const double *alpha_den, void *x, const void *p, void *r,
+                    const void *q, double *rr_out, void *stream);
+int lhpc_cg_step_p(int dtype, int64_t n, const double *beta_num,
+                   const double *beta_den, const void *r, void *p,
+                   void *stream);
+
 /* ------------------------------------------------------------------- I/O
  * SURVEY §8f rank 4 (the reference has no file formats).  Host-only.
  * .lcsr: 64-byte header {"LHPCCSR1", version 1, dtype, n_rows, n_cols, nnz,

@@ -54,7 +54,8 @@ ABI_SYMBOLS = (
     "lhpc_gen_powerlaw_row_ptr", "lhpc_gen_fill_cols", "lhpc_gen_fill_values",
     "lhpc_row_ptr_narrow", "lhpc_radix_sort_u32", "lhpc_radix_sort_pairs_u32",
     "lhpc_radix_sort_pairs_u64", "lhpc_coo_to_csr", "lhpc_csr_save", "lhpc_csr_load_header",
-    "lhpc_csr_load", "lhpc_mm_read_header", "lhpc_mm_read_coo",
+    "lhpc_csr_load", "lhpc_mm_read_header", "lhpc_mm_read_coo", "lhpc_cg_solve", "lhpc_vec_dot",
+    "lhpc_cg_step_xr", "lhpc_cg_step_p",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -125,6 +126,10 @@ _sig("lhpc_radix_sort_u32", _i, _p, _i64, _i, _i, _i, _p)
 _sig("lhpc_radix_sort_pairs_u32", _i, _p, _p, _i64, _i, _i, _i, _p)
 _sig("lhpc_radix_sort_pairs_u64", _i, _p, _p, _i64, _i, _i, _i, _p)
 _sig("lhpc_coo_to_csr", _i, _i, _i64, _i64, _i64, _p, _p, _p, _p, _i, _p, _p, C.POINTER(_i64), _i, _p)
+_sig("lhpc_cg_solve", _i, _p, _p, _p, _d, _i, _i, C.POINTER(_i), C.POINTER(_d), _p)
+_sig("lhpc_vec_dot", _i, _i, _i64, _p, _p, _p, _p)
+_sig("lhpc_cg_step_xr", _i, _i, _i64, _p, _p, _p, _p, _p, _p, _p, _p)
+_sig("lhpc_cg_step_p", _i, _i, _i64, _p, _p, _p, _p, _p)
 _sig("lhpc_csr_save", _i, C.c_char_p, _i, _i64, _i64, _i64, _p, _i, _p, _p)
 _sig("lhpc_csr_load_header", _i, C.c_char_p, C.POINTER(_i), C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64),
      C.POINTER(_i))
@@ -508,3 +513,67 @@ def read_matrix_market(path: str, dtype=F64, row_ptr_bits: int = 64):
     v = vals.astype(np.float32) if dtype == F32 else vals
     rp, col, val = coo_to_csr(n_rows, n_cols, rows, cols, v, row_ptr_bits=row_ptr_bits)
     return rp, col, val, n_cols
+
+
+# ------------------------------------------------------------ CG
+def _dtype_code(t) -> int:
+    return F32 if _elem_bytes(t) == 4 else F64
+
+
+def cg(plan: "SpMVPlan", b, x=None, tol: float = 1e-8, max_iter: int = 1000, check_every: int = 1,
+       stream=None):
+    """Solve A·x = b (A SPD, the plan's matrix) by conjugate gradient on the
+    GPU.  ``b`` (and ``x``, the initial guess, default 0) are device tensors
+    of the plan's dtype; x is updated in place.  Returns (x, iterations,
+    ‖r‖/‖b‖).  See include/lhpc.h lhpc_cg_solve."""
+    import torch
+    if x is None:
+        x = torch.zeros_like(b)
+    bp, bd = _buf(b)
+    xp, xd = _buf(x, writable=True)
+    if not (bd and xd):
+        raise ValueError("cg: b and x must be device tensors")
+    st = _dev_stream(b, stream)
+    it, res = C.c_int(0), C.c_double(0.0)
+    _check(lib.lhpc_cg_solve(plan._h, bp, xp, tol, max_iter, check_every, C.byref(it), C.byref(res),
+                             _stream_ptr(st)), "lhpc_cg_solve")
+    return x, it.value, res.value
+
+
+def vec_dot(a, b, out, stream=None):
+    """out (1-element float64 device tensor) = a·b, asynchronously."""
+    st = _dev_stream(a, stream)
+    _check(lib.lhpc_vec_dot(_dtype_code(a), _numel(a), _buf(a)[0], _buf(b)[0], out.data_ptr(), _stream_ptr(st)),
+           "lhpc_vec_dot")
+    return out
+
+
+def cg_step_xr(alpha_num, alpha_den, x, p, r, q, rr_out, stream=None):
+    st = _dev_stream(x, stream)
+    _check(lib.lhpc_cg_step_xr(_dtype_code(x), _numel(x), alpha_num.data_ptr(), alpha_den.data_ptr(), x.data_ptr(),
+                               p.data_ptr(), r.data_ptr(), q.data_ptr(), rr_out.data_ptr(), _stream_ptr(st)),
+           "lhpc_cg_step_xr")
+
+
+def cg_step_p(beta_num, beta_den, r, p, stream=None):
+    st = _dev_stream(r, stream)
+    _check(lib.lhpc_cg_step_p(_dtype_code(r), _numel(r), beta_num.data_ptr(), beta_den.data_ptr(), r.data_ptr(),
+                              p.data_ptr(), _stream_ptr(st)), "lhpc_cg_step_p")
+
+
+def gen_laplacian_2d(nx: int, ny: int, dtype=F64, shift: float = 0.0):
+    """5-point Dirichlet Laplacian on an nx×ny grid (row i = y·nx + x;
+    diagonal 4 + shift, −1 to each existing neighbour): symmetric positive
+    definite, columns sorted.  Returns (row_ptr int64, col_idx int32, val).
+    Host-side workload generator for the CG solver."""
+    n = nx * ny
+    i = np.arange(n, dtype=np.int64)
+    y, x = np.divmod(i, nx)
+    off = np.array([-nx, -1, 0, 1, nx], dtype=np.int64)  # ascending column order
+    mask = np.stack([y > 0, x > 0, np.ones(n, bool), x < nx - 1, y < ny - 1], axis=1)
+    cols = (i[:, None] + off[None, :])[mask].astype(np.int32)
+    w = np.where(off == 0, 4.0 + shift, -1.0)
+    vals = np.broadcast_to(w, (n, 5))[mask].astype(np.float32 if dtype == F32 else np.float64)
+    rp = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(mask.sum(axis=1), out=rp[1:])
+    return rp, cols, vals

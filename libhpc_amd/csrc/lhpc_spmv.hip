@@ -568,6 +568,28 @@ __global__ __launch_bounds__(kBlock) void k_xslice_reduce(const P *__restrict__ 
 }
 
 // ------------------------------------------------------------- host side
+// Distinct 128-B x lines touched per nonzero, over up to 32 evenly spaced
+// chunks of 8192 consecutive rows (1.0 = no reuse within a chunk).
+template <typename RP>
+double gather_lines_per_nnz(const RP &rp, const int32_t *col, int64_t n_rows, size_t tsz) {
+  constexpr int64_t kChunk = 8192, kSamples = 32;
+  const int shift = tsz == 8 ? 4 : 5;  // 16 doubles / 32 floats per line
+  const int64_t chunks = (n_rows + kChunk - 1) / kChunk;
+  const int64_t step = std::max<int64_t>(1, chunks / kSamples);
+  int64_t lines = 0, nz = 0;
+  std::vector<int32_t> buf;
+  for (int64_t c = 0; c < chunks; c += step) {
+    const int64_t r0 = c * kChunk, r1 = std::min(n_rows, r0 + kChunk);
+    const int64_t k0 = rp[r0], k1 = rp[r1];
+    buf.resize(static_cast<size_t>(k1 - k0));
+    for (int64_t k = k0; k < k1; ++k) buf[static_cast<size_t>(k - k0)] = col[k] >> shift;
+    std::sort(buf.begin(), buf.end());
+    lines += std::unique(buf.begin(), buf.end()) - buf.begin();
+    nz += k1 - k0;
+  }
+  return nz ? static_cast<double>(lines) / static_cast<double>(nz) : 1.0;
+}
+
 bool is_gfx950(int dev) {
   hipDeviceProp_t p;
   if (hipGetDeviceProperties(&p, dev) != hipSuccess) return false;
@@ -857,9 +879,18 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
   const double x_bytes = static_cast<double>(n_cols) * static_cast<double>(tsz);
   double slice_mb = 5.0;
   if (const char *env = std::getenv("LHPC_XSLICE_MB")) slice_mb = std::max(0.25, std::atof(env));
-  const bool want_xslice = (flags & LHPC_PLAN_FORCE_XSLICE) ||
-                           (!(flags & (LHPC_PLAN_FORCE_ROWGROUP | LHPC_PLAN_FORCE_ADAPTIVE)) &&
-                            x_bytes > 8.0e6);
+  // ... and only when the gathers have no locality of their own: a banded or
+  // structured matrix (stencil operators, the CG Laplacian) re-reads each x
+  // line from neighbouring rows, which the row-local kernels already serve
+  // from L2, while XSLICE would add S partials per row.  Measure it: distinct
+  // 128-B x lines per nonzero over sampled 8192-row chunks (≈0.8 for C2's
+  // uniform columns, ≈0.03 for a 2-D Laplacian); ≤ 0.25 counts as local.
+  double locality_thr = 0.25;
+  if (const char *env = std::getenv("LHPC_SPMV_LOCALITY")) locality_thr = std::atof(env);
+  const bool auto_ok = !(flags & (LHPC_PLAN_FORCE_ROWGROUP | LHPC_PLAN_FORCE_ADAPTIVE));
+  const bool want_xslice =
+      (flags & LHPC_PLAN_FORCE_XSLICE) ||
+      (auto_ok && x_bytes > 8.0e6 && gather_lines_per_nnz(rp, col_idx, n_rows, tsz) > locality_thr);
   if (want_xslice && nnz > 0) {
     int P = static_cast<int>(std::ceil(x_bytes / (8.0 * slice_mb * 1.0e6)));
     P = std::max(1, std::min(P, 32));

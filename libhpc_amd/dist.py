@@ -201,3 +201,121 @@ class DistSpMVOverlap:
         for w in works:
             w.wait()
         return self.y_full[:self.blocks.n]
+
+
+# ------------------------------------------------------------------ CG
+class HipOps:
+    """CG vector building blocks on the GPU (include/lhpc.h lhpc_vec_dot /
+    lhpc_cg_step_xr / lhpc_cg_step_p)."""
+
+    def __init__(self, stream=None):
+        self.stream = stream
+
+    def dot(self, a, b, out):
+        from . import vec_dot
+        vec_dot(a, b, out, stream=self.stream)
+
+    def step_xr(self, num, den, x, p, r, q, rr_out):
+        from . import cg_step_xr
+        cg_step_xr(num, den, x, p, r, q, rr_out, stream=self.stream)
+
+    def step_p(self, num, den, r, p):
+        from . import cg_step_p
+        cg_step_p(num, den, r, p, stream=self.stream)
+
+
+class TorchCPUOps:
+    """The same building blocks on CPU tensors — for the gloo tests of the
+    distributed control flow only (the GPU path uses HipOps)."""
+
+    def dot(self, a, b, out):
+        import torch
+        out.copy_(torch.dot(a.double(), b.double()).reshape(1))
+
+    def step_xr(self, num, den, x, p, r, q, rr_out):
+        a = (num / den).to(x.dtype)
+        x.add_(a * p)
+        r.sub_(a * q)
+        self.dot(r, r, rr_out)
+
+    def step_p(self, num, den, r, p):
+        beta = (num / den).to(p.dtype)
+        p.mul_(beta).add_(r)
+
+
+class DistCG:
+    """Conjugate gradient on `world` ranks (one per GPU): contiguous equal row
+    blocks (InterleavedBlocks(n, world, 1)), every rank holding its block of
+    A (an SpMVPlan over the global columns), its blocks of x, r, q and a full
+    replica of p.  Per iteration: local q = A_blk·p; p·q and r·r are
+    all-reduced (RCCL over xGMI with backend "nccl"); after p = r + β·p the
+    p blocks are all-gathered so the next SpMV sees the whole p — the
+    "y becomes the next x" exchange of SURVEY §8e/§8f.  Padding rows (block
+    size × world > n) are empty rows with b = 0, so they stay 0 and do not
+    touch the dots.
+
+    ``local_spmv(p_full_n, q_block)`` computes this rank's block;
+    ``ops``: HipOps (GPU) or TorchCPUOps (gloo tests)."""
+
+    def __init__(self, blocks: InterleavedBlocks, rank: int, local_spmv: Callable, ops, like, group=None):
+        import torch
+        assert blocks.K == 1
+        self.blocks, self.rank, self.fn, self.ops, self.group = blocks, rank, local_spmv, ops, group
+        B, W = blocks.B, blocks.world
+        self.p_full = torch.zeros(B * W, dtype=like.dtype, device=like.device)
+        self.p = torch.zeros(B, dtype=like.dtype, device=like.device)
+        self.r = torch.zeros_like(self.p)
+        self.q = torch.zeros_like(self.p)
+        self.s = torch.zeros(4, dtype=torch.float64, device=like.device)  # rr0, rr1, pq, bb
+
+    def _allreduce(self, t):
+        import torch.distributed as dist
+        if self.blocks.world > 1:
+            dist.all_reduce(t, group=self.group)
+
+    def _gather(self, dst, src):
+        import torch.distributed as dist
+        if self.blocks.world > 1:
+            dist.all_gather_into_tensor(dst, src, group=self.group)
+        else:
+            dst.copy_(src)
+
+    def solve(self, b, x, tol: float = 1e-8, max_iter: int = 1000, check_every: int = 1):
+        """b, x: this rank's blocks (length B, padded rows 0); x updated in
+        place.  Returns (x, iterations, ‖r‖/‖b‖)."""
+        n = self.blocks.n
+        s = self.s
+        rr = [s[0:1], s[1:2]]
+        pq, bb = s[2:3], s[3:4]
+        self.ops.dot(b, b, bb)
+        self._allreduce(bb)
+        self._gather(self.p_full, x)          # x_full for r = b − A·x
+        self.fn(self.p_full[:n], self.q)
+        self.r.copy_(b)
+        self.r.sub_(self.q)
+        self.p.copy_(self.r)
+        self.ops.dot(self.r, self.r, rr[0])
+        self._allreduce(rr[0])
+        h_bb = float(bb.item())
+        stop = tol * tol * (h_bb if h_bb > 0 else 1.0)
+        h_rr = float(rr[0].item())
+        cur, it = 0, 0
+        if h_rr > stop:
+            self._gather(self.p_full, self.p)
+            for it in range(1, max_iter + 1):
+                self.fn(self.p_full[:n], self.q)
+                self.ops.dot(self.p, self.q, pq)
+                self._allreduce(pq)
+                self.ops.step_xr(rr[cur], pq, x, self.p, self.r, self.q, rr[cur ^ 1])
+                self._allreduce(rr[cur ^ 1])
+                if it % check_every == 0 or it == max_iter:
+                    h_rr = float(rr[cur ^ 1].item())
+                    if not np.isfinite(h_rr):
+                        raise FloatingPointError("DistCG: breakdown (non-finite residual)")
+                    if h_rr <= stop:
+                        break
+                self.ops.step_p(rr[cur ^ 1], rr[cur], self.r, self.p)
+                self._gather(self.p_full, self.p)
+                cur ^= 1
+        res = float(np.sqrt(max(h_rr, 0.0)) / np.sqrt(h_bb if h_bb > 0 else 1.0))
+        return x, it, res

@@ -342,3 +342,59 @@ ORACLE_API int64_t NAME(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32
 }
 ORACLE_COO(oracle_coo_to_csr_f64, double)
 ORACLE_COO(oracle_coo_to_csr_f32, float)
+
+/* ------------------------------------------------------------------ CG
+ * Conjugate gradient in fp64 (no reference counterpart):
+ * the textbook recurrence the GPU solver (lhpc_solver.hip) runs —
+ *   r = b - A·x; p = r; rr = r·r
+ *   loop: q = A·p; α = rr / p·q; x += α·p; r -= α·q; rr' = r·r;
+ *         stop if rr' ≤ tol²·b·b; β = rr'/rr; p = r + β·p
+ * with sequential ascending-index sums.  Returns the iterations run;
+ * *resid = ‖r‖/‖b‖ of the recursive residual.  x is the initial guess in.  */
+ORACLE_API int oracle_cg_f64(int64_t n, const void *rp, int bits, const int32_t *col, const double *val,
+                             const double *b, double *x, double tol, int max_iter, double *resid) {
+  double *r = (double *)malloc((size_t)(n > 0 ? n : 1) * 8), *p = (double *)malloc((size_t)(n > 0 ? n : 1) * 8),
+         *q = (double *)malloc((size_t)(n > 0 ? n : 1) * 8);
+  double bb = 0.0, rr = 0.0;
+  for (int64_t i = 0; i < n; ++i) bb += b[i] * b[i];
+  for (int64_t i = 0; i < n; ++i) {
+    double s = 0.0;
+    for (int64_t k = rp_at(rp, bits, i); k < rp_at(rp, bits, i + 1); ++k) s += val[k] * x[col[k]];
+    r[i] = b[i] - s;
+    p[i] = r[i];
+    rr += r[i] * r[i];
+  }
+  const double stop = tol * tol * (bb > 0.0 ? bb : 1.0);
+  int it = 0;
+  if (rr > stop) {
+    for (it = 1; it <= max_iter; ++it) {
+      double pq = 0.0;
+      for (int64_t i = 0; i < n; ++i) {
+        double s = 0.0;
+        for (int64_t k = rp_at(rp, bits, i); k < rp_at(rp, bits, i + 1); ++k) s += val[k] * p[col[k]];
+        q[i] = s;
+      }
+      for (int64_t i = 0; i < n; ++i) pq += p[i] * q[i];
+      const double alpha = rr / pq;
+      double rn = 0.0;
+      for (int64_t i = 0; i < n; ++i) {
+        x[i] += alpha * p[i];
+        r[i] -= alpha * q[i];
+        rn += r[i] * r[i];
+      }
+      if (rn <= stop) {
+        rr = rn;
+        break;
+      }
+      const double beta = rn / rr;
+      for (int64_t i = 0; i < n; ++i) p[i] = r[i] + beta * p[i];
+      rr = rn;
+    }
+    if (it > max_iter) it = max_iter;
+  }
+  *resid = sqrt(rr) / sqrt(bb > 0.0 ? bb : 1.0);
+  free(r);
+  free(p);
+  free(q);
+  return it;
+}

@@ -34,6 +34,8 @@ def load_oracle():
         lib.cpu_blur_x_sse.restype = _i
         lib.cpu_blur_y_sse.restype = _i
         lib.oracle_stencil7.argtypes = [_p, _p, _i64, _i64, _i64, _i64, _f, _f, _i]
+        lib.oracle_cg_f64.argtypes = [_i64, _p, _i, _p, _p, _p, _p, C.c_double, _i, _p]
+        lib.oracle_cg_f64.restype = _i
         lib.oracle_radix_sort_u32.argtypes = [_p, _p, _i64, _i, _i]
         lib.oracle_radix_sort_u64.argtypes = [_p, _p, _i64, _i, _i]
         for f in (lib.oracle_coo_to_csr_f32, lib.oracle_coo_to_csr_f64):
@@ -175,3 +177,24 @@ def ref_gpu_test_keys(n):
     a = np.empty(n, dtype=np.uint32)
     lib.ref_gpu_test_keys(_ptr(a), n)
     return a
+
+
+# ------------------------------------------------------------ CG
+def cg_oracle(rp, col, val, b, x0=None, tol=1e-8, max_iter=1000):
+    """fp64 CG restatement (oracle.c): (x, iterations, ‖r‖/‖b‖)."""
+    lib = load_oracle()
+    n = rp.size - 1
+    v = np.ascontiguousarray(val, dtype=np.float64)
+    bb = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(n) if x0 is None else np.array(x0, dtype=np.float64)
+    res = C.c_double(0.0)
+    it = lib.oracle_cg_f64(n, _ptr(rp), _bits(rp), _ptr(col), _ptr(v), _ptr(bb), _ptr(x), tol, max_iter,
+                           C.byref(res))
+    return x, it, res.value
+
+
+def laplacian_2d(nx, ny, dtype=np.float64, shift=0.0):
+    """5-point Dirichlet Laplacian CSR (libhpc_amd.gen_laplacian_2d; int32 row_ptr)."""
+    import libhpc_amd as L
+    rp, col, val = L.gen_laplacian_2d(nx, ny, L.F32 if dtype == np.float32 else L.F64, shift)
+    return rp.astype(np.int32), col, val

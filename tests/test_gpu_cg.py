@@ -1,0 +1,112 @@
+"""GPU conjugate gradient (lhpc_cg_solve and its building blocks; SURVEY §8f
+rank 3) against the fp64 CG restatement in oracle/oracle.c.
+
+Tolerances (floating point: the GPU sums dots in a different fixed order):
+fp64 — same iteration count ±1 and ‖x_gpu − x_oracle‖ ≤ 1e-8·‖x_oracle‖ at
+tol 1e-10; fp32 vectors — converged to tol 1e-5 and within 1e-4 of the fp64
+solution.  Building blocks: fp64 dots within 1e-12 relative of numpy."""
+import numpy as np
+import pytest
+
+from tests import _support as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(gpu, a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+
+
+@pytest.mark.parametrize("shape", [(64, 48), (200, 150), (7, 1)])
+@pytest.mark.parametrize("flags", [0, 1 << 4, 1 << 6])
+def test_cg_fp64_matches_oracle(lhpc, gpu, shape, flags):
+    rp, col, val = S.laplacian_2d(*shape)
+    n = rp.size - 1
+    b = np.random.default_rng(n).uniform(-1, 1, n)
+    want, it_o, res_o = S.cg_oracle(rp, col, val, b, tol=1e-10, max_iter=5000)
+    with lhpc.SpMVPlan(rp, col, val, n, flags=flags) as plan:
+        x, it, res = lhpc.cg(plan, _dev(gpu, b), tol=1e-10, max_iter=5000)
+    x = x.cpu().numpy()
+    assert abs(it - it_o) <= 1 and res <= 1e-10
+    assert np.linalg.norm(x - want) <= 1e-8 * np.linalg.norm(want)
+
+
+def test_cg_fp32(lhpc, gpu):
+    rp, col, val = S.laplacian_2d(128, 128, dtype=np.float32, shift=0.5)
+    n = rp.size - 1
+    b = np.random.default_rng(3).uniform(-1, 1, n).astype(np.float32)
+    want, _, _ = S.cg_oracle(rp, col, val, b.astype(np.float64), tol=1e-12, max_iter=5000)
+    with lhpc.SpMVPlan(rp, col, val, n) as plan:
+        x, it, res = lhpc.cg(plan, _dev(gpu, b), tol=1e-5, max_iter=5000, check_every=5)
+    assert res <= 1e-5 and it % 5 == 0
+    x = x.cpu().numpy().astype(np.float64)
+    assert np.linalg.norm(x - want) <= 1e-4 * np.linalg.norm(want)
+
+
+def test_cg_warm_start_and_zero_rhs(lhpc, gpu):
+    import torch
+    rp, col, val = S.laplacian_2d(32, 32)
+    n = rp.size - 1
+    with lhpc.SpMVPlan(rp, col, val, n) as plan:
+        x, it, res = lhpc.cg(plan, torch.zeros(n, dtype=torch.float64, device=gpu))
+        assert it == 0 and res == 0.0 and torch.count_nonzero(x) == 0
+        b = _dev(gpu, np.linspace(-1, 1, n))
+        x1, it1, _ = lhpc.cg(plan, b, tol=1e-12)
+        x2, it2, _ = lhpc.cg(plan, b, x=x1.clone(), tol=1e-10)
+        assert it2 <= 1 and torch.allclose(x2, x1, rtol=0, atol=1e-11)
+
+
+def test_cg_breakdown_reported(lhpc, gpu):
+    """[[0,1],[1,0]] with b = e0: p·Ap = 0 on the first step → non-finite → error."""
+    rp = np.array([0, 1, 2], np.int32)
+    col = np.array([1, 0], np.int32)
+    val = np.array([1.0, 1.0])
+    with lhpc.SpMVPlan(rp, col, val, 2) as plan:
+        with pytest.raises(lhpc.LhpcError):
+            lhpc.cg(plan, _dev(gpu, np.array([1.0, 0.0])))
+
+
+def test_cg_building_blocks(lhpc, gpu):
+    import torch
+    rng = np.random.default_rng(7)
+    n = 1_000_003
+    for dt in (np.float64, np.float32):
+        a, b, x, p, r, q = (rng.uniform(-1, 1, n).astype(dt) for _ in range(6))
+        out = torch.zeros(1, dtype=torch.float64, device=gpu)
+        lhpc.vec_dot(_dev(gpu, a), _dev(gpu, b), out)
+        want = float(np.dot(a.astype(np.float64), b.astype(np.float64)))
+        assert abs(out.item() - want) <= 1e-12 * np.abs(a.astype(np.float64) * b).sum()
+        num = torch.tensor([0.75], dtype=torch.float64, device=gpu)
+        den = torch.tensor([1.5], dtype=torch.float64, device=gpu)
+        xd, pd, rd, qd = (_dev(gpu, v) for v in (x, p, r, q))
+        rr = torch.zeros(1, dtype=torch.float64, device=gpu)
+        lhpc.cg_step_xr(num, den, xd, pd, rd, qd, rr)
+        al = dt(0.5)
+        xw = (x + al * p).astype(dt)
+        rw = (r - al * q).astype(dt)
+        assert np.array_equal(xd.cpu().numpy(), xw) and np.array_equal(rd.cpu().numpy(), rw)
+        assert abs(rr.item() - float(np.dot(rw.astype(np.float64), rw))) <= 1e-12 * n
+        lhpc.cg_step_p(num, den, rd, pd)
+        assert np.array_equal(pd.cpu().numpy(), (rw + al * p).astype(dt))
+
+
+def test_dist_cg_hip_ops_world1(lhpc, gpu):
+    """The multi-GPU solver's data path at world 1 (HipOps, padded block plan)
+    converges to the same solution as lhpc_cg_solve."""
+    import torch
+    from libhpc_amd.dist import DistCG, HipOps, InterleavedBlocks
+    rp, col, val = S.laplacian_2d(100, 70)
+    n = rp.size - 1
+    b = np.random.default_rng(11).uniform(-1, 1, n)
+    ib = InterleavedBlocks(n, 1, 1)
+    lrp, lc, lv = ib.local_csr(rp, col, val, 0, 0)
+    with lhpc.SpMVPlan(lrp, lc, lv, n) as plan, lhpc.SpMVPlan(rp, col, val, n) as full:
+        bd = torch.zeros(ib.B, dtype=torch.float64, device=gpu)
+        bd[:n] = _dev(gpu, b)
+        x = torch.zeros_like(bd)
+        solver = DistCG(ib, 0, lambda pf, qb: plan(pf, qb), HipOps(), like=bd)
+        x, it, res = solver.solve(bd, x, tol=1e-10, max_iter=3000)
+        x1, it1, res1 = lhpc.cg(full, _dev(gpu, b), tol=1e-10, max_iter=3000)
+    assert abs(it - it1) <= 1 and res <= 1e-10
+    assert torch.linalg.norm(x[:n] - x1) <= 1e-8 * torch.linalg.norm(x1)
