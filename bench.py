@@ -98,11 +98,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # one rank per GPU; the modulo only matters for the 1-GPU rehearsal of the
+    # N>1 path (LHPC_DIST_BACKEND=gloo, ranks sharing cuda:0) — identity on a full node
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("LHPC_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     def barrier():
         if world > 1:
