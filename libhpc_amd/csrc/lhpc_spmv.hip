@@ -653,7 +653,12 @@ int launch_rowgroup_t(const lhpc_spmv_plan *p, const void *x, void *y, hipStream
 template <typename T, typename I>
 int launch_rowgroup(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
   switch (p->L * 100 + p->R) {
+    case 101: return launch_rowgroup_t<T, I, 1, 1>(p, x, y, s);
+    case 201: return launch_rowgroup_t<T, I, 2, 1>(p, x, y, s);
+    case 202: return launch_rowgroup_t<T, I, 2, 2>(p, x, y, s);
     case 401: return launch_rowgroup_t<T, I, 4, 1>(p, x, y, s);
+    case 402: return launch_rowgroup_t<T, I, 4, 2>(p, x, y, s);
+    case 404: return launch_rowgroup_t<T, I, 4, 4>(p, x, y, s);
     case 802: return launch_rowgroup_t<T, I, 8, 2>(p, x, y, s);
     case 804: return launch_rowgroup_t<T, I, 8, 4>(p, x, y, s);
     case 1601: return launch_rowgroup_t<T, I, 16, 1>(p, x, y, s);
@@ -871,7 +876,13 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
   const double mean = n_rows ? static_cast<double>(nnz) / static_cast<double>(n_rows) : 0;
   const double var = n_rows ? sum2 / static_cast<double>(n_rows) - mean * mean : 0;
   const double cv = mean > 0 ? std::sqrt(std::max(var, 0.0)) / mean : 0;
-  bool adaptive = (cv > 1.0 && maxlen > 256) || maxlen > 4096;
+  // Off the XSLICE path ADAPTIVE (nnz-balanced blocks, coalesced col/val stream,
+  // LDS row sums) is the default: measured equal or faster than ROWGROUP on
+  // uniform rows of 3-40 nnz (within 4% at 8 and 24), and 1.26-1.5× faster on
+  // C1 and the 2-D Laplacians (tools/explore_rowlen.py).
+  // ROWGROUP stays selectable (FORCE_ROWGROUP); `cv`/`maxlen` are kept for info.
+  (void)cv;
+  bool adaptive = true;
   if (flags & LHPC_PLAN_FORCE_ROWGROUP) adaptive = false;
   if (flags & LHPC_PLAN_FORCE_ADAPTIVE) adaptive = true;
   // XSLICE when x outgrows one XCD's 4 MB L2 and rows are short enough for

@@ -263,7 +263,8 @@ class DistCG:
         self.blocks, self.rank, self.fn, self.ops, self.group = blocks, rank, local_spmv, ops, group
         B, W = blocks.B, blocks.world
         self.p_full = torch.zeros(B * W, dtype=like.dtype, device=like.device)
-        self.p = torch.zeros(B, dtype=like.dtype, device=like.device)
+        # world 1: p is the replica itself (no gather copy)
+        self.p = self.p_full[:B] if W == 1 else torch.zeros(B, dtype=like.dtype, device=like.device)
         self.r = torch.zeros_like(self.p)
         self.q = torch.zeros_like(self.p)
         self.s = torch.zeros(4, dtype=torch.float64, device=like.device)  # rr0, rr1, pq, bb
@@ -277,8 +278,8 @@ class DistCG:
         import torch.distributed as dist
         if self.blocks.world > 1:
             dist.all_gather_into_tensor(dst, src, group=self.group)
-        else:
-            dst.copy_(src)
+        elif dst.data_ptr() != src.data_ptr():
+            dst[:src.numel()].copy_(src)
 
     def solve(self, b, x, tol: float = 1e-8, max_iter: int = 1000, check_every: int = 1):
         """b, x: this rank's blocks (length B, padded rows 0); x updated in
