@@ -137,3 +137,27 @@ def test_stencil7_every_impl(lhpc, gpu, impl, store, monkeypatch):
         want = S.stencil7_oracle(u, nz, ny, nx, g, -6.0, 1.0, out=out0.copy())
         got = lhpc.stencil7(_dev(gpu, u), _dev(gpu, out0), nz, ny, nx, g, -6.0, 1.0).cpu().numpy()
         assert np.array_equal(got, want), (impl, store, nz, ny, nx, g)
+
+
+BX_IMPLS = [("wave", "1"), ("wave", "2"), ("wave", "4"), ("wave", "8"), ("wave", "16"), ("wave", "32"),
+            ("lds", "1"), ("lds", "2"), ("lds", "4"), ("lds", "8")]
+
+
+@pytest.mark.parametrize("impl,rows", BX_IMPLS)
+def test_blur_x_every_impl(lhpc, gpu, impl, rows, monkeypatch):
+    """Every blur_x implementation (LHPC_BLUR_X_IMPL / _RW / _ROWS) is bit-exact
+    against the oracle on vector-eligible ragged shapes: nx not a multiple of
+    the 256 / 1024-float segments, ny not a multiple of the row group."""
+    import torch
+    if impl == "wave":
+        monkeypatch.setenv("LHPC_BLUR_X_IMPL", "wave")
+        monkeypatch.setenv("LHPC_BLUR_X_RW", rows)
+    else:
+        monkeypatch.setenv("LHPC_BLUR_X_IMPL", "lds")
+        monkeypatch.setenv("LHPC_BLUR_X_ROWS", rows)
+    for ny, nx, ghost in ((37, 260, 8), (5, 1300, 8), (70, 2048, 12), (1, 4, 8)):
+        a = S.random_padded(((ny + 2 * ghost) * (nx + 2 * ghost),), seed=ny * 31 + nx)
+        want = S.blur_oracle(a, ny, nx, ghost, 8, False)
+        b = torch.empty(ny * nx, dtype=torch.float32, device=gpu)
+        got = lhpc.blur_x(_dev(gpu, a), b, ny, nx, ghost, 8).cpu().numpy()
+        assert np.array_equal(got, want), (impl, rows, ny, nx, ghost)

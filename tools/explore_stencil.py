@@ -16,8 +16,13 @@ n, g = 8192, 8
 a = torch.rand((n + 2 * g) ** 2, device=dev) * 2 - 1
 bb = torch.empty(n * n, device=dev)
 ref = None
-for rows in ("2",):
-    os.environ["LHPC_BLUR_X_ROWS"] = rows
+for rows in os.environ.get("BX_CFGS", "2 wave:2 wave:4 wave:8 wave:16 wave:32 2").split():
+    if rows.startswith("wave"):
+        os.environ["LHPC_BLUR_X_IMPL"] = "wave"
+        os.environ["LHPC_BLUR_X_RW"] = rows.split(":")[1]
+    else:
+        os.environ["LHPC_BLUR_X_IMPL"] = "lds"
+        os.environ["LHPC_BLUR_X_ROWS"] = rows
     t = timeit(lambda: L.blur_x(a, bb, n, n, g, 8, stream=st))
     out = bb.clone()
     if ref is None: ref = out
