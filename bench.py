@@ -353,7 +353,8 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
     plan = L.SpMVPlan(*ib.local_csr(rp, col, val, rank, 0), n)
     bd = torch.zeros(ib.B, dtype=torch.float64, device=dev)
     bd[:r1 - r0] = torch.from_numpy(b[r0:r1]).to(dev)
-    solver = DistCG(ib, rank, lambda pf, qb: plan(pf, qb, stream=stream), HipOps(stream), like=bd)
+    solver = DistCG(ib, rank, lambda pf, qb: plan(pf, qb, stream=stream), HipOps(stream), like=bd,
+                    local_spmv_dot=lambda pf, qb, wb, out: L.spmv_dot(plan, pf, qb, wb, out, stream=stream))
 
     def run(iters):
         x = torch.zeros_like(bd)

@@ -256,6 +256,11 @@ int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
  *   lhpc_cg_step_xr  α = *alpha_num / *alpha_den; x += α·p; r -= α·q; *rr_out = r·r
  *   lhpc_cg_step_p   β = *beta_num / *beta_den; p = r + β·p
  */
+/* y = A·x and *dot_out = w·y (fp64, the stored y) in one pass for ADAPTIVE
+ * plans (the CG p·q fused into the SpMV epilogue; fixed-order reduction),
+ * SpMV + lhpc_vec_dot otherwise.  Device buffers, asynchronous.            */
+int lhpc_spmv_dot(lhpc_spmv_plan *plan, const void *x, void *y, const void *w,
+                  double *dot_out, void *stream);
 int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, double tol,
                   int max_iter, int check_every, int *iters_out,
                   double *resid_out, void *stream);

@@ -55,7 +55,7 @@ ABI_SYMBOLS = (
     "lhpc_row_ptr_narrow", "lhpc_radix_sort_u32", "lhpc_radix_sort_pairs_u32",
     "lhpc_radix_sort_pairs_u64", "lhpc_coo_to_csr", "lhpc_csr_save", "lhpc_csr_load_header",
     "lhpc_csr_load", "lhpc_mm_read_header", "lhpc_mm_read_coo", "lhpc_cg_solve", "lhpc_vec_dot",
-    "lhpc_cg_step_xr", "lhpc_cg_step_p",
+    "lhpc_cg_step_xr", "lhpc_cg_step_p", "lhpc_spmv_dot",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -128,6 +128,7 @@ _sig("lhpc_radix_sort_pairs_u64", _i, _p, _p, _i64, _i, _i, _i, _p)
 _sig("lhpc_coo_to_csr", _i, _i, _i64, _i64, _i64, _p, _p, _p, _p, _i, _p, _p, C.POINTER(_i64), _i, _p)
 _sig("lhpc_cg_solve", _i, _p, _p, _p, _d, _i, _i, C.POINTER(_i), C.POINTER(_d), _p)
 _sig("lhpc_vec_dot", _i, _i, _i64, _p, _p, _p, _p)
+_sig("lhpc_spmv_dot", _i, _p, _p, _p, _p, _p, _p)
 _sig("lhpc_cg_step_xr", _i, _i, _i64, _p, _p, _p, _p, _p, _p, _p, _p)
 _sig("lhpc_cg_step_p", _i, _i, _i64, _p, _p, _p, _p, _p)
 _sig("lhpc_csr_save", _i, C.c_char_p, _i, _i64, _i64, _i64, _p, _i, _p, _p)
@@ -538,6 +539,15 @@ def cg(plan: "SpMVPlan", b, x=None, tol: float = 1e-8, max_iter: int = 1000, che
     _check(lib.lhpc_cg_solve(plan._h, bp, xp, tol, max_iter, check_every, C.byref(it), C.byref(res),
                              _stream_ptr(st)), "lhpc_cg_solve")
     return x, it.value, res.value
+
+
+def spmv_dot(plan: "SpMVPlan", x, y, w, out, stream=None):
+    """y = A·x and out (1-element float64 device tensor) = w·y, asynchronously
+    (one pass for ADAPTIVE plans)."""
+    st = _dev_stream(x, stream)
+    _check(lib.lhpc_spmv_dot(plan._h, x.data_ptr(), y.data_ptr(), w.data_ptr(), out.data_ptr(), _stream_ptr(st)),
+           "lhpc_spmv_dot")
+    return y, out
 
 
 def vec_dot(a, b, out, stream=None):

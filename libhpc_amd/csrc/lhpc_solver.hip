@@ -4,8 +4,8 @@
 // counterpart.
 //
 // Per iteration (HBM-bound vector work around one SpMV):
-//   q = A·p                         lhpc_spmv (XSLICE / ROWGROUP / ADAPTIVE)
-//   pq = p·q                        k_dot_partial + k_dot_finish
+//   q = A·p, pq = p·q               lhpc_spmv_dot (fused into the ADAPTIVE epilogue;
+//                                   SpMV + k_dot_partial/k_dot_finish for other plans)
 //   α = rr/pq; x += α·p; r -= α·q;  k_cg_xr (one pass: reads x p r q, writes x r,
 //   rr' = r·r                         block partials of rr') + k_dot_finish
 //   β = rr'/rr; p = r + β·p         k_cg_p
@@ -234,9 +234,7 @@ extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, doubl
   int status = LHPC_OK;
   if (h_rr > stop) {
     for (it = 1; it <= max_iter; ++it) {
-      LHPC_TRY(lhpc_spmv(plan, p, q, 1, s));
-      if (dtype == LHPC_F32) LHPC_TRY(dot_dev(static_cast<const float *>(p), static_cast<const float *>(q), n, pq, part, s));
-      else LHPC_TRY(dot_dev(static_cast<const double *>(p), static_cast<const double *>(q), n, pq, part, s));
+      LHPC_TRY(lhpc_spmv_dot(plan, p, q, p, pq, s));  // q = A·p and p·q in one pass (ADAPTIVE)
       LHPC_TRY(lhpc_cg_step_xr(dtype, n, rr[cur], pq, x, p, r, q, rr[cur ^ 1], s));
       if (it % check_every == 0 || it == max_iter) {
         LHPC_HIP_TRY(hipMemcpyAsync(&h_rr, rr[cur ^ 1], 8, hipMemcpyDeviceToHost, s));

@@ -110,7 +110,9 @@ template <typename T, typename I>
 __global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
     const I *__restrict__ row_ptr, const int32_t *__restrict__ col,
     const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y,
-    const int64_t *__restrict__ blocks) {
+    const int64_t *__restrict__ blocks, const T *__restrict__ w, double *__restrict__ dpart) {
+  // DOT (w != nullptr): also dpart[block] = Σ_rows y[row]·w[row] over the block's rows
+  // (the stored, rounded y), reduced in a fixed order — the CG p·q fused into the SpMV.
   __shared__ double prod[kBlockNnz];
   __shared__ double wsum[kBlock / kWave];
   const int tid = threadIdx.x;
@@ -132,8 +134,10 @@ __global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
     if (tid == 0) {
       double t = wsum[0];
 #pragma unroll
-      for (int w = 1; w < kBlock / kWave; ++w) t += wsum[w];
-      y[r0] = static_cast<T>(t);
+      for (int i = 1; i < kBlock / kWave; ++i) t += wsum[i];
+      const T yv = static_cast<T>(t);
+      y[r0] = yv;
+      if (w) dpart[blockIdx.x] = static_cast<double>(yv) * static_cast<double>(w[r0]);
     }
     return;
   }
@@ -177,7 +181,24 @@ __global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
     case 2: a = group_sum<2>(a); break;
     default: break;
   }
-  if (grp < nrows && sub == 0) y[r0 + grp] = static_cast<T>(a);
+  double d = 0.0;
+  if (grp < nrows && sub == 0) {
+    const T yv = static_cast<T>(a);
+    y[r0 + grp] = yv;
+    if (w) d = static_cast<double>(yv) * static_cast<double>(w[r0 + grp]);
+  }
+  if (w) {  // block-uniform
+    d = group_sum<kWave>(d);
+    __syncthreads();  // wsum reuse
+    if ((tid & (kWave - 1)) == 0) wsum[tid / kWave] = d;
+    __syncthreads();
+    if (tid == 0) {
+      double t = wsum[0];
+#pragma unroll
+      for (int i = 1; i < kBlock / kWave; ++i) t += wsum[i];
+      dpart[blockIdx.x] = t;
+    }
+  }
 }
 
 // --------------------------------------------------------------- XSLICE
@@ -612,6 +633,7 @@ struct lhpc_spmv_plan {
   int64_t *d_blocks = nullptr;
   int64_t n_blocks = 0, n_long = 0;
   void *d_xstage = nullptr, *d_ystage = nullptr;
+  double *d_dpart = nullptr;  // lhpc_spmv_dot: per-block partials (ADAPTIVE), allocated on first use
   int kernel = LHPC_KERNEL_ROWGROUP;
   int L = 16, R = 4;
   int64_t bytes = 0;
@@ -673,13 +695,43 @@ int launch_rowgroup(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t
 }
 
 template <typename T, typename I>
-int launch_adaptive(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+int launch_adaptive(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s, const void *w = nullptr,
+                    double *dpart = nullptr) {
   if (p->n_blocks == 0) return LHPC_OK;
   hipLaunchKernelGGL((k_spmv_adaptive<T, I>), dim3(static_cast<unsigned>(p->n_blocks)),
                      dim3(kBlock), 0, s, static_cast<const I *>(p->d_row_ptr), p->d_col,
                      static_cast<const T *>(p->d_val), static_cast<const T *>(x),
-                     static_cast<T *>(y), p->d_blocks);
+                     static_cast<T *>(y), p->d_blocks, static_cast<const T *>(w), dpart);
   return check_launch(s);
+}
+
+// Fixed-order two-stage sum of the per-block dot partials: stage 1 reduces
+// 2048 consecutive partials per block (8 independent loads per thread), stage
+// 2 (one block) the ≤ ⌈nb/2048⌉ stage-1 sums.  One block looping over ~10^5
+// partials would serialise on L2 latency.
+constexpr int kFinTile = 2048;
+__global__ __launch_bounds__(kBlock) void k_dpart_finish(const double *__restrict__ part, int64_t nb,
+                                                         double *__restrict__ out) {
+  __shared__ double wsum[kBlock / kWave];
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kFinTile;
+  double v[kFinTile / kBlock];
+#pragma unroll
+  for (int k = 0; k < kFinTile / kBlock; ++k) {
+    const int64_t i = b0 + k * kBlock + threadIdx.x;
+    v[k] = i < nb ? part[i] : 0.0;
+  }
+  double a = 0.0;
+#pragma unroll
+  for (int k = 0; k < kFinTile / kBlock; ++k) a += v[k];
+  a = group_sum<kWave>(a);
+  if ((threadIdx.x & (kWave - 1)) == 0) wsum[threadIdx.x / kWave] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = wsum[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / kWave; ++i) t += wsum[i];
+    out[blockIdx.x] = t;
+  }
 }
 
 template <typename T>
@@ -1091,6 +1143,41 @@ extern "C" int lhpc_spmv(lhpc_spmv_plan *p, const void *x, void *y, int on_devic
   return LHPC_OK;
 }
 
+extern "C" int lhpc_vec_dot(int dtype, int64_t n, const void *a, const void *b, double *out, void *stream);
+
+extern "C" int lhpc_spmv_dot(lhpc_spmv_plan *p, const void *x, void *y, const void *w, double *dot_out,
+                             void *stream) {
+  if (!p || !dot_out || (p->n_cols > 0 && !x) || (p->n_rows > 0 && (!y || !w))) return LHPC_ERR_INVALID_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  LHPC_HIP_TRY(hipSetDevice(p->device));
+  if (p->kernel == LHPC_KERNEL_ADAPTIVE && p->n_blocks > 0) {
+    const int64_t n1 = (p->n_blocks + kFinTile - 1) / kFinTile;  // stage-1 sums, after the partials
+    if (!p->d_dpart)
+      LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_dpart), (p->n_blocks + n1) * sizeof(double), p->bytes));
+    int st;
+    if (p->dtype == LHPC_F32)
+      st = p->rp64 ? launch_adaptive<float, int64_t>(p, x, y, s, w, p->d_dpart)
+                   : launch_adaptive<float, int32_t>(p, x, y, s, w, p->d_dpart);
+    else
+      st = p->rp64 ? launch_adaptive<double, int64_t>(p, x, y, s, w, p->d_dpart)
+                   : launch_adaptive<double, int32_t>(p, x, y, s, w, p->d_dpart);
+    LHPC_TRY(st);
+    double *stage1 = p->d_dpart + p->n_blocks;
+    if (n1 == 1) {
+      hipLaunchKernelGGL(k_dpart_finish, dim3(1), dim3(kBlock), 0, s, p->d_dpart, p->n_blocks, dot_out);
+    } else {
+      hipLaunchKernelGGL(k_dpart_finish, dim3(static_cast<unsigned>(n1)), dim3(kBlock), 0, s, p->d_dpart,
+                         p->n_blocks, stage1);
+      if (n1 > kFinTile) return LHPC_ERR_UNSUPPORTED;  // > 4M blocks (> 8·10^9 nonzeros)
+      hipLaunchKernelGGL(k_dpart_finish, dim3(1), dim3(kBlock), 0, s, stage1, n1, dot_out);
+    }
+    return check_launch(s);
+  }
+  // other kernel families: SpMV, then a separate dot pass
+  LHPC_TRY(lhpc_spmv(p, x, y, 1, stream));
+  return lhpc_vec_dot(p->dtype, p->n_rows, w, y, dot_out, stream);
+}
+
 extern "C" int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *p, lhpc_spmv_plan_info *info) {
   if (!p || !info) return LHPC_ERR_INVALID_ARG;
   info->dtype = p->dtype;
@@ -1116,7 +1203,7 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
   for (void *q : {p->d_row_ptr, static_cast<void *>(p->d_col), p->d_val,
                   static_cast<void *>(p->d_blocks), p->d_xstage, p->d_ystage,
                   p->d_lens, static_cast<void *>(p->d_cbase), p->d_partial,
-                  static_cast<void *>(p->d_arrive)})
+                  static_cast<void *>(p->d_arrive), static_cast<void *>(p->d_dpart)})
     if (q) (void)hipFree(q);
   delete p;
   return LHPC_OK;

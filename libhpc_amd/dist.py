@@ -255,12 +255,17 @@ class DistCG:
     touch the dots.
 
     ``local_spmv(p_full_n, q_block)`` computes this rank's block;
+    ``local_spmv_dot(p_full_n, q_block, w_block, out)``, if given, also
+    writes w·q into ``out`` in the same pass (lhpc_spmv_dot: the p·q dot
+    fused into the ADAPTIVE epilogue);
     ``ops``: HipOps (GPU) or TorchCPUOps (gloo tests)."""
 
-    def __init__(self, blocks: InterleavedBlocks, rank: int, local_spmv: Callable, ops, like, group=None):
+    def __init__(self, blocks: InterleavedBlocks, rank: int, local_spmv: Callable, ops, like, group=None,
+                 local_spmv_dot: Optional[Callable] = None):
         import torch
         assert blocks.K == 1
         self.blocks, self.rank, self.fn, self.ops, self.group = blocks, rank, local_spmv, ops, group
+        self.fn_dot = local_spmv_dot
         B, W = blocks.B, blocks.world
         self.p_full = torch.zeros(B * W, dtype=like.dtype, device=like.device)
         # world 1: p is the replica itself (no gather copy)
@@ -304,8 +309,11 @@ class DistCG:
         if h_rr > stop:
             self._gather(self.p_full, self.p)
             for it in range(1, max_iter + 1):
-                self.fn(self.p_full[:n], self.q)
-                self.ops.dot(self.p, self.q, pq)
+                if self.fn_dot is not None:
+                    self.fn_dot(self.p_full[:n], self.q, self.p, pq)
+                else:
+                    self.fn(self.p_full[:n], self.q)
+                    self.ops.dot(self.p, self.q, pq)
                 self._allreduce(pq)
                 self.ops.step_xr(rr[cur], pq, x, self.p, self.r, self.q, rr[cur ^ 1])
                 self._allreduce(rr[cur ^ 1])

@@ -105,8 +105,31 @@ def test_dist_cg_hip_ops_world1(lhpc, gpu):
         bd = torch.zeros(ib.B, dtype=torch.float64, device=gpu)
         bd[:n] = _dev(gpu, b)
         x = torch.zeros_like(bd)
-        solver = DistCG(ib, 0, lambda pf, qb: plan(pf, qb), HipOps(), like=bd)
+        solver = DistCG(ib, 0, lambda pf, qb: plan(pf, qb), HipOps(), like=bd,
+                        local_spmv_dot=lambda pf, qb, wb, out: lhpc.spmv_dot(plan, pf, qb, wb, out))
         x, it, res = solver.solve(bd, x, tol=1e-10, max_iter=3000)
         x1, it1, res1 = lhpc.cg(full, _dev(gpu, b), tol=1e-10, max_iter=3000)
     assert abs(it - it1) <= 1 and res <= 1e-10
     assert torch.linalg.norm(x[:n] - x1) <= 1e-8 * torch.linalg.norm(x1)
+
+
+@pytest.mark.parametrize("flags", [0, 1 << 4, 1 << 6])
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+def test_spmv_dot(lhpc, gpu, flags, dt):
+    """lhpc_spmv_dot: y bit-identical to lhpc_spmv (same kernel), w·y within
+    1e-12·Σ|w·y| of numpy (fused ADAPTIVE epilogue, or SpMV + dot for the
+    other families); long rows (> 2048 nnz) take the one-row block path."""
+    import torch
+    rp, col, val = lhpc.gen_powerlaw_csr(60_000, 60_000, lmax=5000, dtype=lhpc.F64 if dt == np.float64 else lhpc.F32,
+                                         seed=0x5D07)
+    n = rp.size - 1
+    x = _dev(gpu, np.random.default_rng(1).uniform(-1, 1, n).astype(dt))
+    w = _dev(gpu, np.random.default_rng(2).uniform(-1, 1, n).astype(dt))
+    with lhpc.SpMVPlan(rp, col, val, n, flags=flags) as plan:
+        y0 = plan(x)
+        y = torch.empty_like(y0)
+        out = torch.zeros(1, dtype=torch.float64, device=gpu)
+        lhpc.spmv_dot(plan, x, y, w, out)
+        assert torch.equal(y, y0)
+        yw = y.cpu().numpy().astype(np.float64) * w.cpu().numpy().astype(np.float64)
+        assert abs(out.item() - yw.sum()) <= 1e-12 * np.abs(yw).sum()
