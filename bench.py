@@ -1,6 +1,6 @@
 """bench.py — CSR SpMV throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5|blur_x|blur_y|sort|cg]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c2|c3|c4|c5|blur_x|blur_y|sort|cg]
 
 N=1: BASELINE configs[1] — CSR SpMV, n=10M, nnz=150M (exactly 15 uniform
 distinct sorted columns per row), fp32 values/x/y, A and x resident in HBM.
@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "blur_x", "blur_y", "sort", "cg"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "blur_x", "blur_y", "sort", "cg"])
     ap.add_argument("--n", type=int, default=10_000_000)
     ap.add_argument("--per-row", type=int, default=15)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -116,15 +116,15 @@ def main():
     stream = torch.cuda.current_stream(dev)
     wl = args.workload
     result = {}
-    if wl in ("c2", "c3", "c4"):
-        dt = L.F64 if wl == "c3" else L.F32
+    if wl in ("c1", "c2", "c3", "c4"):
+        dt = L.F64 if wl in ("c1", "c3") else L.F32
         tsz = 8 if dt == L.F64 else 4
-        n = args.n
+        n = 100_000 if wl == "c1" else args.n
         t0 = time.time()
         if wl == "c4":
             rp, col, val = L.gen_powerlaw_csr(n, n, dtype=dt)
         else:
-            rp, col, val = L.gen_uniform_csr(n, n, args.per_row, dtype=dt)
+            rp, col, val = L.gen_uniform_csr(n, n, 10 if wl == "c1" else args.per_row, dtype=dt)
         x = L.gen_values(dt, 0, n, L.SEED_X)
         nnz = int(col.shape[0])
         t_gen = time.time() - t0
@@ -198,11 +198,14 @@ def main():
                    "adaptive": "k_spmv_adaptive"}[kname]
         traffic = load_traffic(f"{wl}_{kname}") if world == 1 else None
         result.update(
-            metric=METRIC, value=gflops, unit="GFLOP/s", n_gpus=world, steps=args.steps,
+            metric=METRIC if wl != "c1" else "CSR SpMV GFLOP/s, n=100k nnz=1M fp64 (BASELINE configs[0])",
+            value=gflops, unit="GFLOP/s", n_gpus=world, steps=args.steps,
             warmup=args.warmup, ms_per_step=per_step * 1e3, higher_is_better=True,
             scaling="strong", vs_baseline=None, dtype="f64" if dt == L.F64 else "f32",
             data="synthetic: deterministic splitmix64 CSR (SURVEY §8d seeds), A/x resident in HBM",
-            config={"workload": {"c2": "BASELINE configs[1]: CSR SpMV n=10M nnz=150M fp32 uniform 15/row",
+            config={"workload": {"c1": "BASELINE configs[0]: CSR SpMV n=100k nnz=1M fp64 uniform 10/row (CPU config; "
+                                       "GPU time beside the 1-thread SIMD baseline)",
+                                 "c2": "BASELINE configs[1]: CSR SpMV n=10M nnz=150M fp32 uniform 15/row",
                                  "c3": "BASELINE configs[2] matrix: CSR SpMV n=10M nnz=150M fp64 uniform 15/row",
                                  "c4": "BASELINE configs[3]: power-law CSR (1..1e4 nnz/row) fp32"}[wl],
                     "n_rows": n, "n_cols": n, "nnz": nnz, "kernel": kname, "slices": info["slices"],
@@ -214,7 +217,8 @@ def main():
             setup_s={"generate": t_gen, "plan": t_plan},
         )
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_spmv_baseline(rp, col, val, x, nnz, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_spmv_baseline(rp, col, val, x, nnz, args.cpu_seconds,
+                                                       threads=1 if wl == "c1" else None)
         for pl in plans:
             pl.close()
     elif wl == "sort":
@@ -233,20 +237,22 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_spmv_baseline(rp, col, val, x, nnz, seconds):
+def cpu_spmv_baseline(rp, col, val, x, nnz, seconds, threads=None):
+    """C1 is quoted single-thread; C2-C4 on all host threads."""
     from tests import _support as S  # oracle/ is test infrastructure: baseline leg only
-    threads = cpu_threads()
+    threads = threads or cpu_threads()
     y, used = S.spmv_cpu_simd(rp, col, val, x, threads=threads)  # warm
     times = []
     t_end = time.perf_counter() + seconds
-    while len(times) < 3 or (time.perf_counter() < t_end and len(times) < 400):
+    while len(times) < 3 or (time.perf_counter() < t_end and len(times) < 200_000):
         t0 = time.perf_counter()
         S.spmv_cpu_simd(rp, col, val, x, threads=threads)
         times.append(time.perf_counter() - t0)
     best = min(times)
     return {"value": 2.0 * nnz / best / 1e9, "unit": "GFLOP/s", "cores": used, "kind": "port",
             "sample": f"full matrix (nnz={nnz}), best of {len(times)} passes "
-                      f"({sum(times):.1f} s), AVX2 gather + OpenMP, oracle/oracle.c cpu_spmv_simd"}
+                      f"({sum(times):.1f} s), AVX2 gather" + (" + OpenMP" if threads > 1 else ", 1 thread")
+                      + ", oracle/oracle.c cpu_spmv_simd"}
 
 
 def stencil_bench(args, L, torch, dev, stream, barrier):
