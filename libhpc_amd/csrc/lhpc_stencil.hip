@@ -802,7 +802,11 @@ constexpr int kDppWaveShr1 = 0x138;  // lane i ← lane i-1 (lane 0 keeps `old`)
 
 // PF = prefetch distance in planes: the ring holds PF + 3 slots (planes z-1, z, z+1 being used,
 // PF planes in flight); its rotation is unrolled so every slot index is a compile-time constant.
-template <int RY, int NJ, int STORE, int PF = 1>  // STORE: 0 plain, 1 non-temporal, 2 none, 3 line-aligned (2, 3: diagnostics)
+// STORE: 0 plain dword stores, 1 non-temporal dword stores, 4 staged: each row's
+// results go to the wave's LDS row (shifted so the body is 16-B aligned) and
+// leave as float4 stores plus ≤ 3-float head/tail pieces (needs a 16-B aligned
+// `out`); 2 no stores and 3 line-aligned rows are timing diagnostics.
+template <int RY, int NJ, int STORE, int PF = 1>
 __global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ u, float *__restrict__ out,
                                                       int64_t nz, int64_t ny, int64_t nx, int64_t g,
                                                       float c0, float c1, int64_t z_begin, int64_t z_end,
@@ -854,8 +858,18 @@ __global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ 
     }
   };
   float diag = 0.f;
+  constexpr int SROW = STORE == 4 ? TW + 4 : 1;
+  __shared__ __attribute__((aligned(16))) float stage[STORE == 4 ? 4 : 1][STORE == 4 ? RY : 1][SROW];
+  const int64_t len = nx - x0 < TW ? nx - x0 : TW;  // outputs of this tile per row
   auto step = [&](const Slot &M, const Slot &Cc, const Slot &Pp, int64_t z) {
     if (z >= ze) return;
+    // staged store: element offset of (z, y0+r, x0) and its 16-B head length, per row
+    int hd[RY];
+#pragma unroll
+    for (int r = 0; r < RY; ++r) {
+      const int64_t e0 = (z + g) * Pyx + rowo[r + 1] + g + x0;
+      hd[r] = static_cast<int>((4 - (e0 & 3)) & 3);
+    }
 #pragma unroll
     for (int r = 0; r < RY; ++r) {
       if (y0 + r >= ny) break;
@@ -883,10 +897,36 @@ __global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ 
         const float res = __fadd_rn(__fmul_rn(c0, cz), __fmul_rn(c1, sum));
         if constexpr (STORE == 2) {
           diag += res;
+        } else if constexpr (STORE == 4) {
+          stage[w][r][kWave * j + lane + ((4 - hd[r]) & 3)] = res;  // x_local + shift: body 16-B aligned
         } else if (x0 + kWave * j + lane < nx) {
           __builtin_amdgcn_raw_buffer_store_b32(fbits(res), ws, (STORE == 3 ? vx - 4 * g : vx) + 256 * j, 0,
                                                 STORE == 1 ? 2 : 0);
         }
+      }
+    }
+    if constexpr (STORE == 4) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int r = 0; r < RY; ++r) {
+        if (y0 + r >= ny) break;
+        const int h = hd[r] < len ? hd[r] : static_cast<int>(len);
+        const int sh = (4 - hd[r]) & 3;
+        float *orow = out + (z + g) * Pyx + rowo[r + 1] + g + x0;
+        const float *st = stage[w][r];
+        if (lane < h) __builtin_nontemporal_store(st[lane + sh], orow + lane);
+        const int nb4 = static_cast<int>((len - h) / 4);
+#pragma unroll
+        for (int k = 0; k < (TW + kWave * 4 - 1) / (kWave * 4); ++k) {
+          const int q = lane + kWave * k;
+          if (q < nb4)
+            __builtin_nontemporal_store(*reinterpret_cast<const f32x4 *>(st + h + 4 * q + sh),
+                                        reinterpret_cast<f32x4 *>(orow + h + 4 * q));
+        }
+        const int t0 = h + 4 * nb4;
+        if (lane < len - t0) __builtin_nontemporal_store(st[t0 + lane + sh], orow + t0 + lane);
       }
     }
   };
@@ -1036,14 +1076,15 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
   const bool use_ring = impl && !std::strcmp(impl, "ring");
   const bool plane32 = (ny + 2 * g) * (nx + 2 * g) < (int64_t{1} << 31);
   const bool use_wide = impl && !std::strcmp(impl, "wide");
-  // Store policy: "plain" | "nt" | "none" / "aligned" (timing diagnostics).  Default: plain for
-  // the buffer ring (measured 220 vs 224-272 us nt), non-temporal for the flat wide ring
-  // (234-238 vs 234-255 us).
+  // Store policy: "staged" | "plain" | "nt" | "none" / "aligned" (timing diagnostics).  Default:
+  // staged float4 stores for the buffer ring (219-220 us vs 225-226 plain on 512^3; plain when
+  // `out` is not 16-B aligned), non-temporal for the flat wide ring (234-238 vs 234-255 us).
   const char *stm = std::getenv("LHPC_STENCIL7_STORE");
   const bool buf_impl = !impl || !std::strcmp(impl, "buf");
-  const int store_mode = stm ? (!std::strcmp(stm, "plain") ? 0 : !std::strcmp(stm, "none") ? 2
-                                : !std::strcmp(stm, "aligned") ? 3 : 1)
-                             : (buf_impl ? 0 : 1);
+  int store_mode = stm ? (!std::strcmp(stm, "plain") ? 0 : !std::strcmp(stm, "none") ? 2
+                          : !std::strcmp(stm, "aligned") ? 3 : !std::strcmp(stm, "staged") ? 4 : 1)
+                       : (buf_impl ? 4 : 1);
+  if (store_mode == 4 && !aligned16(out)) store_mode = 0;  // staged float4 stores need a 16-B base
   // buffer-addressed ring: the in-row byte offset (voffset) must fit 31 bits
   const bool row_b31 = (nx + 2 * g + 1024) * 4 < (int64_t{1} << 31);
   if (buf_impl && row_b31) {
@@ -1081,6 +1122,7 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
     if (store_mode == 1) LHPC_S7B_M(RY, NJ, 1);          \
     else if (store_mode == 2) LHPC_S7B_M(RY, NJ, 2);     \
     else if (store_mode == 3) LHPC_S7B_M(RY, NJ, 3);     \
+    else if (store_mode == 4) LHPC_S7B_M(RY, NJ, 4);     \
     else LHPC_S7B_M(RY, NJ, 0);                          \
   } while (0)
     if (ry == 1 && nj == 8) LHPC_S7B(1, 8);

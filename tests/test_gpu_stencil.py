@@ -119,7 +119,7 @@ S7_IMPLS = ["buf", "buf:2,8,0,2", "buf:4,4,128,3", "buf:2,8,5,3", "buf:2,8,32", 
 
 
 @pytest.mark.parametrize("impl", S7_IMPLS)
-@pytest.mark.parametrize("store", ["nt", "plain"])
+@pytest.mark.parametrize("store", ["nt", "plain", "staged"])
 def test_stencil7_every_impl(lhpc, gpu, impl, store, monkeypatch):
     """Every stencil7 implementation / tiling / store mode selectable through
     LHPC_STENCIL7_* is bit-exact against the oracle on ragged shapes: nx
