@@ -216,6 +216,8 @@ def main():
                       "alg_bytes_per_call": local_alg, "call_us": call_s * 1e6},
             setup_s={"generate": t_gen, "plan": t_plan},
         )
+        if kname == "xslice" and rank == 0:
+            result["roofline"]["gather"] = gather_ceiling(L, torch, dev, stream, local_nnz, call_s)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_spmv_baseline(rp, col, val, x, nnz, args.cpu_seconds,
                                                        threads=1 if wl == "c1" else None)
@@ -235,6 +237,40 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def gather_ceiling(L, torch, dev, stream, nnz, call_s):
+    """The binding limit of uniform-random SpMV on MI355X is the L2 request
+    rate of 4-byte x gathers, not HBM bandwidth.  Measured
+    live: the same number of random gathers from a 4 MB (L2-resident) table
+    with the probe kernel (liblhpc_probe.so, not part of the ABI), against the
+    SpMV's own gathers per second."""
+    import ctypes as C
+    P = C.CDLL(os.path.join(os.path.dirname(L.LIB_PATH), "liblhpc_probe.so"))
+    m = int(nnz)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED0007)
+    idx = torch.randint(0, 1 << 20, (m,), dtype=torch.int32, device=dev, generator=g)
+    table = torch.rand(1 << 20, device=dev, generator=g)
+    out = torch.empty(m, device=dev)
+
+    def run():
+        P.lhpc_probe_gather(C.c_void_p(idx.data_ptr()), C.c_void_p(table.data_ptr()), C.c_void_p(out.data_ptr()),
+                            C.c_int64(m), C.c_void_p(stream.cuda_stream))
+    for _ in range(3):
+        run()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(10):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) * 1e-3 / 10
+    ceil_gps = m / t
+    got = m / call_s
+    return {"unit": "G gathers/s", "achieved": got / 1e9, "ceiling": ceil_gps / 1e9, "frac": got / ceil_gps,
+            "note": "ceiling = the same number of 4-B random gathers from an L2-resident 4 MB table (probe kernel)"}
 
 
 def cpu_spmv_baseline(rp, col, val, x, nnz, seconds, threads=None):
