@@ -239,6 +239,35 @@ def main():
         dist.destroy_process_group()
 
 
+def copy_ceiling(L, torch, dev, stream, nbytes, achieved_gbps):
+    """Attainable read+write rate for the same bytes (report a
+    measured copy bandwidth beside the 8 TB/s peak): the best copy probe
+    measured (8 B/lane, non-temporal, grid-stride; tools/probe_copy.py),
+    moving nbytes/2 in and nbytes/2 out, timed live on the bench stream."""
+    import ctypes as C
+    P = C.CDLL(os.path.join(os.path.dirname(L.LIB_PATH), "liblhpc_probe.so"))
+    half = (nbytes // 2) // 16 * 16
+    src = torch.empty(half // 4, dtype=torch.float32, device=dev).uniform_()
+    dst = torch.empty_like(src)
+
+    def run():
+        P.lhpc_probe_copy_w(C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()), C.c_int64(half),
+                            C.c_int(16384), C.c_int(8), C.c_int(1), C.c_void_p(stream.cuda_stream))
+    for _ in range(3):
+        run()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(10):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    gbps = 2 * half / (e0.elapsed_time(e1) * 1e-3 / 10) / 1e9
+    del src, dst
+    return {"unit": "GB/s", "copy": gbps, "frac": achieved_gbps / gbps,
+            "note": "same bytes copied by the 8 B/lane non-temporal grid-stride probe"}
+
+
 def gather_ceiling(L, torch, dev, stream, nnz, call_s):
     """The binding limit of uniform-random SpMV on MI355X is the L2 request
     rate of 4-byte x gathers, not HBM bandwidth.  Measured
@@ -344,13 +373,14 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         per = float(tt.item())
     ach = 8.0 * cells / per / 1e9 / world
+    copy = copy_ceiling(L, torch, dev, stream, int(8 * cells // world), ach) if rank == 0 else None
     out = dict(metric=f"{wl} Gcell/s (8 B/cell algorithmic)", value=cells / per / 1e9, unit="Gcell/s",
                n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=per * 1e3,
                higher_is_better=True, scaling="strong" if wl == "c5" else "weak", vs_baseline=None, dtype="f32",
                data="synthetic U[-1,1)", config={"workload": workload},
                roofline={"bound": "hbm", "kernel": name, "achieved": ach, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,
-                         "traffic": load_traffic(wl) if world == 1 else None})
+                         "traffic": load_traffic(wl) if world == 1 else None, "copy": copy})
     if wl == "c5" and world == 1 and not args.no_cpu_baseline:
         from tests import _support as S
         lib = S.load_oracle()
