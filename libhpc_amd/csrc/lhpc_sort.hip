@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "lhpc_common.hpp"
 
@@ -33,7 +34,7 @@ namespace lhpc {
 namespace {
 
 constexpr int kSortThreads = 256;
-constexpr int kSortMaxBlocks = 2048;
+constexpr int kSortMaxResident = 2048;  // resident-block cap (and fallback if occupancy query fails)
 
 template <typename K>
 __device__ __forceinline__ uint32_t digit_of(K k, int shift, uint32_t mask) {
@@ -240,8 +241,8 @@ int64_t sort_grid_cap() {
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT>, kSortThreads, 0) !=
             hipSuccess ||
         cus <= 0 || per_cu <= 0)
-      return kSortMaxBlocks;
-    cap = std::min<int64_t>(kSortMaxBlocks, int64_t{cus} * per_cu);
+      return kSortMaxResident;
+    cap = std::min<int64_t>(kSortMaxResident, int64_t{cus} * per_cu);
   }
   return cap;
 }
@@ -251,7 +252,14 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
   if (n <= 1 || begin_bit >= end_bit) return LHPC_OK;
   constexpr int TILE = IPT * kSortThreads;
   const int64_t ntiles = (n + TILE - 1) / TILE;
-  int64_t nb = std::min<int64_t>(sort_grid_cap<K, HAS_V, IPT>(), ntiles);
+  // Grid: up to 8 waves of resident blocks, but at least ~3 tiles per block. More, shorter blocks even out
+  // the tail of the even-share split (500M keys: 768 blocks 8.94 ms, 6144 blocks 8.16 ms); below ~3 tiles
+  // per block the per-block digit-count rows outweigh the gain (100M keys: 8192 blocks 1.89 ms, 30000 2.19).
+  const int64_t res = sort_grid_cap<K, HAS_V, IPT>();
+  static const int64_t waves = std::getenv("LHPC_SORT_WAVES") ? std::max(1, std::atoi(std::getenv("LHPC_SORT_WAVES"))) : 8;
+  int64_t cap = std::min<int64_t>(waves * res, std::max<int64_t>(res, ntiles / 3));
+  if (const char *e = std::getenv("LHPC_SORT_BLOCKS")) cap = std::max<int64_t>(1, std::atoll(e));  // tuning knob
+  int64_t nb = std::min<int64_t>(cap, ntiles);
   const int64_t per = (ntiles + nb - 1) / nb;
   nb = (ntiles + per - 1) / per;
   DevBuf k2, v2, counts, dbase;

@@ -40,7 +40,7 @@ for n in [int(x) for x in os.environ.get("SORT_NS", "1000000 16000000 100000000 
     src = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device=dev)
     k = torch.empty_like(src)
     tmin, tavg = timed(lambda: k.copy_(src), lambda: L.radix_sort(k, stream=st))
-    ok = bool((k[1:].view(torch.int32).to(torch.int64) & 0xFFFFFFFF >= (k[:-1].to(torch.int64) & 0xFFFFFFFF)).all()) if n < 200_000_000 else None
+    ok = bool(((k[1:].to(torch.int64) & 0xFFFFFFFF) >= (k[:-1].to(torch.int64) & 0xFFFFFFFF)).all()) if n < 200_000_000 else None
     print(json.dumps(dict(k="sort_u32", n=n, ms=tmin * 1e3, ms_avg=tavg * 1e3, Gkeys=n / tmin / 1e9,
                           GBps_alg=32 * n / tmin / 1e9, sorted=ok)), flush=True)
     out = torch.empty_like(src)
