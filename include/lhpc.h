@@ -74,14 +74,16 @@ enum lhpc_plan_flags {
    * fp64 data always uses fp64 partials.  FAST_PARTIALS is the fp32 default,
    * kept as a flag for callers that name it.                               */
   LHPC_PLAN_FAST_PARTIALS = 1u << 7,
-  LHPC_PLAN_EXACT_PARTIALS = 1u << 8
+  LHPC_PLAN_EXACT_PARTIALS = 1u << 8,
+  LHPC_PLAN_FORCE_XTILE = 1u << 9
 };
 
 /* kernel families a plan can select (lhpc_spmv_plan_info.kernel)          */
 enum lhpc_spmv_kernel {
   LHPC_KERNEL_ROWGROUP = 0, /* L lanes per row, wave64 DPP reduction        */
   LHPC_KERNEL_ADAPTIVE = 1, /* nnz-balanced row blocks + long-row split     */
-  LHPC_KERNEL_XSLICE = 2    /* XCD-local column slices + partial reduce     */
+  LHPC_KERNEL_XSLICE = 2,   /* XCD-local column slices + partial reduce     */
+  LHPC_KERNEL_XTILE = 3     /* x tiles in LDS: tile gather + chunk reduce   */
 };
 
 typedef struct lhpc_spmv_plan lhpc_spmv_plan;
@@ -97,8 +99,9 @@ typedef struct lhpc_spmv_plan_info {
   int64_t device_bytes;/* HBM held by the plan                              */
   int device;          /* HIP device ordinal                                */
   int launches;        /* kernel launches per lhpc_spmv call                */
-  int slices;          /* XSLICE: column slices S (8 per XCD phase)         */
-  int64_t slice_width; /* XSLICE: columns per slice                         */
+  int slices;          /* XSLICE: column slices S (8 per XCD phase);
+                          XTILE: x tiles S                                  */
+  int64_t slice_width; /* XSLICE / XTILE: columns per slice / tile          */
 } lhpc_spmv_plan_info;
 
 /* ------------------------------------------------------------- runtime   */

@@ -29,6 +29,7 @@ __all__ = [
     "csr_partition_rows", "blur_x", "blur_y", "stencil7", "stencil7_planes",
     "gen_uniform_csr", "gen_powerlaw_csr", "gen_values", "padded_shape",
     "PLAN_VALIDATE", "PLAN_FORCE_ROWGROUP", "PLAN_FORCE_ADAPTIVE", "PLAN_FORCE_XSLICE", "PLAN_FAST_PARTIALS", "PLAN_EXACT_PARTIALS",
+    "PLAN_FORCE_XTILE", "KERNEL_XTILE",
     "KERNEL_ROWGROUP", "KERNEL_ADAPTIVE", "KERNEL_XSLICE",
 ]
 
@@ -42,7 +43,8 @@ PLAN_FORCE_ADAPTIVE = 1 << 5
 PLAN_FORCE_XSLICE = 1 << 6
 PLAN_FAST_PARTIALS = 1 << 7
 PLAN_EXACT_PARTIALS = 1 << 8
-KERNEL_ROWGROUP, KERNEL_ADAPTIVE, KERNEL_XSLICE = 0, 1, 2
+PLAN_FORCE_XTILE = 1 << 9
+KERNEL_ROWGROUP, KERNEL_ADAPTIVE, KERNEL_XSLICE, KERNEL_XTILE = 0, 1, 2, 3
 
 # every symbol include/lhpc.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = (

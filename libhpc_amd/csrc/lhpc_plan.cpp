@@ -124,4 +124,129 @@ int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, 
   return LHPC_OK;
 }
 
+int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
+                int64_t W, int M, int Rmax, int64_t piece_nnz, XtileHost &o) {
+  const int64_t nnz = rp_at(rp, bits, n_rows) - rp_at(rp, bits, 0);
+  if (W < 8 || M < 64 || M > 65536 || Rmax < 1) return LHPC_ERR_INVALID_ARG;
+  const int64_t S = n_cols > 0 ? (n_cols + W - 1) / W : 1;
+  if (S > 4096 || nnz + 8 * S >= INT32_MAX || n_rows >= INT32_MAX) return LHPC_ERR_UNSUPPORTED;
+  o.S = static_cast<int>(S);
+  o.W = W;
+  o.M = M;
+  o.Rmax = Rmax;
+  auto RP = [&](int64_t i) { return rp_at(rp, bits, i); };
+  // first row r in [lo, n_rows] with rp[r] >= e
+  auto lower_row = [&](int64_t lo, int64_t e) {
+    int64_t hi = n_rows;
+    while (lo < hi) {
+      const int64_t mid = lo + (hi - lo) / 2;
+      if (RP(mid) < e) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  };
+  // ---- chunks: (ce, cr) pairs; invariant: cr[c] = first row with rp >= ce[c]
+  //      (or a row whose predecessors starting at ce[c] are empty)
+  o.ce.assign(1, 0);
+  o.cr.assign(1, 0);
+  {
+    int64_t e = 0, r = 0;
+    while (!(e == nnz && r == n_rows)) {
+      int64_t en, rb;
+      if (e + M >= nnz) {
+        en = nnz;
+        rb = n_rows;
+      } else {
+        const int64_t target = e + M;
+        // last row q with rp[q] <= target
+        const int64_t q = lower_row(r, target + 1) - 1;
+        if (q >= r && RP(q) > e + M / 2) {
+          en = RP(q);  // cut at a row start
+        } else {
+          en = target;  // cut mid-row
+        }
+        rb = lower_row(r, en);
+      }
+      if (rb - r > Rmax) {
+        rb = r + Rmax;
+        en = RP(rb);
+      }
+      o.ce.push_back(static_cast<int32_t>(en));
+      o.cr.push_back(static_cast<int32_t>(rb));
+      e = en;
+      r = rb;
+    }
+  }
+  const int64_t C = static_cast<int64_t>(o.ce.size()) - 1;
+  o.n_chunks = C;
+  if (static_cast<double>(C + 1) * static_cast<double>(S) > 2.7e8) return LHPC_ERR_UNSUPPORTED;
+  o.cont.clear();
+  for (int64_t c = 0; c < C; ++c) {
+    const int64_t r0 = o.cr[c], r1 = o.cr[c + 1];
+    if (r1 > r0 && RP(r1) > o.ce[c + 1]) o.cont.push_back(static_cast<int32_t>(c));
+  }
+  // ---- per (chunk, tile) counts → segment offsets in (tile, chunk) order
+  o.segoff.assign(static_cast<size_t>((C + 1) * S), 0);
+  int32_t *cnt = o.segoff.data() + S;  // row c+1 temporarily holds count[c]
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t c = 0; c < C; ++c) {
+    int32_t *cc = cnt + c * S;
+    for (int64_t k = o.ce[c]; k < o.ce[c + 1]; ++k) ++cc[col[k] / W];
+  }
+  std::vector<int64_t> tbase(static_cast<size_t>(S) + 1, 0);
+  {
+    std::vector<int64_t> tot(static_cast<size_t>(S), 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t s = 0; s < S; ++s) {
+      int64_t t = 0;
+      for (int64_t c = 0; c < C; ++c) t += cnt[c * S + s];
+      tot[static_cast<size_t>(s)] = t;
+    }
+    for (int64_t s = 0; s < S; ++s) tbase[s + 1] = tbase[s] + (tot[s] + 7) / 8 * 8;
+  }
+  o.total = tbase[S];
+  // exclusive prefix down each tile column: segoff[c][s] = tbase[s] + Σ_{c'<c} count[c'][s]
+#pragma omp parallel for schedule(static)
+  for (int64_t s = 0; s < S; ++s) {
+    int64_t acc = tbase[s];
+    for (int64_t c = 0; c <= C; ++c) {
+      const int64_t n = c < C ? o.segoff[(c + 1) * S + s] : 0;
+      o.segoff[c * S + s] = static_cast<int32_t>(acc);
+      acc += n;
+    }
+  }
+  // ---- scatter (stable: CSR order inside each segment)
+  o.col16.reset(new uint16_t[o.total > 0 ? o.total : 1]());
+  o.perm.reset(new uint16_t[o.total > 0 ? o.total : 1]());
+#pragma omp parallel
+  {
+    std::vector<int32_t> cur(static_cast<size_t>(S));
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t c = 0; c < C; ++c) {
+      std::memcpy(cur.data(), o.segoff.data() + c * S, sizeof(int32_t) * static_cast<size_t>(S));
+      const int64_t e0 = o.ce[c];
+      for (int64_t k = e0; k < o.ce[c + 1]; ++k) {
+        const int64_t s = col[k] / W;
+        const int32_t g = cur[static_cast<size_t>(s)]++;
+        o.col16[g] = static_cast<uint16_t>(col[k] - s * W);
+        o.perm[g] = static_cast<uint16_t>(k - e0);
+      }
+    }
+  }
+  // ---- gather workgroups: each non-empty tile split into pieces of ≈ piece_nnz
+  o.pieces.clear();
+  const int64_t pn = std::max<int64_t>(8, (piece_nnz + 7) / 8 * 8);
+  for (int64_t s = 0; s < S; ++s) {
+    const int64_t len = tbase[s + 1] - tbase[s];
+    if (len == 0) continue;
+    const int64_t P = (len + pn - 1) / pn;
+    const int64_t step = ((len + P - 1) / P + 7) / 8 * 8;
+    for (int64_t g = tbase[s]; g < tbase[s + 1]; g += step) {
+      o.pieces.push_back(static_cast<int32_t>(g));
+      o.pieces.push_back(static_cast<int32_t>(std::min(g + step, tbase[s + 1])));
+      o.pieces.push_back(static_cast<int32_t>(s));
+    }
+  }
+  return LHPC_OK;
+}
+
 }  // namespace lhpc

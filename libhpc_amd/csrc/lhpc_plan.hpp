@@ -5,6 +5,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <memory>
+#include <vector>
 
 namespace lhpc {
 
@@ -34,6 +35,41 @@ struct XsliceHost {
 // one slice, or > 255 with allow16 = false (the jagged kernel is uint8-only).
 int build_xslice(const void *row_ptr, int rp_bits, const int32_t *col, const void *val,
                  size_t tsz, int64_t n_rows, int64_t n_cols, int S, bool jagged, XsliceHost &out);
+
+// XTILE: x tiled by column into S tiles of W columns, each tile small enough
+// to sit in one workgroup's LDS (fp32 40960 / fp64 20480 columns = 160 KB).
+// Two passes per SpMV:
+//   gather : a workgroup loads tile s of x into LDS and streams the tile's
+//            nonzeros (col16 = column − s·W), writing xg[g] = x[col] — every
+//            x read is an LDS gather, every HBM access is a coalesced stream;
+//   reduce : a workgroup owns a chunk of ≤ M consecutive CSR nonzeros, reads
+//            the chunk's S segments of xg (one per tile) and scatters them
+//            into LDS at perm[g] (the nonzero's position in the chunk), then
+//            multiplies by val (CSR order) and sums rows merge-path style.
+// The stream is ordered (tile, chunk, CSR position): segment (s, c) is
+// [segoff[c·S + s], segoff[(c+1)·S + s]).  Each tile's stream starts at a
+// multiple of 8 (padding entries are written by gather, never read).
+// Chunks cut the CSR order at row starts where one lies in the back half of
+// the M window, else mid-row; a chunk owns the rows that start in it (≤ Rmax)
+// and a row cut by a chunk end is finished by a fix-up over `cont`.
+struct XtileHost {
+  int S = 0;
+  int64_t W = 0;
+  int M = 0, Rmax = 0;
+  int64_t n_chunks = 0;
+  int64_t total = 0;                 // padded stream length
+  std::vector<int32_t> ce, cr;       // [C+1] chunk first nonzero / first owned row
+  std::vector<int32_t> segoff;       // [(C+1)·S]
+  std::vector<int32_t> pieces;       // gather workgroups: (g0, g1, s) triples
+  std::vector<int32_t> cont;         // chunks whose last owned row runs past the chunk
+  std::unique_ptr<uint16_t[]> col16, perm;  // [total]
+};
+
+// 0 on success; LHPC_ERR_UNSUPPORTED when the layout does not fit its
+// index types (nnz + padding ≥ 2^31, S > 4096, or an oversized segment table).
+// piece_nnz: target nonzeros per gather workgroup (multiple of 8 is used).
+int build_xtile(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_rows,
+                int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, XtileHost &out);
 
 // in-slice length of row r in slice s
 inline int xs_len(const XsliceHost &o, int s, int64_t r) {

@@ -588,6 +588,279 @@ __global__ __launch_bounds__(kBlock) void k_xslice_reduce(const P *__restrict__ 
     if (i0 + j < n_rows) y[i0 + j] = static_cast<T>(a[j]);
 }
 
+// ---------------------------------------------------------------- XTILE
+// (layout: lhpc_plan.hpp XtileHost)
+constexpr int kXtGatherBlock = 1024;  // gather: 16 waves per CU, one tile of x in LDS
+constexpr int kXtBlock = 256;         // reduce
+constexpr int kXtRun = 16;            // reduce: nonzeros per thread (merge-path run)
+constexpr int kXtM = kXtBlock * kXtRun;  // chunk capacity (nonzeros)
+constexpr int kXtRmax = 1024;            // rows owned per chunk
+template <typename T> struct XtTile;
+template <> struct XtTile<float> { static constexpr int W = 40960; };   // 160 KB
+template <> struct XtTile<double> { static constexpr int W = 20480; };  // 160 KB
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// gather: block b streams pieces[3b..3b+1] of tile pieces[3b+2]; 8 nonzeros
+// per thread and step (one 16-B col16 load, 8 LDS gathers, 8 contiguous xg
+// stores), U steps in flight.  Piece bounds are multiples of 8.
+template <typename T, int U>
+__global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
+    const int32_t *__restrict__ pieces, const uint16_t *__restrict__ col16,
+    const T *__restrict__ x, int64_t n_cols, T *__restrict__ xg) {
+  constexpr int W = XtTile<T>::W;
+  __shared__ T xt[W];
+  const int tid = threadIdx.x;
+  const int g0 = pieces[3 * blockIdx.x], g1 = pieces[3 * blockIdx.x + 1];
+  const int64_t c0 = static_cast<int64_t>(pieces[3 * blockIdx.x + 2]) * W;
+  const int wlen = static_cast<int>((n_cols - c0) < W ? (n_cols - c0) : W);
+  constexpr int PT = W / kXtGatherBlock;
+  T tv[PT];
+#pragma unroll
+  for (int i = 0; i < PT; ++i) {
+    const int j = i * kXtGatherBlock + tid;
+    tv[i] = j < wlen ? x[c0 + j] : T(0);
+  }
+#pragma unroll
+  for (int i = 0; i < PT; ++i) xt[i * kXtGatherBlock + tid] = tv[i];
+  __syncthreads();
+  const int q0 = g0 >> 3, q1 = g1 >> 3;  // 8-entry groups
+  const u32x4 *cv = reinterpret_cast<const u32x4 *>(col16);
+  for (int q = q0 + tid; q < q1; q += U * kXtGatherBlock) {
+    u32x4 w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int qq = q + u * kXtGatherBlock;
+      w[u] = qq < q1 ? __builtin_nontemporal_load(cv + qq) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int qq = q + u * kXtGatherBlock;
+      T o[8];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        o[2 * h] = xt[w[u][h] & 0xFFFFu];
+        o[2 * h + 1] = xt[w[u][h] >> 16];
+      }
+      if (qq < q1) {
+        if constexpr (sizeof(T) == 4) {
+          f32x4 *d = reinterpret_cast<f32x4 *>(xg + static_cast<int64_t>(qq) * 8);
+          d[0] = f32x4{o[0], o[1], o[2], o[3]};
+          d[1] = f32x4{o[4], o[5], o[6], o[7]};
+        } else {
+          typedef double f64x2 __attribute__((ext_vector_type(2)));
+          f64x2 *d = reinterpret_cast<f64x2 *>(xg + static_cast<int64_t>(qq) * 8);
+#pragma unroll
+          for (int h = 0; h < 4; ++h) d[h] = f64x2{o[2 * h], o[2 * h + 1]};
+        }
+      }
+    }
+  }
+}
+
+// reduce: one block per chunk c = (b % 8)·Cx + b / 8, so each XCD walks a
+// contiguous run of chunks and the xg lines two neighbouring chunks share
+// stay in its L2.  Dynamic LDS: xs[M] T, vs[M] T, hp[256] f64, tp[256] f64,
+// rpl[Rmax+1] i32, pre[S+1] i32, sst[S] i32, wsum[4] i32.
+template <typename T>
+__global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
+    const int32_t *__restrict__ ce, const int32_t *__restrict__ cr,
+    const int32_t *__restrict__ segoff, int S, int64_t C, int64_t Cx,
+    const T *__restrict__ xg, const uint16_t *__restrict__ perm, const T *__restrict__ val,
+    const int32_t *__restrict__ rp, T *__restrict__ y, double *__restrict__ carry) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  T *xs = reinterpret_cast<T *>(smem);
+  T *vs = xs + kXtM;
+  double *hp = reinterpret_cast<double *>(vs + kXtM);
+  double *tp = hp + kXtBlock;
+  int32_t *rpl = reinterpret_cast<int32_t *>(tp + kXtBlock);
+  int32_t *pre = rpl + (kXtRmax + 1);
+  int32_t *sst = pre + (S + 1);
+  int32_t *wsum = sst + S;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1), wv = tid / kWave;
+  const int64_t c = static_cast<int64_t>(blockIdx.x % 8) * Cx + blockIdx.x / 8;
+  if (c >= C) return;  // block-uniform
+  const int e0 = ce[c], m = ce[c + 1] - e0;
+  const int r0 = cr[c], R = cr[c + 1] - r0;
+
+  // val (CSR order, coalesced) first: independent of everything below
+  T v[kXtRun];
+#pragma unroll
+  for (int i = 0; i < kXtRun; ++i) {
+    const int k = i * kXtBlock + tid;
+    v[i] = k < m ? ld_stream(val + e0 + k) : T(0);
+  }
+  for (int j = tid; j <= R; j += kXtBlock) rpl[j] = rp[r0 + j] - e0;
+  // segment starts/lengths; thread t owns tiles [t·G, t·G+G)
+  const int G = (S + kXtBlock - 1) / kXtBlock;
+  int lsum = 0;
+  for (int i = 0; i < G; ++i) {
+    const int s = tid * G + i;
+    if (s < S) {
+      const int a = segoff[c * S + s];
+      sst[s] = a;
+      lsum += segoff[(c + 1) * S + s] - a;
+    }
+  }
+  // block exclusive scan of lsum
+  int inc = lsum;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int t = __shfl_up(inc, d, kWave);
+    if (lane >= d) inc += t;
+  }
+  if (lane == kWave - 1) wsum[wv] = inc;
+#pragma unroll
+  for (int i = 0; i < kXtRun; ++i) vs[i * kXtBlock + tid] = v[i];
+  __syncthreads();
+  int wbase = 0;
+  for (int w = 0; w < wv; ++w) wbase += wsum[w];
+  {
+    int run = wbase + inc - lsum;
+    for (int i = 0; i < G; ++i) {
+      const int s = tid * G + i;
+      if (s < S) {
+        pre[s] = run;
+        run += segoff[(c + 1) * S + s] - sst[s];
+      }
+    }
+    if (tid == kXtBlock - 1) pre[S] = run;
+  }
+  __syncthreads();
+
+  // phase A: flat position f -> (segment, offset); xs[perm] = xg
+  {
+    int src[kXtRun];
+    int lo = 0;
+#pragma unroll
+    for (int u = 0; u < kXtRun; ++u) {
+      const int f = u * kXtBlock + tid;
+      src[u] = -1;
+      if (f < m) {
+        int hi = S;  // largest s with pre[s] <= f, in [lo, S)
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (pre[mid] <= f) lo = mid; else hi = mid;
+        }
+        src[u] = sst[lo] + (f - pre[lo]);
+      }
+    }
+    T xv[kXtRun];
+    uint16_t pv[kXtRun];
+#pragma unroll
+    for (int u = 0; u < kXtRun; ++u) {
+      const int sidx = src[u] >= 0 ? src[u] : 0;
+      xv[u] = xg[sidx];
+      pv[u] = perm[sidx];
+    }
+#pragma unroll
+    for (int u = 0; u < kXtRun; ++u)
+      if (src[u] >= 0) xs[pv[u]] = xv[u];
+  }
+  __syncthreads();
+
+  // empty owned rows
+  for (int j = tid; j < R; j += kXtBlock)
+    if (rpl[j] == rpl[j + 1]) y[r0 + j] = T(0);
+
+  // phase B: thread t sums its run [16t, 16t+16) merge-path style
+  const int i0 = tid * kXtRun;
+  const int i1 = (i0 + kXtRun) < m ? (i0 + kXtRun) : m;
+  bool head = false, head_ended = false, tail = false;
+  int jr = -1;
+  double acc = 0.0;
+  if (i0 < i1) {
+    // jr = last row with rpl[jr] <= i0 (−1: the chunk's head row)
+    int lo = -1, hi = R;  // rpl[R] >= m > i0
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (rpl[mid] <= i0) lo = mid; else hi = mid;
+    }
+    jr = lo;
+    bool started = jr >= 0 && rpl[jr] == i0;
+    bool first = true;
+    int nextb = rpl[jr + 1];
+#pragma unroll
+    for (int j = 0; j < kXtRun; ++j) {
+      const int i = i0 + j;
+      if (i < i1) {
+        if (i == nextb) {  // row jr ends before i
+          if (first && !started) {
+            hp[tid] = acc;
+            head = true;
+            head_ended = true;
+          } else {
+            y[r0 + jr] = static_cast<T>(acc);
+          }
+          first = false;
+          ++jr;
+          while (rpl[jr + 1] <= i) ++jr;  // skip empty rows
+          started = true;
+          nextb = rpl[jr + 1];
+          acc = 0.0;
+        }
+        acc += static_cast<double>(vs[i]) * static_cast<double>(xs[i]);
+      }
+    }
+    const bool ended = nextb == i1;
+    if (first && !started) {
+      hp[tid] = acc;
+      head = true;
+      head_ended = ended;
+    } else if (ended) {
+      y[r0 + jr] = static_cast<T>(acc);
+    } else {
+      tp[tid] = acc;
+      tail = true;
+    }
+  }
+  __syncthreads();
+  // combine pieces of rows that cross thread runs (fixed order: run order)
+  const int tlast = m > 0 ? (m - 1) / kXtRun : -1;
+  if (tid == 0 && !(m > 0 && rpl[0] > 0)) carry[2 * c] = 0.0;  // no head piece
+  if (head && (head_ended || tid == tlast)) {
+    // the row of this thread's head piece: jh (−1 = the chunk's head row)
+    int jh;
+    {
+      int lo = -1, hi = R;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (rpl[mid] <= i0) lo = mid; else hi = mid;
+      }
+      jh = lo;
+    }
+    const int ts = jh >= 0 ? rpl[jh] / kXtRun : 0;
+    double s = jh >= 0 ? tp[ts] : hp[0];
+    for (int u = ts + 1; u <= tid; ++u) s += hp[u];
+    if (jh < 0) {
+      carry[2 * c] = s;  // this chunk's piece of the previous chunk's row
+    } else if (head_ended) {
+      y[r0 + jh] = static_cast<T>(s);
+    } else {
+      carry[2 * c + 1] = s;  // row continues into the next chunk
+    }
+  }
+  if (tail && tid == tlast) carry[2 * c + 1] = tp[tid];  // own tail row continues past the chunk
+}
+
+// rows cut by a chunk end: y[row] = tail piece + head pieces, chunk order
+template <typename T>
+__global__ __launch_bounds__(kXtBlock) void k_xtile_fixup(
+    const int32_t *__restrict__ cont, int64_t n_cont, const int32_t *__restrict__ cr, int64_t C,
+    const double *__restrict__ carry, T *__restrict__ y) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kXtBlock + threadIdx.x;
+  if (i >= n_cont) return;
+  const int64_t c = cont[i];
+  double s = carry[2 * c + 1];
+  for (int64_t d = c + 1; d < C; ++d) {
+    s += carry[2 * d];
+    if (cr[d + 1] > cr[d]) break;
+  }
+  y[cr[c + 1] - 1] = static_cast<T>(s);
+}
+
 // ------------------------------------------------------------- host side
 // Distinct 128-B x lines touched per nonzero, over up to 32 evenly spaced
 // chunks of 8192 consecutive rows (1.0 = no reuse within a chunk).
@@ -646,6 +919,14 @@ struct lhpc_spmv_plan {
   void *d_lens = nullptr;
   int64_t *d_cbase = nullptr;
   void *d_partial = nullptr;
+  // XTILE
+  int64_t xt_C = 0, xt_pieces = 0, xt_cont = 0, xt_total = 0;
+  size_t xt_lds = 0;
+  int xt_u = 4;
+  int32_t *d_ce = nullptr, *d_cr = nullptr, *d_segoff = nullptr, *d_pieces = nullptr, *d_cont = nullptr;
+  uint16_t *d_col16 = nullptr, *d_perm = nullptr;
+  void *d_xg = nullptr;
+  double *d_carry = nullptr;
 };
 
 namespace {
@@ -828,8 +1109,43 @@ int launch_xslice(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s
   return check_launch(s);
 }
 
+size_t xtile_lds_bytes(size_t tsz, int S) {
+  return 2 * static_cast<size_t>(kXtM) * tsz + 2 * kXtBlock * sizeof(double) +
+         sizeof(int32_t) * (static_cast<size_t>(kXtRmax) + 1 + 2 * static_cast<size_t>(S) + 1 + 4);
+}
+
+template <typename T>
+int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  if (p->n_rows == 0) return LHPC_OK;
+  T *xg = static_cast<T *>(p->d_xg);
+  if (p->xt_pieces > 0) {
+    const dim3 g(static_cast<unsigned>(p->xt_pieces)), b(kXtGatherBlock);
+    if (p->xt_u == 2)
+      hipLaunchKernelGGL((k_xtile_gather<T, 2>), g, b, 0, s, p->d_pieces, p->d_col16,
+                         static_cast<const T *>(x), p->n_cols, xg);
+    else
+      hipLaunchKernelGGL((k_xtile_gather<T, 4>), g, b, 0, s, p->d_pieces, p->d_col16,
+                         static_cast<const T *>(x), p->n_cols, xg);
+    LHPC_TRY(check_launch(s));
+  }
+  const int64_t Cx = (p->xt_C + 7) / 8;
+  hipLaunchKernelGGL((k_xtile_reduce<T>), dim3(static_cast<unsigned>(8 * Cx)), dim3(kXtBlock),
+                     p->xt_lds, s, p->d_ce, p->d_cr, p->d_segoff, p->S, p->xt_C, Cx, xg, p->d_perm,
+                     static_cast<const T *>(p->d_val), static_cast<const int32_t *>(p->d_row_ptr),
+                     static_cast<T *>(y), p->d_carry);
+  LHPC_TRY(check_launch(s));
+  if (p->xt_cont > 0) {
+    hipLaunchKernelGGL((k_xtile_fixup<T>), dim3(static_cast<unsigned>((p->xt_cont + kXtBlock - 1) / kXtBlock)),
+                       dim3(kXtBlock), 0, s, p->d_cont, p->xt_cont, p->d_cr, p->xt_C, p->d_carry,
+                       static_cast<T *>(y));
+    LHPC_TRY(check_launch(s));
+  }
+  return LHPC_OK;
+}
+
 template <typename T>
 int launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  if (p->kernel == LHPC_KERNEL_XTILE) return launch_xtile<T>(p, x, y, s);
   if (p->kernel == LHPC_KERNEL_XSLICE) return launch_xslice<T>(p, x, y, s);
   if (p->kernel == LHPC_KERNEL_ADAPTIVE)
     return p->rp64 ? launch_adaptive<T, int64_t>(p, x, y, s)
@@ -871,6 +1187,56 @@ std::vector<int64_t> build_blocks(RowPtrView rp, int64_t n_rows, int64_t &n_long
   return b;
 }
 
+}  // namespace
+
+namespace {
+// XTILE plan: re-encode A (lhpc_plan.cpp build_xtile) and copy it to HBM.
+int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val,
+                     size_t tsz) {
+  const int64_t W = tsz == 4 ? XtTile<float>::W : XtTile<double>::W;
+  int cus = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, p->device) == hipSuccess) cus = prop.multiProcessorCount;
+  // ≈ 2 gather workgroups per CU (one resident per CU: 160 KB of LDS each)
+  int64_t piece = std::max<int64_t>(65536, p->nnz / (2 * static_cast<int64_t>(cus)) + 1);
+  if (const char *env = std::getenv("LHPC_XTILE_PIECE")) piece = std::max<int64_t>(8, std::atoll(env));
+  XtileHost xt;
+  const int bst = build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, kXtM, kXtRmax, piece, xt);
+  if (bst != LHPC_OK) return bst;
+  p->kernel = LHPC_KERNEL_XTILE;
+  p->rp64 = 0;
+  p->S = xt.S;
+  p->xs_width = W;
+  p->xt_C = xt.n_chunks;
+  p->xt_pieces = static_cast<int64_t>(xt.pieces.size() / 3);
+  p->xt_cont = static_cast<int64_t>(xt.cont.size());
+  p->xt_total = xt.total;
+  p->xt_lds = xtile_lds_bytes(tsz, xt.S);
+  if (const char *env = std::getenv("LHPC_XTILE_U")) p->xt_u = std::atoi(env) == 2 ? 2 : 4;
+  const void *kfn = tsz == 4 ? reinterpret_cast<const void *>(k_xtile_reduce<float>)
+                             : reinterpret_cast<const void *>(k_xtile_reduce<double>);
+  LHPC_HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
+  const int64_t n_rows = p->n_rows, nnz = p->nnz, C = xt.n_chunks;
+  auto up = [&](void **d, const void *h, size_t n) -> int {
+    LHPC_TRY(dmalloc(d, n, p->bytes));
+    if (n && h) LHPC_HIP_TRY(hipMemcpy(*d, h, n, hipMemcpyHostToDevice));
+    return LHPC_OK;
+  };
+  std::vector<int32_t> rp32(static_cast<size_t>(n_rows + 1));
+  for (int64_t i = 0; i <= n_rows; ++i) rp32[static_cast<size_t>(i)] = static_cast<int32_t>(rp[i]);
+  LHPC_TRY(up(&p->d_row_ptr, rp32.data(), rp32.size() * 4));
+  LHPC_TRY(up(&p->d_val, val, static_cast<size_t>(nnz) * tsz));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_ce), xt.ce.data(), xt.ce.size() * 4));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cr), xt.cr.data(), xt.cr.size() * 4));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_segoff), xt.segoff.data(), xt.segoff.size() * 4));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_pieces), xt.pieces.data(), xt.pieces.size() * 4));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cont), xt.cont.data(), xt.cont.size() * 4));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_col16), xt.col16.get(), static_cast<size_t>(xt.total) * 2));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), xt.perm.get(), static_cast<size_t>(xt.total) * 2));
+  LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total) * tsz));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_carry), nullptr, static_cast<size_t>(2 * C + 2) * 8));
+  return LHPC_OK;
+}
 }  // namespace
 
 extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
@@ -950,10 +1316,28 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
   // uniform columns, ≈0.03 for a 2-D Laplacian); ≤ 0.25 counts as local.
   double locality_thr = 0.25;
   if (const char *env = std::getenv("LHPC_SPMV_LOCALITY")) locality_thr = std::atof(env);
-  const bool auto_ok = !(flags & (LHPC_PLAN_FORCE_ROWGROUP | LHPC_PLAN_FORCE_ADAPTIVE));
-  const bool want_xslice =
-      (flags & LHPC_PLAN_FORCE_XSLICE) ||
-      (auto_ok && x_bytes > 8.0e6 && gather_lines_per_nnz(rp, col_idx, n_rows, tsz) > locality_thr);
+  const bool auto_ok = !(flags & (LHPC_PLAN_FORCE_ROWGROUP | LHPC_PLAN_FORCE_ADAPTIVE |
+                                   LHPC_PLAN_FORCE_XSLICE | LHPC_PLAN_FORCE_XTILE));
+  const bool nolocal =
+      auto_ok && x_bytes > 8.0e6 && gather_lines_per_nnz(rp, col_idx, n_rows, tsz) > locality_thr;
+  // XTILE (x tiles in LDS) is the default for gathers without locality;
+  // LHPC_SPMV_XTILE=0 selects XSLICE instead.
+  bool xtile_env = true;
+  if (const char *env = std::getenv("LHPC_SPMV_XTILE")) xtile_env = std::atoi(env) != 0;
+  const bool want_xtile = (flags & LHPC_PLAN_FORCE_XTILE) || (nolocal && xtile_env);
+  if (want_xtile && n_rows > 0) {
+    int st = build_xtile_plan(p, rp, col_idx, val, tsz);
+    if (st == LHPC_OK) {
+      *out = p;
+      return LHPC_OK;
+    }
+    if (st != LHPC_ERR_UNSUPPORTED) {
+      lhpc_spmv_plan_destroy(p);
+      return st;
+    }
+    // layout does not fit its index types: XSLICE / CSR kernels below
+  }
+  const bool want_xslice = (flags & LHPC_PLAN_FORCE_XSLICE) || nolocal;
   if (want_xslice && nnz > 0) {
     int P = static_cast<int>(std::ceil(x_bytes / (8.0 * slice_mb * 1.0e6)));
     P = std::max(1, std::min(P, 32));
@@ -1192,6 +1576,11 @@ extern "C" int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *p, lhpc_spmv_plan_i
   info->device_bytes = p->bytes;
   info->device = p->device;
   info->launches = p->kernel == LHPC_KERNEL_XSLICE && !p->xs_fused && !p->xs_persist ? 2 : 1;
+  if (p->kernel == LHPC_KERNEL_XTILE) {
+    info->launches = (p->xt_pieces > 0 ? 1 : 0) + 1 + (p->xt_cont > 0 ? 1 : 0);
+    info->n_blocks = p->xt_C;
+    info->n_long_rows = p->xt_cont;
+  }
   info->slices = p->S;
   info->slice_width = p->xs_width;
   return LHPC_OK;
@@ -1203,7 +1592,11 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
   for (void *q : {p->d_row_ptr, static_cast<void *>(p->d_col), p->d_val,
                   static_cast<void *>(p->d_blocks), p->d_xstage, p->d_ystage,
                   p->d_lens, static_cast<void *>(p->d_cbase), p->d_partial,
-                  static_cast<void *>(p->d_arrive), static_cast<void *>(p->d_dpart)})
+                  static_cast<void *>(p->d_arrive), static_cast<void *>(p->d_dpart),
+                  static_cast<void *>(p->d_ce), static_cast<void *>(p->d_cr), static_cast<void *>(p->d_segoff),
+                  static_cast<void *>(p->d_pieces), static_cast<void *>(p->d_cont),
+                  static_cast<void *>(p->d_col16), static_cast<void *>(p->d_perm), p->d_xg,
+                  static_cast<void *>(p->d_carry)})
     if (q) (void)hipFree(q);
   delete p;
   return LHPC_OK;

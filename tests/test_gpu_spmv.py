@@ -24,6 +24,7 @@ FAMILIES = {
     "xslice": 1 << 6,
     "xslice_fast": (1 << 6) | (1 << 7),  # fp32 partials (the fp32 default), separate reduce kernel
     "xslice_exact": (1 << 6) | (1 << 8),  # fp64 partials
+    "xtile": 1 << 9,  # x tiles in LDS: tile gather + merge-path chunk reduce
 }
 GOLDEN_SPMV = sorted(glob.glob(os.path.join(S.GOLDEN, "spmv_*.npz")))
 
@@ -49,6 +50,8 @@ def test_golden(lhpc, gpu, path, family):
     y, info = _run(lhpc, gpu, rp, col, val, x, n_cols, FAMILIES[family])
     if family.startswith("xslice") and rp[-1] > 0:
         assert info["kernel"] == lhpc.KERNEL_XSLICE  # long rows: uint16 lens + wave-reduced rows
+    if family == "xtile":
+        assert info["kernel"] == lhpc.KERNEL_XTILE
     exact = g["y_exact"]
     if "dyadic" in path:
         assert np.array_equal(y, exact.astype(val.dtype)), "dyadic SpMV must be bit-exact"
@@ -57,7 +60,7 @@ def test_golden(lhpc, gpu, path, family):
         S.assert_spmv_close(y, exact, asum)
 
 
-@pytest.mark.parametrize("family", ["auto", "xslice"])
+@pytest.mark.parametrize("family", ["auto", "xslice", "xtile"])
 def test_host_buffers_match_device(lhpc, gpu, family):
     g = S.load_golden("spmv_dyadic_f32_n1000.npz")
     args = (g["row_ptr"], g["col_idx"], g["val"], g["x"], int(g["n_cols"]), FAMILIES[family])
@@ -130,8 +133,7 @@ def test_full_size_c2_c3(lhpc, gpu, dtype):
         rp, col, val = lhpc.gen_uniform_csr(n, n, 15, dtype=dt, dist=dist)
         x = lhpc.gen_values(dt, dist, n, lhpc.SEED_X)
         with lhpc.SpMVPlan(rp, col, val, n) as plan:
-            if dt == lhpc.F32:
-                assert plan.info()["kernel"] == lhpc.KERNEL_XSLICE
+            assert plan.info()["kernel"] == lhpc.KERNEL_XTILE
             xd = torch.from_numpy(x).to(gpu)
             y1 = plan(xd).clone()
             y2 = plan(xd).clone()
@@ -212,3 +214,91 @@ def test_golden_xslice_persistent(lhpc, gpu, path, monkeypatch):
                    FAMILIES["xslice"])
     assert info["launches"] == 1
     assert np.array_equal(y, g["y_exact"].astype(g["val"].dtype))
+
+
+# ------------------------------------------------------------------ XTILE
+def _csr_from_lengths(lengths, n_cols, seed, dyadic):
+    """CSR with the given row lengths, distinct sorted uniform columns per row."""
+    rng = np.random.default_rng(seed)
+    lengths = np.asarray(lengths, dtype=np.int64)
+    rp = np.zeros(len(lengths) + 1, dtype=np.int32)
+    np.cumsum(lengths, out=rp[1:])
+    cols = []
+    for ln in lengths:
+        if ln:
+            cols.append(np.sort(rng.choice(n_cols, size=int(ln), replace=False)).astype(np.int32))
+    col = np.concatenate(cols) if cols else np.zeros(0, dtype=np.int32)
+    if dyadic:
+        val = (rng.integers(-8, 9, size=col.size) / 8.0)
+    else:
+        val = rng.uniform(-1.0, 1.0, size=col.size)
+    return rp, col, val
+
+
+def _check_xtile(lhpc, gpu, lengths, n_cols, dtype, seed, dyadic=True, expect_cont=None):
+    rp, col, val = _csr_from_lengths(lengths, n_cols, seed, dyadic)
+    val = val.astype(dtype)
+    rng = np.random.default_rng(seed + 1)
+    if dyadic:
+        x = (rng.integers(-8, 9, size=n_cols) / 8.0).astype(dtype)
+    else:
+        x = rng.uniform(-1.0, 1.0, size=n_cols).astype(dtype)
+    y, info = _run(lhpc, gpu, rp, col, val, x, n_cols, FAMILIES["xtile"])
+    assert info["kernel"] == lhpc.KERNEL_XTILE
+    if expect_cont is not None:
+        assert (info["n_long_rows"] > 0) == expect_cont
+    y64, yr, asum = S.spmv_oracle(rp, col, val, x)
+    if dyadic:
+        assert np.array_equal(y, yr), "dyadic XTILE SpMV must be bit-exact"
+    else:
+        S.assert_spmv_close(y, y64, asum)
+    return info
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_xtile_long_rows_across_chunks(lhpc, gpu, dtype):
+    """Rows longer than a chunk (4096 nonzeros) are cut by chunk ends and
+    finished by the fix-up: a 30k-row, rows of 5000/4096/4095/9000 between
+    short rows, a long first and a long last row."""
+    lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 3000 + [0, 0] + [30000]
+    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA100, expect_cont=True)
+    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA101, dyadic=False)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_xtile_empty_row_runs(lhpc, gpu, dtype):
+    """More than Rmax (1024) consecutive empty rows, leading and trailing
+    empty rows, and an all-empty tail after the last nonzero."""
+    lengths = [0] * 3000 + [7] * 10 + [0] * 2500 + [1] + [0] * 1500 + [4096] + [0] * 2049
+    _check_xtile(lhpc, gpu, lengths, 150_000, dtype, 0xA200)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_xtile_wide_many_tiles(lhpc, gpu, dtype):
+    """n_cols ≫ n_rows: hundreds of tiles, a ragged last tile, 1-nonzero rows."""
+    rng = np.random.default_rng(0xA300)
+    lengths = rng.integers(0, 40, size=5000)
+    _check_xtile(lhpc, gpu, lengths, 9_000_001, dtype, 0xA301)
+    _check_xtile(lhpc, gpu, np.ones(70_000, dtype=np.int64), 3_000_017, dtype, 0xA302)
+
+
+def test_xtile_small_gather_pieces(lhpc, gpu, monkeypatch):
+    """Several gather workgroups per tile (piece bounds inside a tile) give the same bits."""
+    monkeypatch.setenv("LHPC_XTILE_PIECE", "1000")
+    rng = np.random.default_rng(0xA400)
+    lengths = rng.integers(0, 60, size=20_000)
+    _check_xtile(lhpc, gpu, lengths, 100_000, np.float32, 0xA401)
+    monkeypatch.setenv("LHPC_XTILE_U", "2")
+    _check_xtile(lhpc, gpu, lengths, 100_000, np.float64, 0xA402)
+
+
+def test_xtile_is_auto_choice_without_locality(lhpc, gpu):
+    """x > 8 MB with uniform random columns selects XTILE; LHPC_SPMV_XTILE=0 gives XSLICE."""
+    n = 3_000_000
+    rp, col, val = lhpc.gen_uniform_csr(n, n, 4, dtype=lhpc.F32, dist=1, seed=0xA500)
+    x = lhpc.gen_values(lhpc.F32, 1, n, 0xA501)
+    y, info = _run(lhpc, gpu, rp, col, val, x, n, 0)
+    assert info["kernel"] == lhpc.KERNEL_XTILE
+    assert info["launches"] in (2, 3)
+    _, yr, _ = S.spmv_oracle(rp, col, val, x)
+    assert np.array_equal(y, yr)
