@@ -193,9 +193,10 @@ def main():
         local_alg = local_nnz * (tsz + 4) + (local_rows + len(plans)) * 4 + (n + local_rows) * tsz
         achieved = local_alg / call_s / 1e9
         kname = {L.KERNEL_XSLICE: "xslice", L.KERNEL_ROWGROUP: "rowgroup",
-                 L.KERNEL_ADAPTIVE: "adaptive"}[info["kernel"]]
+                 L.KERNEL_ADAPTIVE: "adaptive", L.KERNEL_XTILE: "xtile"}[info["kernel"]]
         kernels = {"xslice": "k_spmv_xslice+k_xslice_reduce", "rowgroup": "k_spmv_rowgroup",
-                   "adaptive": "k_spmv_adaptive"}[kname]
+                   "adaptive": "k_spmv_adaptive",
+                   "xtile": "k_xtile_gather+k_xtile_reduce" + ("+k_xtile_fixup" if info["n_long_rows"] else "")}[kname]
         traffic = load_traffic(f"{wl}_{kname}") if world == 1 else None
         result.update(
             metric=METRIC if wl != "c1" else "CSR SpMV GFLOP/s, n=100k nnz=1M fp64 (BASELINE configs[0])",
@@ -218,6 +219,14 @@ def main():
         )
         if kname == "xslice" and rank == 0:
             result["roofline"]["gather"] = gather_ceiling(L, torch, dev, stream, local_nnz, call_s)
+        if kname == "xtile":
+            # bytes the XTILE layout streams per call: gather reads
+            # col16 (2 B) + x tiles, writes xg (T); reduce reads xg (T) + perm (2 B) +
+            # val (T) + row_ptr, writes y.  The x-gathers themselves are LDS reads.
+            stream_b = local_nnz * (2 + 2 * tsz + 2 + tsz) + (local_rows + len(plans)) * 4 + (n + local_rows) * tsz
+            result["roofline"]["layout"] = {"stream_bytes_per_call": stream_b,
+                                            "achieved": stream_b / call_s / 1e9,
+                                            "frac": stream_b / call_s / 1e9 / HBM_PEAK_GBPS}
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_spmv_baseline(rp, col, val, x, nnz, args.cpu_seconds,
                                                        threads=1 if wl == "c1" else None)

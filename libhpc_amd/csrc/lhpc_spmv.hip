@@ -594,7 +594,7 @@ constexpr int kXtGatherBlock = 1024;  // gather: 16 waves per CU, one tile of x 
 constexpr int kXtBlock = 256;         // reduce
 constexpr int kXtRun = 16;            // reduce: nonzeros per thread (merge-path run)
 constexpr int kXtM = kXtBlock * kXtRun;  // chunk capacity (nonzeros)
-constexpr int kXtRmax = 1024;            // rows owned per chunk
+constexpr int kXtRmax = 512;             // rows owned per chunk
 template <typename T> struct XtTile;
 template <> struct XtTile<float> { static constexpr int W = 40960; };   // 160 KB
 template <> struct XtTile<double> { static constexpr int W = 20480; };  // 160 KB
@@ -660,189 +660,217 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
 
 // reduce: one block per chunk c = (b % 8)·Cx + b / 8, so each XCD walks a
 // contiguous run of chunks and the xg lines two neighbouring chunks share
-// stay in its L2.  Dynamic LDS: xs[M] T, vs[M] T, hp[256] f64, tp[256] f64,
-// rpl[Rmax+1] i32, pre[S+1] i32, sst[S] i32, wsum[4] i32.
-template <typename T>
+// stay in its L2.  PMC (profiles/r01/xtile_*): the stream equals the
+// algorithmic bytes and the kernel is instruction-issue bound, so both phases
+// are branch-free in the common case:
+//   phase A  wave w owns flat positions [1024w, 1024w+1024) of the chunk's
+//            segment concatenation, in batches of 64.  A wave-uniform cursor
+//            s0 (segment of the batch start) advances batch by batch; a lane
+//            finds its segment as s0 + #(segment starts in (f0, f]) from ONE
+//            LDS read of the next 64 starts, a ballot and ~4 readlanes; the
+//            source index is base[s] + f (base = segment start − prefix).
+//   phase B  thread t owns the run [16t, 16t+16); a bitmap of row starts
+//            (ds_or) drives a segmented scan (reset at a start, add), whose
+//            running value rounded to T is written back in place: a row that
+//            ends inside a run leaves its value at its last position.  Pieces
+//            of rows crossing runs (hp: before the run's first start, tp:
+//            after its last) are combined in run order, and the owned rows'
+//            y is stored coalesced from their last positions.
+// Every load that does not depend on another is issued together: one 16-B
+// chunk descriptor {e0, e1, r0, r1}, then val (the thread's own run as 16-B
+// vectors), row_ptr and the segment table, then xg/perm — three round trips.
+// xs lives in LDS at pidx(i) = i + i/16 (thread t's run at [17t, 17t+16):
+// conflict-free).  Dynamic LDS: xs[M+M/16] T, hp[256] f64, tp[256] f64,
+// bm[M/32] u32, rpl[Rmax+1] i32, pre[S+1] i32, base[S] i32, wsum[4] i32.
+__device__ __forceinline__ int xt_pidx(int i) { return i + (i >> 4); }
+
+template <typename T, int G>
 __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
-    const int32_t *__restrict__ ce, const int32_t *__restrict__ cr,
-    const int32_t *__restrict__ segoff, int S, int64_t C, int64_t Cx,
-    const T *__restrict__ xg, const uint16_t *__restrict__ perm, const T *__restrict__ val,
-    const int32_t *__restrict__ rp, T *__restrict__ y, double *__restrict__ carry) {
+    const int32_t *__restrict__ cdesc, const int32_t *__restrict__ segoff, int S, int64_t C,
+    int64_t Cx, const T *__restrict__ xg, const uint16_t *__restrict__ perm,
+    const T *__restrict__ val, const int32_t *__restrict__ rp, T *__restrict__ y,
+    double *__restrict__ carry) {
+  constexpr int MP = kXtM + kXtM / 16;
+  constexpr int RPT = (kXtRmax + 1 + kXtBlock - 1) / kXtBlock;  // row_ptr loads per thread
+  constexpr int PERW = kXtM / (kXtBlock / kWave);                // flat positions per wave
+  constexpr int NB = PERW / kWave;                               // batches per wave
   extern __shared__ __align__(16) unsigned char smem[];
   T *xs = reinterpret_cast<T *>(smem);
-  T *vs = xs + kXtM;
-  double *hp = reinterpret_cast<double *>(vs + kXtM);
+  double *hp = reinterpret_cast<double *>(xs + MP);
   double *tp = hp + kXtBlock;
-  int32_t *rpl = reinterpret_cast<int32_t *>(tp + kXtBlock);
+  uint32_t *bm = reinterpret_cast<uint32_t *>(tp + kXtBlock);
+  int32_t *rpl = reinterpret_cast<int32_t *>(bm + kXtM / 32);
   int32_t *pre = rpl + (kXtRmax + 1);
-  int32_t *sst = pre + (S + 1);
-  int32_t *wsum = sst + S;
+  int32_t *base = pre + (S + 1);
+  int32_t *wsum = base + S;
 
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1), wv = tid / kWave;
   const int64_t c = static_cast<int64_t>(blockIdx.x % 8) * Cx + blockIdx.x / 8;
   if (c >= C) return;  // block-uniform
-  const int e0 = ce[c], m = ce[c + 1] - e0;
-  const int r0 = cr[c], R = cr[c + 1] - r0;
+  const u32x4 d = *reinterpret_cast<const u32x4 *>(cdesc + 4 * c);
+  const int e0 = static_cast<int>(d[0]), m = static_cast<int>(d[1]) - e0;
+  const int r0 = static_cast<int>(d[2]), R = static_cast<int>(d[3]) - r0;
+  const int i0 = tid * kXtRun;
 
-  // val (CSR order, coalesced) first: independent of everything below
-  T v[kXtRun];
+  // ---- round trip 2: val run, row_ptr, segment table — all issued together
+  typedef T tvec __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
+  constexpr int VW = 16 / sizeof(T), NV = kXtRun / VW;
+  tvec vv[NV];
+  {
+    // the val allocation is padded by one run, so a run may read past nnz
+    const tvec *vp = reinterpret_cast<const tvec *>(val + e0 + (i0 < m ? i0 : 0));
 #pragma unroll
-  for (int i = 0; i < kXtRun; ++i) {
-    const int k = i * kXtBlock + tid;
-    v[i] = k < m ? ld_stream(val + e0 + k) : T(0);
+    for (int q = 0; q < NV; ++q) vv[q] = __builtin_nontemporal_load(vp + q);
   }
-  for (int j = tid; j <= R; j += kXtBlock) rpl[j] = rp[r0 + j] - e0;
-  // segment starts/lengths; thread t owns tiles [t·G, t·G+G)
-  const int G = (S + kXtBlock - 1) / kXtBlock;
+  int rv[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int j = q * kXtBlock + tid;
+    rv[q] = j <= R ? rp[r0 + j] - e0 : 0;
+  }
+  int sa[G], sb[G];
+#pragma unroll
+  for (int q = 0; q < G; ++q) {
+    const int s = tid * G + q;
+    sa[q] = s < S ? segoff[c * S + s] : 0;
+    sb[q] = s < S ? segoff[(c + 1) * S + s] : 0;
+  }
+  if (tid < kXtM / 32) bm[tid] = 0u;
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int j = q * kXtBlock + tid;
+    if (j <= R) rpl[j] = rv[q];
+  }
   int lsum = 0;
-  for (int i = 0; i < G; ++i) {
-    const int s = tid * G + i;
-    if (s < S) {
-      const int a = segoff[c * S + s];
-      sst[s] = a;
-      lsum += segoff[(c + 1) * S + s] - a;
-    }
-  }
-  // block exclusive scan of lsum
+#pragma unroll
+  for (int q = 0; q < G; ++q) lsum += sb[q] - sa[q];
+  // block exclusive scan of the segment lengths → pre[], base[]
   int inc = lsum;
 #pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const int t = __shfl_up(inc, d, kWave);
-    if (lane >= d) inc += t;
+  for (int dd = 1; dd < kWave; dd <<= 1) {
+    const int t = __shfl_up(inc, dd, kWave);
+    if (lane >= dd) inc += t;
   }
   if (lane == kWave - 1) wsum[wv] = inc;
-#pragma unroll
-  for (int i = 0; i < kXtRun; ++i) vs[i * kXtBlock + tid] = v[i];
   __syncthreads();
-  int wbase = 0;
-  for (int w = 0; w < wv; ++w) wbase += wsum[w];
   {
-    int run = wbase + inc - lsum;
-    for (int i = 0; i < G; ++i) {
-      const int s = tid * G + i;
+    int run = inc - lsum;
+    for (int w = 0; w < wv; ++w) run += wsum[w];
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int s = tid * G + q;
       if (s < S) {
         pre[s] = run;
-        run += segoff[(c + 1) * S + s] - sst[s];
+        base[s] = sa[q] - run;
       }
+      run += sb[q] - sa[q];
     }
     if (tid == kXtBlock - 1) pre[S] = run;
   }
+  // row-start bitmap: owned rows starting inside the chunk (empty rows share a bit)
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int j = q * kXtBlock + tid;
+    if (j < R && rv[q] < m) atomicOr(bm + (rv[q] >> 5), 1u << (rv[q] & 31));
+  }
   __syncthreads();
 
-  // phase A: flat position f -> (segment, offset); xs[perm] = xg
+  // ---- round trip 3: xs[perm[src]] = xg[src] for the wave's flat positions
   {
-    int src[kXtRun];
-    int lo = 0;
+    const int fw = wv * PERW;
+    int s0 = 0;  // wave-uniform: largest s with pre[s] <= fw
+    {
+      const int step0 = S > 1 ? 1 << (31 - __builtin_clz(static_cast<unsigned>(S - 1))) : 0;
+      for (int step = step0; step > 0; step >>= 1) {
+        const int cand = s0 + step;
+        if (cand < S && pre[cand < S ? cand : S] <= fw) s0 = cand;
+      }
+      s0 = __builtin_amdgcn_readfirstlane(s0);
+    }
+    int src[NB];
 #pragma unroll
-    for (int u = 0; u < kXtRun; ++u) {
-      const int f = u * kXtBlock + tid;
+    for (int u = 0; u < NB; ++u) {
+      const int f0 = fw + u * kWave, f = f0 + lane;
       src[u] = -1;
-      if (f < m) {
-        int hi = S;  // largest s with pre[s] <= f, in [lo, S)
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (pre[mid] <= f) lo = mid; else hi = mid;
+      if (f0 < m) {  // wave-uniform
+        int cnt = 0;
+        for (int sb0 = s0 + 1;; sb0 += kWave) {  // segment starts after s0, 64 at a time
+          const int idx = sb0 + lane;
+          const int bnd = idx < S ? pre[idx] : INT32_MAX;
+          const uint64_t in = __ballot(bnd <= f0 + kWave - 1);
+          const int K = __popcll(in);
+          for (int k = 0; k < K; ++k) cnt += f >= __builtin_amdgcn_readlane(bnd, k) ? 1 : 0;
+          if (K < kWave) break;
         }
-        src[u] = sst[lo] + (f - pre[lo]);
+        const int sl = s0 + cnt;
+        if (f < m) src[u] = base[sl] + f;
+        s0 = __builtin_amdgcn_readlane(sl, kWave - 1);
       }
     }
-    T xv[kXtRun];
-    uint16_t pv[kXtRun];
+    T xv[NB];
+    uint16_t pv[NB];
 #pragma unroll
-    for (int u = 0; u < kXtRun; ++u) {
+    for (int u = 0; u < NB; ++u) {
       const int sidx = src[u] >= 0 ? src[u] : 0;
       xv[u] = xg[sidx];
       pv[u] = perm[sidx];
     }
 #pragma unroll
-    for (int u = 0; u < kXtRun; ++u)
-      if (src[u] >= 0) xs[pv[u]] = xv[u];
+    for (int u = 0; u < NB; ++u)
+      if (src[u] >= 0) xs[xt_pidx(pv[u])] = xv[u];
   }
   __syncthreads();
 
-  // empty owned rows
-  for (int j = tid; j < R; j += kXtBlock)
-    if (rpl[j] == rpl[j + 1]) y[r0 + j] = T(0);
-
-  // phase B: thread t sums its run [16t, 16t+16) merge-path style
-  const int i0 = tid * kXtRun;
-  const int i1 = (i0 + kXtRun) < m ? (i0 + kXtRun) : m;
-  bool head = false, head_ended = false, tail = false;
-  int jr = -1;
-  double acc = 0.0;
-  if (i0 < i1) {
-    // jr = last row with rpl[jr] <= i0 (−1: the chunk's head row)
-    int lo = -1, hi = R;  // rpl[R] >= m > i0
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (rpl[mid] <= i0) lo = mid; else hi = mid;
-    }
-    jr = lo;
-    bool started = jr >= 0 && rpl[jr] == i0;
-    bool first = true;
-    int nextb = rpl[jr + 1];
+  // ---- phase B: branch-free segmented scan of the thread's run
+  const int n = m - i0 < kXtRun ? (m - i0 > 0 ? m - i0 : 0) : kXtRun;  // valid entries in the run
+  const uint32_t mask = (bm[tid >> 1] >> ((tid & 1) * 16)) & 0xFFFFu;
+  const int hl = mask ? __builtin_ctz(mask) : kXtRun;  // head length (entries before the first start)
+  const int hend = (hl < n ? hl : n) - 1;                // last head position (−1: none)
+  double acc = 0.0, hsave = 0.0;
 #pragma unroll
-    for (int j = 0; j < kXtRun; ++j) {
-      const int i = i0 + j;
-      if (i < i1) {
-        if (i == nextb) {  // row jr ends before i
-          if (first && !started) {
-            hp[tid] = acc;
-            head = true;
-            head_ended = true;
-          } else {
-            y[r0 + jr] = static_cast<T>(acc);
-          }
-          first = false;
-          ++jr;
-          while (rpl[jr + 1] <= i) ++jr;  // skip empty rows
-          started = true;
-          nextb = rpl[jr + 1];
-          acc = 0.0;
-        }
-        acc += static_cast<double>(vs[i]) * static_cast<double>(xs[i]);
-      }
-    }
-    const bool ended = nextb == i1;
-    if (first && !started) {
-      hp[tid] = acc;
-      head = true;
-      head_ended = ended;
-    } else if (ended) {
-      y[r0 + jr] = static_cast<T>(acc);
-    } else {
-      tp[tid] = acc;
-      tail = true;
-    }
+  for (int j = 0; j < kXtRun; ++j) {
+    const double pj = j < n ? static_cast<double>(vv[j / VW][j % VW]) * static_cast<double>(xs[17 * tid + j]) : 0.0;
+    acc = ((mask >> j) & 1u) ? 0.0 : acc;
+    acc += pj;
+    hsave = j == hend ? acc : hsave;
+    xs[17 * tid + j] = static_cast<T>(acc);  // in place; padding slots past m are never read
   }
+  const bool has_head = n > 0 && !(mask & 1u);
+  if (has_head) hp[tid] = hsave;
+  if (n > 0 && mask) tp[tid] = acc;
+  const bool cont = rpl[R] > m;  // the row active at m−1 runs past the chunk
   __syncthreads();
-  // combine pieces of rows that cross thread runs (fixed order: run order)
+  // ---- combine rows that cross runs (fixed order: run order)
   const int tlast = m > 0 ? (m - 1) / kXtRun : -1;
   if (tid == 0 && !(m > 0 && rpl[0] > 0)) carry[2 * c] = 0.0;  // no head piece
-  if (head && (head_ended || tid == tlast)) {
-    // the row of this thread's head piece: jh (−1 = the chunk's head row)
-    int jh;
-    {
-      int lo = -1, hi = R;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (rpl[mid] <= i0) lo = mid; else hi = mid;
+  if (has_head) {
+    const int i1 = i0 + n;
+    const bool end_i1 = i1 < m ? ((bm[i1 >> 5] >> (i1 & 31)) & 1u) != 0 : !cont;
+    const bool ends = hl < n || end_i1;
+    if (ends || tid == tlast) {
+      int u = tid - 1;  // thread where the row started (−1: before the chunk)
+      while (u >= 0 && ((bm[u >> 1] >> ((u & 1) * 16)) & 0xFFFFu) == 0u) --u;
+      double sum = u >= 0 ? tp[u] : 0.0;
+      for (int v = u + 1; v <= tid; ++v) sum += hp[v];
+      if (u < 0) {
+        carry[2 * c] = sum;  // this chunk's piece of the previous chunk's row
+      } else if (ends) {
+        xs[xt_pidx(i0 + hend)] = static_cast<T>(sum);
+      } else {
+        carry[2 * c + 1] = sum;  // row continues into the next chunk
       }
-      jh = lo;
-    }
-    const int ts = jh >= 0 ? rpl[jh] / kXtRun : 0;
-    double s = jh >= 0 ? tp[ts] : hp[0];
-    for (int u = ts + 1; u <= tid; ++u) s += hp[u];
-    if (jh < 0) {
-      carry[2 * c] = s;  // this chunk's piece of the previous chunk's row
-    } else if (head_ended) {
-      y[r0 + jh] = static_cast<T>(s);
-    } else {
-      carry[2 * c + 1] = s;  // row continues into the next chunk
     }
   }
-  if (tail && tid == tlast) carry[2 * c + 1] = tp[tid];  // own tail row continues past the chunk
+  if (tid == tlast && mask && cont) carry[2 * c + 1] = tp[tid];  // own tail row continues
+  __syncthreads();
+  // coalesced y store of the owned rows from their last positions (a row
+  // continuing past the chunk is stored by k_xtile_fixup, later on the stream)
+  for (int j = tid; j < R; j += kXtBlock) {
+    const int a0 = rpl[j], a1 = rpl[j + 1];
+    if (a1 == a0) y[r0 + j] = T(0);
+    else if (a1 <= m) y[r0 + j] = xs[xt_pidx(a1 - 1)];
+  }
 }
 
 // rows cut by a chunk end: y[row] = tail piece + head pieces, chunk order
@@ -923,6 +951,7 @@ struct lhpc_spmv_plan {
   int64_t xt_C = 0, xt_pieces = 0, xt_cont = 0, xt_total = 0;
   size_t xt_lds = 0;
   int xt_u = 4;
+  int32_t *d_cdesc = nullptr;
   int32_t *d_ce = nullptr, *d_cr = nullptr, *d_segoff = nullptr, *d_pieces = nullptr, *d_cont = nullptr;
   uint16_t *d_col16 = nullptr, *d_perm = nullptr;
   void *d_xg = nullptr;
@@ -1110,9 +1139,18 @@ int launch_xslice(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s
 }
 
 size_t xtile_lds_bytes(size_t tsz, int S) {
-  return 2 * static_cast<size_t>(kXtM) * tsz + 2 * kXtBlock * sizeof(double) +
+  return static_cast<size_t>(kXtM + kXtM / 16) * tsz + 2 * kXtBlock * sizeof(double) +
+         kXtM / 32 * sizeof(uint32_t) +
          sizeof(int32_t) * (static_cast<size_t>(kXtRmax) + 1 + 2 * static_cast<size_t>(S) + 1 + 4);
 }
+
+int xtile_g(int S) {
+  const int g = (S + kXtBlock - 1) / kXtBlock;
+  return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : g <= 8 ? 8 : 16;
+}
+
+template <typename T, int G>
+const void *xtile_reduce_fn() { return reinterpret_cast<const void *>(k_xtile_reduce<T, G>); }
 
 template <typename T>
 int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
@@ -1129,10 +1167,19 @@ int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s)
     LHPC_TRY(check_launch(s));
   }
   const int64_t Cx = (p->xt_C + 7) / 8;
-  hipLaunchKernelGGL((k_xtile_reduce<T>), dim3(static_cast<unsigned>(8 * Cx)), dim3(kXtBlock),
-                     p->xt_lds, s, p->d_ce, p->d_cr, p->d_segoff, p->S, p->xt_C, Cx, xg, p->d_perm,
-                     static_cast<const T *>(p->d_val), static_cast<const int32_t *>(p->d_row_ptr),
-                     static_cast<T *>(y), p->d_carry);
+  const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(kXtBlock);
+#define LHPC_XT_RED(GG)                                                                              \
+  hipLaunchKernelGGL((k_xtile_reduce<T, GG>), rg, rb, p->xt_lds, s, p->d_cdesc, p->d_segoff, p->S,  \
+                     p->xt_C, Cx, xg, p->d_perm, static_cast<const T *>(p->d_val),                    \
+                     static_cast<const int32_t *>(p->d_row_ptr), static_cast<T *>(y), p->d_carry)
+  switch (xtile_g(p->S)) {
+    case 1: LHPC_XT_RED(1); break;
+    case 2: LHPC_XT_RED(2); break;
+    case 4: LHPC_XT_RED(4); break;
+    case 8: LHPC_XT_RED(8); break;
+    default: LHPC_XT_RED(16); break;
+  }
+#undef LHPC_XT_RED
   LHPC_TRY(check_launch(s));
   if (p->xt_cont > 0) {
     hipLaunchKernelGGL((k_xtile_fixup<T>), dim3(static_cast<unsigned>((p->xt_cont + kXtBlock - 1) / kXtBlock)),
@@ -1213,9 +1260,17 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   p->xt_total = xt.total;
   p->xt_lds = xtile_lds_bytes(tsz, xt.S);
   if (const char *env = std::getenv("LHPC_XTILE_U")) p->xt_u = std::atoi(env) == 2 ? 2 : 4;
-  const void *kfn = tsz == 4 ? reinterpret_cast<const void *>(k_xtile_reduce<float>)
-                             : reinterpret_cast<const void *>(k_xtile_reduce<double>);
-  LHPC_HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
+  {
+    const int g = xtile_g(xt.S);
+    const void *kfn =
+        tsz == 4 ? (g == 1 ? xtile_reduce_fn<float, 1>() : g == 2 ? xtile_reduce_fn<float, 2>()
+                    : g == 4 ? xtile_reduce_fn<float, 4>() : g == 8 ? xtile_reduce_fn<float, 8>()
+                             : xtile_reduce_fn<float, 16>())
+                 : (g == 1 ? xtile_reduce_fn<double, 1>() : g == 2 ? xtile_reduce_fn<double, 2>()
+                    : g == 4 ? xtile_reduce_fn<double, 4>() : g == 8 ? xtile_reduce_fn<double, 8>()
+                             : xtile_reduce_fn<double, 16>());
+    LHPC_HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
+  }
   const int64_t n_rows = p->n_rows, nnz = p->nnz, C = xt.n_chunks;
   auto up = [&](void **d, const void *h, size_t n) -> int {
     LHPC_TRY(dmalloc(d, n, p->bytes));
@@ -1225,7 +1280,20 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   std::vector<int32_t> rp32(static_cast<size_t>(n_rows + 1));
   for (int64_t i = 0; i <= n_rows; ++i) rp32[static_cast<size_t>(i)] = static_cast<int32_t>(rp[i]);
   LHPC_TRY(up(&p->d_row_ptr, rp32.data(), rp32.size() * 4));
-  LHPC_TRY(up(&p->d_val, val, static_cast<size_t>(nnz) * tsz));
+  // val padded by one run: a reduce thread loads its whole 16-nonzero run as vectors
+  LHPC_TRY(dmalloc(&p->d_val, static_cast<size_t>(nnz + kXtRun) * tsz, p->bytes));
+  LHPC_HIP_TRY(hipMemset(static_cast<unsigned char *>(p->d_val) + nnz * tsz, 0, kXtRun * tsz));
+  if (nnz) LHPC_HIP_TRY(hipMemcpy(p->d_val, val, static_cast<size_t>(nnz) * tsz, hipMemcpyHostToDevice));
+  {
+    std::vector<int32_t> cd(static_cast<size_t>(4 * C + 4));
+    for (int64_t c = 0; c < C; ++c) {
+      cd[4 * c] = xt.ce[c];
+      cd[4 * c + 1] = xt.ce[c + 1];
+      cd[4 * c + 2] = xt.cr[c];
+      cd[4 * c + 3] = xt.cr[c + 1];
+    }
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cdesc), cd.data(), cd.size() * 4));
+  }
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_ce), xt.ce.data(), xt.ce.size() * 4));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cr), xt.cr.data(), xt.cr.size() * 4));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_segoff), xt.segoff.data(), xt.segoff.size() * 4));
@@ -1593,7 +1661,7 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
                   static_cast<void *>(p->d_blocks), p->d_xstage, p->d_ystage,
                   p->d_lens, static_cast<void *>(p->d_cbase), p->d_partial,
                   static_cast<void *>(p->d_arrive), static_cast<void *>(p->d_dpart),
-                  static_cast<void *>(p->d_ce), static_cast<void *>(p->d_cr), static_cast<void *>(p->d_segoff),
+                  static_cast<void *>(p->d_cdesc), static_cast<void *>(p->d_ce), static_cast<void *>(p->d_cr), static_cast<void *>(p->d_segoff),
                   static_cast<void *>(p->d_pieces), static_cast<void *>(p->d_cont),
                   static_cast<void *>(p->d_col16), static_cast<void *>(p->d_perm), p->d_xg,
                   static_cast<void *>(p->d_carry)})
