@@ -124,8 +124,93 @@ int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, 
   return LHPC_OK;
 }
 
+namespace {
+// Chunk-major layout (XtileHost::cm), after the chunks are cut.
+int build_xtile_cm(const int32_t *col, int64_t nnz, int64_t piece_nnz, XtileHost &o) {
+  const int64_t S = o.S, W = o.W, C = o.n_chunks;
+  auto pad8 = [](int64_t v) { return (v + 7) / 8 * 8; };
+  std::vector<int32_t> cnt(static_cast<size_t>(C * S), 0);  // [c][s]
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t c = 0; c < C; ++c) {
+    int32_t *cc = cnt.data() + c * S;
+    for (int64_t k = o.ce[c]; k < o.ce[c + 1]; ++k) ++cc[col[k] / W];
+  }
+  std::vector<int64_t> tbase(static_cast<size_t>(S) + 1, 0);
+  {
+    std::vector<int64_t> tot(static_cast<size_t>(S), 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t s = 0; s < S; ++s) {
+      int64_t t = 0;
+      for (int64_t c = 0; c < C; ++c) t += pad8(cnt[c * S + s]);
+      tot[static_cast<size_t>(s)] = t;
+    }
+    for (int64_t s = 0; s < S; ++s) tbase[s + 1] = tbase[s] + tot[s];
+  }
+  if (tbase[S] >= INT32_MAX - 64) return LHPC_ERR_UNSUPPORTED;
+  o.total = tbase[S];
+  // padded segment starts in (tile, chunk) order; row C = tile ends
+  o.segoff.assign(static_cast<size_t>((C + 1) * S), 0);
+#pragma omp parallel for schedule(static)
+  for (int64_t s = 0; s < S; ++s) {
+    int64_t acc = tbase[s];
+    for (int64_t c = 0; c <= C; ++c) {
+      o.segoff[c * S + s] = static_cast<int32_t>(acc);
+      if (c < C) acc += pad8(cnt[c * S + s]);
+    }
+  }
+  o.col16.reset(new uint16_t[o.total > 0 ? o.total : 1]);
+  std::fill(o.col16.get(), o.col16.get() + (o.total > 0 ? o.total : 1), static_cast<uint16_t>(0xFFFF));
+  o.gdst.reset(new int32_t[o.total / 8 > 0 ? o.total / 8 : 1]);
+  o.perm.reset(new uint16_t[nnz > 0 ? nnz : 1]);
+#pragma omp parallel
+  {
+    std::vector<int32_t> cur_t(static_cast<size_t>(S)), cur_c(static_cast<size_t>(S));
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t c = 0; c < C; ++c) {
+      const int64_t e0 = o.ce[c];
+      const int32_t *cc = cnt.data() + c * S;
+      int64_t pos = e0;  // xg position of segment (c, s): e0 + Σ_{s' < s} cnt
+      for (int64_t s = 0; s < S; ++s) {
+        const int32_t g = o.segoff[c * S + s];
+        cur_t[static_cast<size_t>(s)] = g;
+        cur_c[static_cast<size_t>(s)] = static_cast<int32_t>(pos);
+        for (int32_t j = 0; j < cc[s]; j += 8) o.gdst[(g + j) / 8] = static_cast<int32_t>(pos + j);
+        pos += cc[s];
+      }
+      for (int64_t k = e0; k < o.ce[c + 1]; ++k) {
+        const int64_t s = col[k] / W;
+        o.col16[cur_t[static_cast<size_t>(s)]++] = static_cast<uint16_t>(col[k] - s * W);
+        o.perm[cur_c[static_cast<size_t>(s)]++] = static_cast<uint16_t>(k - e0);
+      }
+    }
+  }
+  // pieces: H chunk ranges × TPX tiles per XCD group; block b = (h, j, x) with
+  // x = b % 8 gathers tile x·TPX + j over chunk range h
+  const int64_t per_tile = S > 0 ? (o.total + S - 1) / S : 0;
+  const int64_t H = std::max<int64_t>(1, std::min<int64_t>(C, (per_tile + piece_nnz / 2) / std::max<int64_t>(8, piece_nnz)));
+  const int64_t TPX = (S + 7) / 8;
+  o.pieces.clear();
+  o.pieces.reserve(static_cast<size_t>(3 * H * TPX * 8));
+  for (int64_t h = 0; h < H; ++h) {
+    const int64_t clo = C * h / H, chi = C * (h + 1) / H;
+    for (int64_t j = 0; j < TPX; ++j)
+      for (int64_t x = 0; x < 8; ++x) {
+        const int64_t s = x * TPX + j;
+        if (s < S) {
+          o.pieces.push_back(o.segoff[clo * S + s]);
+          o.pieces.push_back(o.segoff[chi * S + s]);
+          o.pieces.push_back(static_cast<int32_t>(s));
+        } else {
+          o.pieces.insert(o.pieces.end(), {0, 0, 0});
+        }
+      }
+  }
+  return LHPC_OK;
+}
+}  // namespace
+
 int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
-                int64_t W, int M, int Rmax, int64_t piece_nnz, XtileHost &o) {
+                int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm, XtileHost &o) {
   const int64_t nnz = rp_at(rp, bits, n_rows) - rp_at(rp, bits, 0);
   if (W < 8 || M < 64 || M > 65536 || Rmax < 1) return LHPC_ERR_INVALID_ARG;
   const int64_t S = n_cols > 0 ? (n_cols + W - 1) / W : 1;
@@ -134,6 +219,7 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
   o.W = W;
   o.M = M;
   o.Rmax = Rmax;
+  o.cm = cm;
   auto RP = [&](int64_t i) { return rp_at(rp, bits, i); };
   // first row r in [lo, n_rows] with rp[r] >= e
   auto lower_row = [&](int64_t lo, int64_t e) {
@@ -184,6 +270,7 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
     const int64_t r0 = o.cr[c], r1 = o.cr[c + 1];
     if (r1 > r0 && RP(r1) > o.ce[c + 1]) o.cont.push_back(static_cast<int32_t>(c));
   }
+  if (cm) return build_xtile_cm(col, nnz, piece_nnz, o);
   // ---- per (chunk, tile) counts → segment offsets in (tile, chunk) order
   o.segoff.assign(static_cast<size_t>((C + 1) * S), 0);
   int32_t *cnt = o.segoff.data() + S;  // row c+1 temporarily holds count[c]

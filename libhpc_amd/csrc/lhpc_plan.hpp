@@ -52,24 +52,42 @@ int build_xslice(const void *row_ptr, int rp_bits, const int32_t *col, const voi
 // Chunks cut the CSR order at row starts where one lies in the back half of
 // the M window, else mid-row; a chunk owns the rows that start in it (≤ Rmax)
 // and a row cut by a chunk end is finished by a fix-up over `cont`.
+//
+// cm = true (chunk-major xg, opt-in): gather writes xg in the chunk's
+// segment concatenation order — chunk c occupies [ce[c], ce[c+1]) of xg,
+// tiles ascending inside it — so reduce reads its chunk as one contiguous run
+// and needs no segment table.  Each tile-stream segment is padded to a
+// multiple of 8 (padding col16 = 0xFFFF, never stored); gdst[q] is the xg
+// position of group q's first entry (a group's entries are contiguous in
+// xg), and perm is indexed by xg position.  Pieces are (tile, chunk range)
+// pairs ordered so that blocks b with b % 8 == x (one XCD) gather a
+// contiguous run of tiles — the xg lines of a chunk are then assembled in
+// one L2 — and a whole chunk range before the next (H ranges).
+// cm = false: xg is in tile-stream order (tile, chunk, CSR position), perm is
+// indexed by stream position, and reduce locates its S segments by segoff.
 struct XtileHost {
   int S = 0;
   int64_t W = 0;
   int M = 0, Rmax = 0;
+  bool cm = false;
   int64_t n_chunks = 0;
-  int64_t total = 0;                 // padded stream length
+  int64_t total = 0;                 // padded tile-stream length
   std::vector<int32_t> ce, cr;       // [C+1] chunk first nonzero / first owned row
-  std::vector<int32_t> segoff;       // [(C+1)·S]
-  std::vector<int32_t> pieces;       // gather workgroups: (g0, g1, s) triples
+  std::vector<int32_t> segoff;       // [(C+1)·S] segment starts in the tile stream
+  std::vector<int32_t> pieces;       // gather workgroups: (g0, g1, s) triples (g0 == g1: idle)
   std::vector<int32_t> cont;         // chunks whose last owned row runs past the chunk
-  std::unique_ptr<uint16_t[]> col16, perm;  // [total]
+  std::unique_ptr<uint16_t[]> col16;  // [total]
+  std::unique_ptr<uint16_t[]> perm;   // [total] (cm: [nnz])
+  std::unique_ptr<int32_t[]> gdst;    // cm: [total / 8]
 };
 
 // 0 on success; LHPC_ERR_UNSUPPORTED when the layout does not fit its
 // index types (nnz + padding ≥ 2^31, S > 4096, or an oversized segment table).
-// piece_nnz: target nonzeros per gather workgroup (multiple of 8 is used).
+// piece_nnz: target nonzeros per gather workgroup (multiple of 8 is used;
+// cm: the number of chunk ranges H is derived from it).
 int build_xtile(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_rows,
-                int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, XtileHost &out);
+                int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm,
+                XtileHost &out);
 
 // in-slice length of row r in slice s
 inline int xs_len(const XsliceHost &o, int s, int64_t r) {

@@ -661,14 +661,20 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
 // reduce: one block per chunk c = (b % 8)·Cx + b / 8, so each XCD walks a
 // contiguous run of chunks and the xg lines two neighbouring chunks share
 // stay in its L2.  PMC (profiles/r01/xtile_*): the stream equals the
-// algorithmic bytes and the kernel is instruction-issue bound, so both phases
-// are branch-free in the common case:
-//   phase A  wave w owns flat positions [1024w, 1024w+1024) of the chunk's
-//            segment concatenation, in batches of 64.  A wave-uniform cursor
-//            s0 (segment of the batch start) advances batch by batch; a lane
-//            finds its segment as s0 + #(segment starts in (f0, f]) from ONE
-//            LDS read of the next 64 starts, a ballot and ~4 readlanes; the
-//            source index is base[s] + f (base = segment start − prefix).
+// algorithmic bytes and the kernel is bound by instruction issue and load
+// latency, so both phases are branch-free and every load that does not
+// depend on another is issued together (three round trips per chunk: the
+// 16-B chunk descriptor {e0, e1, r0, r1}; val run + row_ptr + segment table;
+// xg/perm):
+//   scan     the chunk's S segment lengths are prefix-summed (with a count of
+//            non-empty segments packed in the high half), giving each
+//            non-empty segment its rank, base_ne[rank] = segment start −
+//            flat offset, and a bit at its flat offset in sbm (M bits).
+//   phase A  flat position f of the segment concatenation lies in the
+//            non-empty segment of rank popcount(sbm bits ≤ f) − 1: one wave
+//            prefix-scan of the 64 sbm words gives each 64-position batch its
+//            base rank, mbcnt gives the lane's; src = base_ne[rank] + f, and
+//            xs[perm[src]] = xg[src].  Wave w owns batches [16w, 16w+16).
 //   phase B  thread t owns the run [16t, 16t+16); a bitmap of row starts
 //            (ds_or) drives a segmented scan (reset at a start, add), whose
 //            running value rounded to T is written back in place: a row that
@@ -676,12 +682,9 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
 //            of rows crossing runs (hp: before the run's first start, tp:
 //            after its last) are combined in run order, and the owned rows'
 //            y is stored coalesced from their last positions.
-// Every load that does not depend on another is issued together: one 16-B
-// chunk descriptor {e0, e1, r0, r1}, then val (the thread's own run as 16-B
-// vectors), row_ptr and the segment table, then xg/perm — three round trips.
 // xs lives in LDS at pidx(i) = i + i/16 (thread t's run at [17t, 17t+16):
 // conflict-free).  Dynamic LDS: xs[M+M/16] T, hp[256] f64, tp[256] f64,
-// bm[M/32] u32, rpl[Rmax+1] i32, pre[S+1] i32, base[S] i32, wsum[4] i32.
+// bm[M/32] u32, sbm[M/32] u32, rpl[Rmax+1] i32, base_ne[S] i32, wsum[4] i32.
 __device__ __forceinline__ int xt_pidx(int i) { return i + (i >> 4); }
 
 template <typename T, int G>
@@ -692,30 +695,31 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
     double *__restrict__ carry) {
   constexpr int MP = kXtM + kXtM / 16;
   constexpr int RPT = (kXtRmax + 1 + kXtBlock - 1) / kXtBlock;  // row_ptr loads per thread
-  constexpr int PERW = kXtM / (kXtBlock / kWave);                // flat positions per wave
-  constexpr int NB = PERW / kWave;                               // batches per wave
+  constexpr int NB = kXtM / kXtBlock;                            // 64-position batches per wave
+  static_assert(kXtM / kWave == kWave, "one sbm word per lane");
+  typedef T tvec __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
+  constexpr int VW = 16 / sizeof(T), NV = kXtRun / VW;
   extern __shared__ __align__(16) unsigned char smem[];
   T *xs = reinterpret_cast<T *>(smem);
   double *hp = reinterpret_cast<double *>(xs + MP);
   double *tp = hp + kXtBlock;
   uint32_t *bm = reinterpret_cast<uint32_t *>(tp + kXtBlock);
-  int32_t *rpl = reinterpret_cast<int32_t *>(bm + kXtM / 32);
-  int32_t *pre = rpl + (kXtRmax + 1);
-  int32_t *base = pre + (S + 1);
-  int32_t *wsum = base + S;
+  uint32_t *sbm = bm + kXtM / 32;
+  int32_t *rpl = reinterpret_cast<int32_t *>(sbm + kXtM / 32);
+  int32_t *base_ne = rpl + (kXtRmax + 1);
+  int32_t *wsum = base_ne + S;
 
   const int tid = threadIdx.x;
-  const int lane = tid & (kWave - 1), wv = tid / kWave;
+  const int lane = tid & (kWave - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int i0 = tid * kXtRun;
   const int64_t c = static_cast<int64_t>(blockIdx.x % 8) * Cx + blockIdx.x / 8;
   if (c >= C) return;  // block-uniform
   const u32x4 d = *reinterpret_cast<const u32x4 *>(cdesc + 4 * c);
   const int e0 = static_cast<int>(d[0]), m = static_cast<int>(d[1]) - e0;
   const int r0 = static_cast<int>(d[2]), R = static_cast<int>(d[3]) - r0;
-  const int i0 = tid * kXtRun;
 
-  // ---- round trip 2: val run, row_ptr, segment table — all issued together
-  typedef T tvec __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
-  constexpr int VW = 16 / sizeof(T), NV = kXtRun / VW;
+  // ---- round trip 2: val run, row_ptr, segment table (unconditional loads)
   tvec vv[NV];
   {
     // the val allocation is padded by one run, so a run may read past nnz
@@ -723,29 +727,37 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
 #pragma unroll
     for (int q = 0; q < NV; ++q) vv[q] = __builtin_nontemporal_load(vp + q);
   }
-  int rv[RPT];
+  int rv[RPT], sa[G], sb[G];
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
     const int j = q * kXtBlock + tid;
-    rv[q] = j <= R ? rp[r0 + j] - e0 : 0;
+    rv[q] = rp[r0 + (j <= R ? j : R)];
   }
-  int sa[G], sb[G];
 #pragma unroll
   for (int q = 0; q < G; ++q) {
-    const int s = tid * G + q;
-    sa[q] = s < S ? segoff[c * S + s] : 0;
-    sb[q] = s < S ? segoff[(c + 1) * S + s] : 0;
+    const int sI = tid * G + q;
+    const int sc = sI < S ? sI : S - 1;
+    sa[q] = segoff[c * S + sc];
+    sb[q] = segoff[(c + 1) * S + sc];
   }
-  if (tid < kXtM / 32) bm[tid] = 0u;
+  // ---- scan: segment ranks / bases, segment-start and row-start bitmaps
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) rv[q] -= e0;
+  if (tid < kXtM / 32) {
+    bm[tid] = 0u;
+    sbm[tid] = 0u;
+  }
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
     const int j = q * kXtBlock + tid;
     if (j <= R) rpl[j] = rv[q];
   }
-  int lsum = 0;
+  int lsum = 0;  // (length | non-empty count << 16) of this thread's segments
 #pragma unroll
-  for (int q = 0; q < G; ++q) lsum += sb[q] - sa[q];
-  // block exclusive scan of the segment lengths → pre[], base[]
+  for (int q = 0; q < G; ++q) {
+    if (tid * G + q >= S) sb[q] = sa[q];
+    lsum += (sb[q] - sa[q]) + (sb[q] > sa[q] ? 0x10000 : 0);
+  }
   int inc = lsum;
 #pragma unroll
   for (int dd = 1; dd < kWave; dd <<= 1) {
@@ -757,69 +769,61 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
   {
     int run = inc - lsum;
     for (int w = 0; w < wv; ++w) run += wsum[w];
+    int off = run & 0xFFFF, rank = run >> 16;
 #pragma unroll
     for (int q = 0; q < G; ++q) {
-      const int s = tid * G + q;
-      if (s < S) {
-        pre[s] = run;
-        base[s] = sa[q] - run;
+      const int len = sb[q] - sa[q];
+      if (len > 0) {
+        base_ne[rank] = sa[q] - off;
+        atomicOr(sbm + (off >> 5), 1u << (off & 31));
+        ++rank;
       }
-      run += sb[q] - sa[q];
+      off += len;
     }
-    if (tid == kXtBlock - 1) pre[S] = run;
   }
-  // row-start bitmap: owned rows starting inside the chunk (empty rows share a bit)
 #pragma unroll
-  for (int q = 0; q < RPT; ++q) {
+  for (int q = 0; q < RPT; ++q) {  // row starts inside the chunk (empty rows share a bit)
     const int j = q * kXtBlock + tid;
     if (j < R && rv[q] < m) atomicOr(bm + (rv[q] >> 5), 1u << (rv[q] & 31));
   }
   __syncthreads();
 
-  // ---- round trip 3: xs[perm[src]] = xg[src] for the wave's flat positions
+  // ---- phase A: src = base_ne[rank] + f, loads of xg/perm (round trip 3)
+  int src[NB];
   {
-    const int fw = wv * PERW;
-    int s0 = 0;  // wave-uniform: largest s with pre[s] <= fw
-    {
-      const int step0 = S > 1 ? 1 << (31 - __builtin_clz(static_cast<unsigned>(S - 1))) : 0;
-      for (int step = step0; step > 0; step >>= 1) {
-        const int cand = s0 + step;
-        if (cand < S && pre[cand < S ? cand : S] <= fw) s0 = cand;
-      }
-      s0 = __builtin_amdgcn_readfirstlane(s0);
+    const uint64_t wl = static_cast<uint64_t>(sbm[2 * lane]) | (static_cast<uint64_t>(sbm[2 * lane + 1]) << 32);
+    int incl = __popcll(wl);  // inclusive wave scan of the per-batch start counts
+#pragma unroll
+    for (int dd = 1; dd < kWave; dd <<= 1) {
+      const int t = __shfl_up(incl, dd, kWave);
+      if (lane >= dd) incl += t;
     }
-    int src[NB];
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      const int f0 = fw + u * kWave, f = f0 + lane;
-      src[u] = -1;
-      if (f0 < m) {  // wave-uniform
-        int cnt = 0;
-        for (int sb0 = s0 + 1;; sb0 += kWave) {  // segment starts after s0, 64 at a time
-          const int idx = sb0 + lane;
-          const int bnd = idx < S ? pre[idx] : INT32_MAX;
-          const uint64_t in = __ballot(bnd <= f0 + kWave - 1);
-          const int K = __popcll(in);
-          for (int k = 0; k < K; ++k) cnt += f >= __builtin_amdgcn_readlane(bnd, k) ? 1 : 0;
-          if (K < kWave) break;
-        }
-        const int sl = s0 + cnt;
-        if (f < m) src[u] = base[sl] + f;
-        s0 = __builtin_amdgcn_readlane(sl, kWave - 1);
-      }
+      const int q = wv * NB + u;  // batch: flat positions [64q, 64q+64)
+      const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(wl), q);
+      const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(wl >> 32), q);
+      const int rb = (q > 0 ? __builtin_amdgcn_readlane(incl, q - 1) : 0) - 1;
+      const int below = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0));
+      const int own = lane < 32 ? (lo >> lane) & 1 : (hi >> (lane - 32)) & 1;
+      const int f = q * kWave + lane;
+      int rk = rb + below + own;
+      rk = rk < 0 ? 0 : (rk < S ? rk : S - 1);  // clamped: the LDS read stays unconditional
+      const int sv = base_ne[rk] + f;
+      src[u] = f < m ? sv : -1;
     }
-    T xv[NB];
-    uint16_t pv[NB];
-#pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      const int sidx = src[u] >= 0 ? src[u] : 0;
-      xv[u] = xg[sidx];
-      pv[u] = perm[sidx];
-    }
-#pragma unroll
-    for (int u = 0; u < NB; ++u)
-      if (src[u] >= 0) xs[xt_pidx(pv[u])] = xv[u];
   }
+  T xv[NB];
+  uint16_t pv[NB];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int sidx = src[u] >= 0 ? src[u] : 0;
+    xv[u] = xg[sidx];
+    pv[u] = perm[sidx];
+  }
+#pragma unroll
+  for (int u = 0; u < NB; ++u)  // positions past m go to the spare slot MP−1 (never read)
+    xs[src[u] >= 0 ? xt_pidx(pv[u]) : MP - 1] = xv[u];
   __syncthreads();
 
   // ---- phase B: branch-free segmented scan of the thread's run
@@ -830,7 +834,8 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
   double acc = 0.0, hsave = 0.0;
 #pragma unroll
   for (int j = 0; j < kXtRun; ++j) {
-    const double pj = j < n ? static_cast<double>(vv[j / VW][j % VW]) * static_cast<double>(xs[17 * tid + j]) : 0.0;
+    const double pr = static_cast<double>(vv[j / VW][j % VW]) * static_cast<double>(xs[17 * tid + j]);
+    const double pj = j < n ? pr : 0.0;
     acc = ((mask >> j) & 1u) ? 0.0 : acc;
     acc += pj;
     hsave = j == hend ? acc : hsave;
@@ -887,6 +892,197 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_fixup(
     if (cr[d + 1] > cr[d]) break;
   }
   y[cr[c + 1] - 1] = static_cast<T>(s);
+}
+
+// ------------------------------------------------- XTILE, chunk-major xg
+// (layout: lhpc_plan.hpp XtileHost::cm)
+// gather: block b streams pieces[3b..3b+1] of tile pieces[3b+2] (idle when
+// empty).  Per thread and step: one 16-B col16 load (a group of 8 entries of
+// one segment, padding 0xFFFF at its end) and the group's xg position, 8 LDS
+// gathers, and 8 contiguous xg stores — two unaligned 16-B stores for a full
+// group (fp32), per-entry stores for a segment's last group.
+template <typename T, int U>
+__global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather_cm(
+    const int32_t *__restrict__ pieces, const uint16_t *__restrict__ col16,
+    const int32_t *__restrict__ gdst, const T *__restrict__ x, int64_t n_cols, T *__restrict__ xg) {
+  constexpr int W = XtTile<T>::W;
+  __shared__ T xt[W];
+  const int tid = threadIdx.x;
+  const int g0 = pieces[3 * blockIdx.x], g1 = pieces[3 * blockIdx.x + 1];
+  if (g0 == g1) return;  // block-uniform: no entries of this tile in this chunk range
+  const int64_t c0 = static_cast<int64_t>(pieces[3 * blockIdx.x + 2]) * W;
+  const int wlen = static_cast<int>((n_cols - c0) < W ? (n_cols - c0) : W);
+  constexpr int PT = W / kXtGatherBlock;
+  T tv[PT];
+#pragma unroll
+  for (int i = 0; i < PT; ++i) {
+    const int j = i * kXtGatherBlock + tid;
+    tv[i] = j < wlen ? x[c0 + j] : T(0);
+  }
+#pragma unroll
+  for (int i = 0; i < PT; ++i) xt[i * kXtGatherBlock + tid] = tv[i];
+  __syncthreads();
+  typedef T tvec4u __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
+  constexpr int VW = 16 / sizeof(T);
+  const int q0 = g0 >> 3, q1 = g1 >> 3;  // 8-entry groups
+  const u32x4 *cv = reinterpret_cast<const u32x4 *>(col16);
+  for (int q = q0 + tid; q < q1; q += U * kXtGatherBlock) {
+    u32x4 w[U];
+    int dst[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int qq = q + u * kXtGatherBlock;
+      const int qc = qq < q1 ? qq : q0;  // clamped: the loads stay unconditional
+      w[u] = __builtin_nontemporal_load(cv + qc);
+      dst[u] = __builtin_nontemporal_load(gdst + qc);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int qq = q + u * kXtGatherBlock;
+      T o[8];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const uint32_t lo = w[u][h] & 0xFFFFu, hi = w[u][h] >> 16;
+        o[2 * h] = xt[lo < static_cast<uint32_t>(W) ? lo : 0u];
+        o[2 * h + 1] = xt[hi < static_cast<uint32_t>(W) ? hi : 0u];
+      }
+      if (qq < q1) {
+        T *d = xg + dst[u];
+        if ((w[u][3] >> 16) != 0xFFFFu) {  // full group
+#pragma unroll
+          for (int v = 0; v < 8 / VW; ++v) {
+            tvec4u t;
+#pragma unroll
+            for (int e = 0; e < VW; ++e) t[e] = o[v * VW + e];
+            *reinterpret_cast<tvec4u *>(d + v * VW) = t;
+          }
+        } else {
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            if ((w[u][h] & 0xFFFFu) != 0xFFFFu) d[2 * h] = o[2 * h];
+            if ((w[u][h] >> 16) != 0xFFFFu) d[2 * h + 1] = o[2 * h + 1];
+          }
+        }
+      }
+    }
+  }
+}
+
+// reduce over chunk-major xg: block per chunk (XCD-blocked as k_xtile_reduce).
+// Thread t loads its run [16t, 16t+16) of the chunk's val, xg and perm (all
+// contiguous), scatters xs[perm] = xg, and phase B / the run combine / the y
+// store are those of k_xtile_reduce.  Two round trips per chunk: the 16-B
+// descriptor, then every other load.  LDS: xs[M+M/16] T, hp[256] f64,
+// tp[256] f64, bm[M/32] u32, rpl[Rmax+1] i32 (static).
+template <typename T>
+__global__ __launch_bounds__(kXtBlock) void k_xtile_reduce_cm(
+    const int32_t *__restrict__ cdesc, int64_t C, int64_t Cx, const T *__restrict__ xg,
+    const uint16_t *__restrict__ perm, const T *__restrict__ val, const int32_t *__restrict__ rp,
+    T *__restrict__ y, double *__restrict__ carry) {
+  constexpr int MP = kXtM + kXtM / 16;
+  constexpr int RPT = (kXtRmax + 1 + kXtBlock - 1) / kXtBlock;
+  typedef T tvec __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
+  typedef uint16_t pvec __attribute__((ext_vector_type(8), aligned(2)));
+  constexpr int VW = 16 / sizeof(T), NV = kXtRun / VW;
+  __shared__ T xs[MP];
+  __shared__ double hp[kXtBlock], tp[kXtBlock];
+  __shared__ uint32_t bm[kXtM / 32];
+  __shared__ int32_t rpl[kXtRmax + 1];
+
+  const int tid = threadIdx.x;
+  const int i0 = tid * kXtRun;
+  const int64_t c = static_cast<int64_t>(blockIdx.x % 8) * Cx + blockIdx.x / 8;
+  if (c >= C) return;  // block-uniform
+  const u32x4 d = *reinterpret_cast<const u32x4 *>(cdesc + 4 * c);
+  const int e0 = static_cast<int>(d[0]), m = static_cast<int>(d[1]) - e0;
+  const int r0 = static_cast<int>(d[2]), R = static_cast<int>(d[3]) - r0;
+
+  // ---- round trip 2: val / xg / perm runs and row_ptr (unconditional loads;
+  //      the val, xg and perm allocations are padded by one run)
+  const int64_t rb = static_cast<int64_t>(e0) + (i0 < m ? i0 : 0);
+  tvec vv[NV], xv[NV];
+  pvec pv[kXtRun / 8];
+  {
+    const tvec *vp = reinterpret_cast<const tvec *>(val + rb);
+    const tvec *xp = reinterpret_cast<const tvec *>(xg + rb);
+    const pvec *pp = reinterpret_cast<const pvec *>(perm + rb);
+#pragma unroll
+    for (int q = 0; q < NV; ++q) vv[q] = __builtin_nontemporal_load(vp + q);
+#pragma unroll
+    for (int q = 0; q < NV; ++q) xv[q] = __builtin_nontemporal_load(xp + q);
+#pragma unroll
+    for (int q = 0; q < kXtRun / 8; ++q) pv[q] = pp[q];
+  }
+  int rv[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int j = q * kXtBlock + tid;
+    rv[q] = rp[r0 + (j <= R ? j : R)] - e0;
+  }
+  if (tid < kXtM / 32) bm[tid] = 0u;
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int j = q * kXtBlock + tid;
+    if (j <= R) rpl[j] = rv[q];
+  }
+  const int n = m - i0 < kXtRun ? (m - i0 > 0 ? m - i0 : 0) : kXtRun;  // valid entries in the run
+#pragma unroll
+  for (int j = 0; j < kXtRun; ++j)  // entries past m go to the spare slot MP−1 (never read)
+    xs[j < n ? xt_pidx(pv[j / 8][j % 8]) : MP - 1] = xv[j / VW][j % VW];
+  __syncthreads();  // bm zeroed before the ds_or below
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {  // row starts inside the chunk (empty rows share a bit)
+    const int j = q * kXtBlock + tid;
+    if (j < R && rv[q] < m) atomicOr(bm + (rv[q] >> 5), 1u << (rv[q] & 31));
+  }
+  __syncthreads();
+
+  // ---- phase B: branch-free segmented scan of the thread's run
+  const uint32_t mask = (bm[tid >> 1] >> ((tid & 1) * 16)) & 0xFFFFu;
+  const int hl = mask ? __builtin_ctz(mask) : kXtRun;
+  const int hend = (hl < n ? hl : n) - 1;
+  double acc = 0.0, hsave = 0.0;
+#pragma unroll
+  for (int j = 0; j < kXtRun; ++j) {
+    const double pr = static_cast<double>(vv[j / VW][j % VW]) * static_cast<double>(xs[17 * tid + j]);
+    const double pj = j < n ? pr : 0.0;
+    acc = ((mask >> j) & 1u) ? 0.0 : acc;
+    acc += pj;
+    hsave = j == hend ? acc : hsave;
+    xs[17 * tid + j] = static_cast<T>(acc);
+  }
+  const bool has_head = n > 0 && !(mask & 1u);
+  if (has_head) hp[tid] = hsave;
+  if (n > 0 && mask) tp[tid] = acc;
+  const bool cont = rpl[R] > m;
+  __syncthreads();
+  const int tlast = m > 0 ? (m - 1) / kXtRun : -1;
+  if (tid == 0 && !(m > 0 && rpl[0] > 0)) carry[2 * c] = 0.0;
+  if (has_head) {
+    const int i1 = i0 + n;
+    const bool end_i1 = i1 < m ? ((bm[i1 >> 5] >> (i1 & 31)) & 1u) != 0 : !cont;
+    const bool ends = hl < n || end_i1;
+    if (ends || tid == tlast) {
+      int u = tid - 1;
+      while (u >= 0 && ((bm[u >> 1] >> ((u & 1) * 16)) & 0xFFFFu) == 0u) --u;
+      double sum = u >= 0 ? tp[u] : 0.0;
+      for (int v = u + 1; v <= tid; ++v) sum += hp[v];
+      if (u < 0) {
+        carry[2 * c] = sum;
+      } else if (ends) {
+        xs[xt_pidx(i0 + hend)] = static_cast<T>(sum);
+      } else {
+        carry[2 * c + 1] = sum;
+      }
+    }
+  }
+  if (tid == tlast && mask && cont) carry[2 * c + 1] = tp[tid];
+  __syncthreads();
+  for (int j = tid; j < R; j += kXtBlock) {
+    const int a0 = rpl[j], a1 = rpl[j + 1];
+    if (a1 == a0) y[r0 + j] = T(0);
+    else if (a1 <= m) y[r0 + j] = xs[xt_pidx(a1 - 1)];
+  }
 }
 
 // ------------------------------------------------------------- host side
@@ -954,6 +1150,8 @@ struct lhpc_spmv_plan {
   int32_t *d_cdesc = nullptr;
   int32_t *d_ce = nullptr, *d_cr = nullptr, *d_segoff = nullptr, *d_pieces = nullptr, *d_cont = nullptr;
   uint16_t *d_col16 = nullptr, *d_perm = nullptr;
+  int xt_cm = 0;  // chunk-major xg (XtileHost::cm)
+  int32_t *d_gdst = nullptr;
   void *d_xg = nullptr;
   double *d_carry = nullptr;
 };
@@ -1140,8 +1338,8 @@ int launch_xslice(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s
 
 size_t xtile_lds_bytes(size_t tsz, int S) {
   return static_cast<size_t>(kXtM + kXtM / 16) * tsz + 2 * kXtBlock * sizeof(double) +
-         kXtM / 32 * sizeof(uint32_t) +
-         sizeof(int32_t) * (static_cast<size_t>(kXtRmax) + 1 + 2 * static_cast<size_t>(S) + 1 + 4);
+         2 * kXtM / 32 * sizeof(uint32_t) +
+         sizeof(int32_t) * (static_cast<size_t>(kXtRmax) + 1 + static_cast<size_t>(S) + 4);
 }
 
 int xtile_g(int S) {
@@ -1156,6 +1354,26 @@ template <typename T>
 int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
   if (p->n_rows == 0) return LHPC_OK;
   T *xg = static_cast<T *>(p->d_xg);
+  if (p->xt_cm) {
+    if (p->xt_pieces > 0) {
+      const dim3 g(static_cast<unsigned>(p->xt_pieces)), b(kXtGatherBlock);
+      if (p->xt_u == 1)
+        hipLaunchKernelGGL((k_xtile_gather_cm<T, 1>), g, b, 0, s, p->d_pieces, p->d_col16, p->d_gdst,
+                           static_cast<const T *>(x), p->n_cols, xg);
+      else if (p->xt_u == 2)
+        hipLaunchKernelGGL((k_xtile_gather_cm<T, 2>), g, b, 0, s, p->d_pieces, p->d_col16, p->d_gdst,
+                           static_cast<const T *>(x), p->n_cols, xg);
+      else
+        hipLaunchKernelGGL((k_xtile_gather_cm<T, 4>), g, b, 0, s, p->d_pieces, p->d_col16, p->d_gdst,
+                           static_cast<const T *>(x), p->n_cols, xg);
+      LHPC_TRY(check_launch(s));
+    }
+    const int64_t Cx = (p->xt_C + 7) / 8;
+    hipLaunchKernelGGL((k_xtile_reduce_cm<T>), dim3(static_cast<unsigned>(8 * Cx)), dim3(kXtBlock), 0, s,
+                       p->d_cdesc, p->xt_C, Cx, xg, p->d_perm, static_cast<const T *>(p->d_val),
+                       static_cast<const int32_t *>(p->d_row_ptr), static_cast<T *>(y), p->d_carry);
+    LHPC_TRY(check_launch(s));
+  } else {
   if (p->xt_pieces > 0) {
     const dim3 g(static_cast<unsigned>(p->xt_pieces)), b(kXtGatherBlock);
     if (p->xt_u == 2)
@@ -1181,6 +1399,7 @@ int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s)
   }
 #undef LHPC_XT_RED
   LHPC_TRY(check_launch(s));
+  }
   if (p->xt_cont > 0) {
     hipLaunchKernelGGL((k_xtile_fixup<T>), dim3(static_cast<unsigned>((p->xt_cont + kXtBlock - 1) / kXtBlock)),
                        dim3(kXtBlock), 0, s, p->d_cont, p->xt_cont, p->d_cr, p->xt_C, p->d_carry,
@@ -1248,7 +1467,13 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   int64_t piece = std::max<int64_t>(65536, p->nnz / (2 * static_cast<int64_t>(cus)) + 1);
   if (const char *env = std::getenv("LHPC_XTILE_PIECE")) piece = std::max<int64_t>(8, std::atoll(env));
   XtileHost xt;
-  const int bst = build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, kXtM, kXtRmax, piece, xt);
+  // LHPC_XTILE_LAYOUT=cm: chunk-major xg (opt-in: its scattered xg stores make
+  // the gather 2.5x slower on C2 than the reduce saves, DESIGN.md §4 XTILE)
+  int cm = 0;
+  if (const char *env = std::getenv("LHPC_XTILE_LAYOUT")) cm = std::strcmp(env, "cm") == 0;
+  p->xt_cm = cm;
+  const int bst = build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, kXtM, kXtRmax, piece,
+                              cm != 0, xt);
   if (bst != LHPC_OK) return bst;
   p->kernel = LHPC_KERNEL_XTILE;
   p->rp64 = 0;
@@ -1259,8 +1484,11 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   p->xt_cont = static_cast<int64_t>(xt.cont.size());
   p->xt_total = xt.total;
   p->xt_lds = xtile_lds_bytes(tsz, xt.S);
-  if (const char *env = std::getenv("LHPC_XTILE_U")) p->xt_u = std::atoi(env) == 2 ? 2 : 4;
-  {
+  if (const char *env = std::getenv("LHPC_XTILE_U")) {
+    const int u = std::atoi(env);
+    p->xt_u = u <= 1 && cm ? 1 : u == 2 ? 2 : 4;  // U = 1: chunk-major gather only
+  }
+  if (!cm) {
     const int g = xtile_g(xt.S);
     const void *kfn =
         tsz == 4 ? (g == 1 ? xtile_reduce_fn<float, 1>() : g == 2 ? xtile_reduce_fn<float, 2>()
@@ -1296,12 +1524,21 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   }
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_ce), xt.ce.data(), xt.ce.size() * 4));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cr), xt.cr.data(), xt.cr.size() * 4));
-  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_segoff), xt.segoff.data(), xt.segoff.size() * 4));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_pieces), xt.pieces.data(), xt.pieces.size() * 4));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cont), xt.cont.data(), xt.cont.size() * 4));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_col16), xt.col16.get(), static_cast<size_t>(xt.total) * 2));
-  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), xt.perm.get(), static_cast<size_t>(xt.total) * 2));
-  LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total) * tsz));
+  if (cm) {
+    // xg and perm are indexed by nonzero, padded by one reduce run (never stored, read masked)
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_gdst), xt.gdst.get(), static_cast<size_t>(xt.total / 8) * 4));
+    LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_perm), static_cast<size_t>(nnz + kXtRun) * 2, p->bytes));
+    LHPC_HIP_TRY(hipMemset(p->d_perm + nnz, 0, kXtRun * 2));
+    if (nnz) LHPC_HIP_TRY(hipMemcpy(p->d_perm, xt.perm.get(), static_cast<size_t>(nnz) * 2, hipMemcpyHostToDevice));
+    LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(nnz + kXtRun) * tsz));
+  } else {
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_segoff), xt.segoff.data(), xt.segoff.size() * 4));
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), xt.perm.get(), static_cast<size_t>(xt.total) * 2));
+    LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total) * tsz));
+  }
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_carry), nullptr, static_cast<size_t>(2 * C + 2) * 8));
   return LHPC_OK;
 }
@@ -1664,7 +1901,7 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
                   static_cast<void *>(p->d_cdesc), static_cast<void *>(p->d_ce), static_cast<void *>(p->d_cr), static_cast<void *>(p->d_segoff),
                   static_cast<void *>(p->d_pieces), static_cast<void *>(p->d_cont),
                   static_cast<void *>(p->d_col16), static_cast<void *>(p->d_perm), p->d_xg,
-                  static_cast<void *>(p->d_carry)})
+                  static_cast<void *>(p->d_carry), static_cast<void *>(p->d_gdst)})
     if (q) (void)hipFree(q);
   delete p;
   return LHPC_OK;

@@ -235,6 +235,13 @@ def _csr_from_lengths(lengths, n_cols, seed, dyadic):
     return rp, col, val
 
 
+@pytest.fixture(params=["seg", "cm"])
+def xt_layout(request, monkeypatch):
+    """Both XTILE layouts: tile-stream xg + segment table (default) and chunk-major xg."""
+    monkeypatch.setenv("LHPC_XTILE_LAYOUT", request.param)
+    return request.param
+
+
 def _check_xtile(lhpc, gpu, lengths, n_cols, dtype, seed, dyadic=True, expect_cont=None):
     rp, col, val = _csr_from_lengths(lengths, n_cols, seed, dyadic)
     val = val.astype(dtype)
@@ -256,7 +263,7 @@ def _check_xtile(lhpc, gpu, lengths, n_cols, dtype, seed, dyadic=True, expect_co
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_xtile_long_rows_across_chunks(lhpc, gpu, dtype):
+def test_xtile_long_rows_across_chunks(lhpc, gpu, dtype, xt_layout):
     """Rows longer than a chunk (4096 nonzeros) are cut by chunk ends and
     finished by the fix-up: a 30k-row, rows of 5000/4096/4095/9000 between
     short rows, a long first and a long last row."""
@@ -266,7 +273,7 @@ def test_xtile_long_rows_across_chunks(lhpc, gpu, dtype):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_xtile_empty_row_runs(lhpc, gpu, dtype):
+def test_xtile_empty_row_runs(lhpc, gpu, dtype, xt_layout):
     """More than Rmax (1024) consecutive empty rows, leading and trailing
     empty rows, and an all-empty tail after the last nonzero."""
     lengths = [0] * 3000 + [7] * 10 + [0] * 2500 + [1] + [0] * 1500 + [4096] + [0] * 2049
@@ -274,7 +281,7 @@ def test_xtile_empty_row_runs(lhpc, gpu, dtype):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_xtile_wide_many_tiles(lhpc, gpu, dtype):
+def test_xtile_wide_many_tiles(lhpc, gpu, dtype, xt_layout):
     """n_cols ≫ n_rows: hundreds of tiles, a ragged last tile, 1-nonzero rows."""
     rng = np.random.default_rng(0xA300)
     lengths = rng.integers(0, 40, size=5000)
@@ -282,7 +289,7 @@ def test_xtile_wide_many_tiles(lhpc, gpu, dtype):
     _check_xtile(lhpc, gpu, np.ones(70_000, dtype=np.int64), 3_000_017, dtype, 0xA302)
 
 
-def test_xtile_small_gather_pieces(lhpc, gpu, monkeypatch):
+def test_xtile_small_gather_pieces(lhpc, gpu, monkeypatch, xt_layout):
     """Several gather workgroups per tile (piece bounds inside a tile) give the same bits."""
     monkeypatch.setenv("LHPC_XTILE_PIECE", "1000")
     rng = np.random.default_rng(0xA400)

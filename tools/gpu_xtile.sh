@@ -12,9 +12,12 @@ step() { local name=$1 secs=$2; shift 2; echo "== $name $(date +%T)" >> "$O/prog
 for WL in ${WLS:-c2 c3 c4}; do
   step bench_$WL 600 python bench.py --workload $WL --no-cpu-baseline || exit 1
 done
-if [ "${AB:-1}" = 1 ]; then
-  LHPC_SPMV_XTILE=0 step bench_c2_xslice 600 python bench.py --workload c2 --no-cpu-baseline || exit 1
-fi
+# A/B variants: "name:K=V,K=V;..." (default: the tile-stream XTILE layout)
+IFS=';' read -ra VS <<< "${AB_VARIANTS-seg:LHPC_XTILE_LAYOUT=seg}"
+for V in "${VS[@]}"; do
+  name=${V%%:*}; kv=${V#*:}
+  env $(echo "$kv" | tr ',' ' ') timeout -k 10 300 python bench.py --workload c2 --no-cpu-baseline > "$O/bench_c2_$name.log" 2>&1 || exit 1
+done
 cd /tmp
 step prof_c2 600 rocprofv3 --kernel-trace --stats -d "$O/prof_c2" -o run -f csv -- python3 "$R/bench.py" --workload c2 --steps 10 --warmup 3 --no-cpu-baseline || exit 1
 exit 0
