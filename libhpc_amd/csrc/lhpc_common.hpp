@@ -101,6 +101,21 @@ __device__ __forceinline__ A group_sum(A v) {
   return v;
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave: DPP row_shr 1/2/4/8
+// inside each 16-lane row, then the row totals (three readlanes) are added
+// to the rows above them.  No LDS traffic.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  const int p1 = __builtin_amdgcn_readlane(v, 15);
+  const int p2 = p1 + __builtin_amdgcn_readlane(v, 31);
+  const int p3 = p2 + __builtin_amdgcn_readlane(v, 47);
+  const int row = static_cast<int>(__lane_id()) >> 4;
+  return v + (row == 0 ? 0 : row == 1 ? p1 : row == 2 ? p2 : p3);
+}
+
 template <typename T>
 __device__ __forceinline__ T ld_stream(const T *p) {
   return __builtin_nontemporal_load(p);

@@ -315,7 +315,7 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
         const int64_t s = col[k] / W;
         const int32_t g = cur[static_cast<size_t>(s)]++;
         o.col16[g] = static_cast<uint16_t>(col[k] - s * W);
-        o.perm[g] = static_cast<uint16_t>(k - e0);
+        o.perm[g] = static_cast<uint16_t>((k - e0) + ((k - e0) >> 4));  // reduce's LDS slot
       }
     }
   }

@@ -7,6 +7,8 @@
 
 #include <cstdint>
 
+#include "lhpc_common.hpp"
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -118,6 +120,30 @@ __global__ __launch_bounds__(256) void k_gather_sliced(const int32_t *__restrict
 }
 
 }  // namespace
+
+// Check of lhpc::wave_incl_scan (DPP) against a shuffle scan, per wave.
+__global__ __launch_bounds__(256) void k_wave_scan(const int *__restrict__ in, int *__restrict__ dpp,
+                                                   int *__restrict__ ref, int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int v = i < n ? in[i] : 0;
+  int r = v;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(r, d, 64);
+    if (lane >= d) r += t;
+  }
+  const int s = lhpc::wave_incl_scan(v);
+  if (i < n) {
+    dpp[i] = s;
+    ref[i] = r;
+  }
+}
+
+extern "C" int lhpc_probe_wave_scan(const int *in, int *dpp, int *ref, int64_t n, void *stream) {
+  hipLaunchKernelGGL(k_wave_scan, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), in, dpp, ref, n);
+  return static_cast<int>(hipGetLastError());
+}
 
 extern "C" int lhpc_probe_gather_sliced(const int32_t *idx, const float *table, float *out,
                                         int64_t n, int S, int64_t slice_len, int nt, void *stream) {

@@ -686,11 +686,12 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
 // conflict-free).  Dynamic LDS: xs[M+M/16] T, hp[256] f64, tp[256] f64,
 // bm[M/32] u32, sbm[M/32] u32, rpl[Rmax+1] i32, base_ne[S] i32, wsum[4] i32.
 __device__ __forceinline__ int xt_pidx(int i) { return i + (i >> 4); }
+static_assert(kXtRun == 16, "lhpc_plan.cpp build_xtile stores perm as the slot i + i/16");
 
 template <typename T, int G>
 __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
     const int32_t *__restrict__ cdesc, const int32_t *__restrict__ segoff, int S, int64_t C,
-    int64_t Cx, const T *__restrict__ xg, const uint16_t *__restrict__ perm,
+    int64_t Cx, int total, const T *__restrict__ xg, const uint16_t *__restrict__ perm,
     const T *__restrict__ val, const int32_t *__restrict__ rp, T *__restrict__ y,
     double *__restrict__ carry) {
   constexpr int MP = kXtM + kXtM / 16;
@@ -758,12 +759,7 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
     if (tid * G + q >= S) sb[q] = sa[q];
     lsum += (sb[q] - sa[q]) + (sb[q] > sa[q] ? 0x10000 : 0);
   }
-  int inc = lsum;
-#pragma unroll
-  for (int dd = 1; dd < kWave; dd <<= 1) {
-    const int t = __shfl_up(inc, dd, kWave);
-    if (lane >= dd) inc += t;
-  }
+  const int inc = wave_incl_scan(lsum);
   if (lane == kWave - 1) wsum[wv] = inc;
   __syncthreads();
   {
@@ -788,56 +784,56 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
   }
   __syncthreads();
 
-  // ---- phase A: src = base_ne[rank] + f, loads of xg/perm (round trip 3)
+  // ---- phase A: src = base_ne[rank] + f, loads of xg/perm (round trip 3);
+  //      positions past m load the sentinel entry `total` (perm: spare slot MP − 1)
   int src[NB];
   {
     const uint64_t wl = static_cast<uint64_t>(sbm[2 * lane]) | (static_cast<uint64_t>(sbm[2 * lane + 1]) << 32);
-    int incl = __popcll(wl);  // inclusive wave scan of the per-batch start counts
-#pragma unroll
-    for (int dd = 1; dd < kWave; dd <<= 1) {
-      const int t = __shfl_up(incl, dd, kWave);
-      if (lane >= dd) incl += t;
-    }
+    const int incl = wave_incl_scan(__popcll(wl));  // inclusive wave scan of the per-batch start counts
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
       const int q = wv * NB + u;  // batch: flat positions [64q, 64q+64)
+      // (readlane returns int: through uint32_t, or the low word would sign-extend)
       const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(wl), q);
       const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(wl >> 32), q);
-      const int rb = (q > 0 ? __builtin_amdgcn_readlane(incl, q - 1) : 0) - 1;
-      const int below = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0));
-      const int own = lane < 32 ? (lo >> lane) & 1 : (hi >> (lane - 32)) & 1;
+      const uint64_t w = static_cast<uint64_t>(lo) | (static_cast<uint64_t>(hi) << 32);
+      // rank = starts before the batch + starts at batch positions ≤ lane − 1
+      //      = base + (w & 1) + mbcnt(w >> 1)   (base, w: wave-uniform)
+      const int base = (q > 0 ? __builtin_amdgcn_readlane(incl, q - 1) : 0) - 1 + static_cast<int>(w & 1u);
+      const uint64_t w1 = w >> 1;
+      int rk = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(w1 >> 32),
+                                         __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(w1), base));
       const int f = q * kWave + lane;
-      int rk = rb + below + own;
-      rk = rk < 0 ? 0 : (rk < S ? rk : S - 1);  // clamped: the LDS read stays unconditional
-      const int sv = base_ne[rk] + f;
-      src[u] = f < m ? sv : -1;
+      const int sv = base_ne[rk] + f;  // m > 0 ⇒ 0 ≤ rk < S; m = 0: base_ne[−1] (in LDS), unused
+      src[u] = f < m ? sv : total;
     }
   }
   T xv[NB];
   uint16_t pv[NB];
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
-    const int sidx = src[u] >= 0 ? src[u] : 0;
-    xv[u] = xg[sidx];
-    pv[u] = perm[sidx];
+    xv[u] = xg[src[u]];
+    pv[u] = perm[src[u]];  // the LDS slot xt_pidx(position); the sentinel's is MP − 1
   }
 #pragma unroll
-  for (int u = 0; u < NB; ++u)  // positions past m go to the spare slot MP−1 (never read)
-    xs[src[u] >= 0 ? xt_pidx(pv[u]) : MP - 1] = xv[u];
+  for (int u = 0; u < NB; ++u) xs[pv[u]] = xv[u];
+  const int n = m - i0 < kXtRun ? (m - i0 > 0 ? m - i0 : 0) : kXtRun;  // valid entries in the run
+  if (n > 0 && n < kXtRun) {  // the chunk's last run: zero its slots past m (product 0 below)
+    for (int j = n; j < kXtRun; ++j) xs[17 * tid + j] = T(0);
+  }
   __syncthreads();
 
-  // ---- phase B: branch-free segmented scan of the thread's run
-  const int n = m - i0 < kXtRun ? (m - i0 > 0 ? m - i0 : 0) : kXtRun;  // valid entries in the run
+  // ---- phase B: branch-free segmented scan of the thread's run.  The fp32
+  //      product is exact in fp64, so the fma equals the add of the product.
   const uint32_t mask = (bm[tid >> 1] >> ((tid & 1) * 16)) & 0xFFFFu;
   const int hl = mask ? __builtin_ctz(mask) : kXtRun;  // head length (entries before the first start)
   const int hend = (hl < n ? hl : n) - 1;                // last head position (−1: none)
   double acc = 0.0, hsave = 0.0;
 #pragma unroll
   for (int j = 0; j < kXtRun; ++j) {
-    const double pr = static_cast<double>(vv[j / VW][j % VW]) * static_cast<double>(xs[17 * tid + j]);
-    const double pj = j < n ? pr : 0.0;
+    const T v = j < n ? vv[j / VW][j % VW] : T(0);  // past m: 0 · 0
     acc = ((mask >> j) & 1u) ? 0.0 : acc;
-    acc += pj;
+    acc = __builtin_fma(static_cast<double>(v), static_cast<double>(xs[17 * tid + j]), acc);
     hsave = j == hend ? acc : hsave;
     xs[17 * tid + j] = static_cast<T>(acc);  // in place; padding slots past m are never read
   }
@@ -1388,7 +1384,8 @@ int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s)
   const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(kXtBlock);
 #define LHPC_XT_RED(GG)                                                                              \
   hipLaunchKernelGGL((k_xtile_reduce<T, GG>), rg, rb, p->xt_lds, s, p->d_cdesc, p->d_segoff, p->S,  \
-                     p->xt_C, Cx, xg, p->d_perm, static_cast<const T *>(p->d_val),                    \
+                     p->xt_C, Cx, static_cast<int>(p->xt_total), xg, p->d_perm,                      \
+                     static_cast<const T *>(p->d_val),                                                \
                      static_cast<const int32_t *>(p->d_row_ptr), static_cast<T *>(y), p->d_carry)
   switch (xtile_g(p->S)) {
     case 1: LHPC_XT_RED(1); break;
@@ -1536,8 +1533,15 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
     LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(nnz + kXtRun) * tsz));
   } else {
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_segoff), xt.segoff.data(), xt.segoff.size() * 4));
-    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), xt.perm.get(), static_cast<size_t>(xt.total) * 2));
-    LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total) * tsz));
+    // one sentinel entry past the stream: reduce loads it for positions past m,
+    // and its perm is the spare LDS slot M + M/16 − 1
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), nullptr, static_cast<size_t>(xt.total + 1) * 2));
+    if (xt.total) LHPC_HIP_TRY(hipMemcpy(p->d_perm, xt.perm.get(), static_cast<size_t>(xt.total) * 2, hipMemcpyHostToDevice));
+    {
+      const uint16_t spare = static_cast<uint16_t>(kXtM + kXtM / 16 - 1);
+      LHPC_HIP_TRY(hipMemcpy(p->d_perm + xt.total, &spare, 2, hipMemcpyHostToDevice));
+    }
+    LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total + 1) * tsz));
   }
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_carry), nullptr, static_cast<size_t>(2 * C + 2) * 8));
   return LHPC_OK;

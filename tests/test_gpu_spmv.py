@@ -217,6 +217,28 @@ def test_golden_xslice_persistent(lhpc, gpu, path, monkeypatch):
 
 
 # ------------------------------------------------------------------ XTILE
+def test_wave_scan_dpp(lhpc, gpu):
+    """lhpc::wave_incl_scan (DPP row shifts + row_bcast, used by the XTILE
+    reduce) equals a shuffle scan in every wave."""
+    import ctypes as C
+    import torch
+    P = C.CDLL(os.path.join(os.path.dirname(lhpc.LIB_PATH), "liblhpc_probe.so"))
+    rng = np.random.default_rng(0xA0)
+    n = 256 * 37 + 5
+    a = torch.from_numpy(rng.integers(-1000, 1000, size=n).astype(np.int32)).to(gpu)
+    d = torch.empty_like(a)
+    r = torch.empty_like(a)
+    st = P.lhpc_probe_wave_scan(C.c_void_p(a.data_ptr()), C.c_void_p(d.data_ptr()),
+                                C.c_void_p(r.data_ptr()), C.c_int64(n),
+                                C.c_void_p(torch.cuda.current_stream(gpu).cuda_stream))
+    assert st == 0
+    torch.cuda.synchronize()
+    host = a.cpu().numpy().astype(np.int64)
+    exp = np.concatenate([np.cumsum(host[i:i + 64]) for i in range(0, n, 64)])
+    assert np.array_equal(r.cpu().numpy(), exp)
+    assert np.array_equal(d.cpu().numpy(), exp)
+
+
 def _csr_from_lengths(lengths, n_cols, seed, dyadic):
     """CSR with the given row lengths, distinct sorted uniform columns per row."""
     rng = np.random.default_rng(seed)
