@@ -44,8 +44,8 @@ int build_xslice(const void *row_ptr, int rp_bits, const int32_t *col, const voi
 //            x read is an LDS gather, every HBM access is a coalesced stream;
 //   reduce : a workgroup owns a chunk of ≤ M consecutive CSR nonzeros, reads
 //            the chunk's S segments of xg (one per tile) and scatters them
-//            into LDS at perm[g] (the LDS slot i + i/16 of the nonzero's
-//            position i in the chunk; cm: the position itself), then
+//            into LDS at perm[g] (the byte offset (i + i/16)·slot_bytes of
+//            the nonzero's position i in the chunk; cm: i itself), then
 //            multiplies by val (CSR order) and sums rows merge-path style.
 // The stream is ordered (tile, chunk, CSR position): segment (s, c) is
 // [segoff[c·S + s], segoff[(c+1)·S + s]).  Each tile's stream starts at a
@@ -88,7 +88,7 @@ struct XtileHost {
 // cm: the number of chunk ranges H is derived from it).
 int build_xtile(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_rows,
                 int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm,
-                XtileHost &out);
+                int slot_bytes, XtileHost &out);
 
 // in-slice length of row r in slice s
 inline int xs_len(const XsliceHost &o, int s, int64_t r) {

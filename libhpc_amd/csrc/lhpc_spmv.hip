@@ -686,7 +686,7 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
 // conflict-free).  Dynamic LDS: xs[M+M/16] T, hp[256] f64, tp[256] f64,
 // bm[M/32] u32, sbm[M/32] u32, rpl[Rmax+1] i32, base_ne[S] i32, wsum[4] i32.
 __device__ __forceinline__ int xt_pidx(int i) { return i + (i >> 4); }
-static_assert(kXtRun == 16, "lhpc_plan.cpp build_xtile stores perm as the slot i + i/16");
+static_assert(kXtRun == 16, "lhpc_plan.cpp build_xtile stores perm as the slot (i + i/16) · sizeof(T)");
 
 template <typename T, int G>
 __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
@@ -788,38 +788,44 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
   //      positions past m load the sentinel entry `total` (perm: spare slot MP − 1)
   int src[NB];
   {
+    // lane q holds batch q's word; its wave-uniform rank terms (w >> 1, base)
+    // go to an LDS triple that the owning wave reads back as a broadcast:
+    //   rank = starts before the batch − 1 + (w & 1) + mbcnt(w >> 1)
+    // (hp is phase-A scratch here; phase B writes it only after the barrier)
     const uint64_t wl = static_cast<uint64_t>(sbm[2 * lane]) | (static_cast<uint64_t>(sbm[2 * lane + 1]) << 32);
-    const int incl = wave_incl_scan(__popcll(wl));  // inclusive wave scan of the per-batch start counts
+    const int cnt = __popcll(wl);
+    const int incl = wave_incl_scan(cnt);
+    u32x4 *bt = reinterpret_cast<u32x4 *>(hp) + wv * NB;
+    if ((lane >> 4) == wv) {  // lanes [16 wv, 16 wv + 16): this wave's batches
+      const uint64_t w1 = wl >> 1;
+      bt[lane & (NB - 1)] = u32x4{static_cast<uint32_t>(w1), static_cast<uint32_t>(w1 >> 32),
+                                  static_cast<uint32_t>(incl - cnt - 1 + static_cast<int>(wl & 1u)), 0u};
+    }
+    __builtin_amdgcn_wave_barrier();  // LDS is in order within a wave: no block barrier needed
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      const int q = wv * NB + u;  // batch: flat positions [64q, 64q+64)
-      // (readlane returns int: through uint32_t, or the low word would sign-extend)
-      const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(wl), q);
-      const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(wl >> 32), q);
-      const uint64_t w = static_cast<uint64_t>(lo) | (static_cast<uint64_t>(hi) << 32);
-      // rank = starts before the batch + starts at batch positions ≤ lane − 1
-      //      = base + (w & 1) + mbcnt(w >> 1)   (base, w: wave-uniform)
-      const int base = (q > 0 ? __builtin_amdgcn_readlane(incl, q - 1) : 0) - 1 + static_cast<int>(w & 1u);
-      const uint64_t w1 = w >> 1;
-      int rk = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(w1 >> 32),
-                                         __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(w1), base));
-      const int f = q * kWave + lane;
+      const u32x4 t = bt[u];  // uniform address: broadcast
+      const int rk = __builtin_amdgcn_mbcnt_hi(t[1], __builtin_amdgcn_mbcnt_lo(t[0], t[2]));
+      const int f = (wv * NB + u) * kWave + lane;
       const int sv = base_ne[rk] + f;  // m > 0 ⇒ 0 ≤ rk < S; m = 0: base_ne[−1] (in LDS), unused
       src[u] = f < m ? sv : total;
     }
   }
+  static_assert(NB == 16 && kXtBlock / kWave * NB == kWave, "one batch word per lane, 16 per wave");
   T xv[NB];
   uint16_t pv[NB];
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
     xv[u] = xg[src[u]];
-    pv[u] = perm[src[u]];  // the LDS slot xt_pidx(position); the sentinel's is MP − 1
+    pv[u] = perm[src[u]];  // byte offset of the LDS slot xt_pidx(position); the sentinel's: MP − 1
   }
 #pragma unroll
-  for (int u = 0; u < NB; ++u) xs[pv[u]] = xv[u];
+  for (int u = 0; u < NB; ++u) *reinterpret_cast<T *>(reinterpret_cast<unsigned char *>(xs) + pv[u]) = xv[u];
   const int n = m - i0 < kXtRun ? (m - i0 > 0 ? m - i0 : 0) : kXtRun;  // valid entries in the run
-  if (n > 0 && n < kXtRun) {  // the chunk's last run: zero its slots past m (product 0 below)
+  if (n < kXtRun) {  // the chunk's last run (and runs past m): val and x past m → 0 · 0
     for (int j = n; j < kXtRun; ++j) xs[17 * tid + j] = T(0);
+#pragma unroll
+    for (int j = 0; j < kXtRun; ++j) vv[j / VW][j % VW] = j < n ? vv[j / VW][j % VW] : T(0);
   }
   __syncthreads();
 
@@ -831,9 +837,8 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
   double acc = 0.0, hsave = 0.0;
 #pragma unroll
   for (int j = 0; j < kXtRun; ++j) {
-    const T v = j < n ? vv[j / VW][j % VW] : T(0);  // past m: 0 · 0
     acc = ((mask >> j) & 1u) ? 0.0 : acc;
-    acc = __builtin_fma(static_cast<double>(v), static_cast<double>(xs[17 * tid + j]), acc);
+    acc = __builtin_fma(static_cast<double>(vv[j / VW][j % VW]), static_cast<double>(xs[17 * tid + j]), acc);
     hsave = j == hend ? acc : hsave;
     xs[17 * tid + j] = static_cast<T>(acc);  // in place; padding slots past m are never read
   }
@@ -1470,7 +1475,7 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   if (const char *env = std::getenv("LHPC_XTILE_LAYOUT")) cm = std::strcmp(env, "cm") == 0;
   p->xt_cm = cm;
   const int bst = build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, kXtM, kXtRmax, piece,
-                              cm != 0, xt);
+                              cm != 0, static_cast<int>(tsz), xt);
   if (bst != LHPC_OK) return bst;
   p->kernel = LHPC_KERNEL_XTILE;
   p->rp64 = 0;
@@ -1534,11 +1539,11 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   } else {
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_segoff), xt.segoff.data(), xt.segoff.size() * 4));
     // one sentinel entry past the stream: reduce loads it for positions past m,
-    // and its perm is the spare LDS slot M + M/16 − 1
+    // and its perm is the byte offset of the spare LDS slot M + M/16 − 1
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), nullptr, static_cast<size_t>(xt.total + 1) * 2));
     if (xt.total) LHPC_HIP_TRY(hipMemcpy(p->d_perm, xt.perm.get(), static_cast<size_t>(xt.total) * 2, hipMemcpyHostToDevice));
     {
-      const uint16_t spare = static_cast<uint16_t>(kXtM + kXtM / 16 - 1);
+      const uint16_t spare = static_cast<uint16_t>((kXtM + kXtM / 16 - 1) * tsz);
       LHPC_HIP_TRY(hipMemcpy(p->d_perm + xt.total, &spare, 2, hipMemcpyHostToDevice));
     }
     LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total + 1) * tsz));
