@@ -716,24 +716,12 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
   const int i0 = tid * kXtRun;
   const int64_t c = static_cast<int64_t>(blockIdx.x % 8) * Cx + blockIdx.x / 8;
   if (c >= C) return;  // block-uniform
-  const u32x4 d = *reinterpret_cast<const u32x4 *>(cdesc + 4 * c);
-  const int e0 = static_cast<int>(d[0]), m = static_cast<int>(d[1]) - e0;
-  const int r0 = static_cast<int>(d[2]), R = static_cast<int>(d[3]) - r0;
-
-  // ---- round trip 2: val run, row_ptr, segment table (unconditional loads)
-  tvec vv[NV];
-  {
-    // the val allocation is padded by one run, so a run may read past nnz
-    const tvec *vp = reinterpret_cast<const tvec *>(val + e0 + (i0 < m ? i0 : 0));
-#pragma unroll
-    for (int q = 0; q < NV; ++q) vv[q] = __builtin_nontemporal_load(vp + q);
-  }
-  int rv[RPT], sa[G], sb[G];
-#pragma unroll
-  for (int q = 0; q < RPT; ++q) {
-    const int j = q * kXtBlock + tid;
-    rv[q] = rp[r0 + (j <= R ? j : R)];
-  }
+  // ---- round trip 1: the chunk descriptor and the segment table (both
+  //      addressed by c alone), then — without waiting for them — round
+  //      trip 2 (val run and row_ptr, addressed by the descriptor).  The
+  //      segment scan and phase A need only the table, so phase A's xg/perm
+  //      loads go out while val and row_ptr are still in flight.
+  int sa[G], sb[G];
 #pragma unroll
   for (int q = 0; q < G; ++q) {
     const int sI = tid * G + q;
@@ -741,17 +729,26 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
     sa[q] = segoff[c * S + sc];
     sb[q] = segoff[(c + 1) * S + sc];
   }
-  // ---- scan: segment ranks / bases, segment-start and row-start bitmaps
+  const u32x4 d = *reinterpret_cast<const u32x4 *>(cdesc + 4 * c);
+  const int e0 = static_cast<int>(d[0]), m = static_cast<int>(d[1]) - e0;
+  const int r0 = static_cast<int>(d[2]), R = static_cast<int>(d[3]) - r0;
+  tvec vv[NV];
+  {
+    // the val allocation is padded by one run, so a run may read past nnz
+    const tvec *vp = reinterpret_cast<const tvec *>(val + e0 + (i0 < m ? i0 : 0));
 #pragma unroll
-  for (int q = 0; q < RPT; ++q) rv[q] -= e0;
-  if (tid < kXtM / 32) {
-    bm[tid] = 0u;
-    sbm[tid] = 0u;
+    for (int q = 0; q < NV; ++q) vv[q] = __builtin_nontemporal_load(vp + q);
   }
+  int rv[RPT];
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
     const int j = q * kXtBlock + tid;
-    if (j <= R) rpl[j] = rv[q];
+    rv[q] = rp[r0 + (j <= R ? j : R)];
+  }
+  // ---- scan: segment ranks / bases and the segment-start bitmap
+  if (tid < kXtM / 32) {
+    bm[tid] = 0u;
+    sbm[tid] = 0u;
   }
   int lsum = 0;  // (length | non-empty count << 16) of this thread's segments
 #pragma unroll
@@ -776,11 +773,6 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
       }
       off += len;
     }
-  }
-#pragma unroll
-  for (int q = 0; q < RPT; ++q) {  // row starts inside the chunk (empty rows share a bit)
-    const int j = q * kXtBlock + tid;
-    if (j < R && rv[q] < m) atomicOr(bm + (rv[q] >> 5), 1u << (rv[q] & 31));
   }
   __syncthreads();
 
@@ -821,6 +813,14 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
   }
 #pragma unroll
   for (int u = 0; u < NB; ++u) *reinterpret_cast<T *>(reinterpret_cast<unsigned char *>(xs) + pv[u]) = xv[u];
+  // row_ptr (round trip 2) → local row offsets and the row-start bitmap
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int j = q * kXtBlock + tid;
+    rv[q] -= e0;
+    if (j <= R) rpl[j] = rv[q];
+    if (j < R && rv[q] < m) atomicOr(bm + (rv[q] >> 5), 1u << (rv[q] & 31));  // empty rows share a bit
+  }
   const int n = m - i0 < kXtRun ? (m - i0 > 0 ? m - i0 : 0) : kXtRun;  // valid entries in the run
   if (n < kXtRun) {  // the chunk's last run (and runs past m): val and x past m → 0 · 0
     for (int j = n; j < kXtRun; ++j) xs[17 * tid + j] = T(0);
