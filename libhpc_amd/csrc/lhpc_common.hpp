@@ -116,6 +116,59 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v + (row == 0 ? 0 : row == 1 ? p1 : row == 2 ? p2 : p3);
 }
 
+// DPP move of an fp64 value (two dword moves); lanes without a source take `old`.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64_old(double old, double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v), o = __builtin_bit_cast(uint64_t, old);
+  const int lo = __builtin_amdgcn_update_dpp(static_cast<int>(o), static_cast<int>(u), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(static_cast<int>(o >> 32), static_cast<int>(u >> 32), CTRL, 0xF, 0xF,
+                                             false);
+  return __builtin_bit_cast(double, (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) |
+                                        static_cast<uint32_t>(lo));
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<int>(u), l);
+  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<int>(u >> 32), l);
+  return __builtin_bit_cast(double, (static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+// Segmented inclusive scan over the 64 lanes of a wave in fp64: a lane with
+// `f` starts a new segment with its own value, S(l) = f(l) ? v(l) : S(l−1) + v(l).
+// `f` returns whether some lane ≤ l starts a segment.  The association is a
+// fixed tree (DPP row_shr 1/2/4/8 inside 16-lane rows, then the row carries
+// in row order), so the result is deterministic.
+__device__ __forceinline__ double wave_seg_scan(double v, bool &f) {
+  int fl = f ? 1 : 0;
+#define LHPC_SEG_STEP(CTRL)                                                      \
+  {                                                                              \
+    const double vu = dpp_f64_old<CTRL>(0.0, v);                                 \
+    const int fu = __builtin_amdgcn_update_dpp(0, fl, CTRL, 0xF, 0xF, false);    \
+    v = fl ? v : vu + v;                                                         \
+    fl |= fu;                                                                    \
+  }
+  LHPC_SEG_STEP(0x111)  // row_shr:1
+  LHPC_SEG_STEP(0x112)  // row_shr:2
+  LHPC_SEG_STEP(0x114)  // row_shr:4
+  LHPC_SEG_STEP(0x118)  // row_shr:8
+#undef LHPC_SEG_STEP
+  const double v0 = readlane_f64(v, 15), v1 = readlane_f64(v, 31), v2 = readlane_f64(v, 47);
+  const int f0 = __builtin_amdgcn_readlane(fl, 15), f1 = __builtin_amdgcn_readlane(fl, 31),
+            f2 = __builtin_amdgcn_readlane(fl, 47);
+  const double c1 = v0, c2 = f1 ? v1 : c1 + v1, c3 = f2 ? v2 : c2 + v2;  // carries into rows 1..3
+  const int g1 = f0, g2 = g1 | f1, g3 = g2 | f2;
+  const int row = static_cast<int>(__lane_id()) >> 4;
+  const double cr = row == 1 ? c1 : row == 2 ? c2 : c3;
+  const int gr = row == 1 ? g1 : row == 2 ? g2 : g3;
+  if (row > 0) {
+    v = fl ? v : cr + v;
+    fl |= gr;
+  }
+  f = fl != 0;
+  return v;
+}
+
 template <typename T>
 __device__ __forceinline__ T ld_stream(const T *p) {
   return __builtin_nontemporal_load(p);

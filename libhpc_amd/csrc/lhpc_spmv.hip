@@ -685,29 +685,39 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
 // xs lives in LDS at pidx(i) = i + i/16 (thread t's run at [17t, 17t+16):
 // conflict-free).  Dynamic LDS: xs[M+M/16] T, hp[256] f64, tp[256] f64,
 // bm[M/32] u32, sbm[M/32] u32, rpl[Rmax+1] i32, base_ne[S] i32, wsum[4] i32.
+// reduce configurations: BLK threads, chunks of M = 16·BLK nonzeros owning
+// ≤ Rmax rows (fp32 uses BLK = 512; fp64 BLK = 256, whose 4096-entry chunk
+// already takes 44 KB of LDS)
+template <int BLK> struct XtRed {
+  static constexpr int M = BLK * kXtRun, Rmax = M / 8;
+};
+template <typename T> constexpr int xt_red_blk() { return sizeof(T) == 4 ? 512 : 256; }
 __device__ __forceinline__ int xt_pidx(int i) { return i + (i >> 4); }
 static_assert(kXtRun == 16, "lhpc_plan.cpp build_xtile stores perm as the slot (i + i/16) · sizeof(T)");
 
-template <typename T, int G>
-__global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
+template <typename T, int G, int BLK>
+__global__ __launch_bounds__(BLK) void k_xtile_reduce(
     const int32_t *__restrict__ cdesc, const int32_t *__restrict__ segoff, int S, int64_t C,
     int64_t Cx, int total, const T *__restrict__ xg, const uint16_t *__restrict__ perm,
     const T *__restrict__ val, const int32_t *__restrict__ rp, T *__restrict__ y,
     double *__restrict__ carry) {
-  constexpr int MP = kXtM + kXtM / 16;
-  constexpr int RPT = (kXtRmax + 1 + kXtBlock - 1) / kXtBlock;  // row_ptr loads per thread
-  constexpr int NB = kXtM / kXtBlock;                            // 64-position batches per wave
-  static_assert(kXtM / kWave == kWave, "one sbm word per lane");
+  constexpr int M = XtRed<BLK>::M, RMAX = XtRed<BLK>::Rmax;
+  constexpr int MP = M + M / 16;
+  constexpr int RPT = (RMAX + 1 + BLK - 1) / BLK;  // row_ptr loads per thread
+  constexpr int NB = M / BLK;                      // 64-position batches per wave (16)
+  constexpr int NWL = M / kWave / kWave;           // batch words per lane (1 or 2)
+  static_assert(NB == 16 && (NWL == 1 || NWL == 2), "16 batches per wave; ≤ 128 batches per chunk");
   typedef T tvec __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
   constexpr int VW = 16 / sizeof(T), NV = kXtRun / VW;
   extern __shared__ __align__(16) unsigned char smem[];
   T *xs = reinterpret_cast<T *>(smem);
   double *hp = reinterpret_cast<double *>(xs + MP);
-  double *tp = hp + kXtBlock;
-  uint32_t *bm = reinterpret_cast<uint32_t *>(tp + kXtBlock);
-  uint32_t *sbm = bm + kXtM / 32;
-  int32_t *rpl = reinterpret_cast<int32_t *>(sbm + kXtM / 32);
-  int32_t *base_ne = rpl + (kXtRmax + 1);
+  double *ws = hp + BLK;  // per-wave segmented-scan totals
+  int *wsf = reinterpret_cast<int *>(ws + BLK / kWave);
+  uint32_t *bm = reinterpret_cast<uint32_t *>(ws + 2 * (BLK / kWave));
+  uint32_t *sbm = bm + M / 32;
+  int32_t *rpl = reinterpret_cast<int32_t *>(sbm + M / 32);
+  int32_t *base_ne = rpl + (RMAX + 1);
   int32_t *wsum = base_ne + S;
 
   const int tid = threadIdx.x;
@@ -742,11 +752,11 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
   int rv[RPT];
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
-    const int j = q * kXtBlock + tid;
+    const int j = q * BLK + tid;
     rv[q] = rp[r0 + (j <= R ? j : R)];
   }
   // ---- scan: segment ranks / bases and the segment-start bitmap
-  if (tid < kXtM / 32) {
+  if (tid < M / 32) {
     bm[tid] = 0u;
     sbm[tid] = 0u;
   }
@@ -784,11 +794,20 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
     // go to an LDS triple that the owning wave reads back as a broadcast:
     //   rank = starts before the batch − 1 + (w & 1) + mbcnt(w >> 1)
     // (hp is phase-A scratch here; phase B writes it only after the barrier)
-    const uint64_t wl = static_cast<uint64_t>(sbm[2 * lane]) | (static_cast<uint64_t>(sbm[2 * lane + 1]) << 32);
-    const int cnt = __popcll(wl);
-    const int incl = wave_incl_scan(cnt);
+    // lane q holds batch words q (and q + 64 when M = 8192); wave w owns
+    // batches [16w, 16w + 16)
+    const int half = NWL == 2 ? wv >> 2 : 0;  // which 64-batch half this wave's batches are in
+    uint64_t wl = static_cast<uint64_t>(sbm[2 * lane]) | (static_cast<uint64_t>(sbm[2 * lane + 1]) << 32);
+    int cnt = __popcll(wl);
+    int incl = wave_incl_scan(cnt);
+    if (NWL == 2 && half) {
+      const int below = __builtin_amdgcn_readlane(incl, kWave - 1);  // starts in batches 0..63
+      wl = static_cast<uint64_t>(sbm[128 + 2 * lane]) | (static_cast<uint64_t>(sbm[128 + 2 * lane + 1]) << 32);
+      cnt = __popcll(wl);
+      incl = wave_incl_scan(cnt) + below;
+    }
     u32x4 *bt = reinterpret_cast<u32x4 *>(hp) + wv * NB;
-    if ((lane >> 4) == wv) {  // lanes [16 wv, 16 wv + 16): this wave's batches
+    if ((lane >> 4) == (wv & 3)) {  // lanes holding this wave's batches
       const uint64_t w1 = wl >> 1;
       bt[lane & (NB - 1)] = u32x4{static_cast<uint32_t>(w1), static_cast<uint32_t>(w1 >> 32),
                                   static_cast<uint32_t>(incl - cnt - 1 + static_cast<int>(wl & 1u)), 0u};
@@ -803,7 +822,6 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
       src[u] = f < m ? sv : total;
     }
   }
-  static_assert(NB == 16 && kXtBlock / kWave * NB == kWave, "one batch word per lane, 16 per wave");
   T xv[NB];
   uint16_t pv[NB];
 #pragma unroll
@@ -816,7 +834,7 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
   // row_ptr (round trip 2) → local row offsets and the row-start bitmap
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
-    const int j = q * kXtBlock + tid;
+    const int j = q * BLK + tid;
     rv[q] -= e0;
     if (j <= R) rpl[j] = rv[q];
     if (j < R && rv[q] < m) atomicOr(bm + (rv[q] >> 5), 1u << (rv[q] & 31));  // empty rows share a bit
@@ -843,11 +861,28 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
     xs[17 * tid + j] = static_cast<T>(acc);  // in place; padding slots past m are never read
   }
   const bool has_head = n > 0 && !(mask & 1u);
-  if (has_head) hp[tid] = hsave;
-  if (n > 0 && mask) tp[tid] = acc;
   const bool cont = rpl[R] > m;  // the row active at m−1 runs past the chunk
+  // ---- rows that cross runs: segmented scan over threads (run order) of
+  //      x(t) = tail piece if run t holds a row start, else its whole-run sum;
+  //      the row open when run t begins is the exclusive value S(t−1)
+  bool fl = n > 0 && mask != 0u;
+  double sv = wave_seg_scan(fl ? acc : hsave, fl);
+  if (lane == kWave - 1) {
+    ws[wv] = sv;
+    wsf[wv] = fl ? 1 : 0;
+  }
   __syncthreads();
-  // ---- combine rows that cross runs (fixed order: run order)
+  double cw = 0.0;  // segmented carry of the waves before this one
+  int gw = 0;
+  for (int w = 0; w < wv; ++w) {
+    cw = wsf[w] ? ws[w] : cw + ws[w];
+    gw |= wsf[w];
+  }
+  if (!fl) sv = cw + sv;
+  const int fin_incl = (fl ? 1 : 0) | gw;
+  constexpr int kShr1 = 0x138;  // DPP wave_shr:1 (lane l ← lane l−1; lane 0 keeps `old`)
+  const double oin = dpp_f64_old<kShr1>(cw, sv);                                 // S(t−1)
+  const int fin = __builtin_amdgcn_update_dpp(gw, fin_incl, kShr1, 0xF, 0xF, false);  // starts before run t
   const int tlast = m > 0 ? (m - 1) / kXtRun : -1;
   if (tid == 0 && !(m > 0 && rpl[0] > 0)) carry[2 * c] = 0.0;  // no head piece
   if (has_head) {
@@ -855,11 +890,8 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
     const bool end_i1 = i1 < m ? ((bm[i1 >> 5] >> (i1 & 31)) & 1u) != 0 : !cont;
     const bool ends = hl < n || end_i1;
     if (ends || tid == tlast) {
-      int u = tid - 1;  // thread where the row started (−1: before the chunk)
-      while (u >= 0 && ((bm[u >> 1] >> ((u & 1) * 16)) & 0xFFFFu) == 0u) --u;
-      double sum = u >= 0 ? tp[u] : 0.0;
-      for (int v = u + 1; v <= tid; ++v) sum += hp[v];
-      if (u < 0) {
+      const double sum = oin + hsave;
+      if (!fin) {
         carry[2 * c] = sum;  // this chunk's piece of the previous chunk's row
       } else if (ends) {
         xs[xt_pidx(i0 + hend)] = static_cast<T>(sum);
@@ -868,11 +900,11 @@ __global__ __launch_bounds__(kXtBlock) void k_xtile_reduce(
       }
     }
   }
-  if (tid == tlast && mask && cont) carry[2 * c + 1] = tp[tid];  // own tail row continues
+  if (tid == tlast && mask && cont) carry[2 * c + 1] = acc;  // own tail row continues
   __syncthreads();
   // coalesced y store of the owned rows from their last positions (a row
   // continuing past the chunk is stored by k_xtile_fixup, later on the stream)
-  for (int j = tid; j < R; j += kXtBlock) {
+  for (int j = tid; j < R; j += BLK) {
     const int a0 = rpl[j], a1 = rpl[j + 1];
     if (a1 == a0) y[r0 + j] = T(0);
     else if (a1 <= m) y[r0 + j] = xs[xt_pidx(a1 - 1)];
@@ -1337,19 +1369,22 @@ int launch_xslice(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s
   return check_launch(s);
 }
 
-size_t xtile_lds_bytes(size_t tsz, int S) {
-  return static_cast<size_t>(kXtM + kXtM / 16) * tsz + 2 * kXtBlock * sizeof(double) +
-         2 * kXtM / 32 * sizeof(uint32_t) +
-         sizeof(int32_t) * (static_cast<size_t>(kXtRmax) + 1 + static_cast<size_t>(S) + 4);
+template <typename T>
+size_t xtile_lds_bytes(int S) {
+  constexpr int BLK = xt_red_blk<T>(), M = XtRed<BLK>::M, RMAX = XtRed<BLK>::Rmax;
+  return static_cast<size_t>(M + M / 16) * sizeof(T) + (BLK + 2 * (BLK / kWave)) * sizeof(double) +
+         2 * M / 32 * sizeof(uint32_t) +
+         sizeof(int32_t) * (static_cast<size_t>(RMAX) + 1 + static_cast<size_t>(S) + 8);
 }
 
+template <typename T>
 int xtile_g(int S) {
-  const int g = (S + kXtBlock - 1) / kXtBlock;
+  const int g = (S + xt_red_blk<T>() - 1) / xt_red_blk<T>();
   return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : g <= 8 ? 8 : 16;
 }
 
 template <typename T, int G>
-const void *xtile_reduce_fn() { return reinterpret_cast<const void *>(k_xtile_reduce<T, G>); }
+const void *xtile_reduce_fn() { return reinterpret_cast<const void *>(k_xtile_reduce<T, G, xt_red_blk<T>()>); }
 
 template <typename T>
 int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
@@ -1386,13 +1421,14 @@ int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s)
     LHPC_TRY(check_launch(s));
   }
   const int64_t Cx = (p->xt_C + 7) / 8;
-  const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(kXtBlock);
+  constexpr int BLK = xt_red_blk<T>();
+  const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(BLK);
 #define LHPC_XT_RED(GG)                                                                              \
-  hipLaunchKernelGGL((k_xtile_reduce<T, GG>), rg, rb, p->xt_lds, s, p->d_cdesc, p->d_segoff, p->S,  \
+  hipLaunchKernelGGL((k_xtile_reduce<T, GG, BLK>), rg, rb, p->xt_lds, s, p->d_cdesc, p->d_segoff, p->S, \
                      p->xt_C, Cx, static_cast<int>(p->xt_total), xg, p->d_perm,                      \
                      static_cast<const T *>(p->d_val),                                                \
                      static_cast<const int32_t *>(p->d_row_ptr), static_cast<T *>(y), p->d_carry)
-  switch (xtile_g(p->S)) {
+  switch (xtile_g<T>(p->S)) {
     case 1: LHPC_XT_RED(1); break;
     case 2: LHPC_XT_RED(2); break;
     case 4: LHPC_XT_RED(4); break;
@@ -1474,7 +1510,10 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   int cm = 0;
   if (const char *env = std::getenv("LHPC_XTILE_LAYOUT")) cm = std::strcmp(env, "cm") == 0;
   p->xt_cm = cm;
-  const int bst = build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, kXtM, kXtRmax, piece,
+  // chunking: the seg reduce's M / Rmax for this type; the cm reduce's fixed 4096 / 512
+  const int cM = cm ? kXtM : (tsz == 4 ? XtRed<xt_red_blk<float>()>::M : XtRed<xt_red_blk<double>()>::M);
+  const int cR = cm ? kXtRmax : (tsz == 4 ? XtRed<xt_red_blk<float>()>::Rmax : XtRed<xt_red_blk<double>()>::Rmax);
+  const int bst = build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, cM, cR, piece,
                               cm != 0, static_cast<int>(tsz), xt);
   if (bst != LHPC_OK) return bst;
   p->kernel = LHPC_KERNEL_XTILE;
@@ -1485,13 +1524,13 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   p->xt_pieces = static_cast<int64_t>(xt.pieces.size() / 3);
   p->xt_cont = static_cast<int64_t>(xt.cont.size());
   p->xt_total = xt.total;
-  p->xt_lds = xtile_lds_bytes(tsz, xt.S);
+  p->xt_lds = tsz == 4 ? xtile_lds_bytes<float>(xt.S) : xtile_lds_bytes<double>(xt.S);
   if (const char *env = std::getenv("LHPC_XTILE_U")) {
     const int u = std::atoi(env);
     p->xt_u = u <= 1 && cm ? 1 : u == 2 ? 2 : 4;  // U = 1: chunk-major gather only
   }
   if (!cm) {
-    const int g = xtile_g(xt.S);
+    const int g = tsz == 4 ? xtile_g<float>(xt.S) : xtile_g<double>(xt.S);
     const void *kfn =
         tsz == 4 ? (g == 1 ? xtile_reduce_fn<float, 1>() : g == 2 ? xtile_reduce_fn<float, 2>()
                     : g == 4 ? xtile_reduce_fn<float, 4>() : g == 8 ? xtile_reduce_fn<float, 8>()
@@ -1543,7 +1582,7 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), nullptr, static_cast<size_t>(xt.total + 1) * 2));
     if (xt.total) LHPC_HIP_TRY(hipMemcpy(p->d_perm, xt.perm.get(), static_cast<size_t>(xt.total) * 2, hipMemcpyHostToDevice));
     {
-      const uint16_t spare = static_cast<uint16_t>((kXtM + kXtM / 16 - 1) * tsz);
+      const uint16_t spare = static_cast<uint16_t>((cM + cM / 16 - 1) * tsz);
       LHPC_HIP_TRY(hipMemcpy(p->d_perm + xt.total, &spare, 2, hipMemcpyHostToDevice));
     }
     LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total + 1) * tsz));
