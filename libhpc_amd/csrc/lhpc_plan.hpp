@@ -44,8 +44,8 @@ int build_xslice(const void *row_ptr, int rp_bits, const int32_t *col, const voi
 //            x read is an LDS gather, every HBM access is a coalesced stream;
 //   reduce : a workgroup owns a chunk of ≤ M consecutive CSR nonzeros, reads
 //            the chunk's S segments of xg (one per tile) and scatters them
-//            into LDS at perm[g] (the byte offset (i + i/16)·slot_bytes of
-//            the nonzero's position i in the chunk; cm: i itself), then
+//            into LDS at perm[g] (the byte offset xtile_slot(i)·slot_bytes
+//            of the nonzero's position i in the chunk; cm: i itself), then
 //            multiplies by val (CSR order) and sums rows merge-path style.
 // The stream is ordered (tile, chunk, CSR position): segment (s, c) is
 // [segoff[c·S + s], segoff[(c+1)·S + s]).  Each tile's stream starts at a
@@ -89,6 +89,15 @@ struct XtileHost {
 int build_xtile(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_rows,
                 int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm,
                 int slot_bytes, XtileHost &out);
+
+// LDS slot of chunk position i in the XTILE seg reduce (lhpc_spmv.hip
+// xt_slot): run t = i/16 holds 16 elements at 16·t, its 16-B slot q at
+// q ^ swz(t), swz = (t/4) % 4 for 4-B elements, (t/2) % 8 for 8-B ones.
+inline int xtile_slot(int i, int elem_bytes) {
+  const int vw = 16 / elem_bytes, t = i >> 4;
+  const int swz = elem_bytes == 4 ? (t >> 2) & 3 : (t >> 1) & 7;
+  return (i & ~15) | ((((i & 15) / vw) ^ swz) * vw) | (i & (vw - 1));
+}
 
 // in-slice length of row r in slice s
 inline int xs_len(const XsliceHost &o, int s, int64_t r) {

@@ -692,8 +692,19 @@ template <int BLK> struct XtRed {
   static constexpr int M = BLK * kXtRun, Rmax = M / 8;
 };
 template <typename T> constexpr int xt_red_blk() { return sizeof(T) == 4 ? 512 : 256; }
+// LDS slot of chunk position i for the seg reduce (lhpc_plan.hpp xtile_slot):
+// run t = i/16 occupies 16·t … 16·t+15 and its 16-B slot q is stored at
+// q ^ xt_swz(t), so the 16 lanes of a ds_read_b128 group hit 16 distinct
+// bank quads
+template <typename T> __device__ __forceinline__ int xt_swz(int t) {
+  return sizeof(T) == 4 ? (t >> 2) & 3 : (t >> 1) & 7;
+}
+template <typename T> __device__ __forceinline__ int xt_slot(int i) {
+  constexpr int VW = 16 / sizeof(T);
+  return (i & ~15) | ((((i & 15) / VW) ^ xt_swz<T>(i >> 4)) * VW) | (i & (VW - 1));
+}
 __device__ __forceinline__ int xt_pidx(int i) { return i + (i >> 4); }
-static_assert(kXtRun == 16, "lhpc_plan.cpp build_xtile stores perm as the slot (i + i/16) · sizeof(T)");
+static_assert(kXtRun == 16, "lhpc_plan.hpp xtile_slot (host perm) assumes 16-element runs");
 
 template <typename T, int G, int BLK>
 __global__ __launch_bounds__(BLK) void k_xtile_reduce(
@@ -702,22 +713,25 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
     const T *__restrict__ val, const int32_t *__restrict__ rp, T *__restrict__ y,
     double *__restrict__ carry) {
   constexpr int M = XtRed<BLK>::M, RMAX = XtRed<BLK>::Rmax;
-  constexpr int MP = M + M / 16;
   constexpr int RPT = (RMAX + 1 + BLK - 1) / BLK;  // row_ptr loads per thread
   constexpr int NB = M / BLK;                      // 64-position batches per wave (16)
   constexpr int NWL = M / kWave / kWave;           // batch words per lane (1 or 2)
   static_assert(NB == 16 && (NWL == 1 || NWL == 2), "16 batches per wave; ≤ 128 batches per chunk");
   typedef T tvec __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
   constexpr int VW = 16 / sizeof(T), NV = kXtRun / VW;
+  // dynamic LDS (xtile_lds_bytes): xs[M + VW] T (xt_slot layout; slot M is
+  // the sentinel's spare), bt[BLK/64][16] u32x4, ws[BLK/64] f64,
+  // wsf[BLK/64] i32, bm[M/32] u32, sbm[M/32] u32, rpl[RMAX+1] u16 (padded to
+  // 4 B), base_ne[S] i32, wsum[8] i32
   extern __shared__ __align__(16) unsigned char smem[];
   T *xs = reinterpret_cast<T *>(smem);
-  double *hp = reinterpret_cast<double *>(xs + MP);
-  double *ws = hp + BLK;  // per-wave segmented-scan totals
+  u32x4 *bt0 = reinterpret_cast<u32x4 *>(xs + M + VW);
+  double *ws = reinterpret_cast<double *>(bt0 + (BLK / kWave) * NB);  // per-wave segmented-scan totals
   int *wsf = reinterpret_cast<int *>(ws + BLK / kWave);
-  uint32_t *bm = reinterpret_cast<uint32_t *>(ws + 2 * (BLK / kWave));
+  uint32_t *bm = reinterpret_cast<uint32_t *>(wsf + BLK / kWave);
   uint32_t *sbm = bm + M / 32;
-  int32_t *rpl = reinterpret_cast<int32_t *>(sbm + M / 32);
-  int32_t *base_ne = rpl + (RMAX + 1);
+  uint16_t *rpl = reinterpret_cast<uint16_t *>(sbm + M / 32);
+  int32_t *base_ne = reinterpret_cast<int32_t *>(rpl + ((RMAX + 2) & ~1));
   int32_t *wsum = base_ne + S;
 
   const int tid = threadIdx.x;
@@ -787,13 +801,12 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   __syncthreads();
 
   // ---- phase A: src = base_ne[rank] + f, loads of xg/perm (round trip 3);
-  //      positions past m load the sentinel entry `total` (perm: spare slot MP − 1)
+  //      positions past m load the sentinel entry `total` (perm: spare slot M)
   int src[NB];
   {
     // lane q holds batch q's word; its wave-uniform rank terms (w >> 1, base)
     // go to an LDS triple that the owning wave reads back as a broadcast:
     //   rank = starts before the batch − 1 + (w & 1) + mbcnt(w >> 1)
-    // (hp is phase-A scratch here; phase B writes it only after the barrier)
     // lane q holds batch words q (and q + 64 when M = 8192); wave w owns
     // batches [16w, 16w + 16)
     const int half = NWL == 2 ? wv >> 2 : 0;  // which 64-batch half this wave's batches are in
@@ -806,7 +819,7 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
       cnt = __popcll(wl);
       incl = wave_incl_scan(cnt) + below;
     }
-    u32x4 *bt = reinterpret_cast<u32x4 *>(hp) + wv * NB;
+    u32x4 *bt = bt0 + wv * NB;
     if ((lane >> 4) == (wv & 3)) {  // lanes holding this wave's batches
       const uint64_t w1 = wl >> 1;
       bt[lane & (NB - 1)] = u32x4{static_cast<uint32_t>(w1), static_cast<uint32_t>(w1 >> 32),
@@ -827,7 +840,7 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
     xv[u] = xg[src[u]];
-    pv[u] = perm[src[u]];  // byte offset of the LDS slot xt_pidx(position); the sentinel's: MP − 1
+    pv[u] = perm[src[u]];  // byte offset of the LDS slot xt_slot(position); the sentinel's: M
   }
 #pragma unroll
   for (int u = 0; u < NB; ++u) *reinterpret_cast<T *>(reinterpret_cast<unsigned char *>(xs) + pv[u]) = xv[u];
@@ -836,12 +849,12 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   for (int q = 0; q < RPT; ++q) {
     const int j = q * BLK + tid;
     rv[q] -= e0;
-    if (j <= R) rpl[j] = rv[q];
+    if (j <= R) rpl[j] = static_cast<uint16_t>(rv[q] <= m ? rv[q] : m + 1);  // > m: continues
     if (j < R && rv[q] < m) atomicOr(bm + (rv[q] >> 5), 1u << (rv[q] & 31));  // empty rows share a bit
   }
   const int n = m - i0 < kXtRun ? (m - i0 > 0 ? m - i0 : 0) : kXtRun;  // valid entries in the run
   if (n < kXtRun) {  // the chunk's last run (and runs past m): val and x past m → 0 · 0
-    for (int j = n; j < kXtRun; ++j) xs[17 * tid + j] = T(0);
+    for (int j = n; j < kXtRun; ++j) xs[xt_slot<T>(i0 + j)] = T(0);
 #pragma unroll
     for (int j = 0; j < kXtRun; ++j) vv[j / VW][j % VW] = j < n ? vv[j / VW][j % VW] : T(0);
   }
@@ -852,14 +865,23 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   const uint32_t mask = (bm[tid >> 1] >> ((tid & 1) * 16)) & 0xFFFFu;
   const int hl = mask ? __builtin_ctz(mask) : kXtRun;  // head length (entries before the first start)
   const int hend = (hl < n ? hl : n) - 1;                // last head position (−1: none)
+  // the run is NV 16-B slots at 16·tid, slot q stored at q ^ xt_swz (conflict-free ds_read_b128)
+  typedef T lvec __attribute__((ext_vector_type(VW)));
+  lvec *xr = reinterpret_cast<lvec *>(xs + i0);
+  const int swz = xt_swz<T>(tid);
+  lvec xq[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) xq[q] = xr[q ^ swz];
   double acc = 0.0, hsave = 0.0;
 #pragma unroll
   for (int j = 0; j < kXtRun; ++j) {
     acc = ((mask >> j) & 1u) ? 0.0 : acc;
-    acc = __builtin_fma(static_cast<double>(vv[j / VW][j % VW]), static_cast<double>(xs[17 * tid + j]), acc);
+    acc = __builtin_fma(static_cast<double>(vv[j / VW][j % VW]), static_cast<double>(xq[j / VW][j % VW]), acc);
     hsave = j == hend ? acc : hsave;
-    xs[17 * tid + j] = static_cast<T>(acc);  // in place; padding slots past m are never read
+    xq[j / VW][j % VW] = static_cast<T>(acc);  // in place; slots past m are never read
   }
+#pragma unroll
+  for (int q = 0; q < NV; ++q) xr[q ^ swz] = xq[q];
   const bool has_head = n > 0 && !(mask & 1u);
   const bool cont = rpl[R] > m;  // the row active at m−1 runs past the chunk
   // ---- rows that cross runs: segmented scan over threads (run order) of
@@ -894,7 +916,7 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
       if (!fin) {
         carry[2 * c] = sum;  // this chunk's piece of the previous chunk's row
       } else if (ends) {
-        xs[xt_pidx(i0 + hend)] = static_cast<T>(sum);
+        xs[xt_slot<T>(i0 + hend)] = static_cast<T>(sum);
       } else {
         carry[2 * c + 1] = sum;  // row continues into the next chunk
       }
@@ -907,7 +929,7 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   for (int j = tid; j < R; j += BLK) {
     const int a0 = rpl[j], a1 = rpl[j + 1];
     if (a1 == a0) y[r0 + j] = T(0);
-    else if (a1 <= m) y[r0 + j] = xs[xt_pidx(a1 - 1)];
+    else if (a1 <= m) y[r0 + j] = xs[xt_slot<T>(a1 - 1)];
   }
 }
 
@@ -1371,10 +1393,10 @@ int launch_xslice(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s
 
 template <typename T>
 size_t xtile_lds_bytes(int S) {
-  constexpr int BLK = xt_red_blk<T>(), M = XtRed<BLK>::M, RMAX = XtRed<BLK>::Rmax;
-  return static_cast<size_t>(M + M / 16) * sizeof(T) + (BLK + 2 * (BLK / kWave)) * sizeof(double) +
-         2 * M / 32 * sizeof(uint32_t) +
-         sizeof(int32_t) * (static_cast<size_t>(RMAX) + 1 + static_cast<size_t>(S) + 8);
+  constexpr int BLK = xt_red_blk<T>(), M = XtRed<BLK>::M, RMAX = XtRed<BLK>::Rmax, W = BLK / kWave;
+  return static_cast<size_t>(M + 16 / sizeof(T)) * sizeof(T) + W * 16 * 16 + W * (sizeof(double) + 4) +
+         2 * M / 32 * sizeof(uint32_t) + ((RMAX + 2) & ~1) * sizeof(uint16_t) +
+         sizeof(int32_t) * (static_cast<size_t>(S) + 8);
 }
 
 template <typename T>
@@ -1582,7 +1604,7 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), nullptr, static_cast<size_t>(xt.total + 1) * 2));
     if (xt.total) LHPC_HIP_TRY(hipMemcpy(p->d_perm, xt.perm.get(), static_cast<size_t>(xt.total) * 2, hipMemcpyHostToDevice));
     {
-      const uint16_t spare = static_cast<uint16_t>((cM + cM / 16 - 1) * tsz);
+      const uint16_t spare = static_cast<uint16_t>(cM * tsz);  // slot M: one 16-B slot past the chunk
       LHPC_HIP_TRY(hipMemcpy(p->d_perm + xt.total, &spare, 2, hipMemcpyHostToDevice));
     }
     LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total + 1) * tsz));
