@@ -213,7 +213,7 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
                 int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm, int slot_bytes, XtileHost &o) {
   const int64_t nnz = rp_at(rp, bits, n_rows) - rp_at(rp, bits, 0);
   if (W < 8 || M < 64 || M > 65536 || M % 16 || Rmax < 1 || (slot_bytes != 4 && slot_bytes != 8) ||
-      static_cast<int64_t>(M) * slot_bytes >= 65536)
+      M >= 65536)
     return LHPC_ERR_INVALID_ARG;
   const int64_t S = n_cols > 0 ? (n_cols + W - 1) / W : 1;
   if (S > 4096 || nnz + 8 * S >= INT32_MAX || n_rows >= INT32_MAX) return LHPC_ERR_UNSUPPORTED;
@@ -317,7 +317,7 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
         const int64_t s = col[k] / W;
         const int32_t g = cur[static_cast<size_t>(s)]++;
         o.col16[g] = static_cast<uint16_t>(col[k] - s * W);
-        o.perm[g] = static_cast<uint16_t>(xtile_slot(static_cast<int>(k - e0), slot_bytes) * slot_bytes);
+        o.perm[g] = static_cast<uint16_t>(xtile_slot(static_cast<int>(k - e0), slot_bytes));
       }
     }
   }

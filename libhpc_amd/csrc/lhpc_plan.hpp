@@ -44,8 +44,8 @@ int build_xslice(const void *row_ptr, int rp_bits, const int32_t *col, const voi
 //            x read is an LDS gather, every HBM access is a coalesced stream;
 //   reduce : a workgroup owns a chunk of ≤ M consecutive CSR nonzeros, reads
 //            the chunk's S segments of xg (one per tile) and scatters them
-//            into LDS at perm[g] (the byte offset xtile_slot(i)·slot_bytes
-//            of the nonzero's position i in the chunk; cm: i itself), then
+//            into LDS at perm[g] (the slot xtile_slot(i) of the nonzero's
+//            position i in the chunk; cm: i itself), then
 //            multiplies by val (CSR order) and sums rows merge-path style.
 // The stream is ordered (tile, chunk, CSR position): segment (s, c) is
 // [segoff[c·S + s], segoff[(c+1)·S + s]).  Each tile's stream starts at a

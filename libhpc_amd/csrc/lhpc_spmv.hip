@@ -685,13 +685,16 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
 // xs lives in LDS at pidx(i) = i + i/16 (thread t's run at [17t, 17t+16):
 // conflict-free).  Dynamic LDS: xs[M+M/16] T, hp[256] f64, tp[256] f64,
 // bm[M/32] u32, sbm[M/32] u32, rpl[Rmax+1] i32, base_ne[S] i32, wsum[4] i32.
+#ifndef LHPC_XT_RBLK32
+#define LHPC_XT_RBLK32 512
+#endif
 // reduce configurations: BLK threads, chunks of M = 16·BLK nonzeros owning
 // ≤ Rmax rows (fp32 uses BLK = 512; fp64 BLK = 256, whose 4096-entry chunk
 // already takes 44 KB of LDS)
 template <int BLK> struct XtRed {
   static constexpr int M = BLK * kXtRun, Rmax = M / 8;
 };
-template <typename T> constexpr int xt_red_blk() { return sizeof(T) == 4 ? 512 : 256; }
+template <typename T> constexpr int xt_red_blk() { return sizeof(T) == 4 ? LHPC_XT_RBLK32 : 256; }
 // LDS slot of chunk position i for the seg reduce (lhpc_plan.hpp xtile_slot):
 // run t = i/16 occupies 16·t … 16·t+15 and its 16-B slot q is stored at
 // q ^ xt_swz(t), so the 16 lanes of a ds_read_b128 group hit 16 distinct
@@ -708,15 +711,15 @@ static_assert(kXtRun == 16, "lhpc_plan.hpp xtile_slot (host perm) assumes 16-ele
 
 template <typename T, int G, int BLK>
 __global__ __launch_bounds__(BLK) void k_xtile_reduce(
-    const int32_t *__restrict__ cdesc, const int32_t *__restrict__ segoff, int S, int64_t C,
+    const int32_t *__restrict__ cdesc, const int32_t *__restrict__ segoff, int S, int64_t c0, int64_t C,
     int64_t Cx, int total, const T *__restrict__ xg, const uint16_t *__restrict__ perm,
     const T *__restrict__ val, const int32_t *__restrict__ rp, T *__restrict__ y,
     double *__restrict__ carry) {
   constexpr int M = XtRed<BLK>::M, RMAX = XtRed<BLK>::Rmax;
   constexpr int RPT = (RMAX + 1 + BLK - 1) / BLK;  // row_ptr loads per thread
   constexpr int NB = M / BLK;                      // 64-position batches per wave (16)
-  constexpr int NWL = M / kWave / kWave;           // batch words per lane (1 or 2)
-  static_assert(NB == 16 && (NWL == 1 || NWL == 2), "16 batches per wave; ≤ 128 batches per chunk");
+  constexpr int NWL = M / kWave / kWave;           // batch words per lane (1, 2 or 4)
+  static_assert(NB == 16 && (NWL == 1 || NWL == 2 || NWL == 4), "16 batches per wave; ≤ 256 batches per chunk");
   typedef T tvec __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
   constexpr int VW = 16 / sizeof(T), NV = kXtRun / VW;
   // dynamic LDS (xtile_lds_bytes): xs[M + VW] T (xt_slot layout; slot M is
@@ -738,7 +741,7 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   const int lane = tid & (kWave - 1);
   const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int i0 = tid * kXtRun;
-  const int64_t c = static_cast<int64_t>(blockIdx.x % 8) * Cx + blockIdx.x / 8;
+  const int64_t c = c0 + static_cast<int64_t>(blockIdx.x % 8) * Cx + blockIdx.x / 8;  // chunk range [c0, C)
   if (c >= C) return;  // block-uniform
   // ---- round trip 1: the chunk descriptor and the segment table (both
   //      addressed by c alone), then — without waiting for them — round
@@ -809,15 +812,14 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
     //   rank = starts before the batch − 1 + (w & 1) + mbcnt(w >> 1)
     // lane q holds batch words q (and q + 64 when M = 8192); wave w owns
     // batches [16w, 16w + 16)
-    const int half = NWL == 2 ? wv >> 2 : 0;  // which 64-batch half this wave's batches are in
-    uint64_t wl = static_cast<uint64_t>(sbm[2 * lane]) | (static_cast<uint64_t>(sbm[2 * lane + 1]) << 32);
-    int cnt = __popcll(wl);
-    int incl = wave_incl_scan(cnt);
-    if (NWL == 2 && half) {
-      const int below = __builtin_amdgcn_readlane(incl, kWave - 1);  // starts in batches 0..63
-      wl = static_cast<uint64_t>(sbm[128 + 2 * lane]) | (static_cast<uint64_t>(sbm[128 + 2 * lane + 1]) << 32);
+    const int grp = wv >> 2;  // this wave's batches lie in 64-batch group grp (< NWL)
+    uint64_t wl = 0;
+    int cnt = 0, incl = 0, below = 0;
+    for (int g2 = 0; g2 <= grp; ++g2) {  // wave-uniform
+      wl = static_cast<uint64_t>(sbm[128 * g2 + 2 * lane]) | (static_cast<uint64_t>(sbm[128 * g2 + 2 * lane + 1]) << 32);
       cnt = __popcll(wl);
-      incl = wave_incl_scan(cnt) + below;
+      incl = wave_incl_scan(cnt) + below;  // starts in batches ≤ 64·g2 + lane
+      below = __builtin_amdgcn_readlane(incl, kWave - 1);
     }
     u32x4 *bt = bt0 + wv * NB;
     if ((lane >> 4) == (wv & 3)) {  // lanes holding this wave's batches
@@ -840,10 +842,10 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
     xv[u] = xg[src[u]];
-    pv[u] = perm[src[u]];  // byte offset of the LDS slot xt_slot(position); the sentinel's: M
+    pv[u] = perm[src[u]];  // LDS slot xt_slot(position); the sentinel's: M
   }
 #pragma unroll
-  for (int u = 0; u < NB; ++u) *reinterpret_cast<T *>(reinterpret_cast<unsigned char *>(xs) + pv[u]) = xv[u];
+  for (int u = 0; u < NB; ++u) xs[pv[u]] = xv[u];
   // row_ptr (round trip 2) → local row offsets and the row-start bitmap
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
@@ -1202,6 +1204,15 @@ struct lhpc_spmv_plan {
   int64_t xt_C = 0, xt_pieces = 0, xt_cont = 0, xt_total = 0;
   size_t xt_lds = 0;
   int xt_u = 4;
+  // pipelined seg calls: K chunk ranges; range k's gather runs on the caller's
+  // stream, its reduce on xt_s2 once the gather's event fires, so range k's
+  // reduce overlaps range k+1's gather
+  int xt_K = 1;
+  std::vector<int64_t> xt_rc;           // [K+1] chunk bounds
+  std::vector<int64_t> xt_rpo;          // [K+1] offsets (in pieces) of each range's gather pieces
+  int32_t *d_rpieces = nullptr;
+  hipStream_t xt_s2 = nullptr;
+  std::vector<hipEvent_t> xt_ev;        // [K+1]
   int32_t *d_cdesc = nullptr;
   int32_t *d_ce = nullptr, *d_cr = nullptr, *d_segoff = nullptr, *d_pieces = nullptr, *d_cont = nullptr;
   uint16_t *d_col16 = nullptr, *d_perm = nullptr;
@@ -1432,33 +1443,50 @@ int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s)
                        static_cast<const int32_t *>(p->d_row_ptr), static_cast<T *>(y), p->d_carry);
     LHPC_TRY(check_launch(s));
   } else {
-  if (p->xt_pieces > 0) {
-    const dim3 g(static_cast<unsigned>(p->xt_pieces)), b(kXtGatherBlock);
+  auto gather = [&](const int32_t *pieces, int64_t n) -> int {
+    if (n <= 0) return LHPC_OK;
+    const dim3 g(static_cast<unsigned>(n)), b(kXtGatherBlock);
     if (p->xt_u == 2)
-      hipLaunchKernelGGL((k_xtile_gather<T, 2>), g, b, 0, s, p->d_pieces, p->d_col16,
+      hipLaunchKernelGGL((k_xtile_gather<T, 2>), g, b, 0, s, pieces, p->d_col16,
                          static_cast<const T *>(x), p->n_cols, xg);
     else
-      hipLaunchKernelGGL((k_xtile_gather<T, 4>), g, b, 0, s, p->d_pieces, p->d_col16,
+      hipLaunchKernelGGL((k_xtile_gather<T, 4>), g, b, 0, s, pieces, p->d_col16,
                          static_cast<const T *>(x), p->n_cols, xg);
-    LHPC_TRY(check_launch(s));
-  }
-  const int64_t Cx = (p->xt_C + 7) / 8;
-  constexpr int BLK = xt_red_blk<T>();
-  const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(BLK);
-#define LHPC_XT_RED(GG)                                                                              \
-  hipLaunchKernelGGL((k_xtile_reduce<T, GG, BLK>), rg, rb, p->xt_lds, s, p->d_cdesc, p->d_segoff, p->S, \
-                     p->xt_C, Cx, static_cast<int>(p->xt_total), xg, p->d_perm,                      \
-                     static_cast<const T *>(p->d_val),                                                \
+    return check_launch(s);
+  };
+  auto reduce = [&](int64_t c0, int64_t c1, hipStream_t rs) -> int {
+    if (c1 <= c0) return LHPC_OK;
+    const int64_t Cx = (c1 - c0 + 7) / 8;
+    constexpr int BLK = xt_red_blk<T>();
+    const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(BLK);
+#define LHPC_XT_RED(GG)                                                                               \
+  hipLaunchKernelGGL((k_xtile_reduce<T, GG, BLK>), rg, rb, p->xt_lds, rs, p->d_cdesc, p->d_segoff, p->S, \
+                     c0, c1, Cx, static_cast<int>(p->xt_total), xg, p->d_perm,                         \
+                     static_cast<const T *>(p->d_val),                                                 \
                      static_cast<const int32_t *>(p->d_row_ptr), static_cast<T *>(y), p->d_carry)
-  switch (xtile_g<T>(p->S)) {
-    case 1: LHPC_XT_RED(1); break;
-    case 2: LHPC_XT_RED(2); break;
-    case 4: LHPC_XT_RED(4); break;
-    case 8: LHPC_XT_RED(8); break;
-    default: LHPC_XT_RED(16); break;
-  }
+    switch (xtile_g<T>(p->S)) {
+      case 1: LHPC_XT_RED(1); break;
+      case 2: LHPC_XT_RED(2); break;
+      case 4: LHPC_XT_RED(4); break;
+      case 8: LHPC_XT_RED(8); break;
+      default: LHPC_XT_RED(16); break;
+    }
 #undef LHPC_XT_RED
-  LHPC_TRY(check_launch(s));
+    return check_launch(rs);
+  };
+  if (p->xt_K <= 1) {
+    LHPC_TRY(gather(p->d_pieces, p->xt_pieces));
+    LHPC_TRY(reduce(0, p->xt_C, s));
+  } else {
+    for (int k = 0; k < p->xt_K; ++k) {
+      LHPC_TRY(gather(p->d_rpieces + 3 * p->xt_rpo[k], p->xt_rpo[k + 1] - p->xt_rpo[k]));
+      LHPC_HIP_TRY(hipEventRecord(p->xt_ev[k], s));
+      LHPC_HIP_TRY(hipStreamWaitEvent(p->xt_s2, p->xt_ev[k], 0));
+      LHPC_TRY(reduce(p->xt_rc[k], p->xt_rc[k + 1], p->xt_s2));
+    }
+    LHPC_HIP_TRY(hipEventRecord(p->xt_ev[p->xt_K], p->xt_s2));
+    LHPC_HIP_TRY(hipStreamWaitEvent(s, p->xt_ev[p->xt_K], 0));
+  }
   }
   if (p->xt_cont > 0) {
     hipLaunchKernelGGL((k_xtile_fixup<T>), dim3(static_cast<unsigned>((p->xt_cont + kXtBlock - 1) / kXtBlock)),
@@ -1604,12 +1632,47 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), nullptr, static_cast<size_t>(xt.total + 1) * 2));
     if (xt.total) LHPC_HIP_TRY(hipMemcpy(p->d_perm, xt.perm.get(), static_cast<size_t>(xt.total) * 2, hipMemcpyHostToDevice));
     {
-      const uint16_t spare = static_cast<uint16_t>(cM * tsz);  // slot M: one 16-B slot past the chunk
+      const uint16_t spare = static_cast<uint16_t>(cM);  // slot M: one 16-B slot past the chunk
       LHPC_HIP_TRY(hipMemcpy(p->d_perm + xt.total, &spare, 2, hipMemcpyHostToDevice));
     }
     LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total + 1) * tsz));
   }
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_carry), nullptr, static_cast<size_t>(2 * C + 2) * 8));
+  // pipelined ranges (seg): K chunk ranges, one gather piece per (range, tile):
+  // [ceil8(segoff(s, c_k)), ceil8(segoff(s, c_k+1))) — the last range ends at
+  // the tile's padded end.  The 8-entry group straddling a range bound is
+  // gathered with the earlier range, which completes first on the caller's
+  // stream, so every range's entries are written before its reduce starts.
+  // Opt-in (LHPC_XTILE_RANGES=K): measured slower on C2 (K = 2/4/8/16: 0.68–0.73
+  // ms against 0.63 ms at K = 1): the overlapped gather and reduce contend for
+  // the same HBM stream rate instead of filling each other's gaps.
+  int K = 1;
+  if (const char *env = std::getenv("LHPC_XTILE_RANGES")) K = std::max(1, std::atoi(env));
+  K = static_cast<int>(std::min<int64_t>(K, std::max<int64_t>(1, C)));
+  if (!cm && K > 1) {
+    const int64_t S = xt.S;
+    std::vector<int32_t> rpcs;
+    p->xt_rc.assign(static_cast<size_t>(K) + 1, 0);
+    p->xt_rpo.assign(static_cast<size_t>(K) + 1, 0);
+    for (int k = 0; k <= K; ++k) p->xt_rc[k] = C * k / K;
+    for (int k = 0; k < K; ++k) {
+      for (int64_t s = 0; s < S; ++s) {
+        const int64_t g0 = (xt.segoff[static_cast<size_t>(p->xt_rc[k] * S + s)] + 7) & ~int64_t{7};
+        const int64_t g1 = (xt.segoff[static_cast<size_t>(p->xt_rc[k + 1] * S + s)] + 7) & ~int64_t{7};
+        if (g1 > g0) {
+          rpcs.push_back(static_cast<int32_t>(g0));
+          rpcs.push_back(static_cast<int32_t>(g1));
+          rpcs.push_back(static_cast<int32_t>(s));
+        }
+      }
+      p->xt_rpo[k + 1] = static_cast<int64_t>(rpcs.size() / 3);
+    }
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_rpieces), rpcs.data(), rpcs.size() * 4));
+    LHPC_HIP_TRY(hipStreamCreateWithFlags(&p->xt_s2, hipStreamNonBlocking));
+    p->xt_ev.assign(static_cast<size_t>(K) + 1, nullptr);
+    for (auto &e : p->xt_ev) LHPC_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    p->xt_K = K;
+  }
   return LHPC_OK;
 }
 }  // namespace
@@ -1971,8 +2034,12 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
                   static_cast<void *>(p->d_cdesc), static_cast<void *>(p->d_ce), static_cast<void *>(p->d_cr), static_cast<void *>(p->d_segoff),
                   static_cast<void *>(p->d_pieces), static_cast<void *>(p->d_cont),
                   static_cast<void *>(p->d_col16), static_cast<void *>(p->d_perm), p->d_xg,
-                  static_cast<void *>(p->d_carry), static_cast<void *>(p->d_gdst)})
+                  static_cast<void *>(p->d_carry), static_cast<void *>(p->d_gdst),
+                  static_cast<void *>(p->d_rpieces)})
     if (q) (void)hipFree(q);
+  for (hipEvent_t e : p->xt_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (p->xt_s2) (void)hipStreamDestroy(p->xt_s2);
   delete p;
   return LHPC_OK;
 }

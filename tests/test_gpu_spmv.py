@@ -321,6 +321,16 @@ def test_xtile_small_gather_pieces(lhpc, gpu, monkeypatch, xt_layout):
     _check_xtile(lhpc, gpu, lengths, 100_000, np.float64, 0xA402)
 
 
+@pytest.mark.parametrize("ranges", ["2", "5"])
+def test_xtile_pipelined_ranges(lhpc, gpu, monkeypatch, ranges):
+    """LHPC_XTILE_RANGES=K: per-range gathers on the caller's stream, reduces on
+    a second stream; same bits as the single launch, long rows across ranges."""
+    monkeypatch.setenv("LHPC_XTILE_RANGES", ranges)
+    lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 30000 + [0, 0] + [30000]
+    _check_xtile(lhpc, gpu, lengths, 200_000, np.float32, 0xA600, expect_cont=True)
+    _check_xtile(lhpc, gpu, lengths, 200_000, np.float64, 0xA601, dyadic=False)
+
+
 def test_xtile_is_auto_choice_without_locality(lhpc, gpu):
     """x > 8 MB with uniform random columns selects XTILE; LHPC_SPMV_XTILE=0 gives XSLICE."""
     n = 3_000_000
