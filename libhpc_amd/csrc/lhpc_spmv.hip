@@ -688,13 +688,17 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
 #ifndef LHPC_XT_RBLK32
 #define LHPC_XT_RBLK32 512
 #endif
+#ifndef LHPC_XT_RBLK64
+#define LHPC_XT_RBLK64 512
+#endif
 // reduce configurations: BLK threads, chunks of M = 16·BLK nonzeros owning
-// ≤ Rmax rows (fp32 uses BLK = 512; fp64 BLK = 256, whose 4096-entry chunk
-// already takes 44 KB of LDS)
+// ≤ Rmax rows.  BLK = 512 for both types (C2 reduce: 256 → 512 took 470 →
+// 420 µs, 1024 was no faster; C3: 256 → 512 took 1078 → 987 µs at 2 blocks
+// per CU, 73 KB of LDS each)
 template <int BLK> struct XtRed {
   static constexpr int M = BLK * kXtRun, Rmax = M / 8;
 };
-template <typename T> constexpr int xt_red_blk() { return sizeof(T) == 4 ? LHPC_XT_RBLK32 : 256; }
+template <typename T> constexpr int xt_red_blk() { return sizeof(T) == 4 ? LHPC_XT_RBLK32 : LHPC_XT_RBLK64; }
 // LDS slot of chunk position i for the seg reduce (lhpc_plan.hpp xtile_slot):
 // run t = i/16 occupies 16·t … 16·t+15 and its 16-B slot q is stored at
 // q ^ xt_swz(t), so the 16 lanes of a ds_read_b128 group hit 16 distinct
