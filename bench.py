@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--n", type=int, default=10_000_000)
     ap.add_argument("--per-row", type=int, default=15)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--chunks", type=int, default=4, help="N>1: row chunks per rank (all-gather overlap)")
+    ap.add_argument("--chunks", type=int, default=2, help="N>1: row chunks per rank (all-gather overlap; DESIGN.md §6)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
