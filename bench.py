@@ -142,14 +142,33 @@ def main():
             # interleaved row blocks, K chunks per rank: chunk k's RCCL
             # all-gather overlaps the SpMV of chunk k+1 (libhpc_amd/dist.py)
             ib = InterleavedBlocks(n, world, args.chunks)
-            plans, local_nnz = [], 0
-            for k in range(args.chunks):
-                lrp, lc, lv = ib.local_csr(rp, col, val, rank, k)
-                plans.append(L.SpMVPlan(lrp, lc, lv, n))
-                local_nnz += int(lc.shape[0])
+            plans, local_nnz, fns = [], 0, None
+            if args.chunks > 1:
+                # one row-range plan over the rank's K chunks: x is staged once
+                # (one XTILE tile gather), then chunk k is reduced and its
+                # all-gather starts; falls back to a plan per chunk when the
+                # matrix does not select XTILE
+                lrp, lc, lv, splits = ib.local_csr_all(rp, col, val, rank)
+                try:
+                    sp = L.SpMVPlan(lrp, lc, lv, n, splits=splits)
+                except L.LhpcError:
+                    sp = None
+                if sp is not None:
+                    plans, local_nnz = [sp], int(lc.shape[0])
+
+                    def first(xv, yv, pl=sp):
+                        pl.stage(xv, stream=stream)
+                        pl.range(0, yv, stream=stream)
+                    fns = [first] + [lambda xv, yv, k=k, pl=sp: pl.range(k, yv, stream=stream)
+                                     for k in range(1, args.chunks)]
+            if fns is None:
+                for k in range(args.chunks):
+                    lrp, lc, lv = ib.local_csr(rp, col, val, rank, k)
+                    plans.append(L.SpMVPlan(lrp, lc, lv, n))
+                    local_nnz += int(lc.shape[0])
+                fns = [lambda xv, yv, pl=pl: pl(xv, yv, stream=stream) for pl in plans]
             local_rows = ib.B * args.chunks
-            dsp = DistSpMVOverlap(ib, [lambda xv, yv, pl=pl: pl(xv, yv, stream=stream) for pl in plans],
-                                  like=xd)
+            dsp = DistSpMVOverlap(ib, fns, like=xd)
 
             def step():
                 dsp.step(xd)

@@ -138,6 +138,29 @@ int lhpc_spmv(lhpc_spmv_plan *plan, const void *x, void *y,
               int buffers_on_device, void *stream);
 int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *plan,
                             lhpc_spmv_plan_info *info);
+/*
+ * Row-range plans for overlapping a collective with the SpMV (one process
+ * per GPU, libhpc_amd/dist.py): as lhpc_spmv_plan_create, with the plan's
+ * work cut at every row in split_rows (ascending, in (0, n_rows)), so that
+ * range k = rows [split_rows[k-1], split_rows[k]) (split_rows[-1] = 0,
+ * split_rows[n_splits] = n_rows) can be finished on its own:
+ *   lhpc_spmv_stage(plan, x, stream)        stages x (the XTILE tile gather)
+ *   lhpc_spmv_range(plan, k, y_k, stream)   writes range k's rows to y_k
+ * Device buffers only, asynchronous on `stream`; all ranges of one x follow
+ * one stage on the same stream.  LHPC_ERR_UNSUPPORTED when the matrix does
+ * not select the XTILE layout (gathers with locality, or x ≤ 8 MB): use one
+ * plan per range then.  lhpc_spmv on such a plan computes every range.
+ * Replaces the per-block SpMV calls of the reference's row-block split
+ * (no reference interface).
+ */
+int lhpc_spmv_plan_create_split(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
+                                int64_t n_cols, int64_t nnz, const void *row_ptr,
+                                int row_ptr_bits, const int32_t *col_idx,
+                                const void *val, const int *device_ids,
+                                int n_devices, unsigned flags, int n_splits,
+                                const int64_t *split_rows);
+int lhpc_spmv_stage(const lhpc_spmv_plan *plan, const void *x, void *stream);
+int lhpc_spmv_range(const lhpc_spmv_plan *plan, int k, void *y_range, void *stream);
 int lhpc_spmv_plan_destroy(lhpc_spmv_plan *plan);
 
 /*

@@ -58,6 +58,7 @@ ABI_SYMBOLS = (
     "lhpc_radix_sort_pairs_u64", "lhpc_coo_to_csr", "lhpc_csr_save", "lhpc_csr_load_header",
     "lhpc_csr_load", "lhpc_mm_read_header", "lhpc_mm_read_coo", "lhpc_cg_solve", "lhpc_vec_dot",
     "lhpc_cg_step_xr", "lhpc_cg_step_p", "lhpc_spmv_dot",
+    "lhpc_spmv_plan_create_split", "lhpc_spmv_stage", "lhpc_spmv_range",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -111,6 +112,10 @@ _sig("lhpc_device_count", _i)
 _sig("lhpc_spmv_plan_create", _i, C.POINTER(_p), _i, _i64, _i64, _i64, _p, _i, _p,
      _p, _p, _i, _u)
 _sig("lhpc_spmv", _i, _p, _p, _p, _i, _p)
+_sig("lhpc_spmv_plan_create_split", _i, C.POINTER(_p), _i, _i64, _i64, _i64, _p, _i, _p,
+     _p, _p, _i, _u, _i, _p)
+_sig("lhpc_spmv_stage", _i, _p, _p, _p)
+_sig("lhpc_spmv_range", _i, _p, _i, _p, _p)
 _sig("lhpc_spmv_plan_info_get", _i, _p, C.POINTER(PlanInfo))
 _sig("lhpc_spmv_plan_destroy", _i, _p)
 _sig("lhpc_csr_partition_rows", _i, _p, _i, _i64, _i, _p)
@@ -197,7 +202,11 @@ class SpMVPlan:
     """
 
     def __init__(self, row_ptr, col_idx, val, n_cols: int, flags: int = 0,
-                 device: Optional[int] = None):
+                 device: Optional[int] = None, splits=None):
+        """``splits``: ascending rows in (0, n_rows); the plan is then a
+        row-range plan (lhpc_spmv_plan_create_split: stage(x) once, then
+        range(k, y_k) per range) and raises LhpcError (LHPC_ERR_UNSUPPORTED)
+        when the matrix does not select the XTILE layout."""
         row_ptr = np.ascontiguousarray(row_ptr)
         col_idx = np.ascontiguousarray(col_idx, dtype=np.int32)
         val = np.ascontiguousarray(val)
@@ -215,11 +224,21 @@ class SpMVPlan:
         self.nnz = int(col_idx.shape[0])
         self._h = _p()
         dev = (_i * 1)(device) if device is not None else None
-        _check(lib.lhpc_spmv_plan_create(
-            C.byref(self._h), self.dtype, self.n_rows, self.n_cols, self.nnz,
-            row_ptr.ctypes.data, 64 if row_ptr.dtype == np.int64 else 32,
-            col_idx.ctypes.data, val.ctypes.data, dev, 1 if device is not None else 0,
-            flags), "lhpc_spmv_plan_create")
+        if splits is None:
+            self.splits = None
+            _check(lib.lhpc_spmv_plan_create(
+                C.byref(self._h), self.dtype, self.n_rows, self.n_cols, self.nnz,
+                row_ptr.ctypes.data, 64 if row_ptr.dtype == np.int64 else 32,
+                col_idx.ctypes.data, val.ctypes.data, dev, 1 if device is not None else 0,
+                flags), "lhpc_spmv_plan_create")
+        else:
+            sp = np.ascontiguousarray(splits, dtype=np.int64)
+            self.splits = [0] + [int(v) for v in sp] + [self.n_rows]
+            _check(lib.lhpc_spmv_plan_create_split(
+                C.byref(self._h), self.dtype, self.n_rows, self.n_cols, self.nnz,
+                row_ptr.ctypes.data, 64 if row_ptr.dtype == np.int64 else 32,
+                col_idx.ctypes.data, val.ctypes.data, dev, 1 if device is not None else 0,
+                flags, int(sp.shape[0]), sp.ctypes.data), "lhpc_spmv_plan_create_split")
 
     def info(self) -> dict:
         inf = PlanInfo()
@@ -246,6 +265,23 @@ class SpMVPlan:
             stream = torch.cuda.current_stream(y.device)
         _check(lib.lhpc_spmv(self._h, xp, yp, int(xd), _stream_ptr(stream)), "lhpc_spmv")
         return y
+
+    def stage(self, x, stream=None):
+        """Row-range plans: stage x (device tensor) for the ranges that follow."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(x.device)
+        _check(lib.lhpc_spmv_stage(self._h, x.data_ptr(), _stream_ptr(stream)), "lhpc_spmv_stage")
+
+    def range(self, k: int, y_k, stream=None):
+        """Row-range plans: rows [splits[k], splits[k+1]) of A·x into y_k (device)."""
+        if y_k.shape[0] < self.splits[k + 1] - self.splits[k]:
+            raise ValueError("y_k too short for the range")
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(y_k.device)
+        _check(lib.lhpc_spmv_range(self._h, int(k), y_k.data_ptr(), _stream_ptr(stream)), "lhpc_spmv_range")
+        return y_k
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:

@@ -210,7 +210,8 @@ int build_xtile_cm(const int32_t *col, int64_t nnz, int64_t piece_nnz, XtileHost
 }  // namespace
 
 int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
-                int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm, int slot_bytes, XtileHost &o) {
+                int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm, int slot_bytes,
+                const int64_t *splits, int n_splits, XtileHost &o) {
   const int64_t nnz = rp_at(rp, bits, n_rows) - rp_at(rp, bits, 0);
   if (W < 8 || M < 64 || M > 65536 || M % 16 || Rmax < 1 || (slot_bytes != 4 && slot_bytes != 8) ||
       M >= 65536)
@@ -236,11 +237,20 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
   //      (or a row whose predecessors starting at ce[c] are empty)
   o.ce.assign(1, 0);
   o.cr.assign(1, 0);
+  for (int i = 0; i < n_splits; ++i)
+    if (splits[i] <= 0 || splits[i] >= n_rows || (i > 0 && splits[i] <= splits[i - 1]))
+      return LHPC_ERR_INVALID_ARG;
   {
     int64_t e = 0, r = 0;
+    int si = 0;  // next split row after r
     while (!(e == nnz && r == n_rows)) {
       int64_t en, rb;
-      if (e + M >= nnz) {
+      // a split row is done once a chunk starts at it (e == its start, r == it)
+      while (si < n_splits && (RP(splits[si]) < e || (RP(splits[si]) == e && splits[si] <= r))) ++si;
+      if (si < n_splits && RP(splits[si]) <= e + M) {
+        en = RP(splits[si]);  // a range starts at this row: cut there
+        rb = splits[si];
+      } else if (e + M >= nnz) {
         en = nnz;
         rb = n_rows;
       } else {
@@ -266,6 +276,17 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
   }
   const int64_t C = static_cast<int64_t>(o.ce.size()) - 1;
   o.n_chunks = C;
+  // range k = chunks [rchunk[k], rchunk[k+1]): the chunk owning split row k−1 first
+  o.rchunk.assign(1, 0);
+  for (int i = 0; i < n_splits; ++i) {
+    // chunks inside a long row just before the split also have cr == split
+    // (they own no row); the range starts at the one beginning at the split row
+    int64_t c = std::lower_bound(o.cr.begin(), o.cr.end(), static_cast<int32_t>(splits[i])) - o.cr.begin();
+    while (c < C && !(o.cr[c] == splits[i] && o.ce[c] == RP(splits[i]))) ++c;
+    if (c >= C) return LHPC_ERR_INTERNAL;
+    o.rchunk.push_back(c);
+  }
+  o.rchunk.push_back(C);
   if (static_cast<double>(C + 1) * static_cast<double>(S) > 2.7e8) return LHPC_ERR_UNSUPPORTED;
   o.cont.clear();
   for (int64_t c = 0; c < C; ++c) {

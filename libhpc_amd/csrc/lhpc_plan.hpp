@@ -77,6 +77,7 @@ struct XtileHost {
   std::vector<int32_t> segoff;       // [(C+1)·S] segment starts in the tile stream
   std::vector<int32_t> pieces;       // gather workgroups: (g0, g1, s) triples (g0 == g1: idle)
   std::vector<int32_t> cont;         // chunks whose last owned row runs past the chunk
+  std::vector<int64_t> rchunk;       // [n_splits + 2] first chunk of each row range (+ C)
   std::unique_ptr<uint16_t[]> col16;  // [total]
   std::unique_ptr<uint16_t[]> perm;   // [total] (cm: [nnz])
   std::unique_ptr<int32_t[]> gdst;    // cm: [total / 8]
@@ -85,10 +86,12 @@ struct XtileHost {
 // 0 on success; LHPC_ERR_UNSUPPORTED when the layout does not fit its
 // index types (nnz + padding ≥ 2^31, S > 4096, or an oversized segment table).
 // piece_nnz: target nonzeros per gather workgroup (multiple of 8 is used;
-// cm: the number of chunk ranges H is derived from it).
+// cm: the number of chunk ranges H is derived from it).  splits: ascending
+// rows in (0, n_rows) at which a chunk must start (row ranges that can be
+// reduced separately, lhpc_spmv_range); LHPC_ERR_INVALID_ARG otherwise.
 int build_xtile(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_rows,
                 int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm,
-                int slot_bytes, XtileHost &out);
+                int slot_bytes, const int64_t *splits, int n_splits, XtileHost &out);
 
 // LDS slot of chunk position i in the XTILE seg reduce (lhpc_spmv.hip
 // xt_slot): run t = i/16 holds 16 elements at 16·t, its 16-B slot q at

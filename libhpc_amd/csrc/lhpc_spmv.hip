@@ -943,7 +943,7 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
 template <typename T>
 __global__ __launch_bounds__(kXtBlock) void k_xtile_fixup(
     const int32_t *__restrict__ cont, int64_t n_cont, const int32_t *__restrict__ cr, int64_t C,
-    const double *__restrict__ carry, T *__restrict__ y) {
+    const double *__restrict__ carry, T *__restrict__ y) {  // C: end of the chunk range (rows never cross it)
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kXtBlock + threadIdx.x;
   if (i >= n_cont) return;
   const int64_t c = cont[i];
@@ -1212,6 +1212,9 @@ struct lhpc_spmv_plan {
   // stream, its reduce on xt_s2 once the gather's event fires, so range k's
   // reduce overlaps range k+1's gather
   int xt_K = 1;
+  // row ranges (lhpc_spmv_plan_create_split): range k = rows [xt_srow[k],
+  // xt_srow[k+1]) = chunks [xt_src[k], xt_src[k+1]), cont entries [xt_sco[k], xt_sco[k+1])
+  std::vector<int64_t> split_rows, xt_srow, xt_src, xt_sco;
   std::vector<int64_t> xt_rc;           // [K+1] chunk bounds
   std::vector<int64_t> xt_rpo;          // [K+1] offsets (in pieces) of each range's gather pieces
   int32_t *d_rpieces = nullptr;
@@ -1501,6 +1504,55 @@ int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s)
   return LHPC_OK;
 }
 
+// lhpc_spmv_stage: the gather of a split plan; lhpc_spmv_range: range k's
+// reduce + fix-up into y_k (row xt_srow[k] at y_k[0]).
+template <typename T>
+int launch_xtile_stage(const lhpc_spmv_plan *p, const void *x, hipStream_t s) {
+  if (p->xt_pieces <= 0) return LHPC_OK;
+  const dim3 g(static_cast<unsigned>(p->xt_pieces)), b(kXtGatherBlock);
+  T *xg = static_cast<T *>(p->d_xg);
+  if (p->xt_u == 2)
+    hipLaunchKernelGGL((k_xtile_gather<T, 2>), g, b, 0, s, p->d_pieces, p->d_col16,
+                       static_cast<const T *>(x), p->n_cols, xg);
+  else
+    hipLaunchKernelGGL((k_xtile_gather<T, 4>), g, b, 0, s, p->d_pieces, p->d_col16,
+                       static_cast<const T *>(x), p->n_cols, xg);
+  return check_launch(s);
+}
+
+template <typename T>
+int launch_xtile_range(const lhpc_spmv_plan *p, int k, void *yk, hipStream_t s) {
+  const int64_t c0 = p->xt_src[k], c1 = p->xt_src[k + 1];
+  T *y = static_cast<T *>(yk) - p->xt_srow[k];  // rows are written at their plan index
+  T *xg = static_cast<T *>(p->d_xg);
+  if (c1 > c0) {
+    const int64_t Cx = (c1 - c0 + 7) / 8;
+    constexpr int BLK = xt_red_blk<T>();
+    const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(BLK);
+#define LHPC_XT_RED(GG)                                                                               \
+  hipLaunchKernelGGL((k_xtile_reduce<T, GG, BLK>), rg, rb, p->xt_lds, s, p->d_cdesc, p->d_segoff, p->S, \
+                     c0, c1, Cx, static_cast<int>(p->xt_total), xg, p->d_perm,                         \
+                     static_cast<const T *>(p->d_val), static_cast<const int32_t *>(p->d_row_ptr), y,  \
+                     p->d_carry)
+    switch (xtile_g<T>(p->S)) {
+      case 1: LHPC_XT_RED(1); break;
+      case 2: LHPC_XT_RED(2); break;
+      case 4: LHPC_XT_RED(4); break;
+      case 8: LHPC_XT_RED(8); break;
+      default: LHPC_XT_RED(16); break;
+    }
+#undef LHPC_XT_RED
+    LHPC_TRY(check_launch(s));
+  }
+  const int64_t n0 = p->xt_sco[k], n1 = p->xt_sco[k + 1];
+  if (n1 > n0) {
+    hipLaunchKernelGGL((k_xtile_fixup<T>), dim3(static_cast<unsigned>((n1 - n0 + kXtBlock - 1) / kXtBlock)),
+                       dim3(kXtBlock), 0, s, p->d_cont + n0, n1 - n0, p->d_cr, c1, p->d_carry, y);
+    LHPC_TRY(check_launch(s));
+  }
+  return LHPC_OK;
+}
+
 template <typename T>
 int launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
   if (p->kernel == LHPC_KERNEL_XTILE) return launch_xtile<T>(p, x, y, s);
@@ -1568,7 +1620,8 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   const int cM = cm ? kXtM : (tsz == 4 ? XtRed<xt_red_blk<float>()>::M : XtRed<xt_red_blk<double>()>::M);
   const int cR = cm ? kXtRmax : (tsz == 4 ? XtRed<xt_red_blk<float>()>::Rmax : XtRed<xt_red_blk<double>()>::Rmax);
   const int bst = build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, cM, cR, piece,
-                              cm != 0, static_cast<int>(tsz), xt);
+                              cm != 0, static_cast<int>(tsz), p->split_rows.data(),
+                              static_cast<int>(p->split_rows.size()), xt);
   if (bst != LHPC_OK) return bst;
   p->kernel = LHPC_KERNEL_XTILE;
   p->rp64 = 0;
@@ -1642,6 +1695,18 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
     LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total + 1) * tsz));
   }
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_carry), nullptr, static_cast<size_t>(2 * C + 2) * 8));
+  LHPC_HIP_TRY(hipMemset(p->d_carry, 0, static_cast<size_t>(2 * C + 2) * 8));
+  if (!p->split_rows.empty()) {
+    const size_t K = p->split_rows.size() + 1;
+    p->xt_srow.assign(1, 0);
+    p->xt_srow.insert(p->xt_srow.end(), p->split_rows.begin(), p->split_rows.end());
+    p->xt_srow.push_back(n_rows);
+    p->xt_src.assign(xt.rchunk.begin(), xt.rchunk.end());
+    p->xt_sco.assign(K + 1, 0);
+    for (size_t k = 0; k <= K; ++k)
+      p->xt_sco[k] = std::lower_bound(xt.cont.begin(), xt.cont.end(), static_cast<int32_t>(p->xt_src[k])) -
+                     xt.cont.begin();
+  }
   // pipelined ranges (seg): K chunk ranges, one gather piece per (range, tile):
   // [ceil8(segoff(s, c_k)), ceil8(segoff(s, c_k+1))) — the last range ends at
   // the tile's padded end.  The 8-entry group straddling a range bound is
@@ -1681,11 +1746,11 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
 }
 }  // namespace
 
-extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
-                                     int64_t n_cols, int64_t nnz, const void *row_ptr,
-                                     int row_ptr_bits, const int32_t *col_idx,
-                                     const void *val, const int *device_ids,
-                                     int n_devices, unsigned flags) {
+namespace {
+int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
+                     const void *row_ptr, int row_ptr_bits, const int32_t *col_idx, const void *val,
+                     const int *device_ids, int n_devices, unsigned flags, int n_splits,
+                     const int64_t *split_rows) {
   if (!out) return LHPC_ERR_INVALID_ARG;
   *out = nullptr;
   if ((dtype != LHPC_F32 && dtype != LHPC_F64) || n_rows < 0 || n_cols < 0 || nnz < 0 ||
@@ -1716,6 +1781,7 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
 
   auto *p = new (std::nothrow) lhpc_spmv_plan();
   if (!p) return LHPC_ERR_ALLOC;
+  if (n_splits > 0) p->split_rows.assign(split_rows, split_rows + n_splits);
   p->dtype = dtype;
   p->device = dev;
   p->n_rows = n_rows;
@@ -1939,6 +2005,55 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
   }
   *out = p;
   return LHPC_OK;
+}
+}  // namespace
+
+extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
+                                     int64_t n_cols, int64_t nnz, const void *row_ptr,
+                                     int row_ptr_bits, const int32_t *col_idx,
+                                     const void *val, const int *device_ids,
+                                     int n_devices, unsigned flags) {
+  return plan_create_impl(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
+                          device_ids, n_devices, flags, 0, nullptr);
+}
+
+extern "C" int lhpc_spmv_plan_create_split(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
+                                           int64_t n_cols, int64_t nnz, const void *row_ptr,
+                                           int row_ptr_bits, const int32_t *col_idx,
+                                           const void *val, const int *device_ids, int n_devices,
+                                           unsigned flags, int n_splits, const int64_t *split_rows) {
+  if (!out || n_splits < 1 || !split_rows) return LHPC_ERR_INVALID_ARG;
+  for (int i = 0; i < n_splits; ++i)
+    if (split_rows[i] <= 0 || split_rows[i] >= n_rows || (i > 0 && split_rows[i] <= split_rows[i - 1]))
+      return LHPC_ERR_INVALID_ARG;
+  const int st = plan_create_impl(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
+                                  device_ids, n_devices, flags, n_splits, split_rows);
+  if (st != LHPC_OK) return st;
+  const lhpc_spmv_plan *p = *out;
+  if (p->kernel != LHPC_KERNEL_XTILE || p->xt_cm || p->xt_srow.size() != static_cast<size_t>(n_splits) + 2) {
+    lhpc_spmv_plan_destroy(*out);  // ranges exist only in the XTILE tile-stream layout
+    *out = nullptr;
+    return LHPC_ERR_UNSUPPORTED;
+  }
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_spmv_stage(const lhpc_spmv_plan *p, const void *x, void *stream) {
+  if (!p || (p->n_cols > 0 && !x)) return LHPC_ERR_INVALID_ARG;
+  if (p->xt_srow.empty()) return LHPC_ERR_UNSUPPORTED;
+  LHPC_HIP_TRY(hipSetDevice(p->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  return p->dtype == LHPC_F32 ? launch_xtile_stage<float>(p, x, s) : launch_xtile_stage<double>(p, x, s);
+}
+
+extern "C" int lhpc_spmv_range(const lhpc_spmv_plan *p, int k, void *y_range, void *stream) {
+  if (!p || p->xt_srow.empty() || k < 0 || k + 2 > static_cast<int>(p->xt_srow.size()))
+    return LHPC_ERR_INVALID_ARG;
+  if (p->xt_srow[k + 1] > p->xt_srow[k] && !y_range) return LHPC_ERR_INVALID_ARG;
+  LHPC_HIP_TRY(hipSetDevice(p->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  return p->dtype == LHPC_F32 ? launch_xtile_range<float>(p, k, y_range, s)
+                              : launch_xtile_range<double>(p, k, y_range, s);
 }
 
 extern "C" int lhpc_spmv(lhpc_spmv_plan *p, const void *x, void *y, int on_device,

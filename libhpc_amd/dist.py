@@ -170,6 +170,22 @@ class InterleavedBlocks:
         k0, k1 = int(row_ptr[r0]), int(row_ptr[r1])
         return lrp, col_idx[k0:k1], val[k0:k1]
 
+    def local_csr_all(self, row_ptr, col_idx, val, rank: int):
+        """The rank's K chunks as one CSR of K·B rows (chunk k = rows
+        [k·B, (k+1)·B)) and the split rows B, 2B, …, (K−1)·B — the input of
+        one row-range plan (SpMVPlan(..., splits=...))."""
+        parts = [self.local_csr(row_ptr, col_idx, val, rank, k) for k in range(self.K)]
+        lrp = np.zeros(self.K * self.B + 1, dtype=np.int64)
+        off = 0
+        for k, (prp, _, _) in enumerate(parts):
+            lrp[k * self.B:(k + 1) * self.B + 1] = prp.astype(np.int64) + off
+            off += int(prp[-1])
+        if off < 2 ** 31:
+            lrp = lrp.astype(np.int32)
+        col = np.concatenate([c for _, c, _ in parts]) if parts else col_idx[:0]
+        v = np.concatenate([w for _, _, w in parts]) if parts else val[:0]
+        return lrp, col, v, [k * self.B for k in range(1, self.K)]
+
 
 class DistSpMVOverlap:
     """y = A·x on `world` ranks, K chunks per rank, all-gather of chunk k

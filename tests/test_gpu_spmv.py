@@ -331,6 +331,45 @@ def test_xtile_pipelined_ranges(lhpc, gpu, monkeypatch, ranges):
     _check_xtile(lhpc, gpu, lengths, 200_000, np.float64, 0xA601, dyadic=False)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_xtile_split_ranges(lhpc, gpu, dtype):
+    """Row-range plan (lhpc_spmv_plan_create_split): stage once, reduce each
+    range into its own buffer; long rows end at and start right after the
+    split rows; the concatenation equals the whole-matrix oracle bit for bit
+    (dyadic) and lhpc_spmv on the same plan gives the same bits."""
+    import torch
+    lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 30000 + [0, 0] + [30000]
+    n_cols = 200_000
+    rp, col, val = _csr_from_lengths(lengths, n_cols, 0xA700, dyadic=True)
+    val = val.astype(dtype)
+    rng = np.random.default_rng(0xA701)
+    x = (rng.integers(-8, 9, size=n_cols) / 8.0).astype(dtype)
+    n = len(lengths)
+    splits = [1, 51, 57, 20000, n - 1]  # after the long first row, around the long rows, before the last
+    with lhpc.SpMVPlan(rp, col, val, n_cols, flags=FAMILIES["xtile"], splits=splits) as plan:
+        assert plan.info()["kernel"] == lhpc.KERNEL_XTILE
+        xd = torch.from_numpy(x).to(gpu)
+        bounds = [0] + splits + [n]
+        ys = [torch.full((bounds[k + 1] - bounds[k],), float("nan"), dtype=xd.dtype, device=gpu)
+              for k in range(len(bounds) - 1)]
+        for _ in range(2):  # twice: carries from the previous call must not leak
+            plan.stage(xd)
+            for k, yk in enumerate(ys):
+                plan.range(k, yk)
+        y = torch.cat(ys).cpu().numpy()
+        yfull = plan(xd).cpu().numpy()
+    _, yr, _ = S.spmv_oracle(rp, col, val, x)
+    assert np.array_equal(y, yr)
+    assert np.array_equal(yfull, yr)
+
+
+def test_split_plan_unsupported_without_xtile(lhpc, gpu):
+    """A matrix that does not select XTILE (small x) refuses a row-range plan."""
+    rp, col, val = _csr_from_lengths([5] * 1000, 1000, 0xA800, dyadic=True)
+    with pytest.raises(lhpc.LhpcError):
+        lhpc.SpMVPlan(rp, col, val.astype(np.float32), 1000, splits=[500])
+
+
 def test_xtile_is_auto_choice_without_locality(lhpc, gpu):
     """x > 8 MB with uniform random columns selects XTILE; LHPC_SPMV_XTILE=0 gives XSLICE."""
     n = 3_000_000
