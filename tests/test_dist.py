@@ -121,3 +121,26 @@ def test_overlapped_allgather_gloo(world, K):
         p.join(timeout=60)
     for rank, ok in res:
         assert ok is True, f"rank {rank}: {ok}"
+
+
+@pytest.mark.parametrize("world,K,rank", [(2, 2, 0), (2, 2, 1), (3, 4, 2), (8, 2, 7)])
+def test_local_csr_all_concatenates_chunks(world, K, rank):
+    """InterleavedBlocks.local_csr_all (the row-range plan's input) is the
+    rank's K chunk CSRs stacked, with splits at multiples of B."""
+    from libhpc_amd.dist import InterleavedBlocks
+    rng = np.random.default_rng(world * 100 + K * 10 + rank)
+    n = 1003
+    lens = rng.integers(0, 9, size=n)
+    rp = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lens, out=rp[1:])
+    col = rng.integers(0, n, size=int(rp[-1])).astype(np.int32)
+    val = rng.standard_normal(int(rp[-1])).astype(np.float32)
+    ib = InterleavedBlocks(n, world, K)
+    lrp, lc, lv, splits = ib.local_csr_all(rp, col, val, rank)
+    assert splits == [k * ib.B for k in range(1, K)]
+    assert lrp.shape[0] == K * ib.B + 1 and lrp[0] == 0 and lrp[-1] == lc.shape[0] == lv.shape[0]
+    for k in range(K):
+        prp, pc, pv = ib.local_csr(rp, col, val, rank, k)
+        seg = lrp[k * ib.B:(k + 1) * ib.B + 1]
+        assert np.array_equal(seg - seg[0], prp.astype(np.int64))
+        assert np.array_equal(lc[seg[0]:seg[-1]], pc) and np.array_equal(lv[seg[0]:seg[-1]], pv)
