@@ -1610,7 +1610,10 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, p->device) == hipSuccess) cus = prop.multiProcessorCount;
   // ≈ 2 gather workgroups per CU (one resident per CU: 160 KB of LDS each)
-  int64_t piece = std::max<int64_t>(65536, p->nnz / (2 * static_cast<int64_t>(cus)) + 1);
+  // and ≥ 4 tiles' worth of stream per piece, so the tile load (W·T bytes)
+  // stays ≤ 1/4 of a piece's col16 + xg traffic on small (per-rank) matrices
+  const int64_t min_piece = 4 * W * static_cast<int64_t>(tsz) / (2 + static_cast<int64_t>(tsz));
+  int64_t piece = std::max<int64_t>(min_piece, p->nnz / (2 * static_cast<int64_t>(cus)) + 1);
   if (const char *env = std::getenv("LHPC_XTILE_PIECE")) piece = std::max<int64_t>(8, std::atoll(env));
   XtileHost xt;
   // LHPC_XTILE_LAYOUT=cm: chunk-major xg (opt-in: its scattered xg stores make
