@@ -357,7 +357,7 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
         g = 1
         P = n + 2
         cells = n ** 3
-        name = "k_stencil7_buf"
+        name = "k_stencil7_buf4"
         if world == 1:
             u = torch.zeros(P ** 3, device=dev)
             u.view(P, P, P)[1:-1, 1:-1, 1:-1] = torch.rand(n, n, n, device=dev) * 2 - 1

@@ -32,6 +32,7 @@ constexpr int kWave = 64;  // CDNA wavefront; never 32
 // accept these, not HIP_vector_type.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Debug builds check every launch synchronously, the way the reference does
 // under #ifndef NDEBUG (lib/gpu/radix_gpu/src/cuda_radix_sort_v4.cu:104-107).

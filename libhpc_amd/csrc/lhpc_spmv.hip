@@ -599,7 +599,6 @@ template <typename T> struct XtTile;
 template <> struct XtTile<float> { static constexpr int W = 40960; };   // 160 KB
 template <> struct XtTile<double> { static constexpr int W = 20480; };  // 160 KB
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // gather: block b streams pieces[3b..3b+1] of tile pieces[3b+2]; 8 nonzeros
 // per thread and step (one 16-B col16 load, 8 LDS gathers, 8 contiguous xg

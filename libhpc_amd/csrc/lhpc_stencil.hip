@@ -944,6 +944,116 @@ __global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ 
     if (diag == 1234.5f) out[0] = diag;
 }
 
+// x4 ring (`LHPC_STENCIL7_IMPL=buf4`): the buffer ring with 4 consecutive x per
+// lane — lane l of x-block j (256 floats) holds x0 + 256j + 4l .. +3, loaded by
+// one dwordx4 per row and block at 4-B alignment (the 514-float pitch never
+// makes rows 8-B aligned; unaligned 16-B buffer loads run at the full rate).
+// x±1 inside a lane are register moves; across lanes one DPP move per side,
+// whose lane-0 / lane-63 inputs are readlane broadcasts as in k_stencil7_buf.
+// Same operation order per cell, so results are bit-identical.  Needs
+// nx % (64·NJ) == 0: every x4 of a tile then ends at or before column nx-1+g,
+// so none reaches past the array end (a partially out-of-range x4 is not
+// relied on).  STORE: 5 the 4 results leave as one unaligned dwordx4 store,
+// 6 the same non-temporal, 2 no stores (timing diagnostic).
+template <int RY, int NJ, int STORE, int PF = 1>
+__global__ __launch_bounds__(256) void k_stencil7_buf4(const float *__restrict__ u, float *__restrict__ out,
+                                                       int64_t nz, int64_t ny, int64_t nx, int64_t g,
+                                                       float c0, float c1, int64_t z_begin, int64_t z_end,
+                                                       int64_t ntx, int64_t nty, int64_t ntz, int64_t zc) {
+  static_assert(NJ % 4 == 0, "x4 blocks");
+  constexpr int NB = NJ / 4;
+  constexpr int TW = NJ * kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
+  const int64_t t = xcd_tile(blockIdx.x, ntx * nty * ntz);
+  const int64_t x0 = (t % ntx) * TW;
+  const int64_t y0 = (((t / ntx) % nty) * 4 + w) * RY;
+  const int64_t zs = z_begin + (t / (ntx * nty)) * zc;
+  if (zs >= z_end || y0 >= ny) return;  // wave-uniform
+  const int64_t ze = zs + zc < z_end ? zs + zc : z_end;
+  const int64_t Px = nx + 2 * g;
+  const int64_t Pyx = (ny + 2 * g) * Px;
+  const int vx = static_cast<int>((x0 + 4 * lane + g) * 4);
+  const int ve = static_cast<int>((lane == 0 ? x0 - 1 + g : x0 + TW + g) * 4);
+  int64_t rowo[RY + 2];
+#pragma unroll
+  for (int r = 0; r < RY + 2; ++r) {
+    int64_t yy = y0 - 1 + r;
+    yy = yy < ny ? yy : ny;
+    rowo[r] = (yy + g) * Px;
+  }
+  const int64_t total = (nz + 2 * g) * Pyx;
+  auto rsrc = [&](const float *base, int64_t z, int r) {
+    const int64_t off = ((z < nz ? z : nz) + g) * Pyx + rowo[r];
+    const int64_t left = (total - off) * 4;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base + off), 0,
+                                             static_cast<int>(left < 0x7fffffff ? left : 0x7fffffff), 0x00020000);
+  };
+  struct Slot {
+    u32x4 v[RY + 2][NB];
+    float e[RY];
+  };
+  constexpr int NS = PF + 3;
+  Slot R[NS];
+  auto load = [&](Slot &S, int64_t z) {
+#pragma unroll
+    for (int r = 0; r < RY + 2; ++r) {
+      const auto rs = rsrc(u, z, r);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) S.v[r][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, vx + 1024 * j, 0, 0);
+      if (r >= 1 && r <= RY) S.e[r - 1] = bitsf(__builtin_amdgcn_raw_buffer_load_b32(rs, ve, 0, 0));
+    }
+  };
+  float diag = 0.f;
+  auto step = [&](const Slot &M, const Slot &Cc, const Slot &Pp, int64_t z) {
+    if (z >= ze) return;
+#pragma unroll
+    for (int r = 0; r < RY; ++r) {
+      if (y0 + r >= ny) break;
+      const auto ws = rsrc(out, z, r + 1);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const u32x4 c = Cc.v[r + 1][j];
+        const int lft = j > 0 ? __builtin_amdgcn_readlane(static_cast<int>(Cc.v[r + 1][j > 0 ? j - 1 : 0][3]), kWave - 1)
+                              : __builtin_amdgcn_readlane(fbits(Cc.e[r]), 0);
+        const int rgt = j < NB - 1
+                            ? __builtin_amdgcn_readlane(static_cast<int>(Cc.v[r + 1][j < NB - 1 ? j + 1 : 0][0]), 0)
+                            : __builtin_amdgcn_readlane(fbits(Cc.e[r]), kWave - 1);
+        const float xm0 = bitsf(__builtin_amdgcn_update_dpp(lft, static_cast<int>(c[3]), kDppWaveShr1, 0xF, 0xF, false));
+        const float xp3 = bitsf(__builtin_amdgcn_update_dpp(rgt, static_cast<int>(c[0]), kDppWaveShl1, 0xF, 0xF, false));
+        u32x4 res;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float cz = bitsf(static_cast<int>(c[k]));
+          const float xm = k > 0 ? bitsf(static_cast<int>(c[k > 0 ? k - 1 : 0])) : xm0;
+          const float xp = k < 3 ? bitsf(static_cast<int>(c[k < 3 ? k + 1 : 3])) : xp3;
+          float sum = __fadd_rn(bitsf(static_cast<int>(M.v[r + 1][j][k])), bitsf(static_cast<int>(Pp.v[r + 1][j][k])));
+          sum = __fadd_rn(sum, bitsf(static_cast<int>(Cc.v[r][j][k])));
+          sum = __fadd_rn(sum, bitsf(static_cast<int>(Cc.v[r + 2][j][k])));
+          sum = __fadd_rn(sum, xm);
+          sum = __fadd_rn(sum, xp);
+          const float o = __fadd_rn(__fmul_rn(c0, cz), __fmul_rn(c1, sum));
+          if constexpr (STORE == 2) diag += o;
+          res[k] = static_cast<uint32_t>(fbits(o));
+        }
+        if constexpr (STORE != 2)
+          __builtin_amdgcn_raw_buffer_store_b128(res, ws, vx + 1024 * j, 0, STORE == 6 ? 2 : 0);
+      }
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < PF + 2; ++k) load(R[k], zs - 1 + k);
+  for (int64_t z = zs; z < ze; z += NS) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      load(R[(k + PF + 2) % NS], z + k + PF + 1);
+      step(R[k % NS], R[(k + 1) % NS], R[(k + 2) % NS], z + k);
+    }
+  }
+  if constexpr (STORE == 2)
+    if (diag == 1234.5f) out[0] = diag;
+}
+
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 struct HostStage {
@@ -1067,8 +1177,8 @@ int blur_entry(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int6
 int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, int64_t g, float c0,
               float c1, int64_t zb, int64_t ze, hipStream_t s) {
   if (zb >= ze || ny == 0 || nx == 0) return LHPC_OK;
-  // implementation: buf (default); "wide", "ring", "simple", "pf", "reg", "lds" are measured
-  // alternatives
+  // implementation: buf (default; its x4 form buf4 when the x tiles are full); "wide", "ring",
+  // "simple", "pf", "reg", "lds" are measured alternatives
   const char *impl = std::getenv("LHPC_STENCIL7_IMPL");
   const bool use_lds = impl && !std::strcmp(impl, "lds");
   const bool use_reg = impl && !std::strcmp(impl, "reg");
@@ -1080,7 +1190,8 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
   // staged float4 stores for the buffer ring (219-220 us vs 225-226 plain on 512^3; plain when
   // `out` is not 16-B aligned), non-temporal for the flat wide ring (234-238 vs 234-255 us).
   const char *stm = std::getenv("LHPC_STENCIL7_STORE");
-  const bool buf_impl = !impl || !std::strcmp(impl, "buf");
+  const bool buf4_req = impl && !std::strcmp(impl, "buf4");
+  const bool buf_impl = !impl || !std::strcmp(impl, "buf") || buf4_req;
   int store_mode = stm ? (!std::strcmp(stm, "plain") ? 0 : !std::strcmp(stm, "none") ? 2
                           : !std::strcmp(stm, "aligned") ? 3 : !std::strcmp(stm, "staged") ? 4 : 1)
                        : (buf_impl ? 4 : 1);
@@ -1093,8 +1204,12 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
     // more waves — 2,8 at zc 128 (256 blocks) 209-220 us vs 250 us at zc 32 (1024 blocks);
     // prefetch depth (PF) and store policy (plain vs nt) are secondary.
     const char *cfg = std::getenv("LHPC_STENCIL7_BUF");  // "RY,NJ,ZC[,PF]"
-    int ry = 2, nj = 8, zc = 0, pf = 1;
+    int ry = 2, nj = 8, zc = 0, pf = 0;
     if (cfg) std::sscanf(cfg, "%d,%d,%d,%d", &ry, &nj, &zc, &pf);
+    // x4 ring by default when every x tile is full (nx % (64·NJ) == 0): 198-211 us against
+    // 209-225 us for the dword ring on 512^3, same boxes; "buf" forces the dword ring
+    const bool buf4 = (buf4_req || !impl) && (nj == 4 || nj == 8) && nx % (int64_t{nj} * kWave) == 0;
+    if (pf < 1) pf = buf4 ? 2 : 1;  // prefetch planes: x4 PF 2 198 us vs PF 1 210-217 / PF 3 203
     if (zc < 1) {
       const char *bt = std::getenv("LHPC_STENCIL7_BLOCKS");
       const int64_t target = bt ? std::max<int64_t>(1, std::atoll(bt)) : 256;
@@ -1102,6 +1217,37 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
       const int64_t xy = ((nx + tw - 1) / tw) * ((ny + th - 1) / th);
       const int64_t nchunks = std::max<int64_t>(1, (target + xy - 1) / xy);
       zc = static_cast<int>(std::max<int64_t>(4, (ze - zb + nchunks - 1) / nchunks));
+    }
+    if (buf4) {  // x4 ring: non-temporal dwordx4 stores ("plain": plain, "none": diagnostic)
+      const int m4 = stm && !std::strcmp(stm, "none") ? 2 : stm && !std::strcmp(stm, "plain") ? 5 : 6;
+#define LHPC_S74_M(RY, NJ, M)                                                                          \
+  do {                                                                                                 \
+    const int64_t ntx = nx / (NJ * kWave), nty = (ny + 4 * RY - 1) / (4 * RY), ntz = (ze - zb + zc - 1) / zc; \
+    if (pf == 2)                                                                                       \
+      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 2>), dim3(static_cast<unsigned>(ntx * nty * ntz)),   \
+                         dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
+    else if (pf == 3)                                                                                  \
+      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 3>), dim3(static_cast<unsigned>(ntx * nty * ntz)),   \
+                         dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
+    else                                                                                               \
+      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M>), dim3(static_cast<unsigned>(ntx * nty * ntz)),      \
+                         dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
+  } while (0)
+#define LHPC_S74(RY, NJ)                            \
+  do {                                              \
+    if (m4 == 2) LHPC_S74_M(RY, NJ, 2);             \
+    else if (m4 == 5) LHPC_S74_M(RY, NJ, 5);        \
+    else LHPC_S74_M(RY, NJ, 6);                     \
+  } while (0)
+      if (ry == 1 && nj == 8) LHPC_S74(1, 8);
+      else if (ry == 4 && nj == 8) LHPC_S74(4, 8);
+      else if (ry == 2 && nj == 4) LHPC_S74(2, 4);
+      else if (ry == 1 && nj == 4) LHPC_S74(1, 4);
+      else if (ry == 4 && nj == 4) LHPC_S74(4, 4);
+      else LHPC_S74(2, 8);
+#undef LHPC_S74
+#undef LHPC_S74_M
+      return check_launch(s);
     }
 #define LHPC_S7B_M(RY, NJ, M)                                                                         \
   do {                                                                                                \

@@ -139,6 +139,32 @@ def test_stencil7_every_impl(lhpc, gpu, impl, store, monkeypatch):
         assert np.array_equal(got, want), (impl, store, nz, ny, nx, g)
 
 
+S7_BUF4 = ["2,8,0", "2,8,5", "1,8,16", "4,8,32", "2,4,7", "4,4,32"]
+
+
+@pytest.mark.parametrize("cfg", S7_BUF4)
+@pytest.mark.parametrize("store", ["nt", "plain", "none"])
+def test_stencil7_buf4(lhpc, gpu, cfg, store, monkeypatch):
+    """The x4 ring (LHPC_STENCIL7_IMPL=buf4, 4 consecutive x per lane,
+    dwordx4 loads/stores at 4-B alignment) is bit-exact against the oracle on
+    shapes whose nx is a multiple of its tile width — one and several x tiles,
+    ny / nz ragged against the row and z-chunk tiles, ghost widths 1 to 3 (so
+    rows start at every 4-B phase of a 16-B line) — and leaves `out` untouched
+    with stores off.  Other nx fall back to the dword ring (covered above)."""
+    monkeypatch.setenv("LHPC_STENCIL7_IMPL", "buf4")
+    monkeypatch.setenv("LHPC_STENCIL7_BUF", cfg)
+    monkeypatch.setenv("LHPC_STENCIL7_STORE", store)
+    for (nz, ny, nx, g) in ((37, 45, 1024, 1), (9, 19, 512, 2), (3, 2, 1536, 3), (5, 9, 512, 1)):
+        if nx % (64 * int(cfg.split(",")[1])):
+            continue
+        shape = (nz + 2 * g, ny + 2 * g, nx + 2 * g)
+        u = S.random_padded(shape, seed=nz * 7 + nx + g, zero_ghost=False).reshape(-1)
+        out0 = S.random_padded(shape, seed=1234 + g).reshape(-1)
+        want = out0.copy() if store == "none" else S.stencil7_oracle(u, nz, ny, nx, g, -6.0, 1.0, out=out0.copy())
+        got = lhpc.stencil7(_dev(gpu, u), _dev(gpu, out0), nz, ny, nx, g, -6.0, 1.0).cpu().numpy()
+        assert np.array_equal(got, want), (cfg, store, nz, ny, nx, g)
+
+
 BX_IMPLS = [("wave", "1"), ("wave", "2"), ("wave", "4"), ("wave", "8"), ("wave", "16"), ("wave", "32"),
             ("lds", "1"), ("lds", "2"), ("lds", "4"), ("lds", "8")]
 

@@ -60,6 +60,9 @@ def main():
         wb = write.get(k, 0.0)
         ent["kernels"][k] = {"read_bytes": rb, "write_bytes": wb, "dispatches": n[k],
                              "raw_fetch_bytes": fetch[k]}
+        if k.startswith("k_copyw"):  # bench.py's copy-ceiling probe, not part of the workload
+            ent["kernels"][k]["probe"] = True
+            continue
         tot += rb + wb
     ent["bytes_per_call"] = tot
     db[tag] = ent
