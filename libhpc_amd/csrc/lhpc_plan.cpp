@@ -211,10 +211,10 @@ int build_xtile_cm(const int32_t *col, int64_t nnz, int64_t piece_nnz, XtileHost
 
 int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
                 int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm, int slot_bytes,
-                const int64_t *splits, int n_splits, XtileHost &o) {
+                const int64_t *splits, int n_splits, XtileHost &o, int pad) {
   const int64_t nnz = rp_at(rp, bits, n_rows) - rp_at(rp, bits, 0);
   if (W < 8 || M < 64 || M > 65536 || M % 16 || Rmax < 1 || (slot_bytes != 4 && slot_bytes != 8) ||
-      M >= 65536)
+      M >= 65536 || !(pad == 1 || pad == 2 || pad == 4) || (cm && pad != 1))
     return LHPC_ERR_INVALID_ARG;
   const int64_t S = n_cols > 0 ? (n_cols + W - 1) / W : 1;
   if (S > 4096 || nnz + 8 * S >= INT32_MAX || n_rows >= INT32_MAX) return LHPC_ERR_UNSUPPORTED;
@@ -233,6 +233,26 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
     }
     return lo;
   };
+  // nonzeros from e that fit one chunk: M, or with pad > 1 the longest run
+  // whose segments, each padded to a multiple of pad, total ≤ M
+  std::vector<int32_t> tcnt(pad > 1 ? static_cast<size_t>(S) : 0, 0);
+  std::vector<int32_t> touched;
+  auto fit = [&](int64_t e) -> int64_t {
+    if (pad == 1) return M;
+    int64_t k = e, pl = 0;
+    for (; k < nnz; ++k) {
+      const int32_t s = static_cast<int32_t>(col[k] / W);
+      if (tcnt[static_cast<size_t>(s)] % pad == 0) {
+        if (pl + pad > M) break;
+        pl += pad;
+        if (tcnt[static_cast<size_t>(s)] == 0) touched.push_back(s);
+      }
+      ++tcnt[static_cast<size_t>(s)];
+    }
+    for (int32_t s : touched) tcnt[static_cast<size_t>(s)] = 0;
+    touched.clear();
+    return k == nnz ? static_cast<int64_t>(M) : k - e;  // k == nnz: the rest fits
+  };
   // ---- chunks: (ce, cr) pairs; invariant: cr[c] = first row with rp >= ce[c]
   //      (or a row whose predecessors starting at ce[c] are empty)
   o.ce.assign(1, 0);
@@ -245,19 +265,20 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
     int si = 0;  // next split row after r
     while (!(e == nnz && r == n_rows)) {
       int64_t en, rb;
+      const int64_t Mc = fit(e);
       // a split row is done once a chunk starts at it (e == its start, r == it)
       while (si < n_splits && (RP(splits[si]) < e || (RP(splits[si]) == e && splits[si] <= r))) ++si;
-      if (si < n_splits && RP(splits[si]) <= e + M) {
+      if (si < n_splits && RP(splits[si]) <= e + Mc) {
         en = RP(splits[si]);  // a range starts at this row: cut there
         rb = splits[si];
-      } else if (e + M >= nnz) {
+      } else if (e + Mc >= nnz) {
         en = nnz;
         rb = n_rows;
       } else {
-        const int64_t target = e + M;
+        const int64_t target = e + Mc;
         // last row q with rp[q] <= target
         const int64_t q = lower_row(r, target + 1) - 1;
-        if (q >= r && RP(q) > e + M / 2) {
+        if (q >= r && RP(q) > e + Mc / 2) {
           en = RP(q);  // cut at a row start
         } else {
           en = target;  // cut mid-row
@@ -301,6 +322,8 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
   for (int64_t c = 0; c < C; ++c) {
     int32_t *cc = cnt + c * S;
     for (int64_t k = o.ce[c]; k < o.ce[c + 1]; ++k) ++cc[col[k] / W];
+    if (pad > 1)
+      for (int64_t s = 0; s < S; ++s) cc[s] = (cc[s] + pad - 1) / pad * pad;
   }
   std::vector<int64_t> tbase(static_cast<size_t>(S) + 1, 0);
   {
@@ -340,6 +363,12 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
         o.col16[g] = static_cast<uint16_t>(col[k] - s * W);
         o.perm[g] = static_cast<uint16_t>(xtile_slot(static_cast<int>(k - e0), slot_bytes));
       }
+      if (pad > 1)  // segment pads: col16 0 (any tile column), perm = the spare slot M
+        for (int64_t s = 0; s < S; ++s)
+          for (int32_t g = cur[static_cast<size_t>(s)]; g < o.segoff[(c + 1) * S + s]; ++g) {
+            o.col16[g] = 0;
+            o.perm[g] = static_cast<uint16_t>(M);
+          }
     }
   }
   // ---- gather workgroups: each non-empty tile split into pieces of ≈ piece_nnz

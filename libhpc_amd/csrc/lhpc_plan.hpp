@@ -66,6 +66,10 @@ int build_xslice(const void *row_ptr, int rp_bits, const int32_t *col, const voi
 // one L2 — and a whole chunk range before the next (H ranges).
 // cm = false: xg is in tile-stream order (tile, chunk, CSR position), perm is
 // indexed by stream position, and reduce locates its S segments by segoff.
+// pad > 1 (cm = false only): every segment is padded to a multiple of pad
+// (pad entries: col16 0, perm = the spare slot M) so that the reduce loads
+// pad consecutive positions as one aligned vector; chunks are cut so that
+// their padded length stays ≤ M.
 struct XtileHost {
   int S = 0;
   int64_t W = 0;
@@ -91,15 +95,16 @@ struct XtileHost {
 // reduced separately, lhpc_spmv_range); LHPC_ERR_INVALID_ARG otherwise.
 int build_xtile(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_rows,
                 int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm,
-                int slot_bytes, const int64_t *splits, int n_splits, XtileHost &out);
+                int slot_bytes, const int64_t *splits, int n_splits, XtileHost &out,
+                int pad = 1);
 
 // LDS slot of chunk position i in the XTILE seg reduce (lhpc_spmv.hip
-// xt_slot): run t = i/16 holds 16 elements at 16·t, its 16-B slot q at
-// q ^ swz(t), swz = (t/4) % 4 for 4-B elements, (t/2) % 8 for 8-B ones.
+// xt_slot): run t = i/run holds run = 64/elem_bytes elements (64 B) at
+// run·t, its 16-B slot q at q ^ swz(t), swz = (t/4) % 4.
 inline int xtile_slot(int i, int elem_bytes) {
-  const int vw = 16 / elem_bytes, t = i >> 4;
-  const int swz = elem_bytes == 4 ? (t >> 2) & 3 : (t >> 1) & 7;
-  return (i & ~15) | ((((i & 15) / vw) ^ swz) * vw) | (i & (vw - 1));
+  const int vw = 16 / elem_bytes, run = 64 / elem_bytes, t = i / run;
+  const int swz = (t >> 2) & 3;
+  return (i & ~(run - 1)) | ((((i & (run - 1)) / vw) ^ swz) * vw) | (i & (vw - 1));
 }
 
 // in-slice length of row r in slice s

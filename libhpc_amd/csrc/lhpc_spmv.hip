@@ -688,45 +688,50 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
 #define LHPC_XT_RBLK32 512
 #endif
 #ifndef LHPC_XT_RBLK64
-#define LHPC_XT_RBLK64 512
+#define LHPC_XT_RBLK64 1024
 #endif
-// reduce configurations: BLK threads, chunks of M = 16·BLK nonzeros owning
-// ≤ Rmax rows.  BLK = 512 for both types (C2 reduce: 256 → 512 took 470 →
-// 420 µs, 1024 was no faster; C3: 256 → 512 took 1078 → 987 µs at 2 blocks
-// per CU, 73 KB of LDS each)
-template <int BLK> struct XtRed {
-  static constexpr int M = BLK * kXtRun, Rmax = M / 8;
+// reduce configurations: BLK threads, each owning one 64-B run of RUN =
+// 64/sizeof(T) nonzeros (fp32 16, fp64 8); chunks of M = RUN·BLK nonzeros
+// owning ≤ Rmax rows.  A 64-B run keeps LDS per wave at 4 KB for both types,
+// so LDS never caps occupancy below 8 waves per SIMD.  fp32: BLK = 512 (C2
+// reduce: 256 → 512 took 470 → 420 µs, 1024 was no faster).  fp64 with
+// 16-nonzero runs held 8 KB per wave (73 KB per 512-thread block: 2 blocks,
+// 16 waves per CU; C3 reduce 987 µs).
+template <typename T> constexpr int xt_run() { return 64 / static_cast<int>(sizeof(T)); }
+template <typename T, int BLK> struct XtRed {
+  static constexpr int M = BLK * xt_run<T>(), Rmax = M / 8;
 };
 template <typename T> constexpr int xt_red_blk() { return sizeof(T) == 4 ? LHPC_XT_RBLK32 : LHPC_XT_RBLK64; }
 // LDS slot of chunk position i for the seg reduce (lhpc_plan.hpp xtile_slot):
-// run t = i/16 occupies 16·t … 16·t+15 and its 16-B slot q is stored at
+// run t = i/RUN occupies 64 B at 64·t and its 16-B slot q is stored at
 // q ^ xt_swz(t), so the 16 lanes of a ds_read_b128 group hit 16 distinct
-// bank quads
-template <typename T> __device__ __forceinline__ int xt_swz(int t) {
-  return sizeof(T) == 4 ? (t >> 2) & 3 : (t >> 1) & 7;
-}
+// bank quads (4 runs per 256-B bank row, swizzled by the row's index mod 4)
+__device__ __forceinline__ int xt_swz(int t) { return (t >> 2) & 3; }
 template <typename T> __device__ __forceinline__ int xt_slot(int i) {
-  constexpr int VW = 16 / sizeof(T);
-  return (i & ~15) | ((((i & 15) / VW) ^ xt_swz<T>(i >> 4)) * VW) | (i & (VW - 1));
+  constexpr int VW = 16 / sizeof(T), RUN = xt_run<T>();
+  return (i & ~(RUN - 1)) | ((((i & (RUN - 1)) / VW) ^ xt_swz(i / RUN)) * VW) | (i & (VW - 1));
 }
 __device__ __forceinline__ int xt_pidx(int i) { return i + (i >> 4); }
-static_assert(kXtRun == 16, "lhpc_plan.hpp xtile_slot (host perm) assumes 16-element runs");
 
-template <typename T, int G, int BLK>
+template <typename T, int G, int BLK, int P>
 __global__ __launch_bounds__(BLK) void k_xtile_reduce(
     const int32_t *__restrict__ cdesc, const int32_t *__restrict__ segoff, int S, int64_t c0, int64_t C,
     int64_t Cx, int total, const T *__restrict__ xg, const uint16_t *__restrict__ perm,
     const T *__restrict__ val, const int32_t *__restrict__ rp, T *__restrict__ y,
     double *__restrict__ carry) {
-  constexpr int M = XtRed<BLK>::M, RMAX = XtRed<BLK>::Rmax;
+  constexpr int RUN = xt_run<T>(), M = XtRed<T, BLK>::M, RMAX = XtRed<T, BLK>::Rmax;
   constexpr int RPT = (RMAX + 1 + BLK - 1) / BLK;  // row_ptr loads per thread
-  constexpr int NB = M / BLK;                      // 64-position batches per wave (16)
-  constexpr int NWL = M / kWave / kWave;           // batch words per lane (1, 2 or 4)
-  static_assert(NB == 16 && (NWL == 1 || NWL == 2 || NWL == 4), "16 batches per wave; ≤ 256 batches per chunk");
+  constexpr int NB = M / BLK;                      // 64-position batches per wave (= RUN)
+  // P positions per lane in phase A (segments padded to multiples of P, so a
+  // lane's P positions are one aligned vector of xg and of perm): NBP
+  // batches of 64 lanes per wave, M/P bits in the segment-start bitmap
+  constexpr int NBP = NB / P;
+  static_assert((NB == 16 || NB == 8) && (P == 1 || P == 2) && M / P <= 256 * kWave && M >= 4096,
+                "8/16 batches per wave; ≤ 256 batches per chunk; sbm ≥ 128 words");
   typedef T tvec __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
-  constexpr int VW = 16 / sizeof(T), NV = kXtRun / VW;
+  constexpr int VW = 16 / sizeof(T), NV = RUN / VW;
   // dynamic LDS (xtile_lds_bytes): xs[M + VW] T (xt_slot layout; slot M is
-  // the sentinel's spare), bt[BLK/64][16] u32x4, ws[BLK/64] f64,
+  // the sentinel's spare), bt[BLK/64][NB] u32x4, ws[BLK/64] f64,
   // wsf[BLK/64] i32, bm[M/32] u32, sbm[M/32] u32, rpl[RMAX+1] u16 (padded to
   // 4 B), base_ne[S] i32, wsum[8] i32
   extern __shared__ __align__(16) unsigned char smem[];
@@ -743,7 +748,7 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
-  const int i0 = tid * kXtRun;
+  const int i0 = tid * RUN;
   const int64_t c = c0 + static_cast<int64_t>(blockIdx.x % 8) * Cx + blockIdx.x / 8;  // chunk range [c0, C)
   if (c >= C) return;  // block-uniform
   // ---- round trip 1: the chunk descriptor and the segment table (both
@@ -789,6 +794,13 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   const int inc = wave_incl_scan(lsum);
   if (lane == kWave - 1) wsum[wv] = inc;
   __syncthreads();
+  int mf = m;  // flat length of the chunk's (padded) segments
+  if constexpr (P > 1) {
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < BLK / kWave; ++w) tot += wsum[w];
+    mf = tot & 0xFFFF;
+  }
   {
     int run = inc - lsum;
     for (int w = 0; w < wv; ++w) run += wsum[w];
@@ -798,7 +810,7 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
       const int len = sb[q] - sa[q];
       if (len > 0) {
         base_ne[rank] = sa[q] - off;
-        atomicOr(sbm + (off >> 5), 1u << (off & 31));
+        atomicOr(sbm + ((off / P) >> 5), 1u << ((off / P) & 31));
         ++rank;
       }
       off += len;
@@ -807,15 +819,16 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   __syncthreads();
 
   // ---- phase A: src = base_ne[rank] + f, loads of xg/perm (round trip 3);
-  //      positions past m load the sentinel entry `total` (perm: spare slot M)
-  int src[NB];
+  //      positions past mf load the sentinel entry `total` (perm: spare slot M)
+  int src[NBP];
   {
-    // lane q holds batch q's word; its wave-uniform rank terms (w >> 1, base)
-    // go to an LDS triple that the owning wave reads back as a broadcast:
+    // lane q holds batch q's word (a batch = 64 lanes × P positions); its
+    // wave-uniform rank terms (w >> 1, base) go to an LDS triple that the
+    // owning wave reads back as a broadcast:
     //   rank = starts before the batch − 1 + (w & 1) + mbcnt(w >> 1)
-    // lane q holds batch words q (and q + 64 when M = 8192); wave w owns
-    // batches [16w, 16w + 16)
-    const int grp = wv >> 2;  // this wave's batches lie in 64-batch group grp (< NWL)
+    // lane q holds batch words q (and q + 64 … when M/P > 4096); wave w owns
+    // batches [NBP·w, NBP·w + NBP)
+    const int grp = (wv * NBP) >> 6;  // this wave's batches lie in 64-batch group grp
     uint64_t wl = 0;
     int cnt = 0, incl = 0, below = 0;
     for (int g2 = 0; g2 <= grp; ++g2) {  // wave-uniform
@@ -825,32 +838,49 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
       below = __builtin_amdgcn_readlane(incl, kWave - 1);
     }
     u32x4 *bt = bt0 + wv * NB;
-    if ((lane >> 4) == (wv & 3)) {  // lanes holding this wave's batches
+    if (lane / NBP == wv % (kWave / NBP)) {  // lanes holding this wave's batches
       const uint64_t w1 = wl >> 1;
-      bt[lane & (NB - 1)] = u32x4{static_cast<uint32_t>(w1), static_cast<uint32_t>(w1 >> 32),
-                                  static_cast<uint32_t>(incl - cnt - 1 + static_cast<int>(wl & 1u)), 0u};
+      bt[lane & (NBP - 1)] = u32x4{static_cast<uint32_t>(w1), static_cast<uint32_t>(w1 >> 32),
+                                   static_cast<uint32_t>(incl - cnt - 1 + static_cast<int>(wl & 1u)), 0u};
     }
     __builtin_amdgcn_wave_barrier();  // LDS is in order within a wave: no block barrier needed
 #pragma unroll
-    for (int u = 0; u < NB; ++u) {
+    for (int u = 0; u < NBP; ++u) {
       const u32x4 t = bt[u];  // uniform address: broadcast
       const int rk = __builtin_amdgcn_mbcnt_hi(t[1], __builtin_amdgcn_mbcnt_lo(t[0], t[2]));
-      const int f = (wv * NB + u) * kWave + lane;
-      const int sv = base_ne[rk] + f;  // m > 0 ⇒ 0 ≤ rk < S; m = 0: base_ne[−1] (in LDS), unused
-      src[u] = f < m ? sv : total;
+      const int f = ((wv * NBP + u) * kWave + lane) * P;
+      const int sv = base_ne[rk] + f;  // mf > 0 ⇒ 0 ≤ rk < S; mf = 0: base_ne[−1] (in LDS), unused
+      src[u] = f < mf ? sv : total;
     }
   }
-  T xv[NB];
-  uint16_t pv[NB];
+  // plain loads: the segment lines a neighbouring chunk shares must stay in
+  // L2 (non-temporal xg/perm loads: 433 → 555 µs)
+  if constexpr (P == 1) {
+    T xv[NBP];
+    uint16_t pv[NBP];
 #pragma unroll
-  for (int u = 0; u < NB; ++u) {
-    // plain loads: the segment lines a neighbouring chunk shares must stay in
-    // L2 (non-temporal xg/perm loads: 433 → 555 µs)
-    xv[u] = xg[src[u]];
-    pv[u] = perm[src[u]];  // LDS slot xt_slot(position); the sentinel's: M
+    for (int u = 0; u < NBP; ++u) {
+      xv[u] = xg[src[u]];
+      pv[u] = perm[src[u]];  // LDS slot xt_slot(position); the sentinel's: M
+    }
+#pragma unroll
+    for (int u = 0; u < NBP; ++u) xs[pv[u]] = xv[u];
+  } else {
+    // one 2·sizeof(T) xg load and one 4-B perm load per lane and batch
+    typedef T t2 __attribute__((ext_vector_type(2)));
+    t2 xv[NBP];
+    uint32_t pv[NBP];
+#pragma unroll
+    for (int u = 0; u < NBP; ++u) {
+      xv[u] = *reinterpret_cast<const t2 *>(xg + src[u]);
+      pv[u] = *reinterpret_cast<const uint32_t *>(perm + src[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < NBP; ++u) {
+      xs[pv[u] & 0xFFFFu] = xv[u][0];
+      xs[pv[u] >> 16] = xv[u][1];
+    }
   }
-#pragma unroll
-  for (int u = 0; u < NB; ++u) xs[pv[u]] = xv[u];
   // row_ptr (round trip 2) → local row offsets and the row-start bitmap
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
@@ -859,29 +889,29 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
     if (j <= R) rpl[j] = static_cast<uint16_t>(rv[q] <= m ? rv[q] : m + 1);  // > m: continues
     if (j < R && rv[q] < m) atomicOr(bm + (rv[q] >> 5), 1u << (rv[q] & 31));  // empty rows share a bit
   }
-  const int n = m - i0 < kXtRun ? (m - i0 > 0 ? m - i0 : 0) : kXtRun;  // valid entries in the run
-  if (n < kXtRun) {  // the chunk's last run (and runs past m): val and x past m → 0 · 0
-    for (int j = n; j < kXtRun; ++j) xs[xt_slot<T>(i0 + j)] = T(0);
+  const int n = m - i0 < RUN ? (m - i0 > 0 ? m - i0 : 0) : RUN;  // valid entries in the run
+  if (n < RUN) {  // the chunk's last run (and runs past m): val and x past m → 0 · 0
+    for (int j = n; j < RUN; ++j) xs[xt_slot<T>(i0 + j)] = T(0);
 #pragma unroll
-    for (int j = 0; j < kXtRun; ++j) vv[j / VW][j % VW] = j < n ? vv[j / VW][j % VW] : T(0);
+    for (int j = 0; j < RUN; ++j) vv[j / VW][j % VW] = j < n ? vv[j / VW][j % VW] : T(0);
   }
   __syncthreads();
 
   // ---- phase B: branch-free segmented scan of the thread's run.  The fp32
   //      product is exact in fp64, so the fma equals the add of the product.
-  const uint32_t mask = (bm[tid >> 1] >> ((tid & 1) * 16)) & 0xFFFFu;
-  const int hl = mask ? __builtin_ctz(mask) : kXtRun;  // head length (entries before the first start)
+  const uint32_t mask = (bm[i0 >> 5] >> (i0 & 31)) & ((1u << RUN) - 1u);
+  const int hl = mask ? __builtin_ctz(mask) : RUN;  // head length (entries before the first start)
   const int hend = (hl < n ? hl : n) - 1;                // last head position (−1: none)
-  // the run is NV 16-B slots at 16·tid, slot q stored at q ^ xt_swz (conflict-free ds_read_b128)
+  // the run is NV 16-B slots at RUN·tid, slot q stored at q ^ xt_swz (conflict-free ds_read_b128)
   typedef T lvec __attribute__((ext_vector_type(VW)));
   lvec *xr = reinterpret_cast<lvec *>(xs + i0);
-  const int swz = xt_swz<T>(tid);
+  const int swz = xt_swz(tid);
   lvec xq[NV];
 #pragma unroll
   for (int q = 0; q < NV; ++q) xq[q] = xr[q ^ swz];
   double acc = 0.0, hsave = 0.0;
 #pragma unroll
-  for (int j = 0; j < kXtRun; ++j) {
+  for (int j = 0; j < RUN; ++j) {
     acc = ((mask >> j) & 1u) ? 0.0 : acc;
     acc = __builtin_fma(static_cast<double>(vv[j / VW][j % VW]), static_cast<double>(xq[j / VW][j % VW]), acc);
     hsave = j == hend ? acc : hsave;
@@ -912,7 +942,7 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   constexpr int kShr1 = 0x138;  // DPP wave_shr:1 (lane l ← lane l−1; lane 0 keeps `old`)
   const double oin = dpp_f64_old<kShr1>(cw, sv);                                 // S(t−1)
   const int fin = __builtin_amdgcn_update_dpp(gw, fin_incl, kShr1, 0xF, 0xF, false);  // starts before run t
-  const int tlast = m > 0 ? (m - 1) / kXtRun : -1;
+  const int tlast = m > 0 ? (m - 1) / RUN : -1;
   if (tid == 0 && !(m > 0 && rpl[0] > 0)) carry[2 * c] = 0.0;  // no head piece
   if (has_head) {
     const int i1 = i0 + n;
@@ -1225,6 +1255,7 @@ struct lhpc_spmv_plan {
   int32_t *d_ce = nullptr, *d_cr = nullptr, *d_segoff = nullptr, *d_pieces = nullptr, *d_cont = nullptr;
   uint16_t *d_col16 = nullptr, *d_perm = nullptr;
   int xt_cm = 0;  // chunk-major xg (XtileHost::cm)
+  int xt_p = 1;   // reduce phase A positions per lane (segments padded to multiples of xt_p)
   int32_t *d_gdst = nullptr;
   void *d_xg = nullptr;
   double *d_carry = nullptr;
@@ -1412,8 +1443,8 @@ int launch_xslice(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s
 
 template <typename T>
 size_t xtile_lds_bytes(int S) {
-  constexpr int BLK = xt_red_blk<T>(), M = XtRed<BLK>::M, RMAX = XtRed<BLK>::Rmax, W = BLK / kWave;
-  return static_cast<size_t>(M + 16 / sizeof(T)) * sizeof(T) + W * 16 * 16 + W * (sizeof(double) + 4) +
+  constexpr int BLK = xt_red_blk<T>(), M = XtRed<T, BLK>::M, RMAX = XtRed<T, BLK>::Rmax, W = BLK / kWave;
+  return static_cast<size_t>(M + 16 / sizeof(T)) * sizeof(T) + W * xt_run<T>() * 16 + W * (sizeof(double) + 4) +
          2 * M / 32 * sizeof(uint32_t) + ((RMAX + 2) & ~1) * sizeof(uint16_t) +
          sizeof(int32_t) * (static_cast<size_t>(S) + 8);
 }
@@ -1424,8 +1455,13 @@ int xtile_g(int S) {
   return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : g <= 8 ? 8 : 16;
 }
 
-template <typename T, int G>
-const void *xtile_reduce_fn() { return reinterpret_cast<const void *>(k_xtile_reduce<T, G, xt_red_blk<T>()>); }
+template <typename T, int G, int P>
+const void *xtile_reduce_fn() { return reinterpret_cast<const void *>(k_xtile_reduce<T, G, xt_red_blk<T>(), P>); }
+template <typename T, int P>
+const void *xtile_reduce_fn(int g) {
+  return g == 1 ? xtile_reduce_fn<T, 1, P>() : g == 2 ? xtile_reduce_fn<T, 2, P>() : g == 4 ? xtile_reduce_fn<T, 4, P>()
+         : g == 8 ? xtile_reduce_fn<T, 8, P>() : xtile_reduce_fn<T, 16, P>();
+}
 
 template <typename T>
 int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
@@ -1467,11 +1503,18 @@ int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s)
     const int64_t Cx = (c1 - c0 + 7) / 8;
     constexpr int BLK = xt_red_blk<T>();
     const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(BLK);
-#define LHPC_XT_RED(GG)                                                                               \
-  hipLaunchKernelGGL((k_xtile_reduce<T, GG, BLK>), rg, rb, p->xt_lds, rs, p->d_cdesc, p->d_segoff, p->S, \
+#define LHPC_XT_RED1(GG, PP)                                                                             \
+  hipLaunchKernelGGL((k_xtile_reduce<T, GG, BLK, PP>), rg, rb, p->xt_lds, rs, p->d_cdesc, p->d_segoff, p->S, \
                      c0, c1, Cx, static_cast<int>(p->xt_total), xg, p->d_perm,                         \
                      static_cast<const T *>(p->d_val),                                                 \
                      static_cast<const int32_t *>(p->d_row_ptr), static_cast<T *>(y), p->d_carry)
+#define LHPC_XT_RED(GG) \
+  do {                     \
+    if (p->xt_p == 2)      \
+      LHPC_XT_RED1(GG, 2); \
+    else                   \
+      LHPC_XT_RED1(GG, 1); \
+  } while (0)
     switch (xtile_g<T>(p->S)) {
       case 1: LHPC_XT_RED(1); break;
       case 2: LHPC_XT_RED(2); break;
@@ -1480,6 +1523,7 @@ int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s)
       default: LHPC_XT_RED(16); break;
     }
 #undef LHPC_XT_RED
+#undef LHPC_XT_RED1
     return check_launch(rs);
   };
   if (p->xt_K <= 1) {
@@ -1530,11 +1574,18 @@ int launch_xtile_range(const lhpc_spmv_plan *p, int k, void *yk, hipStream_t s) 
     const int64_t Cx = (c1 - c0 + 7) / 8;
     constexpr int BLK = xt_red_blk<T>();
     const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(BLK);
-#define LHPC_XT_RED(GG)                                                                               \
-  hipLaunchKernelGGL((k_xtile_reduce<T, GG, BLK>), rg, rb, p->xt_lds, s, p->d_cdesc, p->d_segoff, p->S, \
+#define LHPC_XT_RED1(GG, PP)                                                                             \
+  hipLaunchKernelGGL((k_xtile_reduce<T, GG, BLK, PP>), rg, rb, p->xt_lds, s, p->d_cdesc, p->d_segoff, p->S, \
                      c0, c1, Cx, static_cast<int>(p->xt_total), xg, p->d_perm,                         \
                      static_cast<const T *>(p->d_val), static_cast<const int32_t *>(p->d_row_ptr), y,  \
                      p->d_carry)
+#define LHPC_XT_RED(GG) \
+  do {                     \
+    if (p->xt_p == 2)      \
+      LHPC_XT_RED1(GG, 2); \
+    else                   \
+      LHPC_XT_RED1(GG, 1); \
+  } while (0)
     switch (xtile_g<T>(p->S)) {
       case 1: LHPC_XT_RED(1); break;
       case 2: LHPC_XT_RED(2); break;
@@ -1543,6 +1594,7 @@ int launch_xtile_range(const lhpc_spmv_plan *p, int k, void *yk, hipStream_t s) 
       default: LHPC_XT_RED(16); break;
     }
 #undef LHPC_XT_RED
+#undef LHPC_XT_RED1
     LHPC_TRY(check_launch(s));
   }
   const int64_t n0 = p->xt_sco[k], n1 = p->xt_sco[k + 1];
@@ -1621,11 +1673,17 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   if (const char *env = std::getenv("LHPC_XTILE_LAYOUT")) cm = std::strcmp(env, "cm") == 0;
   p->xt_cm = cm;
   // chunking: the seg reduce's M / Rmax for this type; the cm reduce's fixed 4096 / 512
-  const int cM = cm ? kXtM : (tsz == 4 ? XtRed<xt_red_blk<float>()>::M : XtRed<xt_red_blk<double>()>::M);
-  const int cR = cm ? kXtRmax : (tsz == 4 ? XtRed<xt_red_blk<float>()>::Rmax : XtRed<xt_red_blk<double>()>::Rmax);
+  const int cM = cm ? kXtM : (tsz == 4 ? XtRed<float, xt_red_blk<float>()>::M : XtRed<double, xt_red_blk<double>()>::M);
+  const int cR = cm ? kXtRmax : (tsz == 4 ? XtRed<float, xt_red_blk<float>()>::Rmax : XtRed<double, xt_red_blk<double>()>::Rmax);
+  // reduce positions per lane (LHPC_XTILE_PAIR=0/1): 2 pads every
+  // (chunk, tile) segment to an even length, so phase A loads xg/perm as
+  // aligned pairs (DESIGN.md §4 XTILE)
+  int pp = 1;
+  if (const char *env = std::getenv("LHPC_XTILE_PAIR")) pp = std::atoi(env) ? 2 : 1;
+  p->xt_p = cm ? 1 : pp;
   const int bst = build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, cM, cR, piece,
                               cm != 0, static_cast<int>(tsz), p->split_rows.data(),
-                              static_cast<int>(p->split_rows.size()), xt);
+                              static_cast<int>(p->split_rows.size()), xt, p->xt_p);
   if (bst != LHPC_OK) return bst;
   p->kernel = LHPC_KERNEL_XTILE;
   p->rp64 = 0;
@@ -1642,13 +1700,8 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   }
   if (!cm) {
     const int g = tsz == 4 ? xtile_g<float>(xt.S) : xtile_g<double>(xt.S);
-    const void *kfn =
-        tsz == 4 ? (g == 1 ? xtile_reduce_fn<float, 1>() : g == 2 ? xtile_reduce_fn<float, 2>()
-                    : g == 4 ? xtile_reduce_fn<float, 4>() : g == 8 ? xtile_reduce_fn<float, 8>()
-                             : xtile_reduce_fn<float, 16>())
-                 : (g == 1 ? xtile_reduce_fn<double, 1>() : g == 2 ? xtile_reduce_fn<double, 2>()
-                    : g == 4 ? xtile_reduce_fn<double, 4>() : g == 8 ? xtile_reduce_fn<double, 8>()
-                             : xtile_reduce_fn<double, 16>());
+    const void *kfn = tsz == 4 ? (p->xt_p == 2 ? xtile_reduce_fn<float, 2>(g) : xtile_reduce_fn<float, 1>(g))
+                               : (p->xt_p == 2 ? xtile_reduce_fn<double, 2>(g) : xtile_reduce_fn<double, 1>(g));
     LHPC_HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
   }
   const int64_t n_rows = p->n_rows, nnz = p->nnz, C = xt.n_chunks;
@@ -1690,13 +1743,14 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_segoff), xt.segoff.data(), xt.segoff.size() * 4));
     // one sentinel entry past the stream: reduce loads it for positions past m,
     // and its perm is the byte offset of the spare LDS slot M + M/16 − 1
-    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), nullptr, static_cast<size_t>(xt.total + 1) * 2));
+    // (xt_p entries: a pair-mode lane loads the sentinel pair)
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), nullptr, static_cast<size_t>(xt.total + 2) * 2));
     if (xt.total) LHPC_HIP_TRY(hipMemcpy(p->d_perm, xt.perm.get(), static_cast<size_t>(xt.total) * 2, hipMemcpyHostToDevice));
     {
-      const uint16_t spare = static_cast<uint16_t>(cM);  // slot M: one 16-B slot past the chunk
-      LHPC_HIP_TRY(hipMemcpy(p->d_perm + xt.total, &spare, 2, hipMemcpyHostToDevice));
+      const uint16_t spare[2] = {static_cast<uint16_t>(cM), static_cast<uint16_t>(cM)};  // slot M: one 16-B slot past the chunk
+      LHPC_HIP_TRY(hipMemcpy(p->d_perm + xt.total, spare, 4, hipMemcpyHostToDevice));
     }
-    LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total + 1) * tsz));
+    LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total + 2) * tsz));
   }
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_carry), nullptr, static_cast<size_t>(2 * C + 2) * 8));
   LHPC_HIP_TRY(hipMemset(p->d_carry, 0, static_cast<size_t>(2 * C + 2) * 8));

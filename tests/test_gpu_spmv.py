@@ -257,10 +257,13 @@ def _csr_from_lengths(lengths, n_cols, seed, dyadic):
     return rp, col, val
 
 
-@pytest.fixture(params=["seg", "cm"])
+@pytest.fixture(params=["seg", "cm", "pair"])
 def xt_layout(request, monkeypatch):
-    """Both XTILE layouts: tile-stream xg + segment table (default) and chunk-major xg."""
-    monkeypatch.setenv("LHPC_XTILE_LAYOUT", request.param)
+    """The XTILE layouts: tile-stream xg + segment table (default), chunk-major
+    xg, and the tile stream with segments padded to even lengths
+    (LHPC_XTILE_PAIR=1: the reduce loads xg/perm as aligned pairs)."""
+    monkeypatch.setenv("LHPC_XTILE_LAYOUT", "cm" if request.param == "cm" else "seg")
+    monkeypatch.setenv("LHPC_XTILE_PAIR", "1" if request.param == "pair" else "0")
     return request.param
 
 
