@@ -1238,7 +1238,7 @@ struct lhpc_spmv_plan {
   // XTILE
   int64_t xt_C = 0, xt_pieces = 0, xt_cont = 0, xt_total = 0;
   size_t xt_lds = 0;
-  int xt_u = 4;
+  int xt_u = 8;  // gather steps in flight (LHPC_XTILE_U; the chunk-major gather caps it at 4)
   // pipelined seg calls: K chunk ranges; range k's gather runs on the caller's
   // stream, its reduce on xt_s2 once the gather's event fires, so range k's
   // reduce overlaps range k+1's gather
@@ -1493,6 +1493,12 @@ int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s)
     if (p->xt_u == 2)
       hipLaunchKernelGGL((k_xtile_gather<T, 2>), g, b, 0, s, pieces, p->d_col16,
                          static_cast<const T *>(x), p->n_cols, xg);
+    else if (p->xt_u == 16)
+      hipLaunchKernelGGL((k_xtile_gather<T, 16>), g, b, 0, s, pieces, p->d_col16,
+                         static_cast<const T *>(x), p->n_cols, xg);
+    else if (p->xt_u == 8)
+      hipLaunchKernelGGL((k_xtile_gather<T, 8>), g, b, 0, s, pieces, p->d_col16,
+                         static_cast<const T *>(x), p->n_cols, xg);
     else
       hipLaunchKernelGGL((k_xtile_gather<T, 4>), g, b, 0, s, pieces, p->d_col16,
                          static_cast<const T *>(x), p->n_cols, xg);
@@ -1558,6 +1564,12 @@ int launch_xtile_stage(const lhpc_spmv_plan *p, const void *x, hipStream_t s) {
   T *xg = static_cast<T *>(p->d_xg);
   if (p->xt_u == 2)
     hipLaunchKernelGGL((k_xtile_gather<T, 2>), g, b, 0, s, p->d_pieces, p->d_col16,
+                       static_cast<const T *>(x), p->n_cols, xg);
+  else if (p->xt_u == 16)
+    hipLaunchKernelGGL((k_xtile_gather<T, 16>), g, b, 0, s, p->d_pieces, p->d_col16,
+                       static_cast<const T *>(x), p->n_cols, xg);
+  else if (p->xt_u == 8)
+    hipLaunchKernelGGL((k_xtile_gather<T, 8>), g, b, 0, s, p->d_pieces, p->d_col16,
                        static_cast<const T *>(x), p->n_cols, xg);
   else
     hipLaunchKernelGGL((k_xtile_gather<T, 4>), g, b, 0, s, p->d_pieces, p->d_col16,
@@ -1696,7 +1708,7 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   p->xt_lds = tsz == 4 ? xtile_lds_bytes<float>(xt.S) : xtile_lds_bytes<double>(xt.S);
   if (const char *env = std::getenv("LHPC_XTILE_U")) {
     const int u = std::atoi(env);
-    p->xt_u = u <= 1 && cm ? 1 : u == 2 ? 2 : 4;  // U = 1: chunk-major gather only
+    p->xt_u = u <= 1 && cm ? 1 : u == 2 ? 2 : u >= 16 && !cm ? 16 : u >= 8 && !cm ? 8 : 4;  // U = 1: chunk-major gather only; 8: tile-stream only
   }
   if (!cm) {
     const int g = tsz == 4 ? xtile_g<float>(xt.S) : xtile_g<double>(xt.S);

@@ -320,8 +320,10 @@ def test_xtile_small_gather_pieces(lhpc, gpu, monkeypatch, xt_layout):
     rng = np.random.default_rng(0xA400)
     lengths = rng.integers(0, 60, size=20_000)
     _check_xtile(lhpc, gpu, lengths, 100_000, np.float32, 0xA401)
-    monkeypatch.setenv("LHPC_XTILE_U", "2")
-    _check_xtile(lhpc, gpu, lengths, 100_000, np.float64, 0xA402)
+    for u in ("2", "4", "16"):  # gather steps in flight (default 8)
+        monkeypatch.setenv("LHPC_XTILE_U", u)
+        _check_xtile(lhpc, gpu, lengths, 100_000, np.float64, 0xA402)
+        _check_xtile(lhpc, gpu, lengths, 100_000, np.float32, 0xA403)
 
 
 @pytest.mark.parametrize("ranges", ["2", "5"])
