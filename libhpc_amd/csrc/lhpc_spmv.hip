@@ -600,6 +600,9 @@ template <> struct XtTile<float> { static constexpr int W = 40960; };   // 160 K
 template <> struct XtTile<double> { static constexpr int W = 20480; };  // 160 KB
 
 
+#ifndef LHPC_XT_GATHER_PRE
+#define LHPC_XT_GATHER_PRE 1
+#endif
 // gather: block b streams pieces[3b..3b+1] of tile pieces[3b+2]; 8 nonzeros
 // per thread and step (one 16-B col16 load, 8 LDS gathers, 8 contiguous xg
 // stores), U steps in flight.  Piece bounds are multiples of 8.
@@ -614,6 +617,19 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
   const int64_t c0 = static_cast<int64_t>(pieces[3 * blockIdx.x + 2]) * W;
   const int wlen = static_cast<int>((n_cols - c0) < W ? (n_cols - c0) : W);
   constexpr int PT = W / kXtGatherBlock;
+  const int q0 = g0 >> 3, q1 = g1 >> 3;  // 8-entry groups
+  const u32x4 *cv = reinterpret_cast<const u32x4 *>(col16);
+  u32x4 w[U];
+  auto load_w = [&](int q) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int qq = q + u * kXtGatherBlock;
+      w[u] = qq < q1 ? __builtin_nontemporal_load(cv + qq) : u32x4{0, 0, 0, 0};
+    }
+  };
+#if LHPC_XT_GATHER_PRE
+  load_w(q0 + tid);  // the first col16 step does not depend on the tile: issue it under the tile load
+#endif
   T tv[PT];
 #pragma unroll
   for (int i = 0; i < PT; ++i) {
@@ -623,15 +639,12 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
 #pragma unroll
   for (int i = 0; i < PT; ++i) xt[i * kXtGatherBlock + tid] = tv[i];
   __syncthreads();
-  const int q0 = g0 >> 3, q1 = g1 >> 3;  // 8-entry groups
-  const u32x4 *cv = reinterpret_cast<const u32x4 *>(col16);
   for (int q = q0 + tid; q < q1; q += U * kXtGatherBlock) {
-    u32x4 w[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int qq = q + u * kXtGatherBlock;
-      w[u] = qq < q1 ? __builtin_nontemporal_load(cv + qq) : u32x4{0, 0, 0, 0};
-    }
+#if LHPC_XT_GATHER_PRE
+    if (q != q0 + tid) load_w(q);
+#else
+    load_w(q);
+#endif
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int qq = q + u * kXtGatherBlock;
