@@ -211,10 +211,10 @@ int build_xtile_cm(const int32_t *col, int64_t nnz, int64_t piece_nnz, XtileHost
 
 int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
                 int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm, int slot_bytes,
-                const int64_t *splits, int n_splits, XtileHost &o, int pad) {
+                const int64_t *splits, int n_splits, XtileHost &o, int pad, bool iperm) {
   const int64_t nnz = rp_at(rp, bits, n_rows) - rp_at(rp, bits, 0);
   if (W < 8 || M < 64 || M > 65536 || M % 16 || Rmax < 1 || (slot_bytes != 4 && slot_bytes != 8) ||
-      M >= 65536 || !(pad == 1 || pad == 2 || pad == 4) || (cm && pad != 1))
+      M >= 65536 || !(pad == 1 || pad == 2 || pad == 4) || (cm && pad != 1) || (iperm && (cm || pad != 1)))
     return LHPC_ERR_INVALID_ARG;
   const int64_t S = n_cols > 0 ? (n_cols + W - 1) / W : 1;
   if (S > 4096 || nnz + 8 * S >= INT32_MAX || n_rows >= INT32_MAX) return LHPC_ERR_UNSUPPORTED;
@@ -350,18 +350,29 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
   // ---- scatter (stable: CSR order inside each segment)
   o.col16.reset(new uint16_t[o.total > 0 ? o.total : 1]());
   o.perm.reset(new uint16_t[o.total > 0 ? o.total : 1]());
+  if (iperm) o.iperm.reset(new uint16_t[static_cast<size_t>(C > 0 ? C : 1) * M]());
 #pragma omp parallel
   {
-    std::vector<int32_t> cur(static_cast<size_t>(S));
+    std::vector<int32_t> cur(static_cast<size_t>(S)), flat(iperm ? static_cast<size_t>(S) : 0);
 #pragma omp for schedule(dynamic, 64)
     for (int64_t c = 0; c < C; ++c) {
       std::memcpy(cur.data(), o.segoff.data() + c * S, sizeof(int32_t) * static_cast<size_t>(S));
+      if (iperm) {  // flat offset of each tile's segment in the chunk's concatenation
+        int32_t f = 0;
+        for (int64_t s = 0; s < S; ++s) {
+          flat[static_cast<size_t>(s)] = f;
+          f += o.segoff[(c + 1) * S + s] - o.segoff[c * S + s];
+        }
+      }
       const int64_t e0 = o.ce[c];
       for (int64_t k = e0; k < o.ce[c + 1]; ++k) {
         const int64_t s = col[k] / W;
         const int32_t g = cur[static_cast<size_t>(s)]++;
         o.col16[g] = static_cast<uint16_t>(col[k] - s * W);
         o.perm[g] = static_cast<uint16_t>(xtile_slot(static_cast<int>(k - e0), slot_bytes));
+        if (iperm)
+          o.iperm[static_cast<size_t>(c) * M + static_cast<size_t>(k - e0)] =
+              static_cast<uint16_t>(flat[static_cast<size_t>(s)] + (g - o.segoff[c * S + s]));
       }
       if (pad > 1)  // segment pads: col16 0 (any tile column), perm = the spare slot M
         for (int64_t s = 0; s < S; ++s)

@@ -85,6 +85,10 @@ struct XtileHost {
   std::unique_ptr<uint16_t[]> col16;  // [total]
   std::unique_ptr<uint16_t[]> perm;   // [total] (cm: [nnz])
   std::unique_ptr<int32_t[]> gdst;    // cm: [total / 8]
+  // iperm mode: [n_chunks·M] — for CSR position i of chunk c, iperm[c·M + i]
+  // is its flat position in the chunk's segment concatenation (tiles
+  // ascending); perm is then not used by the reduce
+  std::unique_ptr<uint16_t[]> iperm;
 };
 
 // 0 on success; LHPC_ERR_UNSUPPORTED when the layout does not fit its
@@ -96,7 +100,7 @@ struct XtileHost {
 int build_xtile(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_rows,
                 int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm,
                 int slot_bytes, const int64_t *splits, int n_splits, XtileHost &out,
-                int pad = 1);
+                int pad = 1, bool iperm = false);
 
 // LDS slot of chunk position i in the XTILE seg reduce (lhpc_spmv.hip
 // xt_slot): run t = i/run holds run = 64/elem_bytes elements (64 B) at

@@ -726,8 +726,14 @@ template <typename T> __device__ __forceinline__ int xt_slot(int i) {
 }
 __device__ __forceinline__ int xt_pidx(int i) { return i + (i >> 4); }
 
+#ifndef LHPC_XT_IP_DMA
+#define LHPC_XT_IP_DMA 1  // iperm reduce, fp32: xg → LDS by global_load_lds (no VGPRs)
+#endif
+#ifndef LHPC_XT_IP_WAVES
+#define LHPC_XT_IP_WAVES 8  // iperm reduce: 8 waves/SIMD (fp32 66 → 64 VGPRs + 8 B spill: C2 593 → 580 µs)
+#endif
 template <typename T, int G, int BLK, int P>
-__global__ __launch_bounds__(BLK) void k_xtile_reduce(
+__global__ __launch_bounds__(BLK, P == 3 ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce(
     const int32_t *__restrict__ cdesc, const int32_t *__restrict__ segoff, int S, int64_t c0, int64_t C,
     int64_t Cx, int total, const T *__restrict__ xg, const uint16_t *__restrict__ perm,
     const T *__restrict__ val, const int32_t *__restrict__ rp, T *__restrict__ y,
@@ -738,8 +744,13 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   // P positions per lane in phase A (segments padded to multiples of P, so a
   // lane's P positions are one aligned vector of xg and of perm): NBP
   // batches of 64 lanes per wave, M/P bits in the segment-start bitmap
-  constexpr int NBP = NB / P;
-  static_assert((NB == 16 || NB == 8) && (P == 1 || P == 2) && M / P <= 256 * kWave && M >= 4096,
+  // P = 3 (iperm mode): one position per lane; phase A stores xg in flat
+  // (segment concatenation) order and phase B gathers each CSR position's x
+  // through iperm (CSR order, read with val) instead of scattering by perm
+  constexpr bool IP = P == 3;
+  constexpr int PP = IP ? 1 : P;
+  constexpr int NBP = NB / PP;
+  static_assert((NB == 16 || NB == 8) && (PP == 1 || PP == 2) && M / PP <= 256 * kWave && M >= 4096,
                 "8/16 batches per wave; ≤ 256 batches per chunk; sbm ≥ 128 words");
   typedef T tvec __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
   constexpr int VW = 16 / sizeof(T), NV = RUN / VW;
@@ -787,6 +798,13 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
 #pragma unroll
     for (int q = 0; q < NV; ++q) vv[q] = __builtin_nontemporal_load(vp + q);
   }
+  constexpr int NIP = IP ? RUN * 2 / 16 : 1;  // 16-B iperm vectors per run
+  u32x4 ipv[NIP];
+  if constexpr (IP) {  // perm points at iperm: [chunk][M] u16, CSR order
+    const u32x4 *ip = reinterpret_cast<const u32x4 *>(perm + c * M + i0);
+#pragma unroll
+    for (int q = 0; q < NIP; ++q) ipv[q] = __builtin_nontemporal_load(ip + q);
+  }
   int rv[RPT];
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
@@ -808,7 +826,7 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   if (lane == kWave - 1) wsum[wv] = inc;
   __syncthreads();
   int mf = m;  // flat length of the chunk's (padded) segments
-  if constexpr (P > 1) {
+  if constexpr (PP > 1) {
     int tot = 0;
 #pragma unroll
     for (int w = 0; w < BLK / kWave; ++w) tot += wsum[w];
@@ -823,7 +841,7 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
       const int len = sb[q] - sa[q];
       if (len > 0) {
         base_ne[rank] = sa[q] - off;
-        atomicOr(sbm + ((off / P) >> 5), 1u << ((off / P) & 31));
+        atomicOr(sbm + ((off / PP) >> 5), 1u << ((off / PP) & 31));
         ++rank;
       }
       off += len;
@@ -861,14 +879,35 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
     for (int u = 0; u < NBP; ++u) {
       const u32x4 t = bt[u];  // uniform address: broadcast
       const int rk = __builtin_amdgcn_mbcnt_hi(t[1], __builtin_amdgcn_mbcnt_lo(t[0], t[2]));
-      const int f = ((wv * NBP + u) * kWave + lane) * P;
+      const int f = ((wv * NBP + u) * kWave + lane) * PP;
       const int sv = base_ne[rk] + f;  // mf > 0 ⇒ 0 ≤ rk < S; mf = 0: base_ne[−1] (in LDS), unused
       src[u] = f < mf ? sv : total;
     }
   }
   // plain loads: the segment lines a neighbouring chunk shares must stay in
   // L2 (non-temporal xg/perm loads: 433 → 555 µs)
-  if constexpr (P == 1) {
+  if constexpr (IP) {
+    // flat order: lane-linear LDS stores (no perm loads, no scatter)
+#if LHPC_XT_IP_DMA
+    if constexpr (sizeof(T) == 4) {
+      // LDS-DMA: each lane's xg element lands at the batch's base + 4·lane
+      // (exactly the flat order), no VGPR destination; drained by the
+      // vmcnt(0) before the barrier below
+#pragma unroll
+      for (int u = 0; u < NBP; ++u)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(xg + src[u]),
+                                         (__attribute__((address_space(3))) void *)(xs + (wv * NBP + u) * kWave),
+                                         4, 0, 0);
+    } else
+#endif
+    {
+      T xv[NBP];
+#pragma unroll
+      for (int u = 0; u < NBP; ++u) xv[u] = xg[src[u]];
+#pragma unroll
+      for (int u = 0; u < NBP; ++u) xs[(wv * NBP + u) * kWave + lane] = xv[u];
+    }
+  } else if constexpr (P == 1) {
     T xv[NBP];
     uint16_t pv[NBP];
 #pragma unroll
@@ -904,7 +943,8 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   }
   const int n = m - i0 < RUN ? (m - i0 > 0 ? m - i0 : 0) : RUN;  // valid entries in the run
   if (n < RUN) {  // the chunk's last run (and runs past m): val and x past m → 0 · 0
-    for (int j = n; j < RUN; ++j) xs[xt_slot<T>(i0 + j)] = T(0);
+    if constexpr (!IP)
+      for (int j = n; j < RUN; ++j) xs[xt_slot<T>(i0 + j)] = T(0);
 #pragma unroll
     for (int j = 0; j < RUN; ++j) vv[j / VW][j % VW] = j < n ? vv[j / VW][j % VW] : T(0);
   }
@@ -920,8 +960,24 @@ __global__ __launch_bounds__(BLK) void k_xtile_reduce(
   lvec *xr = reinterpret_cast<lvec *>(xs + i0);
   const int swz = xt_swz(tid);
   lvec xq[NV];
+  if constexpr (IP) {
+    // gather the run's x from the flat array, then (after every thread has
+    // read) the running sums below go back in the CSR (xt_slot) layout
+    // unconditional reads (iperm past m is 0, a valid slot), so all RUN
+    // ds_reads issue before the first wait; then x past m → 0
+    T gx[RUN];
 #pragma unroll
-  for (int q = 0; q < NV; ++q) xq[q] = xr[q ^ swz];
+    for (int j = 0; j < RUN; ++j) {
+      const uint32_t w = ipv[j / 8][(j % 8) / 2];
+      gx[j] = xs[static_cast<int>((j & 1) ? (w >> 16) : (w & 0xFFFFu))];
+    }
+#pragma unroll
+    for (int j = 0; j < RUN; ++j) xq[j / VW][j % VW] = j < n ? gx[j] : T(0);
+    __syncthreads();
+  } else {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) xq[q] = xr[q ^ swz];
+  }
   double acc = 0.0, hsave = 0.0;
 #pragma unroll
   for (int j = 0; j < RUN; ++j) {
@@ -1531,6 +1587,8 @@ int launch_xtile(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s)
   do {                     \
     if (p->xt_p == 2)      \
       LHPC_XT_RED1(GG, 2); \
+    else if (p->xt_p == 3) \
+      LHPC_XT_RED1(GG, 3); \
     else                   \
       LHPC_XT_RED1(GG, 1); \
   } while (0)
@@ -1608,6 +1666,8 @@ int launch_xtile_range(const lhpc_spmv_plan *p, int k, void *yk, hipStream_t s) 
   do {                     \
     if (p->xt_p == 2)      \
       LHPC_XT_RED1(GG, 2); \
+    else if (p->xt_p == 3) \
+      LHPC_XT_RED1(GG, 3); \
     else                   \
       LHPC_XT_RED1(GG, 1); \
   } while (0)
@@ -1703,12 +1763,18 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   // reduce positions per lane (LHPC_XTILE_PAIR=0/1): 2 pads every
   // (chunk, tile) segment to an even length, so phase A loads xg/perm as
   // aligned pairs (DESIGN.md §4 XTILE)
-  int pp = 1;
-  if (const char *env = std::getenv("LHPC_XTILE_PAIR")) pp = std::atoi(env) ? 2 : 1;
+  // xt_p = 3 (default; LHPC_XTILE_IPERM=0 selects the perm scatter, 1): the
+  // reduce keeps the chunk's segments in flat order in LDS and gathers each
+  // CSR position's x through iperm (CSR order, read with val) instead of
+  // scattering them by perm (DESIGN.md §4 XTILE: C2 589 → 580 µs, C3 1169 → 1086 µs)
+  int pp = 3;
+  if (const char *env = std::getenv("LHPC_XTILE_IPERM")) pp = std::atoi(env) ? 3 : 1;
+  if (const char *env = std::getenv("LHPC_XTILE_PAIR")) pp = std::atoi(env) ? 2 : pp;
   p->xt_p = cm ? 1 : pp;
   const int bst = build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, cM, cR, piece,
                               cm != 0, static_cast<int>(tsz), p->split_rows.data(),
-                              static_cast<int>(p->split_rows.size()), xt, p->xt_p);
+                              static_cast<int>(p->split_rows.size()), xt, p->xt_p == 2 ? 2 : 1,
+                              p->xt_p == 3);
   if (bst != LHPC_OK) return bst;
   p->kernel = LHPC_KERNEL_XTILE;
   p->rp64 = 0;
@@ -1725,8 +1791,12 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   }
   if (!cm) {
     const int g = tsz == 4 ? xtile_g<float>(xt.S) : xtile_g<double>(xt.S);
-    const void *kfn = tsz == 4 ? (p->xt_p == 2 ? xtile_reduce_fn<float, 2>(g) : xtile_reduce_fn<float, 1>(g))
-                               : (p->xt_p == 2 ? xtile_reduce_fn<double, 2>(g) : xtile_reduce_fn<double, 1>(g));
+    const void *kfn = tsz == 4 ? (p->xt_p == 2   ? xtile_reduce_fn<float, 2>(g)
+                                  : p->xt_p == 3 ? xtile_reduce_fn<float, 3>(g)
+                                                 : xtile_reduce_fn<float, 1>(g))
+                               : (p->xt_p == 2   ? xtile_reduce_fn<double, 2>(g)
+                                  : p->xt_p == 3 ? xtile_reduce_fn<double, 3>(g)
+                                                 : xtile_reduce_fn<double, 1>(g));
     LHPC_HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
   }
   const int64_t n_rows = p->n_rows, nnz = p->nnz, C = xt.n_chunks;
@@ -1769,9 +1839,12 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
     // one sentinel entry past the stream: reduce loads it for positions past m,
     // and its perm is the byte offset of the spare LDS slot M + M/16 − 1
     // (xt_p entries: a pair-mode lane loads the sentinel pair)
-    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), nullptr, static_cast<size_t>(xt.total + 2) * 2));
-    if (xt.total) LHPC_HIP_TRY(hipMemcpy(p->d_perm, xt.perm.get(), static_cast<size_t>(xt.total) * 2, hipMemcpyHostToDevice));
-    {
+    if (p->xt_p == 3) {  // iperm mode: the reduce reads iperm ([C][M], CSR order) in perm's place
+      const size_t ni = static_cast<size_t>(C > 0 ? C : 1) * static_cast<size_t>(cM);
+      LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), xt.iperm.get(), ni * 2));
+    } else {
+      LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), nullptr, static_cast<size_t>(xt.total + 2) * 2));
+      if (xt.total) LHPC_HIP_TRY(hipMemcpy(p->d_perm, xt.perm.get(), static_cast<size_t>(xt.total) * 2, hipMemcpyHostToDevice));
       const uint16_t spare[2] = {static_cast<uint16_t>(cM), static_cast<uint16_t>(cM)};  // slot M: one 16-B slot past the chunk
       LHPC_HIP_TRY(hipMemcpy(p->d_perm + xt.total, spare, 4, hipMemcpyHostToDevice));
     }

@@ -257,13 +257,16 @@ def _csr_from_lengths(lengths, n_cols, seed, dyadic):
     return rp, col, val
 
 
-@pytest.fixture(params=["seg", "cm", "pair"])
+@pytest.fixture(params=["seg", "cm", "pair", "iperm"])
 def xt_layout(request, monkeypatch):
     """The XTILE layouts: tile-stream xg + segment table (default), chunk-major
-    xg, and the tile stream with segments padded to even lengths
-    (LHPC_XTILE_PAIR=1: the reduce loads xg/perm as aligned pairs)."""
+    xg, the tile stream with segments padded to even lengths
+    (LHPC_XTILE_PAIR=1: the reduce loads xg/perm as aligned pairs), and the
+    iperm reduce (LHPC_XTILE_IPERM=1: xg kept in flat order in LDS, each CSR
+    position's x gathered through a CSR-order index)."""
     monkeypatch.setenv("LHPC_XTILE_LAYOUT", "cm" if request.param == "cm" else "seg")
     monkeypatch.setenv("LHPC_XTILE_PAIR", "1" if request.param == "pair" else "0")
+    monkeypatch.setenv("LHPC_XTILE_IPERM", "1" if request.param == "iperm" else "0")
     return request.param
 
 
