@@ -1767,7 +1767,10 @@ int build_xtile_plan(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, c
   // reduce keeps the chunk's segments in flat order in LDS and gathers each
   // CSR position's x through iperm (CSR order, read with val) instead of
   // scattering them by perm (DESIGN.md §4 XTILE: C2 589 → 580 µs, C3 1169 → 1086 µs)
-  int pp = 3;
+  // Only for ≥ 32 chunks per CU: with fewer (per-rank matrices at N ≥ 4) the
+  // perm reduce's shorter blocks win (W = 8 rank of C2: 0.088 against
+  // 0.093 ms; W = 1: 0.626 against 0.611 ms; profiles/r01/explore_scaling_*)
+  int pp = p->nnz >= 32LL * cus * cM ? 3 : 1;
   if (const char *env = std::getenv("LHPC_XTILE_IPERM")) pp = std::atoi(env) ? 3 : 1;
   if (const char *env = std::getenv("LHPC_XTILE_PAIR")) pp = std::atoi(env) ? 2 : pp;
   p->xt_p = cm ? 1 : pp;
