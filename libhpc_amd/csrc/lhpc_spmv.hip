@@ -726,6 +726,9 @@ template <typename T> __device__ __forceinline__ int xt_slot(int i) {
 }
 __device__ __forceinline__ int xt_pidx(int i) { return i + (i >> 4); }
 
+#ifndef LHPC_XT_IP_LATE
+#define LHPC_XT_IP_LATE 1  // iperm loaded after phase A's xg loads are issued (not live during the rank math)
+#endif
 #ifndef LHPC_XT_IP_DMA
 #define LHPC_XT_IP_DMA 1  // iperm reduce, fp32: xg → LDS by global_load_lds (no VGPRs)
 #endif
@@ -800,11 +803,14 @@ __global__ __launch_bounds__(BLK, P == 3 ? LHPC_XT_IP_WAVES : 1) void k_xtile_re
   }
   constexpr int NIP = IP ? RUN * 2 / 16 : 1;  // 16-B iperm vectors per run
   u32x4 ipv[NIP];
-  if constexpr (IP) {  // perm points at iperm: [chunk][M] u16, CSR order
+  // perm points at iperm ([chunk][M] u16, CSR order); loaded with phase A's
+  // xg round trip (LHPC_XT_IP_LATE) or here with val
+  auto load_ipv = [&]() {
     const u32x4 *ip = reinterpret_cast<const u32x4 *>(perm + c * M + i0);
 #pragma unroll
     for (int q = 0; q < NIP; ++q) ipv[q] = __builtin_nontemporal_load(ip + q);
-  }
+  };
+  if constexpr (IP && !LHPC_XT_IP_LATE) load_ipv();
   int rv[RPT];
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
@@ -898,6 +904,7 @@ __global__ __launch_bounds__(BLK, P == 3 ? LHPC_XT_IP_WAVES : 1) void k_xtile_re
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(xg + src[u]),
                                          (__attribute__((address_space(3))) void *)(xs + (wv * NBP + u) * kWave),
                                          4, 0, 0);
+      if constexpr (LHPC_XT_IP_LATE) load_ipv();
     } else
 #endif
     {
@@ -906,6 +913,7 @@ __global__ __launch_bounds__(BLK, P == 3 ? LHPC_XT_IP_WAVES : 1) void k_xtile_re
       for (int u = 0; u < NBP; ++u) xv[u] = xg[src[u]];
 #pragma unroll
       for (int u = 0; u < NBP; ++u) xs[(wv * NBP + u) * kWave + lane] = xv[u];
+      if constexpr (LHPC_XT_IP_LATE) load_ipv();
     }
   } else if constexpr (P == 1) {
     T xv[NBP];
