@@ -1,6 +1,6 @@
-// lhpc_plan.cpp — plan-time re-encoding of CSR into the XSLICE layout
-// (see lhpc_plan.hpp).  Host only, OpenMP over 64-row chunks; the output is
-// identical for any thread count.
+// lhpc_plan.cpp — plan-time CSR validation and re-encodings of CSR into the
+// XSLICE and XTILE layouts (see lhpc_plan.hpp).  Host only, OpenMP; every
+// output is identical for any thread count.
 #include "lhpc_plan.hpp"
 
 #include <omp.h>
@@ -19,8 +19,20 @@ inline int64_t rp_at(const void *rp, int bits, int64_t i) {
 }
 }  // namespace
 
+int validate_csr(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols, int64_t nnz) {
+  if (n_rows < 0 || nnz < 0 || rp_at(rp, bits, 0) != 0 || rp_at(rp, bits, n_rows) != nnz) return LHPC_ERR_BAD_CSR;
+  int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
+  for (int64_t i = 0; i < n_rows; ++i) bad |= rp_at(rp, bits, i + 1) < rp_at(rp, bits, i) ? 1 : 0;
+  if (bad) return LHPC_ERR_BAD_CSR;
+  const uint32_t lim = static_cast<uint32_t>(n_cols);  // n_cols ≤ INT32_MAX; a negative col wraps above it
+#pragma omp parallel for schedule(static) reduction(| : bad)
+  for (int64_t k = 0; k < nnz; ++k) bad |= static_cast<uint32_t>(col[k]) >= lim ? 1 : 0;
+  return bad ? LHPC_ERR_BAD_CSR : LHPC_OK;
+}
+
 int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, size_t tsz,
-                 int64_t n_rows, int64_t n_cols, int S, bool jagged, XsliceHost &o) {
+                 int64_t n_rows, int64_t n_cols, int S, XsliceHost &o) {
   if (S < 1 || S > 256) return LHPC_ERR_INVALID_ARG;
   o.S = S;
   o.n_rows = n_rows;
@@ -51,7 +63,7 @@ int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, 
       l16[static_cast<size_t>(s) * o.n_rows_pad + r] = static_cast<uint16_t>(std::min(cnt[s], 65535));
     }
   }
-  if (bad || (jagged && maxc > 255)) return LHPC_ERR_UNSUPPORTED;
+  if (bad) return LHPC_ERR_UNSUPPORTED;
   o.lens_bytes = maxc > 255 ? 2 : 1;
   o.lens.reset(new uint8_t[nl * o.lens_bytes]);
   if (o.lens_bytes == 2) {
@@ -78,7 +90,7 @@ int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, 
   }
   o.cbase[S * o.n_chunks] = acc;
   if (acc != nnz) return LHPC_ERR_INTERNAL;
-  // pass 2: jagged-diagonal fill, one 64-row chunk per iteration (all slices)
+  // pass 2: fill, one 64-row chunk per iteration (all slices)
 #pragma omp parallel
   {
     std::vector<int64_t> order;   // element ids of the chunk, bucketed by (row, slice)
@@ -107,114 +119,20 @@ int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, 
           std::memcpy(o.val.get() + pos * tsz, static_cast<const unsigned char *>(val) + e * tsz, tsz);
           ++pos;
         };
-        if (!jagged) {
-          for (int r = 0; r < 64; ++r)
-            for (int j = 0; j < l[r]; ++j)
-              emit(order[static_cast<size_t>(start[static_cast<size_t>(r) * (S + 1) + s] + j)]);
-          continue;
-        }
-        int maxl = 0;
-        for (int r = 0; r < 64; ++r) maxl = std::max(maxl, static_cast<int>(l[r]));
-        for (int j = 0; j < maxl; ++j)
-          for (int r = 0; r < 64; ++r)
-            if (l[r] > j) emit(order[static_cast<size_t>(start[static_cast<size_t>(r) * (S + 1) + s] + j)]);
+        for (int r = 0; r < 64; ++r)
+          for (int j = 0; j < l[r]; ++j)
+            emit(order[static_cast<size_t>(start[static_cast<size_t>(r) * (S + 1) + s] + j)]);
       }
     }
   }
   return LHPC_OK;
 }
-
-namespace {
-// Chunk-major layout (XtileHost::cm), after the chunks are cut.
-int build_xtile_cm(const int32_t *col, int64_t nnz, int64_t piece_nnz, XtileHost &o) {
-  const int64_t S = o.S, W = o.W, C = o.n_chunks;
-  auto pad8 = [](int64_t v) { return (v + 7) / 8 * 8; };
-  std::vector<int32_t> cnt(static_cast<size_t>(C * S), 0);  // [c][s]
-#pragma omp parallel for schedule(dynamic, 64)
-  for (int64_t c = 0; c < C; ++c) {
-    int32_t *cc = cnt.data() + c * S;
-    for (int64_t k = o.ce[c]; k < o.ce[c + 1]; ++k) ++cc[col[k] / W];
-  }
-  std::vector<int64_t> tbase(static_cast<size_t>(S) + 1, 0);
-  {
-    std::vector<int64_t> tot(static_cast<size_t>(S), 0);
-#pragma omp parallel for schedule(static)
-    for (int64_t s = 0; s < S; ++s) {
-      int64_t t = 0;
-      for (int64_t c = 0; c < C; ++c) t += pad8(cnt[c * S + s]);
-      tot[static_cast<size_t>(s)] = t;
-    }
-    for (int64_t s = 0; s < S; ++s) tbase[s + 1] = tbase[s] + tot[s];
-  }
-  if (tbase[S] >= INT32_MAX - 64) return LHPC_ERR_UNSUPPORTED;
-  o.total = tbase[S];
-  // padded segment starts in (tile, chunk) order; row C = tile ends
-  o.segoff.assign(static_cast<size_t>((C + 1) * S), 0);
-#pragma omp parallel for schedule(static)
-  for (int64_t s = 0; s < S; ++s) {
-    int64_t acc = tbase[s];
-    for (int64_t c = 0; c <= C; ++c) {
-      o.segoff[c * S + s] = static_cast<int32_t>(acc);
-      if (c < C) acc += pad8(cnt[c * S + s]);
-    }
-  }
-  o.col16.reset(new uint16_t[o.total > 0 ? o.total : 1]);
-  std::fill(o.col16.get(), o.col16.get() + (o.total > 0 ? o.total : 1), static_cast<uint16_t>(0xFFFF));
-  o.gdst.reset(new int32_t[o.total / 8 > 0 ? o.total / 8 : 1]);
-  o.perm.reset(new uint16_t[nnz > 0 ? nnz : 1]);
-#pragma omp parallel
-  {
-    std::vector<int32_t> cur_t(static_cast<size_t>(S)), cur_c(static_cast<size_t>(S));
-#pragma omp for schedule(dynamic, 64)
-    for (int64_t c = 0; c < C; ++c) {
-      const int64_t e0 = o.ce[c];
-      const int32_t *cc = cnt.data() + c * S;
-      int64_t pos = e0;  // xg position of segment (c, s): e0 + Σ_{s' < s} cnt
-      for (int64_t s = 0; s < S; ++s) {
-        const int32_t g = o.segoff[c * S + s];
-        cur_t[static_cast<size_t>(s)] = g;
-        cur_c[static_cast<size_t>(s)] = static_cast<int32_t>(pos);
-        for (int32_t j = 0; j < cc[s]; j += 8) o.gdst[(g + j) / 8] = static_cast<int32_t>(pos + j);
-        pos += cc[s];
-      }
-      for (int64_t k = e0; k < o.ce[c + 1]; ++k) {
-        const int64_t s = col[k] / W;
-        o.col16[cur_t[static_cast<size_t>(s)]++] = static_cast<uint16_t>(col[k] - s * W);
-        o.perm[cur_c[static_cast<size_t>(s)]++] = static_cast<uint16_t>(k - e0);
-      }
-    }
-  }
-  // pieces: H chunk ranges × TPX tiles per XCD group; block b = (h, j, x) with
-  // x = b % 8 gathers tile x·TPX + j over chunk range h
-  const int64_t per_tile = S > 0 ? (o.total + S - 1) / S : 0;
-  const int64_t H = std::max<int64_t>(1, std::min<int64_t>(C, (per_tile + piece_nnz / 2) / std::max<int64_t>(8, piece_nnz)));
-  const int64_t TPX = (S + 7) / 8;
-  o.pieces.clear();
-  o.pieces.reserve(static_cast<size_t>(3 * H * TPX * 8));
-  for (int64_t h = 0; h < H; ++h) {
-    const int64_t clo = C * h / H, chi = C * (h + 1) / H;
-    for (int64_t j = 0; j < TPX; ++j)
-      for (int64_t x = 0; x < 8; ++x) {
-        const int64_t s = x * TPX + j;
-        if (s < S) {
-          o.pieces.push_back(o.segoff[clo * S + s]);
-          o.pieces.push_back(o.segoff[chi * S + s]);
-          o.pieces.push_back(static_cast<int32_t>(s));
-        } else {
-          o.pieces.insert(o.pieces.end(), {0, 0, 0});
-        }
-      }
-  }
-  return LHPC_OK;
-}
-}  // namespace
 
 int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
-                int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm, int slot_bytes,
-                const int64_t *splits, int n_splits, XtileHost &o, int pad, bool iperm) {
+                int64_t W, int M, int Rmax, int64_t piece_nnz, int slot_bytes,
+                const int64_t *splits, int n_splits, bool iperm, XtileHost &o) {
   const int64_t nnz = rp_at(rp, bits, n_rows) - rp_at(rp, bits, 0);
-  if (W < 8 || M < 64 || M > 65536 || M % 16 || Rmax < 1 || (slot_bytes != 4 && slot_bytes != 8) ||
-      M >= 65536 || !(pad == 1 || pad == 2 || pad == 4) || (cm && pad != 1) || (iperm && (cm || pad != 1)))
+  if (W < 8 || M < 64 || M >= 65536 || M % 16 || Rmax < 1 || (slot_bytes != 4 && slot_bytes != 8))
     return LHPC_ERR_INVALID_ARG;
   const int64_t S = n_cols > 0 ? (n_cols + W - 1) / W : 1;
   if (S > 4096 || nnz + 8 * S >= INT32_MAX || n_rows >= INT32_MAX) return LHPC_ERR_UNSUPPORTED;
@@ -222,7 +140,6 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
   o.W = W;
   o.M = M;
   o.Rmax = Rmax;
-  o.cm = cm;
   auto RP = [&](int64_t i) { return rp_at(rp, bits, i); };
   // first row r in [lo, n_rows] with rp[r] >= e
   auto lower_row = [&](int64_t lo, int64_t e) {
@@ -232,26 +149,6 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
       if (RP(mid) < e) lo = mid + 1; else hi = mid;
     }
     return lo;
-  };
-  // nonzeros from e that fit one chunk: M, or with pad > 1 the longest run
-  // whose segments, each padded to a multiple of pad, total ≤ M
-  std::vector<int32_t> tcnt(pad > 1 ? static_cast<size_t>(S) : 0, 0);
-  std::vector<int32_t> touched;
-  auto fit = [&](int64_t e) -> int64_t {
-    if (pad == 1) return M;
-    int64_t k = e, pl = 0;
-    for (; k < nnz; ++k) {
-      const int32_t s = static_cast<int32_t>(col[k] / W);
-      if (tcnt[static_cast<size_t>(s)] % pad == 0) {
-        if (pl + pad > M) break;
-        pl += pad;
-        if (tcnt[static_cast<size_t>(s)] == 0) touched.push_back(s);
-      }
-      ++tcnt[static_cast<size_t>(s)];
-    }
-    for (int32_t s : touched) tcnt[static_cast<size_t>(s)] = 0;
-    touched.clear();
-    return k == nnz ? static_cast<int64_t>(M) : k - e;  // k == nnz: the rest fits
   };
   // ---- chunks: (ce, cr) pairs; invariant: cr[c] = first row with rp >= ce[c]
   //      (or a row whose predecessors starting at ce[c] are empty)
@@ -265,7 +162,7 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
     int si = 0;  // next split row after r
     while (!(e == nnz && r == n_rows)) {
       int64_t en, rb;
-      const int64_t Mc = fit(e);
+      const int64_t Mc = M;
       // a split row is done once a chunk starts at it (e == its start, r == it)
       while (si < n_splits && (RP(splits[si]) < e || (RP(splits[si]) == e && splits[si] <= r))) ++si;
       if (si < n_splits && RP(splits[si]) <= e + Mc) {
@@ -314,7 +211,6 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
     const int64_t r0 = o.cr[c], r1 = o.cr[c + 1];
     if (r1 > r0 && RP(r1) > o.ce[c + 1]) o.cont.push_back(static_cast<int32_t>(c));
   }
-  if (cm) return build_xtile_cm(col, nnz, piece_nnz, o);
   // ---- per (chunk, tile) counts → segment offsets in (tile, chunk) order
   o.segoff.assign(static_cast<size_t>((C + 1) * S), 0);
   int32_t *cnt = o.segoff.data() + S;  // row c+1 temporarily holds count[c]
@@ -322,8 +218,6 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
   for (int64_t c = 0; c < C; ++c) {
     int32_t *cc = cnt + c * S;
     for (int64_t k = o.ce[c]; k < o.ce[c + 1]; ++k) ++cc[col[k] / W];
-    if (pad > 1)
-      for (int64_t s = 0; s < S; ++s) cc[s] = (cc[s] + pad - 1) / pad * pad;
   }
   std::vector<int64_t> tbase(static_cast<size_t>(S) + 1, 0);
   {
@@ -349,8 +243,10 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
   }
   // ---- scatter (stable: CSR order inside each segment)
   o.col16.reset(new uint16_t[o.total > 0 ? o.total : 1]());
-  o.perm.reset(new uint16_t[o.total > 0 ? o.total : 1]());
-  if (iperm) o.iperm.reset(new uint16_t[static_cast<size_t>(C > 0 ? C : 1) * M]());
+  if (iperm)
+    o.iperm.reset(new uint16_t[nnz > 0 ? nnz : 1]());
+  else
+    o.perm.reset(new uint16_t[o.total > 0 ? o.total : 1]());
 #pragma omp parallel
   {
     std::vector<int32_t> cur(static_cast<size_t>(S)), flat(iperm ? static_cast<size_t>(S) : 0);
@@ -369,17 +265,11 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
         const int64_t s = col[k] / W;
         const int32_t g = cur[static_cast<size_t>(s)]++;
         o.col16[g] = static_cast<uint16_t>(col[k] - s * W);
-        o.perm[g] = static_cast<uint16_t>(xtile_slot(static_cast<int>(k - e0), slot_bytes));
         if (iperm)
-          o.iperm[static_cast<size_t>(c) * M + static_cast<size_t>(k - e0)] =
-              static_cast<uint16_t>(flat[static_cast<size_t>(s)] + (g - o.segoff[c * S + s]));
+          o.iperm[k] = static_cast<uint16_t>(flat[static_cast<size_t>(s)] + (g - o.segoff[c * S + s]));
+        else
+          o.perm[g] = static_cast<uint16_t>(xtile_slot(static_cast<int>(k - e0), slot_bytes));
       }
-      if (pad > 1)  // segment pads: col16 0 (any tile column), perm = the spare slot M
-        for (int64_t s = 0; s < S; ++s)
-          for (int32_t g = cur[static_cast<size_t>(s)]; g < o.segoff[(c + 1) * S + s]; ++g) {
-            o.col16[g] = 0;
-            o.perm[g] = static_cast<uint16_t>(M);
-          }
     }
   }
   // ---- gather workgroups: each non-empty tile split into pieces of ≈ piece_nnz

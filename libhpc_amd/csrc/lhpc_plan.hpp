@@ -1,5 +1,5 @@
 // lhpc_plan.hpp — host-side plan-time re-encodings of A (built by g++ with
-// OpenMP in lhpc_plan.cpp; consumed by the HIP plan in lhpc_spmv.hip).
+// OpenMP in lhpc_plan.cpp; consumed by the HIP plans in lhpc_spmv_*.hip).
 #pragma once
 
 #include <cstddef>
@@ -9,15 +9,19 @@
 
 namespace lhpc {
 
+// CSR sanity, always run by lhpc_spmv_plan_create before any layout pass
+// indexes host arrays by row_ptr or col_idx: row_ptr[0] == 0, row_ptr
+// non-decreasing, row_ptr[n_rows] == nnz, every col_idx in [0, n_cols).
+// 0 or LHPC_ERR_BAD_CSR.  OpenMP, one pass over row_ptr and col_idx.
+int validate_csr(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
+                 int64_t nnz);
+
 // XSLICE: A split by column into S slices of `width` columns; inside a
-// slice, rows are grouped in 64-row chunks (one wave per chunk).  A chunk's
-// nonzeros are stored either
-//   jagged = true : jagged-diagonal order — all rows' 1st in-slice element,
-//                   then all 2nd elements, ... (lane-per-row kernel), or
-//   jagged = false: CSR order — row by row (stream kernel: the wave loads the
-//                   chunk's elements contiguously, products go through LDS).
-// Element j of a row is its j-th in-slice element in the caller's order, so
-// each row accumulates in its CSR order either way.
+// slice, rows are grouped in 64-row chunks (one wave per chunk), and a
+// chunk's in-slice nonzeros are stored in CSR order (row by row; the wave
+// loads them contiguously and stages the products in LDS).  Element j of a
+// row is its j-th in-slice element in the caller's order, so each row
+// accumulates in its CSR order.
 struct XsliceHost {
   int S = 0;
   int64_t width = 0;
@@ -32,9 +36,9 @@ struct XsliceHost {
 };
 
 // 0 on success; LHPC_ERR_UNSUPPORTED when some row has > 65535 nonzeros in
-// one slice, or > 255 with allow16 = false (the jagged kernel is uint8-only).
+// one slice.
 int build_xslice(const void *row_ptr, int rp_bits, const int32_t *col, const void *val,
-                 size_t tsz, int64_t n_rows, int64_t n_cols, int S, bool jagged, XsliceHost &out);
+                 size_t tsz, int64_t n_rows, int64_t n_cols, int S, XsliceHost &out);
 
 // XTILE: x tiled by column into S tiles of W columns, each tile small enough
 // to sit in one workgroup's LDS (fp32 40960 / fp64 20480 columns = 160 KB).
@@ -42,10 +46,12 @@ int build_xslice(const void *row_ptr, int rp_bits, const int32_t *col, const voi
 //   gather : a workgroup loads tile s of x into LDS and streams the tile's
 //            nonzeros (col16 = column − s·W), writing xg[g] = x[col] — every
 //            x read is an LDS gather, every HBM access is a coalesced stream;
-//   reduce : a workgroup owns a chunk of ≤ M consecutive CSR nonzeros, reads
-//            the chunk's S segments of xg (one per tile) and scatters them
-//            into LDS at perm[g] (the slot xtile_slot(i) of the nonzero's
-//            position i in the chunk; cm: i itself), then
+//   reduce : a workgroup owns a chunk of ≤ M consecutive CSR nonzeros and
+//            reads the chunk's S segments of xg (one per tile).  perm mode
+//            scatters them into LDS at perm[g] (the slot xtile_slot(i) of the
+//            nonzero's chunk position i); iperm mode keeps them in flat order
+//            (the chunk's segment concatenation, tiles ascending) and gathers
+//            CSR position i's x from flat slot iperm[e0 + i].  Then it
 //            multiplies by val (CSR order) and sums rows merge-path style.
 // The stream is ordered (tile, chunk, CSR position): segment (s, c) is
 // [segoff[c·S + s], segoff[(c+1)·S + s]).  Each tile's stream starts at a
@@ -53,56 +59,36 @@ int build_xslice(const void *row_ptr, int rp_bits, const int32_t *col, const voi
 // Chunks cut the CSR order at row starts where one lies in the back half of
 // the M window, else mid-row; a chunk owns the rows that start in it (≤ Rmax)
 // and a row cut by a chunk end is finished by a fix-up over `cont`.
-//
-// cm = true (chunk-major xg, opt-in): gather writes xg in the chunk's
-// segment concatenation order — chunk c occupies [ce[c], ce[c+1]) of xg,
-// tiles ascending inside it — so reduce reads its chunk as one contiguous run
-// and needs no segment table.  Each tile-stream segment is padded to a
-// multiple of 8 (padding col16 = 0xFFFF, never stored); gdst[q] is the xg
-// position of group q's first entry (a group's entries are contiguous in
-// xg), and perm is indexed by xg position.  Pieces are (tile, chunk range)
-// pairs ordered so that blocks b with b % 8 == x (one XCD) gather a
-// contiguous run of tiles — the xg lines of a chunk are then assembled in
-// one L2 — and a whole chunk range before the next (H ranges).
-// cm = false: xg is in tile-stream order (tile, chunk, CSR position), perm is
-// indexed by stream position, and reduce locates its S segments by segoff.
-// pad > 1 (cm = false only): every segment is padded to a multiple of pad
-// (pad entries: col16 0, perm = the spare slot M) so that the reduce loads
-// pad consecutive positions as one aligned vector; chunks are cut so that
-// their padded length stays ≤ M.
 struct XtileHost {
   int S = 0;
   int64_t W = 0;
   int M = 0, Rmax = 0;
-  bool cm = false;
   int64_t n_chunks = 0;
   int64_t total = 0;                 // padded tile-stream length
   std::vector<int32_t> ce, cr;       // [C+1] chunk first nonzero / first owned row
   std::vector<int32_t> segoff;       // [(C+1)·S] segment starts in the tile stream
-  std::vector<int32_t> pieces;       // gather workgroups: (g0, g1, s) triples (g0 == g1: idle)
+  std::vector<int32_t> pieces;       // gather workgroups: (g0, g1, s) triples
   std::vector<int32_t> cont;         // chunks whose last owned row runs past the chunk
   std::vector<int64_t> rchunk;       // [n_splits + 2] first chunk of each row range (+ C)
   std::unique_ptr<uint16_t[]> col16;  // [total]
-  std::unique_ptr<uint16_t[]> perm;   // [total] (cm: [nnz])
-  std::unique_ptr<int32_t[]> gdst;    // cm: [total / 8]
-  // iperm mode: [n_chunks·M] — for CSR position i of chunk c, iperm[c·M + i]
-  // is its flat position in the chunk's segment concatenation (tiles
-  // ascending); perm is then not used by the reduce
+  std::unique_ptr<uint16_t[]> perm;   // perm mode: [total]
+  // iperm mode: [nnz] in CSR order — for nonzero k of chunk c, iperm[k] is its
+  // flat position in the chunk's segment concatenation (tiles ascending)
   std::unique_ptr<uint16_t[]> iperm;
 };
 
 // 0 on success; LHPC_ERR_UNSUPPORTED when the layout does not fit its
 // index types (nnz + padding ≥ 2^31, S > 4096, or an oversized segment table).
-// piece_nnz: target nonzeros per gather workgroup (multiple of 8 is used;
-// cm: the number of chunk ranges H is derived from it).  splits: ascending
-// rows in (0, n_rows) at which a chunk must start (row ranges that can be
-// reduced separately, lhpc_spmv_range); LHPC_ERR_INVALID_ARG otherwise.
+// piece_nnz: target nonzeros per gather workgroup (a multiple of 8 is used).
+// splits: ascending rows in (0, n_rows) at which a chunk must start (row
+// ranges that can be reduced separately, lhpc_spmv_range);
+// LHPC_ERR_INVALID_ARG otherwise.  iperm selects the reduce's index stream
+// (perm for false, iperm for true; only the selected one is built).
 int build_xtile(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_rows,
-                int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, bool cm,
-                int slot_bytes, const int64_t *splits, int n_splits, XtileHost &out,
-                int pad = 1, bool iperm = false);
+                int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, int slot_bytes,
+                const int64_t *splits, int n_splits, bool iperm, XtileHost &out);
 
-// LDS slot of chunk position i in the XTILE seg reduce (lhpc_spmv.hip
+// LDS slot of chunk position i in the XTILE reduce (lhpc_spmv_xtile.hip
 // xt_slot): run t = i/run holds run = 64/elem_bytes elements (64 B) at
 // run·t, its 16-B slot q at q ^ swz(t), swz = (t/4) % 4.
 inline int xtile_slot(int i, int elem_bytes) {

@@ -1,0 +1,325 @@
+// lhpc_spmv_csr.hip — CSR SpMV kernels that keep the caller's CSR layout
+// (y[i] = Σ_{k=row_ptr[i]}^{row_ptr[i+1]-1} val[k]·x[col_idx[k]]; the
+// reference has no SpMV).  Numerics: fp64 accumulation in
+// registers, one rounding at the store (SURVEY §8c binding recommendation).
+//   ROWGROUP  L lanes per row (L | 64), R rows per lane group per wave, all
+//             loads hoisted so a wave keeps R gathers + R val/col loads in
+//             flight; the row sum is a DPP butterfly inside one 16-lane DPP
+//             row for L <= 16 (no LDS), then one coalesced y store per wave.
+//   ADAPTIVE  nnz-balanced row blocks: a 256-thread workgroup streams up to
+//             kBlockNnz contiguous nonzeros (coalesced), stages fp64 products
+//             in LDS, and reduces each row with L = 256/rows lanes; a row
+//             longer than kBlockNnz gets a workgroup to itself.  For skewed
+//             (power-law) row lengths.  Deterministic: fixed trees only.
+// Both read val/col_idx with non-temporal loads (streamed once) so the
+// gathered x keeps its place in L2 / Infinity Cache.
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "lhpc_spmv_impl.hpp"
+
+namespace lhpc {
+namespace {
+
+constexpr int kBlockNnz = 2048;  // ADAPTIVE: nonzeros per stream block
+
+// ------------------------------------------------------------- ROWGROUP
+template <typename T, typename I, int L, int R>
+__global__ __launch_bounds__(kBlock) void k_spmv_rowgroup(
+    const I *__restrict__ row_ptr, const int32_t *__restrict__ col,
+    const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y,
+    int64_t n_rows) {
+  constexpr int G = kWave / L;     // lane groups (rows) per wave per step
+  constexpr int WR = G * R;        // rows per wave
+  static_assert(WR <= kWave, "one y store per wave");
+  const int lane = threadIdx.x & (kWave - 1);
+  const int sub = lane & (L - 1);  // lane within its group
+  const int grp = lane / L;        // group within the wave
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
+  const int64_t row0 = wave * WR;
+  if (row0 >= n_rows) return;  // wave-uniform
+
+  int64_t s[R], e[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = row0 + r * G + grp;
+    if (row < n_rows) {
+      s[r] = row_ptr[row];
+      e[r] = row_ptr[row + 1];
+    } else {
+      s[r] = e[r] = 0;
+    }
+  }
+  // first L-wide chunk of every row, loads hoisted for memory-level parallelism
+  int32_t c[R];
+  T v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t k = s[r] + sub;
+    c[r] = -1;
+    v[r] = T(0);
+    if (k < e[r]) {
+      c[r] = ld_stream(col + k);
+      v[r] = ld_stream(val + k);
+    }
+  }
+  double acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    acc[r] = 0.0;
+    if (c[r] >= 0) acc[r] = static_cast<double>(v[r]) * static_cast<double>(x[c[r]]);
+  }
+  // rows longer than L (rare for the uniform workload)
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    for (int64_t k = s[r] + sub + L; k < e[r]; k += L)
+      acc[r] += static_cast<double>(ld_stream(val + k)) *
+                static_cast<double>(x[ld_stream(col + k)]);
+  }
+  // all 64 lanes active here: DPP reads never see a disabled source lane
+  T out = T(0);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const T tot = static_cast<T>(group_sum<L>(acc[r]));
+    // lane l (< WR) stores row row0 + l = row0 + (l/G)*G + l%G: take the
+    // sum of step r = l/G from group g = l%G
+    const T mine = __shfl(tot, (lane % G) * L, kWave);
+    if (lane / G == r) out = mine;
+  }
+  if (lane < WR && row0 + lane < n_rows) __builtin_nontemporal_store(out, y + row0 + lane);
+}
+
+// ------------------------------------------------------------- ADAPTIVE
+// blocks[b] = first row of block b; blocks[n_blocks] = n_rows.
+template <typename T, typename I>
+__global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
+    const I *__restrict__ row_ptr, const int32_t *__restrict__ col,
+    const T *__restrict__ val, const T *__restrict__ x, T *__restrict__ y,
+    const int64_t *__restrict__ blocks, const T *__restrict__ w, double *__restrict__ dpart) {
+  // DOT (w != nullptr): also dpart[block] = Σ_rows y[row]·w[row] over the block's rows
+  // (the stored, rounded y), reduced in a fixed order — the CG p·q fused into the SpMV.
+  __shared__ double prod[kBlockNnz];
+  __shared__ double wsum[kBlock / kWave];
+  const int tid = threadIdx.x;
+  const int64_t r0 = blocks[blockIdx.x];
+  const int64_t r1 = blocks[blockIdx.x + 1];
+  const int64_t base = row_ptr[r0];
+  const int64_t cnt = static_cast<int64_t>(row_ptr[r1]) - base;
+  const int64_t nrows = r1 - r0;
+
+  if (cnt > kBlockNnz) {
+    // one long row: strided per-thread sums, then a fixed block tree
+    double a = 0.0;
+    for (int64_t k = tid; k < cnt; k += kBlock)
+      a += static_cast<double>(ld_stream(val + base + k)) *
+           static_cast<double>(x[ld_stream(col + base + k)]);
+    a = group_sum<kWave>(a);
+    if ((tid & (kWave - 1)) == 0) wsum[tid / kWave] = a;
+    __syncthreads();
+    if (tid == 0) {
+      double t = wsum[0];
+#pragma unroll
+      for (int i = 1; i < kBlock / kWave; ++i) t += wsum[i];
+      const T yv = static_cast<T>(t);
+      y[r0] = yv;
+      if (w) dpart[blockIdx.x] = static_cast<double>(yv) * static_cast<double>(w[r0]);
+    }
+    return;
+  }
+  // stream phase: every thread products kBlockNnz/kBlock nonzeros
+  constexpr int PER = kBlockNnz / kBlock;
+  int32_t c[PER];
+  T v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int64_t k = i * kBlock + tid;
+    c[i] = -1;
+    v[i] = T(0);
+    if (k < cnt) {
+      c[i] = ld_stream(col + base + k);
+      v[i] = ld_stream(val + base + k);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = i * kBlock + tid;
+    if (c[i] >= 0) prod[k] = static_cast<double>(v[i]) * static_cast<double>(x[c[i]]);
+  }
+  __syncthreads();
+  // reduce: L lanes per row, L = largest power of two with nrows*L <= 256
+  int L = kWave;
+  while (L > 1 && nrows * L > kBlock) L >>= 1;
+  const int grp = tid / L, sub = tid & (L - 1);
+  double a = 0.0;
+  int64_t rs = 0, re = 0;
+  if (grp < nrows) {
+    rs = static_cast<int64_t>(row_ptr[r0 + grp]) - base;
+    re = static_cast<int64_t>(row_ptr[r0 + grp + 1]) - base;
+    for (int64_t k = rs + sub; k < re; k += L) a += prod[k];
+  }
+  switch (L) {  // block-uniform
+    case 64: a = group_sum<64>(a); break;
+    case 32: a = group_sum<32>(a); break;
+    case 16: a = group_sum<16>(a); break;
+    case 8: a = group_sum<8>(a); break;
+    case 4: a = group_sum<4>(a); break;
+    case 2: a = group_sum<2>(a); break;
+    default: break;
+  }
+  double d = 0.0;
+  if (grp < nrows && sub == 0) {
+    const T yv = static_cast<T>(a);
+    y[r0 + grp] = yv;
+    if (w) d = static_cast<double>(yv) * static_cast<double>(w[r0 + grp]);
+  }
+  if (w) {  // block-uniform
+    d = group_sum<kWave>(d);
+    __syncthreads();  // wsum reuse
+    if ((tid & (kWave - 1)) == 0) wsum[tid / kWave] = d;
+    __syncthreads();
+    if (tid == 0) {
+      double t = wsum[0];
+#pragma unroll
+      for (int i = 1; i < kBlock / kWave; ++i) t += wsum[i];
+      dpart[blockIdx.x] = t;
+    }
+  }
+}
+
+template <typename T, typename I, int L, int R>
+int launch_rowgroup_t(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  constexpr int WR = (kWave / L) * R;
+  const int64_t waves = (p->n_rows + WR - 1) / WR;
+  const int64_t blocks = (waves * kWave + kBlock - 1) / kBlock;
+  if (blocks == 0) return LHPC_OK;
+  hipLaunchKernelGGL((k_spmv_rowgroup<T, I, L, R>), dim3(static_cast<unsigned>(blocks)),
+                     dim3(kBlock), 0, s, static_cast<const I *>(p->d_row_ptr), p->d_col,
+                     static_cast<const T *>(p->d_val), static_cast<const T *>(x),
+                     static_cast<T *>(y), p->n_rows);
+  return check_launch(s);
+}
+
+template <typename T, typename I>
+int launch_rowgroup(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  switch (p->L * 100 + p->R) {
+    case 101: return launch_rowgroup_t<T, I, 1, 1>(p, x, y, s);
+    case 201: return launch_rowgroup_t<T, I, 2, 1>(p, x, y, s);
+    case 202: return launch_rowgroup_t<T, I, 2, 2>(p, x, y, s);
+    case 401: return launch_rowgroup_t<T, I, 4, 1>(p, x, y, s);
+    case 402: return launch_rowgroup_t<T, I, 4, 2>(p, x, y, s);
+    case 404: return launch_rowgroup_t<T, I, 4, 4>(p, x, y, s);
+    case 802: return launch_rowgroup_t<T, I, 8, 2>(p, x, y, s);
+    case 804: return launch_rowgroup_t<T, I, 8, 4>(p, x, y, s);
+    case 1601: return launch_rowgroup_t<T, I, 16, 1>(p, x, y, s);
+    case 1602: return launch_rowgroup_t<T, I, 16, 2>(p, x, y, s);
+    case 1604: return launch_rowgroup_t<T, I, 16, 4>(p, x, y, s);
+    case 1608: return launch_rowgroup_t<T, I, 16, 8>(p, x, y, s);
+    case 3201: return launch_rowgroup_t<T, I, 32, 1>(p, x, y, s);
+    case 3202: return launch_rowgroup_t<T, I, 32, 2>(p, x, y, s);
+    case 6401: return launch_rowgroup_t<T, I, 64, 1>(p, x, y, s);
+    default: return LHPC_ERR_UNSUPPORTED;
+  }
+}
+
+template <typename T, typename I>
+int launch_adaptive(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s, const void *w = nullptr,
+                    double *dpart = nullptr) {
+  if (p->n_blocks == 0) return LHPC_OK;
+  hipLaunchKernelGGL((k_spmv_adaptive<T, I>), dim3(static_cast<unsigned>(p->n_blocks)),
+                     dim3(kBlock), 0, s, static_cast<const I *>(p->d_row_ptr), p->d_col,
+                     static_cast<const T *>(p->d_val), static_cast<const T *>(x),
+                     static_cast<T *>(y), p->d_blocks, static_cast<const T *>(w), dpart);
+  return check_launch(s);
+}
+
+// Fixed-order two-stage sum of the per-block dot partials: stage 1 reduces
+// 2048 consecutive partials per block (8 independent loads per thread), stage
+// 2 (one block) the ≤ ⌈nb/2048⌉ stage-1 sums.  One block looping over ~10^5
+// partials would serialise on L2 latency.
+constexpr int kFinTile = 2048;
+__global__ __launch_bounds__(kBlock) void k_dpart_finish(const double *__restrict__ part, int64_t nb,
+                                                         double *__restrict__ out) {
+  __shared__ double wsum[kBlock / kWave];
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kFinTile;
+  double v[kFinTile / kBlock];
+#pragma unroll
+  for (int k = 0; k < kFinTile / kBlock; ++k) {
+    const int64_t i = b0 + k * kBlock + threadIdx.x;
+    v[k] = i < nb ? part[i] : 0.0;
+  }
+  double a = 0.0;
+#pragma unroll
+  for (int k = 0; k < kFinTile / kBlock; ++k) a += v[k];
+  a = group_sum<kWave>(a);
+  if ((threadIdx.x & (kWave - 1)) == 0) wsum[threadIdx.x / kWave] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = wsum[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / kWave; ++i) t += wsum[i];
+    out[blockIdx.x] = t;
+  }
+}
+
+}  // namespace
+
+// Row blocks for ADAPTIVE: greedy, each block <= kBlockNnz nonzeros and
+// <= kBlock rows, or a single row of any length.
+std::vector<int64_t> csr_build_blocks(RowPtrView rp, int64_t n_rows, int64_t &n_long) {
+  std::vector<int64_t> b;
+  b.reserve(static_cast<size_t>(n_rows / 64 + 2));
+  n_long = 0;
+  int64_t r = 0;
+  while (r < n_rows) {
+    b.push_back(r);
+    const int64_t start = rp[r];
+    if (rp[r + 1] - start > kBlockNnz) {
+      ++n_long;
+      ++r;
+      continue;
+    }
+    int64_t end = r + 1;
+    while (end < n_rows && end - r < kBlock && rp[end + 1] - start <= kBlockNnz) ++end;
+    r = end;
+  }
+  b.push_back(n_rows);
+  return b;
+}
+
+int csr_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  const bool f32 = p->dtype == LHPC_F32;
+  if (p->kernel == LHPC_KERNEL_ADAPTIVE)
+    return f32 ? (p->rp64 ? launch_adaptive<float, int64_t>(p, x, y, s) : launch_adaptive<float, int32_t>(p, x, y, s))
+               : (p->rp64 ? launch_adaptive<double, int64_t>(p, x, y, s) : launch_adaptive<double, int32_t>(p, x, y, s));
+  return f32 ? (p->rp64 ? launch_rowgroup<float, int64_t>(p, x, y, s) : launch_rowgroup<float, int32_t>(p, x, y, s))
+             : (p->rp64 ? launch_rowgroup<double, int64_t>(p, x, y, s) : launch_rowgroup<double, int32_t>(p, x, y, s));
+}
+
+int csr_launch_dot(lhpc_spmv_plan *p, const void *x, void *y, const void *w, double *dot_out, hipStream_t s) {
+  if (p->kernel != LHPC_KERNEL_ADAPTIVE || p->n_blocks == 0) return LHPC_ERR_UNSUPPORTED;
+  const int64_t n1 = (p->n_blocks + kFinTile - 1) / kFinTile;  // stage-1 sums, after the partials
+  if (n1 > kFinTile) return LHPC_ERR_UNSUPPORTED;                // > 4M blocks (> 8·10^9 nonzeros)
+  if (!p->d_dpart)
+    LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_dpart), (p->n_blocks + n1) * sizeof(double), p->bytes));
+  int st;
+  if (p->dtype == LHPC_F32)
+    st = p->rp64 ? launch_adaptive<float, int64_t>(p, x, y, s, w, p->d_dpart)
+                 : launch_adaptive<float, int32_t>(p, x, y, s, w, p->d_dpart);
+  else
+    st = p->rp64 ? launch_adaptive<double, int64_t>(p, x, y, s, w, p->d_dpart)
+                 : launch_adaptive<double, int32_t>(p, x, y, s, w, p->d_dpart);
+  LHPC_TRY(st);
+  double *stage1 = p->d_dpart + p->n_blocks;
+  if (n1 == 1) {
+    hipLaunchKernelGGL(k_dpart_finish, dim3(1), dim3(kBlock), 0, s, p->d_dpart, p->n_blocks, dot_out);
+  } else {
+    hipLaunchKernelGGL(k_dpart_finish, dim3(static_cast<unsigned>(n1)), dim3(kBlock), 0, s, p->d_dpart,
+                       p->n_blocks, stage1);
+    LHPC_TRY(check_launch(s));
+    hipLaunchKernelGGL(k_dpart_finish, dim3(1), dim3(kBlock), 0, s, stage1, n1, dot_out);
+  }
+  return check_launch(s);
+}
+
+}  // namespace lhpc

@@ -1,0 +1,98 @@
+// lhpc_spmv_impl.hpp — the SpMV plan object and the interface between the
+// kernel-family translation units:
+//   lhpc_spmv.hip         plan creation (kernel selection), the C ABI
+//   lhpc_spmv_csr.hip     ROWGROUP / ADAPTIVE (CSR kept as is)
+//   lhpc_spmv_xslice.hip  XSLICE (XCD-local column slices + partial reduce)
+//   lhpc_spmv_xtile.hip   XTILE (x tiles in LDS: tile gather + chunk reduce)
+// The reference has no SpMV: the operator is
+// y[i] = Σ_{k=row_ptr[i]}^{row_ptr[i+1]-1} val[k]·x[col_idx[k]].
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "lhpc_common.hpp"
+
+struct lhpc_spmv_plan {
+  int dtype = LHPC_F32;
+  int device = 0;
+  int rp64 = 0;  // device row_ptr is int64
+  int64_t n_rows = 0, n_cols = 0, nnz = 0;
+  void *d_row_ptr = nullptr;
+  int32_t *d_col = nullptr;
+  void *d_val = nullptr;
+  int64_t *d_blocks = nullptr;
+  int64_t n_blocks = 0, n_long = 0;
+  void *d_xstage = nullptr, *d_ystage = nullptr;
+  double *d_dpart = nullptr;  // lhpc_spmv_dot: per-block partials (ADAPTIVE), allocated on first use
+  int kernel = LHPC_KERNEL_ROWGROUP;
+  int L = 16, R = 4;
+  int64_t bytes = 0;
+  // XSLICE
+  int S = 0;
+  int xs_nb = 2, xs_p64 = 0, xs_lens16 = 0;
+  int64_t xs_width = 0, xs_chunks = 0, xs_rows_pad = 0, xs_bps = 0;
+  void *d_lens = nullptr;
+  int64_t *d_cbase = nullptr;
+  void *d_partial = nullptr;
+  // XTILE
+  int64_t xt_C = 0, xt_pieces = 0, xt_cont = 0, xt_total = 0;
+  size_t xt_lds = 0;
+  int xt_u = 8;  // gather steps in flight (LHPC_XTILE_U)
+  // row ranges (lhpc_spmv_plan_create_split): range k = rows [xt_srow[k],
+  // xt_srow[k+1]) = chunks [xt_src[k], xt_src[k+1]), cont entries [xt_sco[k], xt_sco[k+1])
+  std::vector<int64_t> split_rows, xt_srow, xt_src, xt_sco;
+  int32_t *d_cdesc = nullptr;
+  int32_t *d_cr = nullptr, *d_segoff = nullptr, *d_pieces = nullptr, *d_cont = nullptr;
+  uint16_t *d_col16 = nullptr, *d_perm = nullptr;
+  int xt_p = 1;  // reduce: 1 perm scatter, 3 iperm gather (DESIGN.md §4 XTILE)
+  void *d_xg = nullptr;
+  double *d_carry = nullptr;
+};
+
+namespace lhpc {
+
+constexpr int kBlock = 256;
+
+// Host view of row_ptr regardless of width.
+struct RowPtrView {
+  const void *p;
+  int bits;
+  int64_t operator[](int64_t i) const {
+    return bits == 64 ? static_cast<const int64_t *>(p)[i] : static_cast<const int32_t *>(p)[i];
+  }
+};
+
+// hipMalloc that books the bytes on the plan; LHPC_ERR_ALLOC on OOM.
+inline int dmalloc(void **p, size_t n, int64_t &acct) {
+  if (n == 0) n = 16;
+  hipError_t e = hipMalloc(p, n);
+  if (e == hipErrorOutOfMemory) return LHPC_ERR_ALLOC;
+  if (e != hipSuccess) return static_cast<int>(e);
+  acct += static_cast<int64_t>(n);
+  return LHPC_OK;
+}
+
+// ---- lhpc_spmv_csr.hip
+int csr_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s);
+// ADAPTIVE with the fused y·w epilogue: *dot_out = Σ y[i]·w[i] (fixed order)
+int csr_launch_dot(lhpc_spmv_plan *p, const void *x, void *y, const void *w, double *dot_out, hipStream_t s);
+// ADAPTIVE row blocks (≤ 2048 nonzeros and ≤ 256 rows, or one long row)
+std::vector<int64_t> csr_build_blocks(RowPtrView rp, int64_t n_rows, int64_t &n_long);
+
+// ---- lhpc_spmv_xslice.hip
+int xslice_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s);
+// LHPC_ERR_UNSUPPORTED: some row too long for the slice layout (caller falls back)
+int xslice_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz,
+                 unsigned flags);
+
+// ---- lhpc_spmv_xtile.hip
+int xtile_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s);
+int xtile_stage(const lhpc_spmv_plan *p, const void *x, hipStream_t s);
+int xtile_range(const lhpc_spmv_plan *p, int k, void *yk, hipStream_t s);
+// LHPC_ERR_UNSUPPORTED: the layout does not fit its index types (caller falls back)
+int xtile_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz);
+
+}  // namespace lhpc

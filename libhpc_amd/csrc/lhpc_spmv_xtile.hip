@@ -1,0 +1,647 @@
+// lhpc_spmv_xtile.hip — XTILE: CSR SpMV with x tiles in LDS (DESIGN.md §4
+// XTILE; layout: lhpc_plan.hpp XtileHost).  The default for matrices whose
+// x does not fit L2 and whose gathers have no locality (C2–C4): every x read
+// is an LDS read, every HBM access a coalesced stream.
+//   gather  one workgroup per (tile, piece): tile s of x (160 KB) in LDS, the
+//           tile's nonzeros streamed as u16 column offsets; writes xg[g] =
+//           x[col] in tile-stream order;
+//   reduce  one workgroup per chunk of ≤ M CSR nonzeros: the chunk's S
+//           segments of xg into LDS, a segmented scan of the products per
+//           row in CSR order (fp64), the owned rows' y stored coalesced;
+//   fixup   rows cut by a chunk end: their fp64 pieces added in chunk order.
+// Numerics: fp32 products are exact in fp64 and summed in fp64, rounded once
+// at the store; fp64 products are rounded once, as in the reference loop.
+// Dyadic inputs are bit-exact.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "lhpc_plan.hpp"
+#include "lhpc_spmv_impl.hpp"
+
+namespace lhpc {
+namespace {
+
+constexpr int kXtGatherBlock = 1024;  // gather: 16 waves per CU, one tile of x in LDS
+constexpr int kXtFixBlock = 256;      // fix-up
+template <typename T> struct XtTile;
+template <> struct XtTile<float> { static constexpr int W = 40960; };   // 160 KB
+template <> struct XtTile<double> { static constexpr int W = 20480; };  // 160 KB
+
+// gather: block b streams pieces[3b..3b+1] of tile pieces[3b+2]; 8 nonzeros
+// per thread and step (one 16-B col16 load, 8 LDS gathers, 8 contiguous xg
+// stores), U steps in flight.  Piece bounds are multiples of 8.  The first
+// col16 step does not depend on the tile, so it is issued under the tile load.
+// (A fused form that also streamed val in tile order and wrote val·x[col]
+// was slower: C2 603 → 621 µs, C3 1141 → 1736 µs)
+template <typename T, int U>
+__global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
+    const int32_t *__restrict__ pieces, const uint16_t *__restrict__ col16,
+    const T *__restrict__ x, int64_t n_cols, T *__restrict__ xg) {
+  constexpr int W = XtTile<T>::W;
+  __shared__ T xt[W];
+  const int tid = threadIdx.x;
+  const int g0 = pieces[3 * blockIdx.x], g1 = pieces[3 * blockIdx.x + 1];
+  const int64_t c0 = static_cast<int64_t>(pieces[3 * blockIdx.x + 2]) * W;
+  const int wlen = static_cast<int>((n_cols - c0) < W ? (n_cols - c0) : W);
+  constexpr int PT = W / kXtGatherBlock;
+  const int q0 = g0 >> 3, q1 = g1 >> 3;  // 8-entry groups
+  const u32x4 *cv = reinterpret_cast<const u32x4 *>(col16);
+  u32x4 w[U];
+  auto load_w = [&](int q) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int qq = q + u * kXtGatherBlock;
+      w[u] = qq < q1 ? __builtin_nontemporal_load(cv + qq) : u32x4{0, 0, 0, 0};
+    }
+  };
+  load_w(q0 + tid);
+  T tvv[PT];
+#pragma unroll
+  for (int i = 0; i < PT; ++i) {
+    const int j = i * kXtGatherBlock + tid;
+    tvv[i] = j < wlen ? x[c0 + j] : T(0);
+  }
+#pragma unroll
+  for (int i = 0; i < PT; ++i) xt[i * kXtGatherBlock + tid] = tvv[i];
+  __syncthreads();
+  for (int q = q0 + tid; q < q1; q += U * kXtGatherBlock) {
+    if (q != q0 + tid) load_w(q);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int qq = q + u * kXtGatherBlock;
+      T o[8];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        o[2 * h] = xt[w[u][h] & 0xFFFFu];
+        o[2 * h + 1] = xt[w[u][h] >> 16];
+      }
+      if (qq < q1) {
+        if constexpr (sizeof(T) == 4) {
+          f32x4 *d = reinterpret_cast<f32x4 *>(xg + static_cast<int64_t>(qq) * 8);
+          d[0] = f32x4{o[0], o[1], o[2], o[3]};
+          d[1] = f32x4{o[4], o[5], o[6], o[7]};
+        } else {
+          typedef double f64x2 __attribute__((ext_vector_type(2)));
+          f64x2 *d = reinterpret_cast<f64x2 *>(xg + static_cast<int64_t>(qq) * 8);
+#pragma unroll
+          for (int h = 0; h < 4; ++h) d[h] = f64x2{o[2 * h], o[2 * h + 1]};
+        }
+      }
+    }
+  }
+}
+
+// reduce: one block per chunk c = (b % 8)·Cx + b / 8, so each XCD walks a
+// contiguous run of chunks and the xg lines two neighbouring chunks share
+// stay in its L2.  Both phases are branch-free and every load that does not
+// depend on another is issued together (three round trips per chunk: the
+// 16-B chunk descriptor {e0, e1, r0, r1} with the segment table; val run +
+// row_ptr; xg (+ perm / iperm)):
+//   scan     the chunk's S segment lengths are prefix-summed (with a count of
+//            non-empty segments packed in the high half), giving each
+//            non-empty segment its rank, base_ne[rank] = segment start −
+//            flat offset, and a bit at its flat offset in sbm (M bits).
+//   phase A  flat position f of the segment concatenation lies in the
+//            non-empty segment of rank popcount(sbm bits ≤ f) − 1: a wave
+//            prefix-scan of the sbm words gives each 64-position batch its
+//            base rank, mbcnt gives the lane's; src = base_ne[rank] + f.
+//            perm mode: xs[perm[src]] = xg[src] (CSR slot order); iperm mode:
+//            xs[f] = xg[src] (flat order, fp32 by LDS-DMA).
+//   phase B  thread t owns the run [RUN·t, RUN·t+RUN) (iperm mode: gathered
+//            from xs through iperm[e0 + i]); a bitmap of row starts drives a
+//            segmented scan (reset at a start, fma), whose running value
+//            rounded to T is written back in place: a row that ends inside a
+//            run leaves its value at its last position.  Rows crossing runs
+//            are combined by a segmented scan over the threads, rows crossing
+//            chunks leave fp64 pieces in `carry`, and the owned rows' y is
+//            stored coalesced from their last positions.
+#ifndef LHPC_XT_RBLK32
+#define LHPC_XT_RBLK32 512
+#endif
+#ifndef LHPC_XT_RBLK64
+#define LHPC_XT_RBLK64 1024
+#endif
+// reduce configurations: BLK threads, each owning one 64-B run of RUN =
+// 64/sizeof(T) nonzeros (fp32 16, fp64 8); chunks of M = RUN·BLK nonzeros
+// owning ≤ Rmax rows.  A 64-B run keeps LDS per wave at 4 KB for both types,
+// so LDS never caps occupancy below 8 waves per SIMD.  fp32: BLK = 512 (C2
+// reduce: 256 → 512 took 470 → 420 µs, 1024 was no faster).  fp64 with
+// 16-nonzero runs held 8 KB per wave (73 KB per 512-thread block: 2 blocks,
+// 16 waves per CU; C3 reduce 987 µs).
+template <typename T> constexpr int xt_run() { return 64 / static_cast<int>(sizeof(T)); }
+template <typename T, int BLK> struct XtRed {
+  static constexpr int M = BLK * xt_run<T>(), Rmax = M / 8;
+};
+template <typename T> constexpr int xt_red_blk() { return sizeof(T) == 4 ? LHPC_XT_RBLK32 : LHPC_XT_RBLK64; }
+// LDS slot of chunk position i (lhpc_plan.hpp xtile_slot): run t = i/RUN
+// occupies 64 B at 64·t and its 16-B slot q is stored at q ^ xt_swz(t), so
+// the 16 lanes of a ds_read_b128 group hit 16 distinct bank quads (4 runs per
+// 256-B bank row, swizzled by the row's index mod 4)
+__device__ __forceinline__ int xt_swz(int t) { return (t >> 2) & 3; }
+template <typename T> __device__ __forceinline__ int xt_slot(int i) {
+  constexpr int VW = 16 / sizeof(T), RUN = xt_run<T>();
+  return (i & ~(RUN - 1)) | ((((i & (RUN - 1)) / VW) ^ xt_swz(i / RUN)) * VW) | (i & (VW - 1));
+}
+
+#ifndef LHPC_XT_IP_WAVES
+#define LHPC_XT_IP_WAVES 8  // iperm reduce: 8 waves/SIMD (fp32 66 → 64 VGPRs: C2 593 → 580 µs)
+#endif
+template <typename T, int G, int BLK, bool IP>
+__global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce(
+    const int32_t *__restrict__ cdesc, const int32_t *__restrict__ segoff, int S, int64_t c0, int64_t C,
+    int64_t Cx, int total, const T *__restrict__ xg, const uint16_t *__restrict__ perm,
+    const T *__restrict__ val, const int32_t *__restrict__ rp, T *__restrict__ y,
+    double *__restrict__ carry) {
+  constexpr int RUN = xt_run<T>(), M = XtRed<T, BLK>::M, RMAX = XtRed<T, BLK>::Rmax;
+  constexpr int RPT = (RMAX + 1 + BLK - 1) / BLK;  // row_ptr loads per thread
+  constexpr int NB = M / BLK;                      // 64-position batches per wave (= RUN)
+  static_assert((NB == 16 || NB == 8) && M <= 256 * kWave && M >= 4096,
+                "8/16 batches per wave; ≤ 256 batches per chunk; sbm ≥ 128 words");
+  typedef T tvec __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
+  typedef uint32_t ivec __attribute__((ext_vector_type(4), aligned(2)));
+  constexpr int VW = 16 / sizeof(T), NV = RUN / VW;
+  // dynamic LDS (xtile_lds_bytes): xs[M + VW] T (slot M is the sentinel's
+  // spare), bt[BLK/64][NB] u32x4, ws[BLK/64] f64, wsf[BLK/64] i32, bm[M/32]
+  // u32, sbm[M/32] u32, rpl[RMAX+1] u16 (padded to 4 B), base_ne[S] i32, wsum[8] i32
+  extern __shared__ __align__(16) unsigned char smem[];
+  T *xs = reinterpret_cast<T *>(smem);
+  u32x4 *bt0 = reinterpret_cast<u32x4 *>(xs + M + VW);
+  double *ws = reinterpret_cast<double *>(bt0 + (BLK / kWave) * NB);  // per-wave segmented-scan totals
+  int *wsf = reinterpret_cast<int *>(ws + BLK / kWave);
+  uint32_t *bm = reinterpret_cast<uint32_t *>(wsf + BLK / kWave);
+  uint32_t *sbm = bm + M / 32;
+  uint16_t *rpl = reinterpret_cast<uint16_t *>(sbm + M / 32);
+  int32_t *base_ne = reinterpret_cast<int32_t *>(rpl + ((RMAX + 2) & ~1));
+  int32_t *wsum = base_ne + S;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int i0 = tid * RUN;
+  const int64_t c = c0 + static_cast<int64_t>(blockIdx.x % 8) * Cx + blockIdx.x / 8;  // chunk range [c0, C)
+  if (c >= C) return;  // block-uniform
+  // ---- round trip 1: the chunk descriptor and the segment table (both
+  //      addressed by c alone), then — without waiting for them — round
+  //      trip 2 (val run and row_ptr, addressed by the descriptor).  The
+  //      segment scan and phase A need only the table, so phase A's xg loads
+  //      go out while val and row_ptr are still in flight.
+  int sa[G], sb[G];
+#pragma unroll
+  for (int q = 0; q < G; ++q) {
+    const int sI = tid * G + q;
+    const int sc = sI < S ? sI : S - 1;
+    sa[q] = segoff[c * S + sc];
+    sb[q] = segoff[(c + 1) * S + sc];
+  }
+  const u32x4 d = *reinterpret_cast<const u32x4 *>(cdesc + 4 * c);
+  const int e0 = static_cast<int>(d[0]), m = static_cast<int>(d[1]) - e0;
+  const int r0 = static_cast<int>(d[2]), R = static_cast<int>(d[3]) - r0;
+  tvec vv[NV];
+  {
+    // the val allocation is padded by one run, so a run may read past nnz
+    const tvec *vp = reinterpret_cast<const tvec *>(val + e0 + (i0 < m ? i0 : 0));
+#pragma unroll
+    for (int q = 0; q < NV; ++q) vv[q] = __builtin_nontemporal_load(vp + q);
+  }
+  constexpr int NIP = IP ? RUN * 2 / 16 : 1;  // 16-B iperm vectors per run
+  ivec ipv[NIP];
+  // iperm ([nnz + RUN] u16, CSR order, padded like val): loaded once phase
+  // A's xg loads are issued, so it is not live during the rank math
+  auto load_ipv = [&]() {
+    const ivec *ip = reinterpret_cast<const ivec *>(perm + e0 + (i0 < m ? i0 : 0));
+#pragma unroll
+    for (int q = 0; q < NIP; ++q) ipv[q] = __builtin_nontemporal_load(ip + q);
+  };
+  int rv[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int j = q * BLK + tid;
+    rv[q] = rp[r0 + (j <= R ? j : R)];
+  }
+  // ---- scan: segment ranks / bases and the segment-start bitmap
+  if (tid < M / 32) {
+    bm[tid] = 0u;
+    sbm[tid] = 0u;
+  }
+  int lsum = 0;  // (length | non-empty count << 16) of this thread's segments
+#pragma unroll
+  for (int q = 0; q < G; ++q) {
+    if (tid * G + q >= S) sb[q] = sa[q];
+    lsum += (sb[q] - sa[q]) + (sb[q] > sa[q] ? 0x10000 : 0);
+  }
+  const int inc = wave_incl_scan(lsum);
+  if (lane == kWave - 1) wsum[wv] = inc;
+  __syncthreads();
+  {
+    int run = inc - lsum;
+    for (int w = 0; w < wv; ++w) run += wsum[w];
+    int off = run & 0xFFFF, rank = run >> 16;
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int len = sb[q] - sa[q];
+      if (len > 0) {
+        base_ne[rank] = sa[q] - off;
+        atomicOr(sbm + (off >> 5), 1u << (off & 31));
+        ++rank;
+      }
+      off += len;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase A: src = base_ne[rank] + f, xg loads (round trip 3);
+  //      positions past m load the sentinel entry `total` (perm: spare slot M)
+  int src[NB];
+  {
+    // lane q holds batch q's word; the wave-uniform rank terms (w >> 1,
+    // base) go to an LDS triple that the owning wave reads back as a
+    // broadcast:  rank = starts before the batch − 1 + (w & 1) + mbcnt(w >> 1)
+    // (lanes hold batch words q and q + 64 … when M > 4096); wave w owns
+    // batches [NB·w, NB·w + NB)
+    const int grp = (wv * NB) >> 6;  // this wave's batches lie in 64-batch group grp
+    uint64_t wl = 0;
+    int cnt = 0, incl = 0, below = 0;
+    for (int g2 = 0; g2 <= grp; ++g2) {  // wave-uniform
+      wl = static_cast<uint64_t>(sbm[128 * g2 + 2 * lane]) | (static_cast<uint64_t>(sbm[128 * g2 + 2 * lane + 1]) << 32);
+      cnt = __popcll(wl);
+      incl = wave_incl_scan(cnt) + below;  // starts in batches ≤ 64·g2 + lane
+      below = __builtin_amdgcn_readlane(incl, kWave - 1);
+    }
+    u32x4 *bt = bt0 + wv * NB;
+    if (lane / NB == wv % (kWave / NB)) {  // lanes holding this wave's batches
+      const uint64_t w1 = wl >> 1;
+      bt[lane & (NB - 1)] = u32x4{static_cast<uint32_t>(w1), static_cast<uint32_t>(w1 >> 32),
+                                  static_cast<uint32_t>(incl - cnt - 1 + static_cast<int>(wl & 1u)), 0u};
+    }
+    __builtin_amdgcn_wave_barrier();  // LDS is in order within a wave: no block barrier needed
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const u32x4 t = bt[u];  // uniform address: broadcast
+      const int rk = __builtin_amdgcn_mbcnt_hi(t[1], __builtin_amdgcn_mbcnt_lo(t[0], t[2]));
+      const int f = (wv * NB + u) * kWave + lane;
+      const int sv = base_ne[rk] + f;  // m > 0 ⇒ 0 ≤ rk < S; m = 0: base_ne[−1] (in LDS), unused
+      src[u] = f < m ? sv : total;
+    }
+  }
+  // plain loads: the segment lines a neighbouring chunk shares must stay in
+  // L2 (non-temporal xg/perm loads: 433 → 555 µs)
+  if constexpr (IP) {
+    if constexpr (sizeof(T) == 4) {
+      // LDS-DMA: each lane's xg element lands at the batch's base + 4·lane
+      // (exactly the flat order), no VGPR destination
+#pragma unroll
+      for (int u = 0; u < NB; ++u)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(xg + src[u]),
+                                         (__attribute__((address_space(3))) void *)(xs + (wv * NB + u) * kWave),
+                                         4, 0, 0);
+      load_ipv();
+    } else {
+      T xv[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) xv[u] = xg[src[u]];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) xs[(wv * NB + u) * kWave + lane] = xv[u];
+      load_ipv();
+    }
+  } else {
+    T xv[NB];
+    uint16_t pv[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      xv[u] = xg[src[u]];
+      pv[u] = perm[src[u]];  // LDS slot xt_slot(position); the sentinel's: M
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) xs[pv[u]] = xv[u];
+  }
+  // row_ptr (round trip 2) → local row offsets and the row-start bitmap
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int j = q * BLK + tid;
+    rv[q] -= e0;
+    if (j <= R) rpl[j] = static_cast<uint16_t>(rv[q] <= m ? rv[q] : m + 1);  // > m: continues
+    if (j < R && rv[q] < m) atomicOr(bm + (rv[q] >> 5), 1u << (rv[q] & 31));  // empty rows share a bit
+  }
+  const int n = m - i0 < RUN ? (m - i0 > 0 ? m - i0 : 0) : RUN;  // valid entries in the run
+  if (n < RUN) {  // the chunk's last run (and runs past m): val and x past m → 0 · 0
+    if constexpr (!IP)
+      for (int j = n; j < RUN; ++j) xs[xt_slot<T>(i0 + j)] = T(0);
+#pragma unroll
+    for (int j = 0; j < RUN; ++j) vv[j / VW][j % VW] = j < n ? vv[j / VW][j % VW] : T(0);
+  }
+  // the LDS-DMA of phase A is counted by vmcnt, which the barrier does not
+  // wait for: drain it before any wave reads another wave's flat slots
+  if constexpr (IP && sizeof(T) == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- phase B: branch-free segmented scan of the thread's run.  The fp32
+  //      product is exact in fp64, so the fma equals the add of the product.
+  const uint32_t mask = (bm[i0 >> 5] >> (i0 & 31)) & ((1u << RUN) - 1u);
+  const int hl = mask ? __builtin_ctz(mask) : RUN;  // head length (entries before the first start)
+  const int hend = (hl < n ? hl : n) - 1;                // last head position (−1: none)
+  // the run is NV 16-B slots at RUN·tid, slot q stored at q ^ xt_swz (conflict-free ds_read_b128)
+  typedef T lvec __attribute__((ext_vector_type(VW)));
+  lvec *xr = reinterpret_cast<lvec *>(xs + i0);
+  const int swz = xt_swz(tid);
+  lvec xq[NV];
+  if constexpr (IP) {
+    // gather the run's x from the flat array, then (after every thread has
+    // read) the running sums below go back in the CSR (xt_slot) layout;
+    // unconditional reads (iperm past m is a valid slot), so all RUN
+    // ds_reads issue before the first wait; then x past m → 0
+    T gx[RUN];
+#pragma unroll
+    for (int j = 0; j < RUN; ++j) {
+      const uint32_t w = ipv[j / 8][(j % 8) / 2];
+      gx[j] = xs[static_cast<int>((j & 1) ? (w >> 16) : (w & 0xFFFFu))];
+    }
+#pragma unroll
+    for (int j = 0; j < RUN; ++j) xq[j / VW][j % VW] = j < n ? gx[j] : T(0);
+    __syncthreads();
+  } else {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) xq[q] = xr[q ^ swz];
+  }
+  double acc = 0.0, hsave = 0.0;
+#pragma unroll
+  for (int j = 0; j < RUN; ++j) {
+    acc = ((mask >> j) & 1u) ? 0.0 : acc;
+    acc = __builtin_fma(static_cast<double>(vv[j / VW][j % VW]), static_cast<double>(xq[j / VW][j % VW]), acc);
+    hsave = j == hend ? acc : hsave;
+    xq[j / VW][j % VW] = static_cast<T>(acc);  // in place; slots past m are never read
+  }
+#pragma unroll
+  for (int q = 0; q < NV; ++q) xr[q ^ swz] = xq[q];
+  const bool has_head = n > 0 && !(mask & 1u);
+  const bool cont = rpl[R] > m;  // the row active at m−1 runs past the chunk
+  // ---- rows that cross runs: segmented scan over threads (run order) of
+  //      x(t) = tail piece if run t holds a row start, else its whole-run sum;
+  //      the row open when run t begins is the exclusive value S(t−1)
+  bool fl = n > 0 && mask != 0u;
+  double sv = wave_seg_scan(fl ? acc : hsave, fl);
+  if (lane == kWave - 1) {
+    ws[wv] = sv;
+    wsf[wv] = fl ? 1 : 0;
+  }
+  __syncthreads();
+  double cw = 0.0;  // segmented carry of the waves before this one
+  int gw = 0;
+  for (int w = 0; w < wv; ++w) {
+    cw = wsf[w] ? ws[w] : cw + ws[w];
+    gw |= wsf[w];
+  }
+  if (!fl) sv = cw + sv;
+  const int fin_incl = (fl ? 1 : 0) | gw;
+  constexpr int kShr1 = 0x138;  // DPP wave_shr:1 (lane l ← lane l−1; lane 0 keeps `old`)
+  const double oin = dpp_f64_old<kShr1>(cw, sv);                                 // S(t−1)
+  const int fin = __builtin_amdgcn_update_dpp(gw, fin_incl, kShr1, 0xF, 0xF, false);  // starts before run t
+  const int tlast = m > 0 ? (m - 1) / RUN : -1;
+  if (tid == 0 && !(m > 0 && rpl[0] > 0)) carry[2 * c] = 0.0;  // no head piece
+  if (has_head) {
+    const int i1 = i0 + n;
+    const bool end_i1 = i1 < m ? ((bm[i1 >> 5] >> (i1 & 31)) & 1u) != 0 : !cont;
+    const bool ends = hl < n || end_i1;
+    if (ends || tid == tlast) {
+      const double sum = oin + hsave;
+      if (!fin) {
+        carry[2 * c] = sum;  // this chunk's piece of the previous chunk's row
+      } else if (ends) {
+        xs[xt_slot<T>(i0 + hend)] = static_cast<T>(sum);
+      } else {
+        carry[2 * c + 1] = sum;  // row continues into the next chunk
+      }
+    }
+  }
+  if (tid == tlast && mask && cont) carry[2 * c + 1] = acc;  // own tail row continues
+  __syncthreads();
+  // coalesced y store of the owned rows from their last positions (a row
+  // continuing past the chunk is stored by k_xtile_fixup, later on the stream)
+  for (int j = tid; j < R; j += BLK) {
+    const int a0 = rpl[j], a1 = rpl[j + 1];
+    if (a1 == a0) y[r0 + j] = T(0);
+    else if (a1 <= m) y[r0 + j] = xs[xt_slot<T>(a1 - 1)];
+  }
+}
+
+// rows cut by a chunk end: y[row] = tail piece + head pieces, chunk order
+template <typename T>
+__global__ __launch_bounds__(kXtFixBlock) void k_xtile_fixup(
+    const int32_t *__restrict__ cont, int64_t n_cont, const int32_t *__restrict__ cr, int64_t C,
+    const double *__restrict__ carry, T *__restrict__ y) {  // C: end of the chunk range (rows never cross it)
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kXtFixBlock + threadIdx.x;
+  if (i >= n_cont) return;
+  const int64_t c = cont[i];
+  double s = carry[2 * c + 1];
+  for (int64_t d = c + 1; d < C; ++d) {
+    s += carry[2 * d];
+    if (cr[d + 1] > cr[d]) break;
+  }
+  y[cr[c + 1] - 1] = static_cast<T>(s);
+}
+
+// ------------------------------------------------------------ launchers
+template <typename T>
+size_t xtile_lds_bytes(int S) {
+  constexpr int BLK = xt_red_blk<T>(), M = XtRed<T, BLK>::M, RMAX = XtRed<T, BLK>::Rmax, W = BLK / kWave;
+  return static_cast<size_t>(M + 16 / sizeof(T)) * sizeof(T) + W * xt_run<T>() * 16 + W * (sizeof(double) + 4) +
+         2 * M / 32 * sizeof(uint32_t) + ((RMAX + 2) & ~1) * sizeof(uint16_t) +
+         sizeof(int32_t) * (static_cast<size_t>(S) + 8);
+}
+
+// segment-table entries per reduce thread
+template <typename T>
+int xtile_g(int S) {
+  const int g = (S + xt_red_blk<T>() - 1) / xt_red_blk<T>();
+  return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : g <= 8 ? 8 : 16;
+}
+
+template <typename T, int G, bool IP>
+const void *xtile_reduce_fn() {
+  return reinterpret_cast<const void *>(k_xtile_reduce<T, G, xt_red_blk<T>(), IP>);
+}
+template <typename T, bool IP>
+const void *xtile_reduce_fn(int g) {
+  return g == 1 ? xtile_reduce_fn<T, 1, IP>() : g == 2 ? xtile_reduce_fn<T, 2, IP>()
+         : g == 4 ? xtile_reduce_fn<T, 4, IP>() : g == 8 ? xtile_reduce_fn<T, 8, IP>() : xtile_reduce_fn<T, 16, IP>();
+}
+template <typename T>
+const void *xtile_reduce_fn(int g, bool ip) {
+  return ip ? xtile_reduce_fn<T, true>(g) : xtile_reduce_fn<T, false>(g);
+}
+
+template <typename T, int U>
+void gather_u(const lhpc_spmv_plan *p, const void *x, hipStream_t s) {
+  hipLaunchKernelGGL((k_xtile_gather<T, U>), dim3(static_cast<unsigned>(p->xt_pieces)), dim3(kXtGatherBlock), 0, s,
+                     p->d_pieces, p->d_col16, static_cast<const T *>(x), p->n_cols, static_cast<T *>(p->d_xg));
+}
+
+template <typename T>
+int launch_gather(const lhpc_spmv_plan *p, const void *x, hipStream_t s) {
+  if (p->xt_pieces <= 0) return LHPC_OK;
+  switch (p->xt_u) {
+    case 2: gather_u<T, 2>(p, x, s); break;
+    case 4: gather_u<T, 4>(p, x, s); break;
+    case 16: gather_u<T, 16>(p, x, s); break;
+    default: gather_u<T, 8>(p, x, s); break;
+  }
+  return check_launch(s);
+}
+
+// reduce of chunks [c0, c1) into y (rows at their plan index), then the fix-up
+// of the rows cut inside the range: cont entries [n0, n1)
+template <typename T>
+int launch_reduce(const lhpc_spmv_plan *p, int64_t c0, int64_t c1, int64_t n0, int64_t n1, T *y,
+                  hipStream_t s) {
+  if (c1 > c0) {
+    const int64_t Cx = (c1 - c0 + 7) / 8;
+    const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(xt_red_blk<T>());
+    const void *fn = xtile_reduce_fn<T>(xtile_g<T>(p->S), p->xt_p == 3);
+    const int32_t *cd = p->d_cdesc, *so = p->d_segoff, *rp = static_cast<const int32_t *>(p->d_row_ptr);
+    int S = p->S, total = static_cast<int>(p->xt_total);
+    const T *xg = static_cast<const T *>(p->d_xg), *val = static_cast<const T *>(p->d_val);
+    const uint16_t *perm = p->d_perm;
+    double *carry = p->d_carry;
+    void *args[] = {&cd, &so, &S, &c0, &c1, const_cast<int64_t *>(&Cx), &total, &xg, &perm, &val, &rp, &y, &carry};
+    LHPC_HIP_TRY(hipLaunchKernel(fn, rg, rb, args, p->xt_lds, s));
+    LHPC_TRY(check_launch(s));
+  }
+  if (n1 > n0) {
+    hipLaunchKernelGGL((k_xtile_fixup<T>), dim3(static_cast<unsigned>((n1 - n0 + kXtFixBlock - 1) / kXtFixBlock)),
+                       dim3(kXtFixBlock), 0, s, p->d_cont + n0, n1 - n0, p->d_cr, c1, p->d_carry, y);
+    LHPC_TRY(check_launch(s));
+  }
+  return LHPC_OK;
+}
+
+template <typename T>
+int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val) {
+  constexpr size_t tsz = sizeof(T);
+  constexpr int64_t W = XtTile<T>::W;
+  constexpr int M = XtRed<T, xt_red_blk<T>()>::M, RMAX = XtRed<T, xt_red_blk<T>()>::Rmax, RUN = xt_run<T>();
+  int cus = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, p->device) == hipSuccess) cus = prop.multiProcessorCount;
+  // ≈ 2 gather workgroups per CU (one resident per CU: 160 KB of LDS each)
+  // and ≥ 4 tiles' worth of stream per piece, so the tile load (W·T bytes)
+  // stays ≤ 1/4 of a piece's col16 + xg traffic on small (per-rank) matrices
+  const int64_t min_piece = 4 * W * static_cast<int64_t>(tsz) / (2 + static_cast<int64_t>(tsz));
+  int64_t piece = std::max<int64_t>(min_piece, p->nnz / (2 * static_cast<int64_t>(cus)) + 1);
+  if (const char *env = std::getenv("LHPC_XTILE_PIECE")) piece = std::max<int64_t>(8, std::atoll(env));
+  // reduce index stream: iperm (gather each CSR position's x from the flat
+  // segment concatenation in LDS) for ≥ 32 full chunks per CU, else perm
+  // (scatter into CSR slots): with fewer chunks (per-rank matrices at N ≥ 4)
+  // the perm reduce's shorter blocks win (W = 8 rank of C2: 0.088 against
+  // 0.093 ms; W = 1: 0.626 against 0.611 ms; profiles/r01/explore_scaling_*)
+  bool ip = p->nnz >= 32LL * cus * M;
+  if (const char *env = std::getenv("LHPC_XTILE_IPERM")) ip = std::atoi(env) != 0;
+  p->xt_p = ip ? 3 : 1;
+  XtileHost xt;
+  LHPC_TRY(build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, M, RMAX, piece, static_cast<int>(tsz),
+                       p->split_rows.data(), static_cast<int>(p->split_rows.size()), ip, xt));
+  p->kernel = LHPC_KERNEL_XTILE;
+  p->rp64 = 0;
+  p->S = xt.S;
+  p->xs_width = W;
+  p->xt_C = xt.n_chunks;
+  p->xt_pieces = static_cast<int64_t>(xt.pieces.size() / 3);
+  p->xt_cont = static_cast<int64_t>(xt.cont.size());
+  p->xt_total = xt.total;
+  p->xt_lds = xtile_lds_bytes<T>(xt.S);
+  if (const char *env = std::getenv("LHPC_XTILE_U")) {
+    const int u = std::atoi(env);
+    p->xt_u = u <= 2 ? 2 : u < 8 ? 4 : u < 16 ? 8 : 16;
+  }
+  LHPC_HIP_TRY(hipFuncSetAttribute(xtile_reduce_fn<T>(xtile_g<T>(xt.S), ip),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
+  const int64_t n_rows = p->n_rows, nnz = p->nnz, C = xt.n_chunks;
+  auto up = [&](void **d, const void *h, size_t n) -> int {
+    LHPC_TRY(dmalloc(d, n, p->bytes));
+    if (n && h) LHPC_HIP_TRY(hipMemcpy(*d, h, n, hipMemcpyHostToDevice));
+    return LHPC_OK;
+  };
+  std::vector<int32_t> rp32(static_cast<size_t>(n_rows + 1));
+  for (int64_t i = 0; i <= n_rows; ++i) rp32[static_cast<size_t>(i)] = static_cast<int32_t>(rp[i]);
+  LHPC_TRY(up(&p->d_row_ptr, rp32.data(), rp32.size() * 4));
+  // val padded by one run: a reduce thread loads its whole run as vectors
+  LHPC_TRY(dmalloc(&p->d_val, static_cast<size_t>(nnz + RUN) * tsz, p->bytes));
+  LHPC_HIP_TRY(hipMemset(static_cast<unsigned char *>(p->d_val) + nnz * tsz, 0, RUN * tsz));
+  if (nnz) LHPC_HIP_TRY(hipMemcpy(p->d_val, val, static_cast<size_t>(nnz) * tsz, hipMemcpyHostToDevice));
+  {
+    std::vector<int32_t> cd(static_cast<size_t>(4 * C + 4));
+    for (int64_t c = 0; c < C; ++c) {
+      cd[4 * c] = xt.ce[c];
+      cd[4 * c + 1] = xt.ce[c + 1];
+      cd[4 * c + 2] = xt.cr[c];
+      cd[4 * c + 3] = xt.cr[c + 1];
+    }
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cdesc), cd.data(), cd.size() * 4));
+  }
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cr), xt.cr.data(), xt.cr.size() * 4));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_pieces), xt.pieces.data(), xt.pieces.size() * 4));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cont), xt.cont.data(), xt.cont.size() * 4));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_col16), xt.col16.get(), static_cast<size_t>(xt.total) * 2));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_segoff), xt.segoff.data(), xt.segoff.size() * 4));
+  if (ip) {
+    // iperm in CSR order, padded by one run like val
+    LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_perm), static_cast<size_t>(nnz + RUN) * 2, p->bytes));
+    LHPC_HIP_TRY(hipMemset(p->d_perm + nnz, 0, RUN * 2));
+    if (nnz) LHPC_HIP_TRY(hipMemcpy(p->d_perm, xt.iperm.get(), static_cast<size_t>(nnz) * 2, hipMemcpyHostToDevice));
+  } else {
+    // one sentinel entry past the stream: the reduce loads it for positions
+    // past m, and its perm is the spare LDS slot M
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), nullptr, static_cast<size_t>(xt.total + 2) * 2));
+    if (xt.total) LHPC_HIP_TRY(hipMemcpy(p->d_perm, xt.perm.get(), static_cast<size_t>(xt.total) * 2, hipMemcpyHostToDevice));
+    const uint16_t spare[2] = {static_cast<uint16_t>(M), static_cast<uint16_t>(M)};
+    LHPC_HIP_TRY(hipMemcpy(p->d_perm + xt.total, spare, 4, hipMemcpyHostToDevice));
+  }
+  LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total + 2) * tsz));
+  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_carry), nullptr, static_cast<size_t>(2 * C + 2) * 8));
+  LHPC_HIP_TRY(hipMemset(p->d_carry, 0, static_cast<size_t>(2 * C + 2) * 8));
+  if (!p->split_rows.empty()) {
+    const size_t K = p->split_rows.size() + 1;
+    p->xt_srow.assign(1, 0);
+    p->xt_srow.insert(p->xt_srow.end(), p->split_rows.begin(), p->split_rows.end());
+    p->xt_srow.push_back(n_rows);
+    p->xt_src.assign(xt.rchunk.begin(), xt.rchunk.end());
+    p->xt_sco.assign(K + 1, 0);
+    for (size_t k = 0; k <= K; ++k)
+      p->xt_sco[k] = std::lower_bound(xt.cont.begin(), xt.cont.end(), static_cast<int32_t>(p->xt_src[k])) -
+                     xt.cont.begin();
+  }
+  return LHPC_OK;
+}
+
+}  // namespace
+
+int xtile_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  if (p->n_rows == 0) return LHPC_OK;
+  if (p->dtype == LHPC_F32) {
+    LHPC_TRY(launch_gather<float>(p, x, s));
+    return launch_reduce<float>(p, 0, p->xt_C, 0, p->xt_cont, static_cast<float *>(y), s);
+  }
+  LHPC_TRY(launch_gather<double>(p, x, s));
+  return launch_reduce<double>(p, 0, p->xt_C, 0, p->xt_cont, static_cast<double *>(y), s);
+}
+
+// lhpc_spmv_stage: the gather of a split plan; lhpc_spmv_range: range k's
+// reduce + fix-up into y_k (row xt_srow[k] at y_k[0]).
+int xtile_stage(const lhpc_spmv_plan *p, const void *x, hipStream_t s) {
+  return p->dtype == LHPC_F32 ? launch_gather<float>(p, x, s) : launch_gather<double>(p, x, s);
+}
+
+int xtile_range(const lhpc_spmv_plan *p, int k, void *yk, hipStream_t s) {
+  const int64_t c0 = p->xt_src[k], c1 = p->xt_src[k + 1], n0 = p->xt_sco[k], n1 = p->xt_sco[k + 1];
+  if (p->dtype == LHPC_F32)
+    return launch_reduce<float>(p, c0, c1, n0, n1, static_cast<float *>(yk) - p->xt_srow[k], s);
+  return launch_reduce<double>(p, c0, c1, n0, n1, static_cast<double *>(yk) - p->xt_srow[k], s);
+}
+
+int xtile_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz) {
+  return tsz == 4 ? build_t<float>(p, rp, col_idx, val) : build_t<double>(p, rp, col_idx, val);
+}
+
+}  // namespace lhpc

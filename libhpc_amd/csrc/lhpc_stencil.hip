@@ -350,440 +350,9 @@ __global__ __launch_bounds__(kS7X *kS7Y) void k_stencil7(const float *__restrict
   }
 }
 
-// 2.5-D LDS version (default).  Block = 64×4 threads owning a 64(x)×32(y)
-// tile (8 rows per thread) and ZC consecutive z planes.  Plane z (interior +
-// 1-cell x/y halo) sits in a double-buffered LDS tile; u(z-1) and u(z+1) of a
-// thread's own cells stay in registers; plane z+1 is loaded while plane z is
-// computed; one barrier per plane.  Coordinates are clamped to the padded
-// domain so partial tiles never read outside the array (their results are
-// not stored).  Same evaluation order as k_stencil7.
-constexpr int kT7X = 64, kT7TY = 4, kT7RY = 8, kT7Y = kT7TY * kT7RY;  // tile 64 x 32
-
-template <int ZC>
-__global__ __launch_bounds__(kT7X *kT7TY) void k_stencil7_lds(const float *__restrict__ u,
-                                                              float *__restrict__ out, int64_t nz,
-                                                              int64_t ny, int64_t nx, int64_t g,
-                                                              float c0, float c1, int64_t z_begin,
-                                                              int64_t z_end) {
-  constexpr int LW = kT7X + 2, LH = kT7Y + 2;
-  __shared__ float plane[2][LH * LW];
-  const int tx = threadIdx.x, ty = threadIdx.y;
-  const int tid = ty * kT7X + tx;
-  const int64_t x0 = static_cast<int64_t>(blockIdx.x) * kT7X;
-  const int64_t y0 = static_cast<int64_t>(blockIdx.y) * kT7Y;
-  const int64_t zs = z_begin + static_cast<int64_t>(blockIdx.z) * ZC;
-  if (zs >= z_end) return;  // block-uniform
-  const int64_t ze = zs + ZC < z_end ? zs + ZC : z_end;
-  const int64_t Px = nx + 2 * g;
-  const int64_t Pyx = (ny + 2 * g) * Px;
-  // padded-array offset of logical (y, x) in plane 0 (clamped to [-1, n])
-  auto off = [&](int64_t y, int64_t x) -> int64_t {
-    y = y < ny ? y : ny;
-    x = x < nx ? x : nx;
-    return (y + g) * Px + (x + g);
-  };
-  const int64_t xc = x0 + tx;
-  int64_t oin[kT7RY];
-#pragma unroll
-  for (int i = 0; i < kT7RY; ++i) oin[i] = off(y0 + ty + kT7TY * i, xc);
-  // halo cells: 0..31 left column, 32..63 right column, 64..127 top row, 128..191 bottom row
-  int64_t ohalo = 0;
-  int hidx = -1;
-  if (tid < 2 * kT7Y + 2 * kT7X) {
-    if (tid < kT7Y) {
-      ohalo = off(y0 + tid, x0 - 1);
-      hidx = (tid + 1) * LW + 0;
-    } else if (tid < 2 * kT7Y) {
-      ohalo = off(y0 + tid - kT7Y, x0 + kT7X);
-      hidx = (tid - kT7Y + 1) * LW + (LW - 1);
-    } else if (tid < 2 * kT7Y + kT7X) {
-      ohalo = off(y0 - 1, x0 + (tid - 2 * kT7Y));
-      hidx = 0 * LW + (tid - 2 * kT7Y + 1);
-    } else {
-      ohalo = off(y0 + kT7Y, x0 + (tid - 2 * kT7Y - kT7X));
-      hidx = (LH - 1) * LW + (tid - 2 * kT7Y - kT7X + 1);
-    }
-  }
-  const float *up = u + (zs + g) * Pyx;  // padded plane of logical z = zs
-  float cprev[kT7RY], ccur[kT7RY], cnext[kT7RY];
-#pragma unroll
-  for (int i = 0; i < kT7RY; ++i) {
-    cprev[i] = up[oin[i] - Pyx];
-    ccur[i] = up[oin[i]];
-  }
-  float hcur = hidx >= 0 ? up[ohalo] : 0.f;
-  int cur = 0;
-#pragma unroll
-  for (int i = 0; i < kT7RY; ++i) plane[cur][(ty + kT7TY * i + 1) * LW + tx + 1] = ccur[i];
-  if (hidx >= 0) plane[cur][hidx] = hcur;
-  __syncthreads();
-  for (int64_t z = zs; z < ze; ++z) {
-    const float *pn = u + (z + 1 + g) * Pyx;  // logical z+1 (<= nz: ghost plane at the end)
-#pragma unroll
-    for (int i = 0; i < kT7RY; ++i) cnext[i] = pn[oin[i]];
-    const float hnext = hidx >= 0 ? pn[ohalo] : 0.f;
-    const float *P = plane[cur];
-#pragma unroll
-    for (int i = 0; i < kT7RY; ++i) {
-      const int ly = ty + kT7TY * i + 1, lx = tx + 1;
-      float sum = __fadd_rn(cprev[i], cnext[i]);
-      sum = __fadd_rn(sum, P[(ly - 1) * LW + lx]);
-      sum = __fadd_rn(sum, P[(ly + 1) * LW + lx]);
-      sum = __fadd_rn(sum, P[ly * LW + lx - 1]);
-      sum = __fadd_rn(sum, P[ly * LW + lx + 1]);
-      const float r = __fadd_rn(__fmul_rn(c0, ccur[i]), __fmul_rn(c1, sum));
-      const int64_t yy = y0 + ty + kT7TY * i;
-      if (xc < nx && yy < ny) __builtin_nontemporal_store(r, out + (z + g) * Pyx + oin[i]);
-    }
-    const int nxt = cur ^ 1;
-#pragma unroll
-    for (int i = 0; i < kT7RY; ++i) {
-      plane[nxt][(ty + kT7TY * i + 1) * LW + tx + 1] = cnext[i];
-      cprev[i] = ccur[i];
-      ccur[i] = cnext[i];
-    }
-    if (hidx >= 0) plane[nxt][hidx] = hnext;
-    __syncthreads();
-    cur = nxt;
-  }
-}
-
-// Register-blocked version: one wave owns 64 consecutive x × RY rows of y and
-// streams ZC z planes.  Per plane it loads RY+2 rows (y0-1 .. y0+RY) of plane
-// z+1 — 1.25 loads per cell at RY = 8 — keeps planes z-1, z, z+1 in
-// registers (y±1 neighbours are register reads), and takes x±1 from the
-// neighbouring lanes (ds_bpermute shuffles); only lanes 0 and 63 load one
-// edge value per row.  No LDS tile, no barriers.  Coordinates are clamped
-// to the padded domain; out-of-range cells are not stored.
-template <int RY, int ZC>
-__global__ __launch_bounds__(256) void k_stencil7_reg(const float *__restrict__ u, float *__restrict__ out,
-                                                      int64_t nz, int64_t ny, int64_t nx, int64_t g,
-                                                      float c0, float c1, int64_t z_begin, int64_t z_end) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wv = threadIdx.x / kWave;
-  const int64_t x0 = static_cast<int64_t>(blockIdx.x) * kWave;
-  const int64_t x = x0 + lane;
-  const int64_t y0 = (static_cast<int64_t>(blockIdx.y) * 4 + wv) * RY;
-  const int64_t zs = z_begin + static_cast<int64_t>(blockIdx.z) * ZC;
-  if (zs >= z_end || y0 >= ny) return;  // wave-uniform
-  const int64_t ze = zs + ZC < z_end ? zs + ZC : z_end;
-  const int64_t Px = nx + 2 * g;
-  const int64_t Pyx = (ny + 2 * g) * Px;
-  const int64_t xo = (x < nx ? x : nx) + g;
-  int64_t ex = lane == 0 ? x0 - 1 : x0 + kWave;  // edge column for lanes 0 / 63
-  ex = (ex < nx ? ex : nx) + g;
-  const bool edge = lane == 0 || lane == kWave - 1;
-  int64_t ro[RY + 2];  // row offsets of y0-1 .. y0+RY (clamped)
-#pragma unroll
-  for (int j = 0; j < RY + 2; ++j) {
-    int64_t yy = y0 - 1 + j;
-    yy = yy < ny ? yy : ny;
-    ro[j] = (yy + g) * Px;
-  }
-  const float *pz = u + (zs + g) * Pyx;
-  float m[RY], c[RY + 2], p[RY + 2], e[RY];
-#pragma unroll
-  for (int i = 0; i < RY; ++i) m[i] = pz[ro[i + 1] + xo - Pyx];
-#pragma unroll
-  for (int j = 0; j < RY + 2; ++j) c[j] = pz[ro[j] + xo];
-  for (int64_t z = zs; z < ze; ++z) {
-    const float *pn = pz + Pyx;
-#pragma unroll
-    for (int j = 0; j < RY + 2; ++j) p[j] = pn[ro[j] + xo];
-    if (edge) {
-#pragma unroll
-      for (int i = 0; i < RY; ++i) e[i] = pz[ro[i + 1] + ex];
-    }
-    float *po = out + (z + g) * Pyx;
-#pragma unroll
-    for (int i = 0; i < RY; ++i) {
-      const float cz = c[i + 1];
-      float xm = __shfl_up(cz, 1, kWave);
-      float xp = __shfl_down(cz, 1, kWave);
-      if (lane == 0) xm = e[i];
-      if (lane == kWave - 1) xp = e[i];
-      float sum = __fadd_rn(m[i], p[i + 1]);
-      sum = __fadd_rn(sum, c[i]);
-      sum = __fadd_rn(sum, c[i + 2]);
-      sum = __fadd_rn(sum, xm);
-      sum = __fadd_rn(sum, xp);
-      const float r = __fadd_rn(__fmul_rn(c0, cz), __fmul_rn(c1, sum));
-      if (x < nx && y0 + i < ny) __builtin_nontemporal_store(r, po + ro[i + 1] + xo);
-    }
-#pragma unroll
-    for (int i = 0; i < RY; ++i) m[i] = c[i + 1];
-#pragma unroll
-    for (int j = 0; j < RY + 2; ++j) c[j] = p[j];
-    pz = pn;
-  }
-}
-
-// Streaming version with deep z prefetch (default).  Thread = one (y, x)
-// column of a 64×4 tile, ZC planes; the z loop is unrolled by 4 and the 4
-// planes after the current group are loaded one group ahead, so every wave
-// keeps 4 HBM plane loads (+ 8 L1/L2 y-neighbour loads) in flight instead of
-// one.  x±1 come from neighbouring lanes (ds_bpermute), lanes 0/63 load their
-// edge.  The register ring is rotated by the unroll (static indices only).
-template <int ZC>
-__global__ __launch_bounds__(256) void k_stencil7_pf(const float *__restrict__ u, float *__restrict__ out,
-                                                     int64_t nz, int64_t ny, int64_t nx, int64_t g,
-                                                     float c0, float c1, int64_t z_begin, int64_t z_end,
-                                                     int64_t ntx, int64_t nty, int64_t ntz) {
-  static_assert(ZC % 4 == 0, "z chunk is a multiple of the unroll");
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t t = xcd_tile(blockIdx.x, ntx * nty * ntz);  // x-fastest tiles, XCD-contiguous
-  const int64_t x0 = (t % ntx) * kWave;
-  const int64_t x = x0 + lane;
-  const int64_t y = ((t / ntx) % nty) * 4 + threadIdx.x / kWave;
-  const int64_t zs = z_begin + (t / (ntx * nty)) * ZC;
-  if (zs >= z_end || y >= ny) return;  // wave-uniform
-  const int64_t ze = zs + ZC < z_end ? zs + ZC : z_end;
-  const int64_t Px = nx + 2 * g;
-  const int64_t Pyx = (ny + 2 * g) * Px;
-  const int64_t xo = (x < nx ? x : nx) + g;
-  int64_t ex = lane == 0 ? x0 - 1 : x0 + kWave;
-  ex = (ex < nx ? ex : nx) + g;
-  const bool edge = lane == 0 || lane == kWave - 1;
-  const bool store = x < nx;
-  const int64_t ro = (y + g) * Px;
-  // clamp plane reads to the last existing padded plane (nz + g)
-  const int64_t zmax = nz;  // logical z of the last ghost plane we may read
-  auto ld = [&](int64_t z) -> float {  // center value of logical plane z (clamped)
-    const int64_t zz = z < zmax ? z : zmax;
-    return u[(zz + g) * Pyx + ro + xo];  // plain: neighbours re-read this line as y±1
-  };
-  float r0 = ld(zs - 1), r1 = ld(zs), r2 = ld(zs + 1), r3 = ld(zs + 2), r4 = ld(zs + 3), r5 = ld(zs + 4);
-  for (int64_t z = zs; z < ze; z += 4) {
-    // prefetch the next group's planes z+5 .. z+8
-    const float n0 = ld(z + 5), n1 = ld(z + 6), n2 = ld(z + 7), n3 = ld(z + 8);
-    float ym[4], yp[4], e[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t zz = (z + k) < zmax ? (z + k) : zmax;
-      const float *pl = u + (zz + g) * Pyx + ro + xo;
-      ym[k] = pl[-Px];
-      yp[k] = pl[Px];
-    }
-    if (edge) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int64_t zz = (z + k) < zmax ? (z + k) : zmax;
-        e[k] = u[(zz + g) * Pyx + ro + ex];
-      }
-    }
-    const float cz[4] = {r1, r2, r3, r4};
-    const float zm[4] = {r0, r1, r2, r3};
-    const float zp[4] = {r2, r3, r4, r5};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float xm = __shfl_up(cz[k], 1, kWave);
-      float xp = __shfl_down(cz[k], 1, kWave);
-      if (lane == 0) xm = e[k];
-      if (lane == kWave - 1) xp = e[k];
-      float sum = __fadd_rn(zm[k], zp[k]);
-      sum = __fadd_rn(sum, ym[k]);
-      sum = __fadd_rn(sum, yp[k]);
-      sum = __fadd_rn(sum, xm);
-      sum = __fadd_rn(sum, xp);
-      const float r = __fadd_rn(__fmul_rn(c0, cz[k]), __fmul_rn(c1, sum));
-      if (store && z + k < ze) out[(z + k + g) * Pyx + ro + xo] = r;
-    }
-    r0 = r4;
-    r1 = r5;
-    r2 = n0;
-    r3 = n1;
-    r4 = n2;
-    r5 = n3;
-  }
-}
-
-// Ring version (default).  A wave covers 64 consecutive x of which lanes
-// 1..62 produce output (lanes 0/63 only supply x±1 through shuffles: no edge
-// loads), RY rows of y, and streams ZC z planes through a 4-plane register
-// ring (planes z-1, z, z+1 and the one being loaded, z+2).  The rotation is
-// unrolled 4× so no register is ever copied: every load's first use is one
-// plane-step after it was issued and s_waitcnt leaves the newest plane's
-// RY+2 loads in flight.  Tiles are XCD-remapped (x fastest) so row-edge
-// cache lines and y halo rows are shared inside one L2.
-template <int RY, int ZC, bool DIAG_NOSTORE = false>
-__global__ __launch_bounds__(256) void k_stencil7_ring(const float *__restrict__ u, float *__restrict__ out,
-                                                       int64_t nz, int64_t ny, int64_t nx, int64_t g,
-                                                       float c0, float c1, int64_t z_begin, int64_t z_end,
-                                                       int64_t ntx, int64_t nty, int64_t ntz) {
-  static_assert(ZC % 4 == 0, "z chunk is a multiple of the ring");
-  constexpr int XW = kWave - 2;  // output columns per wave
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t t = xcd_tile(blockIdx.x, ntx * nty * ntz);
-  const int64_t x = (t % ntx) * XW - 1 + lane;  // lanes 0 / 63 are the x halo
-  const int64_t y0 = (((t / ntx) % nty) * 4 + threadIdx.x / kWave) * RY;
-  const int64_t zs = z_begin + (t / (ntx * nty)) * ZC;
-  if (zs >= z_end || y0 >= ny) return;  // wave-uniform
-  const int64_t ze = zs + ZC < z_end ? zs + ZC : z_end;
-  const int64_t Px = nx + 2 * g;
-  const int64_t Pyx = (ny + 2 * g) * Px;
-  const int64_t xo = (x < nx ? x : nx) + g;  // x >= -1 always
-  const bool store = lane >= 1 && lane <= kWave - 2 && x < nx;
-  int64_t ro[RY + 2];
-#pragma unroll
-  for (int j = 0; j < RY + 2; ++j) {
-    int64_t yy = y0 - 1 + j;
-    yy = yy < ny ? yy : ny;
-    ro[j] = (yy + g) * Px + xo;
-  }
-  auto plane = [&](int64_t z) -> const float * {  // logical plane z (clamped to the last ghost plane)
-    return u + ((z < nz ? z : nz) + g) * Pyx;
-  };
-  float A[RY + 2], B[RY + 2], C[RY + 2], D[RY + 2];
-  auto load = [&](float(&R)[RY + 2], int64_t z) {
-    const float *pl = plane(z);
-#pragma unroll
-    for (int j = 0; j < RY + 2; ++j) R[j] = pl[ro[j]];
-  };
-  float diag = 0.f;  // DIAG_NOSTORE: keeps the arithmetic live without the stores
-  auto step = [&](const float(&M)[RY + 2], const float(&Cc)[RY + 2], const float(&Pp)[RY + 2], int64_t z) {
-    float *po = out + (z + g) * Pyx;
-#pragma unroll
-    for (int i = 0; i < RY; ++i) {
-      const float cz = Cc[i + 1];
-      const float xm = __shfl_up(cz, 1, kWave);
-      const float xp = __shfl_down(cz, 1, kWave);
-      float sum = __fadd_rn(M[i + 1], Pp[i + 1]);
-      sum = __fadd_rn(sum, Cc[i]);
-      sum = __fadd_rn(sum, Cc[i + 2]);
-      sum = __fadd_rn(sum, xm);
-      sum = __fadd_rn(sum, xp);
-      const float r = __fadd_rn(__fmul_rn(c0, cz), __fmul_rn(c1, sum));
-      if constexpr (DIAG_NOSTORE)
-        diag += r;
-      else if (store && z < ze && y0 + i < ny)
-        po[ro[i + 1]] = r;
-    }
-  };
-  load(A, zs - 1);
-  load(B, zs);
-  load(C, zs + 1);
-  for (int64_t z = zs; z < ze; z += 4) {
-    load(D, z + 2);
-    step(A, B, C, z);
-    load(A, z + 3);
-    step(B, C, D, z + 1);
-    load(B, z + 4);
-    step(C, D, A, z + 2);
-    load(C, z + 5);
-    step(D, A, B, z + 3);
-  }
-  if constexpr (DIAG_NOSTORE)
-    if (diag == 1234.5f) out[0] = diag;
-}
-
-// Wide-ring version (default).  Like k_stencil7_ring, but a wave covers NJ×64
-// consecutive x (lane l, block j → x = x0 + 64j + l) so that nearly every
-// 128-B line of an output row is written by one wave's NJ back-to-back
-// stores (the padded 514-float rows are not line-aligned; lines split across
-// waves that store at different times cost partial-line merges — measured
-// 116 µs without stores vs 296 µs with them on the 64-wide ring).  x±1 inside
-// the tile come from shuffles / readlanes of the neighbouring block; the two
-// tile-edge values are loaded by lanes 0 and 63 as part of the plane ring.
-template <int RY, int NJ, int ZC, int STORE = 0>  // STORE: 0 plain, 1 non-temporal, 2 none (diagnostic)
-__global__ __launch_bounds__(256) void k_stencil7_wide(const float *__restrict__ u, float *__restrict__ out,
-                                                       int64_t nz, int64_t ny, int64_t nx, int64_t g,
-                                                       float c0, float c1, int64_t z_begin, int64_t z_end,
-                                                       int64_t ntx, int64_t nty, int64_t ntz) {
-  static_assert(ZC % 4 == 0, "z chunk is a multiple of the ring");
-  constexpr int TW = NJ * kWave;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t t = xcd_tile(blockIdx.x, ntx * nty * ntz);
-  const int64_t x0 = (t % ntx) * TW;
-  const int64_t y0 = (((t / ntx) % nty) * 4 + threadIdx.x / kWave) * RY;
-  const int64_t zs = z_begin + (t / (ntx * nty)) * ZC;
-  if (zs >= z_end || y0 >= ny) return;  // wave-uniform
-  const int64_t ze = zs + ZC < z_end ? zs + ZC : z_end;
-  const int64_t Px = nx + 2 * g;
-  const int64_t Pyx = (ny + 2 * g) * Px;
-  // in-plane offsets fit 32 bits (the host checks one padded plane < 2^31 cells)
-  int xo[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int64_t x = x0 + kWave * j + lane;
-    xo[j] = static_cast<int>((x < nx ? x : nx) + g);
-  }
-  int64_t ex64 = lane == 0 ? x0 - 1 : x0 + TW;  // lane 0: left halo, lane 63: right halo
-  const int ex = static_cast<int>((ex64 < nx ? ex64 : nx) + g);
-  int ro[RY + 2];
-#pragma unroll
-  for (int r = 0; r < RY + 2; ++r) {
-    int64_t yy = y0 - 1 + r;
-    yy = yy < ny ? yy : ny;
-    ro[r] = static_cast<int>((yy + g) * Px);
-  }
-  auto plane = [&](int64_t z) -> const float * { return u + ((z < nz ? z : nz) + g) * Pyx; };
-  // ring slot: rows y0-1 .. y0+RY, NJ values each, + edge values for rows y0 .. y0+RY-1
-  struct Slot {
-    float v[RY + 2][NJ];
-    float e[RY];
-  };
-  Slot A, B, C, D;
-  auto load = [&](Slot &S, int64_t z) {
-    const float *pl = plane(z);
-#pragma unroll
-    for (int r = 0; r < RY + 2; ++r)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) S.v[r][j] = pl[ro[r] + xo[j]];
-#pragma unroll
-    for (int r = 0; r < RY; ++r) S.e[r] = pl[ro[r + 1] + ex];
-  };
-  float diag = 0.f;
-  auto step = [&](const Slot &M, const Slot &Cc, const Slot &Pp, int64_t z) {
-    if (z >= ze) return;
-    float *po = out + (z + g) * Pyx;
-#pragma unroll
-    for (int r = 0; r < RY; ++r) {
-      if (y0 + r >= ny) break;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const float cz = Cc.v[r + 1][j];
-        float xm = __shfl_up(cz, 1, kWave);
-        float xp = __shfl_down(cz, 1, kWave);
-        const float lft = j > 0 ? __shfl(Cc.v[r + 1][j > 0 ? j - 1 : 0], kWave - 1, kWave) : Cc.e[r];
-        const float rgt = j < NJ - 1 ? __shfl(Cc.v[r + 1][j < NJ - 1 ? j + 1 : 0], 0, kWave) : Cc.e[r];
-        if (lane == 0) xm = lft;
-        if (lane == kWave - 1) xp = rgt;
-        float sum = __fadd_rn(M.v[r + 1][j], Pp.v[r + 1][j]);
-        sum = __fadd_rn(sum, Cc.v[r][j]);
-        sum = __fadd_rn(sum, Cc.v[r + 2][j]);
-        sum = __fadd_rn(sum, xm);
-        sum = __fadd_rn(sum, xp);
-        const float res = __fadd_rn(__fmul_rn(c0, cz), __fmul_rn(c1, sum));
-        if constexpr (STORE == 2) {
-          diag += res;
-        } else if (x0 + kWave * j + lane < nx) {
-          if constexpr (STORE == 1)
-            __builtin_nontemporal_store(res, po + ro[r + 1] + xo[j]);
-          else
-            po[ro[r + 1] + xo[j]] = res;
-        }
-      }
-    }
-  };
-  load(A, zs - 1);
-  load(B, zs);
-  load(C, zs + 1);
-  for (int64_t z = zs; z < ze; z += 4) {
-    load(D, z + 2);
-    step(A, B, C, z);
-    load(A, z + 3);
-    step(B, C, D, z + 1);
-    load(B, z + 4);
-    step(C, D, A, z + 2);
-    load(C, z + 5);
-    step(D, A, B, z + 3);
-  }
-  if constexpr (STORE == 2)
-    if (diag == 1234.5f) out[0] = diag;
-}
-
-// Buffer-addressed wide ring (default).  Same tiling and summation order as
-// k_stencil7_wide, re-addressed so the ring costs registers only for data:
+// Buffer-addressed ring: a wave owns RY rows × 64·NJ consecutive x and streams
+// a z chunk through a register ring of planes (z-1, z, z+1 in use, PF
+// loading), addressed so the ring costs registers only for data:
 //  * loads/stores are raw buffer ops on per-row descriptors (scalar base =
 //    plane + row), voffset = one per-lane VGPR (x), the 64-float block step an
 //    immediate — no 64-bit VGPR address per load (the flat version spent ~200
@@ -805,7 +374,7 @@ constexpr int kDppWaveShr1 = 0x138;  // lane i ← lane i-1 (lane 0 keeps `old`)
 // STORE: 0 plain dword stores, 1 non-temporal dword stores, 4 staged: each row's
 // results go to the wave's LDS row (shifted so the body is 16-B aligned) and
 // leave as float4 stores plus ≤ 3-float head/tail pieces (needs a 16-B aligned
-// `out`); 2 no stores and 3 line-aligned rows are timing diagnostics.
+// `out`).
 template <int RY, int NJ, int STORE, int PF = 1>
 __global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ u, float *__restrict__ out,
                                                       int64_t nz, int64_t ny, int64_t nx, int64_t g,
@@ -857,7 +426,6 @@ __global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ 
       if (r >= 1 && r <= RY) S.e[r - 1] = bitsf(__builtin_amdgcn_raw_buffer_load_b32(rs, ve, 0, 0));
     }
   };
-  float diag = 0.f;
   constexpr int SROW = STORE == 4 ? TW + 4 : 1;
   __shared__ __attribute__((aligned(16))) float stage[STORE == 4 ? 4 : 1][STORE == 4 ? RY : 1][SROW];
   const int64_t len = nx - x0 < TW ? nx - x0 : TW;  // outputs of this tile per row
@@ -873,11 +441,7 @@ __global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ 
 #pragma unroll
     for (int r = 0; r < RY; ++r) {
       if (y0 + r >= ny) break;
-      auto ws = rsrc(out, z, r + 1);
-      if constexpr (STORE == 3) {  // diagnostic: same stores, row start rounded down to a 128-B line
-        const int64_t off = ((z < nz ? z : nz) + g) * Pyx + rowo[r + 1];
-        ws = __builtin_amdgcn_make_buffer_rsrc(out + (off & ~int64_t{31}), 0, 0x7fffffff, 0x00020000);
-      }
+      const auto ws = rsrc(out, z, r + 1);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const float cz = Cc.v[r + 1][j];
@@ -895,13 +459,10 @@ __global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ 
         sum = __fadd_rn(sum, xm);
         sum = __fadd_rn(sum, xp);
         const float res = __fadd_rn(__fmul_rn(c0, cz), __fmul_rn(c1, sum));
-        if constexpr (STORE == 2) {
-          diag += res;
-        } else if constexpr (STORE == 4) {
+        if constexpr (STORE == 4) {
           stage[w][r][kWave * j + lane + ((4 - hd[r]) & 3)] = res;  // x_local + shift: body 16-B aligned
         } else if (x0 + kWave * j + lane < nx) {
-          __builtin_amdgcn_raw_buffer_store_b32(fbits(res), ws, (STORE == 3 ? vx - 4 * g : vx) + 256 * j, 0,
-                                                STORE == 1 ? 2 : 0);
+          __builtin_amdgcn_raw_buffer_store_b32(fbits(res), ws, vx + 256 * j, 0, STORE == 1 ? 2 : 0);
         }
       }
     }
@@ -940,8 +501,6 @@ __global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ 
       step(R[k % NS], R[(k + 1) % NS], R[(k + 2) % NS], z + k);
     }
   }
-  if constexpr (STORE == 2)
-    if (diag == 1234.5f) out[0] = diag;
 }
 
 // x4 ring (`LHPC_STENCIL7_IMPL=buf4`): the buffer ring with 4 consecutive x per
@@ -954,7 +513,7 @@ __global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ 
 // nx % (64·NJ) == 0: every x4 of a tile then ends at or before column nx-1+g,
 // so none reaches past the array end (a partially out-of-range x4 is not
 // relied on).  STORE: 5 the 4 results leave as one unaligned dwordx4 store,
-// 6 the same non-temporal, 2 no stores (timing diagnostic).
+// 6 the same non-temporal.
 template <int RY, int NJ, int STORE, int PF = 1>
 __global__ __launch_bounds__(256) void k_stencil7_buf4(const float *__restrict__ u, float *__restrict__ out,
                                                        int64_t nz, int64_t ny, int64_t nx, int64_t g,
@@ -1004,7 +563,6 @@ __global__ __launch_bounds__(256) void k_stencil7_buf4(const float *__restrict__
       if (r >= 1 && r <= RY) S.e[r - 1] = bitsf(__builtin_amdgcn_raw_buffer_load_b32(rs, ve, 0, 0));
     }
   };
-  float diag = 0.f;
   auto step = [&](const Slot &M, const Slot &Cc, const Slot &Pp, int64_t z) {
     if (z >= ze) return;
 #pragma unroll
@@ -1033,11 +591,9 @@ __global__ __launch_bounds__(256) void k_stencil7_buf4(const float *__restrict__
           sum = __fadd_rn(sum, xm);
           sum = __fadd_rn(sum, xp);
           const float o = __fadd_rn(__fmul_rn(c0, cz), __fmul_rn(c1, sum));
-          if constexpr (STORE == 2) diag += o;
           res[k] = static_cast<uint32_t>(fbits(o));
         }
-        if constexpr (STORE != 2)
-          __builtin_amdgcn_raw_buffer_store_b128(res, ws, vx + 1024 * j, 0, STORE == 6 ? 2 : 0);
+        __builtin_amdgcn_raw_buffer_store_b128(res, ws, vx + 1024 * j, 0, STORE == 6 ? 2 : 0);
       }
     }
   };
@@ -1050,8 +606,6 @@ __global__ __launch_bounds__(256) void k_stencil7_buf4(const float *__restrict__
       step(R[k % NS], R[(k + 1) % NS], R[(k + 2) % NS], z + k);
     }
   }
-  if constexpr (STORE == 2)
-    if (diag == 1234.5f) out[0] = diag;
 }
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -1072,11 +626,6 @@ int blur_launch(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int
   if (!ydir) {
     if (nb == 8) {
       constexpr int SEG = 4 * kBlurThreads;
-      const int rows = [] {
-        const char *e = std::getenv("LHPC_BLUR_X_ROWS");
-        const int r = e ? std::atoi(e) : 2;
-        return (r == 1 || r == 2 || r == 4 || r == 8) ? r : 2;
-      }();
       const int64_t nseg = (nx + SEG - 1) / SEG;
       const bool vec = aligned16(a) && aligned16(b) && P % 4 == 0 && nx % 4 == 0 &&
                        (ghost - 8) % 4 == 0;
@@ -1084,10 +633,10 @@ int blur_launch(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int
 #define LHPC_BX(V, R)                                                                                  \
   hipLaunchKernelGGL((k_blur_x<8, V, R>), dim3(static_cast<unsigned>(((ny + R - 1) / R) * nseg)), bd, 0, s, \
                      a, b, ny, nx, ghost)
-      // default: the wave-private kernel, 2 rows per wave (measured 85 us vs 99-103 us for the
-      // block-LDS kernel on 8192^2); "lds" selects k_blur_x (LHPC_BLUR_X_ROWS)
-      const char *ximpl = std::getenv("LHPC_BLUR_X_IMPL");
-      if (vec && !(ximpl && !std::strcmp(ximpl, "lds"))) {
+      // the wave-private kernel, 2 rows per wave (measured 85 us against 99-103 us for the
+      // block-LDS kernel on 8192^2); the block-LDS kernel only for rows that
+      // are not 16-B aligned
+      if (vec) {
         const char *e = std::getenv("LHPC_BLUR_X_RW");
         const int rw = e ? std::atoi(e) : 2;
         const int64_t nseg256 = (nx + 255) / 256;
@@ -1106,13 +655,6 @@ int blur_launch(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int
           default: LHPC_BXW(8); break;
         }
 #undef LHPC_BXW
-      } else if (vec) {
-        switch (rows) {
-          case 1: LHPC_BX(true, 1); break;
-          case 8: LHPC_BX(true, 8); break;
-          case 4: LHPC_BX(true, 4); break;
-          default: LHPC_BX(true, 2); break;
-        }
       } else {
         LHPC_BX(false, 2);
       }
@@ -1177,24 +719,18 @@ int blur_entry(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int6
 int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, int64_t g, float c0,
               float c1, int64_t zb, int64_t ze, hipStream_t s) {
   if (zb >= ze || ny == 0 || nx == 0) return LHPC_OK;
-  // implementation: buf (default; its x4 form buf4 when the x tiles are full); "wide", "ring",
-  // "simple", "pf", "reg", "lds" are measured alternatives
+  // implementation: the buffer ring ("buf"), in its x4 form ("buf4") when the x
+  // tiles are full; the thread-per-column kernel only when a row's byte
+  // offset does not fit a buffer voffset.  The measured alternatives (LDS
+  // 2.5-D tile, register ring, deep prefetch, flat wide ring) are in DESIGN.md §4.
   const char *impl = std::getenv("LHPC_STENCIL7_IMPL");
-  const bool use_lds = impl && !std::strcmp(impl, "lds");
-  const bool use_reg = impl && !std::strcmp(impl, "reg");
-  const bool use_pf = impl && !std::strcmp(impl, "pf");
-  const bool use_ring = impl && !std::strcmp(impl, "ring");
-  const bool plane32 = (ny + 2 * g) * (nx + 2 * g) < (int64_t{1} << 31);
-  const bool use_wide = impl && !std::strcmp(impl, "wide");
-  // Store policy: "staged" | "plain" | "nt" | "none" / "aligned" (timing diagnostics).  Default:
-  // staged float4 stores for the buffer ring (219-220 us vs 225-226 plain on 512^3; plain when
-  // `out` is not 16-B aligned), non-temporal for the flat wide ring (234-238 vs 234-255 us).
+  // Store policy of the dword ring: "staged" (default: float4 stores via the
+  // wave's LDS row, 219-220 us vs 225-226 plain on 512^3; plain when `out` is
+  // not 16-B aligned) | "plain" | "nt".
   const char *stm = std::getenv("LHPC_STENCIL7_STORE");
   const bool buf4_req = impl && !std::strcmp(impl, "buf4");
   const bool buf_impl = !impl || !std::strcmp(impl, "buf") || buf4_req;
-  int store_mode = stm ? (!std::strcmp(stm, "plain") ? 0 : !std::strcmp(stm, "none") ? 2
-                          : !std::strcmp(stm, "aligned") ? 3 : !std::strcmp(stm, "staged") ? 4 : 1)
-                       : (buf_impl ? 4 : 1);
+  int store_mode = stm ? (!std::strcmp(stm, "plain") ? 0 : !std::strcmp(stm, "staged") ? 4 : 1) : 4;
   if (store_mode == 4 && !aligned16(out)) store_mode = 0;  // staged float4 stores need a 16-B base
   // buffer-addressed ring: the in-row byte offset (voffset) must fit 31 bits
   const bool row_b31 = (nx + 2 * g + 1024) * 4 < (int64_t{1} << 31);
@@ -1218,8 +754,8 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
       const int64_t nchunks = std::max<int64_t>(1, (target + xy - 1) / xy);
       zc = static_cast<int>(std::max<int64_t>(4, (ze - zb + nchunks - 1) / nchunks));
     }
-    if (buf4) {  // x4 ring: non-temporal dwordx4 stores ("plain": plain, "none": diagnostic)
-      const int m4 = stm && !std::strcmp(stm, "none") ? 2 : stm && !std::strcmp(stm, "plain") ? 5 : 6;
+    if (buf4) {  // x4 ring: non-temporal dwordx4 stores ("plain": plain)
+      const int m4 = stm && !std::strcmp(stm, "plain") ? 5 : 6;
 #define LHPC_S74_M(RY, NJ, M)                                                                          \
   do {                                                                                                 \
     const int64_t ntx = nx / (NJ * kWave), nty = (ny + 4 * RY - 1) / (4 * RY), ntz = (ze - zb + zc - 1) / zc; \
@@ -1235,8 +771,7 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
   } while (0)
 #define LHPC_S74(RY, NJ)                            \
   do {                                              \
-    if (m4 == 2) LHPC_S74_M(RY, NJ, 2);             \
-    else if (m4 == 5) LHPC_S74_M(RY, NJ, 5);        \
+    if (m4 == 5) LHPC_S74_M(RY, NJ, 5);             \
     else LHPC_S74_M(RY, NJ, 6);                     \
   } while (0)
       if (ry == 1 && nj == 8) LHPC_S74(1, 8);
@@ -1266,8 +801,6 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
 #define LHPC_S7B(RY, NJ)                                 \
   do {                                                   \
     if (store_mode == 1) LHPC_S7B_M(RY, NJ, 1);          \
-    else if (store_mode == 2) LHPC_S7B_M(RY, NJ, 2);     \
-    else if (store_mode == 3) LHPC_S7B_M(RY, NJ, 3);     \
     else if (store_mode == 4) LHPC_S7B_M(RY, NJ, 4);     \
     else LHPC_S7B_M(RY, NJ, 0);                          \
   } while (0)
@@ -1279,67 +812,6 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
     else LHPC_S7B(2, 8);
 #undef LHPC_S7B
 #undef LHPC_S7B_M
-    return check_launch(s);
-  }
-  if ((use_wide || !impl) && plane32) {
-    const char *cfg = std::getenv("LHPC_STENCIL7_WIDE");  // "RY,NJ"
-    int ry = 2, nj = 8;  // measured best on 512^3
-    if (cfg) std::sscanf(cfg, "%d,%d", &ry, &nj);
-    constexpr int ZC = 32;
-#define LHPC_S7W_M(RY, NJ, M)                                                                        \
-  do {                                                                                               \
-    const int64_t ntx = (nx + NJ * kWave - 1) / (NJ * kWave), nty = (ny + 4 * RY - 1) / (4 * RY),       \
-                  ntz = (ze - zb + ZC - 1) / ZC;                                                     \
-    hipLaunchKernelGGL((k_stencil7_wide<RY, NJ, ZC, M>), dim3(static_cast<unsigned>(ntx * nty * ntz)), \
-                       dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz);         \
-  } while (0)
-#define LHPC_S7W(RY, NJ)                       \
-  do {                                         \
-    if (store_mode == 1) LHPC_S7W_M(RY, NJ, 1); \
-    else if (store_mode == 2) LHPC_S7W_M(RY, NJ, 2); \
-    else LHPC_S7W_M(RY, NJ, 0);                \
-  } while (0)
-    if (ry == 1 && nj == 8) LHPC_S7W(1, 8);
-    else if (ry == 4 && nj == 2) LHPC_S7W(4, 2);
-    else if (ry == 1 && nj == 4) LHPC_S7W(1, 4);
-    else if (ry == 2 && nj == 4) LHPC_S7W(2, 4);
-    else LHPC_S7W(2, 8);
-#undef LHPC_S7W
-#undef LHPC_S7W_M
-    return check_launch(s);
-  }
-  if (use_ring) {
-    constexpr int RY = 4, ZC = 32;
-    const int64_t ntx = (nx + kWave - 3) / (kWave - 2), nty = (ny + 4 * RY - 1) / (4 * RY),
-                  ntz = (ze - zb + ZC - 1) / ZC;
-    const char *diag = std::getenv("LHPC_STENCIL7_DIAG_NOSTORE");  // diagnostic timing build only
-    if (diag && std::atoi(diag))
-      hipLaunchKernelGGL((k_stencil7_ring<RY, ZC, true>), dim3(static_cast<unsigned>(ntx * nty * ntz)), dim3(256), 0,
-                         s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz);
-    else
-      hipLaunchKernelGGL((k_stencil7_ring<RY, ZC>), dim3(static_cast<unsigned>(ntx * nty * ntz)), dim3(256), 0, s,
-                         u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz);
-    return check_launch(s);
-  }
-  if (use_pf) {
-    constexpr int ZC = 32;
-    const int64_t ntx = (nx + kWave - 1) / kWave, nty = (ny + 3) / 4, ntz = (ze - zb + ZC - 1) / ZC;
-    hipLaunchKernelGGL((k_stencil7_pf<ZC>), dim3(static_cast<unsigned>(ntx * nty * ntz)), dim3(256), 0, s, u, out,
-                       nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz);
-    return check_launch(s);
-  }
-  if (use_reg) {
-    constexpr int RY = 8, ZC = 32;
-    dim3 grid(static_cast<unsigned>((nx + kWave - 1) / kWave), static_cast<unsigned>((ny + 4 * RY - 1) / (4 * RY)),
-              static_cast<unsigned>((ze - zb + ZC - 1) / ZC));
-    hipLaunchKernelGGL((k_stencil7_reg<RY, ZC>), grid, dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze);
-    return check_launch(s);
-  }
-  if (use_lds) {
-    constexpr int ZC = 32;
-    dim3 grid(static_cast<unsigned>((nx + kT7X - 1) / kT7X), static_cast<unsigned>((ny + kT7Y - 1) / kT7Y),
-              static_cast<unsigned>((ze - zb + ZC - 1) / ZC));
-    hipLaunchKernelGGL((k_stencil7_lds<ZC>), grid, dim3(kT7X, kT7TY), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze);
     return check_launch(s);
   }
   const int64_t ntx = (nx + kS7X - 1) / kS7X, nty = (ny + kS7Y - 1) / kS7Y, ntz = (ze - zb + kS7Z - 1) / kS7Z;

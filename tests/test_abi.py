@@ -71,6 +71,24 @@ def test_plan_create_bad_csr(lhpc):
     assert st == -2
 
 
+@pytest.mark.parametrize("col", [[0, 5], [0, -1], [0, 2], [-2147483648, 0]])
+@pytest.mark.parametrize("flags", [0, 1 << 9, 1 << 6, 1 << 4])  # default, FORCE_XTILE, FORCE_XSLICE, FORCE_ROWGROUP
+def test_plan_create_rejects_bad_columns_without_validate(lhpc, col, flags):
+    """Out-of-range or negative col_idx is LHPC_ERR_BAD_CSR on every path,
+    with or without LHPC_PLAN_VALIDATE: the layout builders index host
+    arrays by column, so the check runs before any of them (and before the
+    device is touched)."""
+    st, h = _create(lhpc, col=np.array(col, np.int32), flags=flags)
+    assert st == -2 and not h.value
+
+
+def test_plan_create_rejects_decreasing_row_ptr_without_validate(lhpc):
+    st, h = _create(lhpc, n_rows=3, row_ptr=np.array([0, 2, 1, 2], np.int32))
+    assert st == -2 and not h.value
+    st, h = _create(lhpc, n_rows=3, row_ptr=np.array([0, 2, 1, 2], np.int64), bits=64)
+    assert st == -2 and not h.value
+
+
 def test_plan_create_without_device_fails_loudly(lhpc):
     if lhpc.device_count() > 0:
         pytest.skip("a GPU is present")

@@ -171,3 +171,16 @@ def test_coo_to_csr_rejects_out_of_range(lhpc, gpu):
         lhpc.coo_to_csr(4, 4, np.array([0, 4], np.int32), np.array([0, 0], np.int32), np.ones(2, np.float32))
     with pytest.raises(lhpc.LhpcError):
         lhpc.coo_to_csr(4, 4, np.array([0, 1], np.int32), np.array([-1, 0], np.int32), np.ones(2, np.float64))
+
+
+def test_sort_u32_reference_100m(lhpc, gpu):
+    """The reference's largest GPU radix-sort test size, 100,000,000 keys
+    (tests/test_radixsort_gpu_local_count/src/test_radix_local_count.cu:199-201),
+    uniform 32-bit keys: the device sort equals numpy's sort bit for bit."""
+    keys = _keys(100_000_000, "uniform", 0x5EED100)
+    t = _dev(gpu, keys.view(np.int32))
+    lhpc.radix_sort(t)
+    got = _u32_view(t)
+    del t
+    keys.sort(kind="stable")
+    assert np.array_equal(got, keys)

@@ -150,6 +150,72 @@ def test_full_size_c2_c3(lhpc, gpu, dtype):
         del rp, col, val
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_full_size_c4(lhpc, gpu, dtype):
+    """BASELINE configs[3] (C4) at full size, as bench.py --workload c4 builds
+    it: n = 10M power-law rows (l in [1, 10^4], three rows forced to 10^4
+    before the seeded row shuffle), through the default plan (XTILE + chunk fix-ups), against the
+    oracle on every row; the dyadic twin bit-exact; fp32 and fp64 (§8d)."""
+    import torch
+    dt = lhpc.F32 if dtype == "f32" else lhpc.F64
+    n = 10_000_000
+    for dist in (0, 1):
+        rp, col, val = lhpc.gen_powerlaw_csr(n, n, dtype=dt, dist=dist)
+        lens = np.diff(rp)
+        assert lens.max() == 10_000 and np.count_nonzero(lens == 10_000) >= 3  # forced rows, then shuffled
+        x = lhpc.gen_values(dt, dist, n, lhpc.SEED_X)
+        with lhpc.SpMVPlan(rp, col, val, n) as plan:
+            info = plan.info()
+            assert info["kernel"] == lhpc.KERNEL_XTILE and info["n_long_rows"] > 0
+            y = plan(torch.from_numpy(x).to(gpu)).cpu().numpy()
+        y64, yr, asum = S.spmv_oracle(rp, col, val, x)
+        if dist == 1:
+            assert np.array_equal(y, yr)
+        else:
+            S.assert_spmv_close(y, y64, asum)
+        del rp, col, val
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("wl", ["c2", "c3"])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_split_plans_at_rank_sizes(lhpc, gpu, wl, world):
+    """The N > 1 bench path at full C2 / C3 size: for world N and K = 2
+    chunks per rank, the first and the last rank's row-range plan
+    (InterleavedBlocks.local_csr_all → stage → range per chunk) reproduce the
+    oracle's rows of that rank's blocks — bit-exact on the dyadic twin,
+    within the fp bar on random values."""
+    import torch
+    from libhpc_amd.dist import InterleavedBlocks
+    dt = lhpc.F32 if wl == "c2" else lhpc.F64
+    n, K = 10_000_000, 2
+    for dist in (0, 1):
+        rp, col, val = lhpc.gen_uniform_csr(n, n, 15, dtype=dt, dist=dist)
+        x = lhpc.gen_values(dt, dist, n, lhpc.SEED_X)
+        xd = torch.from_numpy(x).to(gpu)
+        y64, yr, asum = S.spmv_oracle(rp, col, val, x)
+        ib = InterleavedBlocks(n, world, K)
+        for rank in (0, world - 1):
+            lrp, lc, lv, splits = ib.local_csr_all(rp, col, val, rank)
+            with lhpc.SpMVPlan(lrp, lc, lv, n, splits=splits) as plan:
+                assert plan.info()["kernel"] == lhpc.KERNEL_XTILE
+                ys = [torch.empty(ib.B, dtype=xd.dtype, device=gpu) for _ in range(K)]
+                plan.stage(xd)
+                for k in range(K):
+                    plan.range(k, ys[k])
+                got = [t.cpu().numpy() for t in ys]
+            for k in range(K):
+                r0, r1 = ib.rows(rank, k)
+                g = got[k][:r1 - r0]
+                assert np.all(got[k][r1 - r0:] == 0)  # padded empty rows
+                if dist == 1:
+                    assert np.array_equal(g, yr[r0:r1]), (wl, world, rank, k)
+                else:
+                    S.assert_spmv_close(g, y64[r0:r1], asum[r0:r1])
+        del rp, col, val
+
+
 def test_partitioned_blocks_concatenate_bit_exact(lhpc, gpu):
     """Row-block split used by multi-GPU runs: per-block plans (rebased row_ptr,
     global columns) concatenate to exactly the unpartitioned y."""
@@ -171,18 +237,6 @@ def test_partitioned_blocks_concatenate_bit_exact(lhpc, gpu):
     assert np.array_equal(np.concatenate(parts), y_full)
 
 
-@pytest.mark.parametrize("path", [p for p in GOLDEN_SPMV if "dyadic" in p or "powerlaw" in p],
-                         ids=lambda p: os.path.basename(p)[5:-4])
-def test_golden_xslice_fused_reduction(lhpc, gpu, path, monkeypatch):
-    """Opt-in fused slice reduction (last-arriver hand-off) gives the same bits."""
-    monkeypatch.setenv("LHPC_XSLICE_FUSE", "1")
-    g = S.load_golden(os.path.basename(path))
-    y, info = _run(lhpc, gpu, g["row_ptr"], g["col_idx"], g["val"], g["x"], int(g["n_cols"]),
-                   FAMILIES["xslice"])
-    assert info["launches"] == 1
-    assert np.array_equal(y, g["y_exact"].astype(g["val"].dtype))
-
-
 def test_interleaved_chunk_plans_on_gpu(lhpc, gpu):
     """The multi-GPU data path at world=1: K interleaved chunk plans (padded
     local CSR blocks, as bench.py --gpus N builds them) assemble to exactly
@@ -202,18 +256,6 @@ def test_interleaved_chunk_plans_on_gpu(lhpc, gpu):
     for p in plans:
         p.close()
     assert np.array_equal(y, y_ref)
-
-
-@pytest.mark.parametrize("path", [p for p in GOLDEN_SPMV if "dyadic" in p or "powerlaw" in p],
-                         ids=lambda p: os.path.basename(p)[5:-4])
-def test_golden_xslice_persistent(lhpc, gpu, path, monkeypatch):
-    """Opt-in persistent partial-free XSLICE gives the same bits on dyadic data."""
-    monkeypatch.setenv("LHPC_XSLICE_PERSIST", "1")
-    g = S.load_golden(os.path.basename(path))
-    y, info = _run(lhpc, gpu, g["row_ptr"], g["col_idx"], g["val"], g["x"], int(g["n_cols"]),
-                   FAMILIES["xslice"])
-    assert info["launches"] == 1
-    assert np.array_equal(y, g["y_exact"].astype(g["val"].dtype))
 
 
 # ------------------------------------------------------------------ XTILE
@@ -257,15 +299,11 @@ def _csr_from_lengths(lengths, n_cols, seed, dyadic):
     return rp, col, val
 
 
-@pytest.fixture(params=["seg", "cm", "pair", "iperm"])
+@pytest.fixture(params=["perm", "iperm"])
 def xt_layout(request, monkeypatch):
-    """The XTILE layouts: tile-stream xg + segment table (default), chunk-major
-    xg, the tile stream with segments padded to even lengths
-    (LHPC_XTILE_PAIR=1: the reduce loads xg/perm as aligned pairs), and the
-    iperm reduce (LHPC_XTILE_IPERM=1: xg kept in flat order in LDS, each CSR
-    position's x gathered through a CSR-order index)."""
-    monkeypatch.setenv("LHPC_XTILE_LAYOUT", "cm" if request.param == "cm" else "seg")
-    monkeypatch.setenv("LHPC_XTILE_PAIR", "1" if request.param == "pair" else "0")
+    """The XTILE reduce index streams: perm (xg scattered into CSR slots) and
+    iperm (xg kept in flat order in LDS, each CSR position's x gathered
+    through a CSR-order index)."""
     monkeypatch.setenv("LHPC_XTILE_IPERM", "1" if request.param == "iperm" else "0")
     return request.param
 
@@ -329,18 +367,8 @@ def test_xtile_small_gather_pieces(lhpc, gpu, monkeypatch, xt_layout):
         _check_xtile(lhpc, gpu, lengths, 100_000, np.float32, 0xA403)
 
 
-@pytest.mark.parametrize("ranges", ["2", "5"])
-def test_xtile_pipelined_ranges(lhpc, gpu, monkeypatch, ranges):
-    """LHPC_XTILE_RANGES=K: per-range gathers on the caller's stream, reduces on
-    a second stream; same bits as the single launch, long rows across ranges."""
-    monkeypatch.setenv("LHPC_XTILE_RANGES", ranges)
-    lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 30000 + [0, 0] + [30000]
-    _check_xtile(lhpc, gpu, lengths, 200_000, np.float32, 0xA600, expect_cont=True)
-    _check_xtile(lhpc, gpu, lengths, 200_000, np.float64, 0xA601, dyadic=False)
-
-
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_xtile_split_ranges(lhpc, gpu, dtype):
+def test_xtile_split_ranges(lhpc, gpu, dtype, xt_layout):
     """Row-range plan (lhpc_spmv_plan_create_split): stage once, reduce each
     range into its own buffer; long rows end at and start right after the
     split rows; the concatenation equals the whole-matrix oracle bit for bit

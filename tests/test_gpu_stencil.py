@@ -115,20 +115,22 @@ def test_stencil7_c5_size(lhpc, gpu):
 
 
 S7_IMPLS = ["buf", "buf:2,8,0,2", "buf:4,4,128,3", "buf:2,8,5,3", "buf:2,8,32", "buf:1,8,16", "buf:1,8,32", "buf:2,4,32", "buf:4,4,32", "buf:1,4,32", "buf:4,8,32",
-            "buf:2,8,4", "wide:2,8", "wide:1,8", "wide:2,4", "ring", "simple", "pf", "reg", "lds"]
+            "buf:2,8,4", "simple"]
 
 
 @pytest.mark.parametrize("impl", S7_IMPLS)
 @pytest.mark.parametrize("store", ["nt", "plain", "staged"])
 def test_stencil7_every_impl(lhpc, gpu, impl, store, monkeypatch):
     """Every stencil7 implementation / tiling / store mode selectable through
-    LHPC_STENCIL7_* is bit-exact against the oracle on ragged shapes: nx
+    LHPC_STENCIL7_* ("simple": the thread-per-column kernel the launcher
+    falls back to when a row's byte offset does not fit a buffer voffset) is
+    bit-exact against the oracle on ragged shapes: nx
     spanning several 512-wide x tiles with a partial last one, ny and nz not
     multiples of the row / z-chunk tiles, ghost widths 1 and 2."""
     name, _, cfg = impl.partition(":")
     monkeypatch.setenv("LHPC_STENCIL7_IMPL", name)
     if cfg:
-        monkeypatch.setenv("LHPC_STENCIL7_BUF" if name == "buf" else "LHPC_STENCIL7_WIDE", cfg)
+        monkeypatch.setenv("LHPC_STENCIL7_BUF", cfg)
     monkeypatch.setenv("LHPC_STENCIL7_STORE", store)
     for (nz, ny, nx, g) in ((37, 45, 1100, 1), (9, 19, 130, 2), (3, 2, 1, 1)):
         shape = (nz + 2 * g, ny + 2 * g, nx + 2 * g)
@@ -143,14 +145,13 @@ S7_BUF4 = ["2,8,0", "2,8,5", "1,8,16", "4,8,32", "2,4,7", "4,4,32"]
 
 
 @pytest.mark.parametrize("cfg", S7_BUF4)
-@pytest.mark.parametrize("store", ["nt", "plain", "none"])
+@pytest.mark.parametrize("store", ["nt", "plain"])
 def test_stencil7_buf4(lhpc, gpu, cfg, store, monkeypatch):
     """The x4 ring (LHPC_STENCIL7_IMPL=buf4, 4 consecutive x per lane,
     dwordx4 loads/stores at 4-B alignment) is bit-exact against the oracle on
     shapes whose nx is a multiple of its tile width — one and several x tiles,
     ny / nz ragged against the row and z-chunk tiles, ghost widths 1 to 3 (so
-    rows start at every 4-B phase of a 16-B line) — and leaves `out` untouched
-    with stores off.  Other nx fall back to the dword ring (covered above)."""
+    rows start at every 4-B phase of a 16-B line).  Other nx fall back to the dword ring (covered above)."""
     monkeypatch.setenv("LHPC_STENCIL7_IMPL", "buf4")
     monkeypatch.setenv("LHPC_STENCIL7_BUF", cfg)
     monkeypatch.setenv("LHPC_STENCIL7_STORE", store)
@@ -160,30 +161,22 @@ def test_stencil7_buf4(lhpc, gpu, cfg, store, monkeypatch):
         shape = (nz + 2 * g, ny + 2 * g, nx + 2 * g)
         u = S.random_padded(shape, seed=nz * 7 + nx + g, zero_ghost=False).reshape(-1)
         out0 = S.random_padded(shape, seed=1234 + g).reshape(-1)
-        want = out0.copy() if store == "none" else S.stencil7_oracle(u, nz, ny, nx, g, -6.0, 1.0, out=out0.copy())
+        want = S.stencil7_oracle(u, nz, ny, nx, g, -6.0, 1.0, out=out0.copy())
         got = lhpc.stencil7(_dev(gpu, u), _dev(gpu, out0), nz, ny, nx, g, -6.0, 1.0).cpu().numpy()
         assert np.array_equal(got, want), (cfg, store, nz, ny, nx, g)
 
 
-BX_IMPLS = [("wave", "1"), ("wave", "2"), ("wave", "4"), ("wave", "8"), ("wave", "16"), ("wave", "32"),
-            ("lds", "1"), ("lds", "2"), ("lds", "4"), ("lds", "8")]
-
-
-@pytest.mark.parametrize("impl,rows", BX_IMPLS)
-def test_blur_x_every_impl(lhpc, gpu, impl, rows, monkeypatch):
-    """Every blur_x implementation (LHPC_BLUR_X_IMPL / _RW / _ROWS) is bit-exact
-    against the oracle on vector-eligible ragged shapes: nx not a multiple of
-    the 256 / 1024-float segments, ny not a multiple of the row group."""
+@pytest.mark.parametrize("rows", ["1", "2", "4", "8", "16", "32"])
+def test_blur_x_every_impl(lhpc, gpu, rows, monkeypatch):
+    """The wave-private blur_x at every rows-per-wave setting (LHPC_BLUR_X_RW)
+    is bit-exact against the oracle on vector-eligible ragged shapes: nx not a
+    multiple of the 256-float segment, ny not a multiple of the row group.
+    (Unaligned shapes take the block-LDS kernel: test_blur_shapes_vs_oracle.)"""
     import torch
-    if impl == "wave":
-        monkeypatch.setenv("LHPC_BLUR_X_IMPL", "wave")
-        monkeypatch.setenv("LHPC_BLUR_X_RW", rows)
-    else:
-        monkeypatch.setenv("LHPC_BLUR_X_IMPL", "lds")
-        monkeypatch.setenv("LHPC_BLUR_X_ROWS", rows)
+    monkeypatch.setenv("LHPC_BLUR_X_RW", rows)
     for ny, nx, ghost in ((37, 260, 8), (5, 1300, 8), (70, 2048, 12), (1, 4, 8)):
         a = S.random_padded(((ny + 2 * ghost) * (nx + 2 * ghost),), seed=ny * 31 + nx)
         want = S.blur_oracle(a, ny, nx, ghost, 8, False)
         b = torch.empty(ny * nx, dtype=torch.float32, device=gpu)
         got = lhpc.blur_x(_dev(gpu, a), b, ny, nx, ghost, 8).cpu().numpy()
-        assert np.array_equal(got, want), (impl, rows, ny, nx, ghost)
+        assert np.array_equal(got, want), (rows, ny, nx, ghost)

@@ -1,5 +1,23 @@
 #!/bin/bash
+# Same-box A/B of bench lines: AB="name:K=V,K=V;name2:..." WLS="c2 c3", then
+# optional tests (TESTS="tests/x.py ..." TESTK=expr).  Output: gpurun_out/ab/.
 set -o pipefail
-R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests/test_gpu_spmv.py -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_spmv.log 2>&1 || exit 1
-timeout -k 10 600 python tools/explore.py --only spmv > gpurun_out/explore3.log 2>&1
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O="$R/gpurun_out/ab"; mkdir -p "$O"
+export TMPDIR=/tmp
+log() { echo "== $* $(date +%T)" >> "$O/progress.log"; }
+IFS=';' read -ra VS <<< "${AB:-base:X=0}"
+for rep in $(seq 1 ${REPS:-1}); do
+  for WL in ${WLS:-c2}; do
+    for V in "${VS[@]}"; do
+      name=${V%%:*}; kv=${V#*:}
+      log "bench $WL $name rep $rep"
+      env $(echo "$kv" | tr ',' ' ') timeout -k 10 300 python bench.py --workload $WL --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench_${WL}_${name}_$rep.log" 2>&1 || { log "FAIL bench $WL $name"; exit 1; }
+    done
+  done
+done
+if [ -n "${TESTS:-}" ]; then
+  log tests
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider ${TESTK:+-k "$TESTK"} > "$O/pytest.log" 2>&1 || { log "FAIL tests"; exit 1; }
+fi
+log done
+exit 0
