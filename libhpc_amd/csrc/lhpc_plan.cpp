@@ -289,4 +289,28 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
   return LHPC_OK;
 }
 
+int xtile_transpose_runs(const XtileHost &o, const void *val, size_t tsz, int run, int64_t tail,
+                         std::vector<int32_t> &vbase, std::unique_ptr<unsigned char[]> &valt,
+                         std::unique_ptr<uint16_t[]> &ipt) {
+  const int64_t C = o.n_chunks, reg = 64 * static_cast<int64_t>(run);
+  std::vector<int64_t> vb(static_cast<size_t>(C) + 1, 0);
+  for (int64_t c = 0; c < C; ++c) vb[c + 1] = vb[c] + (o.ce[c + 1] - o.ce[c] + reg - 1) / reg * reg;
+  if (vb[C] + tail >= INT32_MAX) return LHPC_ERR_UNSUPPORTED;
+  vbase.assign(vb.begin(), vb.end());
+  const size_t total = static_cast<size_t>(vb[C] + tail);
+  valt.reset(new unsigned char[total * tsz]());
+  if (o.iperm) ipt.reset(new uint16_t[total]());
+  const int vw = static_cast<int>(16 / tsz);
+  const unsigned char *vs = static_cast<const unsigned char *>(val);
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t c = 0; c < C; ++c) {
+    const int64_t e0 = o.ce[c], m = o.ce[c + 1] - e0;
+    for (int64_t i = 0; i < m; ++i) {
+      std::memcpy(valt.get() + (vb[c] + xtile_wave_pos(i, run, vw)) * tsz, vs + (e0 + i) * tsz, tsz);
+      if (o.iperm) ipt[static_cast<size_t>(vb[c] + xtile_wave_pos(i, run, 8))] = o.iperm[static_cast<size_t>(e0 + i)];
+    }
+  }
+  return LHPC_OK;
+}
+
 }  // namespace lhpc

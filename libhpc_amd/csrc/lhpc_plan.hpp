@@ -88,6 +88,27 @@ int build_xtile(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_
                 int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, int slot_bytes,
                 const int64_t *splits, int n_splits, bool iperm, XtileHost &out);
 
+// Wave-transposed run layout of the XTILE reduce's per-position streams (val,
+// iperm): chunk position i belongs to thread t = i / run (run = 64 B of
+// values: fp32 16, fp64 8), element j = i % run.  Thread t sits in wave
+// w = t / 64 at lane l = t % 64; the chunk's wave region w holds 64·run
+// positions, and inside it the vw-element vector q of lane l (vw = 16 B /
+// element size) is stored at (q·64 + l)·vw, so the wave's load instruction q
+// reads 64 consecutive 16-B vectors.
+inline int64_t xtile_wave_pos(int64_t i, int run, int vw) {
+  const int64_t t = i / run, j = i % run, w = t / 64, l = t % 64, q = j / vw, r = j % vw;
+  return w * 64 * run + (q * 64 + l) * vw + r;
+}
+
+// Per-chunk region bases (vbase[c]: chunk c's positions start there, each
+// chunk padded to whole wave regions of 64·run positions; vbase[C] = total)
+// and the val (tsz bytes each) and, when o.iperm is set, iperm streams in
+// the wave-transposed layout; padding entries are 0.  Extra `tail` entries
+// of zero padding follow vbase[C].  LHPC_ERR_UNSUPPORTED if vbase[C] ≥ 2^31.
+int xtile_transpose_runs(const XtileHost &o, const void *val, size_t tsz, int run, int64_t tail,
+                         std::vector<int32_t> &vbase, std::unique_ptr<unsigned char[]> &valt,
+                         std::unique_ptr<uint16_t[]> &ipt);
+
 // LDS slot of chunk position i in the XTILE reduce (lhpc_spmv_xtile.hip
 // xt_slot): run t = i/run holds run = 64/elem_bytes elements (64 B) at
 // run·t, its 16-B slot q at q ^ swz(t), swz = (t/4) % 4.

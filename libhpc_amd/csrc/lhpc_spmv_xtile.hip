@@ -162,7 +162,6 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   static_assert((NB == 16 || NB == 8) && M <= 256 * kWave && M >= 4096,
                 "8/16 batches per wave; ≤ 256 batches per chunk; sbm ≥ 128 words");
   typedef T tvec __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
-  typedef uint32_t ivec __attribute__((ext_vector_type(4), aligned(2)));
   constexpr int VW = 16 / sizeof(T), NV = RUN / VW;
   // dynamic LDS (xtile_lds_bytes): xs[M + VW] T (slot M is the sentinel's
   // spare), bt[BLK/64][NB] u32x4, ws[BLK/64] f64, wsf[BLK/64] i32, bm[M/32]
@@ -197,24 +196,32 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     sa[q] = segoff[c * S + sc];
     sb[q] = segoff[(c + 1) * S + sc];
   }
-  const u32x4 d = *reinterpret_cast<const u32x4 *>(cdesc + 4 * c);
+  const u32x4 d = *reinterpret_cast<const u32x4 *>(cdesc + 8 * c);
+  const u32x4 d2 = *reinterpret_cast<const u32x4 *>(cdesc + 8 * c + 4);
   const int e0 = static_cast<int>(d[0]), m = static_cast<int>(d[1]) - e0;
   const int r0 = static_cast<int>(d[2]), R = static_cast<int>(d[3]) - r0;
+  // val and iperm are stored wave-transposed (lhpc_plan.hpp xtile_wave_pos):
+  // in the chunk's wave region w (REG = 64·RUN positions at vbase + w·REG),
+  // 16-B vector q of lane l holds that lane's run elements [q·VW, q·VW + VW),
+  // so each load instruction reads 1 KB contiguous (per-lane runs touched
+  // every 128-B line with 2 lanes per instruction: 4× the L2 requests for
+  // val).  A wave whose region starts past m reads region 0 (masked below).
+  constexpr int REG = kWave * RUN;
+  const int64_t vreg = static_cast<int64_t>(static_cast<int>(d2[0])) + (wv * REG < m ? wv : 0) * REG;
   tvec vv[NV];
   {
-    // the val allocation is padded by one run, so a run may read past nnz
-    const tvec *vp = reinterpret_cast<const tvec *>(val + e0 + (i0 < m ? i0 : 0));
+    const tvec *vp = reinterpret_cast<const tvec *>(val + vreg) + lane;
 #pragma unroll
-    for (int q = 0; q < NV; ++q) vv[q] = __builtin_nontemporal_load(vp + q);
+    for (int q = 0; q < NV; ++q) vv[q] = __builtin_nontemporal_load(vp + q * kWave);
   }
   constexpr int NIP = IP ? RUN * 2 / 16 : 1;  // 16-B iperm vectors per run
-  ivec ipv[NIP];
-  // iperm ([nnz + RUN] u16, CSR order, padded like val): loaded once phase
-  // A's xg loads are issued, so it is not live during the rank math
+  u32x4 ipv[NIP];
+  // iperm: loaded once phase A's xg loads are issued, so it is not live
+  // during the rank math; padding entries are 0 (a valid LDS slot)
   auto load_ipv = [&]() {
-    const ivec *ip = reinterpret_cast<const ivec *>(perm + e0 + (i0 < m ? i0 : 0));
+    const u32x4 *ip = reinterpret_cast<const u32x4 *>(perm + vreg) + lane;
 #pragma unroll
-    for (int q = 0; q < NIP; ++q) ipv[q] = __builtin_nontemporal_load(ip + q);
+    for (int q = 0; q < NIP; ++q) ipv[q] = __builtin_nontemporal_load(ip + q * kWave);
   };
   int rv[RPT];
 #pragma unroll
@@ -557,7 +564,7 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   }
   LHPC_HIP_TRY(hipFuncSetAttribute(xtile_reduce_fn<T>(xtile_g<T>(xt.S), ip),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
-  const int64_t n_rows = p->n_rows, nnz = p->nnz, C = xt.n_chunks;
+  const int64_t n_rows = p->n_rows, C = xt.n_chunks;
   auto up = [&](void **d, const void *h, size_t n) -> int {
     LHPC_TRY(dmalloc(d, n, p->bytes));
     if (n && h) LHPC_HIP_TRY(hipMemcpy(*d, h, n, hipMemcpyHostToDevice));
@@ -566,17 +573,23 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   std::vector<int32_t> rp32(static_cast<size_t>(n_rows + 1));
   for (int64_t i = 0; i <= n_rows; ++i) rp32[static_cast<size_t>(i)] = static_cast<int32_t>(rp[i]);
   LHPC_TRY(up(&p->d_row_ptr, rp32.data(), rp32.size() * 4));
-  // val padded by one run: a reduce thread loads its whole run as vectors
-  LHPC_TRY(dmalloc(&p->d_val, static_cast<size_t>(nnz + RUN) * tsz, p->bytes));
-  LHPC_HIP_TRY(hipMemset(static_cast<unsigned char *>(p->d_val) + nnz * tsz, 0, RUN * tsz));
-  if (nnz) LHPC_HIP_TRY(hipMemcpy(p->d_val, val, static_cast<size_t>(nnz) * tsz, hipMemcpyHostToDevice));
+  // val (and iperm) in the wave-transposed run layout, each chunk padded to
+  // whole wave regions, plus one region of zeros (an empty chunk reads it)
+  std::vector<int32_t> vbase;
+  std::unique_ptr<unsigned char[]> valt;
+  std::unique_ptr<uint16_t[]> ipt;
+  LHPC_TRY(xtile_transpose_runs(xt, val, tsz, RUN, 64 * RUN, vbase, valt, ipt));
+  const size_t nrun = static_cast<size_t>(vbase[C]) + 64 * RUN;
+  LHPC_TRY(up(&p->d_val, valt.get(), nrun * tsz));
+  valt.reset();
   {
-    std::vector<int32_t> cd(static_cast<size_t>(4 * C + 4));
+    std::vector<int32_t> cd(static_cast<size_t>(8 * C + 8), 0);  // {e0, e1, r0, r1, vbase, 0, 0, 0}
     for (int64_t c = 0; c < C; ++c) {
-      cd[4 * c] = xt.ce[c];
-      cd[4 * c + 1] = xt.ce[c + 1];
-      cd[4 * c + 2] = xt.cr[c];
-      cd[4 * c + 3] = xt.cr[c + 1];
+      cd[8 * c] = xt.ce[c];
+      cd[8 * c + 1] = xt.ce[c + 1];
+      cd[8 * c + 2] = xt.cr[c];
+      cd[8 * c + 3] = xt.cr[c + 1];
+      cd[8 * c + 4] = vbase[c];
     }
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cdesc), cd.data(), cd.size() * 4));
   }
@@ -586,10 +599,7 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_col16), xt.col16.get(), static_cast<size_t>(xt.total) * 2));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_segoff), xt.segoff.data(), xt.segoff.size() * 4));
   if (ip) {
-    // iperm in CSR order, padded by one run like val
-    LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_perm), static_cast<size_t>(nnz + RUN) * 2, p->bytes));
-    LHPC_HIP_TRY(hipMemset(p->d_perm + nnz, 0, RUN * 2));
-    if (nnz) LHPC_HIP_TRY(hipMemcpy(p->d_perm, xt.iperm.get(), static_cast<size_t>(nnz) * 2, hipMemcpyHostToDevice));
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), ipt.get(), nrun * 2));
   } else {
     // one sentinel entry past the stream: the reduce loads it for positions
     // past m, and its perm is the spare LDS slot M
