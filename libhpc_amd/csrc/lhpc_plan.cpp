@@ -313,4 +313,19 @@ int xtile_transpose_runs(const XtileHost &o, const void *val, size_t tsz, int ru
   return LHPC_OK;
 }
 
+void xtile_permute_gather_blocks(XtileHost &o, int vw) {
+  const int64_t np = static_cast<int64_t>(o.pieces.size() / 3);
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int64_t b = 0; b < np; ++b) {
+    const int64_t g0 = o.pieces[3 * b], g1 = o.pieces[3 * b + 1];
+    uint16_t tmp[512];
+    for (int64_t g = g0; g + 512 <= g1; g += 512) {
+      uint16_t *c = o.col16.get() + g;
+      for (int l = 0; l < 64; ++l)
+        for (int k = 0; k < 8; ++k) tmp[8 * l + k] = c[xtile_gather_pos(k, l, vw)];
+      std::memcpy(c, tmp, sizeof(tmp));
+    }
+  }
+}
+
 }  // namespace lhpc

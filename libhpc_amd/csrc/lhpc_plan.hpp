@@ -109,6 +109,15 @@ int xtile_transpose_runs(const XtileHost &o, const void *val, size_t tsz, int ru
                          std::vector<int32_t> &vbase, std::unique_ptr<unsigned char[]> &valt,
                          std::unique_ptr<uint16_t[]> &ipt);
 
+// Wave-coalesced gather stores: inside each piece, every full block of 512
+// stream entries (64 lanes × 8 entries, from the piece start) has its col16
+// permuted so that lane l's 8 entries are stream positions
+// (k / vw)·64·vw + vw·l + k % vw, k = 0..7 (vw = 16 B / value size): the
+// gather's 16-B store h of every lane then covers one contiguous KB.  A
+// partial last block keeps lane l's entries at 8·l .. 8·l + 7.
+inline int xtile_gather_pos(int k, int l, int vw) { return (k / vw) * 64 * vw + vw * l + k % vw; }
+void xtile_permute_gather_blocks(XtileHost &o, int vw);
+
 // LDS slot of chunk position i in the XTILE reduce (lhpc_spmv_xtile.hip
 // xt_slot): run t = i/run holds run = 64/elem_bytes elements (64 B) at
 // run·t, its 16-B slot q at q ^ swz(t), swz = (t/4) % 4.

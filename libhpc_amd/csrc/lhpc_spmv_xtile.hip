@@ -43,7 +43,7 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
     const T *__restrict__ x, int64_t n_cols, T *__restrict__ xg) {
   constexpr int W = XtTile<T>::W;
   __shared__ T xt[W];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int g0 = pieces[3 * blockIdx.x], g1 = pieces[3 * blockIdx.x + 1];
   const int64_t c0 = static_cast<int64_t>(pieces[3 * blockIdx.x + 2]) * W;
   const int wlen = static_cast<int>((n_cols - c0) < W ? (n_cols - c0) : W);
@@ -79,16 +79,30 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
         o[2 * h] = xt[w[u][h] & 0xFFFFu];
         o[2 * h + 1] = xt[w[u][h] >> 16];
       }
-      if (qq < q1) {
-        if constexpr (sizeof(T) == 4) {
-          f32x4 *d = reinterpret_cast<f32x4 *>(xg + static_cast<int64_t>(qq) * 8);
-          d[0] = f32x4{o[0], o[1], o[2], o[3]};
-          d[1] = f32x4{o[4], o[5], o[6], o[7]};
-        } else {
-          typedef double f64x2 __attribute__((ext_vector_type(2)));
-          f64x2 *d = reinterpret_cast<f64x2 *>(xg + static_cast<int64_t>(qq) * 8);
+      // a full 64-group block of the piece is stored wave-coalesced: the
+      // plan permuted its col16 (xtile_gather_pos) so that the lane's 16-B
+      // vector h lands at block + h·64·VW + VW·lane and every store
+      // instruction writes 1 KB contiguous; a partial last block keeps the
+      // lane's 8 entries contiguous
+      typedef T tv16 __attribute__((ext_vector_type(16 / sizeof(T))));
+      constexpr int VW = 16 / sizeof(T);
+      const int qb = qq - lane;  // the wave's block (wave-uniform)
+      T *blk = xg + static_cast<int64_t>(qb) * 8;
+      if (qb + kWave <= q1) {
 #pragma unroll
-          for (int h = 0; h < 4; ++h) d[h] = f64x2{o[2 * h], o[2 * h + 1]};
+        for (int h = 0; h < 8 / VW; ++h) {
+          tv16 v;
+#pragma unroll
+          for (int k = 0; k < VW; ++k) v[k] = o[h * VW + k];
+          *reinterpret_cast<tv16 *>(blk + h * kWave * VW + VW * lane) = v;
+        }
+      } else if (qq < q1) {
+#pragma unroll
+        for (int h = 0; h < 8 / VW; ++h) {
+          tv16 v;
+#pragma unroll
+          for (int k = 0; k < VW; ++k) v[k] = o[h * VW + k];
+          *reinterpret_cast<tv16 *>(blk + 8 * lane + h * VW) = v;
         }
       }
     }
@@ -596,6 +610,7 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cr), xt.cr.data(), xt.cr.size() * 4));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_pieces), xt.pieces.data(), xt.pieces.size() * 4));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cont), xt.cont.data(), xt.cont.size() * 4));
+  xtile_permute_gather_blocks(xt, static_cast<int>(16 / tsz));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_col16), xt.col16.get(), static_cast<size_t>(xt.total) * 2));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_segoff), xt.segoff.data(), xt.segoff.size() * 4));
   if (ip) {
