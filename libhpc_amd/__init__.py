@@ -34,7 +34,8 @@ __all__ = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "liblhpc.so")
+# LHPC_LIB_PATH: an alternative build of the same ABI (same-box A/B runs, tools/gpu_ab.sh)
+LIB_PATH = os.environ.get("LHPC_LIB_PATH") or os.path.join(_HERE, "_lib", "liblhpc.so")
 
 F32, F64 = 0, 1
 PLAN_VALIDATE = 1 << 0
