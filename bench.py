@@ -108,7 +108,11 @@ def main():
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # LHPC_DIST_NATIVE=1 under torch.distributed.run with one process: the
+    # native N > 1 path at world 1 (the rehearsal a 1-GPU box allows; RCCL
+    # cannot place two ranks on one GPU)
+    force_native = os.environ.get("LHPC_DIST_NATIVE", "0") == "1" and "RANK" in os.environ
+    if world > 1 or force_native:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = os.environ.get("LHPC_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
@@ -119,6 +123,11 @@ def main():
         torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
+    # N > 1 over RCCL: the native lhpc_dist_* path (one RCCL communicator and
+    # comm stream per process, created from rank 0's unique id); the
+    # torch.distributed form serves the gloo rehearsal or LHPC_DIST_TORCH=1
+    native_dist = (world > 1 or force_native) and dist.get_backend() == "nccl" and \
+        os.environ.get("LHPC_DIST_TORCH", "0") != "1"
     wl = args.workload
     result = {}
     if wl in ("c1", "c2", "c3", "c4"):
@@ -136,17 +145,39 @@ def main():
         from libhpc_amd.dist import DistSpMVOverlap, InterleavedBlocks
         xd = torch.from_numpy(x).to(dev)
         t0 = time.time()
-        if world == 1:
+        if world == 1 and not native_dist:
             plans = [L.SpMVPlan(rp, col, val, n)]
             local_nnz, local_rows = nnz, n
             y_local = torch.empty(n, dtype=xd.dtype, device=dev)
 
             def step():
                 plans[0](xd, y_local, stream=stream)
+        elif native_dist:
+            # native RCCL path behind the C ABI (lhpc_dist_spmv): nnz-balanced
+            # interleaved blocks, K chunks per rank; chunk k is reduced into
+            # the rank's rows of y and broadcast (in place, exact slices) to
+            # every rank on the comm stream while chunk k+1 is reduced
+            comm = L.DistComm.from_torch(local)
+            cuts = L.interleaved_cuts(rp, world, args.chunks)
+            lrp, lc, lv = L.interleaved_local_csr(rp, col, val, cuts, world, args.chunks, rank)
+            dplan = L.DistSpMVPlan(comm, n, n, args.chunks, cuts, lrp, lc, lv)
+            # the same local rows as one plan: the live kernel-only call timing below
+            plans = [L.SpMVPlan(lrp, lc, lv, n)]
+            local_nnz, local_rows = int(lc.shape[0]), int(lrp.shape[0] - 1)
+            y_full = torch.empty(n, dtype=xd.dtype, device=dev)
+
+            class _Native:
+                def step(self, xv):
+                    return dplan(xv, y_full, stream=stream)
+            dsp = _Native()
+
+            def step():
+                dplan(xd, y_full, stream=stream)
         else:
-            # interleaved row blocks, K chunks per rank: chunk k's RCCL
-            # all-gather overlaps the SpMV of chunk k+1 (libhpc_amd/dist.py)
-            ib = InterleavedBlocks(n, world, args.chunks)
+            # torch.distributed form (gloo rehearsal, LHPC_DIST_TORCH=1):
+            # interleaved nnz-balanced row blocks, K chunks per rank; chunk
+            # k's all-gather overlaps the SpMV of chunk k+1 (libhpc_amd/dist.py)
+            ib = InterleavedBlocks(n, world, args.chunks, row_ptr=rp)
             plans, local_nnz, fns = [], 0, None
             if args.chunks > 1:
                 # one row-range plan over the rank's K chunks: x is staged once
@@ -240,7 +271,11 @@ def main():
                                  "c3": "BASELINE configs[2] matrix: CSR SpMV n=10M nnz=150M fp64 uniform 15/row",
                                  "c4": "BASELINE configs[3]: power-law CSR (1..1e4 nnz/row) fp32"}[wl],
                     "n_rows": n, "n_cols": n, "nnz": nnz, "kernel": kname, "slices": info["slices"],
-                    "parallelism": f"row-block x{world}" + (f" (interleaved, {args.chunks} chunks/rank) + RCCL all_gather(y) overlapped" if world > 1 else "")},
+                    "parallelism": f"row-block x{world}" + (
+                        f" (interleaved nnz-balanced, {args.chunks} chunks/rank) + native RCCL broadcast of y "
+                        "chunks (lhpc_dist_spmv) overlapped" if native_dist else
+                        f" (interleaved nnz-balanced, {args.chunks} chunks/rank) + torch.distributed all_gather(y) "
+                        "overlapped" if world > 1 else "")},
             achieved_GBps=alg_bytes / per_step / 1e9,
             roofline={"bound": "hbm", "kernel": kernels, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                       "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
@@ -252,7 +287,7 @@ def main():
         # correctness of the timed output, outside the timed region: y of the
         # last step on 10^5 sampled rows against an fp64 numpy evaluation,
         # |dy| <= 1e-6·Σ|a·x| per row (the parity bar of tests/_support.py)
-        y_out = y_local if world == 1 else dsp.step(xd)  # every rank: the step holds collectives
+        y_out = dsp.step(xd) if (world > 1 or native_dist) else y_local  # every rank: the step holds collectives
         if rank == 0:
             result["check"] = sampled_y_check(rp, col, val, x, y_out.cpu().numpy(), 100_000)
         if kname == "xslice" and rank == 0:
@@ -270,6 +305,9 @@ def main():
                                                        threads=1 if wl == "c1" else None)
         for pl in plans:
             pl.close()
+        if native_dist:  # the plan before its communicator
+            dplan.close()
+            comm.close()
     elif wl == "sort":
         result.update(sort_bench(args, L, torch, dev, stream, barrier, world, rank))
     elif wl == "cg":
@@ -281,7 +319,7 @@ def main():
         result.pop("_cpu", None)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if world > 1 or force_native:
         dist.barrier()
         dist.destroy_process_group()
 
@@ -395,7 +433,8 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
         P = n + 2
         cells = n ** 3
         name = "k_stencil7_buf4"
-        if world == 1:
+        force_native = os.environ.get("LHPC_DIST_NATIVE", "0") == "1" and "RANK" in os.environ
+        if world == 1 and not force_native:
             u = torch.zeros(P ** 3, device=dev)
             u.view(P, P, P)[1:-1, 1:-1, 1:-1] = torch.rand(n, n, n, device=dev) * 2 - 1
             o = torch.zeros_like(u)
@@ -408,10 +447,19 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
             u = torch.zeros((nzl + 2) * P * P, device=dev)
             u.view(nzl + 2, P, P)[1:-1, 1:-1, 1:-1] = torch.rand(nzl, n, n, device=dev) * 2 - 1
             o = torch.zeros_like(u)
-            ds = DistStencil7(nzl, n, n, rank, world, lambda ut, ot, zb, ze: L.stencil7_planes(
-                ut, ot, nzl, n, n, 1, -6.0, 1.0, zb, ze, stream=stream))
-            fn = lambda: ds.step(u, o)  # noqa: E731
-            workload = f"BASELINE configs[4]: 7-point 3-D stencil 512^3 fp32, z-slabs x{world} + RCCL halo"
+            import torch.distributed as dist
+            if dist.get_backend() == "nccl" and os.environ.get("LHPC_DIST_TORCH", "0") != "1":
+                # native: lhpc_dist_stencil7_f32 (RCCL send/recv of the halo planes on
+                # the comm stream while the interior planes run)
+                comm = L.DistComm.from_torch(torch.cuda.current_device())
+                fn = lambda: comm.stencil7(u, o, nzl, n, n, 1, -6.0, 1.0, stream=stream)  # noqa: E731
+                how = "native RCCL halo (lhpc_dist_stencil7_f32)"
+            else:
+                ds = DistStencil7(nzl, n, n, rank, world, lambda ut, ot, zb, ze: L.stencil7_planes(
+                    ut, ot, nzl, n, n, 1, -6.0, 1.0, zb, ze, stream=stream))
+                fn = lambda: ds.step(u, o)  # noqa: E731
+                how = "torch.distributed halo"
+            workload = f"BASELINE configs[4]: 7-point 3-D stencil 512^3 fp32, z-slabs x{world} + {how}"
     else:
         n, g = 8192, 8
         a = torch.rand((n + 2 * g) ** 2, device=dev) * 2 - 1

@@ -5,7 +5,8 @@
  *
  *     0              success (LHPC_OK)
  *     < 0            lhpc error (see lhpc_status below)
- *     > 0            a wrapped hipError_t value
+ *     > 0            a wrapped hipError_t value, or LHPC_RCCL_STATUS_BASE +
+ *                    ncclResult_t for a failed RCCL call (lhpc_dist_*)
  *
  * No exception crosses this boundary.  The C++ drop-in headers
  * (include/hpc/ and include/sparse/ headers) map a non-zero status to
@@ -53,6 +54,8 @@ enum lhpc_status {
   LHPC_ERR_UNSUPPORTED = -5,   /* valid request the build does not support  */
   LHPC_ERR_INTERNAL = -6
 };
+/* RCCL failures: LHPC_RCCL_STATUS_BASE + ncclResult_t (above any hipError_t) */
+#define LHPC_RCCL_STATUS_BASE 10000
 
 /* ----------------------------------------------------------------- dtype */
 enum lhpc_dtype { LHPC_F32 = 0, LHPC_F64 = 1 };
@@ -323,6 +326,58 @@ int lhpc_mm_read_header(const char *path, int64_t *n_rows, int64_t *n_cols,
                         int64_t *nnz_max, int *symmetry, int *field);
 int lhpc_mm_read_coo(const char *path, int32_t *rows, int32_t *cols,
                      double *vals, int64_t *count);
+
+/* --------------------------------------------------- multi-GPU (RCCL)
+ * One process per GPU: each process creates one
+ * communicator over RCCL (xGMI inside a node) on its device, with one
+ * communication stream of its own.  Rank 0 makes the 128-byte unique id
+ * (lhpc_dist_get_unique_id) and the launcher hands it to every rank (MPI,
+ * torch.distributed, a file …); each rank then calls lhpc_dist_comm_create
+ * with the same id.  No reference interface: the reference has no
+ * multi-device code; the overlap follows its chunked
+ * copy/compute pipeline (lib/gpu/transfer_overlap_testsuite/src/
+ * cuda_tut_transfer_overlap.cu:41-142).
+ */
+#define LHPC_DIST_UNIQUE_ID_BYTES 128
+typedef struct lhpc_dist_comm lhpc_dist_comm;
+int lhpc_dist_get_unique_id(unsigned char *id_out /* LHPC_DIST_UNIQUE_ID_BYTES */);
+int lhpc_dist_comm_create(lhpc_dist_comm **out, const unsigned char *id, int nranks, int rank,
+                          int device);
+int lhpc_dist_comm_info(const lhpc_dist_comm *comm, int *nranks, int *rank, int *device);
+int lhpc_dist_comm_destroy(lhpc_dist_comm *comm);
+/* in-place sum over ranks of `count` doubles (the CG dots), async on stream */
+int lhpc_dist_allreduce_sum_f64(lhpc_dist_comm *comm, double *buf, int64_t count, void *stream);
+/*
+ * Distributed y = A·x.  The n_rows rows are cut into nranks·K blocks by
+ * `cuts` (nranks·K + 1 ascending global rows, cuts[0] = 0; nnz-balanced:
+ * lhpc_csr_partition_rows(row_ptr, bits, n_rows, nranks·K, cuts)); block
+ * b = k·nranks + r belongs to rank r as its chunk k.  Each rank passes its
+ * LOCAL CSR: its K blocks stacked in chunk order (row_ptr rebased to 0,
+ * global column indices, host arrays, copied to HBM).  lhpc_dist_spmv reads
+ * the full x (n_cols, device) and leaves the full y (n_rows, device, not x)
+ * on every rank: chunk k is reduced into this rank's rows of y, then a group
+ * of in-place ncclBroadcast (one per root) on the comm stream delivers every
+ * rank's block of chunk k while the compute stream reduces chunk k+1.
+ * Asynchronous on `stream`.  Matrices that do not select the XTILE layout
+ * use one plan per block.
+ */
+typedef struct lhpc_dist_spmv_plan lhpc_dist_spmv_plan;
+int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_comm *comm, int dtype, int64_t n_rows,
+                          int64_t n_cols, int K, const int64_t *cuts, const void *row_ptr,
+                          int row_ptr_bits, const int32_t *col_idx, const void *val, unsigned flags);
+int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream);
+int lhpc_dist_spmv_plan_destroy(lhpc_dist_spmv_plan *d);
+/*
+ * One 7-point stencil step on this rank's z-slab (BASELINE config C5): u and
+ * out are HPCHighDimensionFlatArray<3,float,ghost> buffers of logical
+ * (nzl, ny, nx) on the device; the z ghost planes -1 and nzl of u are the
+ * halo, refreshed from the neighbouring ranks (ncclSend/ncclRecv of the
+ * boundary planes on the comm stream) while the interior planes run; the
+ * first and last rank keep their outer ghost planes (Dirichlet).  Bit-exact
+ * with the single-domain lhpc_stencil7_f32.  Asynchronous on `stream`.
+ */
+int lhpc_dist_stencil7_f32(lhpc_dist_comm *comm, float *u, float *out, int64_t nzl, int64_t ny,
+                           int64_t nx, int64_t ghost, float c0, float c1, void *stream);
 
 #ifdef __cplusplus
 } /* extern "C" */

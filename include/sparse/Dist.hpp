@@ -1,0 +1,131 @@
+// sparse/Dist.hpp — multi-GPU SpMV and stencil in the reference's idiom, one
+// process per GPU, RCCL over xGMI behind the C ABI (include/lhpc.h lhpc_dist_*).
+//
+//   sparse::DistComm              RAII RCCL communicator + comm stream of this rank
+//   sparse::interleaved_cuts(A, nranks, K)        nnz-balanced cuts (nranks·K blocks)
+//   sparse::interleaved_local(A, cuts, nranks, K, rank)   the rank's stacked blocks
+//   sparse::DistSpMVPlan<T>       RAII distributed plan (the rank's local CSR)
+//   sparse::spmv(plan, d_x, d_y, stream)          full y on every rank (device)
+//   sparse::dist_stencil7(comm, d_u, d_out, ...)  z-slab step with RCCL halo planes
+// Non-zero status → std::system_error (include/lhpc_error.hpp).  The
+// reference has no multi-device code; the rank-0 unique id must
+// reach every rank through the launcher's own channel (MPI_Bcast, a file, …).
+#pragma once
+#ifndef LHPC_SPARSE_DIST_HPP_
+#define LHPC_SPARSE_DIST_HPP_
+
+#include <array>
+#include <cstdint>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "../lhpc.h"
+#include "../lhpc_error.hpp"
+#include "CSRMatrix.hpp"
+
+namespace sparse {
+
+class DistComm {
+ public:
+  using unique_id_t = std::array<unsigned char, LHPC_DIST_UNIQUE_ID_BYTES>;
+  static unique_id_t unique_id() {
+    unique_id_t id{};
+    lhpc::checkLhpc(lhpc_dist_get_unique_id(id.data()));
+    return id;
+  }
+  DistComm(const unique_id_t &id, int nranks, int rank, int device) : nranks_(nranks), rank_(rank) {
+    lhpc::checkLhpc(lhpc_dist_comm_create(&comm_, id.data(), nranks, rank, device));
+  }
+  DistComm(const DistComm &) = delete;
+  DistComm &operator=(const DistComm &) = delete;
+  ~DistComm() {
+    if (comm_) lhpc_dist_comm_destroy(comm_);
+  }
+  int nranks() const noexcept { return nranks_; }
+  int rank() const noexcept { return rank_; }
+  lhpc_dist_comm *native() noexcept { return comm_; }
+  // in-place sum over ranks (device doubles), asynchronous on `stream`
+  void allreduce_sum(double *d_buf, std::int64_t count, void *stream = nullptr) {
+    lhpc::checkLhpc(lhpc_dist_allreduce_sum_f64(comm_, d_buf, count, stream));
+  }
+
+ private:
+  lhpc_dist_comm *comm_ = nullptr;
+  int nranks_ = 1, rank_ = 0;
+};
+
+// nnz-balanced cuts of A's rows into nranks·K blocks; block k·nranks + r is
+// rank r's chunk k (lhpc_csr_partition_rows with nranks·K parts).
+template <typename T, typename IndexT, typename OffsetT>
+std::vector<std::int64_t> interleaved_cuts(const CSRMatrix<T, IndexT, OffsetT> &A, int nranks, int K) {
+  std::vector<std::int64_t> cuts(static_cast<std::size_t>(nranks) * K + 1);
+  lhpc::checkLhpc(lhpc_csr_partition_rows(A.row_ptr.data(), sizeof(OffsetT) * 8, A.n_rows, nranks * K, cuts.data()));
+  return cuts;
+}
+
+// The rank's K blocks stacked in chunk order: row_ptr rebased, global columns.
+template <typename T, typename IndexT, typename OffsetT>
+CSRMatrix<T, IndexT, std::int64_t> interleaved_local(const CSRMatrix<T, IndexT, OffsetT> &A,
+                                                     const std::vector<std::int64_t> &cuts, int nranks, int K,
+                                                     int rank) {
+  std::int64_t rows = 0;
+  for (int k = 0; k < K; ++k) rows += cuts[std::size_t(k) * nranks + rank + 1] - cuts[std::size_t(k) * nranks + rank];
+  CSRMatrix<T, IndexT, std::int64_t> L(rows, A.n_cols);
+  std::int64_t at = 0;
+  for (int k = 0; k < K; ++k) {
+    const std::int64_t r0 = cuts[std::size_t(k) * nranks + rank], r1 = cuts[std::size_t(k) * nranks + rank + 1];
+    for (std::int64_t i = r0; i < r1; ++i) {
+      const auto s = A.row_ptr[std::size_t(i)], e = A.row_ptr[std::size_t(i + 1)];
+      L.col_idx.insert(L.col_idx.end(), A.col_idx.begin() + s, A.col_idx.begin() + e);
+      L.val.insert(L.val.end(), A.val.begin() + s, A.val.begin() + e);
+      L.row_ptr[std::size_t(++at)] = static_cast<std::int64_t>(L.col_idx.size());
+    }
+  }
+  return L;
+}
+
+template <typename T>
+class DistSpMVPlan {
+  static_assert(std::is_same_v<T, float> || std::is_same_v<T, double>, "SpMV is fp32 or fp64");
+
+ public:
+  // `local`: this rank's K blocks of the n_rows × n_cols matrix, stacked
+  // (interleaved_local); `cuts`: the nranks·K + 1 global row cuts.
+  template <typename OffsetT>
+  DistSpMVPlan(DistComm &comm, std::int64_t n_rows, std::int64_t n_cols, int K, const std::vector<std::int64_t> &cuts,
+               const CSRMatrix<T, std::int32_t, OffsetT> &local, unsigned flags = LHPC_PLAN_DEFAULT)
+      : n_rows_(n_rows), n_cols_(n_cols) {
+    lhpc::checkLhpc(lhpc_dist_spmv_plan_create(&plan_, comm.native(), std::is_same_v<T, float> ? LHPC_F32 : LHPC_F64,
+                                               n_rows, n_cols, K, cuts.data(), local.row_ptr.data(),
+                                               sizeof(OffsetT) * 8, local.col_idx.data(), local.val.data(), flags));
+  }
+  DistSpMVPlan(const DistSpMVPlan &) = delete;
+  DistSpMVPlan &operator=(const DistSpMVPlan &) = delete;
+  ~DistSpMVPlan() {
+    if (plan_) lhpc_dist_spmv_plan_destroy(plan_);
+  }
+  std::int64_t rows() const noexcept { return n_rows_; }
+  std::int64_t cols() const noexcept { return n_cols_; }
+  lhpc_dist_spmv_plan *native() noexcept { return plan_; }
+
+ private:
+  lhpc_dist_spmv_plan *plan_ = nullptr;
+  std::int64_t n_rows_ = 0, n_cols_ = 0;
+};
+
+// y (all n_rows, device) = A·x (all n_cols, device) on every rank; y != x.
+template <typename T>
+void spmv(DistSpMVPlan<T> &plan, const T *d_x, T *d_y, void *stream = nullptr) {
+  lhpc::checkLhpc(lhpc_dist_spmv(plan.native(), d_x, d_y, stream));
+}
+
+// One 7-point step on this rank's z-slab (HPCHighDimensionFlatArray<3,float,ghost>
+// layout of logical (nzl, ny, nx), device buffers), halo planes over RCCL.
+inline void dist_stencil7(DistComm &comm, float *d_u, float *d_out, std::int64_t nzl, std::int64_t ny,
+                          std::int64_t nx, std::int64_t ghost, float c0, float c1, void *stream = nullptr) {
+  lhpc::checkLhpc(lhpc_dist_stencil7_f32(comm.native(), d_u, d_out, nzl, ny, nx, ghost, c0, c1, stream));
+}
+
+}  // namespace sparse
+#endif  // LHPC_SPARSE_DIST_HPP_

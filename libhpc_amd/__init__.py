@@ -60,6 +60,9 @@ ABI_SYMBOLS = (
     "lhpc_csr_load", "lhpc_mm_read_header", "lhpc_mm_read_coo", "lhpc_cg_solve", "lhpc_vec_dot",
     "lhpc_cg_step_xr", "lhpc_cg_step_p", "lhpc_spmv_dot",
     "lhpc_spmv_plan_create_split", "lhpc_spmv_stage", "lhpc_spmv_range",
+    "lhpc_dist_get_unique_id", "lhpc_dist_comm_create", "lhpc_dist_comm_info", "lhpc_dist_comm_destroy",
+    "lhpc_dist_allreduce_sum_f64", "lhpc_dist_spmv_plan_create", "lhpc_dist_spmv",
+    "lhpc_dist_spmv_plan_destroy", "lhpc_dist_stencil7_f32",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -68,19 +71,15 @@ if not os.path.exists(LIB_PATH):
         "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
 
 def _bind_single_hip_runtime():
-    """One HIP runtime per process.  PyTorch-ROCm bundles its own
-    libamdhip64 (SONAME libamdhip64.so.7, like /opt/rocm's); if ours were
-    loaded first, torch would later load its copy as a second runtime and see
-    no GPU.  Loading torch's copy first makes liblhpc.so bind to it."""
-    import importlib.util
+    """One HIP runtime and one RCCL per process.  PyTorch-ROCm bundles its own
+    libamdhip64 and librccl (SONAMEs libamdhip64.so.7 / librccl.so.1, like
+    /opt/rocm's); if ours were loaded first, torch would later load its
+    copies as a second runtime (and see no GPU).  Importing torch first makes
+    liblhpc.so bind to torch's copies, in torch's own load order."""
     try:
-        spec = importlib.util.find_spec("torch")
-    except (ImportError, ValueError):
-        spec = None
-    if spec and spec.origin:
-        cand = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
-        if os.path.exists(cand):
-            C.CDLL(cand, mode=C.RTLD_GLOBAL)
+        import torch  # noqa: F401
+    except ImportError:
+        pass
 
 
 _bind_single_hip_runtime()
@@ -146,6 +145,15 @@ _sig("lhpc_csr_load", _i, C.c_char_p, _p, _p, _p)
 _sig("lhpc_mm_read_header", _i, C.c_char_p, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i),
      C.POINTER(_i))
 _sig("lhpc_mm_read_coo", _i, C.c_char_p, _p, _p, _p, C.POINTER(_i64))
+_sig("lhpc_dist_get_unique_id", _i, _p)
+_sig("lhpc_dist_comm_create", _i, C.POINTER(_p), _p, _i, _i, _i)
+_sig("lhpc_dist_comm_info", _i, _p, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i))
+_sig("lhpc_dist_comm_destroy", _i, _p)
+_sig("lhpc_dist_allreduce_sum_f64", _i, _p, _p, _i64, _p)
+_sig("lhpc_dist_spmv_plan_create", _i, C.POINTER(_p), _p, _i, _i64, _i64, _i, _p, _p, _i, _p, _p, _u)
+_sig("lhpc_dist_spmv", _i, _p, _p, _p, _p)
+_sig("lhpc_dist_spmv_plan_destroy", _i, _p)
+_sig("lhpc_dist_stencil7_f32", _i, _p, _p, _p, _i64, _i64, _i64, _i64, _f, _f, _p)
 
 
 class LhpcError(RuntimeError):
@@ -626,3 +634,147 @@ def gen_laplacian_2d(nx: int, ny: int, dtype=F64, shift: float = 0.0):
     rp = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(mask.sum(axis=1), out=rp[1:])
     return rp, cols, vals
+
+
+# ------------------------------------------------------------ multi-GPU (RCCL)
+DIST_UNIQUE_ID_BYTES = 128
+
+
+def dist_unique_id() -> bytes:
+    """128-byte RCCL unique id (rank 0 makes it, every rank receives it)."""
+    buf = (C.c_ubyte * DIST_UNIQUE_ID_BYTES)()
+    _check(lib.lhpc_dist_get_unique_id(buf), "lhpc_dist_get_unique_id")
+    return bytes(buf)
+
+
+class DistComm:
+    """One RCCL communicator + communication stream per process and GPU
+    (include/lhpc.h lhpc_dist_comm_*; C++: sparse::DistComm)."""
+
+    def __init__(self, unique_id: bytes, nranks: int, rank: int, device: int):
+        if len(unique_id) != DIST_UNIQUE_ID_BYTES:
+            raise ValueError("unique id must be 128 bytes")
+        uid = (C.c_ubyte * DIST_UNIQUE_ID_BYTES).from_buffer_copy(unique_id)
+        self._h = _p()
+        _check(lib.lhpc_dist_comm_create(C.byref(self._h), uid, int(nranks), int(rank), int(device)),
+               "lhpc_dist_comm_create")
+        self.nranks, self.rank, self.device = int(nranks), int(rank), int(device)
+
+    @classmethod
+    def from_torch(cls, device: int, group=None):
+        """Rank 0's unique id handed to every rank over an initialised
+        torch.distributed group (any backend)."""
+        import torch
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = np.frombuffer(dist_unique_id(), dtype=np.uint8).copy() if rank == 0 else \
+            np.zeros(DIST_UNIQUE_ID_BYTES, dtype=np.uint8)
+        backend = dist.get_backend(group)
+        t = torch.from_numpy(uid)
+        if backend == "nccl":
+            t = t.to(torch.device("cuda", device))
+        dist.broadcast(t, 0, group=group)
+        return cls(t.cpu().numpy().tobytes(), world, rank, device)
+
+    def allreduce_sum_f64(self, t, stream=None):
+        _check(lib.lhpc_dist_allreduce_sum_f64(self._h, t.data_ptr(), t.numel(), _stream_ptr(stream)),
+               "lhpc_dist_allreduce_sum_f64")
+        return t
+
+    def stencil7(self, u, out, nzl, ny, nx, ghost=1, c0=-6.0, c1=1.0, stream=None):
+        """One 7-point step on this rank's z-slab, halo planes exchanged over RCCL."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(u.device)
+        _check(lib.lhpc_dist_stencil7_f32(self._h, u.data_ptr(), out.data_ptr(), nzl, ny, nx, ghost,
+                                          float(c0), float(c1), _stream_ptr(stream)), "lhpc_dist_stencil7_f32")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib.lhpc_dist_comm_destroy(self._h)
+            self._h = _p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def interleaved_cuts(row_ptr, world: int, K: int) -> np.ndarray:
+    """nnz-balanced row cuts into world·K blocks (block k·world + r = rank r's
+    chunk k): lhpc_csr_partition_rows with world·K parts."""
+    return csr_partition_rows(row_ptr, world * K)
+
+
+def interleaved_local_csr(row_ptr, col_idx, val, cuts, world: int, K: int, rank: int):
+    """The rank's K blocks stacked in chunk order (row_ptr rebased, global
+    columns): the local input of DistSpMVPlan / lhpc_dist_spmv_plan_create."""
+    blocks = [(int(cuts[k * world + rank]), int(cuts[k * world + rank + 1])) for k in range(K)]
+    n_local = sum(r1 - r0 for r0, r1 in blocks)
+    lrp = np.zeros(n_local + 1, dtype=np.int64)
+    cols, vals, at, off = [], [], 0, 0
+    for r0, r1 in blocks:
+        k0, k1 = int(row_ptr[r0]), int(row_ptr[r1])
+        lrp[at:at + r1 - r0 + 1] = row_ptr[r0:r1 + 1].astype(np.int64) - k0 + off
+        cols.append(col_idx[k0:k1])
+        vals.append(val[k0:k1])
+        at += r1 - r0
+        off += k1 - k0
+    if off < 2 ** 31:
+        lrp = lrp.astype(np.int32)
+    col = np.concatenate(cols) if cols else col_idx[:0]
+    v = np.concatenate(vals) if vals else val[:0]
+    return lrp, col, v
+
+
+class DistSpMVPlan:
+    """y = A·x over ranks with RCCL behind the C ABI (lhpc_dist_spmv_*):
+    the rank's K interleaved nnz-balanced blocks, x staged once, chunk k
+    reduced then broadcast (in place, exact slices) while chunk k+1 runs.
+    ``row_ptr/col_idx/val`` are the rank's LOCAL stacked CSR
+    (interleaved_local_csr); ``cuts`` the global world·K+1 cuts."""
+
+    def __init__(self, comm: DistComm, n_rows: int, n_cols: int, K: int, cuts, row_ptr, col_idx, val,
+                 flags: int = 0):
+        row_ptr = np.ascontiguousarray(row_ptr)
+        col_idx = np.ascontiguousarray(col_idx, dtype=np.int32)
+        val = np.ascontiguousarray(val)
+        self.cuts = np.ascontiguousarray(cuts, dtype=np.int64)
+        if self.cuts.shape[0] != comm.nranks * K + 1:
+            raise ValueError("cuts must hold nranks*K + 1 rows")
+        self.dtype = F32 if val.dtype == np.float32 else F64
+        self.n_rows, self.n_cols, self.K, self.comm = int(n_rows), int(n_cols), int(K), comm
+        self._h = _p()
+        _check(lib.lhpc_dist_spmv_plan_create(
+            C.byref(self._h), comm._h, self.dtype, self.n_rows, self.n_cols, self.K, self.cuts.ctypes.data,
+            row_ptr.ctypes.data, 64 if row_ptr.dtype == np.int64 else 32, col_idx.ctypes.data, val.ctypes.data,
+            flags), "lhpc_dist_spmv_plan_create")
+
+    def __call__(self, x, y=None, stream=None):
+        """Full y (n_rows) on every rank from the full x (device tensors)."""
+        import torch
+        if y is None:
+            y = torch.empty(self.n_rows, dtype=x.dtype, device=x.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(x.device)
+        _check(lib.lhpc_dist_spmv(self._h, x.data_ptr(), y.data_ptr(), _stream_ptr(stream)), "lhpc_dist_spmv")
+        return y
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib.lhpc_dist_spmv_plan_destroy(self._h)
+            self._h = _p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -1,0 +1,312 @@
+// lhpc_dist.hip — multi-GPU SpMV and stencil behind the C ABI: one process
+// per GPU, one RCCL communicator (over xGMI) and one communication stream per
+// process (SURVEY §8b "one stream and one RCCL comm per device", §8e).
+//
+// The reference has no multi-device code; its only overlap idiom
+// is the chunked copy/compute stream pipeline of
+// lib/gpu/transfer_overlap_testsuite/src/cuda_tut_transfer_overlap.cu:41-142,
+// which the chunk loop of lhpc_dist_spmv follows with a collective in place
+// of the copy.
+//
+//   SpMV   rows cut into nranks·K nnz-balanced blocks (lhpc_csr_partition_rows
+//          with nranks·K parts); block b = k·nranks + r is rank r's chunk k.
+//          A rank stages x once (the XTILE tile gather of a row-range plan
+//          over its K blocks), then for k = 0..K−1 reduces chunk k straight
+//          into its rows of the full y and hands chunk k to the comm stream,
+//          where a group of nranks in-place ncclBroadcast (root r sends block
+//          k·nranks + r) fills every rank's y — exact slices, no padding —
+//          while the compute stream reduces chunk k+1.  y is then the next x
+//          on every rank.
+//   stencil z-slabs with one halo plane per side: ncclSend/ncclRecv to the
+//          z neighbours on the comm stream while the interior planes are
+//          computed; the two boundary planes after the exchange.
+// Status: RCCL failures are LHPC_RCCL_STATUS_BASE + ncclResult_t.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "lhpc_common.hpp"
+
+#define LHPC_NCCL_TRY(expr)                                                \
+  do {                                                                     \
+    ncclResult_t _r = (expr);                                              \
+    if (_r != ncclSuccess) return LHPC_RCCL_STATUS_BASE + static_cast<int>(_r); \
+  } while (0)
+
+static_assert(sizeof(ncclUniqueId) == LHPC_DIST_UNIQUE_ID_BYTES, "ncclUniqueId is 128 bytes");
+
+struct lhpc_dist_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0, device = 0;
+  hipStream_t s_comm = nullptr;
+};
+
+struct lhpc_dist_spmv_plan {
+  lhpc_dist_comm *comm = nullptr;
+  int dtype = LHPC_F32, K = 1;
+  int64_t n_rows = 0, n_cols = 0;
+  std::vector<int64_t> cuts;                // nranks·K + 1 global row cuts
+  lhpc_spmv_plan *split = nullptr;          // row-range plan over the rank's blocks (XTILE)
+  std::vector<int> range_of;                // block k → range index of `split` (−1: empty block)
+  std::vector<lhpc_spmv_plan *> block_plan; // otherwise one plan per non-empty block
+  std::vector<hipEvent_t> ev;               // [K] chunk k reduced
+  hipEvent_t done = nullptr;                // last broadcast issued on the comm stream
+};
+
+namespace {
+
+ncclDataType_t nccl_dt(int dtype) { return dtype == LHPC_F64 ? ncclFloat64 : ncclFloat32; }
+
+void destroy_spmv(lhpc_dist_spmv_plan *d) {
+  if (!d) return;
+  (void)hipSetDevice(d->comm ? d->comm->device : 0);
+  if (d->split) lhpc_spmv_plan_destroy(d->split);
+  for (auto *p : d->block_plan)
+    if (p) lhpc_spmv_plan_destroy(p);
+  for (hipEvent_t e : d->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (d->done) (void)hipEventDestroy(d->done);
+  delete d;
+}
+
+// the broadcasts of chunk k: every rank's block k·nranks + r from root r
+int broadcast_chunk(const lhpc_dist_spmv_plan *d, int k, void *y, hipStream_t cs) {
+  const lhpc_dist_comm *c = d->comm;
+  const size_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
+  LHPC_NCCL_TRY(ncclGroupStart());
+  for (int r = 0; r < c->nranks; ++r) {
+    const int64_t b = static_cast<int64_t>(k) * c->nranks + r;
+    const int64_t cnt = d->cuts[b + 1] - d->cuts[b];
+    if (cnt <= 0) continue;
+    void *p = static_cast<unsigned char *>(y) + d->cuts[b] * tsz;
+    const ncclResult_t st = ncclBroadcast(p, p, static_cast<size_t>(cnt), nccl_dt(d->dtype), r, c->comm, cs);
+    if (st != ncclSuccess) {
+      (void)ncclGroupEnd();
+      return LHPC_RCCL_STATUS_BASE + static_cast<int>(st);
+    }
+  }
+  LHPC_NCCL_TRY(ncclGroupEnd());
+  return LHPC_OK;
+}
+
+}  // namespace
+
+extern "C" int lhpc_dist_get_unique_id(unsigned char *id_out) {
+  if (!id_out) return LHPC_ERR_INVALID_ARG;
+  ncclUniqueId id;
+  LHPC_NCCL_TRY(ncclGetUniqueId(&id));
+  std::memcpy(id_out, &id, sizeof(id));
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_comm_create(lhpc_dist_comm **out, const unsigned char *id, int nranks, int rank,
+                                     int device) {
+  if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks || device < 0) return LHPC_ERR_INVALID_ARG;
+  *out = nullptr;
+  LHPC_HIP_TRY(hipSetDevice(device));
+  auto *c = new (std::nothrow) lhpc_dist_comm();
+  if (!c) return LHPC_ERR_ALLOC;
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  const ncclResult_t st = ncclCommInitRank(&c->comm, nranks, uid, rank);
+  if (st != ncclSuccess) {
+    delete c;
+    return LHPC_RCCL_STATUS_BASE + static_cast<int>(st);
+  }
+  const hipError_t he = hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking);
+  if (he != hipSuccess) {
+    (void)ncclCommDestroy(c->comm);
+    delete c;
+    return static_cast<int>(he);
+  }
+  *out = c;
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_comm_destroy(lhpc_dist_comm *c) {
+  if (!c) return LHPC_OK;
+  (void)hipSetDevice(c->device);
+  if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
+  int st = LHPC_OK;
+  if (c->comm) {
+    const ncclResult_t r = ncclCommDestroy(c->comm);
+    if (r != ncclSuccess) st = LHPC_RCCL_STATUS_BASE + static_cast<int>(r);
+  }
+  if (c->s_comm) (void)hipStreamDestroy(c->s_comm);
+  delete c;
+  return st;
+}
+
+extern "C" int lhpc_dist_comm_info(const lhpc_dist_comm *c, int *nranks, int *rank, int *device) {
+  if (!c) return LHPC_ERR_INVALID_ARG;
+  if (nranks) *nranks = c->nranks;
+  if (rank) *rank = c->rank;
+  if (device) *device = c->device;
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_allreduce_sum_f64(lhpc_dist_comm *c, double *buf, int64_t count, void *stream) {
+  if (!c || (count > 0 && !buf) || count < 0) return LHPC_ERR_INVALID_ARG;
+  if (count == 0) return LHPC_OK;
+  LHPC_HIP_TRY(hipSetDevice(c->device));
+  LHPC_NCCL_TRY(ncclAllReduce(buf, buf, static_cast<size_t>(count), ncclFloat64, ncclSum, c->comm,
+                              static_cast<hipStream_t>(stream)));
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_comm *comm, int dtype,
+                                          int64_t n_rows, int64_t n_cols, int K, const int64_t *cuts,
+                                          const void *row_ptr, int row_ptr_bits, const int32_t *col_idx,
+                                          const void *val, unsigned flags) {
+  if (!out || !comm || !cuts || !row_ptr || K < 1 || n_rows < 0 || n_cols < 0 ||
+      (dtype != LHPC_F32 && dtype != LHPC_F64) || (row_ptr_bits != 32 && row_ptr_bits != 64))
+    return LHPC_ERR_INVALID_ARG;
+  *out = nullptr;
+  const int nr = comm->nranks, rk = comm->rank;
+  const int64_t nb = static_cast<int64_t>(nr) * K;
+  if (cuts[0] != 0 || cuts[nb] != n_rows) return LHPC_ERR_INVALID_ARG;
+  for (int64_t b = 0; b < nb; ++b)
+    if (cuts[b + 1] < cuts[b]) return LHPC_ERR_INVALID_ARG;
+  LHPC_HIP_TRY(hipSetDevice(comm->device));
+  auto *d = new (std::nothrow) lhpc_dist_spmv_plan();
+  if (!d) return LHPC_ERR_ALLOC;
+  d->comm = comm;
+  d->dtype = dtype;
+  d->K = K;
+  d->n_rows = n_rows;
+  d->n_cols = n_cols;
+  d->cuts.assign(cuts, cuts + nb + 1);
+  // the local CSR: the rank's K blocks stacked in chunk order
+  std::vector<int64_t> ls(static_cast<size_t>(K) + 1, 0);
+  for (int k = 0; k < K; ++k) {
+    const int64_t b = static_cast<int64_t>(k) * nr + rk;
+    ls[k + 1] = ls[k] + (cuts[b + 1] - cuts[b]);
+  }
+  const int64_t n_local = ls[K];
+  auto rp_at = [&](int64_t i) {
+    return row_ptr_bits == 64 ? static_cast<const int64_t *>(row_ptr)[i] : static_cast<const int32_t *>(row_ptr)[i];
+  };
+  const int64_t nnz_local = rp_at(n_local);
+  const size_t tsz = dtype == LHPC_F64 ? 8 : 4;
+  int st = LHPC_OK;
+  // splits at the starts of non-empty blocks after the first row
+  std::vector<int64_t> splits;
+  d->range_of.assign(static_cast<size_t>(K), -1);
+  int nrange = 0;
+  for (int k = 0; k < K; ++k) {
+    if (ls[k + 1] == ls[k]) continue;
+    if (ls[k] > 0) splits.push_back(ls[k]);
+    d->range_of[k] = nrange++;
+  }
+  if (!splits.empty())
+    st = lhpc_spmv_plan_create_split(&d->split, dtype, n_local, n_cols, nnz_local, row_ptr, row_ptr_bits, col_idx,
+                                     val, &comm->device, 1, flags, static_cast<int>(splits.size()), splits.data());
+  if (splits.empty() || st == LHPC_ERR_UNSUPPORTED) {
+    // one plan per non-empty block (the matrix does not select XTILE, or the
+    // rank holds a single block)
+    d->split = nullptr;
+    st = LHPC_OK;
+    d->block_plan.assign(static_cast<size_t>(K), nullptr);
+    for (int k = 0; k < K && st == LHPC_OK; ++k) {
+      const int64_t r0 = ls[k], r1 = ls[k + 1];
+      if (r1 == r0) continue;
+      const int64_t e0 = rp_at(r0), e1 = rp_at(r1);
+      std::vector<int64_t> lrp(static_cast<size_t>(r1 - r0 + 1));
+      for (int64_t i = r0; i <= r1; ++i) lrp[static_cast<size_t>(i - r0)] = rp_at(i) - e0;
+      st = lhpc_spmv_plan_create(&d->block_plan[k], dtype, r1 - r0, n_cols, e1 - e0, lrp.data(), 64,
+                                 col_idx + e0, static_cast<const unsigned char *>(val) + e0 * tsz, &comm->device, 1,
+                                 flags);
+    }
+  }
+  if (st == LHPC_OK) {
+    d->ev.assign(static_cast<size_t>(K), nullptr);
+    for (auto &e : d->ev)
+      if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->done, hipEventDisableTiming));
+  }
+  if (st != LHPC_OK) {
+    destroy_spmv(d);
+    return st;
+  }
+  *out = d;
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream) {
+  if (!d || (d->n_cols > 0 && !x) || (d->n_rows > 0 && !y) || (x == y && d->n_rows > 0)) return LHPC_ERR_INVALID_ARG;
+  const lhpc_dist_comm *c = d->comm;
+  LHPC_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
+  if (d->split) LHPC_TRY(lhpc_spmv_stage(d->split, x, stream));
+  for (int k = 0; k < d->K; ++k) {
+    const int64_t b = static_cast<int64_t>(k) * c->nranks + c->rank;
+    void *yk = static_cast<unsigned char *>(y) + d->cuts[b] * tsz;
+    if (d->range_of[k] >= 0) {
+      if (d->split)
+        LHPC_TRY(lhpc_spmv_range(d->split, d->range_of[k], yk, stream));
+      else
+        LHPC_TRY(lhpc_spmv(d->block_plan[k], x, yk, 1, stream));
+    }
+    if (c->nranks > 1) {
+      LHPC_HIP_TRY(hipEventRecord(d->ev[k], s));
+      LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, d->ev[k], 0));
+      LHPC_TRY(broadcast_chunk(d, k, y, c->s_comm));
+    }
+  }
+  if (c->nranks > 1) {
+    LHPC_HIP_TRY(hipEventRecord(d->done, c->s_comm));
+    LHPC_HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
+  }
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_spmv_plan_destroy(lhpc_dist_spmv_plan *d) {
+  destroy_spmv(d);
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_stencil7_f32(lhpc_dist_comm *c, float *u, float *out, int64_t nzl, int64_t ny,
+                                      int64_t nx, int64_t ghost, float c0, float c1, void *stream) {
+  if (!c || !u || !out || nzl < 1 || ny < 0 || nx < 0 || ghost < 1) return LHPC_ERR_INVALID_ARG;
+  LHPC_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t P = (ny + 2 * ghost) * (nx + 2 * ghost);  // padded plane
+  auto plane = [&](int64_t z) { return u + (z + ghost) * P; };  // logical plane z ∈ [−ghost, nzl + ghost)
+  const bool lo = c->rank > 0, hi = c->rank < c->nranks - 1;
+  hipEvent_t ev_in = nullptr, ev_halo = nullptr;
+  if (lo || hi) {
+    LHPC_HIP_TRY(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    LHPC_HIP_TRY(hipEventCreateWithFlags(&ev_halo, hipEventDisableTiming));
+    LHPC_HIP_TRY(hipEventRecord(ev_in, s));  // u complete on the caller's stream
+    LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, ev_in, 0));
+    LHPC_NCCL_TRY(ncclGroupStart());
+    if (lo) {
+      LHPC_NCCL_TRY(ncclSend(plane(0), static_cast<size_t>(P), ncclFloat32, c->rank - 1, c->comm, c->s_comm));
+      LHPC_NCCL_TRY(ncclRecv(plane(-1), static_cast<size_t>(P), ncclFloat32, c->rank - 1, c->comm, c->s_comm));
+    }
+    if (hi) {
+      LHPC_NCCL_TRY(ncclSend(plane(nzl - 1), static_cast<size_t>(P), ncclFloat32, c->rank + 1, c->comm, c->s_comm));
+      LHPC_NCCL_TRY(ncclRecv(plane(nzl), static_cast<size_t>(P), ncclFloat32, c->rank + 1, c->comm, c->s_comm));
+    }
+    LHPC_NCCL_TRY(ncclGroupEnd());
+    LHPC_HIP_TRY(hipEventRecord(ev_halo, c->s_comm));
+  }
+  // interior planes need no halo: they run while the planes travel
+  int st = LHPC_OK;
+  if (nzl > 2) st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, 1, nzl - 1, stream);
+  if (st == LHPC_OK && ev_halo) st = static_cast<int>(hipStreamWaitEvent(s, ev_halo, 0));
+  if (st == LHPC_OK) st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, 0, 1, stream);
+  if (st == LHPC_OK && nzl > 1)
+    st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, nzl - 1, nzl, stream);
+  if (ev_in) (void)hipEventDestroy(ev_in);  // destruction is deferred until the event completes
+  if (ev_halo) (void)hipEventDestroy(ev_halo);
+  return st;
+}

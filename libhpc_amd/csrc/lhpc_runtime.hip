@@ -1,5 +1,6 @@
 // lhpc_runtime.hip — status strings and device discovery for the C ABI.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cstring>
 
@@ -15,6 +16,8 @@ extern "C" const char *lhpc_strerror(int status) {
     case LHPC_ERR_UNSUPPORTED: return "lhpc: unsupported configuration";
     case LHPC_ERR_INTERNAL: return "lhpc: internal error";
     default:
+      if (status >= LHPC_RCCL_STATUS_BASE)
+        return ncclGetErrorString(static_cast<ncclResult_t>(status - LHPC_RCCL_STATUS_BASE));
       if (status > 0) return hipGetErrorString(static_cast<hipError_t>(status));
       return "lhpc: unknown status";
   }

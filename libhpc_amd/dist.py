@@ -146,20 +146,32 @@ class DistStencil7:
 
 # ---------------------------------------------- SpMV with overlapped all-gather
 class InterleavedBlocks:
-    """Row ownership for overlapped all-gather: the rows are cut into
-    world·K blocks of B = ceil(n/(world·K)) rows; global block b = k·world + r
-    belongs to rank r as its chunk k.  The all-gather of chunk k from every
-    rank is then exactly rows [k·world·B, (k+1)·world·B) of y, so each chunk's
-    collective can run while the next chunk computes."""
+    """Row ownership for overlapped all-gather: the rows are cut into world·K
+    blocks; global block b = k·world + r belongs to rank r as its chunk k, so
+    the gather of chunk k from every rank is exactly rows
+    [cuts[k·world], cuts[(k+1)·world]) of y and each chunk's collective can
+    run while the next chunk computes.
 
-    def __init__(self, n_rows: int, world: int, K: int):
+    With ``row_ptr`` the cuts are nnz-balanced (binary search on
+    row_ptr for the nnz targets, lhpc_csr_partition_rows with world·K parts);
+    without it, equal row blocks.  B = the largest block: the torch path pads
+    every block to B rows (all_gather needs equal counts) and compacts y; the
+    native path (libhpc_amd.DistSpMVPlan) broadcasts exact slices."""
+
+    def __init__(self, n_rows: int, world: int, K: int, row_ptr=None):
         self.n, self.world, self.K = n_rows, world, K
-        self.B = -(-n_rows // (world * K)) if n_rows else 0
+        if row_ptr is not None:
+            from . import csr_partition_rows
+            self.cuts = csr_partition_rows(row_ptr, world * K).astype(np.int64)
+        else:
+            b = -(-n_rows // (world * K)) if n_rows else 0
+            self.cuts = np.minimum(np.arange(world * K + 1, dtype=np.int64) * b, n_rows)
+        self.B = int(np.max(np.diff(self.cuts))) if n_rows else 0
+        self.even = bool(np.all(np.diff(self.cuts)[:-1] == self.B)) if n_rows else True
 
     def rows(self, rank: int, k: int):
         b = k * self.world + rank
-        r0 = min(b * self.B, self.n)
-        return r0, min(r0 + self.B, self.n)
+        return int(self.cuts[b]), int(self.cuts[b + 1])
 
     def local_csr(self, row_ptr, col_idx, val, rank: int, k: int):
         r0, r1 = self.rows(rank, k)
@@ -186,10 +198,21 @@ class InterleavedBlocks:
         v = np.concatenate([w for _, _, w in parts]) if parts else val[:0]
         return lrp, col, v, [k * self.B for k in range(1, self.K)]
 
+    def compact_index(self):
+        """Positions of y's rows in the padded gather buffer (K·world·B)."""
+        idx = np.empty(self.n, dtype=np.int64)
+        for b in range(self.world * self.K):
+            r0, r1 = int(self.cuts[b]), int(self.cuts[b + 1])
+            idx[r0:r1] = b * self.B + np.arange(r1 - r0)
+        return idx
+
 
 class DistSpMVOverlap:
     """y = A·x on `world` ranks, K chunks per rank, all-gather of chunk k
-    (async, RCCL stream) overlapped with the SpMV of chunk k+1.
+    (async, RCCL stream) overlapped with the SpMV of chunk k+1 — the
+    torch.distributed form (any backend; the gloo tests and the 1-GPU
+    rehearsal).  The native RCCL form behind the C ABI is
+    libhpc_amd.DistSpMVPlan (lhpc_dist_spmv).
 
     ``local_spmvs[k](x, y_out)`` computes the rank's chunk k (B rows)."""
 
@@ -200,15 +223,18 @@ class DistSpMVOverlap:
         self.group = group
         B, W, K = blocks.B, blocks.world, blocks.K
         self.y_local = torch.zeros(K, B, dtype=like.dtype, device=like.device)
-        self.y_full = torch.empty(K * W * B, dtype=like.dtype, device=like.device)
+        self.y_pad = torch.empty(K * W * B, dtype=like.dtype, device=like.device)
+        self.idx = None if blocks.even else torch.from_numpy(blocks.compact_index()).to(like.device)
+        self.y_full = torch.empty(blocks.n, dtype=like.dtype, device=like.device)
 
     def step(self, x):
+        import torch
         import torch.distributed as dist
         B, W, K = self.blocks.B, self.blocks.world, self.blocks.K
         works = []
         for k in range(K):
             self.fns[k](x, self.y_local[k])
-            out = self.y_full[k * W * B:(k + 1) * W * B]
+            out = self.y_pad[k * W * B:(k + 1) * W * B]
             if W > 1:
                 works.append(dist.all_gather_into_tensor(out, self.y_local[k], group=self.group,
                                                          async_op=True))
@@ -216,7 +242,10 @@ class DistSpMVOverlap:
                 out.copy_(self.y_local[k])
         for w in works:
             w.wait()
-        return self.y_full[:self.blocks.n]
+        if self.idx is None:
+            return self.y_pad[:self.blocks.n]
+        torch.index_select(self.y_pad, 0, self.idx, out=self.y_full)
+        return self.y_full
 
 
 # ------------------------------------------------------------------ CG

@@ -8,7 +8,10 @@
 // AlignedAlloc.hpp fails to link this way; ours must not.
 #include <HPCHighDimensionFlatArray.hpp>
 #include <Stencil.hpp>
+#include <sparse/Dist.hpp>
 #include <sparse/SpMV.hpp>
+
+#include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
@@ -17,6 +20,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <system_error>
+#include <vector>
 
 int second_tu_sum(int n);  // second_tu.cpp
 
@@ -137,6 +141,35 @@ int gpu_mode() {
         const float t0 = -6.f * u(z, yy, xx), t1 = 1.f * s;
         if (t0 + t1 != o(z, yy, xx)) return fail("stencil7 mismatch");
       }
+  // ---- multi-GPU layer at world 1 (sparse/Dist.hpp): K = 2 interleaved
+  //      chunks through lhpc_dist_spmv equal the single-plan y bit for bit
+  {
+    sparse::DistComm comm(sparse::DistComm::unique_id(), 1, 0, 0);
+    const int K = 2;
+    const auto cuts = sparse::interleaved_cuts(A, 1, K);
+    const auto L = sparse::interleaved_local(A, cuts, 1, K, 0);
+    sparse::DistSpMVPlan<float> dplan(comm, n, m, K, cuts, L);
+    float *dx = nullptr, *dy = nullptr;
+    double *dd = nullptr;
+    auto hip_ok = [](hipError_t e) { return e == hipSuccess; };
+    if (!hip_ok(hipMalloc(&dx, sizeof(float) * m)) || !hip_ok(hipMalloc(&dy, sizeof(float) * n)) ||
+        !hip_ok(hipMalloc(&dd, sizeof(double) * 4)))
+      return fail("hipMalloc");
+    if (!hip_ok(hipMemcpy(dx, x.data(), sizeof(float) * m, hipMemcpyHostToDevice))) return fail("hipMemcpy");
+    sparse::spmv(dplan, dx, dy);
+    std::vector<float> yd(static_cast<std::size_t>(n));
+    if (!hip_ok(hipMemcpy(yd.data(), dy, sizeof(float) * n, hipMemcpyDeviceToHost))) return fail("hipMemcpy");
+    for (std::int64_t i = 0; i < n; ++i)
+      if (yd[std::size_t(i)] != y(i)) return fail("dist spmv mismatch");
+    const double h4[4] = {1.5, -2.0, 3.25, 0.0};
+    double b4[4];
+    if (!hip_ok(hipMemcpy(dd, h4, sizeof(h4), hipMemcpyHostToDevice))) return fail("hipMemcpy");
+    comm.allreduce_sum(dd, 4);
+    if (!hip_ok(hipMemcpy(b4, dd, sizeof(b4), hipMemcpyDeviceToHost))) return fail("hipMemcpy");
+    for (int i = 0; i < 4; ++i)
+      if (b4[i] != h4[i]) return fail("allreduce world 1");
+    if (!hip_ok(hipFree(dx)) || !hip_ok(hipFree(dy)) || !hip_ok(hipFree(dd))) return fail("hipFree");
+  }
   std::printf("cpp api gpu: ok (spmv kernel %d)\n", plan.info().kernel);
   return 0;
 }

@@ -77,7 +77,7 @@ def test_distributed_spmv_gloo(world, kind):
     assert max(r[2] for r in res) - min(r[2] for r in res) <= 10_000
 
 
-def _worker_overlap(rank, world, port, K, q):
+def _worker_overlap(rank, world, port, K, q, balanced=False):
     try:
         import torch
         import torch.distributed as dist
@@ -90,7 +90,7 @@ def _worker_overlap(rank, world, port, K, q):
         n = 10_007
         rp, col, val = L.gen_powerlaw_csr(n, n, lmax=500, dtype=L.F32, seed=0xD160)
         x = L.gen_values(L.F32, 0, n, 0xD161)
-        ib = InterleavedBlocks(n, world, K)
+        ib = InterleavedBlocks(n, world, K, row_ptr=rp if balanced else None)
         fns = []
         for k in range(K):
             lrp, lc, lv = ib.local_csr(rp, col, val, rank, k)
@@ -108,12 +108,16 @@ def _worker_overlap(rank, world, port, K, q):
         q.put((rank, repr(e)))
 
 
-@pytest.mark.parametrize("world,K", [(2, 3), (3, 4), (4, 1)])
-def test_overlapped_allgather_gloo(world, K):
+@pytest.mark.parametrize("world,K,balanced", [(2, 3, False), (3, 4, False), (4, 1, False), (2, 3, True),
+                                              (3, 4, True), (4, 2, True)])
+def test_overlapped_allgather_gloo(world, K, balanced):
+    """The torch-collective form of the overlapped SpMV: equal-row or
+    nnz-balanced interleaved blocks (the latter padded for all_gather and
+    compacted), assembled y bit-identical to the unpartitioned oracle."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker_overlap, args=(r, world, port, K, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker_overlap, args=(r, world, port, K, q, balanced)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=240) for _ in range(world))
@@ -144,3 +148,68 @@ def test_local_csr_all_concatenates_chunks(world, K, rank):
         seg = lrp[k * ib.B:(k + 1) * ib.B + 1]
         assert np.array_equal(seg - seg[0], prp.astype(np.int64))
         assert np.array_equal(lc[seg[0]:seg[-1]], pc) and np.array_equal(lv[seg[0]:seg[-1]], pv)
+
+
+@pytest.mark.parametrize("world,K", [(2, 2), (3, 4), (8, 2), (4, 1)])
+def test_interleaved_cuts_are_nnz_balanced(world, K):
+    """cuts by binary search on row_ptr for the nnz targets
+    b·nnz/(world·K) — every block within one row's length of the target."""
+    import libhpc_amd as L
+    from libhpc_amd.dist import InterleavedBlocks
+    n = 50_021
+    rp, _, _ = L.gen_powerlaw_csr(n, n, lmax=3000, dtype=L.F32, seed=0xD170)
+    ib = InterleavedBlocks(n, world, K, row_ptr=rp)
+    assert np.array_equal(ib.cuts, L.interleaved_cuts(rp, world, K))
+    nnz, P = int(rp[-1]), world * K
+    lens = np.diff(rp)
+    for b in range(1, P):
+        target = -(-b * nnz // P)
+        c = int(ib.cuts[b])
+        assert rp[c] >= target and (c == 0 or rp[c - 1] < target)
+    blk = np.diff(rp[ib.cuts])
+    assert blk.max() - blk.min() <= 2 * lens.max()
+
+
+def _native_emulation(rp, col, val, x, world, K):
+    """What every rank of lhpc_dist_spmv holds after a call, emulated on the
+    CPU with the oracle: rank r reduces its local stacked CSR
+    (interleaved_local_csr) into its blocks' rows of y, then chunk k's
+    broadcast from root r copies block k·world + r into every rank's y."""
+    import libhpc_amd as L
+    from tests import _support as S
+    cuts = L.interleaved_cuts(rp, world, K)
+    ys = [np.full(rp.shape[0] - 1, np.nan, dtype=val.dtype) for _ in range(world)]
+    own = []
+    for r in range(world):
+        lrp, lc, lv = L.interleaved_local_csr(rp, col, val, cuts, world, K, r)
+        _, yl, _ = S.spmv_oracle(lrp, lc, lv, x)
+        own.append(yl)
+        at = 0
+        for k in range(K):
+            b0, b1 = int(cuts[k * world + r]), int(cuts[k * world + r + 1])
+            ys[r][b0:b1] = yl[at:at + b1 - b0]
+            at += b1 - b0
+    for k in range(K):  # broadcasts of chunk k
+        for root in range(world):
+            b0, b1 = int(cuts[k * world + root]), int(cuts[k * world + root + 1])
+            for r in range(world):
+                ys[r][b0:b1] = ys[root][b0:b1]
+    return ys
+
+
+@pytest.mark.parametrize("world,K", [(2, 2), (3, 3), (8, 2), (1, 2)])
+def test_native_dist_partition_identity(world, K):
+    """The native RCCL path's data layout (lhpc_dist_spmv_plan_create input
+    and the broadcast schedule of lhpc_dist_spmv), checked on the CPU: every
+    rank ends with the unpartitioned y bit for bit (dyadic values), and the
+    local stacked CSRs cover A exactly once."""
+    import libhpc_amd as L
+    from tests import _support as S
+    n = 30_011
+    rp, col, val = L.gen_powerlaw_csr(n, n, lmax=2000, dtype=L.F32, dist=1, seed=0xD180)
+    x = L.gen_values(L.F32, 1, n, 0xD181)
+    _, want, _ = S.spmv_oracle(rp, col, val, x)
+    cuts = L.interleaved_cuts(rp, world, K)
+    assert sum(int(L.interleaved_local_csr(rp, col, val, cuts, world, K, r)[0][-1]) for r in range(world)) == rp[-1]
+    for r, y in enumerate(_native_emulation(rp, col, val, x, world, K)):
+        assert np.array_equal(y, want), f"rank {r}"

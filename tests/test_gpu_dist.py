@@ -1,0 +1,82 @@
+"""The native multi-GPU layer behind the C ABI (include/lhpc.h lhpc_dist_*:
+one RCCL communicator and comm stream per process) on the GPU box's single
+GPU, world 1: the communicator, the fp64 all-reduce, the distributed SpMV
+(stage, per-chunk reduce into y, broadcast schedule, event ordering) through
+both of its local-plan forms, and the halo stencil.  RCCL cannot put two
+ranks on one GPU; the multi-rank data layout and broadcast schedule are
+checked on the CPU (tests/test_dist.py::test_native_dist_partition_identity)."""
+import numpy as np
+import pytest
+
+from tests import _support as S
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def comm(lhpc, gpu):
+    c = lhpc.DistComm(lhpc.dist_unique_id(), 1, 0, 0)
+    yield c
+    c.close()
+
+
+def test_comm_world1_allreduce(lhpc, gpu, comm):
+    import torch
+    assert comm.nranks == 1 and comm.rank == 0
+    t = torch.arange(1000, dtype=torch.float64, device=gpu)
+    comm.allreduce_sum_f64(t, stream=torch.cuda.current_stream(gpu))
+    torch.cuda.synchronize()
+    assert torch.equal(t.cpu(), torch.arange(1000, dtype=torch.float64))
+
+
+def test_unique_ids_differ(lhpc, gpu):
+    assert lhpc.dist_unique_id() != lhpc.dist_unique_id()
+
+
+@pytest.mark.parametrize("n,per_row,K", [(3_000_000, 6, 1), (3_000_000, 6, 2), (3_000_000, 6, 3),
+                                         (20_000, 7, 2), (20_000, 7, 4)])
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_dist_spmv_world1_matches_single_plan(lhpc, gpu, comm, n, per_row, K, dtype):
+    """lhpc_dist_spmv at world 1 with K chunks equals the single-plan SpMV bit
+    for bit on dyadic values (XTILE row-range plan for the 3M-column matrix,
+    one plan per block for the small one), twice in a row, y != x."""
+    import torch
+    dt = lhpc.F32 if dtype == "f32" else lhpc.F64
+    rp, col, val = lhpc.gen_uniform_csr(n, n, per_row, dtype=dt, dist=1, seed=0xD200 + K)
+    x = lhpc.gen_values(dt, 1, n, 0xD201)
+    xd = torch.from_numpy(x).to(gpu)
+    _, want, _ = S.spmv_oracle(rp, col, val, x)
+    cuts = lhpc.interleaved_cuts(rp, 1, K)
+    lrp, lc, lv = lhpc.interleaved_local_csr(rp, col, val, cuts, 1, K, 0)
+    with lhpc.DistSpMVPlan(comm, n, n, K, cuts, lrp, lc, lv) as d:
+        for _ in range(2):
+            y = torch.full((n,), float("nan"), dtype=xd.dtype, device=gpu)
+            d(xd, y)
+            torch.cuda.synchronize()
+            assert np.array_equal(y.cpu().numpy(), want)
+
+
+def test_dist_spmv_rejects_aliased_xy(lhpc, gpu, comm):
+    import torch
+    n = 1000
+    rp, col, val = lhpc.gen_uniform_csr(n, n, 5, dtype=lhpc.F32, dist=1)
+    cuts = lhpc.interleaved_cuts(rp, 1, 2)
+    with lhpc.DistSpMVPlan(comm, n, n, 2, cuts, *lhpc.interleaved_local_csr(rp, col, val, cuts, 1, 2, 0)) as d:
+        xd = torch.ones(n, device=gpu)
+        with pytest.raises(lhpc.LhpcError):
+            d(xd, xd)
+
+
+@pytest.mark.parametrize("nz,ny,nx", [(37, 45, 1100), (9, 19, 512), (1, 5, 7), (2, 3, 1024)])
+def test_dist_stencil7_world1_matches_single_domain(lhpc, gpu, comm, nz, ny, nx):
+    """lhpc_dist_stencil7_f32 at world 1 (no neighbours: outer ghost planes
+    kept) is bit-identical to lhpc_stencil7_f32 on the same slab."""
+    import torch
+    shape = (nz + 2, ny + 2, nx + 2)
+    u = S.random_padded(shape, seed=nz * 13 + nx, zero_ghost=False).reshape(-1)
+    out0 = S.random_padded(shape, seed=77).reshape(-1)
+    want = S.stencil7_oracle(u, nz, ny, nx, 1, -6.0, 1.0, out=out0.copy())
+    ud = torch.from_numpy(u).to(gpu)
+    od = torch.from_numpy(out0.copy()).to(gpu)
+    comm.stencil7(ud, od, nz, ny, nx, 1, -6.0, 1.0)
+    assert np.array_equal(od.cpu().numpy(), want)
