@@ -145,6 +145,9 @@ _sig("lhpc_csr_load", _i, C.c_char_p, _p, _p, _p)
 _sig("lhpc_mm_read_header", _i, C.c_char_p, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i),
      C.POINTER(_i))
 _sig("lhpc_mm_read_coo", _i, C.c_char_p, _p, _p, _p, C.POINTER(_i64))
+if hasattr(lib, "lhpc_probe_xtile_stamps"):  # diagnostic build only (tools/xt_stamps.py)
+    _sig("lhpc_probe_xtile_stamps", _i, _p, _i64)
+    _sig("lhpc_probe_xtile_stamps_clear", _i)
 _sig("lhpc_dist_get_unique_id", _i, _p)
 _sig("lhpc_dist_comm_create", _i, C.POINTER(_p), _p, _i, _i, _i)
 _sig("lhpc_dist_comm_info", _i, _p, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i))

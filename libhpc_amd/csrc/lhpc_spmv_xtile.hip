@@ -161,6 +161,19 @@ template <typename T> __device__ __forceinline__ int xt_slot(int i) {
   return (i & ~(RUN - 1)) | ((((i & (RUN - 1)) / VW) ^ xt_swz(i / RUN)) * VW) | (i & (VW - 1));
 }
 
+// Diagnostic build only (-DLHPC_XT_STAMPS, tools/xt_stamps.py): thread 0 of
+// every reduce block records s_memrealtime at entry and exit and s_memtime at
+// each phase boundary into g_xt_stamps[block][10]; never in a product build.
+#ifdef LHPC_XT_STAMPS
+__device__ uint64_t g_xt_stamps[1 << 22];
+#define LHPC_XT_STAMP(i, real)                                                                  \
+  if (threadIdx.x == 0)                                                                         \
+    g_xt_stamps[static_cast<uint64_t>(blockIdx.x) * 10 + (i)] =                                 \
+        (real) ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
+#else
+#define LHPC_XT_STAMP(i, real)
+#endif
+
 #ifndef LHPC_XT_IP_WAVES
 #define LHPC_XT_IP_WAVES 8  // iperm reduce: 8 waves/SIMD (fp32 66 → 64 VGPRs: C2 593 → 580 µs)
 #endif
@@ -197,6 +210,8 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   const int i0 = tid * RUN;
   const int64_t c = c0 + static_cast<int64_t>(blockIdx.x % 8) * Cx + blockIdx.x / 8;  // chunk range [c0, C)
   if (c >= C) return;  // block-uniform
+  LHPC_XT_STAMP(0, 1)
+  LHPC_XT_STAMP(1, 0)
   // ---- round trip 1: the chunk descriptor and the segment table (both
   //      addressed by c alone), then — without waiting for them — round
   //      trip 2 (val run and row_ptr, addressed by the descriptor).  The
@@ -257,6 +272,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   const int inc = wave_incl_scan(lsum);
   if (lane == kWave - 1) wsum[wv] = inc;
   __syncthreads();
+  LHPC_XT_STAMP(2, 0)
   {
     int run = inc - lsum;
     for (int w = 0; w < wv; ++w) run += wsum[w];
@@ -273,6 +289,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     }
   }
   __syncthreads();
+  LHPC_XT_STAMP(3, 0)
 
   // ---- phase A: src = base_ne[rank] + f, xg loads (round trip 3);
   //      positions past m load the sentinel entry `total` (perm: spare slot M)
@@ -339,6 +356,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
 #pragma unroll
     for (int u = 0; u < NB; ++u) xs[pv[u]] = xv[u];
   }
+  LHPC_XT_STAMP(4, 0)
   // row_ptr (round trip 2) → local row offsets and the row-start bitmap
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
@@ -358,6 +376,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   // wait for: drain it before any wave reads another wave's flat slots
   if constexpr (IP && sizeof(T) == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  LHPC_XT_STAMP(5, 0)
 
   // ---- phase B: branch-free segmented scan of the thread's run.  The fp32
   //      product is exact in fp64, so the fma equals the add of the product.
@@ -415,6 +434,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     cw = wsf[w] ? ws[w] : cw + ws[w];
     gw |= wsf[w];
   }
+  LHPC_XT_STAMP(6, 0)
   if (!fl) sv = cw + sv;
   const int fin_incl = (fl ? 1 : 0) | gw;
   constexpr int kShr1 = 0x138;  // DPP wave_shr:1 (lane l ← lane l−1; lane 0 keeps `old`)
@@ -439,6 +459,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   }
   if (tid == tlast && mask && cont) carry[2 * c + 1] = acc;  // own tail row continues
   __syncthreads();
+  LHPC_XT_STAMP(7, 0)
   // coalesced y store of the owned rows from their last positions (a row
   // continuing past the chunk is stored by k_xtile_fixup, later on the stream)
   for (int j = tid; j < R; j += BLK) {
@@ -446,6 +467,8 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     if (a1 == a0) y[r0 + j] = T(0);
     else if (a1 <= m) y[r0 + j] = xs[xt_slot<T>(a1 - 1)];
   }
+  LHPC_XT_STAMP(8, 0)
+  LHPC_XT_STAMP(9, 1)
 }
 
 // rows cut by a chunk end: y[row] = tail piece + head pieces, chunk order
@@ -670,3 +693,20 @@ int xtile_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const 
 }
 
 }  // namespace lhpc
+
+#ifdef LHPC_XT_STAMPS
+// diagnostic build: copy the reduce's phase stamps (uint64 [blocks][10]) to host
+extern "C" int lhpc_probe_xtile_stamps(void *out, int64_t n) {
+  if (n > (1 << 22)) n = 1 << 22;
+  LHPC_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(lhpc::g_xt_stamps), static_cast<size_t>(n) * 8, 0,
+                                   hipMemcpyDeviceToHost));
+  return LHPC_OK;
+}
+extern "C" int lhpc_probe_xtile_stamps_clear(void) {
+  static uint64_t zero[1 << 16];
+  for (int64_t o = 0; o < (1 << 22); o += 1 << 16)
+    LHPC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(lhpc::g_xt_stamps), zero, sizeof(zero), static_cast<size_t>(o) * 8,
+                                   hipMemcpyHostToDevice));
+  return LHPC_OK;
+}
+#endif
