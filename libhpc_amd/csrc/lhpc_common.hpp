@@ -7,6 +7,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <cstdint>
 
@@ -27,6 +28,33 @@
 namespace lhpc {
 
 constexpr int kWave = 64;  // CDNA wavefront; never 32
+
+// Host-side phase ranges (plan build, stage, range, collectives …), visible
+// to `rocprofv3 --marker-trace` — the reference marks its sort phases with
+// NVTX the same way (lib/gpu/radix_gpu/src/radix_sort_gpu.cpp:26-28).  A
+// push/pop pair is a no-op call when no tool is attached.
+struct RocTxRange {
+  explicit RocTxRange(const char *name) { roctxRangePushA(name); }
+  ~RocTxRange() { roctxRangePop(); }
+  RocTxRange(const RocTxRange &) = delete;
+  RocTxRange &operator=(const RocTxRange &) = delete;
+};
+
+// Debug-build device bounds trap (-DLHPC_DEBUG_BOUNDS), as the reference
+// traps out-of-range scatter indices (lib/gpu/radix_gpu/include/
+// cuda_radix_scatter.cuh:87,174).  Plans already range-check col_idx on the
+// host (validate_csr), so this guards the plan-built device layouts.  Never
+// compiled into the product build.
+#ifdef LHPC_DEBUG_BOUNDS
+#define LHPC_DEVICE_CHECK(cond) \
+  do {                          \
+    if (!(cond)) __builtin_trap(); \
+  } while (0)
+#else
+#define LHPC_DEVICE_CHECK(cond) \
+  do {                          \
+  } while (0)
+#endif
 
 // Native clang vector types: the nontemporal builtins (global_load ... nt)
 // accept these, not HIP_vector_type.

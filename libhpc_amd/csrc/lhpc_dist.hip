@@ -242,6 +242,7 @@ extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_c
 extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream) {
   if (!d || (d->n_cols > 0 && !x) || (d->n_rows > 0 && !y) || (x == y && d->n_rows > 0)) return LHPC_ERR_INVALID_ARG;
   const lhpc_dist_comm *c = d->comm;
+  lhpc::RocTxRange rx("lhpc_dist_spmv");
   LHPC_HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   const size_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
@@ -258,6 +259,7 @@ extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, vo
     if (c->nranks > 1) {
       LHPC_HIP_TRY(hipEventRecord(d->ev[k], s));
       LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, d->ev[k], 0));
+      lhpc::RocTxRange rb("lhpc_dist_spmv: y chunk exchange");
       LHPC_TRY(broadcast_chunk(d, k, y, c->s_comm));
     }
   }
@@ -282,7 +284,9 @@ extern "C" int lhpc_dist_stencil7_f32(lhpc_dist_comm *c, float *u, float *out, i
   auto plane = [&](int64_t z) { return u + (z + ghost) * P; };  // logical plane z ∈ [−ghost, nzl + ghost)
   const bool lo = c->rank > 0, hi = c->rank < c->nranks - 1;
   hipEvent_t ev_in = nullptr, ev_halo = nullptr;
+  lhpc::RocTxRange rx("lhpc_dist_stencil7_f32");
   if (lo || hi) {
+    lhpc::RocTxRange rh("lhpc_dist_stencil7_f32: halo exchange");
     LHPC_HIP_TRY(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     LHPC_HIP_TRY(hipEventCreateWithFlags(&ev_halo, hipEventDisableTiming));
     LHPC_HIP_TRY(hipEventRecord(ev_in, s));  // u complete on the caller's stream

@@ -192,6 +192,7 @@ extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, doubl
   if (!plan || !b || !x || max_iter < 0 || !(tol >= 0.0)) return LHPC_ERR_INVALID_ARG;
   LHPC_TRY(lhpc_spmv_plan_info_get(plan, &info));
   if (info.n_rows != info.n_cols) return LHPC_ERR_INVALID_ARG;  // CG needs a square (SPD) matrix
+  RocTxRange rx("lhpc_cg_solve");
   const int64_t n = info.n_rows;
   const int dtype = info.dtype;
   const size_t ts = dtype == LHPC_F32 ? 4 : 8;

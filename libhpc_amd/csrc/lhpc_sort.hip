@@ -499,6 +499,7 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
       begin_bit > end_bit)
     return LHPC_ERR_INVALID_ARG;
   if (n >= (int64_t{1} << 32)) return LHPC_ERR_UNSUPPORTED;  // 32-bit ranks
+  RocTxRange rx("lhpc_radix_sort");
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (on_device) return radix_sort_dev<K, HAS_V, IPT>(keys, vals, n, begin_bit, end_bit, s);
   DevBuf dk, dv;
@@ -537,6 +538,7 @@ extern "C" int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_
       (nnz > 0 && (!rows || !cols || !vals || !col_out || !val_out)) || (dtype != LHPC_F32 && dtype != LHPC_F64))
     return LHPC_ERR_INVALID_ARG;
   if (nnz >= (int64_t{1} << 32) || (row_ptr_bits == 32 && nnz >= (int64_t{1} << 31))) return LHPC_ERR_UNSUPPORTED;
+  RocTxRange rx("lhpc_coo_to_csr");
   hipStream_t s = static_cast<hipStream_t>(stream);
   const size_t vb = dtype == LHPC_F32 ? 4 : 8;
   auto run = [&](const int32_t *r, const int32_t *c, const void *v, void *rp, int32_t *co, void *vo,

@@ -231,6 +231,7 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
                                      int row_ptr_bits, const int32_t *col_idx,
                                      const void *val, const int *device_ids,
                                      int n_devices, unsigned flags) {
+  RocTxRange rx("lhpc_spmv_plan_create");
   return plan_create_impl(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
                           device_ids, n_devices, flags, 0, nullptr);
 }
@@ -244,6 +245,7 @@ extern "C" int lhpc_spmv_plan_create_split(lhpc_spmv_plan **out, int dtype, int6
   for (int i = 0; i < n_splits; ++i)
     if (split_rows[i] <= 0 || split_rows[i] >= n_rows || (i > 0 && split_rows[i] <= split_rows[i - 1]))
       return LHPC_ERR_INVALID_ARG;
+  RocTxRange rx("lhpc_spmv_plan_create_split");
   const int st = plan_create_impl(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
                                   device_ids, n_devices, flags, n_splits, split_rows);
   if (st != LHPC_OK) return st;
@@ -259,6 +261,7 @@ extern "C" int lhpc_spmv_plan_create_split(lhpc_spmv_plan **out, int dtype, int6
 extern "C" int lhpc_spmv_stage(const lhpc_spmv_plan *p, const void *x, void *stream) {
   if (!p || (p->n_cols > 0 && !x)) return LHPC_ERR_INVALID_ARG;
   if (p->xt_srow.empty()) return LHPC_ERR_UNSUPPORTED;
+  RocTxRange rx("lhpc_spmv_stage");
   LHPC_HIP_TRY(hipSetDevice(p->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   return xtile_stage(p, x, s);
@@ -268,6 +271,7 @@ extern "C" int lhpc_spmv_range(const lhpc_spmv_plan *p, int k, void *y_range, vo
   if (!p || p->xt_srow.empty() || k < 0 || k + 2 > static_cast<int>(p->xt_srow.size()))
     return LHPC_ERR_INVALID_ARG;
   if (p->xt_srow[k + 1] > p->xt_srow[k] && !y_range) return LHPC_ERR_INVALID_ARG;
+  RocTxRange rx("lhpc_spmv_range");
   LHPC_HIP_TRY(hipSetDevice(p->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   return xtile_range(p, k, y_range, s);
@@ -276,6 +280,7 @@ extern "C" int lhpc_spmv_range(const lhpc_spmv_plan *p, int k, void *y_range, vo
 extern "C" int lhpc_spmv(lhpc_spmv_plan *p, const void *x, void *y, int on_device,
                          void *stream) {
   if (!p || (p->n_cols > 0 && !x) || (p->n_rows > 0 && !y)) return LHPC_ERR_INVALID_ARG;
+  RocTxRange rx("lhpc_spmv");
   hipStream_t s = static_cast<hipStream_t>(stream);
   LHPC_HIP_TRY(hipSetDevice(p->device));
   const size_t tsz = p->dtype == LHPC_F32 ? 4 : 8;

@@ -76,6 +76,7 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
       T o[8];
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
+        LHPC_DEVICE_CHECK((w[u][h] & 0xFFFFu) < static_cast<uint32_t>(W) && (w[u][h] >> 16) < static_cast<uint32_t>(W));
         o[2 * h] = xt[w[u][h] & 0xFFFFu];
         o[2 * h + 1] = xt[w[u][h] >> 16];
       }
@@ -323,6 +324,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
       const int f = (wv * NB + u) * kWave + lane;
       const int sv = base_ne[rk] + f;  // m > 0 ⇒ 0 ≤ rk < S; m = 0: base_ne[−1] (in LDS), unused
       src[u] = f < m ? sv : total;
+      LHPC_DEVICE_CHECK(src[u] >= 0 && src[u] <= total);
     }
   }
   // plain loads: the segment lines a neighbouring chunk shares must stay in
@@ -397,6 +399,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
 #pragma unroll
     for (int j = 0; j < RUN; ++j) {
       const uint32_t w = ipv[j / 8][(j % 8) / 2];
+      LHPC_DEVICE_CHECK(((j & 1) ? (w >> 16) : (w & 0xFFFFu)) < static_cast<uint32_t>(M + VW));
       gx[j] = xs[static_cast<int>((j & 1) ? (w >> 16) : (w & 0xFFFFu))];
     }
 #pragma unroll

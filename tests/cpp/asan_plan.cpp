@@ -1,0 +1,194 @@
+// asan_plan.cpp — host-only driver for the plan-time and I/O code of
+// liblhpc.so (lhpc_plan.cpp, lhpc_gen.cpp, lhpc_io.cpp compiled into this
+// binary with -fsanitize=address,undefined; no HIP).  Mirrors the reference's
+// policy of running every Linux test under ASan
+// (/root/reference/tests/CMakeLists.txt:6-9) for the code a GPU box cannot
+// sanitize: the CSR validation and the XSLICE / XTILE re-encodings that index
+// host arrays by caller-supplied row_ptr / col_idx, and the file readers.
+// Built and run by tests/test_asan.py (`make -C tests/cpp asan`).
+#include <unistd.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lhpc.h"
+#include "../../libhpc_amd/csrc/lhpc_plan.hpp"
+
+static int failures = 0;
+#define CHECK(c)                                                             \
+  do {                                                                       \
+    if (!(c)) {                                                              \
+      std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c);      \
+      ++failures;                                                            \
+    }                                                                        \
+  } while (0)
+
+namespace {
+
+struct Csr {
+  int64_t n = 0, m = 0;
+  std::vector<int64_t> rp;
+  std::vector<int32_t> col;
+  std::vector<float> val;
+};
+
+Csr uniform(int64_t n, int64_t m, int per_row, uint64_t seed) {
+  Csr a;
+  a.n = n;
+  a.m = m;
+  a.rp.resize(static_cast<size_t>(n + 1));
+  CHECK(lhpc_gen_uniform_row_ptr(n, per_row, a.rp.data()) == 0);
+  a.col.resize(static_cast<size_t>(a.rp[n]));
+  CHECK(lhpc_gen_fill_cols(n, m, a.rp.data(), seed, a.col.data()) == 0);
+  a.val.resize(a.col.size());
+  CHECK(lhpc_gen_fill_values(LHPC_F32, 0, static_cast<int64_t>(a.val.size()), seed + 1, a.val.data()) == 0);
+  return a;
+}
+
+Csr powerlaw(int64_t n, int64_t m, int64_t lmax, uint64_t seed) {
+  Csr a;
+  a.n = n;
+  a.m = m;
+  a.rp.resize(static_cast<size_t>(n + 1));
+  int64_t nnz = 0;
+  CHECK(lhpc_gen_powerlaw_row_ptr(n, m, 1.792, 1, lmax, seed, a.rp.data(), &nnz) == 0);
+  a.col.resize(static_cast<size_t>(nnz));
+  CHECK(lhpc_gen_fill_cols(n, m, a.rp.data(), seed, a.col.data()) == 0);
+  a.val.resize(a.col.size());
+  CHECK(lhpc_gen_fill_values(LHPC_F32, 0, nnz, seed + 1, a.val.data()) == 0);
+  return a;
+}
+
+// XTILE invariants: every CSR nonzero appears once in its chunk's segment
+// concatenation, with the column it had; chunks tile the CSR order.
+void check_xtile(const Csr &a, bool iperm, const std::vector<int64_t> &splits) {
+  const int64_t W = 4096;
+  const int M = 1024, Rmax = 128;
+  lhpc::XtileHost xt;
+  const int rc = lhpc::build_xtile(a.rp.data(), 64, a.col.data(), a.n, a.m, W, M, Rmax, 3000, 4,
+                                   splits.empty() ? nullptr : splits.data(), static_cast<int>(splits.size()), iperm,
+                                   xt);
+  CHECK(rc == 0);
+  if (rc) return;
+  const int64_t C = xt.n_chunks, S = xt.S;
+  CHECK(xt.ce.front() == 0 && xt.ce[static_cast<size_t>(C)] == a.rp[a.n]);
+  for (int64_t c = 0; c < C; ++c) {
+    const int64_t e0 = xt.ce[c], e1 = xt.ce[c + 1];
+    CHECK(e1 >= e0 && e1 - e0 <= M);
+    std::vector<int> seen(static_cast<size_t>(e1 - e0), 0);
+    int64_t flat = 0;
+    for (int64_t s = 0; s < S; ++s) {
+      const int64_t g0 = xt.segoff[c * S + s], g1 = xt.segoff[(c + 1) * S + s];
+      CHECK(g0 <= g1 && g1 <= xt.total);
+      for (int64_t g = g0; g < g1; ++g, ++flat) {
+        if (iperm) continue;
+        (void)xt.perm[g];  // perm mode: every stream entry has a slot
+      }
+    }
+    CHECK(flat == e1 - e0);
+    if (iperm) {
+      for (int64_t k = e0; k < e1; ++k) {
+        const int f = xt.iperm[k];
+        CHECK(f >= 0 && f < flat);
+        if (f >= 0 && f < flat) ++seen[static_cast<size_t>(f)];
+      }
+      for (int v : seen) CHECK(v == 1);
+    }
+  }
+  // the transposed val/iperm streams and the gather-block permutation
+  std::vector<int32_t> vbase;
+  std::unique_ptr<unsigned char[]> valt;
+  std::unique_ptr<uint16_t[]> ipt;
+  CHECK(lhpc::xtile_transpose_runs(xt, a.val.data(), 4, 16, 64 * 16, vbase, valt, ipt) == 0);
+  CHECK(static_cast<int64_t>(vbase.size()) == C + 1);
+  lhpc::xtile_permute_gather_blocks(xt, 4);
+}
+
+void check_bad_csr() {
+  // every builder pass indexes host arrays by col / row_ptr, so validation
+  // must reject these before any of them runs (lhpc_spmv_plan_create)
+  const int64_t rp[] = {0, 2, 3};
+  const int32_t good[] = {0, 4, 2}, big[] = {0, 5, 2}, neg[] = {0, -1, 2};
+  CHECK(lhpc::validate_csr(rp, 64, good, 2, 5, 3) == 0);
+  CHECK(lhpc::validate_csr(rp, 64, big, 2, 5, 3) == LHPC_ERR_BAD_CSR);
+  CHECK(lhpc::validate_csr(rp, 64, neg, 2, 5, 3) == LHPC_ERR_BAD_CSR);
+  const int64_t down[] = {0, 3, 2};
+  CHECK(lhpc::validate_csr(down, 64, good, 2, 5, 2) == LHPC_ERR_BAD_CSR);
+  const int32_t rp32[] = {1, 2, 3};
+  CHECK(lhpc::validate_csr(rp32, 32, good, 2, 5, 3) == LHPC_ERR_BAD_CSR);  // row_ptr[0] != 0
+  CHECK(lhpc::validate_csr(rp, 64, good, 2, 5, 4) == LHPC_ERR_BAD_CSR);     // row_ptr[n] != nnz
+}
+
+void check_io(const Csr &a) {
+  char tmpl[] = "/tmp/lhpc_asan_XXXXXX";
+  const int fd = mkstemp(tmpl);
+  CHECK(fd >= 0);
+  close(fd);
+  const int64_t nnz = a.rp[a.n];
+  CHECK(lhpc_csr_save(tmpl, LHPC_F32, a.n, a.m, nnz, a.rp.data(), 64, a.col.data(), a.val.data()) == 0);
+  int dt = -1, bits = 0;
+  int64_t n = 0, m = 0, z = 0;
+  CHECK(lhpc_csr_load_header(tmpl, &dt, &n, &m, &z, &bits) == 0);
+  CHECK(dt == LHPC_F32 && n == a.n && m == a.m && z == nnz && bits == 64);
+  std::vector<int64_t> rp(static_cast<size_t>(n + 1));
+  std::vector<int32_t> col(static_cast<size_t>(z));
+  std::vector<float> val(static_cast<size_t>(z));
+  CHECK(lhpc_csr_load(tmpl, rp.data(), col.data(), val.data()) == 0);
+  CHECK(rp == a.rp && col == a.col && val == a.val);
+  // truncated file: the loader must refuse, not read past the mapping
+  CHECK(truncate(tmpl, 100) == 0);
+  CHECK(lhpc_csr_load_header(tmpl, &dt, &n, &m, &z, &bits) != 0 || lhpc_csr_load(tmpl, rp.data(), col.data(), val.data()) != 0);
+  std::remove(tmpl);
+  // Matrix Market: symmetric expansion, comments, a bad entry
+  const std::string mtx = std::string(tmpl) + ".mtx";
+  FILE *f = std::fopen(mtx.c_str(), "w");
+  std::fprintf(f, "%%%%MatrixMarket matrix coordinate real symmetric\n%% c\n3 3 3\n1 1 2.0\n2 1 -1.5\n3 3 4e0\n");
+  std::fclose(f);
+  int64_t zmax = 0, cnt = 0;
+  int sym = -1, fld = -1;
+  CHECK(lhpc_mm_read_header(mtx.c_str(), &n, &m, &zmax, &sym, &fld) == 0 && zmax == 6);
+  std::vector<int32_t> r(static_cast<size_t>(zmax)), c(static_cast<size_t>(zmax));
+  std::vector<double> v(static_cast<size_t>(zmax));
+  CHECK(lhpc_mm_read_coo(mtx.c_str(), r.data(), c.data(), v.data(), &cnt) == 0 && cnt == 4);
+  f = std::fopen(mtx.c_str(), "w");
+  std::fprintf(f, "%%%%MatrixMarket matrix coordinate real general\n3 3 2\n1 1 1.0\n4 1 1.0\n");
+  std::fclose(f);
+  CHECK(lhpc_mm_read_header(mtx.c_str(), &n, &m, &zmax, &sym, &fld) == 0);
+  CHECK(lhpc_mm_read_coo(mtx.c_str(), r.data(), c.data(), v.data(), &cnt) != 0);  // row 4 of 3
+  std::remove(mtx.c_str());
+}
+
+}  // namespace
+
+int main() {
+  check_bad_csr();
+  const Csr u = uniform(20000, 30000, 15, 0x5EED0001);
+  const Csr p = powerlaw(20000, 20000, 3000, 0x5EED0004);
+  const Csr e = uniform(777, 100, 0, 7);  // all rows empty
+  for (bool ip : {false, true}) {
+    check_xtile(u, ip, {});
+    check_xtile(p, ip, {});
+    check_xtile(p, ip, {1, 5000, 19999});
+    check_xtile(e, ip, {});
+  }
+  for (int S : {1, 8, 64}) {
+    lhpc::XsliceHost xs;
+    const int rc = lhpc::build_xslice(p.rp.data(), 64, p.col.data(), p.val.data(), 4, p.n, p.m, S, xs);
+    CHECK(rc == 0 || rc == LHPC_ERR_UNSUPPORTED);
+    if (rc == 0) CHECK(xs.nnz == p.rp[p.n]);
+  }
+  int64_t cuts[9];
+  CHECK(lhpc_csr_partition_rows(p.rp.data(), 64, p.n, 8, cuts) == 0);
+  for (int k = 0; k < 8; ++k) CHECK(cuts[k] <= cuts[k + 1]);
+  check_io(u);
+  if (failures) {
+    std::fprintf(stderr, "%d check(s) failed\n", failures);
+    return 1;
+  }
+  std::printf("ALL OK (asan plan/io)\n");
+  return 0;
+}

@@ -217,6 +217,14 @@ int gpu_tests() {
     std::fclose(f);
     auto M = read_matrix_market<double>(mtx);
     CHECK(M.n_rows == 3 && M.n_cols == 3 && M.nnz() == 4);
+    if (!(M.n_rows == 3 && M.n_cols == 3 && M.nnz() == 4)) {
+      std::fprintf(stderr, "mm: %lld x %lld nnz %lld rp", static_cast<long long>(M.n_rows),
+                   static_cast<long long>(M.n_cols), static_cast<long long>(M.nnz()));
+      for (auto v : M.row_ptr) std::fprintf(stderr, " %lld", static_cast<long long>(v));
+      for (std::size_t i = 0; i < M.col_idx.size(); ++i)
+        std::fprintf(stderr, " (%d %g)", static_cast<int>(M.col_idx[i]), static_cast<double>(M.val[i]));
+      std::fprintf(stderr, "\n");
+    }
     const std::int32_t rp_want[] = {0, 2, 3, 4};
     const std::int32_t col_want[] = {0, 1, 0, 2};
     const double val_want[] = {2.0, -1.5, -1.5, 4.0};
