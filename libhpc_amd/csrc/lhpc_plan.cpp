@@ -130,9 +130,10 @@ int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, 
 
 int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
                 int64_t W, int M, int Rmax, int64_t piece_nnz, int slot_bytes,
-                const int64_t *splits, int n_splits, bool iperm, XtileHost &o) {
+                const int64_t *splits, int n_splits, bool iperm, int cut_window, XtileHost &o) {
   const int64_t nnz = rp_at(rp, bits, n_rows) - rp_at(rp, bits, 0);
-  if (W < 8 || M < 64 || M >= 65536 || M % 16 || Rmax < 1 || (slot_bytes != 4 && slot_bytes != 8))
+  if (W < 8 || M < 64 || M >= 65536 || M % 16 || Rmax < 1 || (slot_bytes != 4 && slot_bytes != 8) ||
+      cut_window < 1 || cut_window > M)
     return LHPC_ERR_INVALID_ARG;
   const int64_t S = n_cols > 0 ? (n_cols + W - 1) / W : 1;
   if (S > 4096 || nnz + 8 * S >= INT32_MAX || n_rows >= INT32_MAX) return LHPC_ERR_UNSUPPORTED;
@@ -175,7 +176,7 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
         const int64_t target = e + Mc;
         // last row q with rp[q] <= target
         const int64_t q = lower_row(r, target + 1) - 1;
-        if (q >= r && RP(q) > e + Mc / 2) {
+        if (q >= r && RP(q) > e + Mc - cut_window) {
           en = RP(q);  // cut at a row start
         } else {
           en = target;  // cut mid-row

@@ -56,9 +56,10 @@ int build_xslice(const void *row_ptr, int rp_bits, const int32_t *col, const voi
 // The stream is ordered (tile, chunk, CSR position): segment (s, c) is
 // [segoff[c·S + s], segoff[(c+1)·S + s]).  Each tile's stream starts at a
 // multiple of 8 (padding entries are written by gather, never read).
-// Chunks cut the CSR order at row starts where one lies in the back half of
-// the M window, else mid-row; a chunk owns the rows that start in it (≤ Rmax)
-// and a row cut by a chunk end is finished by a fix-up over `cont`.
+// Chunks cut the CSR order at the last row start in the back `cut_window`
+// entries of the M window, else mid-row (so every chunk but a range's last
+// holds ≥ M − cut_window nonzeros); a chunk owns the rows that start in it
+// (≤ Rmax) and a row cut by a chunk end is finished by a fix-up over `cont`.
 struct XtileHost {
   int S = 0;
   int64_t W = 0;
@@ -80,13 +81,14 @@ struct XtileHost {
 // 0 on success; LHPC_ERR_UNSUPPORTED when the layout does not fit its
 // index types (nnz + padding ≥ 2^31, S > 4096, or an oversized segment table).
 // piece_nnz: target nonzeros per gather workgroup (a multiple of 8 is used).
+// cut_window: see above, in (0, M] (M/2 cuts at any row start in the back half).
 // splits: ascending rows in (0, n_rows) at which a chunk must start (row
 // ranges that can be reduced separately, lhpc_spmv_range);
 // LHPC_ERR_INVALID_ARG otherwise.  iperm selects the reduce's index stream
 // (perm for false, iperm for true; only the selected one is built).
 int build_xtile(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_rows,
                 int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, int slot_bytes,
-                const int64_t *splits, int n_splits, bool iperm, XtileHost &out);
+                const int64_t *splits, int n_splits, bool iperm, int cut_window, XtileHost &out);
 
 // Wave-transposed run layout of the XTILE reduce's per-position streams (val,
 // iperm): chunk position i belongs to thread t = i / run (run = 64 B of

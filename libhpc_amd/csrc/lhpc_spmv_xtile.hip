@@ -586,9 +586,16 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   bool ip = p->nnz >= 32LL * cus * M;
   if (const char *env = std::getenv("LHPC_XTILE_IPERM")) ip = std::atoi(env) != 0;
   p->xt_p = ip ? 3 : 1;
+  // chunk cuts: at the last row start in the back M/32 of the window, else
+  // mid-row (the row's pieces meet in k_xtile_fixup).  Per-chunk costs are
+  // fixed, so full chunks matter on skewed rows: C4 has 19803 chunks when any
+  // row start in the back half is taken, 18454 with the back M/32 (C2: 18316
+  // either way); LHPC_XTILE_CUT overrides (entries, 1..M)
+  int cut = M / 32;
+  if (const char *env = std::getenv("LHPC_XTILE_CUT")) cut = std::min(M, std::max(1, std::atoi(env)));
   XtileHost xt;
   LHPC_TRY(build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, M, RMAX, piece, static_cast<int>(tsz),
-                       p->split_rows.data(), static_cast<int>(p->split_rows.size()), ip, xt));
+                       p->split_rows.data(), static_cast<int>(p->split_rows.size()), ip, cut, xt));
   p->kernel = LHPC_KERNEL_XTILE;
   p->rp64 = 0;
   p->S = xt.S;

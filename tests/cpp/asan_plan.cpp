@@ -65,13 +65,13 @@ Csr powerlaw(int64_t n, int64_t m, int64_t lmax, uint64_t seed) {
 
 // XTILE invariants: every CSR nonzero appears once in its chunk's segment
 // concatenation, with the column it had; chunks tile the CSR order.
-void check_xtile(const Csr &a, bool iperm, const std::vector<int64_t> &splits) {
+void check_xtile(const Csr &a, bool iperm, const std::vector<int64_t> &splits, int cut = 512) {
   const int64_t W = 4096;
   const int M = 1024, Rmax = 128;
   lhpc::XtileHost xt;
   const int rc = lhpc::build_xtile(a.rp.data(), 64, a.col.data(), a.n, a.m, W, M, Rmax, 3000, 4,
                                    splits.empty() ? nullptr : splits.data(), static_cast<int>(splits.size()), iperm,
-                                   xt);
+                                   cut, xt);
   CHECK(rc == 0);
   if (rc) return;
   const int64_t C = xt.n_chunks, S = xt.S;
@@ -173,6 +173,8 @@ int main() {
     check_xtile(u, ip, {});
     check_xtile(p, ip, {});
     check_xtile(p, ip, {1, 5000, 19999});
+    check_xtile(p, ip, {}, 32);
+    check_xtile(p, ip, {77}, 1024);
     check_xtile(e, ip, {});
   }
   for (int S : {1, 8, 64}) {
