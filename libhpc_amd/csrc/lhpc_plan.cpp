@@ -300,7 +300,10 @@ int xtile_transpose_runs(const XtileHost &o, const void *val, size_t tsz, int ru
   vbase.assign(vb.begin(), vb.end());
   const size_t total = static_cast<size_t>(vb[C] + tail);
   valt.reset(new unsigned char[total * tsz]());
-  if (o.iperm) ipt.reset(new uint16_t[total]());
+  if (o.iperm) {  // padding points at the reduce's zero slot M (x = 0 there)
+    ipt.reset(new uint16_t[total]);
+    std::fill(ipt.get(), ipt.get() + total, static_cast<uint16_t>(o.M));
+  }
   const int vw = static_cast<int>(16 / tsz);
   const unsigned char *vs = static_cast<const unsigned char *>(val);
 #pragma omp parallel for schedule(dynamic, 64)

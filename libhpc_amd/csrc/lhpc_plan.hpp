@@ -105,7 +105,8 @@ inline int64_t xtile_wave_pos(int64_t i, int run, int vw) {
 // Per-chunk region bases (vbase[c]: chunk c's positions start there, each
 // chunk padded to whole wave regions of 64·run positions; vbase[C] = total)
 // and the val (tsz bytes each) and, when o.iperm is set, iperm streams in
-// the wave-transposed layout; padding entries are 0.  Extra `tail` entries
+// the wave-transposed layout; val padding is 0, iperm padding is M (the
+// reduce keeps x = 0 in LDS slot M, so a padded position needs no mask).  Extra `tail` entries
 // of zero padding follow vbase[C].  LHPC_ERR_UNSUPPORTED if vbase[C] ≥ 2^31.
 int xtile_transpose_runs(const XtileHost &o, const void *val, size_t tsz, int run, int64_t tail,
                          std::vector<int32_t> &vbase, std::unique_ptr<unsigned char[]> &valt,

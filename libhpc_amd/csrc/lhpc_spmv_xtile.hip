@@ -323,26 +323,40 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
       const int rk = __builtin_amdgcn_mbcnt_hi(t[1], __builtin_amdgcn_mbcnt_lo(t[0], t[2]));
       const int f = (wv * NB + u) * kWave + lane;
       const int sv = base_ne[rk] + f;  // m > 0 ⇒ 0 ≤ rk < S; m = 0: base_ne[−1] (in LDS), unused
-      src[u] = f < m ? sv : total;
-      LHPC_DEVICE_CHECK(src[u] >= 0 && src[u] <= total);
+      if constexpr (IP)
+        src[u] = sv;  // past m: out-of-chunk or out-of-range data into never-read slots
+      else
+        src[u] = f < m ? sv : total;
+      LHPC_DEVICE_CHECK(IP || (src[u] >= 0 && src[u] <= total));
     }
   }
   // plain loads: the segment lines a neighbouring chunk shares must stay in
   // L2 (non-temporal xg/perm loads: 433 → 555 µs)
   if constexpr (IP) {
+    // buffer loads with 32-bit offsets (the plan keeps the xg stream < 2 GiB
+    // in this mode): a position past m loads whatever follows its segment, or
+    // 0 past the stream's end (out of range) — no select and no 64-bit
+    // address per load; those slots are never read (padded positions read
+    // the zero slot M).  Default cache policy: the lines two neighbouring
+    // chunks' segments share must stay in L2 (nt / sc0+nt / sc1+nt: C2
+    // 524 → 554 µs; sc0 523, sc1 527, sc0+sc1 527 µs; one tile with no shared
+    // lines: nt 354 → 331 µs, nt + 16-B LDS-DMA 306 µs — DESIGN.md §4)
+    const __amdgpu_buffer_rsrc_t xr_rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T *>(xg), 0, (total + 2) * static_cast<int>(sizeof(T)), 0x00020000);
     if constexpr (sizeof(T) == 4) {
       // LDS-DMA: each lane's xg element lands at the batch's base + 4·lane
       // (exactly the flat order), no VGPR destination
 #pragma unroll
       for (int u = 0; u < NB; ++u)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(xg + src[u]),
-                                         (__attribute__((address_space(3))) void *)(xs + (wv * NB + u) * kWave),
-                                         4, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            xr_rs, (__attribute__((address_space(3))) void *)(xs + (wv * NB + u) * kWave), 4,
+            src[u] * static_cast<int>(sizeof(T)), 0, 0, 0);
       load_ipv();
     } else {
       T xv[NB];
 #pragma unroll
-      for (int u = 0; u < NB; ++u) xv[u] = xg[src[u]];
+      for (int u = 0; u < NB; ++u)
+        xv[u] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(xr_rs, src[u] * 8, 0, 0));
 #pragma unroll
       for (int u = 0; u < NB; ++u) xs[(wv * NB + u) * kWave + lane] = xv[u];
       load_ipv();
@@ -374,6 +388,8 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
 #pragma unroll
     for (int j = 0; j < RUN; ++j) vv[j / VW][j % VW] = j < n ? vv[j / VW][j % VW] : T(0);
   }
+  if constexpr (IP)
+    if (tid == 0) xs[M] = T(0);  // the zero slot that iperm padding points at
   // the LDS-DMA of phase A is counted by vmcnt, which the barrier does not
   // wait for: drain it before any wave reads another wave's flat slots
   if constexpr (IP && sizeof(T) == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -393,17 +409,15 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   if constexpr (IP) {
     // gather the run's x from the flat array, then (after every thread has
     // read) the running sums below go back in the CSR (xt_slot) layout;
-    // unconditional reads (iperm past m is a valid slot), so all RUN
-    // ds_reads issue before the first wait; then x past m → 0
-    T gx[RUN];
+    // unconditional reads, so all RUN ds_reads issue before the first wait.
+    // A padded position's iperm is the zero slot M, so x past m is already
+    // 0 (a run wholly past m reads another region's iperm: n = 0, unused)
 #pragma unroll
     for (int j = 0; j < RUN; ++j) {
       const uint32_t w = ipv[j / 8][(j % 8) / 2];
       LHPC_DEVICE_CHECK(((j & 1) ? (w >> 16) : (w & 0xFFFFu)) < static_cast<uint32_t>(M + VW));
-      gx[j] = xs[static_cast<int>((j & 1) ? (w >> 16) : (w & 0xFFFFu))];
+      xq[j / VW][j % VW] = xs[static_cast<int>((j & 1) ? (w >> 16) : (w & 0xFFFFu))];
     }
-#pragma unroll
-    for (int j = 0; j < RUN; ++j) xq[j / VW][j % VW] = j < n ? gx[j] : T(0);
     __syncthreads();
   } else {
 #pragma unroll
@@ -585,6 +599,10 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   // 0.093 ms; W = 1: 0.626 against 0.611 ms; profiles/r01/explore_scaling_*)
   bool ip = p->nnz >= 32LL * cus * M;
   if (const char *env = std::getenv("LHPC_XTILE_IPERM")) ip = std::atoi(env) != 0;
+  // the iperm reduce addresses xg with 32-bit buffer offsets: stream + tile
+  // padding (≤ 8 per tile) + one piece of slack must stay below 2 GiB
+  const int64_t stream_max = p->nnz + 8 * ((p->n_cols + W - 1) / W) + 2 * M;
+  if (stream_max * static_cast<int64_t>(tsz) >= (int64_t{1} << 31)) ip = false;
   p->xt_p = ip ? 3 : 1;
   // chunk cuts: at the last row start in the back M/32 of the window, else
   // mid-row (the row's pieces meet in k_xtile_fixup).  Per-chunk costs are
