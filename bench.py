@@ -126,8 +126,13 @@ def main():
     # N > 1 over RCCL: the native lhpc_dist_* path (one RCCL communicator and
     # comm stream per process, created from rank 0's unique id); the
     # torch.distributed form serves the gloo rehearsal or LHPC_DIST_TORCH=1
-    native_dist = (world > 1 or force_native) and dist.get_backend() == "nccl" and \
-        os.environ.get("LHPC_DIST_TORCH", "0") != "1"
+    # LHPC_DIST_P2P=1: the y exchange by direct peer stores into every rank's
+    # registered y (lhpc_dist_p2p_*) instead of RCCL broadcasts; with the gloo
+    # backend (ranks sharing one GPU in a rehearsal) over an RCCL-free
+    # local communicator
+    p2p = os.environ.get("LHPC_DIST_P2P", "0") == "1"
+    native_dist = (world > 1 or force_native) and (
+        (dist.get_backend() == "nccl" and os.environ.get("LHPC_DIST_TORCH", "0") != "1") or p2p)
     wl = args.workload
     result = {}
     if wl in ("c1", "c2", "c3", "c4"):
@@ -157,7 +162,8 @@ def main():
             # interleaved blocks, K chunks per rank; chunk k is reduced into
             # the rank's rows of y and broadcast (in place, exact slices) to
             # every rank on the comm stream while chunk k+1 is reduced
-            comm = L.DistComm.from_torch(local)
+            comm = L.DistComm.from_torch(local) if dist.get_backend() == "nccl" else \
+                L.DistComm.local(world, rank, local)
             cuts = L.interleaved_cuts(rp, world, args.chunks)
             lrp, lc, lv = L.interleaved_local_csr(rp, col, val, cuts, world, args.chunks, rank)
             dplan = L.DistSpMVPlan(comm, n, n, args.chunks, cuts, lrp, lc, lv)
@@ -165,6 +171,8 @@ def main():
             plans = [L.SpMVPlan(lrp, lc, lv, n)]
             local_nnz, local_rows = int(lc.shape[0]), int(lrp.shape[0] - 1)
             y_full = torch.empty(n, dtype=xd.dtype, device=dev)
+            if p2p and world > 1:
+                comm.p2p_setup_torch(y_full)
 
             class _Native:
                 def step(self, xv):
@@ -272,8 +280,9 @@ def main():
                                  "c4": "BASELINE configs[3]: power-law CSR (1..1e4 nnz/row) fp32"}[wl],
                     "n_rows": n, "n_cols": n, "nnz": nnz, "kernel": kname, "slices": info["slices"],
                     "parallelism": f"row-block x{world}" + (
-                        f" (interleaved nnz-balanced, {args.chunks} chunks/rank) + native RCCL broadcast of y "
-                        "chunks (lhpc_dist_spmv) overlapped" if native_dist else
+                        f" (interleaved nnz-balanced, {args.chunks} chunks/rank) + "
+                        + ("direct xGMI peer stores of y chunks (lhpc_dist_p2p)" if p2p else
+                           "native RCCL broadcast of y chunks") + " (lhpc_dist_spmv) overlapped" if native_dist else
                         f" (interleaved nnz-balanced, {args.chunks} chunks/rank) + torch.distributed all_gather(y) "
                         "overlapped" if world > 1 else "")},
             achieved_GBps=alg_bytes / per_step / 1e9,

@@ -368,6 +368,30 @@ int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_comm *comm, 
 int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream);
 int lhpc_dist_spmv_plan_destroy(lhpc_dist_spmv_plan *d);
 /*
+ * Direct peer exchange of y (SURVEY §8e "Optimisation": every pair of
+ * MI355X in a node is connected by xGMI).  Each rank exports its y buffer
+ * (device, ≥ n_rows values, 4-byte multiple) as a blob of IPC handles, the
+ * launcher all-gathers the blobs (any channel, rank order) and every rank
+ * imports them.  lhpc_dist_spmv called with exactly that y then pushes each
+ * chunk's block into every peer's y with one kernel (stores over xGMI, all
+ * links at once) instead of the RCCL broadcasts; per call a READY flag
+ * ("my y may be overwritten": issued on the call's stream, so prior work on
+ * it that reads y is done) and a DONE flag ("my pushes have landed") go to
+ * every peer, and the comm stream waits for all peers' flags (bounded spin;
+ * a timeout sets lhpc_dist_p2p_status and fails the next call).  y must not
+ * be read by any stream other than the call's until the call completes.
+ * Without RCCL, lhpc_dist_comm_create_local gives a communicator for this
+ * exchange only (lhpc_dist_allreduce_sum_f64 / stencil7 need RCCL:
+ * LHPC_ERR_UNSUPPORTED).  Opt-in: the default exchange stays RCCL.
+ */
+#define LHPC_DIST_P2P_BLOB_BYTES 192
+int lhpc_dist_comm_create_local(lhpc_dist_comm **out, int nranks, int rank, int device);
+int lhpc_dist_p2p_export(lhpc_dist_comm *comm, void *y, int64_t bytes,
+                         unsigned char *blob_out /* LHPC_DIST_P2P_BLOB_BYTES */);
+int lhpc_dist_p2p_import(lhpc_dist_comm *comm,
+                         const unsigned char *blobs /* nranks × LHPC_DIST_P2P_BLOB_BYTES */);
+int lhpc_dist_p2p_status(const lhpc_dist_comm *comm);
+/*
  * One 7-point stencil step on this rank's z-slab (BASELINE config C5): u and
  * out are HPCHighDimensionFlatArray<3,float,ghost> buffers of logical
  * (nzl, ny, nx) on the device; the z ghost planes -1 and nzl of u are the

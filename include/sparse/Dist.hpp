@@ -7,6 +7,8 @@
 //   sparse::DistSpMVPlan<T>       RAII distributed plan (the rank's local CSR)
 //   sparse::spmv(plan, d_x, d_y, stream)          full y on every rank (device)
 //   sparse::dist_stencil7(comm, d_u, d_out, ...)  z-slab step with RCCL halo planes
+//   DistComm::local(nranks, rank, device), p2p_export(d_y, bytes) / p2p_import(blobs)
+//                                 opt-in direct xGMI peer exchange of y (lhpc_dist_p2p_*)
 // Non-zero status → std::system_error (include/lhpc_error.hpp).  The
 // reference has no multi-device code; the rank-0 unique id must
 // reach every rank through the launcher's own channel (MPI_Bcast, a file, …).
@@ -37,8 +39,29 @@ class DistComm {
   DistComm(const unique_id_t &id, int nranks, int rank, int device) : nranks_(nranks), rank_(rank) {
     lhpc::checkLhpc(lhpc_dist_comm_create(&comm_, id.data(), nranks, rank, device));
   }
+  // RCCL-free communicator: only the direct peer exchange of a registered y
+  struct local_t {};
+  DistComm(local_t, int nranks, int rank, int device) : nranks_(nranks), rank_(rank) {
+    lhpc::checkLhpc(lhpc_dist_comm_create_local(&comm_, nranks, rank, device));
+  }
+  static DistComm local(int nranks, int rank, int device) { return DistComm(local_t{}, nranks, rank, device); }
+  DistComm(DistComm &&o) noexcept : comm_(std::exchange(o.comm_, nullptr)), nranks_(o.nranks_), rank_(o.rank_) {}
   DistComm(const DistComm &) = delete;
   DistComm &operator=(const DistComm &) = delete;
+  using p2p_blob_t = std::array<unsigned char, LHPC_DIST_P2P_BLOB_BYTES>;
+  // this rank's y window (device, n_rows values) as a blob for every rank;
+  // all-gather the blobs (rank order) through the launcher, then p2p_import:
+  // sparse::spmv(plan, d_x, d_y) with that d_y exchanges by peer stores
+  p2p_blob_t p2p_export(void *d_y, std::int64_t bytes) {
+    p2p_blob_t b{};
+    lhpc::checkLhpc(lhpc_dist_p2p_export(comm_, d_y, bytes, b.data()));
+    return b;
+  }
+  void p2p_import(const std::vector<p2p_blob_t> &blobs) {
+    std::vector<unsigned char> flat;
+    for (const auto &b : blobs) flat.insert(flat.end(), b.begin(), b.end());
+    lhpc::checkLhpc(lhpc_dist_p2p_import(comm_, flat.data()));
+  }
   ~DistComm() {
     if (comm_) lhpc_dist_comm_destroy(comm_);
   }

@@ -62,7 +62,8 @@ ABI_SYMBOLS = (
     "lhpc_spmv_plan_create_split", "lhpc_spmv_stage", "lhpc_spmv_range",
     "lhpc_dist_get_unique_id", "lhpc_dist_comm_create", "lhpc_dist_comm_info", "lhpc_dist_comm_destroy",
     "lhpc_dist_allreduce_sum_f64", "lhpc_dist_spmv_plan_create", "lhpc_dist_spmv",
-    "lhpc_dist_spmv_plan_destroy", "lhpc_dist_stencil7_f32",
+    "lhpc_dist_spmv_plan_destroy", "lhpc_dist_stencil7_f32", "lhpc_dist_comm_create_local",
+    "lhpc_dist_p2p_export", "lhpc_dist_p2p_import", "lhpc_dist_p2p_status",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -157,6 +158,10 @@ _sig("lhpc_dist_spmv_plan_create", _i, C.POINTER(_p), _p, _i, _i64, _i64, _i, _p
 _sig("lhpc_dist_spmv", _i, _p, _p, _p, _p)
 _sig("lhpc_dist_spmv_plan_destroy", _i, _p)
 _sig("lhpc_dist_stencil7_f32", _i, _p, _p, _p, _i64, _i64, _i64, _i64, _f, _f, _p)
+_sig("lhpc_dist_comm_create_local", _i, C.POINTER(_p), _i, _i, _i)
+_sig("lhpc_dist_p2p_export", _i, _p, _p, _i64, _p)
+_sig("lhpc_dist_p2p_import", _i, _p, _p)
+_sig("lhpc_dist_p2p_status", _i, _p)
 
 
 class LhpcError(RuntimeError):
@@ -641,6 +646,7 @@ def gen_laplacian_2d(nx: int, ny: int, dtype=F64, shift: float = 0.0):
 
 # ------------------------------------------------------------ multi-GPU (RCCL)
 DIST_UNIQUE_ID_BYTES = 128
+DIST_P2P_BLOB_BYTES = 192
 
 
 def dist_unique_id() -> bytes:
@@ -662,6 +668,49 @@ class DistComm:
         _check(lib.lhpc_dist_comm_create(C.byref(self._h), uid, int(nranks), int(rank), int(device)),
                "lhpc_dist_comm_create")
         self.nranks, self.rank, self.device = int(nranks), int(rank), int(device)
+
+    @classmethod
+    def local(cls, nranks: int, rank: int, device: int):
+        """A communicator without RCCL (lhpc_dist_comm_create_local): only the
+        direct peer exchange of a registered y window (p2p_setup)."""
+        self = cls.__new__(cls)
+        self._h = _p()
+        _check(lib.lhpc_dist_comm_create_local(C.byref(self._h), int(nranks), int(rank), int(device)),
+               "lhpc_dist_comm_create_local")
+        self.nranks, self.rank, self.device = int(nranks), int(rank), int(device)
+        return self
+
+    def p2p_export(self, y) -> bytes:
+        """This rank's blob (IPC handles) for the y window (a device tensor)."""
+        blob = (C.c_ubyte * DIST_P2P_BLOB_BYTES)()
+        _check(lib.lhpc_dist_p2p_export(self._h, y.data_ptr(), y.numel() * y.element_size(), blob),
+               "lhpc_dist_p2p_export")
+        self._p2p_y = y  # the window must outlive the mapping
+        return bytes(blob)
+
+    def p2p_import(self, blobs):
+        """Every rank's blob, in rank order."""
+        if len(blobs) != self.nranks:
+            raise ValueError("one blob per rank")
+        buf = (C.c_ubyte * (DIST_P2P_BLOB_BYTES * self.nranks)).from_buffer_copy(b"".join(blobs))
+        _check(lib.lhpc_dist_p2p_import(self._h, buf), "lhpc_dist_p2p_import")
+
+    def p2p_setup_torch(self, y, group=None):
+        """Export y, all-gather the blobs over an initialised torch.distributed
+        group (any backend), import them: lhpc_dist_spmv(…, y) then exchanges
+        by direct peer stores."""
+        import torch
+        import torch.distributed as dist
+        mine = np.frombuffer(self.p2p_export(y), dtype=np.uint8).copy()
+        t = torch.from_numpy(mine)
+        if dist.get_backend(group) == "nccl":
+            t = t.to(torch.device("cuda", self.device))
+        parts = [torch.empty_like(t) for _ in range(self.nranks)]
+        dist.all_gather(parts, t, group=group)
+        self.p2p_import([p.cpu().numpy().tobytes() for p in parts])
+
+    def p2p_status(self) -> int:
+        return int(lib.lhpc_dist_p2p_status(self._h))
 
     @classmethod
     def from_torch(cls, device: int, group=None):

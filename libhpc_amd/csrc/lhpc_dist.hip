@@ -17,6 +17,14 @@
 //          k·nranks + r) fills every rank's y — exact slices, no padding —
 //          while the compute stream reduces chunk k+1.  y is then the next x
 //          on every rank.
+//          Opt-in direct peer exchange (SURVEY §8e "Optimisation"): with a
+//          registered y window (lhpc_dist_p2p_export/_import: IPC handles of
+//          every rank's y), chunk k's block is pushed by one kernel straight
+//          into every peer's y over xGMI instead of the broadcasts; per call a
+//          READY flag (this rank's y may be overwritten) and a DONE flag
+//          (this rank's pushes have landed) go to every peer, and the comm
+//          stream waits for all peers' flags with a bounded spin.  Needs no
+//          RCCL communicator (lhpc_dist_comm_create_local).
 //   stencil z-slabs with one halo plane per side: ncclSend/ncclRecv to the
 //          z neighbours on the comm stream while the interior planes are
 //          computed; the two boundary planes after the exchange.
@@ -40,9 +48,20 @@
 static_assert(sizeof(ncclUniqueId) == LHPC_DIST_UNIQUE_ID_BYTES, "ncclUniqueId is 128 bytes");
 
 struct lhpc_dist_comm {
-  ncclComm_t comm = nullptr;
+  ncclComm_t comm = nullptr;  // null for a local (P2P-only) communicator
   int nranks = 1, rank = 0, device = 0;
   hipStream_t s_comm = nullptr;
+  // P2P window: this rank's y (caller-owned) and flags [READY(nranks) |
+  // DONE(nranks)] (owned, uncached device memory), the peers' mapped views
+  void *p2p_buf = nullptr;
+  size_t p2p_bytes = 0;
+  uint32_t *flags = nullptr;
+  bool p2p_ready = false;
+  std::vector<void *> peer_base, peer_flags_base;  // hipIpcOpenMemHandle results (closed at destroy)
+  void **d_peer_buf = nullptr;                     // [nranks] device arrays of peer pointers (self: own)
+  uint32_t **d_peer_flags = nullptr;
+  uint32_t *h_status = nullptr;                    // host-mapped: bit 0 = a flag wait timed out
+  uint32_t epoch = 0;
 };
 
 struct lhpc_dist_spmv_plan {
@@ -55,11 +74,114 @@ struct lhpc_dist_spmv_plan {
   std::vector<lhpc_spmv_plan *> block_plan; // otherwise one plan per non-empty block
   std::vector<hipEvent_t> ev;               // [K] chunk k reduced
   hipEvent_t done = nullptr;                // last broadcast issued on the comm stream
+  hipEvent_t ev_p2p = nullptr;              // P2P: READY signalled on the compute stream
 };
 
 namespace {
 
 ncclDataType_t nccl_dt(int dtype) { return dtype == LHPC_F64 ? ncclFloat64 : ncclFloat32; }
+
+// ---- P2P window kernels
+// flag store into every peer's flag array at `slot` (READY: rank, DONE:
+// nranks + rank), release at system scope: everything this stream did
+// before is visible to the peer first
+__global__ void k_p2p_signal(uint32_t *const *peer_flags, int slot, uint32_t e, int nranks, int self) {
+  const int p = threadIdx.x;
+  if (p < nranks && p != self) __hip_atomic_store(peer_flags[p] + slot, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// wait until every peer's flag at base + p reached epoch e; bounded (~8 s):
+// a missing peer sets status bit 0 instead of hanging the device
+__global__ void k_p2p_wait(const uint32_t *flags, int base, uint32_t e, int nranks, int self, uint32_t *status) {
+  const int p = threadIdx.x;
+  if (p >= nranks || p == self) return;
+  for (uint32_t spins = 0;; ++spins) {
+    const uint32_t f = __hip_atomic_load(flags + base + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (static_cast<int32_t>(f - e) >= 0) return;
+    if (spins > (1u << 21)) {
+      __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(127);
+  }
+}
+// bytes [o0, o1) of this rank's y into the same bytes of every peer's y
+// (offsets are multiples of 4; 16-B stores where both sides are aligned —
+// every y has the same alignment); blockIdx.y = peer
+__global__ __launch_bounds__(256) void k_p2p_push(void *const *peer_buf, const unsigned char *y, int64_t o0,
+                                                  int64_t o1, int self) {
+  const int p = static_cast<int>(blockIdx.y) + (static_cast<int>(blockIdx.y) >= self ? 1 : 0);
+  unsigned char *dst = static_cast<unsigned char *>(peer_buf[p]);
+  int64_t a0 = (o0 + 15) & ~int64_t{15}, a1 = o1 & ~int64_t{15};
+  if (a0 > a1) a0 = a1 = o1;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x, T = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = o0 + 4 * t; i < a0; i += 4 * T)  // head words
+    *reinterpret_cast<uint32_t *>(dst + i) = *reinterpret_cast<const uint32_t *>(y + i);
+  for (int64_t i = a0 + 16 * t; i < a1; i += 16 * T)
+    *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(y + i);
+  for (int64_t i = (a1 > a0 ? a1 : o1) + 4 * t; i < o1; i += 4 * T)  // tail words
+    *reinterpret_cast<uint32_t *>(dst + i) = *reinterpret_cast<const uint32_t *>(y + i);
+  __threadfence_system();
+}
+
+struct P2pBlob {  // LHPC_DIST_P2P_BLOB_BYTES per rank
+  hipIpcMemHandle_t buf, flags;
+  int64_t offset;  // y − its allocation's base
+  int64_t bytes;
+  uint64_t magic;
+};
+static_assert(sizeof(P2pBlob) <= LHPC_DIST_P2P_BLOB_BYTES, "blob size");
+constexpr uint64_t kP2pMagic = 0x6c687063705032ull;  // "lhpcP2"
+
+void p2p_release(lhpc_dist_comm *c) {
+  for (void *b : c->peer_base)
+    if (b) (void)hipIpcCloseMemHandle(b);
+  for (void *b : c->peer_flags_base)
+    if (b) (void)hipIpcCloseMemHandle(b);
+  c->peer_base.clear();
+  c->peer_flags_base.clear();
+  if (c->d_peer_buf) (void)hipFree(c->d_peer_buf);
+  if (c->d_peer_flags) (void)hipFree(c->d_peer_flags);
+  if (c->flags) (void)hipFree(c->flags);
+  if (c->h_status) (void)hipHostFree(c->h_status);
+  c->d_peer_buf = nullptr;
+  c->d_peer_flags = nullptr;
+  c->flags = nullptr;
+  c->h_status = nullptr;
+  c->p2p_buf = nullptr;
+  c->p2p_ready = false;
+}
+
+// the P2P exchange of one call (see the header comment); s = compute stream
+int p2p_exchange_begin(lhpc_dist_comm *c, hipStream_t s, hipEvent_t ev) {
+  ++c->epoch;
+  if (c->epoch == 0) c->epoch = 1;
+  if (*c->h_status) return LHPC_ERR_INTERNAL;  // an earlier flag wait timed out
+  hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(64), 0, s, c->d_peer_flags, c->rank, c->epoch, c->nranks, c->rank);
+  LHPC_HIP_TRY(hipGetLastError());
+  LHPC_HIP_TRY(hipEventRecord(ev, s));
+  LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, ev, 0));
+  hipLaunchKernelGGL(k_p2p_wait, dim3(1), dim3(64), 0, c->s_comm, c->flags, 0, c->epoch, c->nranks, c->rank,
+                     c->h_status);
+  return static_cast<int>(hipGetLastError());
+}
+
+int p2p_push(lhpc_dist_comm *c, int64_t o0, int64_t o1) {
+  if (o1 <= o0 || c->nranks < 2) return LHPC_OK;
+  const int64_t vec = (o1 - o0) / 16 + 1;
+  const unsigned bx = static_cast<unsigned>(std::min<int64_t>(64, (vec + 255) / 256));
+  hipLaunchKernelGGL(k_p2p_push, dim3(bx, static_cast<unsigned>(c->nranks - 1)), dim3(256), 0, c->s_comm,
+                     c->d_peer_buf, static_cast<const unsigned char *>(c->p2p_buf), o0, o1, c->rank);
+  return static_cast<int>(hipGetLastError());
+}
+
+int p2p_exchange_end(lhpc_dist_comm *c) {
+  hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(64), 0, c->s_comm, c->d_peer_flags, c->nranks + c->rank, c->epoch,
+                     c->nranks, c->rank);
+  LHPC_HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_p2p_wait, dim3(1), dim3(64), 0, c->s_comm, c->flags, c->nranks, c->epoch, c->nranks, c->rank,
+                     c->h_status);
+  return static_cast<int>(hipGetLastError());
+}
 
 void destroy_spmv(lhpc_dist_spmv_plan *d) {
   if (!d) return;
@@ -70,6 +192,7 @@ void destroy_spmv(lhpc_dist_spmv_plan *d) {
   for (hipEvent_t e : d->ev)
     if (e) (void)hipEventDestroy(e);
   if (d->done) (void)hipEventDestroy(d->done);
+  if (d->ev_p2p) (void)hipEventDestroy(d->ev_p2p);
   delete d;
 }
 
@@ -130,10 +253,96 @@ extern "C" int lhpc_dist_comm_create(lhpc_dist_comm **out, const unsigned char *
   return LHPC_OK;
 }
 
+extern "C" int lhpc_dist_comm_create_local(lhpc_dist_comm **out, int nranks, int rank, int device) {
+  if (!out || nranks < 1 || rank < 0 || rank >= nranks || device < 0 || nranks > 64) return LHPC_ERR_INVALID_ARG;
+  *out = nullptr;
+  LHPC_HIP_TRY(hipSetDevice(device));
+  auto *c = new (std::nothrow) lhpc_dist_comm();
+  if (!c) return LHPC_ERR_ALLOC;
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  const hipError_t he = hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking);
+  if (he != hipSuccess) {
+    delete c;
+    return static_cast<int>(he);
+  }
+  *out = c;
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_p2p_export(lhpc_dist_comm *c, void *y, int64_t bytes, unsigned char *blob_out) {
+  if (!c || !y || bytes <= 0 || bytes % 4 || !blob_out || c->nranks > 64) return LHPC_ERR_INVALID_ARG;
+  lhpc::RocTxRange rx("lhpc_dist_p2p_export");
+  LHPC_HIP_TRY(hipSetDevice(c->device));
+  p2p_release(c);
+  P2pBlob b{};
+  void *base = nullptr;
+  size_t size = 0;
+  LHPC_HIP_TRY(hipMemGetAddressRange(reinterpret_cast<hipDeviceptr_t *>(&base), &size, y));
+  if (static_cast<unsigned char *>(y) + bytes > static_cast<unsigned char *>(base) + size) return LHPC_ERR_INVALID_ARG;
+  LHPC_HIP_TRY(hipIpcGetMemHandle(&b.buf, base));
+  b.offset = static_cast<unsigned char *>(y) - static_cast<unsigned char *>(base);
+  b.bytes = bytes;
+  b.magic = kP2pMagic;
+  // flags: uncached, so a peer's store is seen by the next poll; zeroed
+  LHPC_HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void **>(&c->flags), 2 * 64 * sizeof(uint32_t),
+                                     hipDeviceMallocUncached));
+  LHPC_HIP_TRY(hipMemset(c->flags, 0, 2 * 64 * sizeof(uint32_t)));
+  LHPC_HIP_TRY(hipIpcGetMemHandle(&b.flags, c->flags));
+  LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_status), sizeof(uint32_t), hipHostMallocMapped));
+  *c->h_status = 0;
+  c->p2p_buf = y;
+  c->p2p_bytes = static_cast<size_t>(bytes);
+  c->epoch = 0;
+  std::memset(blob_out, 0, LHPC_DIST_P2P_BLOB_BYTES);
+  std::memcpy(blob_out, &b, sizeof(b));
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_p2p_import(lhpc_dist_comm *c, const unsigned char *blobs) {
+  if (!c || !blobs || !c->p2p_buf || !c->flags) return LHPC_ERR_INVALID_ARG;
+  lhpc::RocTxRange rx("lhpc_dist_p2p_import");
+  LHPC_HIP_TRY(hipSetDevice(c->device));
+  const int nr = c->nranks;
+  std::vector<void *> bufs(static_cast<size_t>(nr), nullptr), flg(static_cast<size_t>(nr), nullptr);
+  c->peer_base.assign(static_cast<size_t>(nr), nullptr);
+  c->peer_flags_base.assign(static_cast<size_t>(nr), nullptr);
+  for (int r = 0; r < nr; ++r) {
+    P2pBlob b;
+    std::memcpy(&b, blobs + static_cast<size_t>(r) * LHPC_DIST_P2P_BLOB_BYTES, sizeof(b));
+    if (b.magic != kP2pMagic || static_cast<size_t>(b.bytes) != c->p2p_bytes) return LHPC_ERR_INVALID_ARG;
+    if (r == c->rank) {
+      bufs[r] = c->p2p_buf;
+      flg[r] = c->flags;
+      continue;
+    }
+    void *pb = nullptr, *pf = nullptr;
+    LHPC_HIP_TRY(hipIpcOpenMemHandle(&pb, b.buf, hipIpcMemLazyEnablePeerAccess));
+    c->peer_base[r] = pb;
+    LHPC_HIP_TRY(hipIpcOpenMemHandle(&pf, b.flags, hipIpcMemLazyEnablePeerAccess));
+    c->peer_flags_base[r] = pf;
+    bufs[r] = static_cast<unsigned char *>(pb) + b.offset;
+    flg[r] = pf;
+  }
+  LHPC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_peer_buf), nr * sizeof(void *)));
+  LHPC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_peer_flags), nr * sizeof(void *)));
+  LHPC_HIP_TRY(hipMemcpy(c->d_peer_buf, bufs.data(), nr * sizeof(void *), hipMemcpyHostToDevice));
+  LHPC_HIP_TRY(hipMemcpy(c->d_peer_flags, flg.data(), nr * sizeof(void *), hipMemcpyHostToDevice));
+  c->p2p_ready = true;
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_p2p_status(const lhpc_dist_comm *c) {
+  if (!c) return LHPC_ERR_INVALID_ARG;
+  return c->h_status && *c->h_status ? LHPC_ERR_INTERNAL : LHPC_OK;
+}
+
 extern "C" int lhpc_dist_comm_destroy(lhpc_dist_comm *c) {
   if (!c) return LHPC_OK;
   (void)hipSetDevice(c->device);
   if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
+  p2p_release(c);
   int st = LHPC_OK;
   if (c->comm) {
     const ncclResult_t r = ncclCommDestroy(c->comm);
@@ -155,6 +364,7 @@ extern "C" int lhpc_dist_comm_info(const lhpc_dist_comm *c, int *nranks, int *ra
 extern "C" int lhpc_dist_allreduce_sum_f64(lhpc_dist_comm *c, double *buf, int64_t count, void *stream) {
   if (!c || (count > 0 && !buf) || count < 0) return LHPC_ERR_INVALID_ARG;
   if (count == 0) return LHPC_OK;
+  if (!c->comm) return LHPC_ERR_UNSUPPORTED;  // local (P2P-only) communicator
   LHPC_HIP_TRY(hipSetDevice(c->device));
   LHPC_NCCL_TRY(ncclAllReduce(buf, buf, static_cast<size_t>(count), ncclFloat64, ncclSum, c->comm,
                               static_cast<hipStream_t>(stream)));
@@ -230,6 +440,7 @@ extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_c
     for (auto &e : d->ev)
       if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->done, hipEventDisableTiming));
+    if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->ev_p2p, hipEventDisableTiming));
   }
   if (st != LHPC_OK) {
     destroy_spmv(d);
@@ -241,11 +452,15 @@ extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_c
 
 extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream) {
   if (!d || (d->n_cols > 0 && !x) || (d->n_rows > 0 && !y) || (x == y && d->n_rows > 0)) return LHPC_ERR_INVALID_ARG;
-  const lhpc_dist_comm *c = d->comm;
+  lhpc_dist_comm *c = d->comm;
   lhpc::RocTxRange rx("lhpc_dist_spmv");
   LHPC_HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   const size_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
+  // the y exchange: direct peer stores into the registered window, else RCCL
+  const bool p2p = c->nranks > 1 && c->p2p_ready && y == c->p2p_buf && c->p2p_bytes >= d->n_rows * tsz;
+  if (c->nranks > 1 && !p2p && !c->comm) return LHPC_ERR_INVALID_ARG;  // local comm: y must be the window
+  if (p2p) LHPC_TRY(p2p_exchange_begin(c, s, d->ev_p2p));
   if (d->split) LHPC_TRY(lhpc_spmv_stage(d->split, x, stream));
   for (int k = 0; k < d->K; ++k) {
     const int64_t b = static_cast<int64_t>(k) * c->nranks + c->rank;
@@ -260,10 +475,14 @@ extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, vo
       LHPC_HIP_TRY(hipEventRecord(d->ev[k], s));
       LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, d->ev[k], 0));
       lhpc::RocTxRange rb("lhpc_dist_spmv: y chunk exchange");
-      LHPC_TRY(broadcast_chunk(d, k, y, c->s_comm));
+      if (p2p)
+        LHPC_TRY(p2p_push(c, d->cuts[b] * static_cast<int64_t>(tsz), d->cuts[b + 1] * static_cast<int64_t>(tsz)));
+      else
+        LHPC_TRY(broadcast_chunk(d, k, y, c->s_comm));
     }
   }
   if (c->nranks > 1) {
+    if (p2p) LHPC_TRY(p2p_exchange_end(c));
     LHPC_HIP_TRY(hipEventRecord(d->done, c->s_comm));
     LHPC_HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
   }
@@ -278,6 +497,7 @@ extern "C" int lhpc_dist_spmv_plan_destroy(lhpc_dist_spmv_plan *d) {
 extern "C" int lhpc_dist_stencil7_f32(lhpc_dist_comm *c, float *u, float *out, int64_t nzl, int64_t ny,
                                       int64_t nx, int64_t ghost, float c0, float c1, void *stream) {
   if (!c || !u || !out || nzl < 1 || ny < 0 || nx < 0 || ghost < 1) return LHPC_ERR_INVALID_ARG;
+  if (!c->comm && c->nranks > 1) return LHPC_ERR_UNSUPPORTED;  // halos travel over RCCL
   LHPC_HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t P = (ny + 2 * ghost) * (nx + 2 * ghost);  // padded plane

@@ -168,6 +168,26 @@ int gpu_mode() {
     if (!hip_ok(hipMemcpy(b4, dd, sizeof(b4), hipMemcpyDeviceToHost))) return fail("hipMemcpy");
     for (int i = 0; i < 4; ++i)
       if (b4[i] != h4[i]) return fail("allreduce world 1");
+    // RCCL-free local communicator with a registered y window (world 1:
+    // no peers; the P2P calls and the dist plan must still work through it)
+    {
+      auto lc = sparse::DistComm::local(1, 0, 0);
+      const auto blob = lc.p2p_export(dy, static_cast<std::int64_t>(sizeof(float) * n));
+      lc.p2p_import({blob});
+      sparse::DistSpMVPlan<float> lplan(lc, n, m, K, cuts, L);
+      if (!hip_ok(hipMemset(dy, 0xFF, sizeof(float) * n))) return fail("hipMemset");
+      sparse::spmv(lplan, dx, dy);
+      if (!hip_ok(hipMemcpy(yd.data(), dy, sizeof(float) * n, hipMemcpyDeviceToHost))) return fail("hipMemcpy");
+      for (std::int64_t i = 0; i < n; ++i)
+        if (yd[std::size_t(i)] != y(i)) return fail("local-comm dist spmv mismatch");
+      bool threw = false;
+      try {
+        lc.allreduce_sum(dd, 4);  // needs RCCL
+      } catch (const std::system_error &) {
+        threw = true;
+      }
+      if (!threw) return fail("allreduce on a local communicator must fail");
+    }
     if (!hip_ok(hipFree(dx)) || !hip_ok(hipFree(dy)) || !hip_ok(hipFree(dd))) return fail("hipFree");
   }
   std::printf("cpp api gpu: ok (spmv kernel %d)\n", plan.info().kernel);

@@ -80,3 +80,34 @@ def test_dist_stencil7_world1_matches_single_domain(lhpc, gpu, comm, nz, ny, nx)
     od = torch.from_numpy(out0.copy()).to(gpu)
     comm.stencil7(ud, od, nz, ny, nx, 1, -6.0, 1.0)
     assert np.array_equal(od.cpu().numpy(), want)
+
+
+def test_dist_spmv_p2p_two_ranks_one_gpu(lhpc, gpu):
+    """The direct peer exchange (lhpc_dist_p2p_export/_import, READY/DONE
+    flags, push kernel) with two processes on the box's one GPU: IPC-mapped
+    windows, RCCL-free local communicators, blobs over gloo.  Both ranks'
+    assembled y equal the oracle bit for bit (dyadic), three calls in a row
+    (epochs), fp32 XTILE row-range and fp64 per-block local plans.  (On one
+    GPU the pushes are device-local; over xGMI they are the same stores.)"""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT="29631")
+    procs = [subprocess.Popen([sys.executable, os.path.join(root, "tests", "p2p_two_ranks.py")],
+                              env=dict(env, RANK=str(r), LOCAL_RANK="0"), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=240)
+            assert p.returncode == 0, e[-3000:]
+            outs.append(json.loads(o.strip().splitlines()[-1]))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for o in outs:
+        assert all(o["ok"]) and len(o["ok"]) == 6, o
+        assert all(s == 0 for s in o["status"]), o
