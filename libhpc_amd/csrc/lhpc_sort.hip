@@ -230,6 +230,19 @@ struct DevBuf {
   }
 };
 
+// Staging buffers of the host-buffer entry points: plain hipMalloc (not the
+// stream-ordered pool) and synchronous copies.  Asynchronous pageable copies
+// into pool memory on the null stream were seen to land after the kernel
+// that read them (rows read as 0 in 4 of 25 runs of tests/cpp
+// test_sparse_grid gpu, the 4-entry Matrix Market case).
+struct HostStage {
+  void *p = nullptr;
+  ~HostStage() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 16); }
+};
+
 // resident downsweep blocks on this device (CUs × blocks per CU), cached per kernel
 template <typename K, bool HAS_V, int IPT>
 int64_t sort_grid_cap() {
@@ -502,16 +515,16 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
   RocTxRange rx("lhpc_radix_sort");
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (on_device) return radix_sort_dev<K, HAS_V, IPT>(keys, vals, n, begin_bit, end_bit, s);
-  DevBuf dk, dv;
-  LHPC_HIP_TRY(dk.alloc(static_cast<size_t>(n) * sizeof(K), s));
-  if (HAS_V) LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(n) * 4, s));
-  LHPC_HIP_TRY(hipMemcpyAsync(dk.p, keys, static_cast<size_t>(n) * sizeof(K), hipMemcpyHostToDevice, s));
-  if (HAS_V) LHPC_HIP_TRY(hipMemcpyAsync(dv.p, vals, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice, s));
+  HostStage dk, dv;
+  LHPC_HIP_TRY(dk.alloc(static_cast<size_t>(n) * sizeof(K)));
+  if (HAS_V) LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(n) * 4));
+  LHPC_HIP_TRY(hipMemcpy(dk.p, keys, static_cast<size_t>(n) * sizeof(K), hipMemcpyHostToDevice));
+  if (HAS_V) LHPC_HIP_TRY(hipMemcpy(dv.p, vals, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice));
   LHPC_TRY((radix_sort_dev<K, HAS_V, IPT>(static_cast<K *>(dk.p), static_cast<uint32_t *>(dv.p), n, begin_bit,
                                           end_bit, s)));
-  LHPC_HIP_TRY(hipMemcpyAsync(keys, dk.p, static_cast<size_t>(n) * sizeof(K), hipMemcpyDeviceToHost, s));
-  if (HAS_V) LHPC_HIP_TRY(hipMemcpyAsync(vals, dv.p, static_cast<size_t>(n) * 4, hipMemcpyDeviceToHost, s));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
+  LHPC_HIP_TRY(hipMemcpy(keys, dk.p, static_cast<size_t>(n) * sizeof(K), hipMemcpyDeviceToHost));
+  if (HAS_V) LHPC_HIP_TRY(hipMemcpy(vals, dv.p, static_cast<size_t>(n) * 4, hipMemcpyDeviceToHost));
   return LHPC_OK;
 }
 }  // namespace
@@ -551,27 +564,26 @@ extern "C" int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_
   };
   if (on_device) return run(rows, cols, vals, row_ptr, col_out, val_out, nnz_out);
   const size_t rpb = static_cast<size_t>(n_rows + 1) * (row_ptr_bits / 8);
-  DevBuf dr, dc, dv, drp, dco, dvo;
-  LHPC_HIP_TRY(dr.alloc(static_cast<size_t>(nnz) * 4, s));
-  LHPC_HIP_TRY(dc.alloc(static_cast<size_t>(nnz) * 4, s));
-  LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(nnz) * vb, s));
-  LHPC_HIP_TRY(drp.alloc(rpb, s));
-  LHPC_HIP_TRY(dco.alloc(static_cast<size_t>(nnz) * 4, s));
-  LHPC_HIP_TRY(dvo.alloc(static_cast<size_t>(nnz) * vb, s));
+  HostStage dr, dc, dv, drp, dco, dvo;
+  LHPC_HIP_TRY(dr.alloc(static_cast<size_t>(nnz) * 4));
+  LHPC_HIP_TRY(dc.alloc(static_cast<size_t>(nnz) * 4));
+  LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(nnz) * vb));
+  LHPC_HIP_TRY(drp.alloc(rpb));
+  LHPC_HIP_TRY(dco.alloc(static_cast<size_t>(nnz) * 4));
+  LHPC_HIP_TRY(dvo.alloc(static_cast<size_t>(nnz) * vb));
   if (nnz > 0) {
-    LHPC_HIP_TRY(hipMemcpyAsync(dr.p, rows, static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice, s));
-    LHPC_HIP_TRY(hipMemcpyAsync(dc.p, cols, static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice, s));
-    LHPC_HIP_TRY(hipMemcpyAsync(dv.p, vals, static_cast<size_t>(nnz) * vb, hipMemcpyHostToDevice, s));
+    LHPC_HIP_TRY(hipMemcpy(dr.p, rows, static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice));
+    LHPC_HIP_TRY(hipMemcpy(dc.p, cols, static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice));
+    LHPC_HIP_TRY(hipMemcpy(dv.p, vals, static_cast<size_t>(nnz) * vb, hipMemcpyHostToDevice));
   }
   int64_t un = 0;
   LHPC_TRY(run(static_cast<int32_t *>(dr.p), static_cast<int32_t *>(dc.p), dv.p, drp.p,
-               static_cast<int32_t *>(dco.p), dvo.p, &un));
-  LHPC_HIP_TRY(hipMemcpyAsync(row_ptr, drp.p, rpb, hipMemcpyDeviceToHost, s));
+               static_cast<int32_t *>(dco.p), dvo.p, &un));  // ends with a stream synchronize
+  LHPC_HIP_TRY(hipMemcpy(row_ptr, drp.p, rpb, hipMemcpyDeviceToHost));
   if (un > 0) {
-    LHPC_HIP_TRY(hipMemcpyAsync(col_out, dco.p, static_cast<size_t>(un) * 4, hipMemcpyDeviceToHost, s));
-    LHPC_HIP_TRY(hipMemcpyAsync(val_out, dvo.p, static_cast<size_t>(un) * vb, hipMemcpyDeviceToHost, s));
+    LHPC_HIP_TRY(hipMemcpy(col_out, dco.p, static_cast<size_t>(un) * 4, hipMemcpyDeviceToHost));
+    LHPC_HIP_TRY(hipMemcpy(val_out, dvo.p, static_cast<size_t>(un) * vb, hipMemcpyDeviceToHost));
   }
-  LHPC_HIP_TRY(hipStreamSynchronize(s));
   if (nnz_out) *nnz_out = un;
   return LHPC_OK;
 }

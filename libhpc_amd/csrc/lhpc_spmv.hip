@@ -291,17 +291,17 @@ extern "C" int lhpc_spmv(lhpc_spmv_plan *p, const void *x, void *y, int on_devic
       LHPC_TRY(dmalloc(&p->d_xstage, static_cast<size_t>(p->n_cols) * tsz, p->bytes));
       LHPC_TRY(dmalloc(&p->d_ystage, static_cast<size_t>(p->n_rows) * tsz, p->bytes));
     }
-    LHPC_HIP_TRY(hipMemcpyAsync(p->d_xstage, x, static_cast<size_t>(p->n_cols) * tsz,
-                                hipMemcpyHostToDevice, s));
+    // host buffers: synchronous copies (see lhpc_sort.hip HostStage); the
+    // staging buffers are only touched by host-buffer calls, which end synced
+    LHPC_HIP_TRY(hipMemcpy(p->d_xstage, x, static_cast<size_t>(p->n_cols) * tsz, hipMemcpyHostToDevice));
     dx = p->d_xstage;
     dy = p->d_ystage;
   }
   const int st = launch(p, dx, dy, s);
   if (st != LHPC_OK) return st;
   if (!on_device) {
-    LHPC_HIP_TRY(hipMemcpyAsync(y, p->d_ystage, static_cast<size_t>(p->n_rows) * tsz,
-                                hipMemcpyDeviceToHost, s));
     LHPC_HIP_TRY(hipStreamSynchronize(s));
+    LHPC_HIP_TRY(hipMemcpy(y, p->d_ystage, static_cast<size_t>(p->n_rows) * tsz, hipMemcpyDeviceToHost));
   }
   return LHPC_OK;
 }

@@ -708,11 +708,11 @@ int blur_entry(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int6
   HostStage da, db;
   LHPC_HIP_TRY(hipMalloc(&da.d, in_bytes ? in_bytes : 16));
   LHPC_HIP_TRY(hipMalloc(&db.d, out_bytes ? out_bytes : 16));
-  LHPC_HIP_TRY(hipMemcpyAsync(da.d, a, in_bytes, hipMemcpyHostToDevice, s));
+  LHPC_HIP_TRY(hipMemcpy(da.d, a, in_bytes, hipMemcpyHostToDevice));  // host buffers: synchronous copies
   LHPC_TRY(blur_launch(ydir, static_cast<float *>(da.d), static_cast<float *>(db.d), ny, nx, ghost,
                        nblur, s));
-  LHPC_HIP_TRY(hipMemcpyAsync(b, db.d, out_bytes, hipMemcpyDeviceToHost, s));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
+  LHPC_HIP_TRY(hipMemcpy(b, db.d, out_bytes, hipMemcpyDeviceToHost));
   return LHPC_OK;
 }
 
@@ -853,12 +853,12 @@ extern "C" int lhpc_stencil7_f32(const float *u, float *out, int64_t nz, int64_t
   HostStage du, dout;
   LHPC_HIP_TRY(hipMalloc(&du.d, bytes));
   LHPC_HIP_TRY(hipMalloc(&dout.d, bytes));
-  LHPC_HIP_TRY(hipMemcpyAsync(du.d, u, bytes, hipMemcpyHostToDevice, s));
+  LHPC_HIP_TRY(hipMemcpy(du.d, u, bytes, hipMemcpyHostToDevice));  // host buffers: synchronous copies
   // ghost cells of `out` keep the caller's values
-  LHPC_HIP_TRY(hipMemcpyAsync(dout.d, out, bytes, hipMemcpyHostToDevice, s));
+  LHPC_HIP_TRY(hipMemcpy(dout.d, out, bytes, hipMemcpyHostToDevice));
   LHPC_TRY(s7_launch(static_cast<float *>(du.d), static_cast<float *>(dout.d), nz, ny, nx, ghost, c0,
                      c1, 0, nz, s));
-  LHPC_HIP_TRY(hipMemcpyAsync(out, dout.d, bytes, hipMemcpyDeviceToHost, s));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
+  LHPC_HIP_TRY(hipMemcpy(out, dout.d, bytes, hipMemcpyDeviceToHost));
   return LHPC_OK;
 }
