@@ -355,9 +355,11 @@ int lhpc_dist_allreduce_sum_f64(lhpc_dist_comm *comm, double *buf, int64_t count
  * LOCAL CSR: its K blocks stacked in chunk order (row_ptr rebased to 0,
  * global column indices, host arrays, copied to HBM).  lhpc_dist_spmv reads
  * the full x (n_cols, device) and leaves the full y (n_rows, device, not x)
- * on every rank: chunk k is reduced into this rank's rows of y, then a group
- * of in-place ncclBroadcast (one per root) on the comm stream delivers every
- * rank's block of chunk k while the compute stream reduces chunk k+1.
+ * on every rank: chunk k is reduced into this rank's rows of y, then the
+ * comm stream delivers every rank's block of chunk k while the compute
+ * stream reduces chunk k+1: one in-place ncclAllGather when chunk k's
+ * blocks are all the same size (uniform rows), else a group of in-place
+ * ncclBroadcast (one per root, exact slices).
  * Asynchronous on `stream`.  Matrices that do not select the XTILE layout
  * use one plan per block.
  */

@@ -13,10 +13,10 @@
 //          A rank stages x once (the XTILE tile gather of a row-range plan
 //          over its K blocks), then for k = 0..K−1 reduces chunk k straight
 //          into its rows of the full y and hands chunk k to the comm stream,
-//          where a group of nranks in-place ncclBroadcast (root r sends block
-//          k·nranks + r) fills every rank's y — exact slices, no padding —
-//          while the compute stream reduces chunk k+1.  y is then the next x
-//          on every rank.
+//          where one in-place ncclAllGather (equal-size blocks) or a group of
+//          nranks in-place ncclBroadcast (root r sends block k·nranks + r;
+//          exact slices, no padding) fills every rank's y while the compute
+//          stream reduces chunk k+1.  y is then the next x on every rank.
 //          Opt-in direct peer exchange (SURVEY §8e "Optimisation"): with a
 //          registered y window (lhpc_dist_p2p_export/_import: IPC handles of
 //          every rank's y), chunk k's block is pushed by one kernel straight
@@ -33,6 +33,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -75,6 +76,8 @@ struct lhpc_dist_spmv_plan {
   std::vector<hipEvent_t> ev;               // [K] chunk k reduced
   hipEvent_t done = nullptr;                // last broadcast issued on the comm stream
   hipEvent_t ev_p2p = nullptr;              // P2P: READY signalled on the compute stream
+  bool force_bcast = false;                 // LHPC_DIST_BCAST=1: broadcasts even for equal blocks (tests)
+  bool exchange_always = false;             // LHPC_DIST_EXCHANGE=1: run the RCCL exchange at world 1 (tests)
 };
 
 namespace {
@@ -196,10 +199,24 @@ void destroy_spmv(lhpc_dist_spmv_plan *d) {
   delete d;
 }
 
-// the broadcasts of chunk k: every rank's block k·nranks + r from root r
+// the exchange of chunk k: every rank's block k·nranks + r to every rank.
+// Blocks k·nranks … k·nranks + nranks − 1 are contiguous in y; when they are
+// all the same size (uniform rows: nnz-balanced cuts are equal-row cuts, as
+// for C2/C3) it is one in-place ncclAllGather, else a group of in-place
+// ncclBroadcast (root r sends its block; exact slices, no padding)
 int broadcast_chunk(const lhpc_dist_spmv_plan *d, int k, void *y, hipStream_t cs) {
   const lhpc_dist_comm *c = d->comm;
   const size_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
+  const int64_t b0 = static_cast<int64_t>(k) * c->nranks, cnt0 = d->cuts[b0 + 1] - d->cuts[b0];
+  bool equal = !d->force_bcast;
+  for (int r = 1; r < c->nranks && equal; ++r) equal = d->cuts[b0 + r + 1] - d->cuts[b0 + r] == cnt0;
+  if (equal) {
+    if (cnt0 == 0) return LHPC_OK;
+    unsigned char *base = static_cast<unsigned char *>(y) + d->cuts[b0] * tsz;
+    LHPC_NCCL_TRY(ncclAllGather(base + static_cast<size_t>(c->rank) * cnt0 * tsz, base, static_cast<size_t>(cnt0),
+                                nccl_dt(d->dtype), c->comm, cs));
+    return LHPC_OK;
+  }
   LHPC_NCCL_TRY(ncclGroupStart());
   for (int r = 0; r < c->nranks; ++r) {
     const int64_t b = static_cast<int64_t>(k) * c->nranks + r;
@@ -393,6 +410,8 @@ extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_c
   d->n_rows = n_rows;
   d->n_cols = n_cols;
   d->cuts.assign(cuts, cuts + nb + 1);
+  if (const char *e = std::getenv("LHPC_DIST_BCAST")) d->force_bcast = std::atoi(e) != 0;
+  if (const char *e = std::getenv("LHPC_DIST_EXCHANGE")) d->exchange_always = std::atoi(e) != 0;
   // the local CSR: the rank's K blocks stacked in chunk order
   std::vector<int64_t> ls(static_cast<size_t>(K) + 1, 0);
   for (int k = 0; k < K; ++k) {
@@ -461,6 +480,9 @@ extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, vo
   const bool p2p = c->nranks > 1 && c->p2p_ready && y == c->p2p_buf && c->p2p_bytes >= d->n_rows * tsz;
   if (c->nranks > 1 && !p2p && !c->comm) return LHPC_ERR_INVALID_ARG;  // local comm: y must be the window
   if (p2p) LHPC_TRY(p2p_exchange_begin(c, s, d->ev_p2p));
+  // the RCCL exchange also runs at world 1 under LHPC_DIST_EXCHANGE=1 (an
+  // in-place no-op there: lets the 1-GPU tests drive its calls and offsets)
+  const bool xchg = c->nranks > 1 || (d->exchange_always && c->comm);
   if (d->split) LHPC_TRY(lhpc_spmv_stage(d->split, x, stream));
   for (int k = 0; k < d->K; ++k) {
     const int64_t b = static_cast<int64_t>(k) * c->nranks + c->rank;
@@ -471,7 +493,7 @@ extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, vo
       else
         LHPC_TRY(lhpc_spmv(d->block_plan[k], x, yk, 1, stream));
     }
-    if (c->nranks > 1) {
+    if (xchg) {
       LHPC_HIP_TRY(hipEventRecord(d->ev[k], s));
       LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, d->ev[k], 0));
       lhpc::RocTxRange rb("lhpc_dist_spmv: y chunk exchange");
@@ -481,7 +503,7 @@ extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, vo
         LHPC_TRY(broadcast_chunk(d, k, y, c->s_comm));
     }
   }
-  if (c->nranks > 1) {
+  if (xchg) {
     if (p2p) LHPC_TRY(p2p_exchange_end(c));
     LHPC_HIP_TRY(hipEventRecord(d->done, c->s_comm));
     LHPC_HIP_TRY(hipStreamWaitEvent(s, d->done, 0));

@@ -56,6 +56,34 @@ def test_dist_spmv_world1_matches_single_plan(lhpc, gpu, comm, n, per_row, K, dt
             assert np.array_equal(y.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("mode", ["allgather", "broadcast"])
+@pytest.mark.parametrize("uniform", [True, False])
+def test_dist_spmv_world1_rccl_exchange(lhpc, gpu, comm, monkeypatch, mode, uniform):
+    """The RCCL y exchange driven at world 1 (LHPC_DIST_EXCHANGE=1: the
+    in-place collective is a no-op there, so y must come out unchanged):
+    equal-size blocks go through one in-place ncclAllGather per chunk,
+    unequal ones (power-law rows) or LHPC_DIST_BCAST=1 through the broadcast
+    group; three calls, K = 3."""
+    import torch
+    monkeypatch.setenv("LHPC_DIST_EXCHANGE", "1")
+    monkeypatch.setenv("LHPC_DIST_BCAST", "1" if mode == "broadcast" else "0")
+    n, K = 600_000, 3
+    if uniform:
+        rp, col, val = lhpc.gen_uniform_csr(n, n, 6, dtype=lhpc.F32, dist=1, seed=0xD300)
+    else:
+        rp, col, val = lhpc.gen_powerlaw_csr(n, n, dtype=lhpc.F32, dist=1, seed=0xD301)
+    x = lhpc.gen_values(lhpc.F32, 1, n, 0xD302)
+    xd = torch.from_numpy(x).to(gpu)
+    _, want, _ = S.spmv_oracle(rp, col, val, x)
+    cuts = lhpc.interleaved_cuts(rp, 1, K)
+    with lhpc.DistSpMVPlan(comm, n, n, K, cuts, *lhpc.interleaved_local_csr(rp, col, val, cuts, 1, K, 0)) as d:
+        for _ in range(3):
+            y = torch.full((n,), float("nan"), dtype=xd.dtype, device=gpu)
+            d(xd, y)
+            torch.cuda.synchronize()
+            assert np.array_equal(y.cpu().numpy(), want)
+
+
 def test_dist_spmv_rejects_aliased_xy(lhpc, gpu, comm):
     import torch
     n = 1000
