@@ -273,19 +273,33 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
       }
     }
   }
-  // ---- gather workgroups: each non-empty tile split into pieces of ≈ piece_nnz
+  // ---- gather workgroups: each non-empty tile split into pieces of ≈ piece_nnz.
+  //      Order: tiles in runs of 8, and inside a run piece k of the 8 tiles
+  //      before piece k + 1, so the pieces of one tile are 8 workgroups
+  //      apart — the same XCD under round-robin dispatch — and the x tile
+  //      the second one loads is an L2 hit.  (Placement only; any order is
+  //      correct.)
   o.pieces.clear();
   const int64_t pn = std::max<int64_t>(8, (piece_nnz + 7) / 8 * 8);
-  for (int64_t s = 0; s < S; ++s) {
-    const int64_t len = tbase[s + 1] - tbase[s];
-    if (len == 0) continue;
-    const int64_t P = (len + pn - 1) / pn;
-    const int64_t step = ((len + P - 1) / P + 7) / 8 * 8;
-    for (int64_t g = tbase[s]; g < tbase[s + 1]; g += step) {
-      o.pieces.push_back(static_cast<int32_t>(g));
-      o.pieces.push_back(static_cast<int32_t>(std::min(g + step, tbase[s + 1])));
-      o.pieces.push_back(static_cast<int32_t>(s));
+  for (int64_t s0 = 0; s0 < S; s0 += 8) {
+    std::vector<int64_t> step(8, 0), np(8, 0);
+    int64_t kmax = 0;
+    for (int64_t s = s0; s < std::min<int64_t>(S, s0 + 8); ++s) {
+      const int64_t len = tbase[s + 1] - tbase[s];
+      if (len == 0) continue;
+      const int64_t P = (len + pn - 1) / pn;
+      step[s - s0] = ((len + P - 1) / P + 7) / 8 * 8;
+      np[s - s0] = (len + step[s - s0] - 1) / step[s - s0];
+      kmax = std::max(kmax, np[s - s0]);
     }
+    for (int64_t k = 0; k < kmax; ++k)
+      for (int64_t s = s0; s < std::min<int64_t>(S, s0 + 8); ++s) {
+        if (k >= np[s - s0]) continue;
+        const int64_t g = tbase[s] + k * step[s - s0];
+        o.pieces.push_back(static_cast<int32_t>(g));
+        o.pieces.push_back(static_cast<int32_t>(std::min(g + step[s - s0], tbase[s + 1])));
+        o.pieces.push_back(static_cast<int32_t>(s));
+      }
   }
   return LHPC_OK;
 }
