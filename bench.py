@@ -282,7 +282,8 @@ def main():
                     "parallelism": f"row-block x{world}" + (
                         f" (interleaved nnz-balanced, {args.chunks} chunks/rank) + "
                         + ("direct xGMI peer stores of y chunks (lhpc_dist_p2p)" if p2p else
-                           "native RCCL broadcast of y chunks") + " (lhpc_dist_spmv) overlapped" if native_dist else
+                           "native RCCL exchange of y chunks (in-place all-gather for equal blocks, else "
+                           "broadcasts)") + " (lhpc_dist_spmv) overlapped" if native_dist else
                         f" (interleaved nnz-balanced, {args.chunks} chunks/rank) + torch.distributed all_gather(y) "
                         "overlapped" if world > 1 else "")},
             achieved_GBps=alg_bytes / per_step / 1e9,
