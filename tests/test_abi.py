@@ -118,3 +118,25 @@ def test_single_hip_runtime_with_torch():
             "print(len({l.split()[-1] for l in m.splitlines() if 'libamdhip64' in l}))" % ROOT)
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True)
     assert out.stdout.strip() == "1"
+
+
+def test_dist_calls_reject_bad_arguments_before_any_device_work(lhpc):
+    """The multi-GPU entry points validate their arguments first (no device,
+    no RCCL needed): null handles, bad ranks, a null window, foreign blobs."""
+    import ctypes as C
+    L = lhpc.lib
+    h = C.c_void_p()
+    assert L.lhpc_dist_comm_create_local(None, 2, 0, 0) == -1
+    assert L.lhpc_dist_comm_create_local(C.byref(h), 0, 0, 0) == -1      # no ranks
+    assert L.lhpc_dist_comm_create_local(C.byref(h), 2, 2, 0) == -1      # rank out of range
+    assert L.lhpc_dist_comm_create_local(C.byref(h), 65, 0, 0) == -1     # > 64 ranks
+    assert L.lhpc_dist_comm_create(C.byref(h), None, 1, 0, 0) == -1      # no unique id
+    blob = (C.c_ubyte * lhpc.DIST_P2P_BLOB_BYTES)()
+    assert L.lhpc_dist_p2p_export(None, None, 4, blob) == -1
+    assert L.lhpc_dist_p2p_import(None, blob) == -1
+    assert L.lhpc_dist_p2p_status(None) == -1
+    assert L.lhpc_dist_spmv(None, None, None, None) == -1
+    assert L.lhpc_dist_spmv_plan_destroy(None) == 0
+    assert L.lhpc_dist_comm_destroy(None) == 0
+    assert L.lhpc_dist_allreduce_sum_f64(None, None, 1, None) == -1
+    assert L.lhpc_dist_stencil7_f32(None, None, None, 1, 1, 1, 1, 1.0, 1.0, None) == -1
