@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--chunks", type=int, default=2, help="N>1: row chunks per rank (all-gather overlap; DESIGN.md §6)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dtype", default="auto", choices=["auto", "f32", "f64"],
+                    help="SpMV value type (auto: the config's own — fp64 for c1/c3, fp32 for c2/c4; "
+                         "SURVEY §8d also runs C4 in fp64)")
     return ap.parse_args()
 
 
@@ -137,6 +140,9 @@ def main():
     result = {}
     if wl in ("c1", "c2", "c3", "c4"):
         dt = L.F64 if wl in ("c1", "c3") else L.F32
+        if args.dtype != "auto":
+            dt = L.F64 if args.dtype == "f64" else L.F32
+        dtag = "" if dt == (L.F64 if wl in ("c1", "c3") else L.F32) else ("f64" if dt == L.F64 else "f32")
         tsz = 8 if dt == L.F64 else 4
         n = 100_000 if wl == "c1" else args.n
         t0 = time.time()
@@ -266,7 +272,7 @@ def main():
         kernels = {"xslice": "k_spmv_xslice+k_xslice_reduce", "rowgroup": "k_spmv_rowgroup",
                    "adaptive": "k_spmv_adaptive",
                    "xtile": "k_xtile_gather+k_xtile_reduce" + ("+k_xtile_fixup" if info["n_long_rows"] else "")}[kname]
-        traffic = load_traffic(f"{wl}_{kname}") if world == 1 else None
+        traffic = load_traffic(f"{wl}{dtag}_{kname}") if world == 1 else None
         result.update(
             metric=METRIC if wl != "c1" else "CSR SpMV GFLOP/s, n=100k nnz=1M fp64 (BASELINE configs[0])",
             value=gflops, unit="GFLOP/s", n_gpus=world, steps=args.steps,
@@ -277,7 +283,8 @@ def main():
                                        "GPU time beside the 1-thread SIMD baseline)",
                                  "c2": "BASELINE configs[1]: CSR SpMV n=10M nnz=150M fp32 uniform 15/row",
                                  "c3": "BASELINE configs[2] matrix: CSR SpMV n=10M nnz=150M fp64 uniform 15/row",
-                                 "c4": "BASELINE configs[3]: power-law CSR (1..1e4 nnz/row) fp32"}[wl],
+                                 "c4": "BASELINE configs[3]: power-law CSR (1..1e4 nnz/row) fp32"}[wl]
+                    + (f" (run in {dtag})" if dtag else ""),
                     "n_rows": n, "n_cols": n, "nnz": nnz, "kernel": kname, "slices": info["slices"],
                     "parallelism": f"row-block x{world}" + (
                         f" (interleaved nnz-balanced, {args.chunks} chunks/rank) + "
