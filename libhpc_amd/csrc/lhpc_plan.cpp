@@ -331,6 +331,27 @@ int xtile_transpose_runs(const XtileHost &o, const void *val, size_t tsz, int ru
   return LHPC_OK;
 }
 
+void xtile_range_pieces(XtileHost &o, int64_t piece_nnz, std::vector<int64_t> &rpc) {
+  const int64_t S = o.S, K = static_cast<int64_t>(o.rchunk.size()) - 1;
+  const int64_t pn = std::max<int64_t>(8, (piece_nnz + 7) / 8 * 8);
+  auto up8 = [](int64_t v) { return (v + 7) / 8 * 8; };
+  o.pieces.clear();
+  rpc.assign(1, 0);
+  for (int64_t k = 0; k < K; ++k) {
+    for (int64_t s = 0; s < S; ++s) {
+      const int64_t a = up8(o.segoff[o.rchunk[k] * S + s]), b = up8(o.segoff[o.rchunk[k + 1] * S + s]);
+      if (b <= a) continue;
+      const int64_t P = (b - a + pn - 1) / pn, step = up8((b - a + P - 1) / P);
+      for (int64_t g = a; g < b; g += step) {
+        o.pieces.push_back(static_cast<int32_t>(g));
+        o.pieces.push_back(static_cast<int32_t>(std::min(b, g + step)));
+        o.pieces.push_back(static_cast<int32_t>(s));
+      }
+    }
+    rpc.push_back(static_cast<int64_t>(o.pieces.size() / 3));
+  }
+}
+
 void xtile_permute_gather_blocks(XtileHost &o, int vw) {
   const int64_t np = static_cast<int64_t>(o.pieces.size() / 3);
 #pragma omp parallel for schedule(dynamic, 4)

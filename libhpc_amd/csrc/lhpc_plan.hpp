@@ -120,6 +120,12 @@ int xtile_transpose_runs(const XtileHost &o, const void *val, size_t tsz, int ru
 // partial last block keeps lane l's entries at 8·l .. 8·l + 7.
 inline int xtile_gather_pos(int k, int l, int vw) { return (k / vw) * 64 * vw + vw * l + k % vw; }
 void xtile_permute_gather_blocks(XtileHost &o, int vw);
+// replace o.pieces by per-range pieces: range k's part of tile s is
+// [⌈segoff[rchunk[k]][s]⌉₈, ⌈segoff[rchunk[k+1]][s]⌉₈) (the ≤ 7 entries of
+// range k before its rounded start were written by range k − 1's gather: a
+// gathered entry depends only on its position), cut into ≈ piece_nnz pieces;
+// rpc[k] = first piece of range k.
+void xtile_range_pieces(XtileHost &o, int64_t piece_nnz, std::vector<int64_t> &rpc);
 
 // LDS slot of chunk position i in the XTILE reduce (lhpc_spmv_xtile.hip
 // xt_slot): run t = i/run holds run = 64/elem_bytes elements (64 B) at

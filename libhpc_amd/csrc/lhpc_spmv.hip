@@ -337,7 +337,8 @@ extern "C" int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *p, lhpc_spmv_plan_i
   info->device = p->device;
   info->launches = p->kernel == LHPC_KERNEL_XSLICE ? 2 : 1;
   if (p->kernel == LHPC_KERNEL_XTILE) {
-    info->launches = (p->xt_pieces > 0 ? 1 : 0) + 1 + (p->xt_cont > 0 ? 1 : 0);
+    info->launches = p->xt_mall > 1 ? 2 * p->xt_mall + (p->xt_cont > 0 ? 1 : 0)
+                                    : (p->xt_pieces > 0 ? 1 : 0) + 1 + (p->xt_cont > 0 ? 1 : 0);
     info->n_blocks = p->xt_C;
     info->n_long_rows = p->xt_cont;
   }

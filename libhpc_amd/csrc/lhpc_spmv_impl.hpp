@@ -41,6 +41,11 @@ struct lhpc_spmv_plan {
   int64_t xt_C = 0, xt_pieces = 0, xt_cont = 0, xt_total = 0;
   size_t xt_lds = 0;
   int xt_u = 8;  // gather steps in flight (LHPC_XTILE_U)
+  // cache-sized ranges (LHPC_XTILE_MALL=K): a call runs gather k, reduce k
+  // for k < K so range k's xg is still in the Infinity Cache when its reduce
+  // reads it; range k's gather pieces are [xt_rpc[k], xt_rpc[k+1])
+  int xt_mall = 0;
+  std::vector<int64_t> xt_rpc;
   // row ranges (lhpc_spmv_plan_create_split): range k = rows [xt_srow[k],
   // xt_srow[k+1]) = chunks [xt_src[k], xt_src[k+1]), cont entries [xt_sco[k], xt_sco[k+1])
   std::vector<int64_t> split_rows, xt_srow, xt_src, xt_sco;

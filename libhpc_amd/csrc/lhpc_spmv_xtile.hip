@@ -535,19 +535,21 @@ const void *xtile_reduce_fn(int g, bool ip) {
 }
 
 template <typename T, int U>
-void gather_u(const lhpc_spmv_plan *p, const void *x, hipStream_t s) {
-  hipLaunchKernelGGL((k_xtile_gather<T, U>), dim3(static_cast<unsigned>(p->xt_pieces)), dim3(kXtGatherBlock), 0, s,
-                     p->d_pieces, p->d_col16, static_cast<const T *>(x), p->n_cols, static_cast<T *>(p->d_xg));
+void gather_u(const lhpc_spmv_plan *p, const void *x, int64_t q0, int64_t q1, hipStream_t s) {
+  hipLaunchKernelGGL((k_xtile_gather<T, U>), dim3(static_cast<unsigned>(q1 - q0)), dim3(kXtGatherBlock), 0, s,
+                     p->d_pieces + 3 * q0, p->d_col16, static_cast<const T *>(x), p->n_cols, static_cast<T *>(p->d_xg));
 }
 
+// gather pieces [q0, q1) (default: all)
 template <typename T>
-int launch_gather(const lhpc_spmv_plan *p, const void *x, hipStream_t s) {
-  if (p->xt_pieces <= 0) return LHPC_OK;
+int launch_gather(const lhpc_spmv_plan *p, const void *x, hipStream_t s, int64_t q0 = 0, int64_t q1 = -1) {
+  if (q1 < 0) q1 = p->xt_pieces;
+  if (q1 <= q0) return LHPC_OK;
   switch (p->xt_u) {
-    case 2: gather_u<T, 2>(p, x, s); break;
-    case 4: gather_u<T, 4>(p, x, s); break;
-    case 16: gather_u<T, 16>(p, x, s); break;
-    default: gather_u<T, 8>(p, x, s); break;
+    case 2: gather_u<T, 2>(p, x, q0, q1, s); break;
+    case 4: gather_u<T, 4>(p, x, q0, q1, s); break;
+    case 16: gather_u<T, 16>(p, x, q0, q1, s); break;
+    default: gather_u<T, 8>(p, x, q0, q1, s); break;
   }
   return check_launch(s);
 }
@@ -611,6 +613,27 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   // either way); LHPC_XTILE_CUT overrides (entries, 1..M)
   int cut = M / 32;
   if (const char *env = std::getenv("LHPC_XTILE_CUT")) cut = std::min(M, std::max(1, std::atoi(env)));
+  // cache-sized ranges: K nnz-balanced row ranges, gathered and reduced in
+  // turn, so that each range's xg (≈ 200 MB) is still in the 256 MB Infinity
+  // Cache when its reduce reads it back.  fp32 only: each extra range re-reads
+  // x (n_cols·T) in its gather.  Same box: C2 reduce 352 → 295
+  // µs, gather 163 → 179 µs, call 523.5 → 483.8 µs at K = 3 (K = 4: 506.7);
+  // C3 (fp64, K = 6: 200 MB ranges) 928 → 944 µs, so not for fp64
+  int mall = 0;
+  {
+    const int64_t xg_bytes = p->nnz * static_cast<int64_t>(tsz);
+    if (tsz == 4 && xg_bytes > (int64_t{256} << 20))
+      mall = static_cast<int>(std::min<int64_t>(8, (xg_bytes + (int64_t{200} << 20) - 1) / (int64_t{200} << 20)));
+  }
+  if (const char *env = std::getenv("LHPC_XTILE_MALL")) mall = std::atoi(env);
+  if (p->split_rows.empty() && mall > 1 && p->n_rows >= 2LL * mall) {
+    std::vector<int64_t> cuts(static_cast<size_t>(mall) + 1);
+    LHPC_TRY(lhpc_csr_partition_rows(rp.p, rp.bits, p->n_rows, mall, cuts.data()));
+    for (int k = 1; k < mall; ++k)
+      if (cuts[k] > 0 && cuts[k] < p->n_rows && (p->split_rows.empty() || cuts[k] > p->split_rows.back()))
+        p->split_rows.push_back(cuts[k]);
+    p->xt_mall = static_cast<int>(p->split_rows.size()) + 1;
+  }
   XtileHost xt;
   LHPC_TRY(build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, M, RMAX, piece, static_cast<int>(tsz),
                        p->split_rows.data(), static_cast<int>(p->split_rows.size()), ip, cut, xt));
@@ -659,6 +682,14 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cdesc), cd.data(), cd.size() * 4));
   }
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cr), xt.cr.data(), xt.cr.size() * 4));
+  if (p->xt_mall > 1) {
+    // one gather round per range: ≈ one piece per (tile, range) part, so each
+    // range loads every tile once (only one 160-KB gather block fits a CU)
+    int64_t rpn = std::max<int64_t>(min_piece, p->nnz / p->xt_mall / static_cast<int64_t>(cus) * 5 / 4 + 1);
+    if (const char *env = std::getenv("LHPC_XTILE_MALL_PIECE")) rpn = std::max<int64_t>(8, std::atoll(env));
+    xtile_range_pieces(xt, rpn, p->xt_rpc);
+    p->xt_pieces = static_cast<int64_t>(xt.pieces.size() / 3);
+  }
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_pieces), xt.pieces.data(), xt.pieces.size() * 4));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cont), xt.cont.data(), xt.cont.size() * 4));
   xtile_permute_gather_blocks(xt, static_cast<int>(16 / tsz));
@@ -693,8 +724,21 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
 
 }  // namespace
 
+template <typename T>
+int launch_mall(const lhpc_spmv_plan *p, const void *x, T *y, hipStream_t s) {
+  for (int k = 0; k < p->xt_mall; ++k) {
+    LHPC_TRY(launch_gather<T>(p, x, s, p->xt_rpc[k], p->xt_rpc[k + 1]));
+    LHPC_TRY(launch_reduce<T>(p, p->xt_src[k], p->xt_src[k + 1], 0, 0, y, s));
+  }
+  // one fix-up for every range's cut rows (their carries stay in place)
+  return launch_reduce<T>(p, p->xt_C, p->xt_C, 0, p->xt_cont, y, s);
+}
+
 int xtile_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
   if (p->n_rows == 0) return LHPC_OK;
+  if (p->xt_mall > 1)
+    return p->dtype == LHPC_F32 ? launch_mall<float>(p, x, static_cast<float *>(y), s)
+                                : launch_mall<double>(p, x, static_cast<double *>(y), s);
   if (p->dtype == LHPC_F32) {
     LHPC_TRY(launch_gather<float>(p, x, s));
     return launch_reduce<float>(p, 0, p->xt_C, 0, p->xt_cont, static_cast<float *>(y), s);

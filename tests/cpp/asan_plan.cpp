@@ -99,6 +99,28 @@ void check_xtile(const Csr &a, bool iperm, const std::vector<int64_t> &splits, i
       for (int v : seen) CHECK(v == 1);
     }
   }
+  // cache-sized ranges: range pieces cover the stream once, and every entry
+  // of range k is gathered by range k's pieces or an earlier range's
+  {
+    std::vector<int64_t> rpc;
+    lhpc::xtile_range_pieces(xt, 700, rpc);
+    const int64_t K = static_cast<int64_t>(xt.rchunk.size()) - 1;
+    CHECK(static_cast<int64_t>(rpc.size()) == K + 1 && static_cast<size_t>(rpc[K]) == xt.pieces.size() / 3);
+    std::vector<int> by(static_cast<size_t>(xt.total), -1);
+    for (int64_t k = 0; k < K; ++k)
+      for (int64_t q = rpc[k]; q < rpc[k + 1]; ++q) {
+        const int64_t g0 = xt.pieces[3 * q], g1 = xt.pieces[3 * q + 1], s = xt.pieces[3 * q + 2];
+        CHECK(g0 % 8 == 0 && g0 < g1 && g1 <= xt.total && s >= 0 && s < S);
+        for (int64_t g = g0; g < g1 && g < xt.total; ++g) {
+          CHECK(by[static_cast<size_t>(g)] < 0);
+          by[static_cast<size_t>(g)] = static_cast<int>(k);
+        }
+      }
+    for (int64_t k = 0; k < K; ++k)
+      for (int64_t s = 0; s < S; ++s)
+        for (int64_t g = xt.segoff[xt.rchunk[k] * S + s]; g < xt.segoff[xt.rchunk[k + 1] * S + s]; ++g)
+          CHECK(by[static_cast<size_t>(g)] >= 0 && by[static_cast<size_t>(g)] <= k);
+  }
   // the transposed val/iperm streams and the gather-block permutation
   std::vector<int32_t> vbase;
   std::unique_ptr<unsigned char[]> valt;

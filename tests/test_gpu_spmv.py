@@ -134,6 +134,8 @@ def test_full_size_c2_c3(lhpc, gpu, dtype):
         x = lhpc.gen_values(dt, dist, n, lhpc.SEED_X)
         with lhpc.SpMVPlan(rp, col, val, n) as plan:
             assert plan.info()["kernel"] == lhpc.KERNEL_XTILE
+            # fp32: 600 MB of xg → three cache-sized ranges (gather + reduce each)
+            assert plan.info()["launches"] == (6 if dtype == "f32" else 2)
             xd = torch.from_numpy(x).to(gpu)
             y1 = plan(xd).clone()
             y2 = plan(xd).clone()
@@ -168,6 +170,7 @@ def test_full_size_c4(lhpc, gpu, dtype):
         with lhpc.SpMVPlan(rp, col, val, n) as plan:
             info = plan.info()
             assert info["kernel"] == lhpc.KERNEL_XTILE and info["n_long_rows"] > 0
+            assert info["launches"] == (7 if dtype == "f32" else 3)  # fp32: three cache-sized ranges
             y = plan(torch.from_numpy(x).to(gpu)).cpu().numpy()
         y64, yr, asum = S.spmv_oracle(rp, col, val, x)
         if dist == 1:
@@ -397,6 +400,37 @@ def test_xtile_split_ranges(lhpc, gpu, dtype, xt_layout):
     _, yr, _ = S.spmv_oracle(rp, col, val, x)
     assert np.array_equal(y, yr)
     assert np.array_equal(yfull, yr)
+
+
+@pytest.mark.parametrize("ranges", [2, 3, 5])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_xtile_cache_ranges(lhpc, gpu, monkeypatch, dtype, ranges, xt_layout):
+    """Cache-sized ranges (LHPC_XTILE_MALL=K, the default for large fp32
+    plans): gather k and reduce k in turn over K nnz-balanced row ranges,
+    each range's gather pieces rounded up to 8-entry bounds inside a tile (its
+    first ≤ 7 entries come from the previous range's gather), one fix-up for
+    every range's cut rows.  Long rows crossing chunks, a tiny piece size (so
+    ranges hold several pieces per tile), two calls in a row; bit-exact."""
+    import torch
+    monkeypatch.setenv("LHPC_XTILE_MALL", str(ranges))
+    lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 30000 + [0, 0] + [30000]
+    n_cols = 200_000
+    rp, col, val = _csr_from_lengths(lengths, n_cols, 0xA900 + ranges, dyadic=True)
+    val = val.astype(dtype)
+    rng = np.random.default_rng(0xA9F0 + ranges)
+    x = (rng.integers(-8, 9, size=n_cols) / 8.0).astype(dtype)
+    _, yr, _ = S.spmv_oracle(rp, col, val, x)
+    for piece in ("", "1000"):
+        if piece:
+            monkeypatch.setenv("LHPC_XTILE_MALL_PIECE", piece)
+        with lhpc.SpMVPlan(rp, col, val, n_cols, flags=FAMILIES["xtile"]) as plan:
+            info = plan.info()
+            assert info["kernel"] == lhpc.KERNEL_XTILE
+            assert info["launches"] == 2 * ranges + (1 if info["n_long_rows"] else 0)
+            xd = torch.from_numpy(x).to(gpu)
+            for _ in range(2):  # carries from the previous call must not leak
+                y = plan(xd).cpu().numpy()
+                assert np.array_equal(y, yr)
 
 
 def test_split_plan_unsupported_without_xtile(lhpc, gpu):
