@@ -175,6 +175,11 @@ __device__ uint64_t g_xt_stamps[1 << 22];
 #define LHPC_XT_STAMP(i, real)
 #endif
 
+#ifndef LHPC_XT_XG_CPOL
+// xg LDS-DMA cache policy.  With cache-sized ranges (C2, same box, two runs
+// each): default 0 → reduce 292 µs; nt (2) 381 µs; sc0 (1) 292 µs; sc1 (16) 303 µs
+#define LHPC_XT_XG_CPOL 0
+#endif
 #ifndef LHPC_XT_IP_WAVES
 #define LHPC_XT_IP_WAVES 8  // iperm reduce: 8 waves/SIMD (fp32 66 → 64 VGPRs: C2 593 → 580 µs)
 #endif
@@ -350,7 +355,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
       for (int u = 0; u < NB; ++u)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             xr_rs, (__attribute__((address_space(3))) void *)(xs + (wv * NB + u) * kWave), 4,
-            src[u] * static_cast<int>(sizeof(T)), 0, 0, 0);
+            src[u] * static_cast<int>(sizeof(T)), 0, 0, LHPC_XT_XG_CPOL);
       load_ipv();
     } else {
       T xv[NB];

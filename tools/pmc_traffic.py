@@ -1,6 +1,11 @@
 """Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-launch byte counts.
 
   python tools/pmc_traffic.py <tag> <fetch_dir> <write_dir> [calib_dir] [--out profiles/traffic.json]
+                             [--per-call KERNEL=N ...]
+
+--per-call k_xtile_gather=3 says a call launches that kernel 3 times (XTILE
+cache-sized ranges): its per-dispatch average is multiplied by 3 in
+bytes_per_call.
 
 Counters are in KiB per dispatch (FETCH_SIZE = TCC_EA0_RDREQ-based, so
 Infinity-Cache hits are included).  Per MI355X_MICROARCH.md §HBM, FETCH_SIZE
@@ -34,6 +39,12 @@ def main():
     if "--out" in sys.argv:
         out = sys.argv[sys.argv.index("--out") + 1]
         args = [a for a in args if a != out]
+    per_call = {}
+    for i, a in enumerate(sys.argv):
+        if a == "--per-call":
+            k, v = sys.argv[i + 1].split("=")
+            per_call[k] = int(v)
+            args = [b for b in args if b != sys.argv[i + 1]]
     tag, fdir, wdir = args[:3]
     cal = {"k_read16": 1 << 30, "k_read4": 1 << 30}
     factor4 = None
@@ -59,11 +70,11 @@ def main():
         rb = fetch[k] * f4
         wb = write.get(k, 0.0)
         ent["kernels"][k] = {"read_bytes": rb, "write_bytes": wb, "dispatches": n[k],
-                             "raw_fetch_bytes": fetch[k]}
+                             "raw_fetch_bytes": fetch[k], "launches_per_call": per_call.get(k, 1)}
         if k.startswith("k_copyw"):  # bench.py's copy-ceiling probe, not part of the workload
             ent["kernels"][k]["probe"] = True
             continue
-        tot += rb + wb
+        tot += (rb + wb) * per_call.get(k, 1)
     ent["bytes_per_call"] = tot
     db[tag] = ent
     os.makedirs(os.path.dirname(out), exist_ok=True)
