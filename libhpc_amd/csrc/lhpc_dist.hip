@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "lhpc_common.hpp"
+#include "lhpc_spmv_impl.hpp"
 
 #define LHPC_NCCL_TRY(expr)                                                \
   do {                                                                     \
@@ -483,11 +484,17 @@ extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, vo
   // the RCCL exchange also runs at world 1 under LHPC_DIST_EXCHANGE=1 (an
   // in-place no-op there: lets the 1-GPU tests drive its calls and offsets)
   const bool xchg = c->nranks > 1 || (d->exchange_always && c->comm);
-  if (d->split) LHPC_TRY(lhpc_spmv_stage(d->split, x, stream));
+  // a split plan with per-range gather pieces (its xg exceeds the Infinity
+  // Cache) gathers each range right before reducing it; else one stage
+  const bool range_gather = d->split && !d->split->xt_rpc.empty();
+  int gathered = 0;  // ranges [0, gathered) are gathered (in order)
+  if (d->split && !range_gather) LHPC_TRY(lhpc_spmv_stage(d->split, x, stream));
   for (int k = 0; k < d->K; ++k) {
     const int64_t b = static_cast<int64_t>(k) * c->nranks + c->rank;
     void *yk = static_cast<unsigned char *>(y) + d->cuts[b] * tsz;
     if (d->range_of[k] >= 0) {
+      if (range_gather)
+        for (; gathered <= d->range_of[k]; ++gathered) LHPC_TRY(lhpc::xtile_range_gather(d->split, x, gathered, s));
       if (d->split)
         LHPC_TRY(lhpc_spmv_range(d->split, d->range_of[k], yk, stream));
       else

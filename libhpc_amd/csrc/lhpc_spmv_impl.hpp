@@ -96,6 +96,7 @@ int xslice_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const
 // ---- lhpc_spmv_xtile.hip
 int xtile_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s);
 int xtile_stage(const lhpc_spmv_plan *p, const void *x, hipStream_t s);
+int xtile_range_gather(const lhpc_spmv_plan *p, const void *x, int k, hipStream_t s);
 int xtile_range(const lhpc_spmv_plan *p, int k, void *yk, hipStream_t s);
 // LHPC_ERR_UNSUPPORTED: the layout does not fit its index types (caller falls back)
 int xtile_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz);

@@ -631,6 +631,9 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
       mall = static_cast<int>(std::min<int64_t>(8, (xg_bytes + (int64_t{200} << 20) - 1) / (int64_t{200} << 20)));
   }
   if (const char *env = std::getenv("LHPC_XTILE_MALL")) mall = std::atoi(env);
+  // a row-range plan (user splits) whose xg exceeds the cache gets per-range
+  // gather pieces for its own ranges (stage still gathers them all)
+  if (!p->split_rows.empty() && mall > 1) p->xt_mall = static_cast<int>(p->split_rows.size()) + 1;
   if (p->split_rows.empty() && mall > 1 && p->n_rows >= 2LL * mall) {
     std::vector<int64_t> cuts(static_cast<size_t>(mall) + 1);
     LHPC_TRY(lhpc_csr_partition_rows(rp.p, rp.bits, p->n_rows, mall, cuts.data()));
@@ -753,9 +756,17 @@ int xtile_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s)
 }
 
 // lhpc_spmv_stage: the gather of a split plan; lhpc_spmv_range: range k's
-// reduce + fix-up into y_k (row xt_srow[k] at y_k[0]).
+// reduce + fix-up into y_k (row xt_srow[k] at y_k[0]).  xtile_range_gather:
+// range k's gather alone (plans with per-range pieces; ranges gathered in
+// order 0, 1, … — a range's first ≤ 7 entries come from the one before).
 int xtile_stage(const lhpc_spmv_plan *p, const void *x, hipStream_t s) {
   return p->dtype == LHPC_F32 ? launch_gather<float>(p, x, s) : launch_gather<double>(p, x, s);
+}
+
+int xtile_range_gather(const lhpc_spmv_plan *p, const void *x, int k, hipStream_t s) {
+  if (p->xt_rpc.empty() || k < 0 || k + 2 > static_cast<int>(p->xt_rpc.size())) return LHPC_ERR_UNSUPPORTED;
+  return p->dtype == LHPC_F32 ? launch_gather<float>(p, x, s, p->xt_rpc[k], p->xt_rpc[k + 1])
+                              : launch_gather<double>(p, x, s, p->xt_rpc[k], p->xt_rpc[k + 1]);
 }
 
 int xtile_range(const lhpc_spmv_plan *p, int k, void *yk, hipStream_t s) {

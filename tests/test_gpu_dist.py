@@ -36,11 +36,17 @@ def test_unique_ids_differ(lhpc, gpu):
 @pytest.mark.parametrize("n,per_row,K", [(3_000_000, 6, 1), (3_000_000, 6, 2), (3_000_000, 6, 3),
                                          (20_000, 7, 2), (20_000, 7, 4)])
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
-def test_dist_spmv_world1_matches_single_plan(lhpc, gpu, comm, n, per_row, K, dtype):
+@pytest.mark.parametrize("range_gather", [False, True])
+def test_dist_spmv_world1_matches_single_plan(lhpc, gpu, comm, monkeypatch, n, per_row, K, dtype, range_gather):
     """lhpc_dist_spmv at world 1 with K chunks equals the single-plan SpMV bit
     for bit on dyadic values (XTILE row-range plan for the 3M-column matrix,
-    one plan per block for the small one), twice in a row, y != x."""
+    one plan per block for the small one), twice in a row, y != x.
+    range_gather: the row-range plan gets per-range gather pieces (as a plan
+    whose xg exceeds the Infinity Cache does) and each chunk's range is
+    gathered right before its reduce instead of one stage."""
     import torch
+    if range_gather:
+        monkeypatch.setenv("LHPC_XTILE_MALL", "2")
     dt = lhpc.F32 if dtype == "f32" else lhpc.F64
     rp, col, val = lhpc.gen_uniform_csr(n, n, per_row, dtype=dt, dist=1, seed=0xD200 + K)
     x = lhpc.gen_values(dt, 1, n, 0xD201)

@@ -371,12 +371,18 @@ def test_xtile_small_gather_pieces(lhpc, gpu, monkeypatch, xt_layout):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_xtile_split_ranges(lhpc, gpu, dtype, xt_layout):
+@pytest.mark.parametrize("range_pieces", [False, True])
+def test_xtile_split_ranges(lhpc, gpu, monkeypatch, dtype, xt_layout, range_pieces):
     """Row-range plan (lhpc_spmv_plan_create_split): stage once, reduce each
     range into its own buffer; long rows end at and start right after the
     split rows; the concatenation equals the whole-matrix oracle bit for bit
-    (dyadic) and lhpc_spmv on the same plan gives the same bits."""
+    (dyadic) and lhpc_spmv on the same plan gives the same bits.
+    range_pieces: per-range gather pieces (a plan whose xg exceeds the
+    Infinity Cache): stage gathers every range's pieces, lhpc_spmv runs
+    gather k / reduce k."""
     import torch
+    if range_pieces:
+        monkeypatch.setenv("LHPC_XTILE_MALL", "2")
     lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 30000 + [0, 0] + [30000]
     n_cols = 200_000
     rp, col, val = _csr_from_lengths(lengths, n_cols, 0xA700, dyadic=True)
