@@ -52,5 +52,9 @@ for W, K in ((1, 1), (2, 1), (2, 2), (2, 4), (4, 1), (4, 2), (4, 4), (8, 1), (8,
                 sp.range(k, y)
         ts = timed(step_split)
         rec.update(split_ms=ts, split_eff=t1 / W / ts)
+        if sp.info()["launches"] > 3:  # per-range gather pieces: lhpc_spmv runs gather k / reduce k
+            yall = torch.empty(sp.n_rows, device=dev)
+            tr = timed(lambda: sp(x, yall))
+            rec.update(range_gather_ms=tr, range_gather_eff=t1 / W / tr)
         sp.close()
     print(json.dumps(rec), flush=True)
