@@ -152,7 +152,10 @@ int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *plan,
  * Device buffers only, asynchronous on `stream`; all ranges of one x follow
  * one stage on the same stream.  LHPC_ERR_UNSUPPORTED when the matrix does
  * not select the XTILE layout (gathers with locality, or x ≤ 8 MB): use one
- * plan per range then.  lhpc_spmv on such a plan computes every range.
+ * plan per range then.  lhpc_spmv on such a plan computes every range; when
+ * the plan's gathered x stream exceeds the GPU's Infinity Cache (fp32, > 256
+ * MB) it runs gather k then reduce k per range, and lhpc_dist_spmv does the
+ * same per chunk (results identical to stage + ranges).
  * Replaces the per-block SpMV calls of the reference's row-block split
  * (no reference interface).
  */
