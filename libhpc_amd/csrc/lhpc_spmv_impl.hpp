@@ -41,6 +41,7 @@ struct lhpc_spmv_plan {
   int64_t xt_C = 0, xt_pieces = 0, xt_cont = 0, xt_total = 0;
   size_t xt_lds = 0;
   int xt_u = 8;  // gather steps in flight (LHPC_XTILE_U)
+  int xt_nt = 0;  // gather: non-temporal xg stores (LHPC_XTILE_NTSTORE)
   // cache-sized ranges (LHPC_XTILE_MALL=K): a call runs gather k, reduce k
   // for k < K so range k's xg is still in the Infinity Cache when its reduce
   // reads it; range k's gather pieces are [xt_rpc[k], xt_rpc[k+1])

@@ -37,7 +37,7 @@ template <> struct XtTile<double> { static constexpr int W = 20480; };  // 160 K
 // col16 step does not depend on the tile, so it is issued under the tile load.
 // (A fused form that also streamed val in tile order and wrote val·x[col]
 // was slower: C2 603 → 621 µs, C3 1141 → 1736 µs)
-template <typename T, int U>
+template <typename T, int U, bool NT = false>
 __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
     const int32_t *__restrict__ pieces, const uint16_t *__restrict__ col16,
     const T *__restrict__ x, int64_t n_cols, T *__restrict__ xg) {
@@ -95,7 +95,9 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
           tv16 v;
 #pragma unroll
           for (int k = 0; k < VW; ++k) v[k] = o[h * VW + k];
-          *reinterpret_cast<tv16 *>(blk + h * kWave * VW + VW * lane) = v;
+          tv16 *a = reinterpret_cast<tv16 *>(blk + h * kWave * VW + VW * lane);
+          if constexpr (NT) __builtin_nontemporal_store(v, a);
+          else *a = v;
         }
       } else if (qq < q1) {
 #pragma unroll
@@ -103,7 +105,9 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
           tv16 v;
 #pragma unroll
           for (int k = 0; k < VW; ++k) v[k] = o[h * VW + k];
-          *reinterpret_cast<tv16 *>(blk + 8 * lane + h * VW) = v;
+          tv16 *a = reinterpret_cast<tv16 *>(blk + 8 * lane + h * VW);
+          if constexpr (NT) __builtin_nontemporal_store(v, a);
+          else *a = v;
         }
       }
     }
@@ -541,9 +545,9 @@ const void *xtile_reduce_fn(int g, bool ip) {
   return ip ? xtile_reduce_fn<T, true>(g) : xtile_reduce_fn<T, false>(g);
 }
 
-template <typename T, int U>
+template <typename T, int U, bool NT = false>
 void gather_u(const lhpc_spmv_plan *p, const void *x, int64_t q0, int64_t q1, hipStream_t s) {
-  hipLaunchKernelGGL((k_xtile_gather<T, U>), dim3(static_cast<unsigned>(q1 - q0)), dim3(kXtGatherBlock), 0, s,
+  hipLaunchKernelGGL((k_xtile_gather<T, U, NT>), dim3(static_cast<unsigned>(q1 - q0)), dim3(kXtGatherBlock), 0, s,
                      p->d_pieces + 3 * q0, p->d_col16, static_cast<const T *>(x), p->n_cols, static_cast<T *>(p->d_xg));
 }
 
@@ -552,6 +556,10 @@ template <typename T>
 int launch_gather(const lhpc_spmv_plan *p, const void *x, hipStream_t s, int64_t q0 = 0, int64_t q1 = -1) {
   if (q1 < 0) q1 = p->xt_pieces;
   if (q1 <= q0) return LHPC_OK;
+  if (p->xt_nt) {
+    gather_u<T, 8, true>(p, x, q0, q1, s);
+    return check_launch(s);
+  }
   switch (p->xt_u) {
     case 2: gather_u<T, 2>(p, x, q0, q1, s); break;
     case 4: gather_u<T, 4>(p, x, q0, q1, s); break;
@@ -660,6 +668,7 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
     const int u = std::atoi(env);
     p->xt_u = u <= 2 ? 2 : u < 8 ? 4 : u < 16 ? 8 : 16;
   }
+  if (const char *env = std::getenv("LHPC_XTILE_NTSTORE")) p->xt_nt = std::atoi(env) != 0;
   LHPC_HIP_TRY(hipFuncSetAttribute(xtile_reduce_fn<T>(xtile_g<T>(xt.S), ip),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
   const int64_t n_rows = p->n_rows, C = xt.n_chunks;

@@ -371,6 +371,16 @@ def test_xtile_small_gather_pieces(lhpc, gpu, monkeypatch, xt_layout):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_xtile_nt_gather_stores(lhpc, gpu, monkeypatch, dtype, xt_layout):
+    """Non-temporal xg stores in the gather (LHPC_XTILE_NTSTORE=1) give the
+    same bits, with full and partial 64-group store blocks and cut rows."""
+    monkeypatch.setenv("LHPC_XTILE_NTSTORE", "1")
+    lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 3000 + [0, 0] + [30000]
+    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA500, expect_cont=True)
+    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA501, dyadic=False)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("range_pieces", [False, True])
 def test_xtile_split_ranges(lhpc, gpu, monkeypatch, dtype, xt_layout, range_pieces):
     """Row-range plan (lhpc_spmv_plan_create_split): stage once, reduce each
