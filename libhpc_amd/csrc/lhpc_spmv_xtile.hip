@@ -668,6 +668,11 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
     const int u = std::atoi(env);
     p->xt_u = u <= 2 ? 2 : u < 8 ? 4 : u < 16 ? 8 : 16;
   }
+  // non-temporal xg stores when the xg of a single-range plan exceeds the 256
+  // MB Infinity Cache anyway (same box, two runs each: C3 918.6 → 908.8 µs
+  // median); cache-sized ranges need their xg to stay there (C2 with them
+  // non-temporal: 473 → 536 µs)
+  p->xt_nt = p->xt_mall <= 1 && p->nnz * static_cast<int64_t>(tsz) > (int64_t{256} << 20) ? 1 : 0;
   if (const char *env = std::getenv("LHPC_XTILE_NTSTORE")) p->xt_nt = std::atoi(env) != 0;
   LHPC_HIP_TRY(hipFuncSetAttribute(xtile_reduce_fn<T>(xtile_g<T>(xt.S), ip),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
