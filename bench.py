@@ -128,14 +128,33 @@ def main():
     stream = torch.cuda.current_stream(dev)
     # N > 1 over RCCL: the native lhpc_dist_* path (one RCCL communicator and
     # comm stream per process, created from rank 0's unique id); the
-    # torch.distributed form serves the gloo rehearsal or LHPC_DIST_TORCH=1
-    # LHPC_DIST_P2P=1: the y exchange by direct peer stores into every rank's
-    # registered y (lhpc_dist_p2p_*) instead of RCCL broadcasts; with the gloo
-    # backend (ranks sharing one GPU in a rehearsal) over an RCCL-free
-    # local communicator
-    p2p = os.environ.get("LHPC_DIST_P2P", "0") == "1"
+    # torch.distributed form serves the gloo rehearsal or LHPC_DIST_TORCH=1.
+    # The native path times both y exchanges (RCCL collectives and direct
+    # xGMI peer stores into every rank's registered y window) in the same
+    # run, plus SpMV-only and exchange-only steps, and reports the faster
+    # exchange as the headline.  With the gloo backend (ranks
+    # sharing one GPU in a rehearsal) only the peer exchange exists, over an
+    # RCCL-free local communicator.
     native_dist = (world > 1 or force_native) and (
-        (dist.get_backend() == "nccl" and os.environ.get("LHPC_DIST_TORCH", "0") != "1") or p2p)
+        dist.get_backend() == "nccl" and os.environ.get("LHPC_DIST_TORCH", "0") != "1"
+        or os.environ.get("LHPC_DIST_P2P", "0") == "1")
+
+    def timed(fn, steps, warmup):
+        """max-over-ranks seconds per step of fn: W untimed calls, then
+        `steps` calls bracketed by barrier + synchronize."""
+        for _ in range(warmup):
+            fn()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el / steps
     wl = args.workload
     result = {}
     if wl in ("c1", "c2", "c3", "c4"):
@@ -164,29 +183,58 @@ def main():
             def step():
                 plans[0](xd, y_local, stream=stream)
         elif native_dist:
-            # native RCCL path behind the C ABI (lhpc_dist_spmv): nnz-balanced
+            # native path behind the C ABI (lhpc_dist_spmv): nnz-balanced
             # interleaved blocks, K chunks per rank; chunk k is reduced into
-            # the rank's rows of y and broadcast (in place, exact slices) to
-            # every rank on the comm stream while chunk k+1 is reduced
-            comm = L.DistComm.from_torch(local) if dist.get_backend() == "nccl" else \
-                L.DistComm.local(world, rank, local)
+            # the rank's rows of y and exchanged on the comm stream while
+            # chunk k+1 is reduced.  One plan per exchange kind (the kind is
+            # a plan option), each over the same local rows.
+            has_rccl = dist.get_backend() == "nccl"
+            comm = L.DistComm.from_torch(local) if has_rccl else L.DistComm.local(world, rank, local)
             cuts = L.interleaved_cuts(rp, world, args.chunks)
             lrp, lc, lv = L.interleaved_local_csr(rp, col, val, cuts, world, args.chunks, rank)
-            dplan = L.DistSpMVPlan(comm, n, n, args.chunks, cuts, lrp, lc, lv)
+            dplans, xnotes = {}, {}
+            if has_rccl:
+                dplans["rccl"] = L.DistSpMVPlan(comm, n, n, args.chunks, cuts, lrp, lc, lv,
+                                                options={"dist_exchange": L.DIST_EXCHANGE_RCCL,
+                                                         "dist_world1": 1 if world == 1 else 0})
+            y_p2p = torch.empty(n, dtype=xd.dtype, device=dev)
+            if world > 1:
+                try:
+                    comm.p2p_setup_torch(y_p2p)
+                    dplans["p2p"] = L.DistSpMVPlan(comm, n, n, args.chunks, cuts, lrp, lc, lv,
+                                                   options={"dist_exchange": L.DIST_EXCHANGE_P2P})
+                except L.LhpcError as e:  # e.g. no IPC between the ranks' devices
+                    xnotes["p2p"] = f"unavailable: {e}"
+            dplans["none"] = L.DistSpMVPlan(comm, n, n, args.chunks, cuts, lrp, lc, lv,
+                                            options={"dist_exchange": L.DIST_EXCHANGE_NONE})
             # the same local rows as one plan: the live kernel-only call timing below
             plans = [L.SpMVPlan(lrp, lc, lv, n)]
             local_nnz, local_rows = int(lc.shape[0]), int(lrp.shape[0] - 1)
             y_full = torch.empty(n, dtype=xd.dtype, device=dev)
-            if p2p and world > 1:
-                comm.p2p_setup_torch(y_full)
+            ybuf = {"rccl": y_full, "p2p": y_p2p, "none": y_full}
+            # per-exchange end-to-end, exchange-only and SpMV-only steps
+            xtimes = {}
+            for kx in [k for k in ("rccl", "p2p") if k in dplans]:
+                dp, yb = dplans[kx], ybuf[kx]
+                e2e = timed(lambda dp=dp, yb=yb: dp(xd, yb, stream=stream), args.steps, args.warmup)
+                xo = timed(lambda dp=dp, yb=yb: dp.exchange(yb, stream=stream), args.steps, args.warmup)
+                xtimes[kx] = {"step_ms": e2e * 1e3, "exchange_only_ms": xo * 1e3,
+                              "gflops": 2.0 * nnz / e2e / 1e9}
+            spmv_only = timed(lambda: dplans["none"](xd, y_full, stream=stream), args.steps, args.warmup)
+            chosen = min(xtimes, key=lambda k: xtimes[k]["step_ms"]) if xtimes else "none"
+            dplan = dplans[chosen]
+            y_out_buf = ybuf[chosen]
+            exchange_report = {"chosen": chosen, "spmv_only_ms": spmv_only * 1e3, **xtimes, **xnotes,
+                               "note": "step = local SpMV + y exchange (lhpc_dist_spmv); exchange_only = "
+                                       "lhpc_dist_exchange alone; spmv_only = exchange NONE; max over ranks"}
 
             class _Native:
                 def step(self, xv):
-                    return dplan(xv, y_full, stream=stream)
+                    return dplan(xv, y_out_buf, stream=stream)
             dsp = _Native()
 
             def step():
-                dplan(xd, y_full, stream=stream)
+                dplan(xd, y_out_buf, stream=stream)
         else:
             # torch.distributed form (gloo rehearsal, LHPC_DIST_TORCH=1):
             # interleaved nnz-balanced row blocks, K chunks per rank; chunk
@@ -288,9 +336,10 @@ def main():
                     "n_rows": n, "n_cols": n, "nnz": nnz, "kernel": kname, "slices": info["slices"],
                     "parallelism": f"row-block x{world}" + (
                         f" (interleaved nnz-balanced, {args.chunks} chunks/rank) + "
-                        + ("direct xGMI peer stores of y chunks (lhpc_dist_p2p)" if p2p else
+                        + ("direct xGMI peer stores of y chunks (lhpc_dist_p2p windows)" if chosen == "p2p" else
                            "native RCCL exchange of y chunks (in-place all-gather for equal blocks, else "
-                           "broadcasts)") + " (lhpc_dist_spmv) overlapped" if native_dist else
+                           "broadcasts)" if chosen == "rccl" else "no exchange")
+                        + " (lhpc_dist_spmv) overlapped; faster of the measured exchanges" if native_dist else
                         f" (interleaved nnz-balanced, {args.chunks} chunks/rank) + torch.distributed all_gather(y) "
                         "overlapped" if world > 1 else "")},
             achieved_GBps=alg_bytes / per_step / 1e9,
@@ -304,6 +353,8 @@ def main():
         # correctness of the timed output, outside the timed region: y of the
         # last step on 10^5 sampled rows against an fp64 numpy evaluation,
         # |dy| <= 1e-6·Σ|a·x| per row (the parity bar of tests/_support.py)
+        if native_dist:
+            result["exchange"] = exchange_report
         y_out = dsp.step(xd) if (world > 1 or native_dist) else y_local  # every rank: the step holds collectives
         if rank == 0:
             result["check"] = sampled_y_check(rp, col, val, x, y_out.cpu().numpy(), 100_000)
@@ -322,8 +373,9 @@ def main():
                                                        threads=1 if wl == "c1" else None)
         for pl in plans:
             pl.close()
-        if native_dist:  # the plan before its communicator
-            dplan.close()
+        if native_dist:  # the plans before their communicator
+            for dp in dplans.values():
+                dp.close()
             comm.close()
     elif wl == "sort":
         result.update(sort_bench(args, L, torch, dev, stream, barrier, world, rank))

@@ -107,6 +107,81 @@ typedef struct lhpc_spmv_plan_info {
   int64_t slice_width; /* XSLICE / XTILE: columns per slice / tile          */
 } lhpc_spmv_plan_info;
 
+/* ------------------------------------------------------- variant options
+ * Kernel-variant and tuning choices, passed explicitly to the *_opts entry
+ * points below: the library never reads the process environment, so the
+ * same call always builds the same plan.  Every field at 0 means the
+ * automatic choice, i.e. exactly what the plain entry points do.  Call
+ * lhpc_options_init first; struct_size (set by it) lets later ABI versions
+ * append fields.  The reference has no runtime knobs at all (compile-time
+ * template parameters only, SURVEY §5 "Config / flags"); these exist for the
+ * measured alternatives of DESIGN.md §4 and for tests that pin a variant.
+ */
+enum lhpc_xtile_reduce {
+  LHPC_XTILE_REDUCE_AUTO = 0,
+  LHPC_XTILE_REDUCE_PERM = 1,   /* scatter xg into CSR slots through perm     */
+  LHPC_XTILE_REDUCE_IPERM = 2   /* gather CSR positions through iperm         */
+};
+enum lhpc_stencil7_impl {
+  LHPC_S7_AUTO = 0,
+  LHPC_S7_SIMPLE = 1,           /* thread per column                          */
+  LHPC_S7_RING = 2,             /* buffer-addressed dword register ring       */
+  LHPC_S7_RING_X4 = 3           /* x4 ring (16-B rows per lane)               */
+};
+enum lhpc_store_policy {
+  LHPC_STORE_AUTO = 0,
+  LHPC_STORE_PLAIN = 1,
+  LHPC_STORE_NT = 2,            /* non-temporal                               */
+  LHPC_STORE_STAGED = 3         /* stencil7 dword ring: float4 via LDS rows   */
+};
+enum lhpc_dist_exchange {
+  LHPC_DIST_EXCHANGE_AUTO = 0,  /* peer stores when y is a registered window, else RCCL */
+  LHPC_DIST_EXCHANGE_RCCL = 1,  /* in-place all-gather / broadcast group      */
+  LHPC_DIST_EXCHANGE_P2P = 2,   /* direct xGMI peer stores (y must be a window) */
+  LHPC_DIST_EXCHANGE_NONE = 3   /* local rows only (SpMV-only timing)         */
+};
+typedef struct lhpc_options {
+  uint32_t struct_size;         /* sizeof(lhpc_options), set by lhpc_options_init */
+  /* SpMV kernel selection */
+  int32_t spmv_no_xtile;        /* 1: gathers without locality get XSLICE, not XTILE */
+  double spmv_locality;         /* distinct x lines per nonzero above which gathers
+                                   count as random (0: 0.25)                      */
+  int32_t rowgroup_lanes;       /* ROWGROUP: lanes per row L (0: from the mean)  */
+  int32_t rowgroup_rows;        /* ROWGROUP: rows per lane group R               */
+  /* XTILE */
+  int32_t xtile_reduce;         /* enum lhpc_xtile_reduce                        */
+  int32_t xtile_ranges;         /* 1: one range; K ≥ 2: K cache-sized row ranges */
+  int32_t xtile_steps;          /* gather steps in flight: 2, 4, 8 (auto), 16    */
+  int32_t xtile_store;          /* xg stores: LHPC_STORE_PLAIN / _NT             */
+  int32_t xtile_cut;            /* chunk-cut window in nonzeros (0: M/32)        */
+  int32_t xtile_reserved;
+  int64_t xtile_piece;          /* gather piece length in nonzeros               */
+  int64_t xtile_range_piece;    /* the same under cache-sized ranges             */
+  /* XSLICE */
+  int32_t xslice_slices;        /* column slices S (rounded to a multiple of 8)  */
+  int32_t xslice_partial;       /* 1: fp32 partials, 2: fp64 partials            */
+  int32_t xslice_window;        /* 64-nonzero windows per chunk pass (1..4)      */
+  int32_t xslice_reserved;
+  double xslice_mb;             /* target x slice size in MB (0: 5)              */
+  /* stencils */
+  int32_t stencil7_impl;        /* enum lhpc_stencil7_impl                       */
+  int32_t stencil7_store;       /* enum lhpc_store_policy                        */
+  int32_t stencil7_ry;          /* ring tile: rows per wave (1, 2, 4)            */
+  int32_t stencil7_nj;          /* ring tile: 64-column blocks per wave (4, 8)   */
+  int32_t stencil7_zc;          /* z planes per block (0: grid ≈ stencil7_blocks) */
+  int32_t stencil7_pf;          /* prefetch planes (1..3)                        */
+  int32_t stencil7_blocks;      /* target grid size (0: 256)                     */
+  int32_t blur_x_rows;          /* blur_x rows per wave (1, 2, 4, 8, 16, 32)     */
+  int32_t blur_y_vec;           /* blur_y columns per thread (1, 2, 4)           */
+  int32_t blur_y_rows;          /* blur_y output rows per thread (16 … 64)       */
+  /* multi-GPU SpMV (lhpc_dist_spmv) */
+  int32_t dist_exchange;        /* enum lhpc_dist_exchange                       */
+  int32_t dist_broadcast;       /* 1: RCCL broadcast groups even for equal blocks */
+  int32_t dist_world1;          /* 1: issue the RCCL exchange at world 1 (tests) */
+  int32_t reserved[7];
+} lhpc_options;
+void lhpc_options_init(lhpc_options *opts);
+
 /* ------------------------------------------------------------- runtime   */
 const char *lhpc_strerror(int status);
 int lhpc_abi_version(void);
@@ -165,6 +240,15 @@ int lhpc_spmv_plan_create_split(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
                                 const void *val, const int *device_ids,
                                 int n_devices, unsigned flags, int n_splits,
                                 const int64_t *split_rows);
+/* Both of the above with explicit variant options (NULL = all automatic);
+ * n_splits = 0 gives an ordinary plan.                                      */
+int lhpc_spmv_plan_create_opts(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
+                               int64_t n_cols, int64_t nnz, const void *row_ptr,
+                               int row_ptr_bits, const int32_t *col_idx,
+                               const void *val, const int *device_ids,
+                               int n_devices, unsigned flags, int n_splits,
+                               const int64_t *split_rows,
+                               const lhpc_options *opts);
 int lhpc_spmv_stage(const lhpc_spmv_plan *plan, const void *x, void *stream);
 int lhpc_spmv_range(const lhpc_spmv_plan *plan, int k, void *y_range, void *stream);
 int lhpc_spmv_plan_destroy(lhpc_spmv_plan *plan);
@@ -209,6 +293,19 @@ int lhpc_stencil7_f32_planes(const float *u, float *out, int64_t nz,
                              int64_t ny, int64_t nx, int64_t ghost, float c0,
                              float c1, int64_t z_begin, int64_t z_end,
                              void *stream);
+/* the three stencils with explicit variant options (NULL = automatic); the
+ * stencil7 form covers planes [z_begin, z_end) of device buffers           */
+int lhpc_blur_x_f32_opts(const float *a, float *b, int64_t ny, int64_t nx,
+                         int64_t ghost, int nblur, int buffers_on_device,
+                         void *stream, const lhpc_options *opts);
+int lhpc_blur_y_f32_opts(const float *a, float *b, int64_t ny, int64_t nx,
+                         int64_t ghost, int nblur, int buffers_on_device,
+                         void *stream, const lhpc_options *opts);
+int lhpc_stencil7_f32_planes_opts(const float *u, float *out, int64_t nz,
+                                  int64_t ny, int64_t nx, int64_t ghost,
+                                  float c0, float c1, int64_t z_begin,
+                                  int64_t z_end, void *stream,
+                                  const lhpc_options *opts);
 
 /* ------------------------------------------- synthetic workloads (host) */
 /*
@@ -370,31 +467,78 @@ typedef struct lhpc_dist_spmv_plan lhpc_dist_spmv_plan;
 int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_comm *comm, int dtype, int64_t n_rows,
                           int64_t n_cols, int K, const int64_t *cuts, const void *row_ptr,
                           int row_ptr_bits, const int32_t *col_idx, const void *val, unsigned flags);
+/* the same with explicit options (NULL = automatic): the local plans' SpMV
+ * variant fields and the dist_* fields (exchange kind, broadcast groups)   */
+int lhpc_dist_spmv_plan_create_opts(lhpc_dist_spmv_plan **out, lhpc_dist_comm *comm, int dtype,
+                                    int64_t n_rows, int64_t n_cols, int K, const int64_t *cuts,
+                                    const void *row_ptr, int row_ptr_bits, const int32_t *col_idx,
+                                    const void *val, unsigned flags, const lhpc_options *opts);
 int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream);
+/* the exchange of a whole call alone (every chunk, no SpMV): y must already
+ * hold this rank's blocks; for exchange-only timing (bench.py --gpus N)    */
+int lhpc_dist_exchange(lhpc_dist_spmv_plan *d, void *y, void *stream);
 int lhpc_dist_spmv_plan_destroy(lhpc_dist_spmv_plan *d);
 /*
+ * The exchange schedule of lhpc_dist_spmv, as data (host only; the call
+ * issues exactly these transfers, in this order, per chunk k):
+ *   LHPC_XFER_ALLGATHER  chunk k's nranks blocks are equal (count rows each):
+ *                        one in-place all-gather of y[offset, offset +
+ *                        nranks·count), this rank sending y[send_offset, +count)
+ *   LHPC_XFER_BROADCAST  unequal blocks (or dist_broadcast): one in-place
+ *                        broadcast from `root` of y[offset, offset + count) per
+ *                        non-empty block, inside one group per chunk
+ *   LHPC_XFER_PUSH       peer exchange: this rank stores y[offset, +count)
+ *                        (its own block) into every peer's y
+ * Offsets and counts are in elements of y.  exchange: LHPC_DIST_EXCHANGE_RCCL
+ * or _P2P; broadcast: 1 = broadcast groups even for equal blocks.
+ * Returns the number of entries in *n_out (capacity max_out; LHPC_ERR_INVALID_ARG
+ * if too small).  Replaces nothing in the reference (no collectives there).
+ */
+enum lhpc_xfer_kind { LHPC_XFER_ALLGATHER = 1, LHPC_XFER_BROADCAST = 2, LHPC_XFER_PUSH = 3 };
+typedef struct lhpc_dist_xfer {
+  int32_t chunk;
+  int32_t kind;                 /* enum lhpc_xfer_kind                           */
+  int32_t root;                 /* broadcast root / pushing rank (−1: all-gather) */
+  int32_t group;                /* 1 when the entry is inside a chunk's group    */
+  int64_t offset;               /* first element of y the transfer fills          */
+  int64_t count;                /* elements (all-gather: per rank)               */
+  int64_t send_offset;          /* all-gather: this rank's contribution           */
+} lhpc_dist_xfer;
+int lhpc_dist_exchange_schedule(const int64_t *cuts, int nranks, int K, int rank, int exchange,
+                                int broadcast, lhpc_dist_xfer *out, int64_t max_out, int64_t *n_out);
+/*
  * Direct peer exchange of y (SURVEY §8e "Optimisation": every pair of
- * MI355X in a node is connected by xGMI).  Each rank exports its y buffer
+ * MI355X in a node is connected by xGMI).  Each rank exports a y buffer
  * (device, ≥ n_rows values, 4-byte multiple) as a blob of IPC handles, the
  * launcher all-gathers the blobs (any channel, rank order) and every rank
- * imports them.  lhpc_dist_spmv called with exactly that y then pushes each
- * chunk's block into every peer's y with one kernel (stores over xGMI, all
- * links at once) instead of the RCCL broadcasts; per call a READY flag
- * ("my y may be overwritten": issued on the call's stream, so prior work on
- * it that reads y is done) and a DONE flag ("my pushes have landed") go to
- * every peer, and the comm stream waits for all peers' flags (bounded spin;
- * a timeout sets lhpc_dist_p2p_status and fails the next call).  y must not
- * be read by any stream other than the call's until the call completes.
- * Without RCCL, lhpc_dist_comm_create_local gives a communicator for this
- * exchange only (lhpc_dist_allreduce_sum_f64 / stencil7 need RCCL:
- * LHPC_ERR_UNSUPPORTED).  Opt-in: the default exchange stays RCCL.
+ * imports them.  Up to LHPC_DIST_P2P_MAX_WINDOWS windows per communicator
+ * (export/import them in the same order on every rank): with two, the
+ * iterative loop's ping-pong pair (y of call n is x of call n+1) gets peer
+ * stores on every call.  lhpc_dist_spmv with y equal to a window then pushes
+ * each chunk's block into every peer's copy of that window with one kernel
+ * (stores over xGMI, all links at once) instead of RCCL collectives; per
+ * call a READY flag ("my y may be overwritten": issued on the call's
+ * stream, so prior work on it that reads y is done) and a DONE flag ("my
+ * pushes have landed") go to every peer, and the comm stream waits for all
+ * peers' flags with a bounded spin.  A spin that times out sets the
+ * communicator's status word: the pushes and DONE of that call are then
+ * skipped on the device and every later call fails — check
+ * lhpc_dist_p2p_status after synchronising the stream.  y must not be read
+ * by any stream other than the call's until the call completes.  Without
+ * RCCL, lhpc_dist_comm_create_local gives a communicator for this exchange
+ * only (lhpc_dist_allreduce_sum_f64 / stencil7 need RCCL:
+ * LHPC_ERR_UNSUPPORTED).  The exchange kind is a plan option
+ * (lhpc_options.dist_exchange; automatic = peer stores for a window).
  */
 #define LHPC_DIST_P2P_BLOB_BYTES 192
+#define LHPC_DIST_P2P_MAX_WINDOWS 4
 int lhpc_dist_comm_create_local(lhpc_dist_comm **out, int nranks, int rank, int device);
 int lhpc_dist_p2p_export(lhpc_dist_comm *comm, void *y, int64_t bytes,
                          unsigned char *blob_out /* LHPC_DIST_P2P_BLOB_BYTES */);
 int lhpc_dist_p2p_import(lhpc_dist_comm *comm,
                          const unsigned char *blobs /* nranks × LHPC_DIST_P2P_BLOB_BYTES */);
+/* unmaps every window (peer handles closed, flags freed)                   */
+int lhpc_dist_p2p_reset(lhpc_dist_comm *comm);
 int lhpc_dist_p2p_status(const lhpc_dist_comm *comm);
 /*
  * One 7-point stencil step on this rank's z-slab (BASELINE config C5): u and

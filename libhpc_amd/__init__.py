@@ -64,6 +64,9 @@ ABI_SYMBOLS = (
     "lhpc_dist_allreduce_sum_f64", "lhpc_dist_spmv_plan_create", "lhpc_dist_spmv",
     "lhpc_dist_spmv_plan_destroy", "lhpc_dist_stencil7_f32", "lhpc_dist_comm_create_local",
     "lhpc_dist_p2p_export", "lhpc_dist_p2p_import", "lhpc_dist_p2p_status",
+    "lhpc_options_init", "lhpc_spmv_plan_create_opts", "lhpc_blur_x_f32_opts", "lhpc_blur_y_f32_opts",
+    "lhpc_stencil7_f32_planes_opts", "lhpc_dist_spmv_plan_create_opts", "lhpc_dist_exchange",
+    "lhpc_dist_exchange_schedule", "lhpc_dist_p2p_reset",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -79,7 +82,7 @@ def _bind_single_hip_runtime():
     liblhpc.so bind to torch's copies, in torch's own load order."""
     try:
         import torch  # noqa: F401
-    except ImportError:
+    except Exception:  # a broken torch install must not make the C ABI unusable
         pass
 
 
@@ -87,6 +90,52 @@ _bind_single_hip_runtime()
 lib = C.CDLL(LIB_PATH)
 _p, _i, _i64, _u, _u64, _f, _d = (C.c_void_p, C.c_int, C.c_int64, C.c_uint,
                                   C.c_uint64, C.c_float, C.c_double)
+
+
+class Options(C.Structure):
+    """include/lhpc.h lhpc_options: explicit variant choices (0 = automatic).
+    ``Options(xtile_reduce=XTILE_REDUCE_PERM, ...)``; unknown names raise."""
+    _fields_ = [("struct_size", C.c_uint32), ("spmv_no_xtile", C.c_int32), ("spmv_locality", C.c_double),
+                ("rowgroup_lanes", C.c_int32), ("rowgroup_rows", C.c_int32),
+                ("xtile_reduce", C.c_int32), ("xtile_ranges", C.c_int32), ("xtile_steps", C.c_int32),
+                ("xtile_store", C.c_int32), ("xtile_cut", C.c_int32), ("xtile_reserved", C.c_int32),
+                ("xtile_piece", C.c_int64), ("xtile_range_piece", C.c_int64),
+                ("xslice_slices", C.c_int32), ("xslice_partial", C.c_int32), ("xslice_window", C.c_int32),
+                ("xslice_reserved", C.c_int32), ("xslice_mb", C.c_double),
+                ("stencil7_impl", C.c_int32), ("stencil7_store", C.c_int32), ("stencil7_ry", C.c_int32),
+                ("stencil7_nj", C.c_int32), ("stencil7_zc", C.c_int32), ("stencil7_pf", C.c_int32),
+                ("stencil7_blocks", C.c_int32), ("blur_x_rows", C.c_int32), ("blur_y_vec", C.c_int32),
+                ("blur_y_rows", C.c_int32), ("dist_exchange", C.c_int32), ("dist_broadcast", C.c_int32),
+                ("dist_world1", C.c_int32), ("reserved", C.c_int32 * 7)]
+
+    def __init__(self, **kw):
+        super().__init__()
+        lib.lhpc_options_init(C.byref(self))
+        names = {f[0] for f in self._fields_}
+        for k, v in kw.items():
+            if k not in names or k == "struct_size":
+                raise TypeError(f"unknown option {k!r}")
+            setattr(self, k, v)
+
+
+def _opts(o):
+    if o is None:
+        return None
+    if isinstance(o, dict):
+        o = Options(**o)
+    return C.byref(o)
+
+
+XTILE_REDUCE_AUTO, XTILE_REDUCE_PERM, XTILE_REDUCE_IPERM = 0, 1, 2
+S7_AUTO, S7_SIMPLE, S7_RING, S7_RING_X4 = 0, 1, 2, 3
+STORE_AUTO, STORE_PLAIN, STORE_NT, STORE_STAGED = 0, 1, 2, 3
+DIST_EXCHANGE_AUTO, DIST_EXCHANGE_RCCL, DIST_EXCHANGE_P2P, DIST_EXCHANGE_NONE = 0, 1, 2, 3
+XFER_ALLGATHER, XFER_BROADCAST, XFER_PUSH = 1, 2, 3
+
+
+class DistXfer(C.Structure):
+    _fields_ = [("chunk", C.c_int32), ("kind", C.c_int32), ("root", C.c_int32), ("group", C.c_int32),
+                ("offset", C.c_int64), ("count", C.c_int64), ("send_offset", C.c_int64)]
 
 
 class PlanInfo(C.Structure):
@@ -115,6 +164,9 @@ _sig("lhpc_spmv_plan_create", _i, C.POINTER(_p), _i, _i64, _i64, _i64, _p, _i, _
 _sig("lhpc_spmv", _i, _p, _p, _p, _i, _p)
 _sig("lhpc_spmv_plan_create_split", _i, C.POINTER(_p), _i, _i64, _i64, _i64, _p, _i, _p,
      _p, _p, _i, _u, _i, _p)
+_sig("lhpc_spmv_plan_create_opts", _i, C.POINTER(_p), _i, _i64, _i64, _i64, _p, _i, _p,
+     _p, _p, _i, _u, _i, _p, _p)
+_sig("lhpc_options_init", None, _p)
 _sig("lhpc_spmv_stage", _i, _p, _p, _p)
 _sig("lhpc_spmv_range", _i, _p, _i, _p, _p)
 _sig("lhpc_spmv_plan_info_get", _i, _p, C.POINTER(PlanInfo))
@@ -123,6 +175,9 @@ _sig("lhpc_csr_partition_rows", _i, _p, _i, _i64, _i, _p)
 for _n in ("lhpc_blur_x_f32", "lhpc_blur_y_f32"):
     _sig(_n, _i, _p, _p, _i64, _i64, _i64, _i, _i, _p)
 _sig("lhpc_stencil7_f32", _i, _p, _p, _i64, _i64, _i64, _i64, _f, _f, _i, _p)
+for _n in ("lhpc_blur_x_f32_opts", "lhpc_blur_y_f32_opts"):
+    _sig(_n, _i, _p, _p, _i64, _i64, _i64, _i, _i, _p, _p)
+_sig("lhpc_stencil7_f32_planes_opts", _i, _p, _p, _i64, _i64, _i64, _i64, _f, _f, _i64, _i64, _p, _p)
 _sig("lhpc_stencil7_f32_planes", _i, _p, _p, _i64, _i64, _i64, _i64, _f, _f, _i64,
      _i64, _p)
 _sig("lhpc_gen_uniform_row_ptr", _i, _i64, _i, _p)
@@ -155,7 +210,11 @@ _sig("lhpc_dist_comm_info", _i, _p, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i))
 _sig("lhpc_dist_comm_destroy", _i, _p)
 _sig("lhpc_dist_allreduce_sum_f64", _i, _p, _p, _i64, _p)
 _sig("lhpc_dist_spmv_plan_create", _i, C.POINTER(_p), _p, _i, _i64, _i64, _i, _p, _p, _i, _p, _p, _u)
+_sig("lhpc_dist_spmv_plan_create_opts", _i, C.POINTER(_p), _p, _i, _i64, _i64, _i, _p, _p, _i, _p, _p, _u, _p)
 _sig("lhpc_dist_spmv", _i, _p, _p, _p, _p)
+_sig("lhpc_dist_exchange", _i, _p, _p, _p)
+_sig("lhpc_dist_exchange_schedule", _i, _p, _i, _i, _i, _i, _i, _p, _i64, C.POINTER(_i64))
+_sig("lhpc_dist_p2p_reset", _i, _p)
 _sig("lhpc_dist_spmv_plan_destroy", _i, _p)
 _sig("lhpc_dist_stencil7_f32", _i, _p, _p, _p, _i64, _i64, _i64, _i64, _f, _f, _p)
 _sig("lhpc_dist_comm_create_local", _i, C.POINTER(_p), _i, _i, _i)
@@ -219,11 +278,13 @@ class SpMVPlan:
     """
 
     def __init__(self, row_ptr, col_idx, val, n_cols: int, flags: int = 0,
-                 device: Optional[int] = None, splits=None):
+                 device: Optional[int] = None, splits=None, options=None):
         """``splits``: ascending rows in (0, n_rows); the plan is then a
         row-range plan (lhpc_spmv_plan_create_split: stage(x) once, then
         range(k, y_k) per range) and raises LhpcError (LHPC_ERR_UNSUPPORTED)
-        when the matrix does not select the XTILE layout."""
+        when the matrix does not select the XTILE layout.  ``options``: an
+        Options (or dict of its fields) pinning kernel variants
+        (lhpc_spmv_plan_create_opts)."""
         row_ptr = np.ascontiguousarray(row_ptr)
         col_idx = np.ascontiguousarray(col_idx, dtype=np.int32)
         val = np.ascontiguousarray(val)
@@ -241,7 +302,8 @@ class SpMVPlan:
         self.nnz = int(col_idx.shape[0])
         self._h = _p()
         dev = (_i * 1)(device) if device is not None else None
-        if splits is None:
+        self._opts = options if not isinstance(options, dict) else Options(**options)
+        if splits is None and options is None:
             self.splits = None
             _check(lib.lhpc_spmv_plan_create(
                 C.byref(self._h), self.dtype, self.n_rows, self.n_cols, self.nnz,
@@ -249,13 +311,14 @@ class SpMVPlan:
                 col_idx.ctypes.data, val.ctypes.data, dev, 1 if device is not None else 0,
                 flags), "lhpc_spmv_plan_create")
         else:
-            sp = np.ascontiguousarray(splits, dtype=np.int64)
-            self.splits = [0] + [int(v) for v in sp] + [self.n_rows]
-            _check(lib.lhpc_spmv_plan_create_split(
+            sp = np.ascontiguousarray(splits if splits is not None else [], dtype=np.int64)
+            self.splits = None if splits is None else [0] + [int(v) for v in sp] + [self.n_rows]
+            _check(lib.lhpc_spmv_plan_create_opts(
                 C.byref(self._h), self.dtype, self.n_rows, self.n_cols, self.nnz,
                 row_ptr.ctypes.data, 64 if row_ptr.dtype == np.int64 else 32,
                 col_idx.ctypes.data, val.ctypes.data, dev, 1 if device is not None else 0,
-                flags, int(sp.shape[0]), sp.ctypes.data), "lhpc_spmv_plan_create_split")
+                flags, int(sp.shape[0]), sp.ctypes.data if sp.shape[0] else None, _opts(self._opts)),
+                "lhpc_spmv_plan_create_opts")
 
     def info(self) -> dict:
         inf = PlanInfo()
@@ -334,7 +397,7 @@ def padded_shape(dims, ghost):
     return tuple(int(d) + 2 * int(ghost) for d in dims)
 
 
-def _blur(fn, name, a, b, ny, nx, ghost, nblur, stream):
+def _blur(fn, fn_opts, name, a, b, ny, nx, ghost, nblur, stream, options):
     ap, ad = _buf(a, None if _is_torch(a) else np.float32)
     bp, bd = _buf(b, None if _is_torch(b) else np.float32, writable=True)
     if ad != bd:
@@ -342,22 +405,30 @@ def _blur(fn, name, a, b, ny, nx, ghost, nblur, stream):
     if ad and stream is None:
         import torch
         stream = torch.cuda.current_stream(b.device)
-    _check(fn(ap, bp, ny, nx, ghost, nblur, int(ad), _stream_ptr(stream)), name)
+    if options is None:
+        _check(fn(ap, bp, ny, nx, ghost, nblur, int(ad), _stream_ptr(stream)), name)
+    else:
+        _check(fn_opts(ap, bp, ny, nx, ghost, nblur, int(ad), _stream_ptr(stream), _opts(options)), name + "_opts")
     return b
 
 
-def blur_x(a, b, ny: int, nx: int, ghost: int, nblur: int = 8, stream=None):
+def blur_x(a, b, ny: int, nx: int, ghost: int, nblur: int = 8, stream=None, options=None):
     """b(y,x) = Σ_{k=-nblur..nblur} a(y,x+k) (test_hpc_benchmark.cpp:354-368)."""
-    return _blur(lib.lhpc_blur_x_f32, "lhpc_blur_x_f32", a, b, ny, nx, ghost, nblur, stream)
+    return _blur(lib.lhpc_blur_x_f32, lib.lhpc_blur_x_f32_opts, "lhpc_blur_x_f32", a, b, ny, nx, ghost, nblur,
+                 stream, options)
 
 
-def blur_y(a, b, ny: int, nx: int, ghost: int, nblur: int = 8, stream=None):
+def blur_y(a, b, ny: int, nx: int, ghost: int, nblur: int = 8, stream=None, options=None):
     """b(y,x) = Σ_{k=-nblur..nblur} a(y+k,x) (test_hpc_benchmark.cpp:444-457)."""
-    return _blur(lib.lhpc_blur_y_f32, "lhpc_blur_y_f32", a, b, ny, nx, ghost, nblur, stream)
+    return _blur(lib.lhpc_blur_y_f32, lib.lhpc_blur_y_f32_opts, "lhpc_blur_y_f32", a, b, ny, nx, ghost, nblur,
+                 stream, options)
 
 
 def stencil7(u, out, nz: int, ny: int, nx: int, ghost: int = 1, c0: float = -6.0,
-             c1: float = 1.0, stream=None):
+             c1: float = 1.0, stream=None, options=None):
+    """options (device tensors only): lhpc_stencil7_f32_planes_opts over every plane."""
+    if options is not None:
+        return stencil7_planes(u, out, nz, ny, nx, ghost, c0, c1, 0, nz, stream=stream, options=options)
     up, ud = _buf(u, None if _is_torch(u) else np.float32)
     op, od = _buf(out, None if _is_torch(out) else np.float32, writable=True)
     if ud != od:
@@ -370,7 +441,7 @@ def stencil7(u, out, nz: int, ny: int, nx: int, ghost: int = 1, c0: float = -6.0
     return out
 
 
-def stencil7_planes(u, out, nz, ny, nx, ghost, c0, c1, z_begin, z_end, stream=None):
+def stencil7_planes(u, out, nz, ny, nx, ghost, c0, c1, z_begin, z_end, stream=None, options=None):
     up, ud = _buf(u)
     op, od = _buf(out, writable=True)
     if not (ud and od):
@@ -378,8 +449,13 @@ def stencil7_planes(u, out, nz, ny, nx, ghost, c0, c1, z_begin, z_end, stream=No
     if stream is None:
         import torch
         stream = torch.cuda.current_stream(out.device)
-    _check(lib.lhpc_stencil7_f32_planes(up, op, nz, ny, nx, ghost, c0, c1, z_begin, z_end,
-                                        _stream_ptr(stream)), "lhpc_stencil7_f32_planes")
+    if options is None:
+        _check(lib.lhpc_stencil7_f32_planes(up, op, nz, ny, nx, ghost, c0, c1, z_begin, z_end,
+                                            _stream_ptr(stream)), "lhpc_stencil7_f32_planes")
+    else:
+        _check(lib.lhpc_stencil7_f32_planes_opts(up, op, nz, ny, nx, ghost, c0, c1, z_begin, z_end,
+                                                 _stream_ptr(stream), _opts(options)),
+               "lhpc_stencil7_f32_planes_opts")
     return out
 
 
@@ -681,12 +757,18 @@ class DistComm:
         return self
 
     def p2p_export(self, y) -> bytes:
-        """This rank's blob (IPC handles) for the y window (a device tensor)."""
+        """This rank's blob (IPC handles) for a new y window (a device tensor;
+        up to DIST_P2P_MAX_WINDOWS, exported in the same order on every rank)."""
         blob = (C.c_ubyte * DIST_P2P_BLOB_BYTES)()
         _check(lib.lhpc_dist_p2p_export(self._h, y.data_ptr(), y.numel() * y.element_size(), blob),
                "lhpc_dist_p2p_export")
-        self._p2p_y = y  # the window must outlive the mapping
+        self.__dict__.setdefault("_p2p_ys", []).append(y)  # a window must outlive its mapping
         return bytes(blob)
+
+    def p2p_reset(self):
+        """Unmap every window (lhpc_dist_p2p_reset)."""
+        _check(lib.lhpc_dist_p2p_reset(self._h), "lhpc_dist_p2p_reset")
+        self._p2p_ys = []
 
     def p2p_import(self, blobs):
         """Every rank's blob, in rank order."""
@@ -781,6 +863,25 @@ def interleaved_local_csr(row_ptr, col_idx, val, cuts, world: int, K: int, rank:
     return lrp, col, v
 
 
+DIST_P2P_MAX_WINDOWS = 4
+
+
+def dist_exchange_schedule(cuts, nranks: int, K: int, rank: int, exchange: int = DIST_EXCHANGE_RCCL,
+                           broadcast: bool = False):
+    """The transfers lhpc_dist_spmv issues on `rank` (include/lhpc.h
+    lhpc_dist_exchange_schedule): a list of dicts {chunk, kind, root, group,
+    offset, count, send_offset} in issue order."""
+    cuts = np.ascontiguousarray(cuts, dtype=np.int64)
+    if cuts.shape[0] != nranks * K + 1:
+        raise ValueError("cuts must hold nranks*K + 1 rows")
+    cap = nranks * K
+    buf = (DistXfer * max(cap, 1))()
+    n = _i64(0)
+    _check(lib.lhpc_dist_exchange_schedule(cuts.ctypes.data, nranks, K, rank, exchange, int(broadcast), buf, cap,
+                                           C.byref(n)), "lhpc_dist_exchange_schedule")
+    return [{f: getattr(buf[i], f) for f, _ in DistXfer._fields_} for i in range(n.value)]
+
+
 class DistSpMVPlan:
     """y = A·x over ranks with RCCL behind the C ABI (lhpc_dist_spmv_*):
     the rank's K interleaved nnz-balanced blocks, x staged once, chunk k
@@ -789,7 +890,7 @@ class DistSpMVPlan:
     (interleaved_local_csr); ``cuts`` the global world·K+1 cuts."""
 
     def __init__(self, comm: DistComm, n_rows: int, n_cols: int, K: int, cuts, row_ptr, col_idx, val,
-                 flags: int = 0):
+                 flags: int = 0, options=None):
         row_ptr = np.ascontiguousarray(row_ptr)
         col_idx = np.ascontiguousarray(col_idx, dtype=np.int32)
         val = np.ascontiguousarray(val)
@@ -799,10 +900,11 @@ class DistSpMVPlan:
         self.dtype = F32 if val.dtype == np.float32 else F64
         self.n_rows, self.n_cols, self.K, self.comm = int(n_rows), int(n_cols), int(K), comm
         self._h = _p()
-        _check(lib.lhpc_dist_spmv_plan_create(
+        self._opts = options if not isinstance(options, dict) else Options(**options)
+        _check(lib.lhpc_dist_spmv_plan_create_opts(
             C.byref(self._h), comm._h, self.dtype, self.n_rows, self.n_cols, self.K, self.cuts.ctypes.data,
             row_ptr.ctypes.data, 64 if row_ptr.dtype == np.int64 else 32, col_idx.ctypes.data, val.ctypes.data,
-            flags), "lhpc_dist_spmv_plan_create")
+            flags, _opts(self._opts)), "lhpc_dist_spmv_plan_create_opts")
 
     def __call__(self, x, y=None, stream=None):
         """Full y (n_rows) on every rank from the full x (device tensors)."""
@@ -812,6 +914,14 @@ class DistSpMVPlan:
         if stream is None:
             stream = torch.cuda.current_stream(x.device)
         _check(lib.lhpc_dist_spmv(self._h, x.data_ptr(), y.data_ptr(), _stream_ptr(stream)), "lhpc_dist_spmv")
+        return y
+
+    def exchange(self, y, stream=None):
+        """The call's y exchange alone (every chunk; lhpc_dist_exchange)."""
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream(y.device)
+        _check(lib.lhpc_dist_exchange(self._h, y.data_ptr(), _stream_ptr(stream)), "lhpc_dist_exchange")
         return y
 
     def close(self):

@@ -10,6 +10,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/lhpc.h"
 
@@ -28,6 +29,22 @@
 namespace lhpc {
 
 constexpr int kWave = 64;  // CDNA wavefront; never 32
+
+// Variant options (include/lhpc.h lhpc_options): the caller's struct copied
+// over a zeroed one (struct_size bytes, so an older caller's shorter struct
+// leaves the newer fields automatic); NULL = all automatic.  The product
+// build reads no process environment.  A tuning build (-DLHPC_TUNING_ENV,
+// `make tuning`: the A/B scripts under tools/ only) lets LHPC_* variables
+// override fields, so one binary can be swept without recompiling.
+lhpc_options resolve_options(const lhpc_options *in);  // lhpc_runtime.hip
+inline const char *tuning_env(const char *name) {
+#ifdef LHPC_TUNING_ENV
+  return std::getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 // Host-side phase ranges (plan build, stage, range, collectives …), visible
 // to `rocprofv3 --marker-trace` — the reference marks its sort phases with

@@ -17,14 +17,18 @@
 //          nranks in-place ncclBroadcast (root r sends block k·nranks + r;
 //          exact slices, no padding) fills every rank's y while the compute
 //          stream reduces chunk k+1.  y is then the next x on every rank.
-//          Opt-in direct peer exchange (SURVEY §8e "Optimisation"): with a
-//          registered y window (lhpc_dist_p2p_export/_import: IPC handles of
-//          every rank's y), chunk k's block is pushed by one kernel straight
-//          into every peer's y over xGMI instead of the broadcasts; per call a
-//          READY flag (this rank's y may be overwritten) and a DONE flag
-//          (this rank's pushes have landed) go to every peer, and the comm
-//          stream waits for all peers' flags with a bounded spin.  Needs no
-//          RCCL communicator (lhpc_dist_comm_create_local).
+//          Direct peer exchange (SURVEY §8e "Optimisation"): with registered
+//          y windows (lhpc_dist_p2p_export/_import: IPC handles of every
+//          rank's y; up to four, so a ping-pong pair works), chunk k's block
+//          is pushed by one kernel straight into every peer's y over xGMI
+//          instead of the collectives; per call a READY flag (this rank's y
+//          may be overwritten) and a DONE flag (this rank's pushes have
+//          landed) go to every peer, and the comm stream waits for all
+//          peers' flags with a bounded spin.  Needs no RCCL communicator
+//          (lhpc_dist_comm_create_local).  The exchange is a plan option
+//          (lhpc_options.dist_exchange: automatic = peer stores when y is a
+//          window).  Both exchanges issue the transfers of one host
+//          schedule (lhpc_dist_exchange_schedule), which the CPU tests run.
 //   stencil z-slabs with one halo plane per side: ncclSend/ncclRecv to the
 //          z neighbours on the comm stream while the interior planes are
 //          computed; the two boundary planes after the exchange.
@@ -49,48 +53,99 @@
 
 static_assert(sizeof(ncclUniqueId) == LHPC_DIST_UNIQUE_ID_BYTES, "ncclUniqueId is 128 bytes");
 
+// a registered peer-exchange window: one y buffer, mapped on every rank
+struct P2pWindow {
+  void *buf = nullptr;              // this rank's y (caller-owned)
+  size_t bytes = 0;
+  bool ready = false;               // imported: every peer's copy is mapped
+  std::vector<void *> peer_base;    // hipIpcOpenMemHandle results (closed on reset)
+  void **d_peer_buf = nullptr;      // [nranks] device table of peer pointers (self: own)
+  uint64_t narrow = 0;              // bit p: peer p's y has another 16-B phase → 4-B stores
+};
+
 struct lhpc_dist_comm {
   ncclComm_t comm = nullptr;  // null for a local (P2P-only) communicator
   int nranks = 1, rank = 0, device = 0;
   hipStream_t s_comm = nullptr;
-  // P2P window: this rank's y (caller-owned) and flags [READY(nranks) |
-  // DONE(nranks)] (owned, uncached device memory), the peers' mapped views
-  void *p2p_buf = nullptr;
-  size_t p2p_bytes = 0;
+  // P2P: flags [READY(nranks) | DONE(nranks)] (owned, uncached device
+  // memory) shared by every window, the peers' mapped flag arrays, and the
+  // windows in export order
   uint32_t *flags = nullptr;
-  bool p2p_ready = false;
-  std::vector<void *> peer_base, peer_flags_base;  // hipIpcOpenMemHandle results (closed at destroy)
-  void **d_peer_buf = nullptr;                     // [nranks] device arrays of peer pointers (self: own)
+  std::vector<void *> peer_flags_base;
   uint32_t **d_peer_flags = nullptr;
-  uint32_t *h_status = nullptr;                    // host-mapped: bit 0 = a flag wait timed out
+  bool flags_mapped = false;
+  uint32_t *h_status = nullptr;  // host-mapped: bit 0 = a flag wait timed out
   uint32_t epoch = 0;
+  P2pWindow win[LHPC_DIST_P2P_MAX_WINDOWS];
+  int n_win = 0;
 };
 
 struct lhpc_dist_spmv_plan {
   lhpc_dist_comm *comm = nullptr;
   int dtype = LHPC_F32, K = 1;
   int64_t n_rows = 0, n_cols = 0;
+  lhpc_options opt{};                       // resolved: the dist_* fields pick the exchange
   std::vector<int64_t> cuts;                // nranks·K + 1 global row cuts
   lhpc_spmv_plan *split = nullptr;          // row-range plan over the rank's blocks (XTILE)
   std::vector<int> range_of;                // block k → range index of `split` (−1: empty block)
   std::vector<lhpc_spmv_plan *> block_plan; // otherwise one plan per non-empty block
+  // the exchange schedules (lhpc_dist_exchange_schedule), entries of chunk k
+  // at [first[k], first[k+1])
+  std::vector<lhpc_dist_xfer> sched_rccl, sched_p2p;
+  std::vector<int64_t> first_rccl, first_p2p;
   std::vector<hipEvent_t> ev;               // [K] chunk k reduced
-  hipEvent_t done = nullptr;                // last broadcast issued on the comm stream
+  hipEvent_t done = nullptr;                // last exchange issued on the comm stream
   hipEvent_t ev_p2p = nullptr;              // P2P: READY signalled on the compute stream
-  bool force_bcast = false;                 // LHPC_DIST_BCAST=1: broadcasts even for equal blocks (tests)
-  bool exchange_always = false;             // LHPC_DIST_EXCHANGE=1: run the RCCL exchange at world 1 (tests)
 };
 
 namespace {
 
 ncclDataType_t nccl_dt(int dtype) { return dtype == LHPC_F64 ? ncclFloat64 : ncclFloat32; }
 
-// ---- P2P window kernels
+// the schedule of every chunk (see include/lhpc.h lhpc_dist_exchange_schedule)
+int build_schedule(const int64_t *cuts, int nranks, int K, int rank, int exchange, int broadcast,
+                   std::vector<lhpc_dist_xfer> &out, std::vector<int64_t> &first) {
+  out.clear();
+  first.assign(static_cast<size_t>(K) + 1, 0);
+  for (int k = 0; k < K; ++k) {
+    first[k] = static_cast<int64_t>(out.size());
+    const int64_t b0 = static_cast<int64_t>(k) * nranks;
+    if (exchange == LHPC_DIST_EXCHANGE_P2P) {
+      const int64_t b = b0 + rank, cnt = cuts[b + 1] - cuts[b];
+      if (cnt > 0) out.push_back(lhpc_dist_xfer{k, LHPC_XFER_PUSH, rank, 0, cuts[b], cnt, cuts[b]});
+      continue;
+    }
+    const int64_t cnt0 = cuts[b0 + 1] - cuts[b0];
+    bool equal = !broadcast;
+    for (int r = 1; r < nranks && equal; ++r) equal = cuts[b0 + r + 1] - cuts[b0 + r] == cnt0;
+    if (equal) {
+      // uniform rows: the nnz-balanced cuts are equal-row cuts (C2/C3)
+      if (cnt0 > 0) out.push_back(lhpc_dist_xfer{k, LHPC_XFER_ALLGATHER, -1, 0, cuts[b0], cnt0, cuts[b0 + rank]});
+      continue;
+    }
+    for (int r = 0; r < nranks; ++r) {  // exact slices, no padding
+      const int64_t cnt = cuts[b0 + r + 1] - cuts[b0 + r];
+      if (cnt > 0) out.push_back(lhpc_dist_xfer{k, LHPC_XFER_BROADCAST, r, 1, cuts[b0 + r], cnt, cuts[b0 + r]});
+    }
+  }
+  first[K] = static_cast<int64_t>(out.size());
+  return LHPC_OK;
+}
+
+// ---- P2P window kernels.  Every kernel of a call reads the status word
+// first: once a wait has timed out, pushes and DONE flags are skipped (the
+// peers then time out as well), so no rank writes into a peer that never
+// declared its y free, and no call reports a half-exchanged y as done.
+__device__ __forceinline__ bool p2p_failed(const uint32_t *status) {
+  return __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+}
 // flag store into every peer's flag array at `slot` (READY: rank, DONE:
 // nranks + rank), release at system scope: everything this stream did
 // before is visible to the peer first
-__global__ void k_p2p_signal(uint32_t *const *peer_flags, int slot, uint32_t e, int nranks, int self) {
+__global__ void k_p2p_signal(uint32_t *const *peer_flags, int slot, uint32_t e, int nranks, int self,
+                             const uint32_t *status) {
   const int p = threadIdx.x;
+  if (p2p_failed(status)) return;
   if (p < nranks && p != self) __hip_atomic_store(peer_flags[p] + slot, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // wait until every peer's flag at base + p reached epoch e; bounded (~8 s):
@@ -101,28 +156,33 @@ __global__ void k_p2p_wait(const uint32_t *flags, int base, uint32_t e, int nran
   for (uint32_t spins = 0;; ++spins) {
     const uint32_t f = __hip_atomic_load(flags + base + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
     if (static_cast<int32_t>(f - e) >= 0) return;
-    if (spins > (1u << 21)) {
+    if (spins > (1u << 21) || p2p_failed(status)) {
       __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
     __builtin_amdgcn_s_sleep(127);
   }
 }
-// bytes [o0, o1) of this rank's y into the same bytes of every peer's y
-// (offsets are multiples of 4; 16-B stores where both sides are aligned —
-// every y has the same alignment); blockIdx.y = peer
+// bytes [o0, o1) of this rank's y into the same bytes of every peer's y;
+// offsets are multiples of 4.  16-B stores on [a0, a1) (the 16-B aligned
+// interior) for peers whose y has our 16-B phase, head [o0, a0) and tail
+// [a1, o1) as words; a peer with another phase (bit p of `narrow`) gets
+// words throughout.  blockIdx.y = peer
 __global__ __launch_bounds__(256) void k_p2p_push(void *const *peer_buf, const unsigned char *y, int64_t o0,
-                                                  int64_t o1, int self) {
+                                                  int64_t o1, int self, uint64_t narrow, const uint32_t *status) {
+  if (p2p_failed(status)) return;
   const int p = static_cast<int>(blockIdx.y) + (static_cast<int>(blockIdx.y) >= self ? 1 : 0);
   unsigned char *dst = static_cast<unsigned char *>(peer_buf[p]);
-  int64_t a0 = (o0 + 15) & ~int64_t{15}, a1 = o1 & ~int64_t{15};
-  if (a0 > a1) a0 = a1 = o1;
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x, T = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  const uintptr_t yb = reinterpret_cast<uintptr_t>(y);
+  int64_t a0 = static_cast<int64_t>(((yb + o0 + 15) & ~uintptr_t{15}) - yb);
+  int64_t a1 = static_cast<int64_t>(((yb + o1) & ~uintptr_t{15}) - yb);
+  if ((narrow >> p) & 1u || a0 >= a1) a0 = a1 = o1;  // words only
   for (int64_t i = o0 + 4 * t; i < a0; i += 4 * T)  // head words
     *reinterpret_cast<uint32_t *>(dst + i) = *reinterpret_cast<const uint32_t *>(y + i);
   for (int64_t i = a0 + 16 * t; i < a1; i += 16 * T)
     *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(y + i);
-  for (int64_t i = (a1 > a0 ? a1 : o1) + 4 * t; i < o1; i += 4 * T)  // tail words
+  for (int64_t i = a1 + 4 * t; i < o1; i += 4 * T)  // tail words
     *reinterpret_cast<uint32_t *>(dst + i) = *reinterpret_cast<const uint32_t *>(y + i);
   __threadfence_system();
 }
@@ -132,35 +192,53 @@ struct P2pBlob {  // LHPC_DIST_P2P_BLOB_BYTES per rank
   int64_t offset;  // y − its allocation's base
   int64_t bytes;
   uint64_t magic;
+  int32_t window;  // export order
+  int32_t nranks;
 };
 static_assert(sizeof(P2pBlob) <= LHPC_DIST_P2P_BLOB_BYTES, "blob size");
-constexpr uint64_t kP2pMagic = 0x6c687063705032ull;  // "lhpcP2"
+constexpr uint64_t kP2pMagic = 0x6c687063705033ull;  // "lhpcP3"
+
+void window_release(P2pWindow &w) {
+  for (void *b : w.peer_base)
+    if (b) (void)hipIpcCloseMemHandle(b);
+  w.peer_base.clear();
+  if (w.d_peer_buf) (void)hipFree(w.d_peer_buf);
+  w = P2pWindow{};
+}
 
 void p2p_release(lhpc_dist_comm *c) {
-  for (void *b : c->peer_base)
-    if (b) (void)hipIpcCloseMemHandle(b);
+  for (int i = 0; i < c->n_win; ++i) window_release(c->win[i]);
+  c->n_win = 0;
   for (void *b : c->peer_flags_base)
     if (b) (void)hipIpcCloseMemHandle(b);
-  c->peer_base.clear();
   c->peer_flags_base.clear();
-  if (c->d_peer_buf) (void)hipFree(c->d_peer_buf);
   if (c->d_peer_flags) (void)hipFree(c->d_peer_flags);
   if (c->flags) (void)hipFree(c->flags);
   if (c->h_status) (void)hipHostFree(c->h_status);
-  c->d_peer_buf = nullptr;
   c->d_peer_flags = nullptr;
   c->flags = nullptr;
   c->h_status = nullptr;
-  c->p2p_buf = nullptr;
-  c->p2p_ready = false;
+  c->flags_mapped = false;
+  c->epoch = 0;
 }
 
-// the P2P exchange of one call (see the header comment); s = compute stream
+// the ready window whose buffer is y, or null
+const P2pWindow *find_window(const lhpc_dist_comm *c, const void *y, size_t need) {
+  for (int i = 0; i < c->n_win; ++i)
+    if (c->win[i].ready && c->win[i].buf == y && c->win[i].bytes >= need) return &c->win[i];
+  return nullptr;
+}
+
+// the P2P exchange of one call (see the header comment); s = compute stream.
+// The host check of the status word sees the timeouts of calls that have
+// completed (the caller synchronised); a timeout still in flight is caught on
+// the device (the kernels skip) and by the next synchronised check.
 int p2p_exchange_begin(lhpc_dist_comm *c, hipStream_t s, hipEvent_t ev) {
+  if (*c->h_status) return LHPC_ERR_INTERNAL;  // an earlier flag wait timed out
   ++c->epoch;
   if (c->epoch == 0) c->epoch = 1;
-  if (*c->h_status) return LHPC_ERR_INTERNAL;  // an earlier flag wait timed out
-  hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(64), 0, s, c->d_peer_flags, c->rank, c->epoch, c->nranks, c->rank);
+  hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(64), 0, s, c->d_peer_flags, c->rank, c->epoch, c->nranks, c->rank,
+                     c->h_status);
   LHPC_HIP_TRY(hipGetLastError());
   LHPC_HIP_TRY(hipEventRecord(ev, s));
   LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, ev, 0));
@@ -169,18 +247,19 @@ int p2p_exchange_begin(lhpc_dist_comm *c, hipStream_t s, hipEvent_t ev) {
   return static_cast<int>(hipGetLastError());
 }
 
-int p2p_push(lhpc_dist_comm *c, int64_t o0, int64_t o1) {
+int p2p_push(lhpc_dist_comm *c, const P2pWindow *w, int64_t o0, int64_t o1) {
   if (o1 <= o0 || c->nranks < 2) return LHPC_OK;
   const int64_t vec = (o1 - o0) / 16 + 1;
   const unsigned bx = static_cast<unsigned>(std::min<int64_t>(64, (vec + 255) / 256));
   hipLaunchKernelGGL(k_p2p_push, dim3(bx, static_cast<unsigned>(c->nranks - 1)), dim3(256), 0, c->s_comm,
-                     c->d_peer_buf, static_cast<const unsigned char *>(c->p2p_buf), o0, o1, c->rank);
+                     w->d_peer_buf, static_cast<const unsigned char *>(w->buf), o0, o1, c->rank, w->narrow,
+                     c->h_status);
   return static_cast<int>(hipGetLastError());
 }
 
 int p2p_exchange_end(lhpc_dist_comm *c) {
   hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(64), 0, c->s_comm, c->d_peer_flags, c->nranks + c->rank, c->epoch,
-                     c->nranks, c->rank);
+                     c->nranks, c->rank, c->h_status);
   LHPC_HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_p2p_wait, dim3(1), dim3(64), 0, c->s_comm, c->flags, c->nranks, c->epoch, c->nranks, c->rank,
                      c->h_status);
@@ -200,41 +279,89 @@ void destroy_spmv(lhpc_dist_spmv_plan *d) {
   delete d;
 }
 
-// the exchange of chunk k: every rank's block k·nranks + r to every rank.
-// Blocks k·nranks … k·nranks + nranks − 1 are contiguous in y; when they are
-// all the same size (uniform rows: nnz-balanced cuts are equal-row cuts, as
-// for C2/C3) it is one in-place ncclAllGather, else a group of in-place
-// ncclBroadcast (root r sends its block; exact slices, no padding)
-int broadcast_chunk(const lhpc_dist_spmv_plan *d, int k, void *y, hipStream_t cs) {
+// chunk k's RCCL transfers from the schedule: one in-place all-gather, or
+// one group of in-place broadcasts (root r sends its block)
+int issue_rccl_chunk(const lhpc_dist_spmv_plan *d, int k, void *y, hipStream_t cs) {
   const lhpc_dist_comm *c = d->comm;
   const size_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
-  const int64_t b0 = static_cast<int64_t>(k) * c->nranks, cnt0 = d->cuts[b0 + 1] - d->cuts[b0];
-  bool equal = !d->force_bcast;
-  for (int r = 1; r < c->nranks && equal; ++r) equal = d->cuts[b0 + r + 1] - d->cuts[b0 + r] == cnt0;
-  if (equal) {
-    if (cnt0 == 0) return LHPC_OK;
-    unsigned char *base = static_cast<unsigned char *>(y) + d->cuts[b0] * tsz;
-    LHPC_NCCL_TRY(ncclAllGather(base + static_cast<size_t>(c->rank) * cnt0 * tsz, base, static_cast<size_t>(cnt0),
-                                nccl_dt(d->dtype), c->comm, cs));
-    return LHPC_OK;
-  }
-  LHPC_NCCL_TRY(ncclGroupStart());
-  for (int r = 0; r < c->nranks; ++r) {
-    const int64_t b = static_cast<int64_t>(k) * c->nranks + r;
-    const int64_t cnt = d->cuts[b + 1] - d->cuts[b];
-    if (cnt <= 0) continue;
-    void *p = static_cast<unsigned char *>(y) + d->cuts[b] * tsz;
-    const ncclResult_t st = ncclBroadcast(p, p, static_cast<size_t>(cnt), nccl_dt(d->dtype), r, c->comm, cs);
+  unsigned char *yb = static_cast<unsigned char *>(y);
+  const int64_t e0 = d->first_rccl[k], e1 = d->first_rccl[k + 1];
+  if (e1 == e0) return LHPC_OK;
+  const bool group = d->sched_rccl[e0].group != 0;
+  if (group) LHPC_NCCL_TRY(ncclGroupStart());
+  for (int64_t e = e0; e < e1; ++e) {
+    const lhpc_dist_xfer &x = d->sched_rccl[e];
+    ncclResult_t st;
+    if (x.kind == LHPC_XFER_ALLGATHER)
+      st = ncclAllGather(yb + x.send_offset * tsz, yb + x.offset * tsz, static_cast<size_t>(x.count),
+                         nccl_dt(d->dtype), c->comm, cs);
+    else
+      st = ncclBroadcast(yb + x.offset * tsz, yb + x.offset * tsz, static_cast<size_t>(x.count), nccl_dt(d->dtype),
+                         x.root, c->comm, cs);
     if (st != ncclSuccess) {
-      (void)ncclGroupEnd();
+      if (group) (void)ncclGroupEnd();
       return LHPC_RCCL_STATUS_BASE + static_cast<int>(st);
     }
   }
-  LHPC_NCCL_TRY(ncclGroupEnd());
+  if (group) LHPC_NCCL_TRY(ncclGroupEnd());
   return LHPC_OK;
 }
 
+// which exchange a call with this y runs (LHPC_DIST_EXCHANGE_NONE: none);
+// *win = the peer window for P2P
+int pick_exchange(const lhpc_dist_spmv_plan *d, const void *y, const P2pWindow **win) {
+  const lhpc_dist_comm *c = d->comm;
+  const size_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
+  const P2pWindow *w = c->nranks > 1 ? find_window(c, y, static_cast<size_t>(d->n_rows) * tsz) : nullptr;
+  *win = nullptr;
+  int x = d->opt.dist_exchange;
+  if (x == LHPC_DIST_EXCHANGE_NONE) return x;
+  if (c->nranks == 1) return d->opt.dist_world1 && c->comm ? LHPC_DIST_EXCHANGE_RCCL : LHPC_DIST_EXCHANGE_NONE;
+  if (x == LHPC_DIST_EXCHANGE_AUTO) x = w ? LHPC_DIST_EXCHANGE_P2P : LHPC_DIST_EXCHANGE_RCCL;
+  if (x == LHPC_DIST_EXCHANGE_P2P) {
+    if (!w) return LHPC_ERR_INVALID_ARG;  // y is not a registered window
+    *win = w;
+    return x;
+  }
+  return c->comm ? LHPC_DIST_EXCHANGE_RCCL : LHPC_ERR_INVALID_ARG;  // a local comm has no RCCL
+}
+
+// chunk k's exchange on the comm stream, after the compute stream's event
+int exchange_chunk(lhpc_dist_spmv_plan *d, int xk, const P2pWindow *w, int k, void *y, hipStream_t s) {
+  lhpc_dist_comm *c = d->comm;
+  LHPC_HIP_TRY(hipEventRecord(d->ev[k], s));
+  LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, d->ev[k], 0));
+  lhpc::RocTxRange rb("lhpc_dist_spmv: y chunk exchange");
+  if (xk == LHPC_DIST_EXCHANGE_P2P) {
+    const int64_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
+    for (int64_t e = d->first_p2p[k]; e < d->first_p2p[k + 1]; ++e) {
+      const lhpc_dist_xfer &x = d->sched_p2p[e];
+      LHPC_TRY(p2p_push(c, w, x.offset * tsz, (x.offset + x.count) * tsz));
+    }
+    return LHPC_OK;
+  }
+  return issue_rccl_chunk(d, k, y, c->s_comm);
+}
+
 }  // namespace
+
+extern "C" int lhpc_dist_exchange_schedule(const int64_t *cuts, int nranks, int K, int rank, int exchange,
+                                           int broadcast, lhpc_dist_xfer *out, int64_t max_out, int64_t *n_out) {
+  if (!cuts || nranks < 1 || K < 1 || rank < 0 || rank >= nranks || !n_out || max_out < 0 || (max_out > 0 && !out) ||
+      (exchange != LHPC_DIST_EXCHANGE_RCCL && exchange != LHPC_DIST_EXCHANGE_P2P))
+    return LHPC_ERR_INVALID_ARG;
+  const int64_t nb = static_cast<int64_t>(nranks) * K;
+  if (cuts[0] != 0) return LHPC_ERR_INVALID_ARG;
+  for (int64_t b = 0; b < nb; ++b)
+    if (cuts[b + 1] < cuts[b]) return LHPC_ERR_INVALID_ARG;
+  std::vector<lhpc_dist_xfer> v;
+  std::vector<int64_t> first;
+  LHPC_TRY(build_schedule(cuts, nranks, K, rank, exchange, broadcast, v, first));
+  *n_out = static_cast<int64_t>(v.size());
+  if (static_cast<int64_t>(v.size()) > max_out) return LHPC_ERR_INVALID_ARG;
+  if (!v.empty()) std::memcpy(out, v.data(), v.size() * sizeof(lhpc_dist_xfer));
+  return LHPC_OK;
+}
 
 extern "C" int lhpc_dist_get_unique_id(unsigned char *id_out) {
   if (!id_out) return LHPC_ERR_INVALID_ARG;
@@ -291,63 +418,112 @@ extern "C" int lhpc_dist_comm_create_local(lhpc_dist_comm **out, int nranks, int
 
 extern "C" int lhpc_dist_p2p_export(lhpc_dist_comm *c, void *y, int64_t bytes, unsigned char *blob_out) {
   if (!c || !y || bytes <= 0 || bytes % 4 || !blob_out || c->nranks > 64) return LHPC_ERR_INVALID_ARG;
+  if (c->n_win >= LHPC_DIST_P2P_MAX_WINDOWS) return LHPC_ERR_UNSUPPORTED;
+  for (int i = 0; i < c->n_win; ++i)
+    if (c->win[i].buf == y) return LHPC_ERR_INVALID_ARG;  // already a window
   lhpc::RocTxRange rx("lhpc_dist_p2p_export");
   LHPC_HIP_TRY(hipSetDevice(c->device));
-  p2p_release(c);
   P2pBlob b{};
   void *base = nullptr;
   size_t size = 0;
   LHPC_HIP_TRY(hipMemGetAddressRange(reinterpret_cast<hipDeviceptr_t *>(&base), &size, y));
   if (static_cast<unsigned char *>(y) + bytes > static_cast<unsigned char *>(base) + size) return LHPC_ERR_INVALID_ARG;
   LHPC_HIP_TRY(hipIpcGetMemHandle(&b.buf, base));
+  if (!c->flags) {
+    // flags: uncached, so a peer's store is seen by the next poll; zeroed
+    LHPC_HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void **>(&c->flags), 2 * 64 * sizeof(uint32_t),
+                                       hipDeviceMallocUncached));
+    LHPC_HIP_TRY(hipMemset(c->flags, 0, 2 * 64 * sizeof(uint32_t)));
+    LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_status), sizeof(uint32_t), hipHostMallocMapped));
+    *c->h_status = 0;
+    c->epoch = 0;
+  }
+  LHPC_HIP_TRY(hipIpcGetMemHandle(&b.flags, c->flags));
   b.offset = static_cast<unsigned char *>(y) - static_cast<unsigned char *>(base);
   b.bytes = bytes;
   b.magic = kP2pMagic;
-  // flags: uncached, so a peer's store is seen by the next poll; zeroed
-  LHPC_HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void **>(&c->flags), 2 * 64 * sizeof(uint32_t),
-                                     hipDeviceMallocUncached));
-  LHPC_HIP_TRY(hipMemset(c->flags, 0, 2 * 64 * sizeof(uint32_t)));
-  LHPC_HIP_TRY(hipIpcGetMemHandle(&b.flags, c->flags));
-  LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_status), sizeof(uint32_t), hipHostMallocMapped));
-  *c->h_status = 0;
-  c->p2p_buf = y;
-  c->p2p_bytes = static_cast<size_t>(bytes);
-  c->epoch = 0;
+  b.window = c->n_win;
+  b.nranks = c->nranks;
+  P2pWindow &w = c->win[c->n_win++];
+  w = P2pWindow{};
+  w.buf = y;
+  w.bytes = static_cast<size_t>(bytes);
   std::memset(blob_out, 0, LHPC_DIST_P2P_BLOB_BYTES);
   std::memcpy(blob_out, &b, sizeof(b));
   return LHPC_OK;
 }
 
 extern "C" int lhpc_dist_p2p_import(lhpc_dist_comm *c, const unsigned char *blobs) {
-  if (!c || !blobs || !c->p2p_buf || !c->flags) return LHPC_ERR_INVALID_ARG;
+  if (!c || !blobs || !c->flags) return LHPC_ERR_INVALID_ARG;
   lhpc::RocTxRange rx("lhpc_dist_p2p_import");
   LHPC_HIP_TRY(hipSetDevice(c->device));
   const int nr = c->nranks;
+  std::vector<P2pBlob> bl(static_cast<size_t>(nr));
+  for (int r = 0; r < nr; ++r) std::memcpy(&bl[r], blobs + static_cast<size_t>(r) * LHPC_DIST_P2P_BLOB_BYTES, sizeof(P2pBlob));
+  const int wi = bl[c->rank].window;
+  if (wi < 0 || wi >= c->n_win) return LHPC_ERR_INVALID_ARG;
+  P2pWindow &w = c->win[wi];
+  if (w.ready) return LHPC_ERR_INVALID_ARG;  // imported already
+  for (int r = 0; r < nr; ++r)
+    if (bl[r].magic != kP2pMagic || bl[r].window != wi || bl[r].nranks != nr || static_cast<size_t>(bl[r].bytes) != w.bytes)
+      return LHPC_ERR_INVALID_ARG;  // every rank must export the same windows in the same order
+  // open everything first; on any failure close what this call opened
+  std::vector<void *> pb(static_cast<size_t>(nr), nullptr), pf(static_cast<size_t>(nr), nullptr);
+  void **d_buf = nullptr;
+  uint32_t **d_flg = nullptr;
+  auto undo = [&](int st) {
+    for (int r = 0; r < nr; ++r) {
+      if (pb[r]) (void)hipIpcCloseMemHandle(pb[r]);
+      if (pf[r]) (void)hipIpcCloseMemHandle(pf[r]);
+    }
+    if (d_buf) (void)hipFree(d_buf);
+    if (d_flg) (void)hipFree(d_flg);
+    return st;
+  };
   std::vector<void *> bufs(static_cast<size_t>(nr), nullptr), flg(static_cast<size_t>(nr), nullptr);
-  c->peer_base.assign(static_cast<size_t>(nr), nullptr);
-  c->peer_flags_base.assign(static_cast<size_t>(nr), nullptr);
+  uint64_t narrow = 0;
+  const uintptr_t my_phase = reinterpret_cast<uintptr_t>(w.buf) & 15;
   for (int r = 0; r < nr; ++r) {
-    P2pBlob b;
-    std::memcpy(&b, blobs + static_cast<size_t>(r) * LHPC_DIST_P2P_BLOB_BYTES, sizeof(b));
-    if (b.magic != kP2pMagic || static_cast<size_t>(b.bytes) != c->p2p_bytes) return LHPC_ERR_INVALID_ARG;
     if (r == c->rank) {
-      bufs[r] = c->p2p_buf;
+      bufs[r] = w.buf;
       flg[r] = c->flags;
       continue;
     }
-    void *pb = nullptr, *pf = nullptr;
-    LHPC_HIP_TRY(hipIpcOpenMemHandle(&pb, b.buf, hipIpcMemLazyEnablePeerAccess));
-    c->peer_base[r] = pb;
-    LHPC_HIP_TRY(hipIpcOpenMemHandle(&pf, b.flags, hipIpcMemLazyEnablePeerAccess));
-    c->peer_flags_base[r] = pf;
-    bufs[r] = static_cast<unsigned char *>(pb) + b.offset;
-    flg[r] = pf;
+    hipError_t e = hipIpcOpenMemHandle(&pb[r], bl[r].buf, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return undo(static_cast<int>(e));
+    bufs[r] = static_cast<unsigned char *>(pb[r]) + bl[r].offset;
+    if ((reinterpret_cast<uintptr_t>(bufs[r]) & 15) != my_phase) narrow |= uint64_t{1} << r;
+    if (!c->flags_mapped) {
+      e = hipIpcOpenMemHandle(&pf[r], bl[r].flags, hipIpcMemLazyEnablePeerAccess);
+      if (e != hipSuccess) return undo(static_cast<int>(e));
+      flg[r] = pf[r];
+    }
   }
-  LHPC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_peer_buf), nr * sizeof(void *)));
-  LHPC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_peer_flags), nr * sizeof(void *)));
-  LHPC_HIP_TRY(hipMemcpy(c->d_peer_buf, bufs.data(), nr * sizeof(void *), hipMemcpyHostToDevice));
-  LHPC_HIP_TRY(hipMemcpy(c->d_peer_flags, flg.data(), nr * sizeof(void *), hipMemcpyHostToDevice));
-  c->p2p_ready = true;
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(&d_buf), nr * sizeof(void *));
+  if (e == hipSuccess) e = hipMemcpy(d_buf, bufs.data(), nr * sizeof(void *), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !c->flags_mapped) {
+    e = hipMalloc(reinterpret_cast<void **>(&d_flg), nr * sizeof(void *));
+    if (e == hipSuccess) e = hipMemcpy(d_flg, flg.data(), nr * sizeof(void *), hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) return undo(static_cast<int>(e));
+  // commit
+  w.peer_base = pb;
+  w.d_peer_buf = d_buf;
+  w.narrow = narrow;
+  w.ready = true;
+  if (!c->flags_mapped) {
+    c->peer_flags_base = pf;
+    c->d_peer_flags = d_flg;
+    c->flags_mapped = true;
+  }
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_p2p_reset(lhpc_dist_comm *c) {
+  if (!c) return LHPC_ERR_INVALID_ARG;
+  LHPC_HIP_TRY(hipSetDevice(c->device));
+  if (c->s_comm) LHPC_HIP_TRY(hipStreamSynchronize(c->s_comm));
+  p2p_release(c);
   return LHPC_OK;
 }
 
@@ -389,10 +565,10 @@ extern "C" int lhpc_dist_allreduce_sum_f64(lhpc_dist_comm *c, double *buf, int64
   return LHPC_OK;
 }
 
-extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_comm *comm, int dtype,
-                                          int64_t n_rows, int64_t n_cols, int K, const int64_t *cuts,
-                                          const void *row_ptr, int row_ptr_bits, const int32_t *col_idx,
-                                          const void *val, unsigned flags) {
+extern "C" int lhpc_dist_spmv_plan_create_opts(lhpc_dist_spmv_plan **out, lhpc_dist_comm *comm, int dtype,
+                                               int64_t n_rows, int64_t n_cols, int K, const int64_t *cuts,
+                                               const void *row_ptr, int row_ptr_bits, const int32_t *col_idx,
+                                               const void *val, unsigned flags, const lhpc_options *opts) {
   if (!out || !comm || !cuts || !row_ptr || K < 1 || n_rows < 0 || n_cols < 0 ||
       (dtype != LHPC_F32 && dtype != LHPC_F64) || (row_ptr_bits != 32 && row_ptr_bits != 64))
     return LHPC_ERR_INVALID_ARG;
@@ -402,6 +578,8 @@ extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_c
   if (cuts[0] != 0 || cuts[nb] != n_rows) return LHPC_ERR_INVALID_ARG;
   for (int64_t b = 0; b < nb; ++b)
     if (cuts[b + 1] < cuts[b]) return LHPC_ERR_INVALID_ARG;
+  const lhpc_options o = lhpc::resolve_options(opts);
+  if (o.dist_exchange < LHPC_DIST_EXCHANGE_AUTO || o.dist_exchange > LHPC_DIST_EXCHANGE_NONE) return LHPC_ERR_INVALID_ARG;
   LHPC_HIP_TRY(hipSetDevice(comm->device));
   auto *d = new (std::nothrow) lhpc_dist_spmv_plan();
   if (!d) return LHPC_ERR_ALLOC;
@@ -410,9 +588,10 @@ extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_c
   d->K = K;
   d->n_rows = n_rows;
   d->n_cols = n_cols;
+  d->opt = o;
   d->cuts.assign(cuts, cuts + nb + 1);
-  if (const char *e = std::getenv("LHPC_DIST_BCAST")) d->force_bcast = std::atoi(e) != 0;
-  if (const char *e = std::getenv("LHPC_DIST_EXCHANGE")) d->exchange_always = std::atoi(e) != 0;
+  build_schedule(cuts, nr, K, rk, LHPC_DIST_EXCHANGE_RCCL, o.dist_broadcast, d->sched_rccl, d->first_rccl);
+  build_schedule(cuts, nr, K, rk, LHPC_DIST_EXCHANGE_P2P, 0, d->sched_p2p, d->first_p2p);
   // the local CSR: the rank's K blocks stacked in chunk order
   std::vector<int64_t> ls(static_cast<size_t>(K) + 1, 0);
   for (int k = 0; k < K; ++k) {
@@ -436,8 +615,9 @@ extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_c
     d->range_of[k] = nrange++;
   }
   if (!splits.empty())
-    st = lhpc_spmv_plan_create_split(&d->split, dtype, n_local, n_cols, nnz_local, row_ptr, row_ptr_bits, col_idx,
-                                     val, &comm->device, 1, flags, static_cast<int>(splits.size()), splits.data());
+    st = lhpc_spmv_plan_create_opts(&d->split, dtype, n_local, n_cols, nnz_local, row_ptr, row_ptr_bits, col_idx,
+                                    val, &comm->device, 1, flags, static_cast<int>(splits.size()), splits.data(),
+                                    &o);
   if (splits.empty() || st == LHPC_ERR_UNSUPPORTED) {
     // one plan per non-empty block (the matrix does not select XTILE, or the
     // rank holds a single block)
@@ -450,9 +630,9 @@ extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_c
       const int64_t e0 = rp_at(r0), e1 = rp_at(r1);
       std::vector<int64_t> lrp(static_cast<size_t>(r1 - r0 + 1));
       for (int64_t i = r0; i <= r1; ++i) lrp[static_cast<size_t>(i - r0)] = rp_at(i) - e0;
-      st = lhpc_spmv_plan_create(&d->block_plan[k], dtype, r1 - r0, n_cols, e1 - e0, lrp.data(), 64,
-                                 col_idx + e0, static_cast<const unsigned char *>(val) + e0 * tsz, &comm->device, 1,
-                                 flags);
+      st = lhpc_spmv_plan_create_opts(&d->block_plan[k], dtype, r1 - r0, n_cols, e1 - e0, lrp.data(), 64,
+                                      col_idx + e0, static_cast<const unsigned char *>(val) + e0 * tsz,
+                                      &comm->device, 1, flags, 0, nullptr, &o);
     }
   }
   if (st == LHPC_OK) {
@@ -470,6 +650,14 @@ extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_c
   return LHPC_OK;
 }
 
+extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_comm *comm, int dtype,
+                                          int64_t n_rows, int64_t n_cols, int K, const int64_t *cuts,
+                                          const void *row_ptr, int row_ptr_bits, const int32_t *col_idx,
+                                          const void *val, unsigned flags) {
+  return lhpc_dist_spmv_plan_create_opts(out, comm, dtype, n_rows, n_cols, K, cuts, row_ptr, row_ptr_bits, col_idx,
+                                         val, flags, nullptr);
+}
+
 extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream) {
   if (!d || (d->n_cols > 0 && !x) || (d->n_rows > 0 && !y) || (x == y && d->n_rows > 0)) return LHPC_ERR_INVALID_ARG;
   lhpc_dist_comm *c = d->comm;
@@ -477,13 +665,12 @@ extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, vo
   LHPC_HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   const size_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
-  // the y exchange: direct peer stores into the registered window, else RCCL
-  const bool p2p = c->nranks > 1 && c->p2p_ready && y == c->p2p_buf && c->p2p_bytes >= d->n_rows * tsz;
-  if (c->nranks > 1 && !p2p && !c->comm) return LHPC_ERR_INVALID_ARG;  // local comm: y must be the window
-  if (p2p) LHPC_TRY(p2p_exchange_begin(c, s, d->ev_p2p));
-  // the RCCL exchange also runs at world 1 under LHPC_DIST_EXCHANGE=1 (an
-  // in-place no-op there: lets the 1-GPU tests drive its calls and offsets)
-  const bool xchg = c->nranks > 1 || (d->exchange_always && c->comm);
+  // the y exchange: direct peer stores into a registered window, RCCL, or none
+  const P2pWindow *win = nullptr;
+  const int xk = pick_exchange(d, y, &win);
+  if (xk < 0) return xk;
+  if (xk == LHPC_DIST_EXCHANGE_P2P) LHPC_TRY(p2p_exchange_begin(c, s, d->ev_p2p));
+  const bool xchg = xk != LHPC_DIST_EXCHANGE_NONE;
   // a split plan with per-range gather pieces (its xg exceeds the Infinity
   // Cache) gathers each range right before reducing it; else one stage
   const bool range_gather = d->split && !d->split->xt_rpc.empty();
@@ -500,21 +687,31 @@ extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, vo
       else
         LHPC_TRY(lhpc_spmv(d->block_plan[k], x, yk, 1, stream));
     }
-    if (xchg) {
-      LHPC_HIP_TRY(hipEventRecord(d->ev[k], s));
-      LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, d->ev[k], 0));
-      lhpc::RocTxRange rb("lhpc_dist_spmv: y chunk exchange");
-      if (p2p)
-        LHPC_TRY(p2p_push(c, d->cuts[b] * static_cast<int64_t>(tsz), d->cuts[b + 1] * static_cast<int64_t>(tsz)));
-      else
-        LHPC_TRY(broadcast_chunk(d, k, y, c->s_comm));
-    }
+    if (xchg) LHPC_TRY(exchange_chunk(d, xk, win, k, y, s));
   }
   if (xchg) {
-    if (p2p) LHPC_TRY(p2p_exchange_end(c));
+    if (xk == LHPC_DIST_EXCHANGE_P2P) LHPC_TRY(p2p_exchange_end(c));
     LHPC_HIP_TRY(hipEventRecord(d->done, c->s_comm));
     LHPC_HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
   }
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_exchange(lhpc_dist_spmv_plan *d, void *y, void *stream) {
+  if (!d || (d->n_rows > 0 && !y)) return LHPC_ERR_INVALID_ARG;
+  lhpc_dist_comm *c = d->comm;
+  lhpc::RocTxRange rx("lhpc_dist_exchange");
+  LHPC_HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const P2pWindow *win = nullptr;
+  const int xk = pick_exchange(d, y, &win);
+  if (xk < 0) return xk;
+  if (xk == LHPC_DIST_EXCHANGE_NONE) return LHPC_OK;
+  if (xk == LHPC_DIST_EXCHANGE_P2P) LHPC_TRY(p2p_exchange_begin(c, s, d->ev_p2p));
+  for (int k = 0; k < d->K; ++k) LHPC_TRY(exchange_chunk(d, xk, win, k, y, s));
+  if (xk == LHPC_DIST_EXCHANGE_P2P) LHPC_TRY(p2p_exchange_end(c));
+  LHPC_HIP_TRY(hipEventRecord(d->done, c->s_comm));
+  LHPC_HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
   return LHPC_OK;
 }
 

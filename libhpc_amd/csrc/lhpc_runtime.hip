@@ -2,6 +2,9 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "lhpc_common.hpp"
@@ -36,3 +39,68 @@ extern "C" int lhpc_device_count(void) {
   }
   return good;
 }
+
+extern "C" void lhpc_options_init(lhpc_options *o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->struct_size = sizeof(*o);
+}
+
+namespace lhpc {
+namespace {
+#ifdef LHPC_TUNING_ENV
+// tuning build only: LHPC_* variables over the caller's options (the names
+// the A/B scripts of tools/ and DESIGN.md §4 use)
+void env_overlay(lhpc_options &o) {
+  auto i32 = [](const char *n, int32_t &f) {
+    if (const char *e = tuning_env(n)) f = std::atoi(e);
+  };
+  auto i64 = [](const char *n, int64_t &f) {
+    if (const char *e = tuning_env(n)) f = std::atoll(e);
+  };
+  if (const char *e = tuning_env("LHPC_SPMV_XTILE")) o.spmv_no_xtile = std::atoi(e) == 0;
+  if (const char *e = tuning_env("LHPC_SPMV_LOCALITY")) o.spmv_locality = std::atof(e);
+  if (const char *e = tuning_env("LHPC_SPMV_ROWGROUP")) std::sscanf(e, "%d,%d", &o.rowgroup_lanes, &o.rowgroup_rows);
+  if (const char *e = tuning_env("LHPC_XTILE_IPERM"))
+    o.xtile_reduce = std::atoi(e) ? LHPC_XTILE_REDUCE_IPERM : LHPC_XTILE_REDUCE_PERM;
+  if (const char *e = tuning_env("LHPC_XTILE_MALL")) o.xtile_ranges = std::max(1, std::atoi(e));
+  i32("LHPC_XTILE_U", o.xtile_steps);
+  if (const char *e = tuning_env("LHPC_XTILE_NTSTORE")) o.xtile_store = std::atoi(e) ? LHPC_STORE_NT : LHPC_STORE_PLAIN;
+  i32("LHPC_XTILE_CUT", o.xtile_cut);
+  i64("LHPC_XTILE_PIECE", o.xtile_piece);
+  i64("LHPC_XTILE_MALL_PIECE", o.xtile_range_piece);
+  i32("LHPC_XSLICE_S", o.xslice_slices);
+  if (const char *e = tuning_env("LHPC_XSLICE_PARTIAL")) o.xslice_partial = std::strcmp(e, "f64") ? 1 : 2;
+  i32("LHPC_XSLICE_NB", o.xslice_window);
+  if (const char *e = tuning_env("LHPC_XSLICE_MB")) o.xslice_mb = std::atof(e);
+  if (const char *e = tuning_env("LHPC_STENCIL7_IMPL"))
+    o.stencil7_impl = !std::strcmp(e, "buf4") ? LHPC_S7_RING_X4 : !std::strcmp(e, "buf") ? LHPC_S7_RING : LHPC_S7_SIMPLE;
+  if (const char *e = tuning_env("LHPC_STENCIL7_STORE"))
+    o.stencil7_store = !std::strcmp(e, "plain") ? LHPC_STORE_PLAIN : !std::strcmp(e, "staged") ? LHPC_STORE_STAGED : LHPC_STORE_NT;
+  if (const char *e = tuning_env("LHPC_STENCIL7_BUF"))
+    std::sscanf(e, "%d,%d,%d,%d", &o.stencil7_ry, &o.stencil7_nj, &o.stencil7_zc, &o.stencil7_pf);
+  i32("LHPC_STENCIL7_BLOCKS", o.stencil7_blocks);
+  i32("LHPC_BLUR_X_RW", o.blur_x_rows);
+  if (const char *e = tuning_env("LHPC_BLUR_Y_CFG")) std::sscanf(e, "%d,%d", &o.blur_y_vec, &o.blur_y_rows);
+  if (const char *e = tuning_env("LHPC_DIST_P2P")) o.dist_exchange = std::atoi(e) ? LHPC_DIST_EXCHANGE_P2P : LHPC_DIST_EXCHANGE_RCCL;
+  i32("LHPC_DIST_BCAST", o.dist_broadcast);
+  i32("LHPC_DIST_EXCHANGE", o.dist_world1);
+}
+#endif
+}  // namespace
+
+lhpc_options resolve_options(const lhpc_options *in) {
+  lhpc_options o;
+  lhpc_options_init(&o);
+  if (in && in->struct_size >= sizeof(uint32_t)) {
+    const size_t n = in->struct_size < sizeof(o) ? in->struct_size : sizeof(o);
+    std::memcpy(&o, in, n);
+    o.struct_size = sizeof(o);
+  }
+#ifdef LHPC_TUNING_ENV
+  env_overlay(o);
+#endif
+  return o;
+}
+
+}  // namespace lhpc

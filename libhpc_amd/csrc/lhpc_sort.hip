@@ -269,9 +269,10 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
   // the tail of the even-share split (500M keys: 768 blocks 8.94 ms, 6144 blocks 8.16 ms); below ~3 tiles
   // per block the per-block digit-count rows outweigh the gain (100M keys: 8192 blocks 1.89 ms, 30000 2.19).
   const int64_t res = sort_grid_cap<K, HAS_V, IPT>();
-  static const int64_t waves = std::getenv("LHPC_SORT_WAVES") ? std::max(1, std::atoi(std::getenv("LHPC_SORT_WAVES"))) : 8;
+  // grid sweep knobs of the tuning build only (tools/explore_sort.py; lhpc_common.hpp tuning_env)
+  static const int64_t waves = tuning_env("LHPC_SORT_WAVES") ? std::max(1, std::atoi(tuning_env("LHPC_SORT_WAVES"))) : 8;
   int64_t cap = std::min<int64_t>(waves * res, std::max<int64_t>(res, ntiles / 3));
-  if (const char *e = std::getenv("LHPC_SORT_BLOCKS")) cap = std::max<int64_t>(1, std::atoll(e));  // tuning knob
+  if (const char *e = tuning_env("LHPC_SORT_BLOCKS")) cap = std::max<int64_t>(1, std::atoll(e));
   int64_t nb = std::min<int64_t>(cap, ntiles);
   const int64_t per = (ntiles + nb - 1) / nb;
   nb = (ntiles + per - 1) / per;

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <iterator>
 #include <new>
 #include <vector>
 
@@ -61,8 +62,9 @@ int launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
 int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
                      const void *row_ptr, int row_ptr_bits, const int32_t *col_idx, const void *val,
                      const int *device_ids, int n_devices, unsigned flags, int n_splits,
-                     const int64_t *split_rows) {
+                     const int64_t *split_rows, const lhpc_options *opts) {
   if (!out) return LHPC_ERR_INVALID_ARG;
+  const lhpc_options o = resolve_options(opts);
   *out = nullptr;
   if ((dtype != LHPC_F32 && dtype != LHPC_F64) || n_rows < 0 || n_cols < 0 || nnz < 0 ||
       !row_ptr || (row_ptr_bits != 32 && row_ptr_bits != 64) || n_cols > INT32_MAX ||
@@ -88,6 +90,7 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
 
   auto *p = new (std::nothrow) lhpc_spmv_plan();
   if (!p) return LHPC_ERR_ALLOC;
+  p->opt = o;
   if (n_splits > 0) p->split_rows.assign(split_rows, split_rows + n_splits);
   p->dtype = dtype;
   p->device = dev;
@@ -126,17 +129,14 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
   // from L2, while XSLICE would add S partials per row.  Measure it: distinct
   // 128-B x lines per nonzero over sampled 8192-row chunks (≈0.8 for C2's
   // uniform columns, ≈0.03 for a 2-D Laplacian); ≤ 0.25 counts as local.
-  double locality_thr = 0.25;
-  if (const char *env = std::getenv("LHPC_SPMV_LOCALITY")) locality_thr = std::atof(env);
+  const double locality_thr = o.spmv_locality > 0 ? o.spmv_locality : 0.25;
   const bool auto_ok = !(flags & (LHPC_PLAN_FORCE_ROWGROUP | LHPC_PLAN_FORCE_ADAPTIVE |
                                    LHPC_PLAN_FORCE_XSLICE | LHPC_PLAN_FORCE_XTILE));
   const bool nolocal =
       auto_ok && x_bytes > 8.0e6 && gather_lines_per_nnz(rp, col_idx, n_rows, tsz) > locality_thr;
   // XTILE (x tiles in LDS) is the default for gathers without locality;
-  // LHPC_SPMV_XTILE=0 selects XSLICE instead.
-  bool xtile_env = true;
-  if (const char *env = std::getenv("LHPC_SPMV_XTILE")) xtile_env = std::atoi(env) != 0;
-  const bool want_xtile = (flags & LHPC_PLAN_FORCE_XTILE) || (nolocal && xtile_env);
+  // options.spmv_no_xtile selects XSLICE instead.
+  const bool want_xtile = (flags & LHPC_PLAN_FORCE_XTILE) || (nolocal && !o.spmv_no_xtile);
   if (want_xtile && n_rows > 0) {
     int st = xtile_build(p, rp, col_idx, val, tsz);
     if (st == LHPC_OK) {
@@ -172,12 +172,16 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
     p->R = L <= 16 ? 4 : (L == 32 ? 2 : 1);
     if (L == 4) p->R = 1;
   }
-  if (const char *env = std::getenv("LHPC_SPMV_ROWGROUP")) {  // "L,R" bench knob
-    int L = 0, R = 0;
-    if (std::sscanf(env, "%d,%d", &L, &R) == 2 && p->kernel == LHPC_KERNEL_ROWGROUP) {
-      p->L = L;
-      p->R = R;
+  if (p->kernel == LHPC_KERNEL_ROWGROUP && (o.rowgroup_lanes > 0 || o.rowgroup_rows > 0)) {
+    // the (L, R) shapes lhpc_spmv_csr.hip instantiates
+    static const int kShapes[] = {101, 201, 202, 401, 402, 404, 802, 804, 1601, 1602, 1604, 1608, 3201, 3202, 6401};
+    const int want = o.rowgroup_lanes * 100 + o.rowgroup_rows;
+    if (std::find(std::begin(kShapes), std::end(kShapes), want) == std::end(kShapes)) {
+      lhpc_spmv_plan_destroy(p);
+      return LHPC_ERR_INVALID_ARG;
     }
+    p->L = o.rowgroup_lanes;
+    p->R = o.rowgroup_rows;
   }
 
   int st = LHPC_OK;
@@ -233,22 +237,23 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
                                      int n_devices, unsigned flags) {
   RocTxRange rx("lhpc_spmv_plan_create");
   return plan_create_impl(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
-                          device_ids, n_devices, flags, 0, nullptr);
+                          device_ids, n_devices, flags, 0, nullptr, nullptr);
 }
 
-extern "C" int lhpc_spmv_plan_create_split(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
-                                           int64_t n_cols, int64_t nnz, const void *row_ptr,
-                                           int row_ptr_bits, const int32_t *col_idx,
-                                           const void *val, const int *device_ids, int n_devices,
-                                           unsigned flags, int n_splits, const int64_t *split_rows) {
-  if (!out || n_splits < 1 || !split_rows) return LHPC_ERR_INVALID_ARG;
+extern "C" int lhpc_spmv_plan_create_opts(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
+                                          int64_t n_cols, int64_t nnz, const void *row_ptr,
+                                          int row_ptr_bits, const int32_t *col_idx,
+                                          const void *val, const int *device_ids, int n_devices,
+                                          unsigned flags, int n_splits, const int64_t *split_rows,
+                                          const lhpc_options *opts) {
+  if (!out || n_splits < 0 || (n_splits > 0 && !split_rows)) return LHPC_ERR_INVALID_ARG;
   for (int i = 0; i < n_splits; ++i)
     if (split_rows[i] <= 0 || split_rows[i] >= n_rows || (i > 0 && split_rows[i] <= split_rows[i - 1]))
       return LHPC_ERR_INVALID_ARG;
-  RocTxRange rx("lhpc_spmv_plan_create_split");
+  RocTxRange rx("lhpc_spmv_plan_create");
   const int st = plan_create_impl(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
-                                  device_ids, n_devices, flags, n_splits, split_rows);
-  if (st != LHPC_OK) return st;
+                                  device_ids, n_devices, flags, n_splits, split_rows, opts);
+  if (st != LHPC_OK || n_splits == 0) return st;
   const lhpc_spmv_plan *p = *out;
   if (p->kernel != LHPC_KERNEL_XTILE || p->xt_srow.size() != static_cast<size_t>(n_splits) + 2) {
     lhpc_spmv_plan_destroy(*out);  // ranges exist only in the XTILE tile-stream layout
@@ -256,6 +261,16 @@ extern "C" int lhpc_spmv_plan_create_split(lhpc_spmv_plan **out, int dtype, int6
     return LHPC_ERR_UNSUPPORTED;
   }
   return LHPC_OK;
+}
+
+extern "C" int lhpc_spmv_plan_create_split(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
+                                           int64_t n_cols, int64_t nnz, const void *row_ptr,
+                                           int row_ptr_bits, const int32_t *col_idx,
+                                           const void *val, const int *device_ids, int n_devices,
+                                           unsigned flags, int n_splits, const int64_t *split_rows) {
+  if (n_splits < 1) return LHPC_ERR_INVALID_ARG;
+  return lhpc_spmv_plan_create_opts(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
+                                    device_ids, n_devices, flags, n_splits, split_rows, nullptr);
 }
 
 extern "C" int lhpc_spmv_stage(const lhpc_spmv_plan *p, const void *x, void *stream) {

@@ -16,6 +16,7 @@
 #include "lhpc_common.hpp"
 
 struct lhpc_spmv_plan {
+  lhpc_options opt{};  // resolved variant options (lhpc::resolve_options)
   int dtype = LHPC_F32;
   int device = 0;
   int rp64 = 0;  // device row_ptr is int64
@@ -40,9 +41,9 @@ struct lhpc_spmv_plan {
   // XTILE
   int64_t xt_C = 0, xt_pieces = 0, xt_cont = 0, xt_total = 0;
   size_t xt_lds = 0;
-  int xt_u = 8;  // gather steps in flight (LHPC_XTILE_U)
-  int xt_nt = 0;  // gather: non-temporal xg stores (LHPC_XTILE_NTSTORE)
-  // cache-sized ranges (LHPC_XTILE_MALL=K): a call runs gather k, reduce k
+  int xt_u = 8;  // gather steps in flight (lhpc_options.xtile_steps)
+  int xt_nt = 0;  // gather: non-temporal xg stores (lhpc_options.xtile_store)
+  // cache-sized ranges (lhpc_options.xtile_ranges = K): a call runs gather k, reduce k
   // for k < K so range k's xg is still in the Infinity Cache when its reduce
   // reads it; range k's gather pieces are [xt_rpc[k], xt_rpc[k+1])
   int xt_mall = 0;

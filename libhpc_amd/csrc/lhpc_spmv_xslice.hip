@@ -190,23 +190,22 @@ int xslice_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const
                  unsigned flags) {
   const int64_t nnz = p->nnz;
   const double x_bytes = static_cast<double>(p->n_cols) * static_cast<double>(tsz);
-  double slice_mb = 5.0;
-  if (const char *env = std::getenv("LHPC_XSLICE_MB")) slice_mb = std::max(0.25, std::atof(env));
+  const double slice_mb = p->opt.xslice_mb > 0 ? std::max(0.25, p->opt.xslice_mb) : 5.0;
   int P = static_cast<int>(std::ceil(x_bytes / (8.0 * slice_mb * 1.0e6)));
   P = std::max(1, std::min(P, 32));
   int S = 8 * P;
-  if (const char *env = std::getenv("LHPC_XSLICE_S")) S = std::max(1, std::min(256, std::atoi(env)));
+  if (p->opt.xslice_slices > 0) S = std::min(256, p->opt.xslice_slices);
   if (S > 8) S = (S + 7) / 8 * 8;
   XsliceHost xs;
   LHPC_TRY(build_xslice(rp.p, rp.bits, col_idx, val, tsz, p->n_rows, p->n_cols, S, xs));
   p->kernel = LHPC_KERNEL_XSLICE;
   p->S = S;
   p->xs_p64 = (tsz == 8 || ((flags & LHPC_PLAN_EXACT_PARTIALS) && !(flags & LHPC_PLAN_FAST_PARTIALS))) ? 1 : 0;
-  if (const char *env = std::getenv("LHPC_XSLICE_PARTIAL")) p->xs_p64 = tsz == 8 || !std::strcmp(env, "f64");
+  if (p->opt.xslice_partial > 0) p->xs_p64 = tsz == 8 || p->opt.xslice_partial == 2;
   {  // window = NB·64 nonzeros: cover a typical chunk in one window
     const double mean_chunk = xs.n_chunks ? static_cast<double>(nnz) / (static_cast<double>(S) * xs.n_chunks) : 0;
     int nb = static_cast<int>(std::ceil(mean_chunk * 1.2 / kWave));
-    if (const char *env = std::getenv("LHPC_XSLICE_NB")) nb = std::atoi(env);
+    if (p->opt.xslice_window > 0) nb = p->opt.xslice_window;
     p->xs_nb = std::max(1, std::min(nb, 4));
   }
   p->xs_width = xs.width;

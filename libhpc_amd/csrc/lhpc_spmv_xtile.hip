@@ -253,7 +253,12 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   {
     const tvec *vp = reinterpret_cast<const tvec *>(val + vreg) + lane;
 #pragma unroll
+#if defined(LHPC_XT_PROBE_VI)  // timing-only probe: no val / iperm loads
+    for (int q = 0; q < NV; ++q) vv[q] = tvec{};
+    (void)vp;
+#else
     for (int q = 0; q < NV; ++q) vv[q] = __builtin_nontemporal_load(vp + q * kWave);
+#endif
   }
   constexpr int NIP = IP ? RUN * 2 / 16 : 1;  // 16-B iperm vectors per run
   u32x4 ipv[NIP];
@@ -262,7 +267,12 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   auto load_ipv = [&]() {
     const u32x4 *ip = reinterpret_cast<const u32x4 *>(perm + vreg) + lane;
 #pragma unroll
+#if defined(LHPC_XT_PROBE_VI)
+    for (int q = 0; q < NIP; ++q) ipv[q] = u32x4{0, 0, 0, 0};
+    (void)ip;
+#else
     for (int q = 0; q < NIP; ++q) ipv[q] = __builtin_nontemporal_load(ip + q * kWave);
+#endif
   };
   int rv[RPT];
 #pragma unroll
@@ -355,6 +365,20 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     const __amdgpu_buffer_rsrc_t xr_rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<T *>(xg), 0, (total + 2) * static_cast<int>(sizeof(T)), 0x00020000);
     if constexpr (sizeof(T) == 4) {
+#if defined(LHPC_XT_PROBE_XG)
+      // timing-only probe (wrong results): 1 = the chunk's xg as one aligned
+      // contiguous run, 16-B LDS-DMA per lane; 2 = the same, non-temporal;
+      // 3 = no xg loads
+      if constexpr (LHPC_XT_PROBE_XG != 3) {
+#pragma unroll
+        for (int u = 0; u < NB / 4; ++u)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              xr_rs, (__attribute__((address_space(3))) void *)(xs + (wv * NB + 4 * u) * kWave), 16,
+              static_cast<int>((c * M + (wv * NB + 4 * u) * kWave + 4 * lane) * 4), 0, 0,
+              LHPC_XT_PROBE_XG == 2 ? 2 : 0);
+      }
+      (void)src;
+#else
       // LDS-DMA: each lane's xg element lands at the batch's base + 4·lane
       // (exactly the flat order), no VGPR destination
 #pragma unroll
@@ -362,6 +386,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             xr_rs, (__attribute__((address_space(3))) void *)(xs + (wv * NB + u) * kWave), 4,
             src[u] * static_cast<int>(sizeof(T)), 0, 0, LHPC_XT_XG_CPOL);
+#endif
       load_ipv();
     } else {
       T xv[NB];
@@ -524,21 +549,28 @@ size_t xtile_lds_bytes(int S) {
          sizeof(int32_t) * (static_cast<size_t>(S) + 8);
 }
 
-// segment-table entries per reduce thread
+// segment-table entries per reduce thread: G = ⌈S / BLK⌉ rounded up to a
+// power of two.  build_xtile caps S at kXtMaxTiles = 4096, so G ≤ 8 for fp32
+// (BLK 512) and ≤ 4 for fp64 (BLK 1024); only those are instantiated (a G = 16
+// form spilled and could never be selected)
+template <typename T> constexpr int xt_gmax() { return 4096 / xt_red_blk<T>(); }
 template <typename T>
 int xtile_g(int S) {
   const int g = (S + xt_red_blk<T>() - 1) / xt_red_blk<T>();
-  return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : g <= 8 ? 8 : 16;
+  return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : 8;
 }
 
 template <typename T, int G, bool IP>
 const void *xtile_reduce_fn() {
-  return reinterpret_cast<const void *>(k_xtile_reduce<T, G, xt_red_blk<T>(), IP>);
+  if constexpr (G > xt_gmax<T>())
+    return nullptr;
+  else
+    return reinterpret_cast<const void *>(k_xtile_reduce<T, G, xt_red_blk<T>(), IP>);
 }
 template <typename T, bool IP>
 const void *xtile_reduce_fn(int g) {
   return g == 1 ? xtile_reduce_fn<T, 1, IP>() : g == 2 ? xtile_reduce_fn<T, 2, IP>()
-         : g == 4 ? xtile_reduce_fn<T, 4, IP>() : g == 8 ? xtile_reduce_fn<T, 8, IP>() : xtile_reduce_fn<T, 16, IP>();
+         : g == 4 ? xtile_reduce_fn<T, 4, IP>() : xtile_reduce_fn<T, 8, IP>();
 }
 template <typename T>
 const void *xtile_reduce_fn(int g, bool ip) {
@@ -608,14 +640,15 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   // stays ≤ 1/4 of a piece's col16 + xg traffic on small (per-rank) matrices
   const int64_t min_piece = 4 * W * static_cast<int64_t>(tsz) / (2 + static_cast<int64_t>(tsz));
   int64_t piece = std::max<int64_t>(min_piece, p->nnz / (2 * static_cast<int64_t>(cus)) + 1);
-  if (const char *env = std::getenv("LHPC_XTILE_PIECE")) piece = std::max<int64_t>(8, std::atoll(env));
+  const lhpc_options &o = p->opt;
+  if (o.xtile_piece > 0) piece = std::max<int64_t>(8, o.xtile_piece);
   // reduce index stream: iperm (gather each CSR position's x from the flat
   // segment concatenation in LDS) for ≥ 32 full chunks per CU, else perm
   // (scatter into CSR slots): with fewer chunks (per-rank matrices at N ≥ 4)
   // the perm reduce's shorter blocks win (W = 8 rank of C2: 0.088 against
   // 0.093 ms; W = 1: 0.626 against 0.611 ms; profiles/r01/explore_scaling_*)
   bool ip = p->nnz >= 32LL * cus * M;
-  if (const char *env = std::getenv("LHPC_XTILE_IPERM")) ip = std::atoi(env) != 0;
+  if (o.xtile_reduce != LHPC_XTILE_REDUCE_AUTO) ip = o.xtile_reduce == LHPC_XTILE_REDUCE_IPERM;
   // the iperm reduce addresses xg with 32-bit buffer offsets: stream + tile
   // padding (≤ 8 per tile) + one piece of slack must stay below 2 GiB
   const int64_t stream_max = p->nnz + 8 * ((p->n_cols + W - 1) / W) + 2 * M;
@@ -625,9 +658,9 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   // mid-row (the row's pieces meet in k_xtile_fixup).  Per-chunk costs are
   // fixed, so full chunks matter on skewed rows: C4 has 19803 chunks when any
   // row start in the back half is taken, 18454 with the back M/32 (C2: 18316
-  // either way); LHPC_XTILE_CUT overrides (entries, 1..M)
+  // either way); options.xtile_cut overrides (entries, 1..M)
   int cut = M / 32;
-  if (const char *env = std::getenv("LHPC_XTILE_CUT")) cut = std::min(M, std::max(1, std::atoi(env)));
+  if (o.xtile_cut > 0) cut = std::min(M, o.xtile_cut);
   // cache-sized ranges: K nnz-balanced row ranges, gathered and reduced in
   // turn, so that each range's xg (≈ 200 MB) is still in the 256 MB Infinity
   // Cache when its reduce reads it back.  fp32 only: each extra range re-reads
@@ -640,7 +673,7 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
     if (tsz == 4 && xg_bytes > (int64_t{256} << 20))
       mall = static_cast<int>(std::min<int64_t>(8, (xg_bytes + (int64_t{200} << 20) - 1) / (int64_t{200} << 20)));
   }
-  if (const char *env = std::getenv("LHPC_XTILE_MALL")) mall = std::atoi(env);
+  if (o.xtile_ranges > 0) mall = o.xtile_ranges;
   // a row-range plan (user splits) whose xg exceeds the cache gets per-range
   // gather pieces for its own ranges (stage still gathers them all)
   if (!p->split_rows.empty() && mall > 1) p->xt_mall = static_cast<int>(p->split_rows.size()) + 1;
@@ -664,8 +697,8 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   p->xt_cont = static_cast<int64_t>(xt.cont.size());
   p->xt_total = xt.total;
   p->xt_lds = xtile_lds_bytes<T>(xt.S);
-  if (const char *env = std::getenv("LHPC_XTILE_U")) {
-    const int u = std::atoi(env);
+  if (o.xtile_steps > 0) {
+    const int u = o.xtile_steps;
     p->xt_u = u <= 2 ? 2 : u < 8 ? 4 : u < 16 ? 8 : 16;
   }
   // non-temporal xg stores when the xg of a single-range plan exceeds the 256
@@ -673,9 +706,10 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   // median); cache-sized ranges need their xg to stay there (C2 with them
   // non-temporal: 473 → 536 µs)
   p->xt_nt = p->xt_mall <= 1 && p->nnz * static_cast<int64_t>(tsz) > (int64_t{256} << 20) ? 1 : 0;
-  if (const char *env = std::getenv("LHPC_XTILE_NTSTORE")) p->xt_nt = std::atoi(env) != 0;
-  LHPC_HIP_TRY(hipFuncSetAttribute(xtile_reduce_fn<T>(xtile_g<T>(xt.S), ip),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
+  if (o.xtile_store != LHPC_STORE_AUTO) p->xt_nt = o.xtile_store == LHPC_STORE_NT ? 1 : 0;
+  const void *rfn = xtile_reduce_fn<T>(xtile_g<T>(xt.S), ip);
+  if (!rfn) return LHPC_ERR_UNSUPPORTED;  // more tiles than the reduce's segment table holds
+  LHPC_HIP_TRY(hipFuncSetAttribute(rfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
   const int64_t n_rows = p->n_rows, C = xt.n_chunks;
   auto up = [&](void **d, const void *h, size_t n) -> int {
     LHPC_TRY(dmalloc(d, n, p->bytes));
@@ -710,7 +744,7 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
     // one gather round per range: ≈ one piece per (tile, range) part, so each
     // range loads every tile once (only one 160-KB gather block fits a CU)
     int64_t rpn = std::max<int64_t>(min_piece, p->nnz / p->xt_mall / static_cast<int64_t>(cus) * 5 / 4 + 1);
-    if (const char *env = std::getenv("LHPC_XTILE_MALL_PIECE")) rpn = std::max<int64_t>(8, std::atoll(env));
+    if (o.xtile_range_piece > 0) rpn = std::max<int64_t>(8, o.xtile_range_piece);
     xtile_range_pieces(xt, rpn, p->xt_rpc);
     p->xt_pieces = static_cast<int64_t>(xt.pieces.size() / 3);
   }

@@ -619,7 +619,7 @@ struct HostStage {
 };
 
 int blur_launch(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int64_t ghost,
-                int nb, hipStream_t s) {
+                int nb, hipStream_t s, const lhpc_options &o) {
   const int64_t cells = ny * nx;
   if (cells == 0) return LHPC_OK;
   const int64_t P = nx + 2 * ghost;
@@ -637,8 +637,7 @@ int blur_launch(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int
       // block-LDS kernel on 8192^2); the block-LDS kernel only for rows that
       // are not 16-B aligned
       if (vec) {
-        const char *e = std::getenv("LHPC_BLUR_X_RW");
-        const int rw = e ? std::atoi(e) : 2;
+        const int rw = o.blur_x_rows > 0 ? o.blur_x_rows : 2;
         const int64_t nseg256 = (nx + 255) / 256;
 #define LHPC_BXW(RWV)                                                                                        \
   do {                                                                                                       \
@@ -668,12 +667,8 @@ int blur_launch(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int
       const bool vec4 = aligned16(a) && aligned16(b) && P % 4 == 0 && nx % 4 == 0 && ghost % 4 == 0;
       const bool vec2 = aligned16(a) && aligned16(b) && P % 2 == 0 && nx % 2 == 0 && ghost % 2 == 0;
       // register-window shape: VEC columns × TY rows per thread (window TY+16 rows)
-      const int cfg = [] {
-        const char *e = std::getenv("LHPC_BLUR_Y_CFG");  // "vec,ty"
-        int v = 4, t = 16;  // plain loads: 4x16 measured best (84 us, 8192^2)
-        if (e) std::sscanf(e, "%d,%d", &v, &t);
-        return v * 1000 + t;
-      }();
+      // register-window shape (vec, ty); plain loads: 4x16 measured best (84 us, 8192^2)
+      const int cfg = (o.blur_y_vec > 0 ? o.blur_y_vec : 4) * 1000 + (o.blur_y_rows > 0 ? o.blur_y_rows : 16);
 #define LHPC_BY(V, TY)                                                                              \
   do {                                                                                              \
     const int64_t n_ytiles = (ny + TY - 1) / TY;                                                    \
@@ -699,10 +694,11 @@ int blur_launch(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int
 }
 
 int blur_entry(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int64_t ghost,
-               int nblur, int on_device, void *stream) {
+               int nblur, int on_device, void *stream, const lhpc_options *opts) {
   if (!a || !b || ny < 0 || nx < 0 || nblur < 0 || ghost < nblur) return LHPC_ERR_INVALID_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (on_device) return blur_launch(ydir, a, b, ny, nx, ghost, nblur, s);
+  const lhpc_options o = resolve_options(opts);
+  if (on_device) return blur_launch(ydir, a, b, ny, nx, ghost, nblur, s, o);
   const size_t in_bytes = static_cast<size_t>((ny + 2 * ghost) * (nx + 2 * ghost)) * 4;
   const size_t out_bytes = static_cast<size_t>(ny * nx) * 4;
   HostStage da, db;
@@ -710,27 +706,27 @@ int blur_entry(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int6
   LHPC_HIP_TRY(hipMalloc(&db.d, out_bytes ? out_bytes : 16));
   LHPC_HIP_TRY(hipMemcpy(da.d, a, in_bytes, hipMemcpyHostToDevice));  // host buffers: synchronous copies
   LHPC_TRY(blur_launch(ydir, static_cast<float *>(da.d), static_cast<float *>(db.d), ny, nx, ghost,
-                       nblur, s));
+                       nblur, s, o));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
   LHPC_HIP_TRY(hipMemcpy(b, db.d, out_bytes, hipMemcpyDeviceToHost));
   return LHPC_OK;
 }
 
 int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, int64_t g, float c0,
-              float c1, int64_t zb, int64_t ze, hipStream_t s) {
+              float c1, int64_t zb, int64_t ze, hipStream_t s, const lhpc_options &o) {
   if (zb >= ze || ny == 0 || nx == 0) return LHPC_OK;
   // implementation: the buffer ring ("buf"), in its x4 form ("buf4") when the x
   // tiles are full; the thread-per-column kernel only when a row's byte
   // offset does not fit a buffer voffset.  The measured alternatives (LDS
   // 2.5-D tile, register ring, deep prefetch, flat wide ring) are in DESIGN.md §4.
-  const char *impl = std::getenv("LHPC_STENCIL7_IMPL");
-  // Store policy of the dword ring: "staged" (default: float4 stores via the
+  const int impl = o.stencil7_impl;
+  // Store policy of the dword ring: staged (default: float4 stores via the
   // wave's LDS row, 219-220 us vs 225-226 plain on 512^3; plain when `out` is
-  // not 16-B aligned) | "plain" | "nt".
-  const char *stm = std::getenv("LHPC_STENCIL7_STORE");
-  const bool buf4_req = impl && !std::strcmp(impl, "buf4");
-  const bool buf_impl = !impl || !std::strcmp(impl, "buf") || buf4_req;
-  int store_mode = stm ? (!std::strcmp(stm, "plain") ? 0 : !std::strcmp(stm, "staged") ? 4 : 1) : 4;
+  // not 16-B aligned) | plain | nt.
+  const int stm = o.stencil7_store;
+  const bool buf4_req = impl == LHPC_S7_RING_X4;
+  const bool buf_impl = impl == LHPC_S7_AUTO || impl == LHPC_S7_RING || buf4_req;
+  int store_mode = stm == LHPC_STORE_PLAIN ? 0 : stm == LHPC_STORE_NT ? 1 : 4;
   if (store_mode == 4 && !aligned16(out)) store_mode = 0;  // staged float4 stores need a 16-B base
   // buffer-addressed ring: the in-row byte offset (voffset) must fit 31 bits
   const bool row_b31 = (nx + 2 * g + 1024) * 4 < (int64_t{1} << 31);
@@ -739,23 +735,21 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
     // one block per CU (256): measured on 512^3, fewer concurrent z fronts beat
     // more waves — 2,8 at zc 128 (256 blocks) 209-220 us vs 250 us at zc 32 (1024 blocks);
     // prefetch depth (PF) and store policy (plain vs nt) are secondary.
-    const char *cfg = std::getenv("LHPC_STENCIL7_BUF");  // "RY,NJ,ZC[,PF]"
-    int ry = 2, nj = 8, zc = 0, pf = 0;
-    if (cfg) std::sscanf(cfg, "%d,%d,%d,%d", &ry, &nj, &zc, &pf);
+    int ry = o.stencil7_ry > 0 ? o.stencil7_ry : 2, nj = o.stencil7_nj > 0 ? o.stencil7_nj : 8;
+    int zc = o.stencil7_zc, pf = o.stencil7_pf;
     // x4 ring by default when every x tile is full (nx % (64·NJ) == 0): 198-211 us against
     // 209-225 us for the dword ring on 512^3, same boxes; "buf" forces the dword ring
-    const bool buf4 = (buf4_req || !impl) && (nj == 4 || nj == 8) && nx % (int64_t{nj} * kWave) == 0;
+    const bool buf4 = (buf4_req || impl == LHPC_S7_AUTO) && (nj == 4 || nj == 8) && nx % (int64_t{nj} * kWave) == 0;
     if (pf < 1) pf = buf4 ? 2 : 1;  // prefetch planes: x4 PF 2 198 us vs PF 1 210-217 / PF 3 203
     if (zc < 1) {
-      const char *bt = std::getenv("LHPC_STENCIL7_BLOCKS");
-      const int64_t target = bt ? std::max<int64_t>(1, std::atoll(bt)) : 256;
+      const int64_t target = o.stencil7_blocks > 0 ? o.stencil7_blocks : 256;
       const int64_t tw = int64_t{nj} * kWave, th = 4 * int64_t{ry};
       const int64_t xy = ((nx + tw - 1) / tw) * ((ny + th - 1) / th);
       const int64_t nchunks = std::max<int64_t>(1, (target + xy - 1) / xy);
       zc = static_cast<int>(std::max<int64_t>(4, (ze - zb + nchunks - 1) / nchunks));
     }
     if (buf4) {  // x4 ring: non-temporal dwordx4 stores ("plain": plain)
-      const int m4 = stm && !std::strcmp(stm, "plain") ? 5 : 6;
+      const int m4 = stm == LHPC_STORE_PLAIN ? 5 : 6;
 #define LHPC_S74_M(RY, NJ, M)                                                                          \
   do {                                                                                                 \
     const int64_t ntx = nx / (NJ * kWave), nty = (ny + 4 * RY - 1) / (4 * RY), ntz = (ze - zb + zc - 1) / zc; \
@@ -827,27 +821,45 @@ using namespace lhpc;
 
 extern "C" int lhpc_blur_x_f32(const float *a, float *b, int64_t ny, int64_t nx, int64_t ghost,
                                int nblur, int on_device, void *stream) {
-  return blur_entry(false, a, b, ny, nx, ghost, nblur, on_device, stream);
+  return blur_entry(false, a, b, ny, nx, ghost, nblur, on_device, stream, nullptr);
 }
 
 extern "C" int lhpc_blur_y_f32(const float *a, float *b, int64_t ny, int64_t nx, int64_t ghost,
                                int nblur, int on_device, void *stream) {
-  return blur_entry(true, a, b, ny, nx, ghost, nblur, on_device, stream);
+  return blur_entry(true, a, b, ny, nx, ghost, nblur, on_device, stream, nullptr);
+}
+
+extern "C" int lhpc_blur_x_f32_opts(const float *a, float *b, int64_t ny, int64_t nx, int64_t ghost, int nblur,
+                                    int on_device, void *stream, const lhpc_options *opts) {
+  return blur_entry(false, a, b, ny, nx, ghost, nblur, on_device, stream, opts);
+}
+
+extern "C" int lhpc_blur_y_f32_opts(const float *a, float *b, int64_t ny, int64_t nx, int64_t ghost, int nblur,
+                                    int on_device, void *stream, const lhpc_options *opts) {
+  return blur_entry(true, a, b, ny, nx, ghost, nblur, on_device, stream, opts);
+}
+
+extern "C" int lhpc_stencil7_f32_planes_opts(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx,
+                                             int64_t ghost, float c0, float c1, int64_t z_begin, int64_t z_end,
+                                             void *stream, const lhpc_options *opts) {
+  if (!u || !out || nz < 0 || ny < 0 || nx < 0 || ghost < 1 || z_begin < 0 || z_end > nz)
+    return LHPC_ERR_INVALID_ARG;
+  return s7_launch(u, out, nz, ny, nx, ghost, c0, c1, z_begin, z_end, static_cast<hipStream_t>(stream),
+                   resolve_options(opts));
 }
 
 extern "C" int lhpc_stencil7_f32_planes(const float *u, float *out, int64_t nz, int64_t ny,
                                         int64_t nx, int64_t ghost, float c0, float c1,
                                         int64_t z_begin, int64_t z_end, void *stream) {
-  if (!u || !out || nz < 0 || ny < 0 || nx < 0 || ghost < 1 || z_begin < 0 || z_end > nz)
-    return LHPC_ERR_INVALID_ARG;
-  return s7_launch(u, out, nz, ny, nx, ghost, c0, c1, z_begin, z_end, static_cast<hipStream_t>(stream));
+  return lhpc_stencil7_f32_planes_opts(u, out, nz, ny, nx, ghost, c0, c1, z_begin, z_end, stream, nullptr);
 }
 
 extern "C" int lhpc_stencil7_f32(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx,
                                  int64_t ghost, float c0, float c1, int on_device, void *stream) {
   if (!u || !out || nz < 0 || ny < 0 || nx < 0 || ghost < 1) return LHPC_ERR_INVALID_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (on_device) return s7_launch(u, out, nz, ny, nx, ghost, c0, c1, 0, nz, s);
+  const lhpc_options o = resolve_options(nullptr);
+  if (on_device) return s7_launch(u, out, nz, ny, nx, ghost, c0, c1, 0, nz, s, o);
   const size_t bytes =
       static_cast<size_t>((nz + 2 * ghost) * (ny + 2 * ghost) * (nx + 2 * ghost)) * 4;
   HostStage du, dout;
@@ -857,7 +869,7 @@ extern "C" int lhpc_stencil7_f32(const float *u, float *out, int64_t nz, int64_t
   // ghost cells of `out` keep the caller's values
   LHPC_HIP_TRY(hipMemcpy(dout.d, out, bytes, hipMemcpyHostToDevice));
   LHPC_TRY(s7_launch(static_cast<float *>(du.d), static_cast<float *>(dout.d), nz, ny, nx, ghost, c0,
-                     c1, 0, nz, s));
+                     c1, 0, nz, s, o));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
   LHPC_HIP_TRY(hipMemcpy(out, dout.d, bytes, hipMemcpyDeviceToHost));
   return LHPC_OK;

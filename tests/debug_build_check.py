@@ -21,15 +21,15 @@ assert os.path.realpath(L.LIB_PATH) == os.path.realpath(os.environ["LHPC_LIB_PAT
 dev = torch.device("cuda:0")
 lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 3000 + [0, 0] + [30000]
 n = len(lengths)
-for ip in ("0", "1"):
-    os.environ["LHPC_XTILE_IPERM"] = ip
+for ip in (0, 1):
+    opts = {"xtile_reduce": L.XTILE_REDUCE_IPERM if ip else L.XTILE_REDUCE_PERM}
     for dt in (np.float32, np.float64):
-        rp, col, val = _csr_from_lengths(lengths, 200_000, 0xD0 + int(ip), dyadic=True)
+        rp, col, val = _csr_from_lengths(lengths, 200_000, 0xD0 + ip, dyadic=True)
         val = val.astype(dt)
         x = (np.random.default_rng(7).integers(-8, 9, size=200_000) / 8.0).astype(dt)
         _, yr, _ = S.spmv_oracle(rp, col, val, x)
         splits = [1, 57, 2000, n - 1]
-        with L.SpMVPlan(rp, col, val, 200_000, flags=FAMILIES["xtile"], splits=splits) as plan:
+        with L.SpMVPlan(rp, col, val, 200_000, flags=FAMILIES["xtile"], splits=splits, options=opts) as plan:
             xd = torch.from_numpy(x).to(dev)
             y = plan(xd).cpu().numpy()
             assert np.array_equal(y, yr), ("xtile", ip, dt)

@@ -1,7 +1,19 @@
-"""One rank of the direct-peer-exchange test (tests/test_gpu_dist.py::
-test_dist_spmv_p2p_two_ranks_one_gpu): WORLD_SIZE ranks share cuda:0, blobs
-exchanged over gloo, a local (RCCL-free) communicator each, lhpc_dist_spmv
-with the registered y window.  Prints one JSON line.  Test infrastructure."""
+"""One rank of the direct-peer-exchange tests (tests/test_gpu_dist.py::
+test_dist_spmv_p2p_*): WORLD_SIZE ranks share cuda:0, blobs exchanged over
+gloo, a local (RCCL-free) communicator each, lhpc_dist_spmv with registered y
+windows.  Prints one JSON line.  Test infrastructure.
+
+Cases (argv[1]):
+  barrier   three calls per matrix, host barrier + synchronize around each
+            call (fp32 XTILE row-range plan, fp64 per-block plans)
+  loop      the iterative loop with NO host ordering between calls: x ← y
+            copied on the call's stream after every call, so the READY /
+            DONE flags are the only ordering between the ranks; four calls
+  pingpong  two windows (ya, yb): y of call n is x of call n+1, four calls,
+            no host ordering
+  tiny      1–3-row blocks (small n, many chunks) in fp32 and fp64, and a
+            window whose 16-B phase differs between the ranks (word stores)
+"""
 import json
 import os
 import sys
@@ -16,32 +28,112 @@ import torch.distributed as dist  # noqa: E402
 import libhpc_amd as L  # noqa: E402
 from tests import _support as S  # noqa: E402
 
+case = sys.argv[1] if len(sys.argv) > 1 else "barrier"
 dist.init_process_group("gloo")
 rank, world = dist.get_rank(), dist.get_world_size()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
-out = {"rank": rank, "ok": []}
-for n, per_row, K, dt in ((3_000_000, 6, 2, L.F32), (20_000, 7, 3, L.F64)):
-    rp, col, val = L.gen_uniform_csr(n, n, per_row, dtype=dt, dist=1, seed=0xE100 + K)
-    x = L.gen_values(dt, 1, n, 0xE101)
-    _, want, _ = S.spmv_oracle(rp, col, val, x)
+out = {"rank": rank, "case": case, "ok": [], "status": []}
+
+
+def problem(n, per_row, K, dt, seed):
+    rp, col, val = L.gen_uniform_csr(n, n, per_row, dtype=dt, dist=1, seed=seed)
+    x = L.gen_values(dt, 1, n, seed + 1)
     cuts = L.interleaved_cuts(rp, world, K)
-    lrp, lc, lv = L.interleaved_local_csr(rp, col, val, cuts, world, K, rank)
-    comm = L.DistComm.local(world, rank, 0)
-    xd = torch.from_numpy(x).to(dev)
-    y = torch.full((n,), float("nan"), dtype=xd.dtype, device=dev)
-    comm.p2p_setup_torch(y)
-    with L.DistSpMVPlan(comm, n, n, K, cuts, lrp, lc, lv) as d:
-        for it in range(3):
-            y.fill_(float("nan"))
+    return rp, col, val, x, cuts, L.interleaved_local_csr(rp, col, val, cuts, world, K, rank)
+
+
+def iterate_oracle(rp, col, val, x, steps):
+    ys, cur = [], x
+    for _ in range(steps):
+        _, cur, _ = S.spmv_oracle(rp, col, val, cur)
+        ys.append(cur)
+    return ys
+
+
+if case == "barrier":
+    for n, per_row, K, dt in ((3_000_000, 6, 2, L.F32), (20_000, 7, 3, L.F64)):
+        rp, col, val, x, cuts, local = problem(n, per_row, K, dt, 0xE100 + K)
+        _, want, _ = S.spmv_oracle(rp, col, val, x)
+        comm = L.DistComm.local(world, rank, 0)
+        xd = torch.from_numpy(x).to(dev)
+        y = torch.full((n,), float("nan"), dtype=xd.dtype, device=dev)
+        comm.p2p_setup_torch(y)
+        with L.DistSpMVPlan(comm, n, n, K, cuts, *local) as d:
+            for it in range(3):
+                y.fill_(float("nan"))
+                torch.cuda.synchronize()
+                dist.barrier()  # every rank's y reset before anyone's next pushes (READY covers the stream, not this fill)
+                d(xd, y)
+                torch.cuda.synchronize()
+                out["ok"].append(bool(np.array_equal(y.cpu().numpy(), want)))
+                dist.barrier()
+        out["status"].append(comm.p2p_status())
+        comm.close()
+elif case in ("loop", "pingpong"):
+    steps = 4
+    for n, per_row, K, dt in ((2_000_000, 3, 2, L.F32), (30_000, 3, 3, L.F64)):
+        rp, col, val, x, cuts, local = problem(n, per_row, K, dt, 0xE200 + K)
+        want = iterate_oracle(rp, col, val, x, steps)
+        comm = L.DistComm.local(world, rank, 0)
+        s = torch.cuda.current_stream(dev)
+        xd = torch.from_numpy(x).to(dev)
+        if case == "loop":
+            y = torch.full((n,), float("nan"), dtype=xd.dtype, device=dev)
+            comm.p2p_setup_torch(y)
+        else:
+            ya = torch.full((n,), float("nan"), dtype=xd.dtype, device=dev)
+            yb = torch.full((n,), float("nan"), dtype=xd.dtype, device=dev)
+            comm.p2p_setup_torch(ya)  # two windows, same order on every rank
+            comm.p2p_setup_torch(yb)
+        torch.cuda.synchronize()
+        dist.barrier()  # windows mapped everywhere; from here on no host ordering
+        snaps = []
+        with L.DistSpMVPlan(comm, n, n, K, cuts, *local, options={"dist_exchange": L.DIST_EXCHANGE_P2P}) as d:
+            cur = xd
+            for it in range(steps):
+                if case == "loop":
+                    d(cur, y, stream=s)
+                    snaps.append(y.clone())  # on the stream, after the call's DONE wait
+                    xd.copy_(y)  # x ← y on the call's stream (reads y before the next READY)
+                    cur = xd
+                else:
+                    dst = ya if it % 2 == 0 else yb
+                    d(cur, dst, stream=s)
+                    snaps.append(dst.clone())
+                    cur = dst
             torch.cuda.synchronize()
-            dist.barrier()  # every rank's y reset before anyone's next pushes (READY covers the stream, not this fill)
-            d(xd, y)
-            torch.cuda.synchronize()
-            good = bool(np.array_equal(y.cpu().numpy(), want))
-            out["ok"].append(good)
-            dist.barrier()
-    out.setdefault("status", []).append(comm.p2p_status())
-    comm.close()
+        for it in range(steps):
+            out["ok"].append(bool(np.array_equal(snaps[it].cpu().numpy(), want[it])))
+        dist.barrier()
+        out["status"].append(comm.p2p_status())
+        comm.close()
+elif case == "tiny":
+    for n, K, dt, shift in ((41, 16, L.F64, 0), (43, 16, L.F32, 0), (41, 9, L.F32, 1), (37, 5, L.F64, 0)):
+        rp, col, val, x, cuts, local = problem(n, 3, K, dt, 0xE300 + n + K)
+        _, want, _ = S.spmv_oracle(rp, col, val, x)
+        comm = L.DistComm.local(world, rank, 0)
+        xd = torch.from_numpy(x).to(dev)
+        # shift: rank 1's window starts one element into its buffer, so the
+        # two windows differ in 16-B phase and the pushes use word stores
+        base = torch.full((n + 4,), float("nan"), dtype=xd.dtype, device=dev)
+        off = shift if rank == 1 else 0
+        y = base[off:off + n]
+        comm.p2p_setup_torch(y)
+        torch.cuda.synchronize()
+        dist.barrier()
+        with L.DistSpMVPlan(comm, n, n, K, cuts, *local, options={"dist_exchange": L.DIST_EXCHANGE_P2P}) as d:
+            for it in range(2):
+                d(xd, y)
+                torch.cuda.synchronize()
+                out["ok"].append(bool(np.array_equal(y.cpu().numpy(), want)))
+                dist.barrier()
+                y.fill_(float("nan"))
+                torch.cuda.synchronize()
+                dist.barrier()
+        out["status"].append(comm.p2p_status())
+        comm.close()
+else:
+    raise SystemExit(f"unknown case {case}")
 print(json.dumps(out), flush=True)
 dist.destroy_process_group()

@@ -170,46 +170,111 @@ def test_interleaved_cuts_are_nnz_balanced(world, K):
     assert blk.max() - blk.min() <= 2 * lens.max()
 
 
-def _native_emulation(rp, col, val, x, world, K):
-    """What every rank of lhpc_dist_spmv holds after a call, emulated on the
-    CPU with the oracle: rank r reduces its local stacked CSR
-    (interleaved_local_csr) into its blocks' rows of y, then chunk k's
-    broadcast from root r copies block k·world + r into every rank's y."""
+def _local_rows(rp, col, val, x, world, K, cuts):
+    """Every rank's y before the exchange: rank r's stacked local CSR
+    (interleaved_local_csr, the input of lhpc_dist_spmv_plan_create) reduced
+    with the oracle into its blocks' rows; every other row NaN."""
     import libhpc_amd as L
     from tests import _support as S
-    cuts = L.interleaved_cuts(rp, world, K)
     ys = [np.full(rp.shape[0] - 1, np.nan, dtype=val.dtype) for _ in range(world)]
-    own = []
     for r in range(world):
         lrp, lc, lv = L.interleaved_local_csr(rp, col, val, cuts, world, K, r)
         _, yl, _ = S.spmv_oracle(lrp, lc, lv, x)
-        own.append(yl)
         at = 0
         for k in range(K):
             b0, b1 = int(cuts[k * world + r]), int(cuts[k * world + r + 1])
             ys[r][b0:b1] = yl[at:at + b1 - b0]
             at += b1 - b0
-    for k in range(K):  # broadcasts of chunk k
-        for root in range(world):
-            b0, b1 = int(cuts[k * world + root]), int(cuts[k * world + root + 1])
-            for r in range(world):
-                ys[r][b0:b1] = ys[root][b0:b1]
     return ys
 
 
-@pytest.mark.parametrize("world,K", [(2, 2), (3, 3), (8, 2), (1, 2)])
-def test_native_dist_partition_identity(world, K):
-    """The native RCCL path's data layout (lhpc_dist_spmv_plan_create input
-    and the broadcast schedule of lhpc_dist_spmv), checked on the CPU: every
-    rank ends with the unpartitioned y bit for bit (dyadic values), and the
-    local stacked CSRs cover A exactly once."""
+def _run_schedules(ys, cuts, world, K, exchange, broadcast=False):
+    """Execute, on the CPU, the transfers every rank's lhpc_dist_spmv issues
+    (lhpc_dist_exchange_schedule — the same host function the device path
+    walks) with RCCL / peer-store semantics, checking on the way that the
+    ranks' collectives match (same calls, same order: a mismatch would hang
+    RCCL) and that each in-place all-gather sends from its own slot."""
+    import libhpc_amd as L
+    sched = [L.dist_exchange_schedule(cuts, world, K, r, exchange, broadcast) for r in range(world)]
+    for k in range(K):
+        per = [[e for e in sched[r] if e["chunk"] == k] for r in range(world)]
+        if exchange == L.DIST_EXCHANGE_RCCL:
+            sig = [[(e["kind"], e["root"], e["group"], e["offset"], e["count"]) for e in per[r]] for r in range(world)]
+            assert all(sg == sig[0] for sg in sig), f"chunk {k}: collectives differ between ranks"
+            for j in range(len(per[0])):
+                e0 = per[0][j]
+                if e0["kind"] == L.XFER_ALLGATHER:
+                    off, cnt = e0["offset"], e0["count"]
+                    parts = []
+                    for r in range(world):
+                        assert per[r][j]["send_offset"] == off + r * cnt, "in-place all-gather slot"
+                        parts.append(ys[r][off + r * cnt:off + (r + 1) * cnt].copy())
+                    for r in range(world):
+                        for q in range(world):
+                            ys[r][off + q * cnt:off + (q + 1) * cnt] = parts[q]
+                else:
+                    assert e0["kind"] == L.XFER_BROADCAST and e0["group"] == 1
+                    off, cnt, root = e0["offset"], e0["count"], e0["root"]
+                    data = ys[root][off:off + cnt].copy()
+                    for r in range(world):
+                        ys[r][off:off + cnt] = data
+        else:
+            for r in range(world):
+                for e in per[r]:
+                    assert e["kind"] == L.XFER_PUSH and e["root"] == r
+                    off, cnt = e["offset"], e["count"]
+                    b = k * world + r
+                    assert (off, off + cnt) == (int(cuts[b]), int(cuts[b + 1])), "a rank pushes exactly its block"
+                    for q in range(world):
+                        if q != r:
+                            ys[q][off:off + cnt] = ys[r][off:off + cnt]
+    return sched
+
+
+@pytest.mark.parametrize("world,K", [(2, 2), (3, 3), (8, 2), (1, 2), (8, 1)])
+@pytest.mark.parametrize("kind", ["powerlaw", "uniform", "tiny"])
+@pytest.mark.parametrize("exchange", ["rccl", "rccl_bcast", "p2p"])
+def test_native_dist_exchange_schedule(world, K, kind, exchange):
+    """The native path's data layout (lhpc_dist_spmv_plan_create input) and
+    its exchange schedule (lhpc_dist_exchange_schedule, the function
+    broadcast/push issuing walks), run on the CPU for every rank: unequal
+    nnz-balanced blocks (power-law rows: broadcast groups), equal blocks
+    (uniform rows: one in-place all-gather per chunk), and a matrix with
+    fewer rows than blocks (empty blocks); every rank ends with the
+    unpartitioned y bit for bit (dyadic values), and the local stacked CSRs
+    cover A exactly once (SURVEY §8c partition identity)."""
     import libhpc_amd as L
     from tests import _support as S
-    n = 30_011
-    rp, col, val = L.gen_powerlaw_csr(n, n, lmax=2000, dtype=L.F32, dist=1, seed=0xD180)
-    x = L.gen_values(L.F32, 1, n, 0xD181)
+    if kind == "powerlaw":
+        n = 30_011
+        rp, col, val = L.gen_powerlaw_csr(n, n, lmax=2000, dtype=L.F32, dist=1, seed=0xD180)
+    elif kind == "uniform":
+        n = 4_096 * world * K
+        rp, col, val = L.gen_uniform_csr(n, n, 5, dtype=L.F64, dist=1, seed=0xD182)
+    else:
+        n = 5
+        rp, col, val = L.gen_uniform_csr(n, n, 2, dtype=L.F64, dist=1, seed=0xD183)
+    x = L.gen_values(L.F32 if val.dtype == np.float32 else L.F64, 1, n, 0xD181)
     _, want, _ = S.spmv_oracle(rp, col, val, x)
     cuts = L.interleaved_cuts(rp, world, K)
     assert sum(int(L.interleaved_local_csr(rp, col, val, cuts, world, K, r)[0][-1]) for r in range(world)) == rp[-1]
-    for r, y in enumerate(_native_emulation(rp, col, val, x, world, K)):
+    ys = _local_rows(rp, col, val, x, world, K, cuts)
+    xk = L.DIST_EXCHANGE_P2P if exchange == "p2p" else L.DIST_EXCHANGE_RCCL
+    sched = _run_schedules(ys, cuts, world, K, xk, broadcast=exchange == "rccl_bcast")
+    for r, y in enumerate(ys):
         assert np.array_equal(y, want), f"rank {r}"
+    kinds = {e["kind"] for s in sched for e in s}
+    if exchange == "p2p":
+        assert kinds <= {L.XFER_PUSH}
+    elif exchange == "rccl_bcast" or (kind == "powerlaw" and world > 1):
+        assert kinds <= {L.XFER_BROADCAST}
+    elif kind == "uniform":
+        assert kinds == {L.XFER_ALLGATHER}
+
+
+def test_exchange_schedule_rejects_bad_input():
+    import libhpc_amd as L
+    with pytest.raises(L.LhpcError):
+        L.dist_exchange_schedule([0, 5, 3, 8, 9], 2, 2, 0)  # cuts not ascending
+    with pytest.raises(L.LhpcError):
+        L.dist_exchange_schedule([0, 1, 2, 3, 4], 2, 2, 2)  # rank out of range

@@ -37,7 +37,7 @@ def test_unique_ids_differ(lhpc, gpu):
                                          (20_000, 7, 2), (20_000, 7, 4)])
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
 @pytest.mark.parametrize("range_gather", [False, True])
-def test_dist_spmv_world1_matches_single_plan(lhpc, gpu, comm, monkeypatch, n, per_row, K, dtype, range_gather):
+def test_dist_spmv_world1_matches_single_plan(lhpc, gpu, comm, n, per_row, K, dtype, range_gather):
     """lhpc_dist_spmv at world 1 with K chunks equals the single-plan SpMV bit
     for bit on dyadic values (XTILE row-range plan for the 3M-column matrix,
     one plan per block for the small one), twice in a row, y != x.
@@ -45,8 +45,7 @@ def test_dist_spmv_world1_matches_single_plan(lhpc, gpu, comm, monkeypatch, n, p
     whose xg exceeds the Infinity Cache does) and each chunk's range is
     gathered right before its reduce instead of one stage."""
     import torch
-    if range_gather:
-        monkeypatch.setenv("LHPC_XTILE_MALL", "2")
+    opts = {"xtile_ranges": 2} if range_gather else None
     dt = lhpc.F32 if dtype == "f32" else lhpc.F64
     rp, col, val = lhpc.gen_uniform_csr(n, n, per_row, dtype=dt, dist=1, seed=0xD200 + K)
     x = lhpc.gen_values(dt, 1, n, 0xD201)
@@ -54,7 +53,7 @@ def test_dist_spmv_world1_matches_single_plan(lhpc, gpu, comm, monkeypatch, n, p
     _, want, _ = S.spmv_oracle(rp, col, val, x)
     cuts = lhpc.interleaved_cuts(rp, 1, K)
     lrp, lc, lv = lhpc.interleaved_local_csr(rp, col, val, cuts, 1, K, 0)
-    with lhpc.DistSpMVPlan(comm, n, n, K, cuts, lrp, lc, lv) as d:
+    with lhpc.DistSpMVPlan(comm, n, n, K, cuts, lrp, lc, lv, options=opts) as d:
         for _ in range(2):
             y = torch.full((n,), float("nan"), dtype=xd.dtype, device=gpu)
             d(xd, y)
@@ -64,15 +63,15 @@ def test_dist_spmv_world1_matches_single_plan(lhpc, gpu, comm, monkeypatch, n, p
 
 @pytest.mark.parametrize("mode", ["allgather", "broadcast"])
 @pytest.mark.parametrize("uniform", [True, False])
-def test_dist_spmv_world1_rccl_exchange(lhpc, gpu, comm, monkeypatch, mode, uniform):
-    """The RCCL y exchange driven at world 1 (LHPC_DIST_EXCHANGE=1: the
+def test_dist_spmv_world1_rccl_exchange(lhpc, gpu, comm, mode, uniform):
+    """The RCCL y exchange driven at world 1 (options.dist_world1: the
     in-place collective is a no-op there, so y must come out unchanged):
     equal-size blocks go through one in-place ncclAllGather per chunk,
-    unequal ones (power-law rows) or LHPC_DIST_BCAST=1 through the broadcast
-    group; three calls, K = 3."""
+    unequal ones (power-law rows) or options.dist_broadcast through the
+    broadcast group; three calls, K = 3; then the exchange alone
+    (lhpc_dist_exchange) leaves y as it is."""
     import torch
-    monkeypatch.setenv("LHPC_DIST_EXCHANGE", "1")
-    monkeypatch.setenv("LHPC_DIST_BCAST", "1" if mode == "broadcast" else "0")
+    opts = {"dist_world1": 1, "dist_broadcast": 1 if mode == "broadcast" else 0}
     n, K = 600_000, 3
     if uniform:
         rp, col, val = lhpc.gen_uniform_csr(n, n, 6, dtype=lhpc.F32, dist=1, seed=0xD300)
@@ -82,12 +81,16 @@ def test_dist_spmv_world1_rccl_exchange(lhpc, gpu, comm, monkeypatch, mode, unif
     xd = torch.from_numpy(x).to(gpu)
     _, want, _ = S.spmv_oracle(rp, col, val, x)
     cuts = lhpc.interleaved_cuts(rp, 1, K)
-    with lhpc.DistSpMVPlan(comm, n, n, K, cuts, *lhpc.interleaved_local_csr(rp, col, val, cuts, 1, K, 0)) as d:
+    with lhpc.DistSpMVPlan(comm, n, n, K, cuts, *lhpc.interleaved_local_csr(rp, col, val, cuts, 1, K, 0),
+                           options=opts) as d:
         for _ in range(3):
             y = torch.full((n,), float("nan"), dtype=xd.dtype, device=gpu)
             d(xd, y)
             torch.cuda.synchronize()
             assert np.array_equal(y.cpu().numpy(), want)
+        d.exchange(y)
+        torch.cuda.synchronize()
+        assert np.array_equal(y.cpu().numpy(), want)
 
 
 def test_dist_spmv_rejects_aliased_xy(lhpc, gpu, comm):
@@ -116,20 +119,29 @@ def test_dist_stencil7_world1_matches_single_domain(lhpc, gpu, comm, nz, ny, nx)
     assert np.array_equal(od.cpu().numpy(), want)
 
 
-def test_dist_spmv_p2p_two_ranks_one_gpu(lhpc, gpu):
+P2P_CASES = {"barrier": 6, "loop": 8, "pingpong": 8, "tiny": 8}
+
+
+@pytest.mark.parametrize("case", list(P2P_CASES))
+def test_dist_spmv_p2p_two_ranks_one_gpu(lhpc, gpu, case):
     """The direct peer exchange (lhpc_dist_p2p_export/_import, READY/DONE
     flags, push kernel) with two processes on the box's one GPU: IPC-mapped
-    windows, RCCL-free local communicators, blobs over gloo.  Both ranks'
-    assembled y equal the oracle bit for bit (dyadic), three calls in a row
-    (epochs), fp32 XTILE row-range and fp64 per-block local plans.  (On one
-    GPU the pushes are device-local; over xGMI they are the same stores.)"""
+    windows, RCCL-free local communicators, blobs over gloo; every rank's
+    assembled y equals the oracle bit for bit (dyadic).  Cases
+    (tests/p2p_two_ranks.py): host-barriered calls (fp32 XTILE row-range and
+    fp64 per-block plans); the iterative loop x ← y with no host ordering
+    between calls (the flags are the only ordering); two windows ping-ponged
+    (y of call n is x of call n+1); 1–3-row blocks and windows of different
+    16-B phase.  (On one GPU the pushes are device-local; over xGMI they are
+    the same stores.)"""
     import json
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT="29631")
-    procs = [subprocess.Popen([sys.executable, os.path.join(root, "tests", "p2p_two_ranks.py")],
+    port = str(29631 + list(P2P_CASES).index(case))
+    env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    procs = [subprocess.Popen([sys.executable, os.path.join(root, "tests", "p2p_two_ranks.py"), case],
                               env=dict(env, RANK=str(r), LOCAL_RANK="0"), stdout=subprocess.PIPE,
                               stderr=subprocess.PIPE, text=True) for r in range(2)]
     outs = []
@@ -143,5 +155,5 @@ def test_dist_spmv_p2p_two_ranks_one_gpu(lhpc, gpu):
             if p.poll() is None:
                 p.kill()
     for o in outs:
-        assert all(o["ok"]) and len(o["ok"]) == 6, o
+        assert all(o["ok"]) and len(o["ok"]) == P2P_CASES[case], o
         assert all(s == 0 for s in o["status"]), o

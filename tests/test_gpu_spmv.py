@@ -29,9 +29,9 @@ FAMILIES = {
 GOLDEN_SPMV = sorted(glob.glob(os.path.join(S.GOLDEN, "spmv_*.npz")))
 
 
-def _run(lhpc, gpu, rp, col, val, x, n_cols, flags, device_buffers=True):
+def _run(lhpc, gpu, rp, col, val, x, n_cols, flags, device_buffers=True, options=None):
     import torch
-    with lhpc.SpMVPlan(rp, col, val, n_cols, flags=flags) as plan:
+    with lhpc.SpMVPlan(rp, col, val, n_cols, flags=flags, options=options) as plan:
         if device_buffers:
             xd = torch.from_numpy(x).to(gpu)
             y = plan(xd).cpu().numpy()
@@ -303,15 +303,15 @@ def _csr_from_lengths(lengths, n_cols, seed, dyadic):
 
 
 @pytest.fixture(params=["perm", "iperm"])
-def xt_layout(request, monkeypatch):
+def xt_layout(request):
     """The XTILE reduce index streams: perm (xg scattered into CSR slots) and
     iperm (xg kept in flat order in LDS, each CSR position's x gathered
-    through a CSR-order index)."""
-    monkeypatch.setenv("LHPC_XTILE_IPERM", "1" if request.param == "iperm" else "0")
-    return request.param
+    through a CSR-order index), pinned through lhpc_options.xtile_reduce.
+    Returns the options dict the test extends."""
+    return {"xtile_reduce": 2 if request.param == "iperm" else 1}
 
 
-def _check_xtile(lhpc, gpu, lengths, n_cols, dtype, seed, dyadic=True, expect_cont=None):
+def _check_xtile(lhpc, gpu, lengths, n_cols, dtype, seed, dyadic=True, expect_cont=None, opts=None):
     rp, col, val = _csr_from_lengths(lengths, n_cols, seed, dyadic)
     val = val.astype(dtype)
     rng = np.random.default_rng(seed + 1)
@@ -319,7 +319,7 @@ def _check_xtile(lhpc, gpu, lengths, n_cols, dtype, seed, dyadic=True, expect_co
         x = (rng.integers(-8, 9, size=n_cols) / 8.0).astype(dtype)
     else:
         x = rng.uniform(-1.0, 1.0, size=n_cols).astype(dtype)
-    y, info = _run(lhpc, gpu, rp, col, val, x, n_cols, FAMILIES["xtile"])
+    y, info = _run(lhpc, gpu, rp, col, val, x, n_cols, FAMILIES["xtile"], options=opts)
     assert info["kernel"] == lhpc.KERNEL_XTILE
     if expect_cont is not None:
         assert (info["n_long_rows"] > 0) == expect_cont
@@ -337,8 +337,8 @@ def test_xtile_long_rows_across_chunks(lhpc, gpu, dtype, xt_layout):
     finished by the fix-up: a 30k-row, rows of 5000/4096/4095/9000 between
     short rows, a long first and a long last row."""
     lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 3000 + [0, 0] + [30000]
-    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA100, expect_cont=True)
-    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA101, dyadic=False)
+    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA100, expect_cont=True, opts=xt_layout)
+    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA101, dyadic=False, opts=xt_layout)
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
@@ -346,7 +346,7 @@ def test_xtile_empty_row_runs(lhpc, gpu, dtype, xt_layout):
     """More than Rmax (1024) consecutive empty rows, leading and trailing
     empty rows, and an all-empty tail after the last nonzero."""
     lengths = [0] * 3000 + [7] * 10 + [0] * 2500 + [1] + [0] * 1500 + [4096] + [0] * 2049
-    _check_xtile(lhpc, gpu, lengths, 150_000, dtype, 0xA200)
+    _check_xtile(lhpc, gpu, lengths, 150_000, dtype, 0xA200, opts=xt_layout)
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
@@ -354,35 +354,35 @@ def test_xtile_wide_many_tiles(lhpc, gpu, dtype, xt_layout):
     """n_cols ≫ n_rows: hundreds of tiles, a ragged last tile, 1-nonzero rows."""
     rng = np.random.default_rng(0xA300)
     lengths = rng.integers(0, 40, size=5000)
-    _check_xtile(lhpc, gpu, lengths, 9_000_001, dtype, 0xA301)
-    _check_xtile(lhpc, gpu, np.ones(70_000, dtype=np.int64), 3_000_017, dtype, 0xA302)
+    _check_xtile(lhpc, gpu, lengths, 9_000_001, dtype, 0xA301, opts=xt_layout)
+    _check_xtile(lhpc, gpu, np.ones(70_000, dtype=np.int64), 3_000_017, dtype, 0xA302, opts=xt_layout)
 
 
-def test_xtile_small_gather_pieces(lhpc, gpu, monkeypatch, xt_layout):
+def test_xtile_small_gather_pieces(lhpc, gpu, xt_layout):
     """Several gather workgroups per tile (piece bounds inside a tile) give the same bits."""
-    monkeypatch.setenv("LHPC_XTILE_PIECE", "1000")
+    opts = dict(xt_layout, xtile_piece=1000)
     rng = np.random.default_rng(0xA400)
     lengths = rng.integers(0, 60, size=20_000)
-    _check_xtile(lhpc, gpu, lengths, 100_000, np.float32, 0xA401)
-    for u in ("2", "4", "16"):  # gather steps in flight (default 8)
-        monkeypatch.setenv("LHPC_XTILE_U", u)
-        _check_xtile(lhpc, gpu, lengths, 100_000, np.float64, 0xA402)
-        _check_xtile(lhpc, gpu, lengths, 100_000, np.float32, 0xA403)
+    _check_xtile(lhpc, gpu, lengths, 100_000, np.float32, 0xA401, opts=opts)
+    for u in (2, 4, 16):  # gather steps in flight (default 8)
+        opts["xtile_steps"] = u
+        _check_xtile(lhpc, gpu, lengths, 100_000, np.float64, 0xA402, opts=opts)
+        _check_xtile(lhpc, gpu, lengths, 100_000, np.float32, 0xA403, opts=opts)
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_xtile_nt_gather_stores(lhpc, gpu, monkeypatch, dtype, xt_layout):
-    """Non-temporal xg stores in the gather (LHPC_XTILE_NTSTORE=1) give the
-    same bits, with full and partial 64-group store blocks and cut rows."""
-    monkeypatch.setenv("LHPC_XTILE_NTSTORE", "1")
+def test_xtile_nt_gather_stores(lhpc, gpu, dtype, xt_layout):
+    """Non-temporal xg stores in the gather (options.xtile_store = STORE_NT)
+    give the same bits, with full and partial 64-group store blocks and cut rows."""
+    opts = dict(xt_layout, xtile_store=lhpc.STORE_NT)
     lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 3000 + [0, 0] + [30000]
-    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA500, expect_cont=True)
-    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA501, dyadic=False)
+    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA500, expect_cont=True, opts=opts)
+    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA501, dyadic=False, opts=opts)
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("range_pieces", [False, True])
-def test_xtile_split_ranges(lhpc, gpu, monkeypatch, dtype, xt_layout, range_pieces):
+def test_xtile_split_ranges(lhpc, gpu, dtype, xt_layout, range_pieces):
     """Row-range plan (lhpc_spmv_plan_create_split): stage once, reduce each
     range into its own buffer; long rows end at and start right after the
     split rows; the concatenation equals the whole-matrix oracle bit for bit
@@ -391,8 +391,7 @@ def test_xtile_split_ranges(lhpc, gpu, monkeypatch, dtype, xt_layout, range_piec
     Infinity Cache): stage gathers every range's pieces, lhpc_spmv runs
     gather k / reduce k."""
     import torch
-    if range_pieces:
-        monkeypatch.setenv("LHPC_XTILE_MALL", "2")
+    opts = dict(xt_layout, xtile_ranges=2 if range_pieces else 0)
     lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 30000 + [0, 0] + [30000]
     n_cols = 200_000
     rp, col, val = _csr_from_lengths(lengths, n_cols, 0xA700, dyadic=True)
@@ -401,7 +400,7 @@ def test_xtile_split_ranges(lhpc, gpu, monkeypatch, dtype, xt_layout, range_piec
     x = (rng.integers(-8, 9, size=n_cols) / 8.0).astype(dtype)
     n = len(lengths)
     splits = [1, 51, 57, 20000, n - 1]  # after the long first row, around the long rows, before the last
-    with lhpc.SpMVPlan(rp, col, val, n_cols, flags=FAMILIES["xtile"], splits=splits) as plan:
+    with lhpc.SpMVPlan(rp, col, val, n_cols, flags=FAMILIES["xtile"], splits=splits, options=opts) as plan:
         assert plan.info()["kernel"] == lhpc.KERNEL_XTILE
         xd = torch.from_numpy(x).to(gpu)
         bounds = [0] + splits + [n]
@@ -420,15 +419,15 @@ def test_xtile_split_ranges(lhpc, gpu, monkeypatch, dtype, xt_layout, range_piec
 
 @pytest.mark.parametrize("ranges", [2, 3, 5])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_xtile_cache_ranges(lhpc, gpu, monkeypatch, dtype, ranges, xt_layout):
-    """Cache-sized ranges (LHPC_XTILE_MALL=K, the default for large fp32
+def test_xtile_cache_ranges(lhpc, gpu, dtype, ranges, xt_layout):
+    """Cache-sized ranges (options.xtile_ranges = K, the default for large fp32
     plans): gather k and reduce k in turn over K nnz-balanced row ranges,
     each range's gather pieces rounded up to 8-entry bounds inside a tile (its
     first ≤ 7 entries come from the previous range's gather), one fix-up for
     every range's cut rows.  Long rows crossing chunks, a tiny piece size (so
     ranges hold several pieces per tile), two calls in a row; bit-exact."""
     import torch
-    monkeypatch.setenv("LHPC_XTILE_MALL", str(ranges))
+    opts = dict(xt_layout, xtile_ranges=ranges)
     lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 30000 + [0, 0] + [30000]
     n_cols = 200_000
     rp, col, val = _csr_from_lengths(lengths, n_cols, 0xA900 + ranges, dyadic=True)
@@ -436,10 +435,9 @@ def test_xtile_cache_ranges(lhpc, gpu, monkeypatch, dtype, ranges, xt_layout):
     rng = np.random.default_rng(0xA9F0 + ranges)
     x = (rng.integers(-8, 9, size=n_cols) / 8.0).astype(dtype)
     _, yr, _ = S.spmv_oracle(rp, col, val, x)
-    for piece in ("", "1000"):
-        if piece:
-            monkeypatch.setenv("LHPC_XTILE_MALL_PIECE", piece)
-        with lhpc.SpMVPlan(rp, col, val, n_cols, flags=FAMILIES["xtile"]) as plan:
+    for piece in (0, 1000):
+        opts["xtile_range_piece"] = piece
+        with lhpc.SpMVPlan(rp, col, val, n_cols, flags=FAMILIES["xtile"], options=opts) as plan:
             info = plan.info()
             assert info["kernel"] == lhpc.KERNEL_XTILE
             assert info["launches"] == 2 * ranges + (1 if info["n_long_rows"] else 0)
@@ -457,7 +455,7 @@ def test_split_plan_unsupported_without_xtile(lhpc, gpu):
 
 
 def test_xtile_is_auto_choice_without_locality(lhpc, gpu):
-    """x > 8 MB with uniform random columns selects XTILE; LHPC_SPMV_XTILE=0 gives XSLICE."""
+    """x > 8 MB with uniform random columns selects XTILE; options.spmv_no_xtile gives XSLICE."""
     n = 3_000_000
     rp, col, val = lhpc.gen_uniform_csr(n, n, 4, dtype=lhpc.F32, dist=1, seed=0xA500)
     x = lhpc.gen_values(lhpc.F32, 1, n, 0xA501)
@@ -466,3 +464,22 @@ def test_xtile_is_auto_choice_without_locality(lhpc, gpu):
     assert info["launches"] in (2, 3)
     _, yr, _ = S.spmv_oracle(rp, col, val, x)
     assert np.array_equal(y, yr)
+    y2, info2 = _run(lhpc, gpu, rp, col, val, x, n, 0, options={"spmv_no_xtile": 1})
+    assert info2["kernel"] == lhpc.KERNEL_XSLICE
+    assert np.array_equal(y2, yr)
+
+
+@pytest.mark.parametrize("lanes,rows", [(4, 4), (16, 8), (64, 1)])
+def test_rowgroup_shape_option(lhpc, gpu, lanes, rows):
+    """options.rowgroup_lanes/rows pin the ROWGROUP shape (same bits on
+    dyadic inputs); a shape the library does not instantiate is refused."""
+    rp, col, val = lhpc.gen_powerlaw_csr(20_000, 20_000, lmax=300, dtype=lhpc.F32, dist=1, seed=0xA600)
+    x = lhpc.gen_values(lhpc.F32, 1, 20_000, 0xA601)
+    y, info = _run(lhpc, gpu, rp, col, val, x, 20_000, FAMILIES["rowgroup"],
+                   options={"rowgroup_lanes": lanes, "rowgroup_rows": rows})
+    assert info["lanes_per_row"] == lanes and info["rows_per_group"] == rows
+    _, yr, _ = S.spmv_oracle(rp, col, val, x)
+    assert np.array_equal(y, yr)
+    with pytest.raises(lhpc.LhpcError):
+        lhpc.SpMVPlan(rp, col, val, 20_000, flags=FAMILIES["rowgroup"],
+                      options={"rowgroup_lanes": 8, "rowgroup_rows": 8})

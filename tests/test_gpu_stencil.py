@@ -118,26 +118,33 @@ S7_IMPLS = ["buf", "buf:2,8,0,2", "buf:4,4,128,3", "buf:2,8,5,3", "buf:2,8,32", 
             "buf:2,8,4", "simple"]
 
 
+def _s7_options(lhpc, name, cfg, store):
+    """lhpc_options fields for a stencil7 variant: impl name, "RY,NJ,ZC[,PF]", store policy."""
+    o = {"stencil7_impl": {"buf": lhpc.S7_RING, "buf4": lhpc.S7_RING_X4, "simple": lhpc.S7_SIMPLE}[name],
+         "stencil7_store": {"nt": lhpc.STORE_NT, "plain": lhpc.STORE_PLAIN, "staged": lhpc.STORE_STAGED}[store]}
+    if cfg:
+        for k, v in zip(("stencil7_ry", "stencil7_nj", "stencil7_zc", "stencil7_pf"), cfg.split(",")):
+            o[k] = int(v)
+    return o
+
+
 @pytest.mark.parametrize("impl", S7_IMPLS)
 @pytest.mark.parametrize("store", ["nt", "plain", "staged"])
-def test_stencil7_every_impl(lhpc, gpu, impl, store, monkeypatch):
+def test_stencil7_every_impl(lhpc, gpu, impl, store):
     """Every stencil7 implementation / tiling / store mode selectable through
-    LHPC_STENCIL7_* ("simple": the thread-per-column kernel the launcher
+    lhpc_options.stencil7_* ("simple": the thread-per-column kernel the launcher
     falls back to when a row's byte offset does not fit a buffer voffset) is
     bit-exact against the oracle on ragged shapes: nx
     spanning several 512-wide x tiles with a partial last one, ny and nz not
     multiples of the row / z-chunk tiles, ghost widths 1 and 2."""
     name, _, cfg = impl.partition(":")
-    monkeypatch.setenv("LHPC_STENCIL7_IMPL", name)
-    if cfg:
-        monkeypatch.setenv("LHPC_STENCIL7_BUF", cfg)
-    monkeypatch.setenv("LHPC_STENCIL7_STORE", store)
+    opts = _s7_options(lhpc, name, cfg, store)
     for (nz, ny, nx, g) in ((37, 45, 1100, 1), (9, 19, 130, 2), (3, 2, 1, 1)):
         shape = (nz + 2 * g, ny + 2 * g, nx + 2 * g)
         u = S.random_padded(shape, seed=nz * 7 + nx + g, zero_ghost=False).reshape(-1)
         out0 = S.random_padded(shape, seed=1234 + g).reshape(-1)
         want = S.stencil7_oracle(u, nz, ny, nx, g, -6.0, 1.0, out=out0.copy())
-        got = lhpc.stencil7(_dev(gpu, u), _dev(gpu, out0), nz, ny, nx, g, -6.0, 1.0).cpu().numpy()
+        got = lhpc.stencil7(_dev(gpu, u), _dev(gpu, out0), nz, ny, nx, g, -6.0, 1.0, options=opts).cpu().numpy()
         assert np.array_equal(got, want), (impl, store, nz, ny, nx, g)
 
 
@@ -146,15 +153,13 @@ S7_BUF4 = ["2,8,0", "2,8,5", "1,8,16", "4,8,32", "2,4,7", "4,4,32"]
 
 @pytest.mark.parametrize("cfg", S7_BUF4)
 @pytest.mark.parametrize("store", ["nt", "plain"])
-def test_stencil7_buf4(lhpc, gpu, cfg, store, monkeypatch):
-    """The x4 ring (LHPC_STENCIL7_IMPL=buf4, 4 consecutive x per lane,
+def test_stencil7_buf4(lhpc, gpu, cfg, store):
+    """The x4 ring (stencil7_impl = S7_RING_X4, 4 consecutive x per lane,
     dwordx4 loads/stores at 4-B alignment) is bit-exact against the oracle on
     shapes whose nx is a multiple of its tile width — one and several x tiles,
     ny / nz ragged against the row and z-chunk tiles, ghost widths 1 to 3 (so
     rows start at every 4-B phase of a 16-B line).  Other nx fall back to the dword ring (covered above)."""
-    monkeypatch.setenv("LHPC_STENCIL7_IMPL", "buf4")
-    monkeypatch.setenv("LHPC_STENCIL7_BUF", cfg)
-    monkeypatch.setenv("LHPC_STENCIL7_STORE", store)
+    opts = _s7_options(lhpc, "buf4", cfg, store)
     for (nz, ny, nx, g) in ((37, 45, 1024, 1), (9, 19, 512, 2), (3, 2, 1536, 3), (5, 9, 512, 1)):
         if nx % (64 * int(cfg.split(",")[1])):
             continue
@@ -162,21 +167,20 @@ def test_stencil7_buf4(lhpc, gpu, cfg, store, monkeypatch):
         u = S.random_padded(shape, seed=nz * 7 + nx + g, zero_ghost=False).reshape(-1)
         out0 = S.random_padded(shape, seed=1234 + g).reshape(-1)
         want = S.stencil7_oracle(u, nz, ny, nx, g, -6.0, 1.0, out=out0.copy())
-        got = lhpc.stencil7(_dev(gpu, u), _dev(gpu, out0), nz, ny, nx, g, -6.0, 1.0).cpu().numpy()
+        got = lhpc.stencil7(_dev(gpu, u), _dev(gpu, out0), nz, ny, nx, g, -6.0, 1.0, options=opts).cpu().numpy()
         assert np.array_equal(got, want), (cfg, store, nz, ny, nx, g)
 
 
-@pytest.mark.parametrize("rows", ["1", "2", "4", "8", "16", "32"])
-def test_blur_x_every_impl(lhpc, gpu, rows, monkeypatch):
-    """The wave-private blur_x at every rows-per-wave setting (LHPC_BLUR_X_RW)
+@pytest.mark.parametrize("rows", [1, 2, 4, 8, 16, 32])
+def test_blur_x_every_impl(lhpc, gpu, rows):
+    """The wave-private blur_x at every rows-per-wave setting (options.blur_x_rows)
     is bit-exact against the oracle on vector-eligible ragged shapes: nx not a
     multiple of the 256-float segment, ny not a multiple of the row group.
     (Unaligned shapes take the block-LDS kernel: test_blur_shapes_vs_oracle.)"""
     import torch
-    monkeypatch.setenv("LHPC_BLUR_X_RW", rows)
     for ny, nx, ghost in ((37, 260, 8), (5, 1300, 8), (70, 2048, 12), (1, 4, 8)):
         a = S.random_padded(((ny + 2 * ghost) * (nx + 2 * ghost),), seed=ny * 31 + nx)
         want = S.blur_oracle(a, ny, nx, ghost, 8, False)
         b = torch.empty(ny * nx, dtype=torch.float32, device=gpu)
-        got = lhpc.blur_x(_dev(gpu, a), b, ny, nx, ghost, 8).cpu().numpy()
+        got = lhpc.blur_x(_dev(gpu, a), b, ny, nx, ghost, 8, options={"blur_x_rows": rows}).cpu().numpy()
         assert np.array_equal(got, want), (rows, ny, nx, ghost)

@@ -4,6 +4,8 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O="$R/gpurun_out/ab"; mkdir -p "$O"
 export TMPDIR=/tmp
+# variants set LHPC_* knobs: only the tuning build reads them (make -C libhpc_amd/csrc tuning)
+[ -f "$R/libhpc_amd/_lib_tuning/liblhpc.so" ] && export LHPC_LIB_PATH=${LHPC_LIB_PATH:-$R/libhpc_amd/_lib_tuning/liblhpc.so}
 log() { echo "== $* $(date +%T)" >> "$O/progress.log"; }
 IFS=';' read -ra VS <<< "${AB:-base:X=0}"
 for rep in $(seq 1 ${REPS:-1}); do
