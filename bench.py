@@ -221,7 +221,18 @@ def main():
                 xtimes[kx] = {"step_ms": e2e * 1e3, "exchange_only_ms": xo * 1e3,
                               "gflops": 2.0 * nnz / e2e / 1e9}
             spmv_only = timed(lambda: dplans["none"](xd, y_full, stream=stream), args.steps, args.warmup)
-            chosen = min(xtimes, key=lambda k: xtimes[k]["step_ms"]) if xtimes else "none"
+            # the peer exchange competes only with a y identical on every rank
+            # to the RCCL one (read on the device, through this GPU's caches)
+            if "p2p" in xtimes and "rccl" in xtimes:
+                dplans["rccl"](xd, y_full, stream=stream)
+                dplans["p2p"](xd, y_p2p, stream=stream)
+                same = torch.tensor([1 if torch.equal(y_full, y_p2p) else 0], dtype=torch.int32, device=dev)
+                dist.all_reduce(same, op=dist.ReduceOp.MIN)
+                xtimes["p2p"]["same_y_as_rccl"] = bool(same.item())
+                if not same.item():
+                    xtimes["p2p"]["excluded"] = "y differs from the RCCL exchange"
+            eligible = [k for k in xtimes if "excluded" not in xtimes[k]]
+            chosen = min(eligible, key=lambda k: xtimes[k]["step_ms"]) if eligible else "none"
             dplan = dplans[chosen]
             y_out_buf = ybuf[chosen]
             exchange_report = {"chosen": chosen, "spmv_only_ms": spmv_only * 1e3, **xtimes, **xnotes,

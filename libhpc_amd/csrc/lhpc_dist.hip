@@ -76,6 +76,7 @@ struct lhpc_dist_comm {
   bool flags_mapped = false;
   uint32_t *h_status = nullptr;  // host-mapped: bit 0 = a flag wait timed out
   uint32_t epoch = 0;
+  int cus = 256;  // compute units of the device (k_p2p_acquire_all grid)
   P2pWindow win[LHPC_DIST_P2P_MAX_WINDOWS];
   int n_win = 0;
 };
@@ -163,6 +164,12 @@ __global__ void k_p2p_wait(const uint32_t *flags, int base, uint32_t e, int nran
     __builtin_amdgcn_s_sleep(127);
   }
 }
+// after every peer's DONE: a system-scope acquire on every XCD.  The peers'
+// stores reached this GPU's memory over xGMI without passing its L2s, so a
+// line of y that an XCD's L2 still holds from before (the gather of the next
+// call reads y as x) could be stale; one block per CU (dealt round-robin
+// over the XCDs) invalidates them all before the compute stream continues.
+__global__ void k_p2p_acquire_all() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
 // bytes [o0, o1) of this rank's y into the same bytes of every peer's y;
 // offsets are multiples of 4.  16-B stores on [a0, a1) (the 16-B aligned
 // interior) for peers whose y has our 16-B phase, head [o0, a0) and tail
@@ -263,6 +270,8 @@ int p2p_exchange_end(lhpc_dist_comm *c) {
   LHPC_HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_p2p_wait, dim3(1), dim3(64), 0, c->s_comm, c->flags, c->nranks, c->epoch, c->nranks, c->rank,
                      c->h_status);
+  LHPC_HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_p2p_acquire_all, dim3(static_cast<unsigned>(c->cus)), dim3(64), 0, c->s_comm);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -381,6 +390,8 @@ extern "C" int lhpc_dist_comm_create(lhpc_dist_comm **out, const unsigned char *
   c->nranks = nranks;
   c->rank = rank;
   c->device = device;
+  (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (c->cus < 8) c->cus = 256;
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
   const ncclResult_t st = ncclCommInitRank(&c->comm, nranks, uid, rank);
@@ -407,6 +418,8 @@ extern "C" int lhpc_dist_comm_create_local(lhpc_dist_comm **out, int nranks, int
   c->nranks = nranks;
   c->rank = rank;
   c->device = device;
+  (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (c->cus < 8) c->cus = 256;
   const hipError_t he = hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking);
   if (he != hipSuccess) {
     delete c;

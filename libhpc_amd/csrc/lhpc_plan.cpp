@@ -206,7 +206,7 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
     o.rchunk.push_back(c);
   }
   o.rchunk.push_back(C);
-  if (static_cast<double>(C + 1) * static_cast<double>(S) > 2.7e8) return LHPC_ERR_UNSUPPORTED;
+  if (M > 65535 / (kXtSegHi - 1)) return LHPC_ERR_UNSUPPORTED;  // seg lo fits 16 bits
   o.cont.clear();
   for (int64_t c = 0; c < C; ++c) {
     const int64_t r0 = o.cr[c], r1 = o.cr[c + 1];
@@ -329,6 +329,20 @@ int xtile_transpose_runs(const XtileHost &o, const void *val, size_t tsz, int ru
     }
   }
   return LHPC_OK;
+}
+
+void xtile_segment_table(const XtileHost &o, std::vector<uint32_t> &seg, std::vector<int32_t> &hi) {
+  const int64_t S = o.S, C = o.n_chunks, H = (C + kXtSegHi - 1) / kXtSegHi;
+  seg.assign(static_cast<size_t>(std::max<int64_t>(C, 1) * S), 0u);
+  hi.assign(static_cast<size_t>(std::max<int64_t>(H, 1) * S), 0);
+#pragma omp parallel for schedule(static)
+  for (int64_t c = 0; c < C; ++c) {
+    const int32_t *a = o.segoff.data() + c * S, *b = a + S, *h = o.segoff.data() + (c / kXtSegHi) * kXtSegHi * S;
+    if (c % kXtSegHi == 0) std::memcpy(hi.data() + (c / kXtSegHi) * S, a, sizeof(int32_t) * static_cast<size_t>(S));
+    for (int64_t s = 0; s < S; ++s)
+      seg[static_cast<size_t>(c * S + s)] =
+          static_cast<uint32_t>(a[s] - h[s]) | (static_cast<uint32_t>(b[s] - a[s]) << 16);
+  }
 }
 
 void xtile_range_pieces(XtileHost &o, int64_t piece_nnz, std::vector<int64_t> &rpc) {

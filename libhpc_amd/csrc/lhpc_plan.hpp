@@ -78,8 +78,17 @@ struct XtileHost {
   std::unique_ptr<uint16_t[]> iperm;
 };
 
+// Device form of the segment table (the reduce reads one 4-B word per tile
+// and chunk instead of two starts): seg[c·S + s] = lo | len << 16 with
+// start(c, s) = hi[⌊c / kXtSegHi⌋·S + s] + lo and len = start(c+1, s) −
+// start(c, s) ≤ M; lo ≤ (kXtSegHi − 1)·M < 2^16 for M ≤ 8192.  Size ≈ 4.6 B
+// per (chunk, tile): 21 MB for C2, 1.3 GB at n = 80M (where a dense int32
+// table of starts hit the old 2.7e8-entry limit).
+constexpr int kXtSegHi = 7;
+void xtile_segment_table(const XtileHost &o, std::vector<uint32_t> &seg, std::vector<int32_t> &hi);
+
 // 0 on success; LHPC_ERR_UNSUPPORTED when the layout does not fit its
-// index types (nnz + padding ≥ 2^31, S > 4096, or an oversized segment table).
+// index types (nnz + padding ≥ 2^31 or S > 4096).
 // piece_nnz: target nonzeros per gather workgroup (a multiple of 8 is used).
 // cut_window: see above, in (0, M] (M/2 cuts at any row start in the back half).
 // splits: ascending rows in (0, n_rows) at which a chunk must start (row

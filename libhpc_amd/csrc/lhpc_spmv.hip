@@ -368,7 +368,7 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
   for (void *q : {p->d_row_ptr, static_cast<void *>(p->d_col), p->d_val, static_cast<void *>(p->d_blocks),
                   p->d_xstage, p->d_ystage, p->d_lens, static_cast<void *>(p->d_cbase), p->d_partial,
                   static_cast<void *>(p->d_dpart), static_cast<void *>(p->d_cdesc), static_cast<void *>(p->d_cr),
-                  static_cast<void *>(p->d_segoff), static_cast<void *>(p->d_pieces), static_cast<void *>(p->d_cont),
+                  static_cast<void *>(p->d_seghi), static_cast<void *>(p->d_seg), static_cast<void *>(p->d_pieces), static_cast<void *>(p->d_cont),
                   static_cast<void *>(p->d_col16), static_cast<void *>(p->d_perm), p->d_xg,
                   static_cast<void *>(p->d_carry)})
     if (q) (void)hipFree(q);

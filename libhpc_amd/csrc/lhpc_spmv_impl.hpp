@@ -52,7 +52,8 @@ struct lhpc_spmv_plan {
   // xt_srow[k+1]) = chunks [xt_src[k], xt_src[k+1]), cont entries [xt_sco[k], xt_sco[k+1])
   std::vector<int64_t> split_rows, xt_srow, xt_src, xt_sco;
   int32_t *d_cdesc = nullptr;
-  int32_t *d_cr = nullptr, *d_segoff = nullptr, *d_pieces = nullptr, *d_cont = nullptr;
+  int32_t *d_cr = nullptr, *d_seghi = nullptr, *d_pieces = nullptr, *d_cont = nullptr;
+  uint32_t *d_seg = nullptr;  // segment table (lhpc_plan.hpp xtile_segment_table)
   uint16_t *d_col16 = nullptr, *d_perm = nullptr;
   int xt_p = 1;  // reduce: 1 perm scatter, 3 iperm gather (DESIGN.md §4 XTILE)
   void *d_xg = nullptr;

@@ -95,9 +95,28 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
           tv16 v;
 #pragma unroll
           for (int k = 0; k < VW; ++k) v[k] = o[h * VW + k];
+#if defined(LHPC_XT_PROBE_GROUPED)
+          // timing-only probe (wrong results): the store pattern of a tile-
+          // grouped xg layout — groups of G tiles on one XCD (blocks with
+          // equal b % 8, consecutive b / 8), every (tile, chunk) segment 9
+          // 16-B units, stored at ((group·Cp + chunk)·G + tile in group)·9 + j
+          {
+            constexpr int G = LHPC_XT_PROBE_GROUPED, LQ = 9;
+            const int bx = blockIdx.x % 8, bj = blockIdx.x / 8;
+            const int64_t gi = (bj / G) * 8 + bx, tg = bj % G;
+            const int64_t qv = static_cast<int64_t>(qb - q0) * 8 / VW + h * kWave + lane;  // 16-B unit in the piece
+            const int64_t cp = static_cast<int64_t>(q1 - q0) * 8 / VW / LQ + 1;
+            const int64_t units = static_cast<int64_t>(gridDim.x) * cp * LQ;  // ≈ the launch's share of xg
+            const int64_t d = (((gi * cp + qv / LQ) * G + tg) * LQ + qv % LQ) % units;
+            tv16 *a = reinterpret_cast<tv16 *>(xg) + d;
+            if constexpr (NT) __builtin_nontemporal_store(v, a);
+            else *a = v;
+          }
+#else
           tv16 *a = reinterpret_cast<tv16 *>(blk + h * kWave * VW + VW * lane);
           if constexpr (NT) __builtin_nontemporal_store(v, a);
           else *a = v;
+#endif
         }
       } else if (qq < q1) {
 #pragma unroll
@@ -191,7 +210,8 @@ __device__ uint64_t g_xt_stamps[1 << 22];
 #endif
 template <typename T, int G, int BLK, bool IP>
 __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce(
-    const int32_t *__restrict__ cdesc, const int32_t *__restrict__ segoff, int S, int64_t c0, int64_t C,
+    const int32_t *__restrict__ cdesc, const uint32_t *__restrict__ seg, const int32_t *__restrict__ seghi, int S,
+    int64_t c0, int64_t C,
     int64_t Cx, int total, const T *__restrict__ xg, const uint16_t *__restrict__ perm,
     const T *__restrict__ val, const int32_t *__restrict__ rp, T *__restrict__ y,
     double *__restrict__ carry) {
@@ -234,8 +254,10 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   for (int q = 0; q < G; ++q) {
     const int sI = tid * G + q;
     const int sc = sI < S ? sI : S - 1;
-    sa[q] = segoff[c * S + sc];
-    sb[q] = segoff[(c + 1) * S + sc];
+    // segment table (lhpc_plan.hpp xtile_segment_table): start = hi + lo, end = start + len
+    const uint32_t w = seg[c * S + sc];
+    sa[q] = seghi[(c / kXtSegHi) * S + sc] + static_cast<int>(w & 0xFFFFu);
+    sb[q] = sa[q] + static_cast<int>(w >> 16);
   }
   const u32x4 d = *reinterpret_cast<const u32x4 *>(cdesc + 8 * c);
   const u32x4 d2 = *reinterpret_cast<const u32x4 *>(cdesc + 8 * c + 4);
@@ -368,14 +390,20 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
 #if defined(LHPC_XT_PROBE_XG)
       // timing-only probe (wrong results): 1 = the chunk's xg as one aligned
       // contiguous run, 16-B LDS-DMA per lane; 2 = the same, non-temporal;
-      // 3 = no xg loads
-      if constexpr (LHPC_XT_PROBE_XG != 3) {
+      // 3 = no xg loads; 4 = one contiguous run, 4-B LDS-DMA per lane
+      if constexpr (LHPC_XT_PROBE_XG == 1 || LHPC_XT_PROBE_XG == 2) {
 #pragma unroll
         for (int u = 0; u < NB / 4; ++u)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
               xr_rs, (__attribute__((address_space(3))) void *)(xs + (wv * NB + 4 * u) * kWave), 16,
               static_cast<int>((c * M + (wv * NB + 4 * u) * kWave + 4 * lane) * 4), 0, 0,
               LHPC_XT_PROBE_XG == 2 ? 2 : 0);
+      } else if constexpr (LHPC_XT_PROBE_XG == 4) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              xr_rs, (__attribute__((address_space(3))) void *)(xs + (wv * NB + u) * kWave), 4,
+              static_cast<int>((c * M + (wv * NB + u) * kWave + lane) * 4), 0, 0, 0);
       }
       (void)src;
 #else
@@ -389,12 +417,37 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
 #endif
       load_ipv();
     } else {
+#if defined(LHPC_XT_PROBE_XG)
+      // timing-only probes, fp64: 1 = contiguous 16-B loads per lane (two
+      // positions each) + ds_write_b128; 3 = none; 4 = contiguous 8-B loads
+      if constexpr (LHPC_XT_PROBE_XG == 1 || LHPC_XT_PROBE_XG == 2) {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        d2 xv[NB / 2];
+#pragma unroll
+        for (int u = 0; u < NB / 2; ++u)
+          xv[u] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(
+                                             xr_rs, static_cast<int>((c * M + (wv * NB + 2 * u) * kWave + 2 * lane) * 8), 0,
+                                             LHPC_XT_PROBE_XG == 2 ? 2 : 0));
+#pragma unroll
+        for (int u = 0; u < NB / 2; ++u) *reinterpret_cast<d2 *>(xs + (wv * NB + 2 * u) * kWave + 2 * lane) = xv[u];
+      } else if constexpr (LHPC_XT_PROBE_XG == 4) {
+        T xv[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+          xv[u] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(
+                                            xr_rs, static_cast<int>((c * M + (wv * NB + u) * kWave + lane) * 8), 0, 0));
+#pragma unroll
+        for (int u = 0; u < NB; ++u) xs[(wv * NB + u) * kWave + lane] = xv[u];
+      }
+      (void)src;
+#else
       T xv[NB];
 #pragma unroll
       for (int u = 0; u < NB; ++u)
         xv[u] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(xr_rs, src[u] * 8, 0, 0));
 #pragma unroll
       for (int u = 0; u < NB; ++u) xs[(wv * NB + u) * kWave + lane] = xv[u];
+#endif
       load_ipv();
     }
   } else {
@@ -610,12 +663,13 @@ int launch_reduce(const lhpc_spmv_plan *p, int64_t c0, int64_t c1, int64_t n0, i
     const int64_t Cx = (c1 - c0 + 7) / 8;
     const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(xt_red_blk<T>());
     const void *fn = xtile_reduce_fn<T>(xtile_g<T>(p->S), p->xt_p == 3);
-    const int32_t *cd = p->d_cdesc, *so = p->d_segoff, *rp = static_cast<const int32_t *>(p->d_row_ptr);
+    const int32_t *cd = p->d_cdesc, *sh = p->d_seghi, *rp = static_cast<const int32_t *>(p->d_row_ptr);
+    const uint32_t *so = p->d_seg;
     int S = p->S, total = static_cast<int>(p->xt_total);
     const T *xg = static_cast<const T *>(p->d_xg), *val = static_cast<const T *>(p->d_val);
     const uint16_t *perm = p->d_perm;
     double *carry = p->d_carry;
-    void *args[] = {&cd, &so, &S, &c0, &c1, const_cast<int64_t *>(&Cx), &total, &xg, &perm, &val, &rp, &y, &carry};
+    void *args[] = {&cd, &so, &sh, &S, &c0, &c1, const_cast<int64_t *>(&Cx), &total, &xg, &perm, &val, &rp, &y, &carry};
     LHPC_HIP_TRY(hipLaunchKernel(fn, rg, rb, args, p->xt_lds, s));
     LHPC_TRY(check_launch(s));
   }
@@ -752,7 +806,13 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cont), xt.cont.data(), xt.cont.size() * 4));
   xtile_permute_gather_blocks(xt, static_cast<int>(16 / tsz));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_col16), xt.col16.get(), static_cast<size_t>(xt.total) * 2));
-  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_segoff), xt.segoff.data(), xt.segoff.size() * 4));
+  {
+    std::vector<uint32_t> seg;
+    std::vector<int32_t> seghi;
+    xtile_segment_table(xt, seg, seghi);
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_seg), seg.data(), seg.size() * 4));
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_seghi), seghi.data(), seghi.size() * 4));
+  }
   if (ip) {
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), ipt.get(), nrun * 2));
   } else {

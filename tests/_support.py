@@ -198,3 +198,17 @@ def laplacian_2d(nx, ny, dtype=np.float64, shift=0.0):
     import libhpc_amd as L
     rp, col, val = L.gen_laplacian_2d(nx, ny, L.F32 if dtype == np.float32 else L.F64, shift)
     return rp.astype(np.int32), col, val
+
+
+def sampled_rows_fp64(rp, col, val, x, m, seed=0x5EED00C1):
+    """(rows, y64, Σ|a·x|) on m seeded rows, fp64 numpy (no oracle/ code):
+    the full-size checks where the oracle's whole-matrix pass is too slow."""
+    n = rp.shape[0] - 1
+    rows = np.sort(np.random.default_rng(seed).choice(n, size=min(m, n), replace=False))
+    lo, hi = rp[rows].astype(np.int64), rp[rows + 1].astype(np.int64)
+    lens = hi - lo
+    idx = np.repeat(lo - np.concatenate(([0], np.cumsum(lens)[:-1])), lens) + np.arange(lens.sum())
+    prod = val[idx].astype(np.float64) * x[col[idx]].astype(np.float64)
+    seg = np.repeat(np.arange(rows.size), lens)
+    return rows, np.bincount(seg, weights=prod, minlength=rows.size), \
+        np.bincount(seg, weights=np.abs(prod), minlength=rows.size)

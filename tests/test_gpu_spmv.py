@@ -153,6 +153,32 @@ def test_full_size_c2_c3(lhpc, gpu, dtype):
 
 
 @pytest.mark.slow
+def test_xtile_large_n_80m(lhpc, gpu):
+    """XTILE beyond C2: n = 80M rows and columns, 15 uniform nonzeros per row
+    (nnz = 1.2e9, 1954 x tiles, 146K chunks; fp32).  The dense segment table
+    of starts needed 2.9e8 entries and the plan fell to XSLICE; the two-level
+    table (lhpc_plan.hpp xtile_segment_table) keeps it XTILE.  Dyadic values:
+    10^5 sampled rows bit-exact against fp64 numpy (exact here), and run to
+    run determinism on the whole y."""
+    import torch
+    n = 80_000_000
+    rp, col, val = lhpc.gen_uniform_csr(n, n, 15, dtype=lhpc.F32, dist=1, seed=0x8000)
+    x = lhpc.gen_values(lhpc.F32, 1, n, 0x8001)
+    with lhpc.SpMVPlan(rp, col, val, n) as plan:
+        info = plan.info()
+        assert info["kernel"] == lhpc.KERNEL_XTILE and info["slices"] == -(-n // 40960)
+        xd = torch.from_numpy(x).to(gpu)
+        y1 = plan(xd).clone()
+        y2 = plan(xd)
+        torch.cuda.synchronize()
+        assert torch.equal(y1, y2)
+        y = y1.cpu().numpy()
+        del xd, y1, y2
+    rows, y64, _ = S.sampled_rows_fp64(rp, col, val, x, 100_000)
+    assert np.array_equal(y[rows].astype(np.float64), y64)
+
+
+@pytest.mark.slow
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
 def test_full_size_c4(lhpc, gpu, dtype):
     """BASELINE configs[3] (C4) at full size, as bench.py --workload c4 builds
