@@ -8,7 +8,11 @@
 //   sparse::spmv(plan, d_x, d_y, stream)          full y on every rank (device)
 //   sparse::dist_stencil7(comm, d_u, d_out, ...)  z-slab step with RCCL halo planes
 //   DistComm::local(nranks, rank, device), p2p_export(d_y, bytes) / p2p_import(blobs)
-//                                 opt-in direct xGMI peer exchange of y (lhpc_dist_p2p_*)
+//                                 direct xGMI peer exchange of y into registered
+//                                 windows (up to LHPC_DIST_P2P_MAX_WINDOWS: a
+//                                 ping-pong pair), p2p_reset()
+//   sparse::exchange(plan, d_y, stream)           the y exchange alone
+//   sparse::exchange_schedule(cuts, nranks, K, rank, kind)   the transfers, as data
 // Non-zero status → std::system_error (include/lhpc_error.hpp).  The
 // reference has no multi-device code; the rank-0 unique id must
 // reach every rank through the launcher's own channel (MPI_Bcast, a file, …).
@@ -62,6 +66,9 @@ class DistComm {
     for (const auto &b : blobs) flat.insert(flat.end(), b.begin(), b.end());
     lhpc::checkLhpc(lhpc_dist_p2p_import(comm_, flat.data()));
   }
+  void p2p_reset() { lhpc::checkLhpc(lhpc_dist_p2p_reset(comm_)); }
+  // LHPC_ERR_INTERNAL after a peer flag wait timed out (check after a stream sync)
+  int p2p_status() const { return lhpc_dist_p2p_status(comm_); }
   ~DistComm() {
     if (comm_) lhpc_dist_comm_destroy(comm_);
   }
@@ -117,11 +124,12 @@ class DistSpMVPlan {
   // (interleaved_local); `cuts`: the nranks·K + 1 global row cuts.
   template <typename OffsetT>
   DistSpMVPlan(DistComm &comm, std::int64_t n_rows, std::int64_t n_cols, int K, const std::vector<std::int64_t> &cuts,
-               const CSRMatrix<T, std::int32_t, OffsetT> &local, unsigned flags = LHPC_PLAN_DEFAULT)
+               const CSRMatrix<T, std::int32_t, OffsetT> &local, unsigned flags = LHPC_PLAN_DEFAULT,
+               const lhpc_options *opts = nullptr)
       : n_rows_(n_rows), n_cols_(n_cols) {
-    lhpc::checkLhpc(lhpc_dist_spmv_plan_create(&plan_, comm.native(), std::is_same_v<T, float> ? LHPC_F32 : LHPC_F64,
-                                               n_rows, n_cols, K, cuts.data(), local.row_ptr.data(),
-                                               sizeof(OffsetT) * 8, local.col_idx.data(), local.val.data(), flags));
+    lhpc::checkLhpc(lhpc_dist_spmv_plan_create_opts(
+        &plan_, comm.native(), std::is_same_v<T, float> ? LHPC_F32 : LHPC_F64, n_rows, n_cols, K, cuts.data(),
+        local.row_ptr.data(), sizeof(OffsetT) * 8, local.col_idx.data(), local.val.data(), flags, opts));
   }
   DistSpMVPlan(const DistSpMVPlan &) = delete;
   DistSpMVPlan &operator=(const DistSpMVPlan &) = delete;
@@ -141,6 +149,24 @@ class DistSpMVPlan {
 template <typename T>
 void spmv(DistSpMVPlan<T> &plan, const T *d_x, T *d_y, void *stream = nullptr) {
   lhpc::checkLhpc(lhpc_dist_spmv(plan.native(), d_x, d_y, stream));
+}
+
+// the y exchange of a call alone (every chunk; y holds this rank's blocks)
+template <typename T>
+void exchange(DistSpMVPlan<T> &plan, T *d_y, void *stream = nullptr) {
+  lhpc::checkLhpc(lhpc_dist_exchange(plan.native(), d_y, stream));
+}
+
+// the transfers lhpc_dist_spmv issues on `rank` (kind LHPC_DIST_EXCHANGE_RCCL / _P2P)
+inline std::vector<lhpc_dist_xfer> exchange_schedule(const std::vector<std::int64_t> &cuts, int nranks, int K,
+                                                     int rank, int kind = LHPC_DIST_EXCHANGE_RCCL,
+                                                     bool broadcast = false) {
+  std::vector<lhpc_dist_xfer> v(static_cast<std::size_t>(nranks) * K);
+  std::int64_t n = 0;
+  lhpc::checkLhpc(lhpc_dist_exchange_schedule(cuts.data(), nranks, K, rank, kind, broadcast ? 1 : 0, v.data(),
+                                              static_cast<std::int64_t>(v.size()), &n));
+  v.resize(static_cast<std::size_t>(n));
+  return v;
 }
 
 // One 7-point step on this rank's z-slab (HPCHighDimensionFlatArray<3,float,ghost>

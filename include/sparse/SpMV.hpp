@@ -2,6 +2,7 @@
 //
 //   sparse::SpMVPlan<T>  RAII owner of the HBM copy of A (one per GPU)
 //   sparse::spmv(plan, x, y)  with x, y hpc::HPCHighDimensionFlatArray<1,T,...>
+//   sparse::default_options()  lhpc_options for pinning a kernel variant
 //                             (host, synchronous) or raw HBM pointers (async)
 // Forwards to the C ABI (include/lhpc.h); non-zero status → std::system_error
 // (include/lhpc_error.hpp).  The reference has no SpMV; the
@@ -21,6 +22,14 @@
 
 namespace sparse {
 
+// Variant options (include/lhpc.h lhpc_options), initialised to automatic:
+//   auto o = sparse::default_options(); o.xtile_reduce = LHPC_XTILE_REDUCE_PERM;
+inline lhpc_options default_options() {
+  lhpc_options o;
+  lhpc_options_init(&o);
+  return o;
+}
+
 template <typename T>
 class SpMVPlan {
   static_assert(std::is_same_v<T, float> || std::is_same_v<T, double>, "SpMV is fp32 or fp64");
@@ -28,13 +37,14 @@ class SpMVPlan {
  public:
   template <typename OffsetT>
   explicit SpMVPlan(const CSRMatrix<T, std::int32_t, OffsetT> &A, int device = -1,
-                    unsigned flags = LHPC_PLAN_DEFAULT)
+                    unsigned flags = LHPC_PLAN_DEFAULT, const lhpc_options *opts = nullptr)
       : n_rows_(A.n_rows), n_cols_(A.n_cols) {
     const int dev[1] = {device};
-    lhpc::checkLhpc(lhpc_spmv_plan_create(&plan_, std::is_same_v<T, float> ? LHPC_F32 : LHPC_F64,
-                                          A.n_rows, A.n_cols, A.nnz(), A.row_ptr.data(),
-                                          sizeof(OffsetT) * 8, A.col_idx.data(), A.val.data(),
-                                          device >= 0 ? dev : nullptr, device >= 0 ? 1 : 0, flags));
+    lhpc::checkLhpc(lhpc_spmv_plan_create_opts(&plan_, std::is_same_v<T, float> ? LHPC_F32 : LHPC_F64,
+                                               A.n_rows, A.n_cols, A.nnz(), A.row_ptr.data(),
+                                               sizeof(OffsetT) * 8, A.col_idx.data(), A.val.data(),
+                                               device >= 0 ? dev : nullptr, device >= 0 ? 1 : 0, flags, 0, nullptr,
+                                               opts));
   }
   SpMVPlan(const SpMVPlan &) = delete;
   SpMVPlan &operator=(const SpMVPlan &) = delete;

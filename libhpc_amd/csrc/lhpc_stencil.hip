@@ -509,12 +509,15 @@ __global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ 
 // makes rows 8-B aligned; unaligned 16-B buffer loads run at the full rate).
 // x±1 inside a lane are register moves; across lanes one DPP move per side,
 // whose lane-0 / lane-63 inputs are readlane broadcasts as in k_stencil7_buf.
-// Same operation order per cell, so results are bit-identical.  Needs
-// nx % (64·NJ) == 0: every x4 of a tile then ends at or before column nx-1+g,
-// so none reaches past the array end (a partially out-of-range x4 is not
-// relied on).  STORE: 5 the 4 results leave as one unaligned dwordx4 store,
-// 6 the same non-temporal.
-template <int RY, int NJ, int STORE, int PF = 1>
+// Same operation order per cell, so results are bit-identical.  With
+// nx % (64·NJ) == 0 (PART false) every x4 of a tile ends at or before column
+// nx-1+g.  PART: the last x tile is partial; its 256-column blocks that reach
+// past nx (a wave-uniform test) load their x4s as four dword buffer loads
+// (the row's ghost column and whatever follows it, 0 past the array end —
+// never a partially out-of-range x4) and store only the lane's columns below
+// nx: a whole x4 as one dwordx4, a 1–3-column remainder as dwords.  STORE: 5
+// the 4 results leave as one unaligned dwordx4 store, 6 the same non-temporal.
+template <int RY, int NJ, int STORE, int PF = 1, bool PART = false>
 __global__ __launch_bounds__(256) void k_stencil7_buf4(const float *__restrict__ u, float *__restrict__ out,
                                                        int64_t nz, int64_t ny, int64_t nx, int64_t g,
                                                        float c0, float c1, int64_t z_begin, int64_t z_end,
@@ -559,7 +562,15 @@ __global__ __launch_bounds__(256) void k_stencil7_buf4(const float *__restrict__
     for (int r = 0; r < RY + 2; ++r) {
       const auto rs = rsrc(u, z, r);
 #pragma unroll
-      for (int j = 0; j < NB; ++j) S.v[r][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, vx + 1024 * j, 0, 0);
+      for (int j = 0; j < NB; ++j) {
+        if (PART && x0 + 256 * (j + 1) > nx) {  // block reaches past nx: dword loads
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            S.v[r][j][k] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, vx + 1024 * j + 4 * k, 0, 0));
+        } else {
+          S.v[r][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, vx + 1024 * j, 0, 0);
+        }
+      }
       if (r >= 1 && r <= RY) S.e[r - 1] = bitsf(__builtin_amdgcn_raw_buffer_load_b32(rs, ve, 0, 0));
     }
   };
@@ -593,7 +604,20 @@ __global__ __launch_bounds__(256) void k_stencil7_buf4(const float *__restrict__
           const float o = __fadd_rn(__fmul_rn(c0, cz), __fmul_rn(c1, sum));
           res[k] = static_cast<uint32_t>(fbits(o));
         }
-        __builtin_amdgcn_raw_buffer_store_b128(res, ws, vx + 1024 * j, 0, STORE == 6 ? 2 : 0);
+        if (PART && x0 + 256 * (j + 1) > nx) {
+          const int64_t vc = nx - (x0 + 256 * j + 4 * lane);  // this lane's columns below nx
+          if (vc >= 4) {
+            __builtin_amdgcn_raw_buffer_store_b128(res, ws, vx + 1024 * j, 0, STORE == 6 ? 2 : 0);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+              if (k < vc)
+                __builtin_amdgcn_raw_buffer_store_b32(static_cast<int>(res[k]), ws, vx + 1024 * j + 4 * k, 0,
+                                                      STORE == 6 ? 2 : 0);
+          }
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(res, ws, vx + 1024 * j, 0, STORE == 6 ? 2 : 0);
+        }
       }
     }
   };
@@ -739,7 +763,9 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
     int zc = o.stencil7_zc, pf = o.stencil7_pf;
     // x4 ring by default when every x tile is full (nx % (64·NJ) == 0): 198-211 us against
     // 209-225 us for the dword ring on 512^3, same boxes; "buf" forces the dword ring
-    const bool buf4 = (buf4_req || impl == LHPC_S7_AUTO) && (nj == 4 || nj == 8) && nx % (int64_t{nj} * kWave) == 0;
+    // (partial last x tiles included: k_stencil7_buf4<…, PART>)
+    const bool buf4 = (buf4_req || impl == LHPC_S7_AUTO) && (nj == 4 || nj == 8);
+    const bool part = nx % (int64_t{nj} * kWave) != 0;
     if (pf < 1) pf = buf4 ? 2 : 1;  // prefetch planes: x4 PF 2 198 us vs PF 1 210-217 / PF 3 203
     if (zc < 1) {
       const int64_t target = o.stencil7_blocks > 0 ? o.stencil7_blocks : 256;
@@ -750,18 +776,24 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
     }
     if (buf4) {  // x4 ring: non-temporal dwordx4 stores ("plain": plain)
       const int m4 = stm == LHPC_STORE_PLAIN ? 5 : 6;
-#define LHPC_S74_M(RY, NJ, M)                                                                          \
-  do {                                                                                                 \
-    const int64_t ntx = nx / (NJ * kWave), nty = (ny + 4 * RY - 1) / (4 * RY), ntz = (ze - zb + zc - 1) / zc; \
-    if (pf == 2)                                                                                       \
-      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 2>), dim3(static_cast<unsigned>(ntx * nty * ntz)),   \
+#define LHPC_S74_P(RY, NJ, M, P)                                                                        \
+  do {                                                                                                  \
+    const int64_t ntx = (nx + NJ * kWave - 1) / (NJ * kWave), nty = (ny + 4 * RY - 1) / (4 * RY),          \
+                  ntz = (ze - zb + zc - 1) / zc;                                                        \
+    if (pf == 2)                                                                                        \
+      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 2, P>), dim3(static_cast<unsigned>(ntx * nty * ntz)), \
                          dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
-    else if (pf == 3)                                                                                  \
-      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 3>), dim3(static_cast<unsigned>(ntx * nty * ntz)),   \
+    else if (pf == 3)                                                                                   \
+      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 3, P>), dim3(static_cast<unsigned>(ntx * nty * ntz)), \
                          dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
-    else                                                                                               \
-      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M>), dim3(static_cast<unsigned>(ntx * nty * ntz)),      \
+    else                                                                                                \
+      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 1, P>), dim3(static_cast<unsigned>(ntx * nty * ntz)), \
                          dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
+  } while (0)
+#define LHPC_S74_M(RY, NJ, M)              \
+  do {                                     \
+    if (part) LHPC_S74_P(RY, NJ, M, true); \
+    else LHPC_S74_P(RY, NJ, M, false);     \
   } while (0)
 #define LHPC_S74(RY, NJ)                            \
   do {                                              \
@@ -776,6 +808,7 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
       else LHPC_S74(2, 8);
 #undef LHPC_S74
 #undef LHPC_S74_M
+#undef LHPC_S74_P
       return check_launch(s);
     }
 #define LHPC_S7B_M(RY, NJ, M)                                                                         \

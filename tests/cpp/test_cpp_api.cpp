@@ -188,6 +188,24 @@ int gpu_mode() {
       }
       if (!threw) return fail("allreduce on a local communicator must fail");
     }
+    // explicit variant options: the RCCL exchange driven at world 1 (an
+    // in-place no-op), then the exchange alone; the schedule as data
+    {
+      auto o = sparse::default_options();
+      o.dist_exchange = LHPC_DIST_EXCHANGE_RCCL;
+      o.dist_world1 = 1;
+      o.dist_broadcast = 1;
+      sparse::DistSpMVPlan<float> oplan(comm, n, m, K, cuts, L, LHPC_PLAN_DEFAULT, &o);
+      sparse::spmv(oplan, dx, dy);
+      sparse::exchange(oplan, dy);
+      if (!hip_ok(hipMemcpy(yd.data(), dy, sizeof(float) * n, hipMemcpyDeviceToHost))) return fail("hipMemcpy");
+      for (std::int64_t i = 0; i < n; ++i)
+        if (yd[std::size_t(i)] != y(i)) return fail("options dist spmv mismatch");
+      const auto sched = sparse::exchange_schedule(cuts, 1, K, 0, LHPC_DIST_EXCHANGE_RCCL, true);
+      std::int64_t rows = 0;
+      for (const auto &t : sched) rows += t.kind == LHPC_XFER_BROADCAST ? t.count : 0;
+      if (rows != n) return fail("broadcast schedule covers every row once");
+    }
     if (!hip_ok(hipFree(dx)) || !hip_ok(hipFree(dy)) || !hip_ok(hipFree(dd))) return fail("hipFree");
   }
   std::printf("cpp api gpu: ok (spmv kernel %d)\n", plan.info().kernel);

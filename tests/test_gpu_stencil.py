@@ -158,11 +158,13 @@ def test_stencil7_buf4(lhpc, gpu, cfg, store):
     dwordx4 loads/stores at 4-B alignment) is bit-exact against the oracle on
     shapes whose nx is a multiple of its tile width — one and several x tiles,
     ny / nz ragged against the row and z-chunk tiles, ghost widths 1 to 3 (so
-    rows start at every 4-B phase of a 16-B line).  Other nx fall back to the dword ring (covered above)."""
+    rows start at every 4-B phase of a 16-B line) — and on ragged nx, where the
+    last x tile is partial (dword loads and stores past nx, every lane phase
+    of the last x4: nx % 4 = 0..3, nx < 4)."""
     opts = _s7_options(lhpc, "buf4", cfg, store)
-    for (nz, ny, nx, g) in ((37, 45, 1024, 1), (9, 19, 512, 2), (3, 2, 1536, 3), (5, 9, 512, 1)):
-        if nx % (64 * int(cfg.split(",")[1])):
-            continue
+    for (nz, ny, nx, g) in ((37, 45, 1024, 1), (9, 19, 512, 2), (3, 2, 1536, 3), (5, 9, 512, 1),
+                            (37, 45, 1100, 1), (9, 19, 130, 2), (3, 2, 1, 1), (5, 7, 517, 3), (2, 3, 1541, 1),
+                            (4, 5, 768, 2), (3, 4, 258, 1), (6, 3, 3, 2)):
         shape = (nz + 2 * g, ny + 2 * g, nx + 2 * g)
         u = S.random_padded(shape, seed=nz * 7 + nx + g, zero_ghost=False).reshape(-1)
         out0 = S.random_padded(shape, seed=1234 + g).reshape(-1)
