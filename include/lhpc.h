@@ -126,7 +126,8 @@ enum lhpc_stencil7_impl {
   LHPC_S7_AUTO = 0,
   LHPC_S7_SIMPLE = 1,           /* thread per column                          */
   LHPC_S7_RING = 2,             /* buffer-addressed dword register ring       */
-  LHPC_S7_RING_X4 = 3           /* x4 ring (16-B rows per lane)               */
+  LHPC_S7_RING_X4 = 3,          /* x4 ring (16-B rows per lane)               */
+  LHPC_S7_RING_X4_LDS = 4       /* x4 ring, inner halo rows shared via LDS    */
 };
 enum lhpc_store_policy {
   LHPC_STORE_AUTO = 0,

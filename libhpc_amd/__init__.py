@@ -127,7 +127,7 @@ def _opts(o):
 
 
 XTILE_REDUCE_AUTO, XTILE_REDUCE_PERM, XTILE_REDUCE_IPERM = 0, 1, 2
-S7_AUTO, S7_SIMPLE, S7_RING, S7_RING_X4 = 0, 1, 2, 3
+S7_AUTO, S7_SIMPLE, S7_RING, S7_RING_X4, S7_RING_X4_LDS = 0, 1, 2, 3, 4
 STORE_AUTO, STORE_PLAIN, STORE_NT, STORE_STAGED = 0, 1, 2, 3
 DIST_EXCHANGE_AUTO, DIST_EXCHANGE_RCCL, DIST_EXCHANGE_P2P, DIST_EXCHANGE_NONE = 0, 1, 2, 3
 XFER_ALLGATHER, XFER_BROADCAST, XFER_PUSH = 1, 2, 3

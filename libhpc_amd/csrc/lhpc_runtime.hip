@@ -74,7 +74,8 @@ void env_overlay(lhpc_options &o) {
   i32("LHPC_XSLICE_NB", o.xslice_window);
   if (const char *e = tuning_env("LHPC_XSLICE_MB")) o.xslice_mb = std::atof(e);
   if (const char *e = tuning_env("LHPC_STENCIL7_IMPL"))
-    o.stencil7_impl = !std::strcmp(e, "buf4") ? LHPC_S7_RING_X4 : !std::strcmp(e, "buf") ? LHPC_S7_RING : LHPC_S7_SIMPLE;
+    o.stencil7_impl = !std::strcmp(e, "buf4lds") ? LHPC_S7_RING_X4_LDS : !std::strcmp(e, "buf4") ? LHPC_S7_RING_X4
+                      : !std::strcmp(e, "buf") ? LHPC_S7_RING : LHPC_S7_SIMPLE;
   if (const char *e = tuning_env("LHPC_STENCIL7_STORE"))
     o.stencil7_store = !std::strcmp(e, "plain") ? LHPC_STORE_PLAIN : !std::strcmp(e, "staged") ? LHPC_STORE_STAGED : LHPC_STORE_NT;
   if (const char *e = tuning_env("LHPC_STENCIL7_BUF"))

@@ -517,7 +517,13 @@ __global__ __launch_bounds__(256) void k_stencil7_buf(const float *__restrict__ 
 // never a partially out-of-range x4) and store only the lane's columns below
 // nx: a whole x4 as one dwordx4, a 1–3-column remainder as dwords.  STORE: 5
 // the 4 results leave as one unaligned dwordx4 store, 6 the same non-temporal.
-template <int RY, int NJ, int STORE, int PF = 1, bool PART = false>
+// SHARE: the four waves of a block hold consecutive row groups, so a wave's
+// y±1 halo rows of the centre plane are its neighbours' edge rows: those go
+// through LDS (double-buffered by plane parity, one block barrier per plane)
+// and only the block's outer two halo rows are loaded, 10 rows per plane and
+// block instead of 16.  Waves past ny then stay to the end (barriers) and
+// store nothing.  Same values in the same registers: bit-identical.
+template <int RY, int NJ, int STORE, int PF = 1, bool PART = false, bool SHARE = false>
 __global__ __launch_bounds__(256) void k_stencil7_buf4(const float *__restrict__ u, float *__restrict__ out,
                                                        int64_t nz, int64_t ny, int64_t nx, int64_t g,
                                                        float c0, float c1, int64_t z_begin, int64_t z_end,
@@ -531,7 +537,9 @@ __global__ __launch_bounds__(256) void k_stencil7_buf4(const float *__restrict__
   const int64_t x0 = (t % ntx) * TW;
   const int64_t y0 = (((t / ntx) % nty) * 4 + w) * RY;
   const int64_t zs = z_begin + (t / (ntx * nty)) * zc;
-  if (zs >= z_end || y0 >= ny) return;  // wave-uniform
+  if (zs >= z_end) return;                // block-uniform
+  if (!SHARE && y0 >= ny) return;         // wave-uniform
+  __shared__ u32x4 hx[SHARE ? 2 : 1][SHARE ? 4 : 1][2][NB][kWave];
   const int64_t ze = zs + zc < z_end ? zs + zc : z_end;
   const int64_t Px = nx + 2 * g;
   const int64_t Pyx = (ny + 2 * g) * Px;
@@ -560,6 +568,8 @@ __global__ __launch_bounds__(256) void k_stencil7_buf4(const float *__restrict__
   auto load = [&](Slot &S, int64_t z) {
 #pragma unroll
     for (int r = 0; r < RY + 2; ++r) {
+      // SHARE: inner halo rows come from the neighbouring wave through LDS
+      if (SHARE && ((r == 0 && w > 0) || (r == RY + 1 && w < 3))) continue;
       const auto rs = rsrc(u, z, r);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
@@ -574,8 +584,22 @@ __global__ __launch_bounds__(256) void k_stencil7_buf4(const float *__restrict__
       if (r >= 1 && r <= RY) S.e[r - 1] = bitsf(__builtin_amdgcn_raw_buffer_load_b32(rs, ve, 0, 0));
     }
   };
-  auto step = [&](const Slot &M, const Slot &Cc, const Slot &Pp, int64_t z) {
-    if (z >= ze) return;
+  auto step = [&](const Slot &M, Slot &Cc, const Slot &Pp, int64_t z) {
+    if (z >= ze) return;  // block-uniform
+    if constexpr (SHARE) {
+      const int par = static_cast<int>(z & 1);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        hx[par][w][0][j][lane] = Cc.v[1][j];
+        hx[par][w][1][j][lane] = Cc.v[RY][j];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        if (w > 0) Cc.v[0][j] = hx[par][w - 1][1][j][lane];
+        if (w < 3) Cc.v[RY + 1][j] = hx[par][w + 1][0][j][lane];
+      }
+    }
 #pragma unroll
     for (int r = 0; r < RY; ++r) {
       if (y0 + r >= ny) break;
@@ -748,7 +772,7 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
   // wave's LDS row, 219-220 us vs 225-226 plain on 512^3; plain when `out` is
   // not 16-B aligned) | plain | nt.
   const int stm = o.stencil7_store;
-  const bool buf4_req = impl == LHPC_S7_RING_X4;
+  const bool buf4_req = impl == LHPC_S7_RING_X4 || impl == LHPC_S7_RING_X4_LDS;
   const bool buf_impl = impl == LHPC_S7_AUTO || impl == LHPC_S7_RING || buf4_req;
   int store_mode = stm == LHPC_STORE_PLAIN ? 0 : stm == LHPC_STORE_NT ? 1 : 4;
   if (store_mode == 4 && !aligned16(out)) store_mode = 0;  // staged float4 stores need a 16-B base
@@ -766,6 +790,9 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
     // (partial last x tiles included: k_stencil7_buf4<…, PART>)
     const bool buf4 = (buf4_req || impl == LHPC_S7_AUTO) && (nj == 4 || nj == 8);
     const bool part = nx % (int64_t{nj} * kWave) != 0;
+    // LDS-shared halo rows (x4 ring, prefetch depth 2): the default (512^3,
+    // same box, two runs each: 206.8 / 198.4 µs → 201.3 / 193.2 µs)
+    const bool share = impl == LHPC_S7_RING_X4_LDS || impl == LHPC_S7_AUTO;
     if (pf < 1) pf = buf4 ? 2 : 1;  // prefetch planes: x4 PF 2 198 us vs PF 1 210-217 / PF 3 203
     if (zc < 1) {
       const int64_t target = o.stencil7_blocks > 0 ? o.stencil7_blocks : 256;
@@ -780,7 +807,10 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
   do {                                                                                                  \
     const int64_t ntx = (nx + NJ * kWave - 1) / (NJ * kWave), nty = (ny + 4 * RY - 1) / (4 * RY),          \
                   ntz = (ze - zb + zc - 1) / zc;                                                        \
-    if (pf == 2)                                                                                        \
+    if (share)                                                                                          \
+      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 2, P, true>), dim3(static_cast<unsigned>(ntx * nty * ntz)), \
+                         dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
+    else if (pf == 2)                                                                                   \
       hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 2, P>), dim3(static_cast<unsigned>(ntx * nty * ntz)), \
                          dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
     else if (pf == 3)                                                                                   \

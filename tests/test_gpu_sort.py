@@ -184,3 +184,42 @@ def test_sort_u32_reference_100m(lhpc, gpu):
     del t
     keys.sort(kind="stable")
     assert np.array_equal(got, keys)
+
+
+@pytest.mark.parametrize("poison", [0x00, 0xA5, 0xFF])
+def test_coo_to_csr_poisoned_pool(lhpc, gpu, poison):
+    """Regression for the round-2 host-path race: the on-device
+    sort / scan / COO→CSR still take their scratch from the stream-ordered
+    pool (lhpc_sort.hip DevBuf).  Every scratch buffer must be fully written
+    before it is read, so results must not depend on what the pool hands
+    back: the pool is left filled with 0x00 / 0xA5 / 0xFF before each call
+    (liblhpc_probe.so lhpc_probe_poison_pool, on the call's stream), for the
+    4-entry symmetric Matrix Market case that failed, tiny and ragged COO
+    inputs with duplicates and empty rows, and the sorts they run."""
+    import ctypes as C
+    import os
+    import torch
+    P = C.CDLL(os.path.join(os.path.dirname(lhpc.LIB_PATH), "liblhpc_probe.so"))
+    P.lhpc_probe_poison_pool.argtypes = [C.c_int64, C.c_int, C.c_void_p]
+    st = torch.cuda.current_stream(gpu)
+    cases = [(3, 3, np.array([0, 1, 0, 2]), np.array([0, 0, 1, 2]), np.array([2.0, -1.5, -1.5, 4.0]))]
+    rng = np.random.default_rng(0x9015 + poison)
+    for n_rows, n_cols, nnz in ((1, 1, 1), (5, 7, 2), (64, 65, 300), (1000, 50, 5000), (3, 100_000, 4099)):
+        cases.append((n_rows, n_cols, rng.integers(0, n_rows, nnz), rng.integers(0, n_cols, nnz),
+                      rng.integers(-8, 9, nnz) / 8.0))
+    for n_rows, n_cols, r, c, v in cases:
+        r, c, v = r.astype(np.int32), c.astype(np.int32), v.astype(np.float64)
+        want = S.coo_oracle(n_rows, n_cols, r, c, v)
+        for _ in range(3):
+            assert P.lhpc_probe_poison_pool(1 << 24, poison, st.cuda_stream) == 0
+            rp, col, val = lhpc.coo_to_csr(n_rows, n_cols, _dev(gpu, r), _dev(gpu, c), _dev(gpu, v), stream=st)
+            torch.cuda.synchronize()
+            assert np.array_equal(rp.cpu().numpy(), want[0]), (n_rows, n_cols, r.size)
+            assert np.array_equal(col.cpu().numpy(), want[1]) and np.array_equal(val.cpu().numpy(), want[2])
+    keys = rng.integers(0, 1 << 32, 5000, dtype=np.uint64).astype(np.uint32)
+    for _ in range(3):
+        assert P.lhpc_probe_poison_pool(1 << 24, poison, st.cuda_stream) == 0
+        kd = _dev(gpu, keys.view(np.int32))
+        lhpc.radix_sort(kd, stream=st)
+        torch.cuda.synchronize()
+        assert np.array_equal(_u32_view(kd), np.sort(keys))

@@ -120,7 +120,8 @@ S7_IMPLS = ["buf", "buf:2,8,0,2", "buf:4,4,128,3", "buf:2,8,5,3", "buf:2,8,32", 
 
 def _s7_options(lhpc, name, cfg, store):
     """lhpc_options fields for a stencil7 variant: impl name, "RY,NJ,ZC[,PF]", store policy."""
-    o = {"stencil7_impl": {"buf": lhpc.S7_RING, "buf4": lhpc.S7_RING_X4, "simple": lhpc.S7_SIMPLE}[name],
+    o = {"stencil7_impl": {"buf": lhpc.S7_RING, "buf4": lhpc.S7_RING_X4, "buf4lds": lhpc.S7_RING_X4_LDS,
+                           "simple": lhpc.S7_SIMPLE}[name],
          "stencil7_store": {"nt": lhpc.STORE_NT, "plain": lhpc.STORE_PLAIN, "staged": lhpc.STORE_STAGED}[store]}
     if cfg:
         for k, v in zip(("stencil7_ry", "stencil7_nj", "stencil7_zc", "stencil7_pf"), cfg.split(",")):
@@ -153,7 +154,8 @@ S7_BUF4 = ["2,8,0", "2,8,5", "1,8,16", "4,8,32", "2,4,7", "4,4,32"]
 
 @pytest.mark.parametrize("cfg", S7_BUF4)
 @pytest.mark.parametrize("store", ["nt", "plain"])
-def test_stencil7_buf4(lhpc, gpu, cfg, store):
+@pytest.mark.parametrize("impl", ["buf4", "buf4lds"])
+def test_stencil7_buf4(lhpc, gpu, cfg, store, impl):
     """The x4 ring (stencil7_impl = S7_RING_X4, 4 consecutive x per lane,
     dwordx4 loads/stores at 4-B alignment) is bit-exact against the oracle on
     shapes whose nx is a multiple of its tile width — one and several x tiles,
@@ -161,7 +163,7 @@ def test_stencil7_buf4(lhpc, gpu, cfg, store):
     rows start at every 4-B phase of a 16-B line) — and on ragged nx, where the
     last x tile is partial (dword loads and stores past nx, every lane phase
     of the last x4: nx % 4 = 0..3, nx < 4)."""
-    opts = _s7_options(lhpc, "buf4", cfg, store)
+    opts = _s7_options(lhpc, impl, cfg, store)
     for (nz, ny, nx, g) in ((37, 45, 1024, 1), (9, 19, 512, 2), (3, 2, 1536, 3), (5, 9, 512, 1),
                             (37, 45, 1100, 1), (9, 19, 130, 2), (3, 2, 1, 1), (5, 7, 517, 3), (2, 3, 1541, 1),
                             (4, 5, 768, 2), (3, 4, 258, 1), (6, 3, 3, 2)):
