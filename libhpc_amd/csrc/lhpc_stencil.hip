@@ -783,7 +783,11 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
     // one block per CU (256): measured on 512^3, fewer concurrent z fronts beat
     // more waves — 2,8 at zc 128 (256 blocks) 209-220 us vs 250 us at zc 32 (1024 blocks);
     // prefetch depth (PF) and store policy (plain vs nt) are secondary.
-    int ry = o.stencil7_ry > 0 ? o.stencil7_ry : 2, nj = o.stencil7_nj > 0 ? o.stencil7_nj : 8;
+    // default tile: 2 rows × 8 blocks for the dword ring; 2 rows × 4 blocks (256 x) for the
+    // x4 ring with LDS-shared halos (512^3, same box, three runs each: 2,8 200.9 µs, 2,4 195.6,
+    // 1,8 196.0, 4,8 214.7; 384 / 512 blocks instead of 256: 232-234 µs)
+    const bool x4_default = impl == LHPC_S7_AUTO || impl == LHPC_S7_RING_X4_LDS;
+    int ry = o.stencil7_ry > 0 ? o.stencil7_ry : 2, nj = o.stencil7_nj > 0 ? o.stencil7_nj : (x4_default ? 4 : 8);
     int zc = o.stencil7_zc, pf = o.stencil7_pf;
     // x4 ring by default when every x tile is full (nx % (64·NJ) == 0): 198-211 us against
     // 209-225 us for the dword ring on 512^3, same boxes; "buf" forces the dword ring

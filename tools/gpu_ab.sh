@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box A/B of bench lines: AB="name:K=V,K=V;name2:..." WLS="c2 c3", then
+# Same-box A/B of bench lines: AB="name:K=V&K=V;name2:..." WLS="c2 c3", then
 # optional tests (TESTS="tests/x.py ..." TESTK=expr).  Output: gpurun_out/ab/.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O="$R/gpurun_out/ab"; mkdir -p "$O"
@@ -13,7 +13,7 @@ for rep in $(seq 1 ${REPS:-1}); do
     for V in "${VS[@]}"; do
       name=${V%%:*}; kv=${V#*:}
       log "bench $WL $name rep $rep"
-      env $(echo "$kv" | tr ',' ' ') timeout -k 10 300 python bench.py --workload $WL --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench_${WL}_${name}_$rep.log" 2>&1 || { log "FAIL bench $WL $name"; exit 1; }
+      env $(echo "$kv" | tr '&' ' ') timeout -k 10 300 python bench.py --workload $WL --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench_${WL}_${name}_$rep.log" 2>&1 || { log "FAIL bench $WL $name"; exit 1; }
     done
   done
 done
