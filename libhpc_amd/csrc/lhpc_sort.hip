@@ -234,7 +234,9 @@ struct DevBuf {
 // stream-ordered pool) and synchronous copies.  Asynchronous pageable copies
 // into pool memory on the null stream were seen to land after the kernel
 // that read them (rows read as 0 in 4 of 25 runs of tests/cpp
-// test_sparse_grid gpu, the 4-entry Matrix Market case).
+// test_sparse_grid gpu, the 4-entry Matrix Market case).  Every step of that
+// path was ordered on the one caller stream; DESIGN.md §9 traces it and
+// records what was ruled out.
 struct HostStage {
   void *p = nullptr;
   ~HostStage() {
@@ -490,11 +492,14 @@ int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *r
     hipLaunchKernelGGL((k_coo_rowptr<int32_t>), dim3(gr), dim3(256), 0, s, kp, pp, gp, nnz, n_rows, cb,
                        static_cast<int32_t *>(row_ptr));
   LHPC_TRY(check_launch(s));
+  // the two status words are read after the stream has drained, with
+  // synchronous copies: no asynchronous copy touches pageable host memory
+  // anywhere in the COO->CSR path
   int hbad = 0;
   uint32_t hnnz = 0;
-  LHPC_HIP_TRY(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
-  LHPC_HIP_TRY(hipMemcpyAsync(&hnnz, gp, 4, hipMemcpyDeviceToHost, s));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
+  LHPC_HIP_TRY(hipMemcpy(&hbad, bad, 4, hipMemcpyDeviceToHost));
+  LHPC_HIP_TRY(hipMemcpy(&hnnz, gp, 4, hipMemcpyDeviceToHost));
   if (hbad) return LHPC_ERR_INVALID_ARG;
   if (nnz_out) *nnz_out = hnnz;
   return LHPC_OK;
