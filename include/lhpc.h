@@ -122,6 +122,11 @@ enum lhpc_xtile_reduce {
   LHPC_XTILE_REDUCE_PERM = 1,   /* scatter xg into CSR slots through perm     */
   LHPC_XTILE_REDUCE_IPERM = 2   /* gather CSR positions through iperm         */
 };
+enum lhpc_xtile_align {
+  LHPC_XTILE_ALIGN_AUTO = 0,
+  LHPC_XTILE_ALIGN_OFF = 1,     /* segments packed back to back               */
+  LHPC_XTILE_ALIGN_UNITS = 2    /* every segment padded to 16 B (iperm only)  */
+};
 enum lhpc_stencil7_impl {
   LHPC_S7_AUTO = 0,
   LHPC_S7_SIMPLE = 1,           /* thread per column                          */
@@ -155,7 +160,7 @@ typedef struct lhpc_options {
   int32_t xtile_steps;          /* gather steps in flight: 2, 4, 8 (auto), 16    */
   int32_t xtile_store;          /* xg stores: LHPC_STORE_PLAIN / _NT             */
   int32_t xtile_cut;            /* chunk-cut window in nonzeros (0: M/32)        */
-  int32_t xtile_reserved;
+  int32_t xtile_align;          /* enum lhpc_xtile_align                         */
   int64_t xtile_piece;          /* gather piece length in nonzeros               */
   int64_t xtile_range_piece;    /* the same under cache-sized ranges             */
   /* XSLICE */

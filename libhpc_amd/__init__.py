@@ -98,7 +98,7 @@ class Options(C.Structure):
     _fields_ = [("struct_size", C.c_uint32), ("spmv_no_xtile", C.c_int32), ("spmv_locality", C.c_double),
                 ("rowgroup_lanes", C.c_int32), ("rowgroup_rows", C.c_int32),
                 ("xtile_reduce", C.c_int32), ("xtile_ranges", C.c_int32), ("xtile_steps", C.c_int32),
-                ("xtile_store", C.c_int32), ("xtile_cut", C.c_int32), ("xtile_reserved", C.c_int32),
+                ("xtile_store", C.c_int32), ("xtile_cut", C.c_int32), ("xtile_align", C.c_int32),
                 ("xtile_piece", C.c_int64), ("xtile_range_piece", C.c_int64),
                 ("xslice_slices", C.c_int32), ("xslice_partial", C.c_int32), ("xslice_window", C.c_int32),
                 ("xslice_reserved", C.c_int32), ("xslice_mb", C.c_double),
@@ -127,6 +127,7 @@ def _opts(o):
 
 
 XTILE_REDUCE_AUTO, XTILE_REDUCE_PERM, XTILE_REDUCE_IPERM = 0, 1, 2
+XTILE_ALIGN_AUTO, XTILE_ALIGN_OFF, XTILE_ALIGN_UNITS = 0, 1, 2
 S7_AUTO, S7_SIMPLE, S7_RING, S7_RING_X4, S7_RING_X4_LDS = 0, 1, 2, 3, 4
 STORE_AUTO, STORE_PLAIN, STORE_NT, STORE_STAGED = 0, 1, 2, 3
 DIST_EXCHANGE_AUTO, DIST_EXCHANGE_RCCL, DIST_EXCHANGE_P2P, DIST_EXCHANGE_NONE = 0, 1, 2, 3

@@ -130,10 +130,10 @@ int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, 
 
 int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
                 int64_t W, int M, int Rmax, int64_t piece_nnz, int slot_bytes,
-                const int64_t *splits, int n_splits, bool iperm, int cut_window, XtileHost &o) {
+                const int64_t *splits, int n_splits, bool iperm, int cut_window, XtileHost &o, int unit) {
   const int64_t nnz = rp_at(rp, bits, n_rows) - rp_at(rp, bits, 0);
   if (W < 8 || M < 64 || M >= 65536 || M % 16 || Rmax < 1 || (slot_bytes != 4 && slot_bytes != 8) ||
-      cut_window < 1 || cut_window > M)
+      cut_window < 1 || cut_window > M || (unit != 1 && unit != 2 && unit != 4) || (unit > 1 && !iperm))
     return LHPC_ERR_INVALID_ARG;
   const int64_t S = n_cols > 0 ? (n_cols + W - 1) / W : 1;
   if (S > 4096 || nnz + 8 * S >= INT32_MAX || n_rows >= INT32_MAX) return LHPC_ERR_UNSUPPORTED;
@@ -141,7 +141,29 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
   o.W = W;
   o.M = M;
   o.Rmax = Rmax;
+  o.unit = unit;
+  const int64_t U = unit;
+  auto pad = [U](int64_t len) { return (len + U - 1) / U * U; };
   auto RP = [&](int64_t i) { return rp_at(rp, bits, i); };
+  // aligned segments: the longest window [e, e + len) whose padded length
+  // Σ_s ⌈count_s / U⌉·U stays ≤ M (monotone in len, so any shorter cut fits)
+  std::vector<int32_t> wcnt(unit > 1 ? static_cast<size_t>(S) : 0, 0);
+  std::vector<int32_t> touched;
+  auto window = [&](int64_t e) -> int64_t {
+    if (U == 1) return M;
+    int64_t k = e, padded = 0;
+    for (; k < nnz; ++k) {
+      const int64_t s = col[k] / W;
+      const int64_t add = wcnt[static_cast<size_t>(s)] % U == 0 ? U : 0;
+      if (padded + add > M) break;
+      if (wcnt[static_cast<size_t>(s)] == 0) touched.push_back(static_cast<int32_t>(s));
+      ++wcnt[static_cast<size_t>(s)];
+      padded += add;
+    }
+    for (const int32_t s : touched) wcnt[static_cast<size_t>(s)] = 0;
+    touched.clear();
+    return k - e;
+  };
   // first row r in [lo, n_rows] with rp[r] >= e
   auto lower_row = [&](int64_t lo, int64_t e) {
     int64_t hi = n_rows;
@@ -163,7 +185,10 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
     int si = 0;  // next split row after r
     while (!(e == nnz && r == n_rows)) {
       int64_t en, rb;
-      const int64_t Mc = M;
+      const int64_t Mc = window(e);
+      // a cut inside the window: row starts in its back cut_window entries
+      // (scaled to the window when padding shortens it)
+      const int64_t cw = U == 1 ? cut_window : std::max<int64_t>(1, cut_window * Mc / M);
       // a split row is done once a chunk starts at it (e == its start, r == it)
       while (si < n_splits && (RP(splits[si]) < e || (RP(splits[si]) == e && splits[si] <= r))) ++si;
       if (si < n_splits && RP(splits[si]) <= e + Mc) {
@@ -176,7 +201,7 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
         const int64_t target = e + Mc;
         // last row q with rp[q] <= target
         const int64_t q = lower_row(r, target + 1) - 1;
-        if (q >= r && RP(q) > e + Mc - cut_window) {
+        if (q >= r && RP(q) > e + Mc - cw) {
           en = RP(q);  // cut at a row start
         } else {
           en = target;  // cut mid-row
@@ -219,6 +244,8 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
   for (int64_t c = 0; c < C; ++c) {
     int32_t *cc = cnt + c * S;
     for (int64_t k = o.ce[c]; k < o.ce[c + 1]; ++k) ++cc[col[k] / W];
+    if (U > 1)  // aligned segments: padding at each segment's end
+      for (int64_t s = 0; s < S; ++s) cc[s] = static_cast<int32_t>(pad(cc[s]));
   }
   std::vector<int64_t> tbase(static_cast<size_t>(S) + 1, 0);
   {
@@ -231,6 +258,7 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
     }
     for (int64_t s = 0; s < S; ++s) tbase[s + 1] = tbase[s] + (tot[s] + 7) / 8 * 8;
   }
+  if (tbase[S] >= INT32_MAX) return LHPC_ERR_UNSUPPORTED;  // segment padding pushed the stream past int32
   o.total = tbase[S];
   // exclusive prefix down each tile column: segoff[c][s] = tbase[s] + Σ_{c'<c} count[c'][s]
 #pragma omp parallel for schedule(static)

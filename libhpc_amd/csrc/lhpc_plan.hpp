@@ -55,7 +55,8 @@ int build_xslice(const void *row_ptr, int rp_bits, const int32_t *col, const voi
 //            multiplies by val (CSR order) and sums rows merge-path style.
 // The stream is ordered (tile, chunk, CSR position): segment (s, c) is
 // [segoff[c·S + s], segoff[(c+1)·S + s]).  Each tile's stream starts at a
-// multiple of 8 (padding entries are written by gather, never read).
+// multiple of 8 (padding entries are written by gather, never read); with
+// unit > 1 every segment's length is also a multiple of `unit`.
 // Chunks cut the CSR order at the last row start in the back `cut_window`
 // entries of the M window, else mid-row (so every chunk but a range's last
 // holds ≥ M − cut_window nonzeros); a chunk owns the rows that start in it
@@ -64,6 +65,7 @@ struct XtileHost {
   int S = 0;
   int64_t W = 0;
   int M = 0, Rmax = 0;
+  int unit = 1;                      // every segment padded to a multiple of `unit` entries
   int64_t n_chunks = 0;
   int64_t total = 0;                 // padded tile-stream length
   std::vector<int32_t> ce, cr;       // [C+1] chunk first nonzero / first owned row
@@ -95,9 +97,15 @@ void xtile_segment_table(const XtileHost &o, std::vector<uint32_t> &seg, std::ve
 // ranges that can be reduced separately, lhpc_spmv_range);
 // LHPC_ERR_INVALID_ARG otherwise.  iperm selects the reduce's index stream
 // (perm for false, iperm for true; only the selected one is built).
+// unit > 1 (iperm only; 2 or 4): aligned segments — every (tile, chunk)
+// segment is padded at its end to a multiple of `unit` entries, so each
+// starts on a 16-B boundary of xg and the reduce loads it in 16-B units
+// (padding entries: col16 0, never referenced by iperm); chunks are then cut
+// so that their padded length, not their nonzero count, stays ≤ M.
 int build_xtile(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_rows,
                 int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, int slot_bytes,
-                const int64_t *splits, int n_splits, bool iperm, int cut_window, XtileHost &out);
+                const int64_t *splits, int n_splits, bool iperm, int cut_window, XtileHost &out,
+                int unit = 1);
 
 // Wave-transposed run layout of the XTILE reduce's per-position streams (val,
 // iperm): chunk position i belongs to thread t = i / run (run = 64 B of

@@ -67,6 +67,7 @@ void env_overlay(lhpc_options &o) {
   i32("LHPC_XTILE_U", o.xtile_steps);
   if (const char *e = tuning_env("LHPC_XTILE_NTSTORE")) o.xtile_store = std::atoi(e) ? LHPC_STORE_NT : LHPC_STORE_PLAIN;
   i32("LHPC_XTILE_CUT", o.xtile_cut);
+  i32("LHPC_XTILE_ALIGN", o.xtile_align);
   i64("LHPC_XTILE_PIECE", o.xtile_piece);
   i64("LHPC_XTILE_MALL_PIECE", o.xtile_range_piece);
   i32("LHPC_XSLICE_S", o.xslice_slices);

@@ -56,6 +56,7 @@ struct lhpc_spmv_plan {
   uint32_t *d_seg = nullptr;  // segment table (lhpc_plan.hpp xtile_segment_table)
   uint16_t *d_col16 = nullptr, *d_perm = nullptr;
   int xt_p = 1;  // reduce: 1 perm scatter, 3 iperm gather (DESIGN.md §4 XTILE)
+  int xt_al = 0;  // aligned segments: 16-B units (lhpc_options.xtile_align)
   void *d_xg = nullptr;
   double *d_carry = nullptr;
 };

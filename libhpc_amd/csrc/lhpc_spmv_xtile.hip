@@ -208,7 +208,11 @@ __device__ uint64_t g_xt_stamps[1 << 22];
 #ifndef LHPC_XT_IP_WAVES
 #define LHPC_XT_IP_WAVES 8  // iperm reduce: 8 waves/SIMD (fp32 66 → 64 VGPRs: C2 593 → 580 µs)
 #endif
-template <typename T, int G, int BLK, bool IP>
+// AL (iperm only): aligned segments (lhpc_plan.hpp build_xtile unit > 1) —
+// every segment starts on a 16-B boundary and spans whole 16-B units of VW
+// positions, so phase A ranks units instead of positions (M/VW ≤ 64 batches
+// of 64 units) and each lane moves one 16-B unit by LDS-DMA, fp64 included.
+template <typename T, int G, int BLK, bool IP, bool AL>
 __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce(
     const int32_t *__restrict__ cdesc, const uint32_t *__restrict__ seg, const int32_t *__restrict__ seghi, int S,
     int64_t c0, int64_t C,
@@ -222,6 +226,9 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
                 "8/16 batches per wave; ≤ 256 batches per chunk; sbm ≥ 128 words");
   typedef T tvec __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
   constexpr int VW = 16 / sizeof(T), NV = RUN / VW;
+  static_assert(!AL || IP, "aligned segments need the iperm reduce");
+  constexpr int NBU = NB / VW;  // AL: 64-unit batches per wave
+  static_assert(!AL || NBU * (BLK / kWave) <= kWave, "AL: a chunk's unit batches fit one wave's lanes");
   // dynamic LDS (xtile_lds_bytes): xs[M + VW] T (slot M is the sentinel's
   // spare), bt[BLK/64][NB] u32x4, ws[BLK/64] f64, wsf[BLK/64] i32, bm[M/32]
   // u32, sbm[M/32] u32, rpl[RMAX+1] u16 (padded to 4 B), base_ne[S] i32, wsum[8] i32
@@ -326,7 +333,9 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
       const int len = sb[q] - sa[q];
       if (len > 0) {
         base_ne[rank] = sa[q] - off;
-        atomicOr(sbm + (off >> 5), 1u << (off & 31));
+        const int ub = AL ? off / VW : off;  // AL: the bitmap marks start units
+        LHPC_DEVICE_CHECK(!AL || (off % VW == 0 && sa[q] % VW == 0));
+        atomicOr(sbm + (ub >> 5), 1u << (ub & 31));
         ++rank;
       }
       off += len;
@@ -338,7 +347,26 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   // ---- phase A: src = base_ne[rank] + f, xg loads (round trip 3);
   //      positions past m load the sentinel entry `total` (perm: spare slot M)
   int src[NB];
-  {
+  if constexpr (AL) {
+    // unit u of batch j covers flat positions VW·((wv·NBU + j)·64 + lane) …;
+    // lane q holds unit batch q's bitmap word (≤ 64 batches: one pass)
+    const uint64_t wl = static_cast<uint64_t>(sbm[2 * lane]) | (static_cast<uint64_t>(sbm[2 * lane + 1]) << 32);
+    const int cnt = __popcll(wl);
+    const int incl = wave_incl_scan(cnt);
+    u32x4 *bt = bt0 + wv * NB;
+    if (lane / NBU == wv) {
+      const uint64_t w1 = wl >> 1;
+      bt[lane & (NBU - 1)] = u32x4{static_cast<uint32_t>(w1), static_cast<uint32_t>(w1 >> 32),
+                                   static_cast<uint32_t>(incl - cnt - 1 + static_cast<int>(wl & 1u)), 0u};
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int u = 0; u < NBU; ++u) {
+      const u32x4 t = bt[u];
+      const int rk = __builtin_amdgcn_mbcnt_hi(t[1], __builtin_amdgcn_mbcnt_lo(t[0], t[2]));
+      src[u] = base_ne[rk] + ((wv * NBU + u) * kWave + lane) * VW;  // a multiple of VW: 16-B aligned
+    }
+  } else {
     // lane q holds batch q's word; the wave-uniform rank terms (w >> 1,
     // base) go to an LDS triple that the owning wave reads back as a
     // broadcast:  rank = starts before the batch − 1 + (w & 1) + mbcnt(w >> 1)
@@ -386,7 +414,21 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     // lines: nt 354 → 331 µs, nt + 16-B LDS-DMA 306 µs — DESIGN.md §4)
     const __amdgpu_buffer_rsrc_t xr_rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<T *>(xg), 0, (total + 2) * static_cast<int>(sizeof(T)), 0x00020000);
-    if constexpr (sizeof(T) == 4) {
+    if constexpr (AL) {
+      // one 16-B unit per lane, straight into its flat slots (64 units = 1 KB
+      // of LDS per instruction); a unit past the chunk loads what follows its
+      // segment (or 0 past the stream) into slots nothing reads.  Device pass
+      // only: the host pass's semantic check rejects the 16-B size (a gfx950
+      // feature) without a diagnostic and then drops the kernel's host stub
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+      for (int u = 0; u < NBU; ++u)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            xr_rs, (__attribute__((address_space(3))) void *)(xs + (wv * NBU + u) * kWave * VW), 16,
+            src[u] * static_cast<int>(sizeof(T)), 0, 0, LHPC_XT_XG_CPOL);
+#endif
+      load_ipv();
+    } else if constexpr (sizeof(T) == 4) {
 #if defined(LHPC_XT_PROBE_XG)
       // timing-only probe (wrong results): 1 = the chunk's xg as one aligned
       // contiguous run, 16-B LDS-DMA per lane; 2 = the same, non-temporal;
@@ -481,7 +523,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     if (tid == 0) xs[M] = T(0);  // the zero slot that iperm padding points at
   // the LDS-DMA of phase A is counted by vmcnt, which the barrier does not
   // wait for: drain it before any wave reads another wave's flat slots
-  if constexpr (IP && sizeof(T) == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (IP && (sizeof(T) == 4 || AL)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   LHPC_XT_STAMP(5, 0)
 
@@ -613,21 +655,23 @@ int xtile_g(int S) {
   return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : 8;
 }
 
-template <typename T, int G, bool IP>
+template <typename T, int G, bool IP, bool AL>
 const void *xtile_reduce_fn() {
-  if constexpr (G > xt_gmax<T>())
+  if constexpr (G > xt_gmax<T>() || (AL && !IP))
     return nullptr;
   else
-    return reinterpret_cast<const void *>(k_xtile_reduce<T, G, xt_red_blk<T>(), IP>);
+    return reinterpret_cast<const void *>(k_xtile_reduce<T, G, xt_red_blk<T>(), IP, AL>);
 }
-template <typename T, bool IP>
+template <typename T, bool IP, bool AL>
 const void *xtile_reduce_fn(int g) {
-  return g == 1 ? xtile_reduce_fn<T, 1, IP>() : g == 2 ? xtile_reduce_fn<T, 2, IP>()
-         : g == 4 ? xtile_reduce_fn<T, 4, IP>() : xtile_reduce_fn<T, 8, IP>();
+  return g == 1 ? xtile_reduce_fn<T, 1, IP, AL>() : g == 2 ? xtile_reduce_fn<T, 2, IP, AL>()
+         : g == 4 ? xtile_reduce_fn<T, 4, IP, AL>() : xtile_reduce_fn<T, 8, IP, AL>();
 }
+// ip: iperm reduce; al: aligned segments (iperm only, else nullptr)
 template <typename T>
-const void *xtile_reduce_fn(int g, bool ip) {
-  return ip ? xtile_reduce_fn<T, true>(g) : xtile_reduce_fn<T, false>(g);
+const void *xtile_reduce_fn(int g, bool ip, bool al) {
+  if (al) return ip ? xtile_reduce_fn<T, true, true>(g) : nullptr;
+  return ip ? xtile_reduce_fn<T, true, false>(g) : xtile_reduce_fn<T, false, false>(g);
 }
 
 template <typename T, int U, bool NT = false>
@@ -662,7 +706,7 @@ int launch_reduce(const lhpc_spmv_plan *p, int64_t c0, int64_t c1, int64_t n0, i
   if (c1 > c0) {
     const int64_t Cx = (c1 - c0 + 7) / 8;
     const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(xt_red_blk<T>());
-    const void *fn = xtile_reduce_fn<T>(xtile_g<T>(p->S), p->xt_p == 3);
+    const void *fn = xtile_reduce_fn<T>(xtile_g<T>(p->S), p->xt_p == 3, p->xt_al != 0);
     const int32_t *cd = p->d_cdesc, *sh = p->d_seghi, *rp = static_cast<const int32_t *>(p->d_row_ptr);
     const uint32_t *so = p->d_seg;
     int S = p->S, total = static_cast<int>(p->xt_total);
@@ -705,9 +749,19 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   if (o.xtile_reduce != LHPC_XTILE_REDUCE_AUTO) ip = o.xtile_reduce == LHPC_XTILE_REDUCE_IPERM;
   // the iperm reduce addresses xg with 32-bit buffer offsets: stream + tile
   // padding (≤ 8 per tile) + one piece of slack must stay below 2 GiB
-  const int64_t stream_max = p->nnz + 8 * ((p->n_cols + W - 1) / W) + 2 * M;
+  const int64_t n_tiles = (p->n_cols + W - 1) / W;
+  const int64_t stream_max = p->nnz + 8 * n_tiles + 2 * M;
   if (stream_max * static_cast<int64_t>(tsz) >= (int64_t{1} << 31)) ip = false;
   p->xt_p = ip ? 3 : 1;
+  // aligned segments (iperm only): each (tile, chunk) segment padded to 16 B
+  // (≤ VW − 1 entries per segment, ≤ 3 per 4 nonzeros in the worst case)
+  constexpr int VW = static_cast<int>(16 / tsz);
+  bool al = false;
+  if (o.xtile_align == LHPC_XTILE_ALIGN_UNITS) al = true;
+  if (al && (!ip || (stream_max + (VW - 1) * std::min<int64_t>(p->nnz, n_tiles * (p->nnz / (M / 2) + 2))) *
+                                static_cast<int64_t>(tsz) >= (int64_t{1} << 31)))
+    al = false;
+  p->xt_al = al ? 1 : 0;
   // chunk cuts: at the last row start in the back M/32 of the window, else
   // mid-row (the row's pieces meet in k_xtile_fixup).  Per-chunk costs are
   // fixed, so full chunks matter on skewed rows: C4 has 19803 chunks when any
@@ -741,7 +795,7 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   }
   XtileHost xt;
   LHPC_TRY(build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, M, RMAX, piece, static_cast<int>(tsz),
-                       p->split_rows.data(), static_cast<int>(p->split_rows.size()), ip, cut, xt));
+                       p->split_rows.data(), static_cast<int>(p->split_rows.size()), ip, cut, xt, al ? VW : 1));
   p->kernel = LHPC_KERNEL_XTILE;
   p->rp64 = 0;
   p->S = xt.S;
@@ -761,7 +815,7 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   // non-temporal: 473 → 536 µs)
   p->xt_nt = p->xt_mall <= 1 && p->nnz * static_cast<int64_t>(tsz) > (int64_t{256} << 20) ? 1 : 0;
   if (o.xtile_store != LHPC_STORE_AUTO) p->xt_nt = o.xtile_store == LHPC_STORE_NT ? 1 : 0;
-  const void *rfn = xtile_reduce_fn<T>(xtile_g<T>(xt.S), ip);
+  const void *rfn = xtile_reduce_fn<T>(xtile_g<T>(xt.S), ip, al);
   if (!rfn) return LHPC_ERR_UNSUPPORTED;  // more tiles than the reduce's segment table holds
   LHPC_HIP_TRY(hipFuncSetAttribute(rfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
   const int64_t n_rows = p->n_rows, C = xt.n_chunks;

@@ -65,13 +65,15 @@ Csr powerlaw(int64_t n, int64_t m, int64_t lmax, uint64_t seed) {
 
 // XTILE invariants: every CSR nonzero appears once in its chunk's segment
 // concatenation, with the column it had; chunks tile the CSR order.
-void check_xtile(const Csr &a, bool iperm, const std::vector<int64_t> &splits, int cut = 512) {
+// unit > 1 (aligned segments): every segment starts and ends on a multiple
+// of unit, the padded concatenation stays ≤ M, iperm skips the padding.
+void check_xtile(const Csr &a, bool iperm, const std::vector<int64_t> &splits, int cut = 512, int unit = 1) {
   const int64_t W = 4096;
   const int M = 1024, Rmax = 128;
   lhpc::XtileHost xt;
   const int rc = lhpc::build_xtile(a.rp.data(), 64, a.col.data(), a.n, a.m, W, M, Rmax, 3000, 4,
                                    splits.empty() ? nullptr : splits.data(), static_cast<int>(splits.size()), iperm,
-                                   cut, xt);
+                                   cut, xt, unit);
   CHECK(rc == 0);
   if (rc) return;
   const int64_t C = xt.n_chunks, S = xt.S;
@@ -79,24 +81,30 @@ void check_xtile(const Csr &a, bool iperm, const std::vector<int64_t> &splits, i
   for (int64_t c = 0; c < C; ++c) {
     const int64_t e0 = xt.ce[c], e1 = xt.ce[c + 1];
     CHECK(e1 >= e0 && e1 - e0 <= M);
-    std::vector<int> seen(static_cast<size_t>(e1 - e0), 0);
+    std::vector<int> seen(static_cast<size_t>(M), 0);
     int64_t flat = 0;
     for (int64_t s = 0; s < S; ++s) {
       const int64_t g0 = xt.segoff[c * S + s], g1 = xt.segoff[(c + 1) * S + s];
       CHECK(g0 <= g1 && g1 <= xt.total);
+      CHECK(g0 % unit == 0 && (g1 - g0) % unit == 0);
       for (int64_t g = g0; g < g1; ++g, ++flat) {
         if (iperm) continue;
         (void)xt.perm[g];  // perm mode: every stream entry has a slot
       }
     }
-    CHECK(flat == e1 - e0);
+    CHECK(unit == 1 ? flat == e1 - e0 : (flat >= e1 - e0 && flat <= M));
     if (iperm) {
       for (int64_t k = e0; k < e1; ++k) {
         const int f = xt.iperm[k];
         CHECK(f >= 0 && f < flat);
         if (f >= 0 && f < flat) ++seen[static_cast<size_t>(f)];
       }
-      for (int v : seen) CHECK(v == 1);
+      int64_t hits = 0;
+      for (int v : seen) {
+        CHECK(v <= 1);
+        hits += v;
+      }
+      CHECK(hits == e1 - e0);
     }
   }
   // cache-sized ranges: range pieces cover the stream once, and every entry
@@ -198,6 +206,12 @@ int main() {
     check_xtile(p, ip, {}, 32);
     check_xtile(p, ip, {77}, 1024);
     check_xtile(e, ip, {});
+  }
+  for (int unit : {2, 4}) {  // aligned segments (iperm only)
+    check_xtile(u, true, {}, 512, unit);
+    check_xtile(p, true, {1, 5000, 19999}, 512, unit);
+    check_xtile(p, true, {}, 32, unit);
+    check_xtile(e, true, {}, 512, unit);
   }
   for (int S : {1, 8, 64}) {
     lhpc::XsliceHost xs;

@@ -35,6 +35,23 @@ def test_nm_exports_match_header():
     assert set(declared_functions()) <= exported
 
 
+def test_no_unresolved_kernel_handles():
+    """Every kernel the library launches has its host handle defined in the
+    library: an undefined `lhpc::` symbol means a kernel instantiation whose
+    host stub the compiler dropped (the aligned-segment reduce once lost its
+    stubs to a host-pass check of a gfx950-only builtin) — the .so links, then
+    fails at load or launch on the GPU box."""
+    import subprocess
+    for lib in ("_lib/liblhpc.so", "_lib/liblhpc_probe.so"):
+        path = os.path.join(ROOT, "libhpc_amd", lib)
+        if not os.path.exists(path):
+            continue
+        out = subprocess.run(["nm", "-C", "--undefined-only", path], capture_output=True, text=True,
+                             check=True).stdout
+        bad = [l.strip() for l in out.splitlines() if "lhpc::" in l]
+        assert not bad, f"{lib}: unresolved: {bad[:4]}"
+
+
 def test_abi_version_and_strerror(lhpc):
     assert lhpc.lib.lhpc_abi_version() == 1
     for st in (0, -1, -2, -3, -4, -5, -6):

@@ -328,13 +328,17 @@ def _csr_from_lengths(lengths, n_cols, seed, dyadic):
     return rp, col, val
 
 
-@pytest.fixture(params=["perm", "iperm"])
+@pytest.fixture(params=["perm", "iperm", "iperm_aligned"])
 def xt_layout(request):
     """The XTILE reduce index streams: perm (xg scattered into CSR slots) and
     iperm (xg kept in flat order in LDS, each CSR position's x gathered
-    through a CSR-order index), pinned through lhpc_options.xtile_reduce.
+    through a CSR-order index), pinned through lhpc_options.xtile_reduce;
+    iperm_aligned: iperm over aligned segments (every (tile, chunk) segment
+    padded to 16 B, loaded in 16-B units; lhpc_options.xtile_align).
     Returns the options dict the test extends."""
-    return {"xtile_reduce": 2 if request.param == "iperm" else 1}
+    if request.param == "iperm_aligned":
+        return {"xtile_reduce": 2, "xtile_align": 2}
+    return {"xtile_reduce": 2 if request.param == "iperm" else 1, "xtile_align": 1}
 
 
 def _check_xtile(lhpc, gpu, lengths, n_cols, dtype, seed, dyadic=True, expect_cont=None, opts=None):
