@@ -5,23 +5,31 @@
 N=1: BASELINE configs[1] — CSR SpMV, n=10M, nnz=150M (exactly 15 uniform
 distinct sorted columns per row), fp32 values/x/y, A and x resident in HBM.
 N>1 (launched by torch.distributed.run, one rank per GPU): the SAME matrix is
-split into N nnz-balanced contiguous row blocks (strong scaling); a step is
-the local SpMV plus the RCCL all-gather of y over xGMI (torch.distributed
-backend "nccl" = RCCL), i.e. the exchange that makes y the next x.
+split into N·K nnz-balanced interleaved row blocks, K = --chunks per rank
+(strong scaling); a step is the rank's local SpMV plus the y exchange over
+xGMI that makes y the next x, chunk k's exchange overlapping chunk k+1's
+reduce.  The native path (lhpc_dist_*) times both exchanges in the same run —
+RCCL collectives (backend "nccl" = RCCL) and direct peer stores into every
+rank's registered y window — plus SpMV-only and exchange-only steps, and
+reports the faster exchange whose y equals the RCCL one.
 
 One step = one y = A·x over the whole matrix.  W untimed warmup steps, then
 exactly K timed steps between barrier + device synchronize; the max over ranks
 is reported.  value = 2·nnz·K / time (GFLOP/s, whole job).
 
 Extra objects on the JSON line:
-  roofline      the SpMV call on rank 0 (XSLICE = k_spmv_xslice + k_xslice_reduce,
-                see DESIGN.md): achieved = algorithmic bytes per call
-                (nnz·(4+4) + (n+1)·4 + 2·n·4, x counted once) ÷ average call
-                time from HIP events on the launch stream; peak 8.0 TB/s;
-                traffic = PMC HBM bytes per call from profiles/ (or null).
+  roofline      the SpMV call on rank 0 (XTILE for C2-C4 = k_xtile_gather +
+                k_xtile_reduce (+ k_xtile_fixup)):
+                achieved = algorithmic bytes per call (nnz·(4+4) + (n+1)·4 +
+                2·n·4 for fp32, x counted once) ÷ average call time from HIP
+                events on the launch stream; peak 8.0 TB/s; traffic = PMC
+                fabric bytes per call from profiles/traffic.json (or null);
+                layout = the same call against the bytes the XTILE layout
+                streams.
   cpu_baseline  rank 0, N=1 only: the AVX2 + OpenMP CSR SpMV of oracle/ (the
                 reference has no CPU SpMV) on the same matrix, timed
-                for ~10 s on the box's host cores.
+                for ~10 s on the box's host cores (OpenMP placement and host
+                CPU / NUMA nodes recorded in the object).
 
 --workload sort (not the headline): the reference's only
 published GPU number — radix sort of 500M uint32 keys (README.md:52, ~360 ms
@@ -484,6 +492,39 @@ def sampled_y_check(rp, col, val, x, y, m, seed=0x5EED00C1):
             "bound": "|dy| <= 1e-6*sum|a*x| per row vs fp64 numpy"}
 
 
+def host_info():
+    """Which host produced a CPU baseline: CPU model, the CPUs this process may
+    run on, and the NUMA nodes those CPUs belong to (the OpenMP threads are
+    bound close, one per core, inside that set)."""
+    info = {"cpu_model": None, "affinity_cpus": None, "numa_nodes": None}
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["cpu_model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+        info["affinity_cpus"] = len(cpus)
+        mine, nodes = set(cpus), set()
+        base = "/sys/devices/system/node"
+        for d in os.listdir(base):
+            if not (d.startswith("node") and d[4:].isdigit()):
+                continue
+            node_cpus = set()
+            for part in open(os.path.join(base, d, "cpulist")).read().strip().split(","):
+                if part:
+                    lo, _, hi = part.partition("-")
+                    node_cpus.update(range(int(lo), int(hi or lo) + 1))
+            if node_cpus & mine:
+                nodes.add(int(d[4:]))
+        info["numa_nodes"] = sorted(nodes) or None
+    except OSError:
+        pass
+    return info
+
+
 def cpu_spmv_baseline(rp, col, val, x, nnz, seconds, threads=None):
     """C1 is quoted single-thread; C2-C4 on all host threads."""
     from tests import _support as S  # oracle/ is test infrastructure: baseline leg only
@@ -500,7 +541,8 @@ def cpu_spmv_baseline(rp, col, val, x, nnz, seconds, threads=None):
             "sample": f"full matrix (nnz={nnz}), best of {len(times)} passes "
                       f"({sum(times):.1f} s), AVX2 gather" + (" + OpenMP" if threads > 1 else ", 1 thread")
                       + ", oracle/oracle.c cpu_spmv_simd",
-            "omp": {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OMP_PROC_BIND", "OMP_PLACES")}}
+            "omp": {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OMP_PROC_BIND", "OMP_PLACES")},
+            "host": host_info()}
 
 
 def stencil_bench(args, L, torch, dev, stream, barrier):
@@ -587,7 +629,7 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
             lib.oracle_stencil7(uh.ctypes.data, oh.ctypes.data, n, n, n, g, -6.0, 1.0, th)
             ts.append(time.perf_counter() - t0)
         out["_cpu"] = {"value": cells / min(ts) / 1e9, "unit": "Gcell/s", "cores": th, "kind": "port",
-                       "sample": f"full 512^3 grid, best of {len(ts)} passes, OpenMP oracle_stencil7"}
+                       "sample": f"full 512^3 grid, best of {len(ts)} passes, OpenMP oracle_stencil7", "host": host_info()}
     if wl in ("blur_x", "blur_y") and not args.no_cpu_baseline:
         from tests import _support as S
         lib = S.load_oracle()
@@ -603,7 +645,8 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
             fnc(ah.ctypes.data, bh.ctypes.data, n, n, g, th)
             ts.append(time.perf_counter() - t0)
         out["_cpu"] = {"value": cells / min(ts) / 1e9, "unit": "Gcell/s", "cores": th, "kind": "port",
-                       "sample": f"full 8192^2 grid, best of {len(ts)} passes, reference SSE loop restated"}
+                       "sample": f"full 8192^2 grid, best of {len(ts)} passes, reference SSE loop restated",
+                       "host": host_info()}
     return out
 
 
@@ -664,7 +707,8 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
                                   x.ctypes.data, 0.0, 5, C.byref(res_c))
             ts.append((time.perf_counter() - t0) / max(k, 1))
         out["cpu_baseline"] = {"value": 1.0 / min(ts), "unit": "iter/s", "cores": 1, "kind": "port",
-                               "sample": f"{k} iterations of the fp64 CG restatement (oracle.c), best of {len(ts)}"}
+                               "sample": f"{k} iterations of the fp64 CG restatement (oracle.c), best of {len(ts)}",
+                               "host": host_info()}
     plan.close()
     return out
 
@@ -740,7 +784,8 @@ def cpu_sort_baseline(keys, src, seconds):
     assert np.all(a[1:] >= a[:-1])
     return {"value": m / min(ts) / 1e9, "unit": "Gkeys/s", "cores": cpu_threads(), "kind": kind,
             "sample": f"50M of the same keys, best of {len(ts)} sorts"
-                      + (" (reference radix_sort, OpenMP)" if kind == "reference" else " (C LSD restatement)")}
+                      + (" (reference radix_sort, OpenMP)" if kind == "reference" else " (C LSD restatement)"),
+            "host": host_info()}
 
 
 if __name__ == "__main__":

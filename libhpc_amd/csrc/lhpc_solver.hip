@@ -214,7 +214,17 @@ extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, doubl
   double *rr[2] = {sc.d, sc.d + 1}, *pq = sc.d + 2, *bb = sc.d + 3, *part = sc.d + 8;
   const int g = vec_grid(n);
   int it = 0;
-  double h_rr = 0.0, h_bb = 0.0;
+  // the two scalars the host loop reads come back into pinned memory: no
+  // asynchronous copy touches pageable host memory
+  double *hs = nullptr;
+  LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&hs), 2 * sizeof(double), hipHostMallocDefault));
+  struct HostFree {
+    double *p;
+    ~HostFree() { (void)hipHostFree(p); }
+  } hf{hs};
+  double &h_rr = hs[0], &h_bb = hs[1];
+  h_rr = 0.0;
+  h_bb = 0.0;
   // bb = b·b; q = A·x; r = b - q; p = r; rr = r·r
   if (dtype == LHPC_F32) LHPC_TRY(dot_dev(static_cast<const float *>(b), static_cast<const float *>(b), n, bb, part, s));
   else LHPC_TRY(dot_dev(static_cast<const double *>(b), static_cast<const double *>(b), n, bb, part, s));
@@ -227,7 +237,7 @@ extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, doubl
                        static_cast<const double *>(q), static_cast<double *>(r), static_cast<double *>(p), n, part);
   hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(kVecThreads), 0, s, part, g, rr[0]);
   LHPC_TRY(check_launch(s));
-  LHPC_HIP_TRY(hipMemcpyAsync(&h_bb, bb, 8, hipMemcpyDeviceToHost, s));
+  LHPC_HIP_TRY(hipMemcpyAsync(&h_bb, bb, 8, hipMemcpyDeviceToHost, s));  // pinned
   LHPC_HIP_TRY(hipMemcpyAsync(&h_rr, rr[0], 8, hipMemcpyDeviceToHost, s));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
   const double stop = tol * tol * (h_bb > 0.0 ? h_bb : 1.0);
