@@ -206,13 +206,45 @@ def main():
                                                 options={"dist_exchange": L.DIST_EXCHANGE_RCCL,
                                                          "dist_world1": 1 if world == 1 else 0})
             y_p2p = torch.empty(n, dtype=xd.dtype, device=dev)
+
+            def agree(ok):  # every rank takes the same branch (no half-set-up exchange)
+                f = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                                 device=dev if dist.get_backend() == "nccl" else "cpu")
+                dist.all_reduce(f, op=dist.ReduceOp.MIN)
+                return bool(f.item())
             if world > 1:
+                # the peer exchange is an optimisation: if its setup or a short
+                # probe fails on any rank (no IPC between the devices, a flag
+                # wait timing out), every rank drops it and the RCCL exchange
+                # is still measured.  The probe calls hold no collective, and
+                # every flag wait is bounded, so all ranks reach the agreement.
+                pp = None
                 try:
-                    comm.p2p_setup_torch(y_p2p)
-                    dplans["p2p"] = L.DistSpMVPlan(comm, n, n, args.chunks, cuts, lrp, lc, lv,
-                                                   options={"dist_exchange": L.DIST_EXCHANGE_P2P})
-                except L.LhpcError as e:  # e.g. no IPC between the ranks' devices
+                    comm.p2p_setup_torch(y_p2p)  # collective-safe: raises on every rank or none
+                    pp = L.DistSpMVPlan(comm, n, n, args.chunks, cuts, lrp, lc, lv,
+                                        options={"dist_exchange": L.DIST_EXCHANGE_P2P})
+                except Exception as e:  # e.g. no IPC between the ranks' devices
                     xnotes["p2p"] = f"unavailable: {e}"
+                if agree(pp is not None):
+                    ok = True
+                    try:
+                        for _ in range(3):
+                            pp(xd, y_p2p, stream=stream)
+                        torch.cuda.synchronize()
+                        ok = comm.p2p_status() == 0
+                        if not ok:
+                            xnotes["p2p"] = "probe: a flag wait timed out"
+                    except Exception as e:
+                        ok, xnotes["p2p"] = False, f"probe failed: {e}"
+                    if agree(ok):
+                        dplans["p2p"] = pp
+                    else:
+                        xnotes.setdefault("p2p", "probe failed on another rank")
+                        torch.cuda.synchronize()
+                        pp.close()
+                elif pp is not None:
+                    xnotes.setdefault("p2p", "unavailable on another rank")
+                    pp.close()
             dplans["none"] = L.DistSpMVPlan(comm, n, n, args.chunks, cuts, lrp, lc, lv,
                                             options={"dist_exchange": L.DIST_EXCHANGE_NONE})
             # the same local rows as one plan: the live kernel-only call timing below

@@ -781,16 +781,36 @@ class DistComm:
     def p2p_setup_torch(self, y, group=None):
         """Export y, all-gather the blobs over an initialised torch.distributed
         group (any backend), import them: lhpc_dist_spmv(…, y) then exchanges
-        by direct peer stores."""
+        by direct peer stores.
+
+        Collective-safe: every rank takes part in the same collectives
+        whatever fails locally (a rank whose export fails sends a marked empty
+        blob), and if any rank's export or import failed every rank raises
+        LhpcError — no rank is left with a window its peers never mapped."""
         import torch
         import torch.distributed as dist
-        mine = np.frombuffer(self.p2p_export(y), dtype=np.uint8).copy()
-        t = torch.from_numpy(mine)
-        if dist.get_backend(group) == "nccl":
-            t = t.to(torch.device("cuda", self.device))
+        err = None
+        try:
+            blob, ok = self.p2p_export(y), 1
+        except LhpcError as e:
+            blob, ok, err = bytes(DIST_P2P_BLOB_BYTES), 0, e
+        mine = np.frombuffer(blob + bytes([ok]), dtype=np.uint8).copy()
+        dev = torch.device("cuda", self.device) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        t = torch.from_numpy(mine).to(dev)
         parts = [torch.empty_like(t) for _ in range(self.nranks)]
         dist.all_gather(parts, t, group=group)
-        self.p2p_import([p.cpu().numpy().tobytes() for p in parts])
+        parts = [p.cpu().numpy() for p in parts]
+        if not all(int(p[-1]) == 1 for p in parts):
+            raise LhpcError(-6, f"p2p export failed on a rank ({err})")  # LHPC_ERR_INTERNAL
+        try:
+            self.p2p_import([p[:-1].tobytes() for p in parts])
+            ok = 1
+        except LhpcError as e:
+            ok, err = 0, e
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if int(flag.item()) != 1:
+            raise LhpcError(-6, f"p2p import failed on a rank ({err})")  # LHPC_ERR_INTERNAL
 
     def p2p_status(self) -> int:
         return int(lib.lhpc_dist_p2p_status(self._h))
