@@ -66,21 +66,20 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const K *__restr
   counts[static_cast<int64_t>(blockIdx.x) * 256 + t] = hist[0][t] + hist[1][t] + hist[2][t] + hist[3][t];
 }
 
-// Block-wide exclusive scan of one value per thread (256 threads); returns the total.
-__device__ __forceinline__ uint32_t block_exscan256(uint32_t v, uint32_t *tmp /*[256]*/, uint32_t &total) {
-  const int t = threadIdx.x;
-  tmp[t] = v;
+// Block-wide exclusive scan of one value per thread (256 threads = 4 waves);
+// returns the total.  DPP scan inside each wave, the four wave totals through
+// LDS: two barriers (the Hillis-Steele form took 16 per call, and the
+// downsweep runs two scans per 4096-key sub-tile).
+__device__ __forceinline__ uint32_t block_exscan256(uint32_t v, uint32_t *tmp /*[≥4]*/, uint32_t &total) {
+  const int t = threadIdx.x, w = t / kWave;
+  const uint32_t inc = static_cast<uint32_t>(wave_incl_scan(static_cast<int>(v)));  // modular add: same bits
+  if ((t & (kWave - 1)) == kWave - 1) tmp[w] = inc;
   __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    const uint32_t add = t >= off ? tmp[t - off] : 0u;
-    __syncthreads();
-    tmp[t] += add;
-    __syncthreads();
-  }
-  total = tmp[255];
-  const uint32_t incl = tmp[t];
-  __syncthreads();
-  return incl - v;
+  const uint32_t t0 = tmp[0], t1 = tmp[1], t2 = tmp[2], t3 = tmp[3];
+  total = t0 + t1 + t2 + t3;
+  const uint32_t off = (w > 0 ? t0 : 0u) + (w > 1 ? t1 : 0u) + (w > 2 ? t2 : 0u);
+  __syncthreads();  // tmp is reused by the caller's next scan
+  return off + inc - v;
 }
 
 // Scan: one workgroup per digit d.  counts[b][d] → exclusive prefix over
