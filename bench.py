@@ -419,6 +419,12 @@ def main():
             result["roofline"]["layout"] = {"stream_bytes_per_call": stream_b,
                                             "achieved": stream_b / call_s / 1e9,
                                             "frac": stream_b / call_s / 1e9 / HBM_PEAK_GBPS}
+        if rank == 0 and world == 1:
+            # the attainable rate for the bytes this call streams (the layout's
+            # for XTILE, else the algorithmic ones), measured live
+            lay = result["roofline"].get("layout")
+            moved = lay["stream_bytes_per_call"] if lay else local_alg
+            result["roofline"]["copy"] = copy_ceiling(L, torch, dev, stream, int(moved), moved / call_s / 1e9)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_spmv_baseline(rp, col, val, x, nnz, args.cpu_seconds,
                                                        threads=1 if wl == "c1" else None)
@@ -446,31 +452,37 @@ def main():
 
 def copy_ceiling(L, torch, dev, stream, nbytes, achieved_gbps):
     """Attainable read+write rate for the same bytes (report a
-    measured copy bandwidth beside the 8 TB/s peak): the best copy probe
-    measured (8 B/lane, non-temporal, grid-stride; tools/probe_copy.py),
-    moving nbytes/2 in and nbytes/2 out, timed live on the bench stream."""
+    measured copy bandwidth beside the 8 TB/s peak), timed live on the bench
+    stream: grid-stride non-temporal copies moving nbytes/2 in and nbytes/2
+    out, at 8 B/lane (the best copy probe measured, tools/probe_copy.py) and
+    16 B/lane (SURVEY §8d's `stall_lg_coalesced_256_best` idiom,
+    cuda_tut_stall_lg.cu:63-71).  `copy` is the faster of the two; `frac`
+    puts achieved_gbps against it."""
     import ctypes as C
     P = C.CDLL(os.path.join(os.path.dirname(L.LIB_PATH), "liblhpc_probe.so"))
     half = (nbytes // 2) // 16 * 16
     src = torch.empty(half // 4, dtype=torch.float32, device=dev).uniform_()
     dst = torch.empty_like(src)
-
-    def run():
-        P.lhpc_probe_copy_w(C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()), C.c_int64(half),
-                            C.c_int(16384), C.c_int(8), C.c_int(1), C.c_void_p(stream.cuda_stream))
-    for _ in range(3):
-        run()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(10):
-        run()
-    e1.record(stream)
-    torch.cuda.synchronize()
-    gbps = 2 * half / (e0.elapsed_time(e1) * 1e-3 / 10) / 1e9
+    rates = {}
+    for width in (8, 16):
+        def run():
+            P.lhpc_probe_copy_w(C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()), C.c_int64(half),
+                                C.c_int(16384), C.c_int(width), C.c_int(1), C.c_void_p(stream.cuda_stream))
+        for _ in range(3):
+            run()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(10):
+            run()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        rates[width] = 2 * half / (e0.elapsed_time(e1) * 1e-3 / 10) / 1e9
     del src, dst
-    return {"unit": "GB/s", "copy": gbps, "frac": achieved_gbps / gbps,
-            "note": "same bytes copied by the 8 B/lane non-temporal grid-stride probe"}
+    gbps = max(rates.values())
+    return {"unit": "GB/s", "copy": gbps, "frac": achieved_gbps / gbps, "copy_8B_lane": rates[8],
+            "copy_16B_lane": rates[16], "bytes": 2 * half,
+            "note": "the same bytes copied by non-temporal grid-stride probes (8 and 16 B/lane); copy = the faster"}
 
 
 def gather_ceiling(L, torch, dev, stream, nnz, call_s):
