@@ -450,6 +450,13 @@ def main():
         dist.destroy_process_group()
 
 
+def probe_lib_path(L):
+    """liblhpc_probe.so (measurement kernels, not on the ABI): next to the
+    loaded liblhpc.so, else the in-tree build (A/B builds ship only liblhpc.so)."""
+    p = os.path.join(os.path.dirname(L.LIB_PATH), "liblhpc_probe.so")
+    return p if os.path.exists(p) else os.path.join(ROOT, "libhpc_amd", "_lib", "liblhpc_probe.so")
+
+
 def copy_ceiling(L, torch, dev, stream, nbytes, achieved_gbps):
     """Attainable read+write rate for the same bytes (report a
     measured copy bandwidth beside the 8 TB/s peak), timed live on the bench
@@ -459,7 +466,7 @@ def copy_ceiling(L, torch, dev, stream, nbytes, achieved_gbps):
     cuda_tut_stall_lg.cu:63-71).  `copy` is the faster of the two; `frac`
     puts achieved_gbps against it."""
     import ctypes as C
-    P = C.CDLL(os.path.join(os.path.dirname(L.LIB_PATH), "liblhpc_probe.so"))
+    P = C.CDLL(probe_lib_path(L))
     half = (nbytes // 2) // 16 * 16
     src = torch.empty(half // 4, dtype=torch.float32, device=dev).uniform_()
     dst = torch.empty_like(src)
@@ -492,7 +499,7 @@ def gather_ceiling(L, torch, dev, stream, nnz, call_s):
     with the probe kernel (liblhpc_probe.so, not part of the ABI), against the
     SpMV's own gathers per second."""
     import ctypes as C
-    P = C.CDLL(os.path.join(os.path.dirname(L.LIB_PATH), "liblhpc_probe.so"))
+    P = C.CDLL(probe_lib_path(L))
     m = int(nnz)
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED0007)

@@ -202,7 +202,13 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
         const K kk = sk[p];
         const uint32_t d = digit_of(kk, shift, mask);
         const uint32_t g = gbase[d] + (static_cast<uint32_t>(p) - tstart[d]);
+#if defined(LHPC_SORT_PROBE) && LHPC_SORT_PROBE == 1
+        // timing-only probe (wrong results): coalesced stores at the input
+        // position instead of the digit-run scatter
+        kout[base + p] = kk + static_cast<K>(g & 0u);
+#else
         kout[g] = kk;
+#endif
         if constexpr (HAS_V) vout[g] = sv[p];
       }
     }
