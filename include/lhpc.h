@@ -157,7 +157,7 @@ typedef struct lhpc_options {
   /* XTILE */
   int32_t xtile_reduce;         /* enum lhpc_xtile_reduce                        */
   int32_t xtile_ranges;         /* 1: one range; K ≥ 2: K cache-sized row ranges */
-  int32_t xtile_steps;          /* gather steps in flight: 2, 4, 8 (auto), 16    */
+  int32_t xtile_steps;          /* gather steps in flight: 2, 4, 8 (auto), 16 (fp32; fp64 caps at 8) */
   int32_t xtile_store;          /* xg stores: LHPC_STORE_PLAIN / _NT             */
   int32_t xtile_cut;            /* chunk-cut window in nonzeros (0: M/32)        */
   int32_t xtile_align;          /* enum lhpc_xtile_align                         */

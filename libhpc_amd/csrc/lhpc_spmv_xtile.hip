@@ -657,7 +657,7 @@ int xtile_g(int S) {
 
 template <typename T, int G, bool IP, bool AL>
 const void *xtile_reduce_fn() {
-  if constexpr (G > xt_gmax<T>() || (AL && !IP))
+  if constexpr (G > xt_gmax<T>() || (AL && !IP) || (AL && G > 4))  // AL at G = 8 spilled (build_t avoids it)
     return nullptr;
   else
     return reinterpret_cast<const void *>(k_xtile_reduce<T, G, xt_red_blk<T>(), IP, AL>);
@@ -692,7 +692,10 @@ int launch_gather(const lhpc_spmv_plan *p, const void *x, hipStream_t s, int64_t
   switch (p->xt_u) {
     case 2: gather_u<T, 2>(p, x, q0, q1, s); break;
     case 4: gather_u<T, 4>(p, x, q0, q1, s); break;
-    case 16: gather_u<T, 16>(p, x, q0, q1, s); break;
+    case 16:  // fp64 at 16 steps needs > 128 VGPRs (it spilled 22): capped at 8
+      if constexpr (sizeof(T) == 8) gather_u<T, 8>(p, x, q0, q1, s);
+      else gather_u<T, 16>(p, x, q0, q1, s);
+      break;
     default: gather_u<T, 8>(p, x, q0, q1, s); break;
   }
   return check_launch(s);
@@ -761,6 +764,9 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   if (al && (!ip || (stream_max + (VW - 1) * std::min<int64_t>(p->nnz, n_tiles * (p->nnz / (M / 2) + 2))) *
                                 static_cast<int64_t>(tsz) >= (int64_t{1} << 31)))
     al = false;
+  // the fp32 aligned reduce with 8 segment-table entries per thread (S > 2048
+  // tiles, n_cols > 84M) would spill a VGPR: packed segments there
+  if (al && xtile_g<T>(static_cast<int>(std::min<int64_t>(n_tiles, 4096))) > 4) al = false;
   p->xt_al = al ? 1 : 0;
   // chunk cuts: at the last row start in the back M/32 of the window, else
   // mid-row (the row's pieces meet in k_xtile_fixup).  Per-chunk costs are
