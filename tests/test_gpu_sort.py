@@ -199,7 +199,10 @@ def test_coo_to_csr_poisoned_pool(lhpc, gpu, poison):
     import ctypes as C
     import os
     import torch
-    P = C.CDLL(os.path.join(os.path.dirname(lhpc.LIB_PATH), "liblhpc_probe.so"))
+    probe = os.path.join(os.path.dirname(lhpc.LIB_PATH), "liblhpc_probe.so")
+    if not os.path.exists(probe):  # an A/B build ships only liblhpc.so
+        probe = os.path.join(os.path.dirname(lhpc.__file__), "_lib", "liblhpc_probe.so")
+    P = C.CDLL(probe)
     P.lhpc_probe_poison_pool.argtypes = [C.c_int64, C.c_int, C.c_void_p]
     st = torch.cuda.current_stream(gpu)
     cases = [(3, 3, np.array([0, 1, 0, 2]), np.array([0, 0, 1, 2]), np.array([2.0, -1.5, -1.5, 4.0]))]
