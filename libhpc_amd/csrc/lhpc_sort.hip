@@ -36,6 +36,17 @@ namespace {
 constexpr int kSortThreads = 256;
 constexpr int kSortMaxResident = 2048;  // resident-block cap (and fallback if occupancy query fails)
 
+// a & ~(b ^ c) as one gfx950 v_bitop3 (LUT index = a·4 + b·2 + c: rows 4
+// and 7).  Device pass only: the host pass's check of the builtin would drop
+// the kernels' host stubs (see lhpc_spmv_xtile.hip, aligned segments)
+__device__ __forceinline__ uint32_t and_xnor(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x90);
+#else
+  return a & ~(b ^ c);
+#endif
+}
+
 template <typename K>
 __device__ __forceinline__ uint32_t digit_of(K k, int shift, uint32_t mask) {
   return static_cast<uint32_t>(k >> shift) & mask;
@@ -165,12 +176,19 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const uint32_t d = digit_of(key[i], shift, mask);
-      uint64_t peers = ~uint64_t{0};
+      // match-any: lanes whose digit equals mine, one ballot per digit bit.
+      // dm = 0 / all-ones from the bit (one signed bitfield extract), and the
+      // mask update peers &= ~(ballot ^ dm) is one 3-input bitop per half
+      // (gfx950 v_bitop3): 4 VALU per bit instead of 7
+      uint32_t plo = ~0u, phi = ~0u;
 #pragma unroll
       for (int bit = 0; bit < 8; ++bit) {
-        const uint64_t bal = __ballot((d >> bit) & 1u);
-        peers &= ((d >> bit) & 1u) ? bal : ~bal;
+        const uint32_t dm = static_cast<uint32_t>(static_cast<int32_t>(d << (31 - bit)) >> 31);
+        const uint64_t bal = __ballot(dm);
+        plo = and_xnor(plo, static_cast<uint32_t>(bal), dm);
+        phi = and_xnor(phi, static_cast<uint32_t>(bal >> 32), dm);
       }
+      const uint64_t peers = (static_cast<uint64_t>(phi) << 32) | plo;
       const uint64_t below = peers & lt_mask;
       const uint32_t before = wcnt[w][d];
       loc[i] = before + static_cast<uint32_t>(__popcll(below));
