@@ -731,7 +731,9 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         per = float(tt.item())
     spmv_b = nnz * (8 + 4) + (n + 1) * 4 + 2 * n * 8
-    vec_b = 11 * n * 8  # p·q (2n), x/r update (read 4n, write 2n), p update (read 2n, write n)
+    # p·q in the SpMV epilogue (w = p read again: n), r update (read r q, write r: 3n),
+    # x/p update (read x p r, write x p: 5n) — k_cg_r + k_cg_xp
+    vec_b = 9 * n * 8
     alg = (spmv_b + vec_b) / world
     out = dict(metric="CG iterations/s, 2-D Laplacian 4096^2 fp64 (SURVEY 8f rank 3)", value=1.0 / per,
                unit="iter/s", n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=per * 1e3,
@@ -739,7 +741,7 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
                data="synthetic: 5-point Laplacian, b = U[-1,1) (SEED_X)",
                config={"workload": f"CG, 2-D Laplacian {nx}^2 fp64, n={n}, nnz={nnz}, {world} GPU(s)",
                        "iterations": it, "relres": res, "kernel": plan.info()["kernel"]},
-               roofline={"bound": "hbm", "kernel": "spmv + k_dot_partial/k_cg_xr/k_cg_p",
+               roofline={"bound": "hbm", "kernel": "spmv_dot + k_cg_r + k_cg_xp",
                          "achieved": alg / per / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": alg / per / 1e9 / HBM_PEAK_GBPS, "traffic": None,
                          "alg_bytes_per_iter": alg})

@@ -390,6 +390,11 @@ int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
  *   lhpc_vec_dot     *out = a·b
  *   lhpc_cg_step_xr  α = *alpha_num / *alpha_den; x += α·p; r -= α·q; *rr_out = r·r
  *   lhpc_cg_step_p   β = *beta_num / *beta_den; p = r + β·p
+ *   lhpc_cg_step_r   α = *alpha_num / *alpha_den; r -= α·q; *rr_out = r·r
+ *   lhpc_cg_step_xp  α as above, β = *beta_num / *beta_den; x += α·p; then
+ *                    p = r + β·p in the same pass (beta_num NULL: x only).
+ *                    step_r + step_xp = step_xr + step_p with one vector
+ *                    pass less, bit-identical results.
  */
 /* y = A·x and *dot_out = w·y (fp64, the stored y) in one pass for ADAPTIVE
  * plans (the CG p·q fused into the SpMV epilogue; fixed-order reduction),
@@ -407,6 +412,13 @@ int lhpc_cg_step_xr(int dtype, int64_t n, const double *alpha_num,
 int lhpc_cg_step_p(int dtype, int64_t n, const double *beta_num,
                    const double *beta_den, const void *r, void *p,
                    void *stream);
+int lhpc_cg_step_r(int dtype, int64_t n, const double *alpha_num,
+                   const double *alpha_den, void *r, const void *q,
+                   double *rr_out, void *stream);
+int lhpc_cg_step_xp(int dtype, int64_t n, const double *alpha_num,
+                    const double *alpha_den, const double *beta_num,
+                    const double *beta_den, void *x, void *p, const void *r,
+                    void *stream);
 
 /* ------------------------------------------------------------------- I/O
  * SURVEY §8f rank 4 (the reference has no file formats).  Host-only.

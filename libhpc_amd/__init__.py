@@ -58,7 +58,7 @@ ABI_SYMBOLS = (
     "lhpc_row_ptr_narrow", "lhpc_radix_sort_u32", "lhpc_radix_sort_pairs_u32",
     "lhpc_radix_sort_pairs_u64", "lhpc_coo_to_csr", "lhpc_csr_save", "lhpc_csr_load_header",
     "lhpc_csr_load", "lhpc_mm_read_header", "lhpc_mm_read_coo", "lhpc_cg_solve", "lhpc_vec_dot",
-    "lhpc_cg_step_xr", "lhpc_cg_step_p", "lhpc_spmv_dot",
+    "lhpc_cg_step_xr", "lhpc_cg_step_p", "lhpc_cg_step_r", "lhpc_cg_step_xp", "lhpc_spmv_dot",
     "lhpc_spmv_plan_create_split", "lhpc_spmv_stage", "lhpc_spmv_range",
     "lhpc_dist_get_unique_id", "lhpc_dist_comm_create", "lhpc_dist_comm_info", "lhpc_dist_comm_destroy",
     "lhpc_dist_allreduce_sum_f64", "lhpc_dist_spmv_plan_create", "lhpc_dist_spmv",
@@ -195,6 +195,8 @@ _sig("lhpc_vec_dot", _i, _i, _i64, _p, _p, _p, _p)
 _sig("lhpc_spmv_dot", _i, _p, _p, _p, _p, _p, _p)
 _sig("lhpc_cg_step_xr", _i, _i, _i64, _p, _p, _p, _p, _p, _p, _p, _p)
 _sig("lhpc_cg_step_p", _i, _i, _i64, _p, _p, _p, _p, _p)
+_sig("lhpc_cg_step_r", _i, _i, _i64, _p, _p, _p, _p, _p, _p)
+_sig("lhpc_cg_step_xp", _i, _i, _i64, _p, _p, _p, _p, _p, _p, _p, _p)
 _sig("lhpc_csr_save", _i, C.c_char_p, _i, _i64, _i64, _i64, _p, _i, _p, _p)
 _sig("lhpc_csr_load_header", _i, C.c_char_p, C.POINTER(_i), C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64),
      C.POINTER(_i))
@@ -701,6 +703,23 @@ def cg_step_p(beta_num, beta_den, r, p, stream=None):
     st = _dev_stream(r, stream)
     _check(lib.lhpc_cg_step_p(_dtype_code(r), _numel(r), beta_num.data_ptr(), beta_den.data_ptr(), r.data_ptr(),
                               p.data_ptr(), _stream_ptr(st)), "lhpc_cg_step_p")
+
+
+def cg_step_r(alpha_num, alpha_den, r, q, rr_out, stream=None):
+    """r -= α·q, rr_out = r·r (α = alpha_num/alpha_den, fp64 device scalars)."""
+    st = _dev_stream(r, stream)
+    _check(lib.lhpc_cg_step_r(_dtype_code(r), _numel(r), alpha_num.data_ptr(), alpha_den.data_ptr(), r.data_ptr(),
+                              q.data_ptr(), rr_out.data_ptr(), _stream_ptr(st)), "lhpc_cg_step_r")
+
+
+def cg_step_xp(alpha_num, alpha_den, beta_num, beta_den, x, p, r, stream=None):
+    """x += α·p, then p = r + β·p in the same pass; beta_num None: x only."""
+    st = _dev_stream(x, stream)
+    bn = beta_num.data_ptr() if beta_num is not None else None
+    bd = beta_den.data_ptr() if beta_den is not None else None
+    rp = r.data_ptr() if r is not None else None
+    _check(lib.lhpc_cg_step_xp(_dtype_code(x), _numel(x), alpha_num.data_ptr(), alpha_den.data_ptr(), bn, bd,
+                               x.data_ptr(), p.data_ptr(), rp, _stream_ptr(st)), "lhpc_cg_step_xp")
 
 
 def gen_laplacian_2d(nx: int, ny: int, dtype=F64, shift: float = 0.0):

@@ -6,9 +6,11 @@
 // Per iteration (HBM-bound vector work around one SpMV):
 //   q = A·p, pq = p·q               lhpc_spmv_dot (fused into the ADAPTIVE epilogue;
 //                                   SpMV + k_dot_partial/k_dot_finish for other plans)
-//   α = rr/pq; x += α·p; r -= α·q;  k_cg_xr (one pass: reads x p r q, writes x r,
-//   rr' = r·r                         block partials of rr') + k_dot_finish
-//   β = rr'/rr; p = r + β·p         k_cg_p
+//   α = rr/pq; r -= α·q; rr' = r·r  k_cg_r (reads r q, writes r, block partials) + k_dot_finish
+//   β = rr'/rr; x += α·p;           k_cg_xp (reads x p r, writes x p)
+//   p = r + β·p
+// (k_cg_xr / k_cg_p, the x update beside the r update, stay as building
+// blocks of the C ABI.)
 // α and β are read on the device from fp64 scalars, so no host round trip is
 // needed between kernels; the host reads rr' only every `check_every`
 // iterations to test convergence.  Dots accumulate in fp64 with a fixed
@@ -91,6 +93,45 @@ __global__ __launch_bounds__(kVecThreads) void k_cg_p(const T *__restrict__ r, T
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kVecThreads + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * kVecThreads)
     p[i] = r[i] + beta * p[i];
+}
+
+// The x update moved next to the p update (k_cg_r + k_cg_xp replace
+// k_cg_xr + k_cg_p): r -= α·q with rr' = r·r reads r, q and writes r; then
+// x += α·p, p = r + β·p reads x, p, r and writes x, p — eight vector passes
+// per iteration instead of nine, the same operations on the same values
+// (bit-identical x, r, p).  β = null: x += α·p only (the last iteration).
+template <typename T>
+__global__ __launch_bounds__(kVecThreads) void k_cg_r(T *__restrict__ r, const T *__restrict__ q, int64_t n,
+                                                      const double *__restrict__ num,
+                                                      const double *__restrict__ den, double *__restrict__ part) {
+  __shared__ double sh[kVecThreads / kWave];
+  const T a = static_cast<T>(*num / *den);
+  double s = 0.0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kVecThreads + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * kVecThreads) {
+    const T ri = r[i] - a * q[i];
+    r[i] = ri;
+    s += static_cast<double>(ri) * static_cast<double>(ri);
+  }
+  const double t = block_sum(s, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+template <typename T, bool P>
+__global__ __launch_bounds__(kVecThreads) void k_cg_xp(T *__restrict__ x, T *__restrict__ p,
+                                                       const T *__restrict__ r, int64_t n,
+                                                       const double *__restrict__ anum,
+                                                       const double *__restrict__ aden,
+                                                       const double *__restrict__ bnum,
+                                                       const double *__restrict__ bden) {
+  const T a = static_cast<T>(*anum / *aden);
+  const T beta = P ? static_cast<T>(*bnum / *bden) : T(0);
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kVecThreads + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * kVecThreads) {
+    const T pi = p[i];
+    x[i] = x[i] + a * pi;
+    if constexpr (P) p[i] = r[i] + beta * pi;
+  }
 }
 
 // r = b - q, p = r, part = block partials of r·r
@@ -186,6 +227,56 @@ extern "C" int lhpc_cg_step_p(int dtype, int64_t n, const double *beta_num, cons
   return check_launch(s);
 }
 
+extern "C" int lhpc_cg_step_r(int dtype, int64_t n, const double *alpha_num, const double *alpha_den, void *r,
+                              const void *q, double *rr_out, void *stream) {
+  if (!dtype_ok(dtype) || n < 0 || !alpha_num || !alpha_den || !rr_out || (n > 0 && (!r || !q)))
+    return LHPC_ERR_INVALID_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  Scratch part;
+  part.s = s;
+  LHPC_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
+  const int g = vec_grid(n);
+  if (dtype == LHPC_F32)
+    hipLaunchKernelGGL((k_cg_r<float>), dim3(g), dim3(kVecThreads), 0, s, static_cast<float *>(r),
+                       static_cast<const float *>(q), n, alpha_num, alpha_den, part.d);
+  else
+    hipLaunchKernelGGL((k_cg_r<double>), dim3(g), dim3(kVecThreads), 0, s, static_cast<double *>(r),
+                       static_cast<const double *>(q), n, alpha_num, alpha_den, part.d);
+  hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(kVecThreads), 0, s, part.d, g, rr_out);
+  return check_launch(s);
+}
+
+extern "C" int lhpc_cg_step_xp(int dtype, int64_t n, const double *alpha_num, const double *alpha_den,
+                               const double *beta_num, const double *beta_den, void *x, void *p, const void *r,
+                               void *stream) {
+  const bool up = beta_num != nullptr;
+  if (!dtype_ok(dtype) || n < 0 || !alpha_num || !alpha_den || (up && !beta_den) ||
+      (n > 0 && (!x || !p || (up && !r))))
+    return LHPC_ERR_INVALID_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int g = vec_grid(n);
+  if (dtype == LHPC_F32) {
+    float *xf = static_cast<float *>(x), *pf = static_cast<float *>(p);
+    const float *rf = static_cast<const float *>(r);
+    if (up)
+      hipLaunchKernelGGL((k_cg_xp<float, true>), dim3(g), dim3(kVecThreads), 0, s, xf, pf, rf, n, alpha_num,
+                         alpha_den, beta_num, beta_den);
+    else
+      hipLaunchKernelGGL((k_cg_xp<float, false>), dim3(g), dim3(kVecThreads), 0, s, xf, pf, rf, n, alpha_num,
+                         alpha_den, beta_num, beta_den);
+  } else {
+    double *xd = static_cast<double *>(x), *pd = static_cast<double *>(p);
+    const double *rd = static_cast<const double *>(r);
+    if (up)
+      hipLaunchKernelGGL((k_cg_xp<double, true>), dim3(g), dim3(kVecThreads), 0, s, xd, pd, rd, n, alpha_num,
+                         alpha_den, beta_num, beta_den);
+    else
+      hipLaunchKernelGGL((k_cg_xp<double, false>), dim3(g), dim3(kVecThreads), 0, s, xd, pd, rd, n, alpha_num,
+                         alpha_den, beta_num, beta_den);
+  }
+  return check_launch(s);
+}
+
 extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int max_iter,
                              int check_every, int *iters_out, double *resid_out, void *stream) {
   lhpc_spmv_plan_info info{};
@@ -246,7 +337,7 @@ extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, doubl
   if (h_rr > stop) {
     for (it = 1; it <= max_iter; ++it) {
       LHPC_TRY(lhpc_spmv_dot(plan, p, q, p, pq, s));  // q = A·p and p·q in one pass (ADAPTIVE)
-      LHPC_TRY(lhpc_cg_step_xr(dtype, n, rr[cur], pq, x, p, r, q, rr[cur ^ 1], s));
+      LHPC_TRY(lhpc_cg_step_r(dtype, n, rr[cur], pq, r, q, rr[cur ^ 1], s));
       if (it % check_every == 0 || it == max_iter) {
         LHPC_HIP_TRY(hipMemcpyAsync(&h_rr, rr[cur ^ 1], 8, hipMemcpyDeviceToHost, s));
         LHPC_HIP_TRY(hipStreamSynchronize(s));
@@ -254,9 +345,13 @@ extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, doubl
           status = LHPC_ERR_INTERNAL;  // breakdown (p·Ap = 0 or overflow): matrix not SPD?
           break;
         }
-        if (h_rr <= stop) break;
+        if (h_rr <= stop) {
+          LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[cur], pq, nullptr, nullptr, x, p, nullptr, s));  // x += α·p
+          break;
+        }
       }
-      LHPC_TRY(lhpc_cg_step_p(dtype, n, rr[cur ^ 1], rr[cur], r, p, s));
+      // x += α·p, then p = r + β·p (same pass)
+      LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[cur], pq, rr[cur ^ 1], rr[cur], x, p, r, s));
       cur ^= 1;
     }
     if (it > max_iter) it = max_iter;

@@ -268,6 +268,14 @@ class HipOps:
         from . import cg_step_p
         cg_step_p(num, den, r, p, stream=self.stream)
 
+    def step_r(self, num, den, r, q, rr_out):
+        from . import cg_step_r
+        cg_step_r(num, den, r, q, rr_out, stream=self.stream)
+
+    def step_xp(self, anum, aden, bnum, bden, x, p, r):
+        from . import cg_step_xp
+        cg_step_xp(anum, aden, bnum, bden, x, p, r, stream=self.stream)
+
 
 class TorchCPUOps:
     """The same building blocks on CPU tensors — for the gloo tests of the
@@ -286,6 +294,17 @@ class TorchCPUOps:
     def step_p(self, num, den, r, p):
         beta = (num / den).to(p.dtype)
         p.mul_(beta).add_(r)
+
+    def step_r(self, num, den, r, q, rr_out):
+        a = (num / den).to(r.dtype)
+        r.sub_(a * q)
+        self.dot(r, r, rr_out)
+
+    def step_xp(self, anum, aden, bnum, bden, x, p, r):
+        a = (anum / aden).to(x.dtype)
+        x.add_(a * p)
+        if bnum is not None:
+            self.step_p(bnum, bden, r, p)
 
 
 class DistCG:
@@ -360,15 +379,18 @@ class DistCG:
                     self.fn(self.p_full[:n], self.q)
                     self.ops.dot(self.p, self.q, pq)
                 self._allreduce(pq)
-                self.ops.step_xr(rr[cur], pq, x, self.p, self.r, self.q, rr[cur ^ 1])
+                # r -= α·q, rr' = r·r; the x update rides with the p update
+                # (one vector pass less; lhpc_cg_step_r / lhpc_cg_step_xp)
+                self.ops.step_r(rr[cur], pq, self.r, self.q, rr[cur ^ 1])
                 self._allreduce(rr[cur ^ 1])
                 if it % check_every == 0 or it == max_iter:
                     h_rr = float(rr[cur ^ 1].item())
                     if not np.isfinite(h_rr):
                         raise FloatingPointError("DistCG: breakdown (non-finite residual)")
                     if h_rr <= stop:
+                        self.ops.step_xp(rr[cur], pq, None, None, x, self.p, None)
                         break
-                self.ops.step_p(rr[cur ^ 1], rr[cur], self.r, self.p)
+                self.ops.step_xp(rr[cur], pq, rr[cur ^ 1], rr[cur], x, self.p, self.r)
                 self._gather(self.p_full, self.p)
                 cur ^= 1
         res = float(np.sqrt(max(h_rr, 0.0)) / np.sqrt(h_bb if h_bb > 0 else 1.0))

@@ -91,6 +91,34 @@ def test_cg_building_blocks(lhpc, gpu):
         assert np.array_equal(pd.cpu().numpy(), (rw + al * p).astype(dt))
 
 
+def test_cg_fused_steps_match_separate(lhpc, gpu):
+    """lhpc_cg_step_r + lhpc_cg_step_xp (the solver's fused pair) leave x, r,
+    p and r·r bit-identical to lhpc_cg_step_xr + lhpc_cg_step_p; β = NULL
+    updates x only."""
+    import torch
+    rng = np.random.default_rng(8)
+    n = 777_777
+    for dt in (np.float64, np.float32):
+        x, p, r, q = (rng.uniform(-1, 1, n).astype(dt) for _ in range(4))
+        an = torch.tensor([0.3], dtype=torch.float64, device=gpu)
+        ad = torch.tensor([1.7], dtype=torch.float64, device=gpu)
+        bd_ = torch.tensor([2.9], dtype=torch.float64, device=gpu)
+        x1, p1, r1, q1 = (_dev(gpu, v) for v in (x, p, r, q))
+        x2, p2, r2, q2 = (_dev(gpu, v) for v in (x, p, r, q))
+        rr1 = torch.zeros(1, dtype=torch.float64, device=gpu)
+        rr2 = torch.zeros(1, dtype=torch.float64, device=gpu)
+        lhpc.cg_step_xr(an, ad, x1, p1, r1, q1, rr1)
+        lhpc.cg_step_p(rr1, bd_, r1, p1)
+        lhpc.cg_step_r(an, ad, r2, q2, rr2)
+        lhpc.cg_step_xp(an, ad, rr2, bd_, x2, p2, r2)
+        for u, v in ((x1, x2), (p1, p2), (r1, r2), (rr1, rr2)):
+            assert torch.equal(u, v)
+        x3, p3 = _dev(gpu, x), _dev(gpu, p)
+        lhpc.cg_step_xp(an, ad, None, None, x3, p3, None)
+        al = dt(0.3 / 1.7)
+        assert np.array_equal(x3.cpu().numpy(), (x + al * p).astype(dt)) and np.array_equal(p3.cpu().numpy(), p)
+
+
 def test_dist_cg_hip_ops_world1(lhpc, gpu):
     """The multi-GPU solver's data path at world 1 (HipOps, padded block plan)
     converges to the same solution as lhpc_cg_solve."""
