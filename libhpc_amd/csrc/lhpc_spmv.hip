@@ -213,8 +213,16 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
     if (p->kernel == LHPC_KERNEL_ADAPTIVE) {
       std::vector<int64_t> b = csr_build_blocks(rp, n_rows, p->n_long);
       p->n_blocks = static_cast<int64_t>(b.size()) - 1;
-      if ((st = dmalloc(reinterpret_cast<void **>(&p->d_blocks), b.size() * 8, p->bytes))) break;
-      if ((st = static_cast<int>(hipMemcpy(p->d_blocks, b.data(), b.size() * 8, hipMemcpyHostToDevice))))
+      // device table: {first row, its row_ptr} per block boundary, so a block
+      // reads its row and nonzero range with one 32-B load (no dependent
+      // row_ptr round trip)
+      std::vector<int64_t> bp(2 * b.size());
+      for (size_t k = 0; k < b.size(); ++k) {
+        bp[2 * k] = b[k];
+        bp[2 * k + 1] = rp[b[k]];
+      }
+      if ((st = dmalloc(reinterpret_cast<void **>(&p->d_blocks), bp.size() * 8, p->bytes))) break;
+      if ((st = static_cast<int>(hipMemcpy(p->d_blocks, bp.data(), bp.size() * 8, hipMemcpyHostToDevice))))
         break;
     }
   } while (false);

@@ -91,7 +91,8 @@ __global__ __launch_bounds__(kBlock) void k_spmv_rowgroup(
 }
 
 // ------------------------------------------------------------- ADAPTIVE
-// blocks[b] = first row of block b; blocks[n_blocks] = n_rows.
+// blocks[2b] = first row of block b, blocks[2b + 1] = its row_ptr;
+// blocks[2·n_blocks] = n_rows, blocks[2·n_blocks + 1] = nnz.
 template <typename T, typename I>
 __global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
     const I *__restrict__ row_ptr, const int32_t *__restrict__ col,
@@ -102,10 +103,9 @@ __global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
   __shared__ double prod[kBlockNnz];
   __shared__ double wsum[kBlock / kWave];
   const int tid = threadIdx.x;
-  const int64_t r0 = blocks[blockIdx.x];
-  const int64_t r1 = blocks[blockIdx.x + 1];
-  const int64_t base = row_ptr[r0];
-  const int64_t cnt = static_cast<int64_t>(row_ptr[r1]) - base;
+  const int64_t r0 = blocks[2 * blockIdx.x], base = blocks[2 * blockIdx.x + 1];
+  const int64_t r1 = blocks[2 * blockIdx.x + 2];
+  const int64_t cnt = blocks[2 * blockIdx.x + 3] - base;
   const int64_t nrows = r1 - r0;
 
   if (cnt > kBlockNnz) {
@@ -127,6 +127,19 @@ __global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
     }
     return;
   }
+  // the reduce's row bounds (and the dot's w) are loaded with the stream,
+  // not after the barrier: L lanes per row, L = the largest power of two
+  // with nrows·L ≤ 256
+  int L = kWave;
+  while (L > 1 && nrows * L > kBlock) L >>= 1;
+  const int grp = tid / L, sub = tid & (L - 1);
+  int64_t rs = 0, re = 0;
+  T wv = T(0);
+  if (grp < nrows) {
+    rs = static_cast<int64_t>(row_ptr[r0 + grp]) - base;
+    re = static_cast<int64_t>(row_ptr[r0 + grp + 1]) - base;
+    if (w && sub == 0) wv = w[r0 + grp];
+  }
   // stream phase: every thread products kBlockNnz/kBlock nonzeros
   constexpr int PER = kBlockNnz / kBlock;
   int32_t c[PER];
@@ -147,17 +160,10 @@ __global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
     if (c[i] >= 0) prod[k] = static_cast<double>(v[i]) * static_cast<double>(x[c[i]]);
   }
   __syncthreads();
-  // reduce: L lanes per row, L = largest power of two with nrows*L <= 256
-  int L = kWave;
-  while (L > 1 && nrows * L > kBlock) L >>= 1;
-  const int grp = tid / L, sub = tid & (L - 1);
+  // reduce: L lanes per row
   double a = 0.0;
-  int64_t rs = 0, re = 0;
-  if (grp < nrows) {
-    rs = static_cast<int64_t>(row_ptr[r0 + grp]) - base;
-    re = static_cast<int64_t>(row_ptr[r0 + grp + 1]) - base;
+  if (grp < nrows)
     for (int64_t k = rs + sub; k < re; k += L) a += prod[k];
-  }
   switch (L) {  // block-uniform
     case 64: a = group_sum<64>(a); break;
     case 32: a = group_sum<32>(a); break;
@@ -171,7 +177,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
   if (grp < nrows && sub == 0) {
     const T yv = static_cast<T>(a);
     y[r0 + grp] = yv;
-    if (w) d = static_cast<double>(yv) * static_cast<double>(w[r0 + grp]);
+    if (w) d = static_cast<double>(yv) * static_cast<double>(wv);
   }
   if (w) {  // block-uniform
     d = group_sum<kWave>(d);
