@@ -40,13 +40,13 @@ template <> struct XtTile<double> { static constexpr int W = 20480; };  // 160 K
 template <typename T, int U, bool NT = false>
 __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
     const int32_t *__restrict__ pieces, const uint16_t *__restrict__ col16,
-    const T *__restrict__ x, int64_t n_cols, T *__restrict__ xg) {
-  constexpr int W = XtTile<T>::W;
+    const T *__restrict__ x, int64_t n_cols, int tw, T *__restrict__ xg) {
+  constexpr int W = XtTile<T>::W;  // LDS capacity; the plan's tile width tw ≤ W
   __shared__ T xt[W];
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int g0 = pieces[3 * blockIdx.x], g1 = pieces[3 * blockIdx.x + 1];
-  const int64_t c0 = static_cast<int64_t>(pieces[3 * blockIdx.x + 2]) * W;
-  const int wlen = static_cast<int>((n_cols - c0) < W ? (n_cols - c0) : W);
+  const int64_t c0 = static_cast<int64_t>(pieces[3 * blockIdx.x + 2]) * tw;
+  const int wlen = static_cast<int>((n_cols - c0) < tw ? (n_cols - c0) : tw);
   constexpr int PT = W / kXtGatherBlock;
   const int q0 = g0 >> 3, q1 = g1 >> 3;  // 8-entry groups
   const u32x4 *cv = reinterpret_cast<const u32x4 *>(col16);
@@ -677,7 +677,8 @@ const void *xtile_reduce_fn(int g, bool ip, bool al) {
 template <typename T, int U, bool NT = false>
 void gather_u(const lhpc_spmv_plan *p, const void *x, int64_t q0, int64_t q1, hipStream_t s) {
   hipLaunchKernelGGL((k_xtile_gather<T, U, NT>), dim3(static_cast<unsigned>(q1 - q0)), dim3(kXtGatherBlock), 0, s,
-                     p->d_pieces + 3 * q0, p->d_col16, static_cast<const T *>(x), p->n_cols, static_cast<T *>(p->d_xg));
+                     p->d_pieces + 3 * q0, p->d_col16, static_cast<const T *>(x), p->n_cols,
+                     static_cast<int>(p->xs_width), static_cast<T *>(p->d_xg));
 }
 
 // gather pieces [q0, q1) (default: all)
@@ -731,11 +732,22 @@ int launch_reduce(const lhpc_spmv_plan *p, int64_t c0, int64_t c1, int64_t n0, i
 template <typename T>
 int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val) {
   constexpr size_t tsz = sizeof(T);
-  constexpr int64_t W = XtTile<T>::W;
   constexpr int M = XtRed<T, xt_red_blk<T>()>::M, RMAX = XtRed<T, xt_red_blk<T>()>::Rmax, RUN = xt_run<T>();
   int cus = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, p->device) == hipSuccess) cus = prop.multiProcessorCount;
+  // tile width: the LDS capacity XtTile<T>::W, narrowed for fp32 so that the
+  // tile count is a whole multiple of the CUs when that adds ≤ 10% tiles
+  // (C2: 245 → 256 tiles of 39063 columns): a cache-sized range's gather
+  // round of one piece per tile then fills every CU.  fp64 (single range,
+  // ≈ 2 pieces per CU) lost 3% with it (C3 489 → 512 tiles: 0.913 → 0.941 ms)
+  int64_t W = XtTile<T>::W;
+  {
+    const int64_t s0 = (p->n_cols + W - 1) / W, s1 = (s0 + cus - 1) / cus * cus;
+    bool narrow = sizeof(T) == 4 && s1 * 10 <= s0 * 11;
+    if (const char *e = tuning_env("LHPC_XTILE_TW")) narrow = std::atoi(e) != 0;
+    if (narrow && s1 > s0) W = (p->n_cols + s1 - 1) / s1;
+  }
   // ≈ 2 gather workgroups per CU (one resident per CU: 160 KB of LDS each)
   // and ≥ 4 tiles' worth of stream per piece, so the tile load (W·T bytes)
   // stays ≤ 1/4 of a piece's col16 + xg traffic on small (per-rank) matrices

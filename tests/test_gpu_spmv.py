@@ -166,7 +166,9 @@ def test_xtile_large_n_80m(lhpc, gpu):
     x = lhpc.gen_values(lhpc.F32, 1, n, 0x8001)
     with lhpc.SpMVPlan(rp, col, val, n) as plan:
         info = plan.info()
-        assert info["kernel"] == lhpc.KERNEL_XTILE and info["slices"] == -(-n // 40960)
+        # tiles of ≤ 40960 columns (narrowed to a whole multiple of the CUs: 2048 x 39063)
+        assert info["kernel"] == lhpc.KERNEL_XTILE and info["slice_width"] <= 40960
+        assert info["slices"] == -(-n // info["slice_width"]) and info["slices"] >= -(-n // 40960)
         xd = torch.from_numpy(x).to(gpu)
         y1 = plan(xd).clone()
         y2 = plan(xd)
