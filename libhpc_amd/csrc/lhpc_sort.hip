@@ -606,9 +606,13 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
 }
 }  // namespace
 
+// keys-only: 8192-key sub-tiles (32 keys per thread, 246 VGPRs, 2 waves per
+// SIMD): digit runs twice as long, so the scatter writes whole 128-B lines,
+// and half the per-sub-tile scans and barriers per key — same box, three runs
+// each, 500M keys 8.92 → 7.68 ms against 4096-key sub-tiles
 extern "C" int lhpc_radix_sort_u32(uint32_t *keys, int64_t n, int begin_bit, int end_bit, int on_device,
                                    void *stream) {
-  return sort_entry<uint32_t, false, 16>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
+  return sort_entry<uint32_t, false, 32>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
 }
 
 extern "C" int lhpc_radix_sort_pairs_u32(uint32_t *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit,
