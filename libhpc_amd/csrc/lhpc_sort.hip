@@ -158,7 +158,7 @@ __device__ __forceinline__ uint64_t match_any8(uint32_t d) {
 // base of digit t lives in thread t's register; full sub-tiles load and store
 // without bounds checks; one barrier fewer per sub-tile than reading two
 // offset tables (C2-sized sort, same box, three runs each: 9.04 → 8.91 ms).
-template <typename K, bool HAS_V, int IPT>
+template <typename K, bool HAS_V, int IPT, bool PF = true>
 __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const K *__restrict__ kin, K *__restrict__ kout, const uint32_t *__restrict__ vin, uint32_t *__restrict__ vout,
     int64_t n, int shift, uint32_t mask, int64_t per_block, const uint32_t *__restrict__ counts,
@@ -201,16 +201,21 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
       }
     }
   };
-  if (first < last) load_tile(first, key, val);
+  if (PF && first < last) load_tile(first, key, val);
   for (int64_t tile = first; tile < last; ++tile) {
     const int64_t base = tile * TILE;
     const bool full = base + TILE <= n;
 #pragma unroll
     for (int k = 0; k < 4; ++k) wcnt[w][lane + kWave * k] = 0;
-    // next sub-tile in flight under this one's rank / reorder / scatter
+    // PF: next sub-tile in flight under this one's rank / reorder / scatter;
+    // else this sub-tile is loaded here (other workgroups hide the wait)
     K nkey[IPT];
     uint32_t nval[IPT];
-    if (tile + 1 < last) load_tile(tile + 1, nkey, nval);
+    if constexpr (PF) {
+      if (tile + 1 < last) load_tile(tile + 1, nkey, nval);
+    } else {
+      load_tile(tile, key, val);
+    }
     uint32_t loc[IPT];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
@@ -263,10 +268,12 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
         if constexpr (HAS_V) vout[g] = sv[p];
       }
     }
+    if constexpr (PF) {
 #pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      key[i] = nkey[i];
-      if constexpr (HAS_V) val[i] = nval[i];
+      for (int i = 0; i < IPT; ++i) {
+        key[i] = nkey[i];
+        if constexpr (HAS_V) val[i] = nval[i];
+      }
     }
   }
 }
@@ -317,14 +324,14 @@ struct HostStage {
 };
 
 // resident downsweep blocks on this device (CUs × blocks per CU), cached per kernel
-template <typename K, bool HAS_V, int IPT>
+template <typename K, bool HAS_V, int IPT, bool PF>
 int64_t sort_grid_cap() {
   static int64_t cap = 0;
   if (!cap) {
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT>, kSortThreads, 0) !=
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT, PF>, kSortThreads, 0) !=
             hipSuccess ||
         cus <= 0 || per_cu <= 0)
       return kSortMaxResident;
@@ -333,7 +340,7 @@ int64_t sort_grid_cap() {
   return cap;
 }
 
-template <typename K, bool HAS_V, int IPT>
+template <typename K, bool HAS_V, int IPT, bool PF = true>
 int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, hipStream_t s) {
   if (n <= 1 || begin_bit >= end_bit) return LHPC_OK;
   constexpr int TILE = IPT * kSortThreads;
@@ -341,7 +348,7 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
   // Grid: up to 8 waves of resident blocks, but at least ~3 tiles per block. More, shorter blocks even out
   // the tail of the even-share split (500M keys: 768 blocks 8.94 ms, 6144 blocks 8.16 ms); below ~3 tiles
   // per block the per-block digit-count rows outweigh the gain (100M keys: 8192 blocks 1.89 ms, 30000 2.19).
-  const int64_t res = sort_grid_cap<K, HAS_V, IPT>();
+  const int64_t res = sort_grid_cap<K, HAS_V, IPT, PF>();
   // grid sweep knobs of the tuning build only (tools/explore_sort.py; lhpc_common.hpp tuning_env)
   static const int64_t waves = tuning_env("LHPC_SORT_WAVES") ? std::max(1, std::atoi(tuning_env("LHPC_SORT_WAVES"))) : 8;
   int64_t cap = std::min<int64_t>(waves * res, std::max<int64_t>(res, ntiles / 3));
@@ -364,7 +371,7 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
     hipLaunchKernelGGL((k_radix_upsweep<K, TILE>), dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0, s, kin,
                        n, shift, mask, per, cnt);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(kSortThreads), 0, s, cnt, static_cast<int>(nb), db);
-    hipLaunchKernelGGL((k_radix_downsweep<K, HAS_V, IPT>), dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0,
+    hipLaunchKernelGGL((k_radix_downsweep<K, HAS_V, IPT, PF>), dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0,
                        s, kin, kout, vin, vout, n, shift, mask, per, cnt, db);
     std::swap(kin, kout);
     if (HAS_V) std::swap(vin, vout);
@@ -549,7 +556,7 @@ int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *r
   if (nnz > 0) {
     hipLaunchKernelGGL((k_coo_keys<kBits>), dim3(g), dim3(256), 0, s, rows, cols,
                        reinterpret_cast<const uint32_t *>(vals), nnz, n_rows, n_cols, cb, kp, ip, bad);
-    LHPC_TRY((radix_sort_dev<uint64_t, true, 16>(kp, ip, nnz, 0, cb + rb, s)));
+    LHPC_TRY((radix_sort_dev<uint64_t, true, 32, false>(kp, ip, nnz, 0, cb + rb, s)));
     hipLaunchKernelGGL(k_coo_heads, dim3(g), dim3(256), 0, s, kp, nnz, hp);
     LHPC_TRY(exclusive_scan_u32(hp, pp, nnz, gp, s));
     hipLaunchKernelGGL((k_coo_emit<T, kBits>), dim3(g), dim3(256), 0, s, kp, ip, hp, pp, nnz, cb, vals, col_out,
@@ -582,7 +589,7 @@ int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *r
 using namespace lhpc;
 
 namespace {
-template <typename K, bool HAS_V, int IPT>
+template <typename K, bool HAS_V, int IPT, bool PF = true>
 int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, int on_device, void *stream) {
   constexpr int KB = static_cast<int>(sizeof(K) * 8);
   if (n < 0 || (!keys && n > 0) || (HAS_V && !vals && n > 0) || begin_bit < 0 || end_bit > KB ||
@@ -591,13 +598,13 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
   if (n >= (int64_t{1} << 32)) return LHPC_ERR_UNSUPPORTED;  // 32-bit ranks
   RocTxRange rx("lhpc_radix_sort");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (on_device) return radix_sort_dev<K, HAS_V, IPT>(keys, vals, n, begin_bit, end_bit, s);
+  if (on_device) return radix_sort_dev<K, HAS_V, IPT, PF>(keys, vals, n, begin_bit, end_bit, s);
   HostStage dk, dv;
   LHPC_HIP_TRY(dk.alloc(static_cast<size_t>(n) * sizeof(K)));
   if (HAS_V) LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(n) * 4));
   LHPC_HIP_TRY(hipMemcpy(dk.p, keys, static_cast<size_t>(n) * sizeof(K), hipMemcpyHostToDevice));
   if (HAS_V) LHPC_HIP_TRY(hipMemcpy(dv.p, vals, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice));
-  LHPC_TRY((radix_sort_dev<K, HAS_V, IPT>(static_cast<K *>(dk.p), static_cast<uint32_t *>(dv.p), n, begin_bit,
+  LHPC_TRY((radix_sort_dev<K, HAS_V, IPT, PF>(static_cast<K *>(dk.p), static_cast<uint32_t *>(dv.p), n, begin_bit,
                                           end_bit, s)));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
   LHPC_HIP_TRY(hipMemcpy(keys, dk.p, static_cast<size_t>(n) * sizeof(K), hipMemcpyDeviceToHost));
@@ -609,7 +616,10 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
 // keys-only: 8192-key sub-tiles (32 keys per thread, 246 VGPRs, 2 waves per
 // SIMD): digit runs twice as long, so the scatter writes whole 128-B lines,
 // and half the per-sub-tile scans and barriers per key — same box, three runs
-// each, 500M keys 8.92 → 7.68 ms against 4096-key sub-tiles
+// each, 500M keys 8.92 → 7.68 ms against 4096-key sub-tiles (16384-key
+// sub-tiles without the prefetch: 406 VGPRs, 10.15 ms).  64-bit pairs (the
+// COO→CSR sort): 8192-key sub-tiles without the next-sub-tile prefetch (288
+// VGPRs): 150M pairs over 47 bits 8.29 → 7.61 ms, COO→CSR 12.66 → 11.72 ms.
 extern "C" int lhpc_radix_sort_u32(uint32_t *keys, int64_t n, int begin_bit, int end_bit, int on_device,
                                    void *stream) {
   return sort_entry<uint32_t, false, 32>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
@@ -622,7 +632,7 @@ extern "C" int lhpc_radix_sort_pairs_u32(uint32_t *keys, uint32_t *vals, int64_t
 
 extern "C" int lhpc_radix_sort_pairs_u64(uint64_t *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit,
                                          int on_device, void *stream) {
-  return sort_entry<uint64_t, true, 16>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+  return sort_entry<uint64_t, true, 32, false>(keys, vals, n, begin_bit, end_bit, on_device, stream);
 }
 
 extern "C" int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *rows,
