@@ -53,6 +53,14 @@ for n in [int(x) for x in os.environ.get("SORT_NS", "1000000 16000000 100000000 
     torch.cuda.empty_cache()
 
 n = 150_000_000
+ku = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device=dev)
+vu = torch.arange(n, dtype=torch.int32, device=dev)
+k = torch.empty_like(ku); v = torch.empty_like(vu)
+def prep_u():
+    k.copy_(ku); v.copy_(vu)
+tmin, tavg = timed(prep_u, lambda: L.radix_sort_pairs(k, v, 0, 32, stream=st))
+print(json.dumps(dict(k="sort_pairs_u32", n=n, ms=tmin * 1e3, Gkeys=n / tmin / 1e9)), flush=True)
+del ku, vu, k, v
 ks = torch.randint(0, 2**47, (n,), dtype=torch.int64, device=dev)
 vs = torch.arange(n, dtype=torch.int32, device=dev)
 k = torch.empty_like(ks); v = torch.empty_like(vs)
