@@ -14,9 +14,9 @@
 //    scan (one workgroup per digit: per-block exclusive prefixes + digit
 //    totals), downsweep;
 //  * even-share grid sized to the resident downsweep blocks (CUs × blocks per
-//    CU, ≤ 2048): each block walks its own run of TILE-key sub-tiles in order
-//    (the next sub-tile's keys load under the current one's work), so the
-//    per-block histogram table stays ≤ 2 MB;
+//    CU, ≤ 2048): each block walks its own run of TILE-key sub-tiles (8192
+//    keys) in order (keys-only: the next sub-tile's keys load under the
+//    current one's work), so the per-block histogram table stays ≤ 2 MB;
 //  * downsweep ranks stably inside a sub-tile with a wave64 match-any
 //    (8 ballots per key → peer mask; rank = popcount(peers & lanes below)),
 //    per-wave running digit counters in LDS, then reorders the sub-tile in
