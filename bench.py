@@ -54,6 +54,30 @@ import time
 os.environ.setdefault("OMP_PROC_BIND", "close")
 os.environ.setdefault("OMP_PLACES", "cores")
 
+
+def _process_cpus():
+    """The process's CPU set, read from /proc/self/status before any OpenMP
+    runtime loads: once libgomp has bound the master thread (OMP_PROC_BIND),
+    sched_getaffinity(0) reports that thread's place, not the process's set."""
+    try:
+        for line in open("/proc/self/status"):
+            if line.startswith("Cpus_allowed_list:"):
+                cpus = set()
+                for part in line.split(":", 1)[1].strip().split(","):
+                    if part:
+                        lo, _, hi = part.partition("-")
+                        cpus.update(range(int(lo), int(hi or lo) + 1))
+                return sorted(cpus)
+    except OSError:
+        pass
+    try:
+        return sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        return list(range(os.cpu_count() or 1))
+
+
+PROCESS_CPUS = _process_cpus()
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -81,13 +105,11 @@ def parse():
 
 
 def cpu_threads():
+    """OMP_NUM_THREADS (the box sets 16), capped at the process's CPU set:
+    more threads than CPUs would only time-slice."""
     env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit():
-        return int(env)
-    try:
-        return len(os.sched_getaffinity(0))
-    except AttributeError:
-        return os.cpu_count() or 1
+    n = int(env) if env and env.isdigit() and int(env) > 0 else len(PROCESS_CPUS)
+    return max(1, min(n, len(PROCESS_CPUS)))
 
 
 def load_traffic(kernel_tag):
@@ -543,11 +565,12 @@ def sampled_y_check(rp, col, val, x, y, m, seed=0x5EED00C1):
             "bound": "|dy| <= 1e-6*sum|a*x| per row vs fp64 numpy"}
 
 
-def host_info():
+def host_info(threads=None):
     """Which host produced a CPU baseline: CPU model, the CPUs this process may
-    run on, and the NUMA nodes those CPUs belong to (the OpenMP threads are
-    bound close, one per core, inside that set)."""
-    info = {"cpu_model": None, "affinity_cpus": None, "numa_nodes": None}
+    run on (PROCESS_CPUS, read before OpenMP loaded), the NUMA nodes those CPUs
+    belong to, and the threads the baseline ran (bound close, one per core,
+    inside that set)."""
+    info = {"cpu_model": None, "affinity_cpus": None, "numa_nodes": None, "threads": threads}
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
@@ -556,7 +579,7 @@ def host_info():
     except OSError:
         pass
     try:
-        cpus = sorted(os.sched_getaffinity(0))
+        cpus = PROCESS_CPUS
         info["affinity_cpus"] = len(cpus)
         mine, nodes = set(cpus), set()
         base = "/sys/devices/system/node"
@@ -593,7 +616,7 @@ def cpu_spmv_baseline(rp, col, val, x, nnz, seconds, threads=None):
                       f"({sum(times):.1f} s), AVX2 gather" + (" + OpenMP" if threads > 1 else ", 1 thread")
                       + ", oracle/oracle.c cpu_spmv_simd",
             "omp": {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OMP_PROC_BIND", "OMP_PLACES")},
-            "host": host_info()}
+            "host": host_info(used)}
 
 
 def stencil_bench(args, L, torch, dev, stream, barrier):
@@ -680,7 +703,7 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
             lib.oracle_stencil7(uh.ctypes.data, oh.ctypes.data, n, n, n, g, -6.0, 1.0, th)
             ts.append(time.perf_counter() - t0)
         out["_cpu"] = {"value": cells / min(ts) / 1e9, "unit": "Gcell/s", "cores": th, "kind": "port",
-                       "sample": f"full 512^3 grid, best of {len(ts)} passes, OpenMP oracle_stencil7", "host": host_info()}
+                       "sample": f"full 512^3 grid, best of {len(ts)} passes, OpenMP oracle_stencil7", "host": host_info(th)}
     if wl in ("blur_x", "blur_y") and not args.no_cpu_baseline:
         from tests import _support as S
         lib = S.load_oracle()
@@ -697,7 +720,7 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
             ts.append(time.perf_counter() - t0)
         out["_cpu"] = {"value": cells / min(ts) / 1e9, "unit": "Gcell/s", "cores": th, "kind": "port",
                        "sample": f"full 8192^2 grid, best of {len(ts)} passes, reference SSE loop restated",
-                       "host": host_info()}
+                       "host": host_info(used)}
     return out
 
 
@@ -761,7 +784,7 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
             ts.append((time.perf_counter() - t0) / max(k, 1))
         out["cpu_baseline"] = {"value": 1.0 / min(ts), "unit": "iter/s", "cores": 1, "kind": "port",
                                "sample": f"{k} iterations of the fp64 CG restatement (oracle.c), best of {len(ts)}",
-                               "host": host_info()}
+                               "host": host_info(used)}
     plan.close()
     return out
 
@@ -838,7 +861,7 @@ def cpu_sort_baseline(keys, src, seconds):
     return {"value": m / min(ts) / 1e9, "unit": "Gkeys/s", "cores": cpu_threads(), "kind": kind,
             "sample": f"50M of the same keys, best of {len(ts)} sorts"
                       + (" (reference radix_sort, OpenMP)" if kind == "reference" else " (C LSD restatement)"),
-            "host": host_info()}
+            "host": host_info(used)}
 
 
 if __name__ == "__main__":

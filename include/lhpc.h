@@ -361,6 +361,20 @@ int lhpc_radix_sort_pairs_u64(uint64_t *keys, uint32_t *vals, int64_t n,
                               int begin_bit, int end_bit, int on_device,
                               void *stream);
 
+/* ------------------------------------------------------ scratch memory
+ * The on-device sort, COO → CSR and CG entry points take stream-ordered
+ * scratch from a library-owned pool per device (not the device's default
+ * pool, so other hipMallocAsync users in the process are unaffected).  The
+ * pool keeps freed scratch for the next call; lhpc_scratch_trim synchronises
+ * `device` and hands the cached memory back.  lhpc_scratch_poison is test
+ * support: it fills `bytes` of the current device's pool with the byte
+ * `value` and frees them on `stream`, so the next scratch allocations come
+ * back dirty (a kernel that reads scratch it never wrote then sees the
+ * pattern).  No reference counterpart.
+ */
+int lhpc_scratch_trim(int device);
+int lhpc_scratch_poison(int64_t bytes, int value, void *stream);
+
 /* ------------------------------------------------------------ COO → CSR
  * Builds CSR from coordinate triples (the assembly step
  * behind sparse::to_csr(RootGrid), reference lib/sparse/include/RootGrid.hpp:20-22).

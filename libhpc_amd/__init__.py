@@ -66,7 +66,7 @@ ABI_SYMBOLS = (
     "lhpc_dist_p2p_export", "lhpc_dist_p2p_import", "lhpc_dist_p2p_status",
     "lhpc_options_init", "lhpc_spmv_plan_create_opts", "lhpc_blur_x_f32_opts", "lhpc_blur_y_f32_opts",
     "lhpc_stencil7_f32_planes_opts", "lhpc_dist_spmv_plan_create_opts", "lhpc_dist_exchange",
-    "lhpc_dist_exchange_schedule", "lhpc_dist_p2p_reset",
+    "lhpc_dist_exchange_schedule", "lhpc_dist_p2p_reset", "lhpc_scratch_trim", "lhpc_scratch_poison",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -189,6 +189,8 @@ _sig("lhpc_row_ptr_narrow", _i, _p, _i64, _p)
 _sig("lhpc_radix_sort_u32", _i, _p, _i64, _i, _i, _i, _p)
 _sig("lhpc_radix_sort_pairs_u32", _i, _p, _p, _i64, _i, _i, _i, _p)
 _sig("lhpc_radix_sort_pairs_u64", _i, _p, _p, _i64, _i, _i, _i, _p)
+_sig("lhpc_scratch_trim", _i, _i)
+_sig("lhpc_scratch_poison", _i, _i64, _i, _p)
 _sig("lhpc_coo_to_csr", _i, _i, _i64, _i64, _i64, _p, _p, _p, _p, _i, _p, _p, C.POINTER(_i64), _i, _p)
 _sig("lhpc_cg_solve", _i, _p, _p, _p, _d, _i, _i, C.POINTER(_i), C.POINTER(_d), _p)
 _sig("lhpc_vec_dot", _i, _i, _i64, _p, _p, _p, _p)

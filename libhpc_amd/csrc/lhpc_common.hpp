@@ -37,6 +37,15 @@ constexpr int kWave = 64;  // CDNA wavefront; never 32
 // `make tuning`: the A/B scripts under tools/ only) lets LHPC_* variables
 // override fields, so one binary can be swept without recompiling.
 lhpc_options resolve_options(const lhpc_options *in);  // lhpc_runtime.hip
+
+// Stream-ordered scratch from a library-owned pool of the current device
+// (lhpc_runtime.hip): its release threshold is unbounded, so a call's freed
+// scratch is reused by the next one instead of being unmapped at every
+// synchronisation (sort bench lines swung from 8.5 to 95–114 ms on some runs
+// with the default threshold), and the device's default pool — other
+// hipMallocAsync users in the process — is left alone.  Free with
+// hipFreeAsync; lhpc_scratch_trim releases the cached memory.
+hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t s);
 inline const char *tuning_env(const char *name) {
 #ifdef LHPC_TUNING_ENV
   return std::getenv(name);

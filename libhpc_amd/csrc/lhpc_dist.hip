@@ -79,6 +79,9 @@ struct lhpc_dist_comm {
   int cus = 256;  // compute units of the device (k_p2p_acquire_all grid)
   P2pWindow win[LHPC_DIST_P2P_MAX_WINDOWS];
   int n_win = 0;
+  // halo stencil: "u complete on the caller's stream" and "halo planes
+  // landed", created on first use and re-recorded by every step
+  hipEvent_t ev_in = nullptr, ev_halo = nullptr;
 };
 
 struct lhpc_dist_spmv_plan {
@@ -556,6 +559,8 @@ extern "C" int lhpc_dist_comm_destroy(lhpc_dist_comm *c) {
     if (r != ncclSuccess) st = LHPC_RCCL_STATUS_BASE + static_cast<int>(r);
   }
   if (c->s_comm) (void)hipStreamDestroy(c->s_comm);
+  if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+  if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
   delete c;
   return st;
 }
@@ -742,14 +747,14 @@ extern "C" int lhpc_dist_stencil7_f32(lhpc_dist_comm *c, float *u, float *out, i
   const int64_t P = (ny + 2 * ghost) * (nx + 2 * ghost);  // padded plane
   auto plane = [&](int64_t z) { return u + (z + ghost) * P; };  // logical plane z ∈ [−ghost, nzl + ghost)
   const bool lo = c->rank > 0, hi = c->rank < c->nranks - 1;
-  hipEvent_t ev_in = nullptr, ev_halo = nullptr;
   lhpc::RocTxRange rx("lhpc_dist_stencil7_f32");
-  if (lo || hi) {
+  const bool halo = lo || hi;
+  if (halo) {
     lhpc::RocTxRange rh("lhpc_dist_stencil7_f32: halo exchange");
-    LHPC_HIP_TRY(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
-    LHPC_HIP_TRY(hipEventCreateWithFlags(&ev_halo, hipEventDisableTiming));
-    LHPC_HIP_TRY(hipEventRecord(ev_in, s));  // u complete on the caller's stream
-    LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, ev_in, 0));
+    if (!c->ev_in) LHPC_HIP_TRY(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
+    if (!c->ev_halo) LHPC_HIP_TRY(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
+    LHPC_HIP_TRY(hipEventRecord(c->ev_in, s));  // u complete on the caller's stream
+    LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, c->ev_in, 0));
     LHPC_NCCL_TRY(ncclGroupStart());
     if (lo) {
       LHPC_NCCL_TRY(ncclSend(plane(0), static_cast<size_t>(P), ncclFloat32, c->rank - 1, c->comm, c->s_comm));
@@ -760,16 +765,14 @@ extern "C" int lhpc_dist_stencil7_f32(lhpc_dist_comm *c, float *u, float *out, i
       LHPC_NCCL_TRY(ncclRecv(plane(nzl), static_cast<size_t>(P), ncclFloat32, c->rank + 1, c->comm, c->s_comm));
     }
     LHPC_NCCL_TRY(ncclGroupEnd());
-    LHPC_HIP_TRY(hipEventRecord(ev_halo, c->s_comm));
+    LHPC_HIP_TRY(hipEventRecord(c->ev_halo, c->s_comm));
   }
   // interior planes need no halo: they run while the planes travel
   int st = LHPC_OK;
   if (nzl > 2) st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, 1, nzl - 1, stream);
-  if (st == LHPC_OK && ev_halo) st = static_cast<int>(hipStreamWaitEvent(s, ev_halo, 0));
+  if (st == LHPC_OK && halo) st = static_cast<int>(hipStreamWaitEvent(s, c->ev_halo, 0));
   if (st == LHPC_OK) st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, 0, 1, stream);
   if (st == LHPC_OK && nzl > 1)
     st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, nzl - 1, nzl, stream);
-  if (ev_in) (void)hipEventDestroy(ev_in);  // destruction is deferred until the event completes
-  if (ev_halo) (void)hipEventDestroy(ev_halo);
   return st;
 }

@@ -207,17 +207,3 @@ extern "C" int lhpc_probe_copy_w(const void *src, void *dst, int64_t bytes, int 
 #undef LHPC_CW
   return static_cast<int>(hipGetLastError());
 }
-
-// test support (tests/test_gpu_sort.py::test_coo_to_csr_poisoned_pool): leave
-// `bytes` of the device's default stream-ordered pool filled with `value`,
-// so the next hipMallocAsync scratch allocations on `stream` (lhpc_sort.hip
-// DevBuf) come back dirty — a kernel that reads scratch it never wrote then
-// sees this pattern instead of the zeros fresh memory often holds
-extern "C" int lhpc_probe_poison_pool(int64_t bytes, int value, void *stream) {
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  void *p = nullptr;
-  if (hipMallocAsync(&p, static_cast<size_t>(bytes), s) != hipSuccess) return -1;
-  if (hipMemsetAsync(p, value, static_cast<size_t>(bytes), s) != hipSuccess) return -1;
-  if (hipFreeAsync(p, s) != hipSuccess) return -1;
-  return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
-}

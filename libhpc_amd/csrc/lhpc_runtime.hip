@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "lhpc_common.hpp"
 
@@ -89,7 +90,42 @@ void env_overlay(lhpc_options &o) {
   i32("LHPC_DIST_EXCHANGE", o.dist_world1);
 }
 #endif
+
+// library-owned stream-ordered scratch pools, one per device (see
+// lhpc_common.hpp scratch_alloc); created once under a per-device once_flag
+constexpr int kMaxDevices = 64;
+std::once_flag g_pool_once[kMaxDevices];
+hipMemPool_t g_pool[kMaxDevices] = {};
+hipError_t g_pool_err[kMaxDevices] = {};
+
+hipError_t scratch_pool(int dev, hipMemPool_t *out) {
+  if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+  std::call_once(g_pool_once[dev], [dev] {
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    hipError_t e = hipMemPoolCreate(&g_pool[dev], &props);
+    if (e == hipSuccess) {
+      uint64_t thr = UINT64_MAX;  // keep freed scratch for the next call
+      e = hipMemPoolSetAttribute(g_pool[dev], hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    g_pool_err[dev] = e;
+  });
+  *out = g_pool[dev];
+  return g_pool_err[dev];
+}
 }  // namespace
+
+hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t s) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  hipMemPool_t pool;
+  if ((e = scratch_pool(dev, &pool)) != hipSuccess) return e;
+  return hipMallocFromPoolAsync(p, bytes ? bytes : 16, pool, s);
+}
 
 lhpc_options resolve_options(const lhpc_options *in) {
   lhpc_options o;
@@ -106,3 +142,27 @@ lhpc_options resolve_options(const lhpc_options *in) {
 }
 
 }  // namespace lhpc
+
+// Hands the current device's cached scratch back to the driver (the pool
+// keeps freed scratch between calls: GBs after a 500M-key sort).
+extern "C" int lhpc_scratch_trim(int device) {
+  hipMemPool_t pool;
+  LHPC_HIP_TRY(lhpc::scratch_pool(device, &pool));
+  LHPC_HIP_TRY(hipDeviceSynchronize());
+  LHPC_HIP_TRY(hipMemPoolTrimTo(pool, 0));
+  return LHPC_OK;
+}
+
+// Test support: leave `bytes` of the current device's scratch pool filled
+// with `value`, so the next scratch allocations on `stream` come back dirty
+// (tests/test_gpu_sort.py::test_coo_to_csr_poisoned_pool).
+extern "C" int lhpc_scratch_poison(int64_t bytes, int value, void *stream) {
+  if (bytes < 0) return LHPC_ERR_INVALID_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  void *p = nullptr;
+  LHPC_HIP_TRY(lhpc::scratch_alloc(&p, static_cast<size_t>(bytes), s));
+  LHPC_HIP_TRY(hipMemsetAsync(p, value, static_cast<size_t>(bytes), s));
+  LHPC_HIP_TRY(hipFreeAsync(p, s));
+  LHPC_HIP_TRY(hipStreamSynchronize(s));
+  return LHPC_OK;
+}

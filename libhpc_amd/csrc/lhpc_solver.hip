@@ -25,6 +25,7 @@
 #include <cstdint>
 
 #include "lhpc_common.hpp"
+#include "lhpc_spmv_impl.hpp"
 
 namespace lhpc {
 namespace {
@@ -186,7 +187,7 @@ extern "C" int lhpc_vec_dot(int dtype, int64_t n, const void *a, const void *b, 
   hipStream_t s = static_cast<hipStream_t>(stream);
   Scratch part;
   part.s = s;
-  LHPC_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
+  LHPC_HIP_TRY(scratch_alloc(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
   if (dtype == LHPC_F32)
     return dot_dev(static_cast<const float *>(a), static_cast<const float *>(b), n, out, part.d, s);
   return dot_dev(static_cast<const double *>(a), static_cast<const double *>(b), n, out, part.d, s);
@@ -199,7 +200,7 @@ extern "C" int lhpc_cg_step_xr(int dtype, int64_t n, const double *alpha_num, co
   hipStream_t s = static_cast<hipStream_t>(stream);
   Scratch part;
   part.s = s;
-  LHPC_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
+  LHPC_HIP_TRY(scratch_alloc(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
   const int g = vec_grid(n);
   if (dtype == LHPC_F32)
     hipLaunchKernelGGL((k_cg_xr<float>), dim3(g), dim3(kVecThreads), 0, s, static_cast<float *>(x),
@@ -234,7 +235,7 @@ extern "C" int lhpc_cg_step_r(int dtype, int64_t n, const double *alpha_num, con
   hipStream_t s = static_cast<hipStream_t>(stream);
   Scratch part;
   part.s = s;
-  LHPC_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
+  LHPC_HIP_TRY(scratch_alloc(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
   const int g = vec_grid(n);
   if (dtype == LHPC_F32)
     hipLaunchKernelGGL((k_cg_r<float>), dim3(g), dim3(kVecThreads), 0, s, static_cast<float *>(r),
@@ -293,26 +294,26 @@ extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, doubl
   void *vecs = nullptr;
   Scratch sc;
   sc.s = s;
-  LHPC_HIP_TRY(hipMallocAsync(&vecs, static_cast<size_t>(std::max<int64_t>(n, 1)) * ts * 3, s));
+  LHPC_HIP_TRY(scratch_alloc(&vecs, static_cast<size_t>(std::max<int64_t>(n, 1)) * ts * 3, s));
   struct VecFree {
     void *p;
     hipStream_t s;
     ~VecFree() { (void)hipFreeAsync(p, s); }
   } vf{vecs, s};
-  LHPC_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&sc.d), (8 + kDotBlocks) * sizeof(double), s));
+  LHPC_HIP_TRY(scratch_alloc(reinterpret_cast<void **>(&sc.d), (8 + kDotBlocks) * sizeof(double), s));
   char *vb = static_cast<char *>(vecs);
   void *r = vb, *p = vb + static_cast<size_t>(n) * ts, *q = vb + 2 * static_cast<size_t>(n) * ts;
   double *rr[2] = {sc.d, sc.d + 1}, *pq = sc.d + 2, *bb = sc.d + 3, *part = sc.d + 8;
   const int g = vec_grid(n);
   int it = 0;
   // the two scalars the host loop reads come back into pinned memory: no
-  // asynchronous copy touches pageable host memory
-  double *hs = nullptr;
-  LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&hs), 2 * sizeof(double), hipHostMallocDefault));
-  struct HostFree {
-    double *p;
-    ~HostFree() { (void)hipHostFree(p); }
-  } hf{hs};
+  // asynchronous copy touches pageable host memory.  The
+  // buffer belongs to the plan (allocated on the first solve, freed with the
+  // plan): hipHostFree synchronises the whole device, so it is not paid per
+  // solve
+  if (!plan->h_scalars)
+    LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&plan->h_scalars), 2 * sizeof(double), hipHostMallocDefault));
+  double *hs = plan->h_scalars;
   double &h_rr = hs[0], &h_bb = hs[1];
   h_rr = 0.0;
   h_bb = 0.0;

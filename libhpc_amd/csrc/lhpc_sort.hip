@@ -278,23 +278,6 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
   }
 }
 
-// The device's default memory pool keeps what the sort scratch frees (release
-// threshold unbounded, set once per device).  With the default threshold of
-// 0 the pool hands its memory back at every synchronisation and the next call
-// maps a fresh 2 GB (500M keys) inside its stream time; sort bench lines then
-// swung from 8.5 ms to 95–114 ms on some runs of the same box, never since.
-inline void keep_pool_memory() {
-  static bool done[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || done[dev]) return;
-  hipMemPool_t pool;
-  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-    uint64_t thr = UINT64_MAX;
-    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-  }
-  done[dev] = true;
-}
-
 struct DevBuf {
   void *p = nullptr;
   hipStream_t s = nullptr;
@@ -302,9 +285,8 @@ struct DevBuf {
     if (p) (void)hipFreeAsync(p, s);
   }
   hipError_t alloc(size_t bytes, hipStream_t st) {
-    keep_pool_memory();
     s = st;
-    return hipMallocAsync(&p, bytes ? bytes : 16, st);
+    return scratch_alloc(&p, bytes, st);  // library pool (lhpc_common.hpp)
   }
 };
 

@@ -380,6 +380,7 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
                   static_cast<void *>(p->d_col16), static_cast<void *>(p->d_perm), p->d_xg,
                   static_cast<void *>(p->d_carry)})
     if (q) (void)hipFree(q);
+  if (p->h_scalars) (void)hipHostFree(p->h_scalars);
   delete p;
   return LHPC_OK;
 }

@@ -27,6 +27,7 @@ struct lhpc_spmv_plan {
   int64_t *d_blocks = nullptr;
   int64_t n_blocks = 0, n_long = 0;
   void *d_xstage = nullptr, *d_ystage = nullptr;
+  double *h_scalars = nullptr;  // lhpc_cg_solve: 2 pinned host scalars, allocated on first use
   double *d_dpart = nullptr;  // lhpc_spmv_dot: per-block partials (ADAPTIVE), allocated on first use
   int kernel = LHPC_KERNEL_ROWGROUP;
   int L = 16, R = 4;

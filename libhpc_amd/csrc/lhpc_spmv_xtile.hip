@@ -744,7 +744,9 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   int64_t W = XtTile<T>::W;
   {
     const int64_t s0 = (p->n_cols + W - 1) / W, s1 = (s0 + cus - 1) / cus * cus;
-    bool narrow = sizeof(T) == 4 && s1 * 10 <= s0 * 11;
+    // (never past build_xtile's 4096-tile cap: on a CU count that does not
+    // divide 4096 the rounding could otherwise cost a plan its XTILE layout)
+    bool narrow = sizeof(T) == 4 && s1 * 10 <= s0 * 11 && s1 <= 4096;
     if (const char *e = tuning_env("LHPC_XTILE_TW")) narrow = std::atoi(e) != 0;
     if (narrow && s1 > s0) W = (p->n_cols + s1 - 1) / s1;
   }

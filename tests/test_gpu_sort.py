@@ -190,20 +190,15 @@ def test_sort_u32_reference_100m(lhpc, gpu):
 def test_coo_to_csr_poisoned_pool(lhpc, gpu, poison):
     """Regression for the round-2 host-path race: the on-device
     sort / scan / COO→CSR still take their scratch from the stream-ordered
-    pool (lhpc_sort.hip DevBuf).  Every scratch buffer must be fully written
-    before it is read, so results must not depend on what the pool hands
-    back: the pool is left filled with 0x00 / 0xA5 / 0xFF before each call
-    (liblhpc_probe.so lhpc_probe_poison_pool, on the call's stream), for the
+    pool (lhpc_sort.hip DevBuf: the library's own scratch pool).  Every
+    scratch buffer must be fully written before it is read, so results must
+    not depend on what the pool hands back: the pool is left filled with
+    0x00 / 0xA5 / 0xFF before each call (lhpc_scratch_poison, on the call's
+    stream), for the
     4-entry symmetric Matrix Market case that failed, tiny and ragged COO
     inputs with duplicates and empty rows, and the sorts they run."""
-    import ctypes as C
-    import os
     import torch
-    probe = os.path.join(os.path.dirname(lhpc.LIB_PATH), "liblhpc_probe.so")
-    if not os.path.exists(probe):  # an A/B build ships only liblhpc.so
-        probe = os.path.join(os.path.dirname(lhpc.__file__), "_lib", "liblhpc_probe.so")
-    P = C.CDLL(probe)
-    P.lhpc_probe_poison_pool.argtypes = [C.c_int64, C.c_int, C.c_void_p]
+    P = lhpc.lib
     st = torch.cuda.current_stream(gpu)
     cases = [(3, 3, np.array([0, 1, 0, 2]), np.array([0, 0, 1, 2]), np.array([2.0, -1.5, -1.5, 4.0]))]
     rng = np.random.default_rng(0x9015 + poison)
@@ -214,14 +209,14 @@ def test_coo_to_csr_poisoned_pool(lhpc, gpu, poison):
         r, c, v = r.astype(np.int32), c.astype(np.int32), v.astype(np.float64)
         want = S.coo_oracle(n_rows, n_cols, r, c, v)
         for _ in range(3):
-            assert P.lhpc_probe_poison_pool(1 << 24, poison, st.cuda_stream) == 0
+            assert P.lhpc_scratch_poison(1 << 24, poison, st.cuda_stream) == 0
             rp, col, val = lhpc.coo_to_csr(n_rows, n_cols, _dev(gpu, r), _dev(gpu, c), _dev(gpu, v), stream=st)
             torch.cuda.synchronize()
             assert np.array_equal(rp.cpu().numpy(), want[0]), (n_rows, n_cols, r.size)
             assert np.array_equal(col.cpu().numpy(), want[1]) and np.array_equal(val.cpu().numpy(), want[2])
     keys = rng.integers(0, 1 << 32, 5000, dtype=np.uint64).astype(np.uint32)
     for _ in range(3):
-        assert P.lhpc_probe_poison_pool(1 << 24, poison, st.cuda_stream) == 0
+        assert P.lhpc_scratch_poison(1 << 24, poison, st.cuda_stream) == 0
         kd = _dev(gpu, keys.view(np.int32))
         lhpc.radix_sort(kd, stream=st)
         torch.cuda.synchronize()
