@@ -569,7 +569,17 @@ int lhpc_dist_p2p_export(lhpc_dist_comm *comm, void *y, int64_t bytes,
                          unsigned char *blob_out /* LHPC_DIST_P2P_BLOB_BYTES */);
 int lhpc_dist_p2p_import(lhpc_dist_comm *comm,
                          const unsigned char *blobs /* nranks × LHPC_DIST_P2P_BLOB_BYTES */);
-/* unmaps every window (peer handles closed, flags freed)                   */
+/* lhpc_dist_p2p_unmap: undoes the LAST window (y must be its buffer) on this
+ * rank — peer mappings closed, the window dropped whether it was imported or
+ * only exported — after synchronising the comm stream.  A setup whose import
+ * failed on any rank calls it on every rank that exported, so window indices
+ * stay aligned across ranks and no rank keeps a window its peers never mapped.
+ * lhpc_dist_p2p_reset unmaps every window and frees this rank's flag array.
+ * It is COLLECTIVE: every rank resets (peers still hold this rank's flag
+ * array mapped), with a barrier before any rank exports again.  Blobs carry a
+ * flags generation, so an import after a reset remaps the peers' new flag
+ * arrays instead of trusting the old mapping.                              */
+int lhpc_dist_p2p_unmap(lhpc_dist_comm *comm, void *y);
 int lhpc_dist_p2p_reset(lhpc_dist_comm *comm);
 int lhpc_dist_p2p_status(const lhpc_dist_comm *comm);
 /*

@@ -66,7 +66,7 @@ ABI_SYMBOLS = (
     "lhpc_dist_p2p_export", "lhpc_dist_p2p_import", "lhpc_dist_p2p_status",
     "lhpc_options_init", "lhpc_spmv_plan_create_opts", "lhpc_blur_x_f32_opts", "lhpc_blur_y_f32_opts",
     "lhpc_stencil7_f32_planes_opts", "lhpc_dist_spmv_plan_create_opts", "lhpc_dist_exchange",
-    "lhpc_dist_exchange_schedule", "lhpc_dist_p2p_reset", "lhpc_scratch_trim", "lhpc_scratch_poison",
+    "lhpc_dist_exchange_schedule", "lhpc_dist_p2p_reset", "lhpc_dist_p2p_unmap", "lhpc_scratch_trim", "lhpc_scratch_poison",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -220,6 +220,7 @@ _sig("lhpc_dist_spmv", _i, _p, _p, _p, _p)
 _sig("lhpc_dist_exchange", _i, _p, _p, _p)
 _sig("lhpc_dist_exchange_schedule", _i, _p, _i, _i, _i, _i, _i, _p, _i64, C.POINTER(_i64))
 _sig("lhpc_dist_p2p_reset", _i, _p)
+_sig("lhpc_dist_p2p_unmap", _i, _p, _p)
 _sig("lhpc_dist_spmv_plan_destroy", _i, _p)
 _sig("lhpc_dist_stencil7_f32", _i, _p, _p, _p, _i64, _i64, _i64, _i64, _f, _f, _p)
 _sig("lhpc_dist_comm_create_local", _i, C.POINTER(_p), _i, _i, _i)
@@ -788,9 +789,17 @@ class DistComm:
         return bytes(blob)
 
     def p2p_reset(self):
-        """Unmap every window (lhpc_dist_p2p_reset)."""
+        """Unmap every window (lhpc_dist_p2p_reset).  Collective: every rank
+        resets, with a barrier before any rank exports again."""
         _check(lib.lhpc_dist_p2p_reset(self._h), "lhpc_dist_p2p_reset")
         self._p2p_ys = []
+
+    def p2p_unmap(self, y):
+        """Undo the last window (lhpc_dist_p2p_unmap), exported or imported."""
+        _check(lib.lhpc_dist_p2p_unmap(self._h, y.data_ptr()), "lhpc_dist_p2p_unmap")
+        ys = self.__dict__.get("_p2p_ys", [])
+        if ys and ys[-1] is y:
+            ys.pop()
 
     def p2p_import(self, blobs):
         """Every rank's blob, in rank order."""
@@ -799,15 +808,19 @@ class DistComm:
         buf = (C.c_ubyte * (DIST_P2P_BLOB_BYTES * self.nranks)).from_buffer_copy(b"".join(blobs))
         _check(lib.lhpc_dist_p2p_import(self._h, buf), "lhpc_dist_p2p_import")
 
-    def p2p_setup_torch(self, y, group=None):
+    def p2p_setup_torch(self, y, group=None, _fail_import=False):
         """Export y, all-gather the blobs over an initialised torch.distributed
         group (any backend), import them: lhpc_dist_spmv(…, y) then exchanges
         by direct peer stores.
 
         Collective-safe: every rank takes part in the same collectives
         whatever fails locally (a rank whose export fails sends a marked empty
-        blob), and if any rank's export or import failed every rank raises
-        LhpcError — no rank is left with a window its peers never mapped."""
+        blob).  If any rank's export or import failed, every rank that
+        exported undoes this window (lhpc_dist_p2p_unmap) before raising
+        LhpcError, so the ranks' window lists stay aligned and no rank keeps a
+        window its peers never mapped: a caller that catches the error and
+        keeps going gets the RCCL exchange on every rank.  ``_fail_import``
+        (tests) makes this rank's import fail after the export."""
         import torch
         import torch.distributed as dist
         err = None
@@ -821,9 +834,14 @@ class DistComm:
         parts = [torch.empty_like(t) for _ in range(self.nranks)]
         dist.all_gather(parts, t, group=group)
         parts = [p.cpu().numpy() for p in parts]
+        exported = ok == 1
         if not all(int(p[-1]) == 1 for p in parts):
+            if exported:
+                self.p2p_unmap(y)
             raise LhpcError(-6, f"p2p export failed on a rank ({err})")  # LHPC_ERR_INTERNAL
         try:
+            if _fail_import:
+                raise LhpcError(-6, "injected import failure")
             self.p2p_import([p[:-1].tobytes() for p in parts])
             ok = 1
         except LhpcError as e:
@@ -831,6 +849,7 @@ class DistComm:
         flag = torch.tensor([ok], dtype=torch.int32, device=dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
         if int(flag.item()) != 1:
+            self.p2p_unmap(y)  # imported here or not: this rank exported it
             raise LhpcError(-6, f"p2p import failed on a rank ({err})")  # LHPC_ERR_INTERNAL
 
     def p2p_status(self) -> int:

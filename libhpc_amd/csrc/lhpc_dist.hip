@@ -37,7 +37,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
+#include <random>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -71,7 +73,9 @@ struct lhpc_dist_comm {
   // memory) shared by every window, the peers' mapped flag arrays, and the
   // windows in export order
   uint32_t *flags = nullptr;
+  uint64_t flags_gen = 0;              // identifies this flag allocation (in every blob)
   std::vector<void *> peer_flags_base;
+  std::vector<uint64_t> peer_flags_gen;  // the generation of each peer's mapped flags
   uint32_t **d_peer_flags = nullptr;
   bool flags_mapped = false;
   uint32_t *h_status = nullptr;  // host-mapped: bit 0 = a flag wait timed out
@@ -204,6 +208,7 @@ struct P2pBlob {  // LHPC_DIST_P2P_BLOB_BYTES per rank
   uint64_t magic;
   int32_t window;  // export order
   int32_t nranks;
+  uint64_t flags_gen;  // changes when the exporter re-allocates its flags (after a reset)
 };
 static_assert(sizeof(P2pBlob) <= LHPC_DIST_P2P_BLOB_BYTES, "blob size");
 constexpr uint64_t kP2pMagic = 0x6c687063705033ull;  // "lhpcP3"
@@ -222,6 +227,7 @@ void p2p_release(lhpc_dist_comm *c) {
   for (void *b : c->peer_flags_base)
     if (b) (void)hipIpcCloseMemHandle(b);
   c->peer_flags_base.clear();
+  c->peer_flags_gen.clear();
   if (c->d_peer_flags) (void)hipFree(c->d_peer_flags);
   if (c->flags) (void)hipFree(c->flags);
   if (c->h_status) (void)hipHostFree(c->h_status);
@@ -453,6 +459,9 @@ extern "C" int lhpc_dist_p2p_export(lhpc_dist_comm *c, void *y, int64_t bytes, u
     LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_status), sizeof(uint32_t), hipHostMallocMapped));
     *c->h_status = 0;
     c->epoch = 0;
+    static std::atomic<uint64_t> counter{0};
+    c->flags_gen = (std::random_device{}() * 0x9E3779B97F4A7C15ull) ^ (++counter << 1) ^ reinterpret_cast<uintptr_t>(c->flags);
+    if (c->flags_gen == 0) c->flags_gen = 1;
   }
   LHPC_HIP_TRY(hipIpcGetMemHandle(&b.flags, c->flags));
   b.offset = static_cast<unsigned char *>(y) - static_cast<unsigned char *>(base);
@@ -460,6 +469,7 @@ extern "C" int lhpc_dist_p2p_export(lhpc_dist_comm *c, void *y, int64_t bytes, u
   b.magic = kP2pMagic;
   b.window = c->n_win;
   b.nranks = c->nranks;
+  b.flags_gen = c->flags_gen;
   P2pWindow &w = c->win[c->n_win++];
   w = P2pWindow{};
   w.buf = y;
@@ -499,6 +509,11 @@ extern "C" int lhpc_dist_p2p_import(lhpc_dist_comm *c, const unsigned char *blob
   std::vector<void *> bufs(static_cast<size_t>(nr), nullptr), flg(static_cast<size_t>(nr), nullptr);
   uint64_t narrow = 0;
   const uintptr_t my_phase = reinterpret_cast<uintptr_t>(w.buf) & 15;
+  // the peers' flag arrays: mapped by the first import, and again whenever a
+  // peer's blob carries another flags generation (it reset and re-exported)
+  bool remap = !c->flags_mapped;
+  for (int r = 0; r < nr && !remap; ++r)
+    if (r != c->rank && c->peer_flags_gen[static_cast<size_t>(r)] != bl[r].flags_gen) remap = true;
   for (int r = 0; r < nr; ++r) {
     if (r == c->rank) {
       bufs[r] = w.buf;
@@ -509,7 +524,11 @@ extern "C" int lhpc_dist_p2p_import(lhpc_dist_comm *c, const unsigned char *blob
     if (e != hipSuccess) return undo(static_cast<int>(e));
     bufs[r] = static_cast<unsigned char *>(pb[r]) + bl[r].offset;
     if ((reinterpret_cast<uintptr_t>(bufs[r]) & 15) != my_phase) narrow |= uint64_t{1} << r;
-    if (!c->flags_mapped) {
+    if (remap) {
+      if (c->flags_mapped && c->peer_flags_gen[static_cast<size_t>(r)] == bl[r].flags_gen) {
+        flg[r] = c->peer_flags_base[static_cast<size_t>(r)];  // unchanged: keep the mapping
+        continue;
+      }
       e = hipIpcOpenMemHandle(&pf[r], bl[r].flags, hipIpcMemLazyEnablePeerAccess);
       if (e != hipSuccess) return undo(static_cast<int>(e));
       flg[r] = pf[r];
@@ -517,7 +536,7 @@ extern "C" int lhpc_dist_p2p_import(lhpc_dist_comm *c, const unsigned char *blob
   }
   hipError_t e = hipMalloc(reinterpret_cast<void **>(&d_buf), nr * sizeof(void *));
   if (e == hipSuccess) e = hipMemcpy(d_buf, bufs.data(), nr * sizeof(void *), hipMemcpyHostToDevice);
-  if (e == hipSuccess && !c->flags_mapped) {
+  if (e == hipSuccess && remap) {
     e = hipMalloc(reinterpret_cast<void **>(&d_flg), nr * sizeof(void *));
     if (e == hipSuccess) e = hipMemcpy(d_flg, flg.data(), nr * sizeof(void *), hipMemcpyHostToDevice);
   }
@@ -527,11 +546,36 @@ extern "C" int lhpc_dist_p2p_import(lhpc_dist_comm *c, const unsigned char *blob
   w.d_peer_buf = d_buf;
   w.narrow = narrow;
   w.ready = true;
-  if (!c->flags_mapped) {
-    c->peer_flags_base = pf;
+  if (remap) {
+    // close the replaced peer mappings (every window's kernels read peers'
+    // flags through d_peer_flags only, which is swapped here)
+    if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
+    std::vector<void *> base(static_cast<size_t>(nr), nullptr);
+    for (int r = 0; r < nr; ++r) {
+      if (r == c->rank) continue;
+      void *old = c->flags_mapped ? c->peer_flags_base[static_cast<size_t>(r)] : nullptr;
+      if (pf[r]) {
+        if (old) (void)hipIpcCloseMemHandle(old);
+        base[static_cast<size_t>(r)] = pf[r];
+      } else {
+        base[static_cast<size_t>(r)] = old;
+      }
+    }
+    if (c->d_peer_flags) (void)hipFree(c->d_peer_flags);
+    c->peer_flags_base = base;
+    c->peer_flags_gen.assign(static_cast<size_t>(nr), 0);
+    for (int r = 0; r < nr; ++r) c->peer_flags_gen[static_cast<size_t>(r)] = bl[r].flags_gen;
     c->d_peer_flags = d_flg;
     c->flags_mapped = true;
   }
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_p2p_unmap(lhpc_dist_comm *c, void *y) {
+  if (!c || !y || c->n_win == 0 || c->win[c->n_win - 1].buf != y) return LHPC_ERR_INVALID_ARG;
+  LHPC_HIP_TRY(hipSetDevice(c->device));
+  if (c->s_comm) LHPC_HIP_TRY(hipStreamSynchronize(c->s_comm));
+  window_release(c->win[--c->n_win]);
   return LHPC_OK;
 }
 

@@ -13,6 +13,13 @@ Cases (argv[1]):
             no host ordering
   tiny      1–3-row blocks (small n, many chunks) in fp32 and fp64, and a
             window whose 16-B phase differs between the ranks (word stores)
+  rollback  rank 1's import fails (injected) after both exported: both ranks
+            raise and undo the window, an AUTO-exchange call then fails the
+            same way on both (no window: RCCL, which a local comm lacks — no
+            rank takes the P2P path alone), and a second setup lines the
+            windows up again: its P2P calls are bit-exact
+  reset     P2P calls, a collective lhpc_dist_p2p_reset (new flag arrays),
+            re-export / import (peers' flags remapped by generation), calls
 """
 import json
 import os
@@ -133,6 +140,58 @@ elif case == "tiny":
                 dist.barrier()
         out["status"].append(comm.p2p_status())
         comm.close()
+elif case == "rollback":
+    n, K = 50_000, 2
+    rp, col, val, x, cuts, local = problem(n, 5, K, L.F32, 0xE400)
+    _, want, _ = S.spmv_oracle(rp, col, val, x)
+    comm = L.DistComm.local(world, rank, 0)
+    xd = torch.from_numpy(x).to(dev)
+    y = torch.full((n,), float("nan"), dtype=xd.dtype, device=dev)
+    try:
+        comm.p2p_setup_torch(y, _fail_import=(rank == 1))
+        out["ok"].append(False)  # must raise on every rank
+    except L.LhpcError:
+        out["ok"].append(True)
+    with L.DistSpMVPlan(comm, n, n, K, cuts, *local) as d:  # AUTO exchange
+        try:
+            d(xd, y)
+            torch.cuda.synchronize()
+            out["ok"].append(False)  # no window and no RCCL: every rank must refuse
+        except L.LhpcError as e:
+            out["ok"].append(e.status == -1)
+    dist.barrier()
+    comm.p2p_setup_torch(y)  # window 0 again, on both ranks
+    torch.cuda.synchronize()
+    dist.barrier()
+    with L.DistSpMVPlan(comm, n, n, K, cuts, *local) as d:
+        for it in range(2):
+            d(xd, y)
+            torch.cuda.synchronize()
+            out["ok"].append(bool(np.array_equal(y.cpu().numpy(), want)))
+            dist.barrier()
+    out["status"].append(comm.p2p_status())
+    comm.close()
+elif case == "reset":
+    n, K = 60_000, 3
+    rp, col, val, x, cuts, local = problem(n, 4, K, L.F64, 0xE500)
+    _, want, _ = S.spmv_oracle(rp, col, val, x)
+    comm = L.DistComm.local(world, rank, 0)
+    xd = torch.from_numpy(x).to(dev)
+    for rnd in range(3):
+        y = torch.full((n,), float("nan"), dtype=xd.dtype, device=dev)
+        comm.p2p_setup_torch(y)
+        torch.cuda.synchronize()
+        dist.barrier()
+        with L.DistSpMVPlan(comm, n, n, K, cuts, *local, options={"dist_exchange": L.DIST_EXCHANGE_P2P}) as d:
+            for it in range(2):
+                d(xd, y)
+                torch.cuda.synchronize()
+                out["ok"].append(bool(np.array_equal(y.cpu().numpy(), want)))
+                dist.barrier()
+        out["status"].append(comm.p2p_status())
+        comm.p2p_reset()  # collective: every rank, then a barrier before re-export
+        dist.barrier()
+    comm.close()
 else:
     raise SystemExit(f"unknown case {case}")
 print(json.dumps(out), flush=True)

@@ -119,7 +119,7 @@ def test_dist_stencil7_world1_matches_single_domain(lhpc, gpu, comm, nz, ny, nx)
     assert np.array_equal(od.cpu().numpy(), want)
 
 
-P2P_CASES = {"barrier": 6, "loop": 8, "pingpong": 8, "tiny": 8}
+P2P_CASES = {"barrier": 6, "loop": 8, "pingpong": 8, "tiny": 8, "rollback": 4, "reset": 6}
 
 
 @pytest.mark.parametrize("case", list(P2P_CASES))
@@ -132,8 +132,11 @@ def test_dist_spmv_p2p_two_ranks_one_gpu(lhpc, gpu, case):
     fp64 per-block plans); the iterative loop x ← y with no host ordering
     between calls (the flags are the only ordering); two windows ping-ponged
     (y of call n is x of call n+1); 1–3-row blocks and windows of different
-    16-B phase.  (On one GPU the pushes are device-local; over xGMI they are
-    the same stores.)"""
+    16-B phase; a setup whose import fails on one rank rolled back on both
+    (then an AUTO call refused on both, and a fresh setup bit-exact); three
+    rounds of setup / calls / collective reset (flag arrays re-allocated and
+    remapped by generation).  (On one GPU the pushes are device-local; over
+    xGMI they are the same stores.)"""
     import json
     import os
     import subprocess
