@@ -184,7 +184,19 @@ typedef struct lhpc_options {
   int32_t dist_exchange;        /* enum lhpc_dist_exchange                       */
   int32_t dist_broadcast;       /* 1: RCCL broadcast groups even for equal blocks */
   int32_t dist_world1;          /* 1: issue the RCCL exchange at world 1 (tests) */
-  int32_t reserved[7];
+  /* XTILE row parts: a matrix whose tile stream does not fit the int32
+   * stream offsets (nnz + 8·tiles ≥ 2^31) is cut into nnz-balanced row parts,
+   * one XTILE plan each, run in turn on the same x.  0: parts only past that
+   * limit; > 0: at most this many nonzeros per part (tests: the split path
+   * at small sizes)                                                          */
+  int32_t xtile_part_nnz;
+  /* single-process multi-device plans (n_devices > 1) */
+  int32_t multi_chunks;         /* row chunks per device K (0: 2)                */
+  int32_t multi_exchange;       /* enum lhpc_dist_exchange: AUTO/P2P = peer
+                                   stores, RCCL = ncclCommInitAll group
+                                   all-gathers (distinct devices only)          */
+  int32_t multi_force;          /* 1: the multi-device path even for one device */
+  int32_t reserved[3];
 } lhpc_options;
 void lhpc_options_init(lhpc_options *opts);
 
@@ -202,8 +214,19 @@ int lhpc_device_count(void);
  *   col_idx      nnz int32 column indices in [0, n_cols)
  *   val          nnz values of dtype
  *   device_ids   HIP device ordinals; NULL = current device
- *   n_devices    1 (one process drives one GPU; multi-GPU = one process
- *                per GPU, see lhpc_csr_partition_rows)
+ *   n_devices    1: one device.  > 1 (≤ 16): a single-process multi-device
+ *                plan: the rows are cut into n_devices·K
+ *                nnz-balanced blocks (K = options.multi_chunks, default 2;
+ *                block k·n_devices + d is device d's chunk k), each device
+ *                gets its own local plan, stream and comm stream (and RCCL
+ *                comm with options.multi_exchange = RCCL), peer access is
+ *                enabled between the listed devices.  lhpc_spmv then takes x
+ *                and y on device_ids[0] (or host buffers): x is copied to the
+ *                other devices, every device computes its blocks, the blocks
+ *                come back into y.  lhpc_spmv_multi keeps full replicas on
+ *                every device instead.  A device may be listed twice (tests:
+ *                several "devices" sharing one GPU; peer stores only).  The
+ *                alternative, one process per GPU, is lhpc_dist_* below.
  * The plan COPIES A into HBM (and may re-encode it); it never retains the
  * caller's pointers after returning.
  */
@@ -222,6 +245,28 @@ int lhpc_spmv(lhpc_spmv_plan *plan, const void *x, void *y,
               int buffers_on_device, void *stream);
 int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *plan,
                             lhpc_spmv_plan_info *info);
+/*
+ * Multi-device plans: y = A·x with full replicas on every device.  x[d]
+ * (n_cols) and y[d] (n_rows, not x[d]) are HBM pointers on device d; after
+ * the call every y[d] holds the whole y (so y is the next x of an iterative
+ * loop with no host round trip).  streams[d]: the stream on device d the
+ * call is ordered on (NULL array: the plan's own streams); the call is
+ * asynchronous on them.  Device d reduces its chunk k into y[d] and its comm
+ * stream stores that block into every other y[p] (xGMI peer stores: all
+ * links at once) while chunk k+1 is reduced; with options.multi_exchange =
+ * RCCL one group of in-place all-gathers per chunk instead.  No other
+ * stream may read y[d] until its stream passes the call.  Replaces the
+ * per-GPU SpMV calls a single-process caller of the reference would make
+ * (SURVEY §8b "Threading"; no reference interface: the reference has no
+ * multi-device code).
+ */
+int lhpc_spmv_multi(lhpc_spmv_plan *plan, const void *const *x, void *const *y, void *const *streams);
+/* the split of a plan: devices, chunks K, exchange (enum lhpc_dist_exchange;
+ * NONE for a single-device plan), device ordinals (capacity n_devices) and
+ * the n_devices·K + 1 row cuts; any output may be NULL.  A single-device plan
+ * reports one device, K = 1 and cuts {0, n_rows}.                           */
+int lhpc_spmv_plan_multi_info(const lhpc_spmv_plan *plan, int *n_devices, int *chunks, int *exchange,
+                              int *device_ids, int64_t *cuts);
 /*
  * Row-range plans for overlapping a collective with the SpMV (one process
  * per GPU, libhpc_amd/dist.py): as lhpc_spmv_plan_create, with the plan's

@@ -67,6 +67,7 @@ ABI_SYMBOLS = (
     "lhpc_options_init", "lhpc_spmv_plan_create_opts", "lhpc_blur_x_f32_opts", "lhpc_blur_y_f32_opts",
     "lhpc_stencil7_f32_planes_opts", "lhpc_dist_spmv_plan_create_opts", "lhpc_dist_exchange",
     "lhpc_dist_exchange_schedule", "lhpc_dist_p2p_reset", "lhpc_dist_p2p_unmap", "lhpc_scratch_trim", "lhpc_scratch_poison",
+    "lhpc_spmv_multi", "lhpc_spmv_plan_multi_info",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -106,7 +107,8 @@ class Options(C.Structure):
                 ("stencil7_nj", C.c_int32), ("stencil7_zc", C.c_int32), ("stencil7_pf", C.c_int32),
                 ("stencil7_blocks", C.c_int32), ("blur_x_rows", C.c_int32), ("blur_y_vec", C.c_int32),
                 ("blur_y_rows", C.c_int32), ("dist_exchange", C.c_int32), ("dist_broadcast", C.c_int32),
-                ("dist_world1", C.c_int32), ("reserved", C.c_int32 * 7)]
+                ("dist_world1", C.c_int32), ("xtile_part_nnz", C.c_int32), ("multi_chunks", C.c_int32),
+                ("multi_exchange", C.c_int32), ("multi_force", C.c_int32), ("reserved", C.c_int32 * 3)]
 
     def __init__(self, **kw):
         super().__init__()
@@ -171,6 +173,8 @@ _sig("lhpc_options_init", None, _p)
 _sig("lhpc_spmv_stage", _i, _p, _p, _p)
 _sig("lhpc_spmv_range", _i, _p, _i, _p, _p)
 _sig("lhpc_spmv_plan_info_get", _i, _p, C.POINTER(PlanInfo))
+_sig("lhpc_spmv_multi", _i, _p, _p, _p, _p)
+_sig("lhpc_spmv_plan_multi_info", _i, _p, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i), _p, _p)
 _sig("lhpc_spmv_plan_destroy", _i, _p)
 _sig("lhpc_csr_partition_rows", _i, _p, _i, _i64, _i, _p)
 for _n in ("lhpc_blur_x_f32", "lhpc_blur_y_f32"):
@@ -284,13 +288,16 @@ class SpMVPlan:
     """
 
     def __init__(self, row_ptr, col_idx, val, n_cols: int, flags: int = 0,
-                 device: Optional[int] = None, splits=None, options=None):
+                 device: Optional[int] = None, splits=None, options=None, devices=None):
         """``splits``: ascending rows in (0, n_rows); the plan is then a
         row-range plan (lhpc_spmv_plan_create_split: stage(x) once, then
         range(k, y_k) per range) and raises LhpcError (LHPC_ERR_UNSUPPORTED)
         when the matrix does not select the XTILE layout.  ``options``: an
         Options (or dict of its fields) pinning kernel variants
-        (lhpc_spmv_plan_create_opts)."""
+        (lhpc_spmv_plan_create_opts).  ``devices``: a list of HIP device
+        ordinals for a single-process multi-device plan (a
+        device may repeat: several shares of one GPU); ``plan(x, y)`` then
+        takes x, y on devices[0] and ``plan.multi(xs, ys)`` full replicas."""
         row_ptr = np.ascontiguousarray(row_ptr)
         col_idx = np.ascontiguousarray(col_idx, dtype=np.int32)
         val = np.ascontiguousarray(val)
@@ -307,14 +314,21 @@ class SpMVPlan:
         self.n_cols = int(n_cols)
         self.nnz = int(col_idx.shape[0])
         self._h = _p()
-        dev = (_i * 1)(device) if device is not None else None
+        if devices is not None:
+            devices = [int(d) for d in devices]
+            dev = (_i * len(devices))(*devices)
+            ndev = len(devices)
+        else:
+            dev = (_i * 1)(device) if device is not None else None
+            ndev = 1 if device is not None else 0
+        self.devices = devices
         self._opts = options if not isinstance(options, dict) else Options(**options)
         if splits is None and options is None:
             self.splits = None
             _check(lib.lhpc_spmv_plan_create(
                 C.byref(self._h), self.dtype, self.n_rows, self.n_cols, self.nnz,
                 row_ptr.ctypes.data, 64 if row_ptr.dtype == np.int64 else 32,
-                col_idx.ctypes.data, val.ctypes.data, dev, 1 if device is not None else 0,
+                col_idx.ctypes.data, val.ctypes.data, dev, ndev,
                 flags), "lhpc_spmv_plan_create")
         else:
             sp = np.ascontiguousarray(splits if splits is not None else [], dtype=np.int64)
@@ -322,7 +336,7 @@ class SpMVPlan:
             _check(lib.lhpc_spmv_plan_create_opts(
                 C.byref(self._h), self.dtype, self.n_rows, self.n_cols, self.nnz,
                 row_ptr.ctypes.data, 64 if row_ptr.dtype == np.int64 else 32,
-                col_idx.ctypes.data, val.ctypes.data, dev, 1 if device is not None else 0,
+                col_idx.ctypes.data, val.ctypes.data, dev, ndev,
                 flags, int(sp.shape[0]), sp.ctypes.data if sp.shape[0] else None, _opts(self._opts)),
                 "lhpc_spmv_plan_create_opts")
 
@@ -330,6 +344,36 @@ class SpMVPlan:
         inf = PlanInfo()
         _check(lib.lhpc_spmv_plan_info_get(self._h, C.byref(inf)), "lhpc_spmv_plan_info_get")
         return inf.as_dict()
+
+    def multi_info(self) -> dict:
+        """lhpc_spmv_plan_multi_info: devices, chunks K, exchange, row cuts."""
+        nd, k, ex = _i(), _i(), _i()
+        _check(lib.lhpc_spmv_plan_multi_info(self._h, C.byref(nd), C.byref(k), C.byref(ex), None, None),
+               "lhpc_spmv_plan_multi_info")
+        ids = (_i * nd.value)()
+        cuts = np.zeros(nd.value * k.value + 1, dtype=np.int64)
+        _check(lib.lhpc_spmv_plan_multi_info(self._h, None, None, None, ids, cuts.ctypes.data),
+               "lhpc_spmv_plan_multi_info")
+        return {"n_devices": nd.value, "chunks": k.value, "exchange": ex.value, "devices": list(ids), "cuts": cuts}
+
+    def multi(self, xs, ys, streams=None):
+        """lhpc_spmv_multi: full replicas, xs[d]/ys[d] device tensors on
+        device d; every ys[d] holds the whole y afterwards (asynchronous on
+        ``streams[d]``, default torch's current stream of each device)."""
+        import torch
+        n = len(xs)
+        if len(ys) != n:
+            raise ValueError("one x and one y per device")
+        for x, y in zip(xs, ys):
+            if x.shape[0] < self.n_cols or y.shape[0] < self.n_rows:
+                raise ValueError("x/y too short for the plan")
+        if streams is None:
+            streams = [torch.cuda.current_stream(x.device) for x in xs]
+        xa = (_p * n)(*[x.data_ptr() for x in xs])
+        ya = (_p * n)(*[y.data_ptr() for y in ys])
+        sa = (_p * n)(*[_stream_ptr(s) for s in streams])
+        _check(lib.lhpc_spmv_multi(self._h, xa, ya, sa), "lhpc_spmv_multi")
+        return ys
 
     def __call__(self, x, y=None, stream=None):
         """y = A·x.  numpy in → numpy out (synchronous); torch CUDA tensors →

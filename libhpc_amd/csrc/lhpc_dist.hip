@@ -94,9 +94,7 @@ struct lhpc_dist_spmv_plan {
   int64_t n_rows = 0, n_cols = 0;
   lhpc_options opt{};                       // resolved: the dist_* fields pick the exchange
   std::vector<int64_t> cuts;                // nranks·K + 1 global row cuts
-  lhpc_spmv_plan *split = nullptr;          // row-range plan over the rank's blocks (XTILE)
-  std::vector<int> range_of;                // block k → range index of `split` (−1: empty block)
-  std::vector<lhpc_spmv_plan *> block_plan; // otherwise one plan per non-empty block
+  lhpc::LocalPlans lp;                      // the rank's K blocks (lhpc_multi.hip)
   // the exchange schedules (lhpc_dist_exchange_schedule), entries of chunk k
   // at [first[k], first[k+1])
   std::vector<lhpc_dist_xfer> sched_rccl, sched_p2p;
@@ -287,9 +285,7 @@ int p2p_exchange_end(lhpc_dist_comm *c) {
 void destroy_spmv(lhpc_dist_spmv_plan *d) {
   if (!d) return;
   (void)hipSetDevice(d->comm ? d->comm->device : 0);
-  if (d->split) lhpc_spmv_plan_destroy(d->split);
-  for (auto *p : d->block_plan)
-    if (p) lhpc_spmv_plan_destroy(p);
+  lhpc::local_plans_destroy(d->lp);
   for (hipEvent_t e : d->ev)
     if (e) (void)hipEventDestroy(e);
   if (d->done) (void)hipEventDestroy(d->done);
@@ -660,43 +656,8 @@ extern "C" int lhpc_dist_spmv_plan_create_opts(lhpc_dist_spmv_plan **out, lhpc_d
     const int64_t b = static_cast<int64_t>(k) * nr + rk;
     ls[k + 1] = ls[k] + (cuts[b + 1] - cuts[b]);
   }
-  const int64_t n_local = ls[K];
-  auto rp_at = [&](int64_t i) {
-    return row_ptr_bits == 64 ? static_cast<const int64_t *>(row_ptr)[i] : static_cast<const int32_t *>(row_ptr)[i];
-  };
-  const int64_t nnz_local = rp_at(n_local);
-  const size_t tsz = dtype == LHPC_F64 ? 8 : 4;
-  int st = LHPC_OK;
-  // splits at the starts of non-empty blocks after the first row
-  std::vector<int64_t> splits;
-  d->range_of.assign(static_cast<size_t>(K), -1);
-  int nrange = 0;
-  for (int k = 0; k < K; ++k) {
-    if (ls[k + 1] == ls[k]) continue;
-    if (ls[k] > 0) splits.push_back(ls[k]);
-    d->range_of[k] = nrange++;
-  }
-  if (!splits.empty())
-    st = lhpc_spmv_plan_create_opts(&d->split, dtype, n_local, n_cols, nnz_local, row_ptr, row_ptr_bits, col_idx,
-                                    val, &comm->device, 1, flags, static_cast<int>(splits.size()), splits.data(),
-                                    &o);
-  if (splits.empty() || st == LHPC_ERR_UNSUPPORTED) {
-    // one plan per non-empty block (the matrix does not select XTILE, or the
-    // rank holds a single block)
-    d->split = nullptr;
-    st = LHPC_OK;
-    d->block_plan.assign(static_cast<size_t>(K), nullptr);
-    for (int k = 0; k < K && st == LHPC_OK; ++k) {
-      const int64_t r0 = ls[k], r1 = ls[k + 1];
-      if (r1 == r0) continue;
-      const int64_t e0 = rp_at(r0), e1 = rp_at(r1);
-      std::vector<int64_t> lrp(static_cast<size_t>(r1 - r0 + 1));
-      for (int64_t i = r0; i <= r1; ++i) lrp[static_cast<size_t>(i - r0)] = rp_at(i) - e0;
-      st = lhpc_spmv_plan_create_opts(&d->block_plan[k], dtype, r1 - r0, n_cols, e1 - e0, lrp.data(), 64,
-                                      col_idx + e0, static_cast<const unsigned char *>(val) + e0 * tsz,
-                                      &comm->device, 1, flags, 0, nullptr, &o);
-    }
-  }
+  int st = lhpc::local_plans_create(d->lp, dtype, n_cols, K, ls.data(), row_ptr, row_ptr_bits, col_idx, val,
+                                    comm->device, flags, o);
   if (st == LHPC_OK) {
     d->ev.assign(static_cast<size_t>(K), nullptr);
     for (auto &e : d->ev)
@@ -733,22 +694,12 @@ extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, vo
   if (xk < 0) return xk;
   if (xk == LHPC_DIST_EXCHANGE_P2P) LHPC_TRY(p2p_exchange_begin(c, s, d->ev_p2p));
   const bool xchg = xk != LHPC_DIST_EXCHANGE_NONE;
-  // a split plan with per-range gather pieces (its xg exceeds the Infinity
-  // Cache) gathers each range right before reducing it; else one stage
-  const bool range_gather = d->split && !d->split->xt_rpc.empty();
-  int gathered = 0;  // ranges [0, gathered) are gathered (in order)
-  if (d->split && !range_gather) LHPC_TRY(lhpc_spmv_stage(d->split, x, stream));
+  int gathered = 0;  // ranges of a range-gather plan gathered so far (in order)
+  LHPC_TRY(lhpc::local_plans_stage(d->lp, x, s));
   for (int k = 0; k < d->K; ++k) {
     const int64_t b = static_cast<int64_t>(k) * c->nranks + c->rank;
     void *yk = static_cast<unsigned char *>(y) + d->cuts[b] * tsz;
-    if (d->range_of[k] >= 0) {
-      if (range_gather)
-        for (; gathered <= d->range_of[k]; ++gathered) LHPC_TRY(lhpc::xtile_range_gather(d->split, x, gathered, s));
-      if (d->split)
-        LHPC_TRY(lhpc_spmv_range(d->split, d->range_of[k], yk, stream));
-      else
-        LHPC_TRY(lhpc_spmv(d->block_plan[k], x, yk, 1, stream));
-    }
+    LHPC_TRY(lhpc::local_plans_chunk(d->lp, x, k, yk, gathered, s));
     if (xchg) LHPC_TRY(exchange_chunk(d, xk, win, k, y, s));
   }
   if (xchg) {

@@ -54,9 +54,67 @@ bool is_gfx950(int dev) {
 }
 
 int launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
+  if (!p->parts.empty()) {
+    const size_t tsz = p->dtype == LHPC_F32 ? 4 : 8;
+    for (size_t i = 0; i < p->parts.size(); ++i)
+      LHPC_TRY(xtile_launch(p->parts[i], x, static_cast<unsigned char *>(y) + p->part_row[i] * tsz, s));
+    return LHPC_OK;
+  }
   if (p->kernel == LHPC_KERNEL_XTILE) return xtile_launch(p, x, y, s);
   if (p->kernel == LHPC_KERNEL_XSLICE) return xslice_launch(p, x, y, s);
   return csr_launch(p, x, y, s);
+}
+
+// XTILE row parts: the tile stream of one plan is addressed with int32
+// offsets (nnz + 8 padding entries per tile < 2^31, lhpc_plan.cpp
+// build_xtile).  A larger matrix (n ≳ 143M rows at 15 nonzeros per row) is
+// cut into nnz-balanced row parts of ≤ cap nonzeros, each an ordinary XTILE
+// plan over its rows (row_ptr rebased, the caller's col/val at the part's
+// offset) run in turn on the same x, instead of dropping to XSLICE.
+// LHPC_ERR_UNSUPPORTED when some single row exceeds the cap.
+int build_parts(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz,
+                int64_t cap) {
+  const int64_t n_rows = p->n_rows;
+  int64_t n_parts = (p->nnz + cap - 1) / cap;
+  std::vector<int64_t> cuts;
+  for (;; ++n_parts) {  // nnz-balanced cuts; one more part until every part fits
+    cuts.assign(static_cast<size_t>(n_parts) + 1, 0);
+    LHPC_TRY(lhpc_csr_partition_rows(rp.p, rp.bits, n_rows, static_cast<int>(n_parts), cuts.data()));
+    bool fit = true;
+    for (int64_t i = 0; i < n_parts && fit; ++i) {
+      const int64_t r0 = cuts[i], r1 = cuts[i + 1];
+      if (r1 - r0 == 1 && rp[r1] - rp[r0] > cap) return LHPC_ERR_UNSUPPORTED;  // one row past the cap
+      fit = rp[r1] - rp[r0] <= cap;
+    }
+    if (fit) break;
+    if (n_parts > n_rows) return LHPC_ERR_UNSUPPORTED;
+  }
+  std::vector<int64_t> lrp;
+  for (int64_t i = 0; i < n_parts; ++i) {
+    const int64_t r0 = cuts[i], r1 = cuts[i + 1];
+    if (r1 == r0) continue;
+    auto *q = new (std::nothrow) lhpc_spmv_plan();
+    if (!q) return LHPC_ERR_ALLOC;
+    p->parts.push_back(q);
+    p->part_row.push_back(r0);
+    q->opt = p->opt;
+    q->dtype = p->dtype;
+    q->device = p->device;
+    q->n_rows = r1 - r0;
+    q->n_cols = p->n_cols;
+    const int64_t e0 = rp[r0];
+    q->nnz = rp[r1] - e0;
+    lrp.resize(static_cast<size_t>(r1 - r0 + 1));
+    for (int64_t r = r0; r <= r1; ++r) lrp[static_cast<size_t>(r - r0)] = rp[r] - e0;
+    LHPC_TRY(xtile_build(q, RowPtrView{lrp.data(), 64}, col_idx + e0,
+                         static_cast<const unsigned char *>(val) + e0 * static_cast<int64_t>(tsz), tsz));
+    p->bytes += q->bytes;
+  }
+  p->part_row.push_back(n_rows);
+  p->kernel = LHPC_KERNEL_XTILE;
+  p->S = p->parts.empty() ? 0 : p->parts[0]->S;
+  p->xs_width = p->parts.empty() ? 0 : p->parts[0]->xs_width;
+  return LHPC_OK;
 }
 
 int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
@@ -70,7 +128,7 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
       !row_ptr || (row_ptr_bits != 32 && row_ptr_bits != 64) || n_cols > INT32_MAX ||
       (nnz > 0 && (!col_idx || !val)))
     return LHPC_ERR_INVALID_ARG;
-  if (n_devices > 1) return LHPC_ERR_UNSUPPORTED;  // one process per GPU
+  if (n_devices < 0 || (n_devices > 1 && !device_ids)) return LHPC_ERR_INVALID_ARG;
   if (flags & LHPC_PLAN_DEVICE_INPUT) return LHPC_ERR_UNSUPPORTED;
   if (row_ptr_bits == 32 && nnz > INT32_MAX) return LHPC_ERR_INVALID_ARG;
 
@@ -78,6 +136,26 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
   // always: every layout pass below indexes host arrays by row_ptr / col_idx,
   // and every kernel indexes x by col_idx (LHPC_PLAN_VALIDATE is implied)
   LHPC_TRY(validate_csr(row_ptr, row_ptr_bits, col_idx, n_rows, n_cols, nnz));
+
+  // several devices driven by this one host thread: one local
+  // plan, stream, comm stream (and RCCL comm) per device (lhpc_multi.hip)
+  if (n_devices > 1 || (o.multi_force && n_devices == 1 && device_ids)) {
+    if (n_splits > 0) return LHPC_ERR_UNSUPPORTED;
+    auto *p = new (std::nothrow) lhpc_spmv_plan();
+    if (!p) return LHPC_ERR_ALLOC;
+    p->opt = o;
+    p->dtype = dtype;
+    p->n_rows = n_rows;
+    p->n_cols = n_cols;
+    p->nnz = nnz;
+    const int st = multi_create(p, rp, col_idx, val, device_ids, n_devices, flags);
+    if (st != LHPC_OK) {
+      lhpc_spmv_plan_destroy(p);
+      return st;
+    }
+    *out = p;
+    return LHPC_OK;
+  }
 
   int dev = 0;
   if (device_ids && n_devices == 1) {
@@ -138,7 +216,16 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
   // options.spmv_no_xtile selects XSLICE instead.
   const bool want_xtile = (flags & LHPC_PLAN_FORCE_XTILE) || (nolocal && !o.spmv_no_xtile);
   if (want_xtile && n_rows > 0) {
-    int st = xtile_build(p, rp, col_idx, val, tsz);
+    // row parts when the tile stream outgrows its int32 offsets (or a lower
+    // cap is asked for); user row splits keep a single plan
+    const int64_t tiles = (n_cols + (tsz == 4 ? 40960 : 20480) - 1) / (tsz == 4 ? 40960 : 20480);
+    int64_t cap = INT32_MAX - 8 * (tiles + 256) - (int64_t{1} << 16);
+    if (o.xtile_part_nnz > 0) cap = std::min<int64_t>(cap, o.xtile_part_nnz);
+    int st;
+    if (nnz > cap && n_splits == 0 && tiles <= 4096)
+      st = build_parts(p, rp, col_idx, val, tsz, cap);
+    else
+      st = xtile_build(p, rp, col_idx, val, tsz);
     if (st == LHPC_OK) {
       *out = p;
       return LHPC_OK;
@@ -147,6 +234,10 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
       lhpc_spmv_plan_destroy(p);
       return st;
     }
+    for (auto *q : p->parts) lhpc_spmv_plan_destroy(q);
+    p->parts.clear();
+    p->part_row.clear();
+    p->bytes = 0;
     // layout does not fit its index types: XSLICE / CSR kernels below
   }
   const bool want_xslice = (flags & LHPC_PLAN_FORCE_XSLICE) || nolocal;
@@ -305,6 +396,7 @@ extern "C" int lhpc_spmv(lhpc_spmv_plan *p, const void *x, void *y, int on_devic
   if (!p || (p->n_cols > 0 && !x) || (p->n_rows > 0 && !y)) return LHPC_ERR_INVALID_ARG;
   RocTxRange rx("lhpc_spmv");
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p->multi) return multi_home(p, x, y, on_device, s);
   LHPC_HIP_TRY(hipSetDevice(p->device));
   const size_t tsz = p->dtype == LHPC_F32 ? 4 : 8;
   const void *dx = x;
@@ -367,11 +459,25 @@ extern "C" int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *p, lhpc_spmv_plan_i
   }
   info->slices = p->S;
   info->slice_width = p->xs_width;
+  if (!p->parts.empty()) {  // XTILE row parts: totals over the parts
+    info->launches = 0;
+    info->n_blocks = 0;
+    info->n_long_rows = 0;
+    for (const auto *q : p->parts) {
+      lhpc_spmv_plan_info qi{};
+      LHPC_TRY(lhpc_spmv_plan_info_get(q, &qi));
+      info->launches += qi.launches;
+      info->n_blocks += qi.n_blocks;
+      info->n_long_rows += qi.n_long_rows;
+    }
+  }
   return LHPC_OK;
 }
 
 extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
   if (!p) return LHPC_OK;
+  if (p->multi) multi_free(p);
+  for (auto *q : p->parts) lhpc_spmv_plan_destroy(q);
   (void)hipSetDevice(p->device);
   for (void *q : {p->d_row_ptr, static_cast<void *>(p->d_col), p->d_val, static_cast<void *>(p->d_blocks),
                   p->d_xstage, p->d_ystage, p->d_lens, static_cast<void *>(p->d_cbase), p->d_partial,

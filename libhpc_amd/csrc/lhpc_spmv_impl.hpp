@@ -60,6 +60,14 @@ struct lhpc_spmv_plan {
   int xt_al = 0;  // aligned segments: 16-B units (lhpc_options.xtile_align)
   void *d_xg = nullptr;
   double *d_carry = nullptr;
+  // XTILE row parts (lhpc_options.xtile_part_nnz): a matrix whose tile stream
+  // exceeds the int32 stream offsets is cut into nnz-balanced row parts, one
+  // XTILE plan each (rows [part_row[i], part_row[i+1]) of y), run in turn on
+  // the same x; this plan then holds no arrays of its own
+  std::vector<lhpc_spmv_plan *> parts;
+  std::vector<int64_t> part_row;
+  // single-process multi-device plan (n_devices > 1; lhpc_multi.hip)
+  struct lhpc_multi *multi = nullptr;
 };
 
 namespace lhpc {
@@ -84,6 +92,50 @@ inline int dmalloc(void **p, size_t n, int64_t &acct) {
   acct += static_cast<int64_t>(n);
   return LHPC_OK;
 }
+
+// ---- lhpc_multi.hip: one rank's (or one device's) share of a row-block
+// split.  Its K blocks (block k·nranks + rank of the global cuts) stacked in
+// chunk order form a local CSR (row_ptr rebased, global columns); one
+// row-range XTILE plan over them (split at every block start) stages x once
+// and reduces chunk k on its own, else (the matrix does not select XTILE,
+// or a single block) one plan per non-empty block.
+struct LocalPlans {
+  int K = 0;
+  std::vector<int64_t> ls;                  // local row offset of chunk k (K + 1)
+  lhpc_spmv_plan *split = nullptr;          // row-range plan over the K blocks (XTILE)
+  std::vector<int> range_of;                // chunk k → range index of `split` (−1: empty)
+  std::vector<lhpc_spmv_plan *> block_plan; // otherwise one plan per non-empty block
+  // a split plan with per-range gather pieces (its xg exceeds the Infinity
+  // Cache) gathers each range right before reducing it; else one stage
+  bool range_gather() const { return split && !split->xt_rpc.empty(); }
+};
+// ls: K + 1 local row offsets; row_ptr/col/val: the local CSR (host)
+int local_plans_create(LocalPlans &lp, int dtype, int64_t n_cols, int K, const int64_t *ls, const void *row_ptr,
+                       int row_ptr_bits, const int32_t *col_idx, const void *val, int device, unsigned flags,
+                       const lhpc_options &o);
+void local_plans_destroy(LocalPlans &lp);
+// the call's stage (all of x's tiles; no-op for range-gather and block plans)
+int local_plans_stage(const LocalPlans &lp, const void *x, hipStream_t s);
+// chunk k's rows into yk (its first row at yk[0]); `gathered` counts the
+// ranges a range-gather plan has gathered so far in this call (start at 0)
+int local_plans_chunk(const LocalPlans &lp, const void *x, int k, void *yk, int &gathered, hipStream_t s);
+// the rank's local CSR from the GLOBAL one: rows of blocks k·nranks + rank,
+// stacked (K + 1 local offsets in ls); no copy of col/val for one block
+struct LocalCsr {
+  std::vector<int64_t> ls, rp;
+  std::vector<int32_t> col;
+  std::vector<unsigned char> val;
+  const int32_t *colp = nullptr;
+  const void *valp = nullptr;
+};
+// the single-process multi-device plan (n_devices > 1 or options.multi_force)
+int multi_create(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, const int *device_ids,
+                 int n_devices, unsigned flags);
+void multi_free(lhpc_spmv_plan *p);
+// lhpc_spmv on it: x, y on device_ids[0] (on_device) or host buffers
+int multi_home(lhpc_spmv_plan *p, const void *x, void *y, int on_device, hipStream_t s);
+void local_csr_from_global(LocalCsr &out, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz,
+                           const int64_t *cuts, int nranks, int K, int rank);
 
 // ---- lhpc_spmv_csr.hip
 int csr_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s);

@@ -157,3 +157,21 @@ def test_dist_calls_reject_bad_arguments_before_any_device_work(lhpc):
     assert L.lhpc_dist_comm_destroy(None) == 0
     assert L.lhpc_dist_allreduce_sum_f64(None, None, 1, None) == -1
     assert L.lhpc_dist_stencil7_f32(None, None, None, 1, 1, 1, 1, 1.0, 1.0, None) == -1
+
+
+def test_multi_device_plan_argument_checks(lhpc):
+    """lhpc_spmv_plan_create's multi-device arguments are checked before any
+    device is touched: n_devices > 1 needs device ids, at most 16 devices,
+    and row splits are single-device only (CPU: no GPU needed)."""
+    import ctypes as C
+    rp = np.array([0, 1, 2], dtype=np.int32)
+    col = np.array([0, 1], dtype=np.int32)
+    val = np.ones(2, dtype=np.float32)
+    h = C.c_void_p()
+    args = (C.byref(h), lhpc.F32, 2, 2, 2, rp.ctypes.data, 32, col.ctypes.data, val.ctypes.data)
+    assert lhpc.lib.lhpc_spmv_plan_create(*args, None, 2, 0) == -1  # no device ids
+    assert lhpc.lib.lhpc_spmv_plan_create(*args, (C.c_int * 17)(*([0] * 17)), 17, 0) == -1  # > 16 devices
+    assert lhpc.lib.lhpc_spmv_plan_create(*args, (C.c_int * 2)(0, 0), -1, 0) == -1
+    sp = np.array([1], dtype=np.int64)
+    assert lhpc.lib.lhpc_spmv_plan_create_opts(*args, (C.c_int * 2)(0, 0), 2, 0, 1, sp.ctypes.data, None) == -5
+    assert not h.value

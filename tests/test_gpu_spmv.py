@@ -515,3 +515,74 @@ def test_rowgroup_shape_option(lhpc, gpu, lanes, rows):
     with pytest.raises(lhpc.LhpcError):
         lhpc.SpMVPlan(rp, col, val, 20_000, flags=FAMILIES["rowgroup"],
                       options={"rowgroup_lanes": 8, "rowgroup_rows": 8})
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("cap", [40_000, 100_003])
+def test_xtile_row_parts(lhpc, gpu, dtype, cap, xt_layout):
+    """XTILE row parts (lhpc_options.xtile_part_nnz): the plan cuts the rows
+    into nnz-balanced parts of ≤ cap nonzeros, one XTILE plan each, run in
+    turn on the same x — the path a matrix takes when its tile stream
+    outgrows the int32 offsets (nnz + 8·tiles ≥ 2^31), here forced at small
+    size.  Long rows (up to 30000 nonzeros, i.e. most of a part) and empty
+    rows sit next to the cuts.  Dyadic: bit-exact; random: within the bound;
+    the host-buffer path too.  More launches than a single plan."""
+    lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 3000 + [0, 0] + [30000] + [7] * 4000
+    opts = dict(xt_layout, xtile_part_nnz=cap)
+    info = _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA900, opts=opts)
+    single = _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA900, opts=xt_layout)
+    assert info["launches"] > single["launches"]
+    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xA901, dyadic=False, opts=opts)
+    rp, col, val = _csr_from_lengths(lengths, 200_000, 0xA902, True)
+    val = val.astype(dtype)
+    x = (np.random.default_rng(7).integers(-8, 9, size=200_000) / 8.0).astype(dtype)
+    yh, _ = _run(lhpc, gpu, rp, col, val, x, 200_000, FAMILIES["xtile"], device_buffers=False, options=opts)
+    assert np.array_equal(yh, S.spmv_oracle(rp, col, val, x)[1])
+
+
+def test_xtile_row_parts_row_past_cap(lhpc, gpu):
+    """A single row longer than the part cap cannot be cut into parts: the
+    plan leaves XTILE (as the int32 limit did before parts existed) and the
+    result is still exact."""
+    lengths = [3] * 100 + [50_000] + [3] * 100
+    rp, col, val = _csr_from_lengths(lengths, 100_000, 0xAA00, True)
+    val = val.astype(np.float32)
+    x = (np.random.default_rng(8).integers(-8, 9, size=100_000) / 8.0).astype(np.float32)
+    y, info = _run(lhpc, gpu, rp, col, val, x, 100_000, FAMILIES["xtile"], options={"xtile_part_nnz": 10_000})
+    assert info["kernel"] != lhpc.KERNEL_XTILE
+    assert np.array_equal(y, S.spmv_oracle(rp, col, val, x)[1])
+
+
+@pytest.mark.slow
+def test_xtile_parts_150m_past_int32(lhpc, gpu):
+    """Past the int32 stream: n = 150M rows and columns, 15 uniform nonzeros
+    per row (nnz = 2.25e9 > 2^31, int64 row_ptr, fp32, dyadic values).
+    Before row parts this plan fell to XSLICE; now it stays XTILE (two row
+    parts).  10^5 sampled rows bit-exact against fp64 numpy (exact on
+    dyadic data), the whole y equal run to run, and GFLOP/s printed (C2
+    level expected: per part the same kernels as C2)."""
+    import torch
+    n = 150_000_000
+    rp, col, val = lhpc.gen_uniform_csr(n, n, 15, dtype=lhpc.F32, dist=1, seed=0x15000)
+    assert rp.dtype == np.int64 and int(rp[-1]) > 2**31
+    x = lhpc.gen_values(lhpc.F32, 1, n, 0x15001)
+    with lhpc.SpMVPlan(rp, col, val, n) as plan:
+        info = plan.info()
+        assert info["kernel"] == lhpc.KERNEL_XTILE and info["nnz"] == 15 * n
+        xd = torch.from_numpy(x).to(gpu)
+        y1 = plan(xd).clone()
+        y2 = plan(xd)
+        torch.cuda.synchronize()
+        assert torch.equal(y1, y2)
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(5):
+            plan(xd, y2)
+        t1.record()
+        torch.cuda.synchronize()
+        ms = t0.elapsed_time(t1) / 5
+        print(f"\n150M XTILE parts: {ms:.3f} ms/call, {2 * 15 * n / ms / 1e6:.1f} GFLOP/s, launches {info['launches']}")
+        y = y1.cpu().numpy()
+        del xd, y1, y2
+    rows, y64, _ = S.sampled_rows_fp64(rp, col, val, x, 100_000)
+    assert np.array_equal(y[rows].astype(np.float64), y64)
