@@ -551,6 +551,29 @@ int lhpc_dist_spmv_plan_create_opts(lhpc_dist_spmv_plan **out, lhpc_dist_comm *c
                                     const void *row_ptr, int row_ptr_bits, const int32_t *col_idx,
                                     const void *val, unsigned flags, const lhpc_options *opts);
 int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream);
+/*
+ * Cross-step overlap for iterative use (y of call n is x of call n+1).
+ * lhpc_dist_spmv = lhpc_dist_spmv_begin + lhpc_dist_spmv_end.  _begin issues
+ * the call but leaves the exchange of y in flight (y is NOT complete on
+ * `stream` afterwards); _end makes `stream` wait for it.  When the x of a
+ * _begin is the y of the previous _begin on this plan, the x tiles are
+ * gathered by column part: chunk j's rows of y are one contiguous column
+ * range of the next x (square matrices), so the gather of the tiles inside
+ * it waits only for exchange j of the previous call and runs while the
+ * later chunks still travel (lhpc_dist_chain_parts gives the tile → chunk
+ * map).  Any other x first finishes the pending call.  P2P windows signal
+ * DONE per chunk for this (flag value epoch·64 + chunk + 1; K ≤ 63).
+ * Anchor: the chunked copy/compute overlap of the reference's
+ * lib/gpu/transfer_overlap_testsuite/src/cuda_tut_transfer_overlap.cu:41-142,
+ * carried across steps.
+ */
+int lhpc_dist_spmv_begin(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream);
+int lhpc_dist_spmv_end(lhpc_dist_spmv_plan *d, void *stream);
+/* host only: part[t] for each of the n_tiles x tiles of tile_width columns =
+ * the first exchange chunk j whose end row cuts[(j+1)·nranks] covers the
+ * tile's last column (the order chunks land in) */
+int lhpc_dist_chain_parts(const int64_t *cuts, int nranks, int K, int64_t n_cols, int64_t tile_width,
+                          int32_t *part, int64_t n_tiles);
 /* the exchange of a whole call alone (every chunk, no SpMV): y must already
  * hold this rank's blocks; for exchange-only timing (bench.py --gpus N)    */
 int lhpc_dist_exchange(lhpc_dist_spmv_plan *d, void *y, void *stream);

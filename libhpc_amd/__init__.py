@@ -67,7 +67,8 @@ ABI_SYMBOLS = (
     "lhpc_options_init", "lhpc_spmv_plan_create_opts", "lhpc_blur_x_f32_opts", "lhpc_blur_y_f32_opts",
     "lhpc_stencil7_f32_planes_opts", "lhpc_dist_spmv_plan_create_opts", "lhpc_dist_exchange",
     "lhpc_dist_exchange_schedule", "lhpc_dist_p2p_reset", "lhpc_dist_p2p_unmap", "lhpc_scratch_trim", "lhpc_scratch_poison",
-    "lhpc_spmv_multi", "lhpc_spmv_plan_multi_info",
+    "lhpc_spmv_multi", "lhpc_spmv_plan_multi_info", "lhpc_dist_spmv_begin", "lhpc_dist_spmv_end",
+    "lhpc_dist_chain_parts",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -221,6 +222,9 @@ _sig("lhpc_dist_allreduce_sum_f64", _i, _p, _p, _i64, _p)
 _sig("lhpc_dist_spmv_plan_create", _i, C.POINTER(_p), _p, _i, _i64, _i64, _i, _p, _p, _i, _p, _p, _u)
 _sig("lhpc_dist_spmv_plan_create_opts", _i, C.POINTER(_p), _p, _i, _i64, _i64, _i, _p, _p, _i, _p, _p, _u, _p)
 _sig("lhpc_dist_spmv", _i, _p, _p, _p, _p)
+_sig("lhpc_dist_spmv_begin", _i, _p, _p, _p, _p)
+_sig("lhpc_dist_spmv_end", _i, _p, _p)
+_sig("lhpc_dist_chain_parts", _i, _p, _i, _i, _i64, _i64, _p, _i64)
 _sig("lhpc_dist_exchange", _i, _p, _p, _p)
 _sig("lhpc_dist_exchange_schedule", _i, _p, _i, _i, _i, _i, _i, _p, _i64, C.POINTER(_i64))
 _sig("lhpc_dist_p2p_reset", _i, _p)
@@ -941,6 +945,18 @@ class DistComm:
             pass
 
 
+def dist_chain_parts(cuts, world: int, K: int, n_cols: int, tile_width: int) -> np.ndarray:
+    """lhpc_dist_chain_parts: for each x tile of ``tile_width`` columns, the
+    exchange chunk j after which all its columns have landed (a chained
+    call's gather of the tile waits for exactly that exchange)."""
+    cuts = np.ascontiguousarray(cuts, dtype=np.int64)
+    n_tiles = max(1, -(-int(n_cols) // int(tile_width)))
+    out = np.zeros(n_tiles, dtype=np.int32)
+    _check(lib.lhpc_dist_chain_parts(cuts.ctypes.data, world, K, n_cols, tile_width, out.ctypes.data, n_tiles),
+           "lhpc_dist_chain_parts")
+    return out
+
+
 def interleaved_cuts(row_ptr, world: int, K: int) -> np.ndarray:
     """nnz-balanced row cuts into world·K blocks (block k·world + r = rank r's
     chunk k): lhpc_csr_partition_rows with world·K parts."""
@@ -1020,6 +1036,25 @@ class DistSpMVPlan:
             stream = torch.cuda.current_stream(x.device)
         _check(lib.lhpc_dist_spmv(self._h, x.data_ptr(), y.data_ptr(), _stream_ptr(stream)), "lhpc_dist_spmv")
         return y
+
+    def begin(self, x, y, stream=None):
+        """lhpc_dist_spmv_begin: y = A·x with the exchange of y left in
+        flight; when x is the y of the previous begin, its gather runs by
+        column parts, each waiting only for the exchange that delivers it
+        (cross-step overlap).  ``end`` makes ``stream`` wait for the last
+        begun exchange."""
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream(x.device)
+        _check(lib.lhpc_dist_spmv_begin(self._h, x.data_ptr(), y.data_ptr(), _stream_ptr(stream)),
+               "lhpc_dist_spmv_begin")
+        return y
+
+    def end(self, stream=None):
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream()
+        _check(lib.lhpc_dist_spmv_end(self._h, _stream_ptr(stream)), "lhpc_dist_spmv_end")
 
     def exchange(self, y, stream=None):
         """The call's y exchange alone (every chunk; lhpc_dist_exchange)."""

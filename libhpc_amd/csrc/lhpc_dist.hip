@@ -100,8 +100,14 @@ struct lhpc_dist_spmv_plan {
   std::vector<lhpc_dist_xfer> sched_rccl, sched_p2p;
   std::vector<int64_t> first_rccl, first_p2p;
   std::vector<hipEvent_t> ev;               // [K] chunk k reduced
+  std::vector<hipEvent_t> ev_x;             // [K] chunk k's exchange landed (comm stream)
   hipEvent_t done = nullptr;                // last exchange issued on the comm stream
   hipEvent_t ev_p2p = nullptr;              // P2P: READY signalled on the compute stream
+  // cross-step overlap (lhpc_dist_spmv_begin): the y of a begun call whose
+  // exchange has not been waited for, and whether the local plan can gather
+  // x by column parts (part j = the columns exchange j delivers)
+  const void *pending_y = nullptr;
+  bool chain = false;
 };
 
 namespace {
@@ -271,11 +277,16 @@ int p2p_push(lhpc_dist_comm *c, const P2pWindow *w, int64_t o0, int64_t o1) {
   return static_cast<int>(hipGetLastError());
 }
 
-int p2p_exchange_end(lhpc_dist_comm *c) {
-  hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(64), 0, c->s_comm, c->d_peer_flags, c->nranks + c->rank, c->epoch,
-                     c->nranks, c->rank, c->h_status);
+// after this rank's pushes of chunk j: DONE(j) to every peer (value
+// epoch·64 + j + 1, so one slot per rank carries the chunk progress of the
+// call), then wait for every peer's DONE(j) and drop stale L2 lines of y —
+// from here chunk j of y is complete on this GPU
+int p2p_chunk_done(lhpc_dist_comm *c, int j) {
+  const uint32_t v = c->epoch * 64u + static_cast<uint32_t>(j) + 1u;
+  hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(64), 0, c->s_comm, c->d_peer_flags, c->nranks + c->rank, v, c->nranks,
+                     c->rank, c->h_status);
   LHPC_HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_p2p_wait, dim3(1), dim3(64), 0, c->s_comm, c->flags, c->nranks, c->epoch, c->nranks, c->rank,
+  hipLaunchKernelGGL(k_p2p_wait, dim3(1), dim3(64), 0, c->s_comm, c->flags, c->nranks, v, c->nranks, c->rank,
                      c->h_status);
   LHPC_HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_p2p_acquire_all, dim3(static_cast<unsigned>(c->cus)), dim3(64), 0, c->s_comm);
@@ -287,6 +298,8 @@ void destroy_spmv(lhpc_dist_spmv_plan *d) {
   (void)hipSetDevice(d->comm ? d->comm->device : 0);
   lhpc::local_plans_destroy(d->lp);
   for (hipEvent_t e : d->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : d->ev_x)
     if (e) (void)hipEventDestroy(e);
   if (d->done) (void)hipEventDestroy(d->done);
   if (d->ev_p2p) (void)hipEventDestroy(d->ev_p2p);
@@ -340,7 +353,8 @@ int pick_exchange(const lhpc_dist_spmv_plan *d, const void *y, const P2pWindow *
   return c->comm ? LHPC_DIST_EXCHANGE_RCCL : LHPC_ERR_INVALID_ARG;  // a local comm has no RCCL
 }
 
-// chunk k's exchange on the comm stream, after the compute stream's event
+// chunk k's exchange on the comm stream, after the compute stream's event;
+// ev_x[k] marks it landed on this rank
 int exchange_chunk(lhpc_dist_spmv_plan *d, int xk, const P2pWindow *w, int k, void *y, hipStream_t s) {
   lhpc_dist_comm *c = d->comm;
   LHPC_HIP_TRY(hipEventRecord(d->ev[k], s));
@@ -352,9 +366,20 @@ int exchange_chunk(lhpc_dist_spmv_plan *d, int xk, const P2pWindow *w, int k, vo
       const lhpc_dist_xfer &x = d->sched_p2p[e];
       LHPC_TRY(p2p_push(c, w, x.offset * tsz, (x.offset + x.count) * tsz));
     }
-    return LHPC_OK;
+    LHPC_TRY(p2p_chunk_done(c, k));
+  } else {
+    LHPC_TRY(issue_rccl_chunk(d, k, y, c->s_comm));
   }
-  return issue_rccl_chunk(d, k, y, c->s_comm);
+  LHPC_HIP_TRY(hipEventRecord(d->ev_x[k], c->s_comm));
+  return LHPC_OK;
+}
+
+// a begun call's exchange, waited for on `s` (lhpc_dist_spmv_end)
+int wait_pending(lhpc_dist_spmv_plan *d, hipStream_t s) {
+  if (!d->pending_y) return LHPC_OK;
+  d->pending_y = nullptr;
+  LHPC_HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
+  return LHPC_OK;
 }
 
 }  // namespace
@@ -374,6 +399,21 @@ extern "C" int lhpc_dist_exchange_schedule(const int64_t *cuts, int nranks, int 
   *n_out = static_cast<int64_t>(v.size());
   if (static_cast<int64_t>(v.size()) > max_out) return LHPC_ERR_INVALID_ARG;
   if (!v.empty()) std::memcpy(out, v.data(), v.size() * sizeof(lhpc_dist_xfer));
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_chain_parts(const int64_t *cuts, int nranks, int K, int64_t n_cols, int64_t tile_width,
+                                     int32_t *part, int64_t n_tiles) {
+  if (!cuts || nranks < 1 || K < 1 || n_cols < 0 || tile_width < 1 || !part ||
+      n_tiles < (n_cols + tile_width - 1) / tile_width)
+    return LHPC_ERR_INVALID_ARG;
+  std::vector<int64_t> col_end(static_cast<size_t>(K));
+  for (int j = 0; j < K; ++j) col_end[static_cast<size_t>(j)] = cuts[static_cast<int64_t>(j + 1) * nranks];
+  for (int j = 0; j < K; ++j)
+    if (j > 0 && col_end[j] < col_end[j - 1]) return LHPC_ERR_INVALID_ARG;
+  if (col_end[K - 1] < n_cols) return LHPC_ERR_INVALID_ARG;  // the chunks must cover x
+  for (int64_t t = 0; t < n_tiles; ++t)
+    part[t] = static_cast<int32_t>(lhpc::xtile_part_of_tile(t, tile_width, n_cols, col_end.data(), K));
   return LHPC_OK;
 }
 
@@ -638,6 +678,7 @@ extern "C" int lhpc_dist_spmv_plan_create_opts(lhpc_dist_spmv_plan **out, lhpc_d
     if (cuts[b + 1] < cuts[b]) return LHPC_ERR_INVALID_ARG;
   const lhpc_options o = lhpc::resolve_options(opts);
   if (o.dist_exchange < LHPC_DIST_EXCHANGE_AUTO || o.dist_exchange > LHPC_DIST_EXCHANGE_NONE) return LHPC_ERR_INVALID_ARG;
+  if (K > 63) return LHPC_ERR_INVALID_ARG;  // the P2P DONE flag carries the chunk in 6 bits
   LHPC_HIP_TRY(hipSetDevice(comm->device));
   auto *d = new (std::nothrow) lhpc_dist_spmv_plan();
   if (!d) return LHPC_ERR_ALLOC;
@@ -658,8 +699,18 @@ extern "C" int lhpc_dist_spmv_plan_create_opts(lhpc_dist_spmv_plan **out, lhpc_d
   }
   int st = lhpc::local_plans_create(d->lp, dtype, n_cols, K, ls.data(), row_ptr, row_ptr_bits, col_idx, val,
                                     comm->device, flags, o);
+  // column parts of the stage for chained calls (square matrices: chunk j's
+  // rows of y are columns [cuts[j·N], cuts[(j+1)·N]) of the next x)
+  if (st == LHPC_OK && n_rows == n_cols) {
+    std::vector<int64_t> col_end(static_cast<size_t>(K));
+    for (int j = 0; j < K; ++j) col_end[static_cast<size_t>(j)] = cuts[static_cast<int64_t>(j + 1) * nr];
+    d->chain = lhpc::local_plans_column_parts(d->lp, col_end.data(), K);
+  }
   if (st == LHPC_OK) {
     d->ev.assign(static_cast<size_t>(K), nullptr);
+    d->ev_x.assign(static_cast<size_t>(K), nullptr);
+    for (auto &e : d->ev_x)
+      if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto &e : d->ev)
       if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->done, hipEventDisableTiming));
@@ -681,7 +732,7 @@ extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_c
                                          val, flags, nullptr);
 }
 
-extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream) {
+extern "C" int lhpc_dist_spmv_begin(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream) {
   if (!d || (d->n_cols > 0 && !x) || (d->n_rows > 0 && !y) || (x == y && d->n_rows > 0)) return LHPC_ERR_INVALID_ARG;
   lhpc_dist_comm *c = d->comm;
   lhpc::RocTxRange rx("lhpc_dist_spmv");
@@ -692,10 +743,27 @@ extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, vo
   const P2pWindow *win = nullptr;
   const int xk = pick_exchange(d, y, &win);
   if (xk < 0) return xk;
+  // x is the y of the begun call before (chained): its exchange is still in
+  // flight; with column parts, part j of the stage waits only for exchange j
+  // of that call and runs while the later chunks travel (cross-step overlap),
+  // else the stage waits for the whole exchange.  Any other x: the begun
+  // call is finished first.
+  const bool chained = d->pending_y && d->pending_y == x;
+  if (d->pending_y && !chained) LHPC_TRY(wait_pending(d, s));
   if (xk == LHPC_DIST_EXCHANGE_P2P) LHPC_TRY(p2p_exchange_begin(c, s, d->ev_p2p));
   const bool xchg = xk != LHPC_DIST_EXCHANGE_NONE;
   int gathered = 0;  // ranges of a range-gather plan gathered so far (in order)
-  LHPC_TRY(lhpc::local_plans_stage(d->lp, x, s));
+  if (chained && d->chain) {
+    lhpc::RocTxRange rc("lhpc_dist_spmv: chained stage");
+    for (int j = 0; j < d->K; ++j) {
+      LHPC_HIP_TRY(hipStreamWaitEvent(s, d->ev_x[j], 0));
+      LHPC_TRY(lhpc::local_plans_stage_part(d->lp, x, j, s));
+    }
+    d->pending_y = nullptr;
+  } else {
+    if (chained) LHPC_TRY(wait_pending(d, s));
+    LHPC_TRY(lhpc::local_plans_stage(d->lp, x, s));
+  }
   for (int k = 0; k < d->K; ++k) {
     const int64_t b = static_cast<int64_t>(k) * c->nranks + c->rank;
     void *yk = static_cast<unsigned char *>(y) + d->cuts[b] * tsz;
@@ -703,11 +771,21 @@ extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, vo
     if (xchg) LHPC_TRY(exchange_chunk(d, xk, win, k, y, s));
   }
   if (xchg) {
-    if (xk == LHPC_DIST_EXCHANGE_P2P) LHPC_TRY(p2p_exchange_end(c));
     LHPC_HIP_TRY(hipEventRecord(d->done, c->s_comm));
-    LHPC_HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
+    d->pending_y = y;
   }
   return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_spmv_end(lhpc_dist_spmv_plan *d, void *stream) {
+  if (!d) return LHPC_ERR_INVALID_ARG;
+  LHPC_HIP_TRY(hipSetDevice(d->comm->device));
+  return wait_pending(d, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream) {
+  LHPC_TRY(lhpc_dist_spmv_begin(d, x, y, stream));
+  return lhpc_dist_spmv_end(d, stream);
 }
 
 extern "C" int lhpc_dist_exchange(lhpc_dist_spmv_plan *d, void *y, void *stream) {
@@ -716,13 +794,13 @@ extern "C" int lhpc_dist_exchange(lhpc_dist_spmv_plan *d, void *y, void *stream)
   lhpc::RocTxRange rx("lhpc_dist_exchange");
   LHPC_HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  LHPC_TRY(wait_pending(d, s));
   const P2pWindow *win = nullptr;
   const int xk = pick_exchange(d, y, &win);
   if (xk < 0) return xk;
   if (xk == LHPC_DIST_EXCHANGE_NONE) return LHPC_OK;
   if (xk == LHPC_DIST_EXCHANGE_P2P) LHPC_TRY(p2p_exchange_begin(c, s, d->ev_p2p));
   for (int k = 0; k < d->K; ++k) LHPC_TRY(exchange_chunk(d, xk, win, k, y, s));
-  if (xk == LHPC_DIST_EXCHANGE_P2P) LHPC_TRY(p2p_exchange_end(c));
   LHPC_HIP_TRY(hipEventRecord(d->done, c->s_comm));
   LHPC_HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
   return LHPC_OK;

@@ -106,6 +106,16 @@ int local_plans_stage(const LocalPlans &lp, const void *x, hipStream_t s) {
   return LHPC_OK;
 }
 
+bool local_plans_column_parts(LocalPlans &lp, const int64_t *col_end, int n_parts) {
+  if (!lp.split || lp.range_gather()) return false;
+  return xtile_column_parts(lp.split, col_end, n_parts) == LHPC_OK;
+}
+
+int local_plans_stage_part(const LocalPlans &lp, const void *x, int j, hipStream_t s) {
+  if (!lp.column_parts()) return LHPC_ERR_UNSUPPORTED;
+  return xtile_stage_part(lp.split, x, j, s);
+}
+
 int local_plans_chunk(const LocalPlans &lp, const void *x, int k, void *yk, int &gathered, hipStream_t s) {
   const int r = lp.range_of[static_cast<size_t>(k)];
   if (r < 0) return LHPC_OK;  // empty block

@@ -484,6 +484,7 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
                   static_cast<void *>(p->d_dpart), static_cast<void *>(p->d_cdesc), static_cast<void *>(p->d_cr),
                   static_cast<void *>(p->d_seghi), static_cast<void *>(p->d_seg), static_cast<void *>(p->d_pieces), static_cast<void *>(p->d_cont),
                   static_cast<void *>(p->d_col16), static_cast<void *>(p->d_perm), p->d_xg,
+                  static_cast<void *>(p->d_pieces_cp),
                   static_cast<void *>(p->d_carry)})
     if (q) (void)hipFree(q);
   if (p->h_scalars) (void)hipHostFree(p->h_scalars);

@@ -60,6 +60,12 @@ struct lhpc_spmv_plan {
   int xt_al = 0;  // aligned segments: 16-B units (lhpc_options.xtile_align)
   void *d_xg = nullptr;
   double *d_carry = nullptr;
+  // column parts (xtile_column_parts): the gather pieces reordered so that
+  // part j = pieces [xt_cpf[j], xt_cpf[j+1]) of d_pieces_cp reads x only
+  // below column xt_cpe[j] (a chained distributed call gathers part j as
+  // soon as exchange j of the previous call has landed)
+  int32_t *d_pieces_cp = nullptr;
+  std::vector<int64_t> xt_cpf, xt_cpe;
   // XTILE row parts (lhpc_options.xtile_part_nnz): a matrix whose tile stream
   // exceeds the int32 stream offsets is cut into nnz-balanced row parts, one
   // XTILE plan each (rows [part_row[i], part_row[i+1]) of y), run in turn on
@@ -108,6 +114,7 @@ struct LocalPlans {
   // a split plan with per-range gather pieces (its xg exceeds the Infinity
   // Cache) gathers each range right before reducing it; else one stage
   bool range_gather() const { return split && !split->xt_rpc.empty(); }
+  bool column_parts() const { return split && !split->xt_cpf.empty(); }
 };
 // ls: K + 1 local row offsets; row_ptr/col/val: the local CSR (host)
 int local_plans_create(LocalPlans &lp, int dtype, int64_t n_cols, int K, const int64_t *ls, const void *row_ptr,
@@ -116,6 +123,10 @@ int local_plans_create(LocalPlans &lp, int dtype, int64_t n_cols, int K, const i
 void local_plans_destroy(LocalPlans &lp);
 // the call's stage (all of x's tiles; no-op for range-gather and block plans)
 int local_plans_stage(const LocalPlans &lp, const void *x, hipStream_t s);
+// column parts of the stage (a split plan without range gathers only):
+// col_end as for xtile_column_parts; false when unavailable
+bool local_plans_column_parts(LocalPlans &lp, const int64_t *col_end, int n_parts);
+int local_plans_stage_part(const LocalPlans &lp, const void *x, int j, hipStream_t s);
 // chunk k's rows into yk (its first row at yk[0]); `gathered` counts the
 // ranges a range-gather plan has gathered so far in this call (start at 0)
 int local_plans_chunk(const LocalPlans &lp, const void *x, int k, void *yk, int &gathered, hipStream_t s);
@@ -155,6 +166,14 @@ int xtile_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s)
 int xtile_stage(const lhpc_spmv_plan *p, const void *x, hipStream_t s);
 int xtile_range_gather(const lhpc_spmv_plan *p, const void *x, int k, hipStream_t s);
 int xtile_range(const lhpc_spmv_plan *p, int k, void *yk, hipStream_t s);
+// column parts: col_end[j] ascending, col_end[n_parts-1] ≥ n_cols; tile t goes
+// to the first part whose bound covers its last column.  LHPC_ERR_UNSUPPORTED
+// for plans that gather per row range (cache-sized ranges).
+int xtile_column_parts(lhpc_spmv_plan *p, const int64_t *col_end, int n_parts);
+// the first part whose bound covers the tile's last column (host rule shared
+// with lhpc_dist_chain_parts)
+int xtile_part_of_tile(int64_t tile, int64_t tile_width, int64_t n_cols, const int64_t *col_end, int n_parts);
+int xtile_stage_part(const lhpc_spmv_plan *p, const void *x, int j, hipStream_t s);
 // LHPC_ERR_UNSUPPORTED: the layout does not fit its index types (caller falls back)
 int xtile_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz);
 

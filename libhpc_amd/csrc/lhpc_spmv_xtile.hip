@@ -675,29 +675,31 @@ const void *xtile_reduce_fn(int g, bool ip, bool al) {
 }
 
 template <typename T, int U, bool NT = false>
-void gather_u(const lhpc_spmv_plan *p, const void *x, int64_t q0, int64_t q1, hipStream_t s) {
+void gather_u(const lhpc_spmv_plan *p, const int32_t *pieces, const void *x, int64_t q0, int64_t q1, hipStream_t s) {
   hipLaunchKernelGGL((k_xtile_gather<T, U, NT>), dim3(static_cast<unsigned>(q1 - q0)), dim3(kXtGatherBlock), 0, s,
-                     p->d_pieces + 3 * q0, p->d_col16, static_cast<const T *>(x), p->n_cols,
+                     pieces + 3 * q0, p->d_col16, static_cast<const T *>(x), p->n_cols,
                      static_cast<int>(p->xs_width), static_cast<T *>(p->d_xg));
 }
 
-// gather pieces [q0, q1) (default: all)
+// gather pieces [q0, q1) (default: all) of `pieces` (default: the plan's)
 template <typename T>
-int launch_gather(const lhpc_spmv_plan *p, const void *x, hipStream_t s, int64_t q0 = 0, int64_t q1 = -1) {
+int launch_gather(const lhpc_spmv_plan *p, const void *x, hipStream_t s, int64_t q0 = 0, int64_t q1 = -1,
+                  const int32_t *pieces = nullptr) {
   if (q1 < 0) q1 = p->xt_pieces;
   if (q1 <= q0) return LHPC_OK;
+  if (!pieces) pieces = p->d_pieces;
   if (p->xt_nt) {
-    gather_u<T, 8, true>(p, x, q0, q1, s);
+    gather_u<T, 8, true>(p, pieces, x, q0, q1, s);
     return check_launch(s);
   }
   switch (p->xt_u) {
-    case 2: gather_u<T, 2>(p, x, q0, q1, s); break;
-    case 4: gather_u<T, 4>(p, x, q0, q1, s); break;
+    case 2: gather_u<T, 2>(p, pieces, x, q0, q1, s); break;
+    case 4: gather_u<T, 4>(p, pieces, x, q0, q1, s); break;
     case 16:  // fp64 at 16 steps needs > 128 VGPRs (it spilled 22): capped at 8
-      if constexpr (sizeof(T) == 8) gather_u<T, 8>(p, x, q0, q1, s);
-      else gather_u<T, 16>(p, x, q0, q1, s);
+      if constexpr (sizeof(T) == 8) gather_u<T, 8>(p, pieces, x, q0, q1, s);
+      else gather_u<T, 16>(p, pieces, x, q0, q1, s);
       break;
-    default: gather_u<T, 8>(p, x, q0, q1, s); break;
+    default: gather_u<T, 8>(p, pieces, x, q0, q1, s); break;
   }
   return check_launch(s);
 }
@@ -795,11 +797,18 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   // x (n_cols·T) in its gather.  Same box: C2 reduce 352 → 295
   // µs, gather 163 → 179 µs, call 523.5 → 483.8 µs at K = 3 (K = 4: 506.7);
   // C3 (fp64, K = 6: 200 MB ranges) 928 → 944 µs, so not for fp64
+  // Only while each range still streams ≥ min_piece nonzeros per tile and
+  // K ≤ 8: every range re-loads all S tiles of x, so a wide x (n = 80M:
+  // 1954 tiles; n = 150M: 3662) would spend more on tile loads than the
+  // cache saves — such plans keep one range (the n = 150M plan took 23.6 ms
+  // with 8 ranges per part)
   int mall = 0;
   {
     const int64_t xg_bytes = p->nnz * static_cast<int64_t>(tsz);
-    if (tsz == 4 && xg_bytes > (int64_t{256} << 20))
-      mall = static_cast<int>(std::min<int64_t>(8, (xg_bytes + (int64_t{200} << 20) - 1) / (int64_t{200} << 20)));
+    const int64_t k = (xg_bytes + (int64_t{200} << 20) - 1) / (int64_t{200} << 20);
+    const int64_t tiles = (p->n_cols + W - 1) / W;
+    if (tsz == 4 && xg_bytes > (int64_t{256} << 20) && k <= 8 && p->nnz / k / std::max<int64_t>(1, tiles) >= min_piece)
+      mall = static_cast<int>(k);
   }
   if (o.xtile_ranges > 0) mall = o.xtile_ranges;
   // a row-range plan (user splits) whose xg exceeds the cache gets per-range
@@ -958,6 +967,46 @@ int xtile_range(const lhpc_spmv_plan *p, int k, void *yk, hipStream_t s) {
   if (p->dtype == LHPC_F32)
     return launch_reduce<float>(p, c0, c1, n0, n1, static_cast<float *>(yk) - p->xt_srow[k], s);
   return launch_reduce<double>(p, c0, c1, n0, n1, static_cast<double *>(yk) - p->xt_srow[k], s);
+}
+
+int xtile_part_of_tile(int64_t tile, int64_t tile_width, int64_t n_cols, const int64_t *col_end, int n_parts) {
+  const int64_t last = std::min((tile + 1) * tile_width, n_cols);  // exclusive end of the tile's columns
+  for (int j = 0; j < n_parts; ++j)
+    if (col_end[j] >= last) return j;
+  return n_parts - 1;
+}
+
+int xtile_column_parts(lhpc_spmv_plan *p, const int64_t *col_end, int n_parts) {
+  if (p->kernel != LHPC_KERNEL_XTILE || !p->xt_rpc.empty() || n_parts < 1) return LHPC_ERR_UNSUPPORTED;
+  for (int j = 0; j < n_parts; ++j)
+    if (col_end[j] < 0 || (j > 0 && col_end[j] < col_end[j - 1])) return LHPC_ERR_INVALID_ARG;
+  if (col_end[n_parts - 1] < p->n_cols) return LHPC_ERR_INVALID_ARG;
+  const int64_t np = p->xt_pieces;
+  std::vector<int32_t> pc(static_cast<size_t>(3 * np)), out;
+  out.reserve(pc.size());
+  LHPC_HIP_TRY(hipSetDevice(p->device));
+  if (np) LHPC_HIP_TRY(hipMemcpy(pc.data(), p->d_pieces, pc.size() * 4, hipMemcpyDeviceToHost));
+  // stable partition by part: the pieces are in ascending runs of 8 tiles,
+  // so each part keeps the run order (and its same-XCD tile interleave)
+  p->xt_cpf.assign(1, 0);
+  for (int j = 0; j < n_parts; ++j) {
+    for (int64_t q = 0; q < np; ++q)
+      if (xtile_part_of_tile(pc[3 * q + 2], p->xs_width, p->n_cols, col_end, n_parts) == j)
+        out.insert(out.end(), pc.begin() + 3 * q, pc.begin() + 3 * q + 3);
+    p->xt_cpf.push_back(static_cast<int64_t>(out.size() / 3));
+  }
+  if (p->d_pieces_cp) (void)hipFree(p->d_pieces_cp);
+  p->d_pieces_cp = nullptr;
+  LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_pieces_cp), out.size() * 4, p->bytes));
+  if (!out.empty()) LHPC_HIP_TRY(hipMemcpy(p->d_pieces_cp, out.data(), out.size() * 4, hipMemcpyHostToDevice));
+  p->xt_cpe.assign(col_end, col_end + n_parts);
+  return LHPC_OK;
+}
+
+int xtile_stage_part(const lhpc_spmv_plan *p, const void *x, int j, hipStream_t s) {
+  if (p->xt_cpf.empty() || j < 0 || j + 2 > static_cast<int>(p->xt_cpf.size())) return LHPC_ERR_INVALID_ARG;
+  return p->dtype == LHPC_F32 ? launch_gather<float>(p, x, s, p->xt_cpf[j], p->xt_cpf[j + 1], p->d_pieces_cp)
+                              : launch_gather<double>(p, x, s, p->xt_cpf[j], p->xt_cpf[j + 1], p->d_pieces_cp);
 }
 
 int xtile_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz) {

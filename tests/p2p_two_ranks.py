@@ -20,6 +20,9 @@ Cases (argv[1]):
             windows up again: its P2P calls are bit-exact
   reset     P2P calls, a collective lhpc_dist_p2p_reset (new flag arrays),
             re-export / import (peers' flags remapped by generation), calls
+  chain     cross-step overlap: five chained lhpc_dist_spmv_begin calls over
+            two windows (y of call n is x of call n+1), no end in between —
+            each stage's column part waits for the previous call's DONE(j)
 """
 import json
 import os
@@ -192,6 +195,37 @@ elif case == "reset":
         comm.p2p_reset()  # collective: every rank, then a barrier before re-export
         dist.barrier()
     comm.close()
+elif case == "chain":
+    steps = 5
+    for n, per_row, K, dt in ((3_000_000, 4, 2, L.F32), (40_000, 3, 3, L.F64)):
+        rp, col, val, x, cuts, local = problem(n, per_row, K, dt, 0xE600 + K)
+        want = iterate_oracle(rp, col, val, x, steps)
+        comm = L.DistComm.local(world, rank, 0)
+        s = torch.cuda.current_stream(dev)
+        xd = torch.from_numpy(x).to(dev)
+        ya = torch.full((n,), float("nan"), dtype=xd.dtype, device=dev)
+        yb = torch.full((n,), float("nan"), dtype=xd.dtype, device=dev)
+        comm.p2p_setup_torch(ya)
+        comm.p2p_setup_torch(yb)
+        torch.cuda.synchronize()
+        dist.barrier()
+        snaps = []
+        with L.DistSpMVPlan(comm, n, n, K, cuts, *local, options={"dist_exchange": L.DIST_EXCHANGE_P2P}) as d:
+            cur = xd
+            for it in range(steps):
+                dst = ya if it % 2 == 0 else yb
+                d.begin(cur, dst, stream=s)
+                if it > 0:
+                    snaps.append(cur.clone())  # complete once this call's chained stage waited for it
+                cur = dst
+            d.end(stream=s)
+            snaps.append(cur.clone())
+            torch.cuda.synchronize()
+        for it in range(steps):
+            out["ok"].append(bool(np.array_equal(snaps[it].cpu().numpy(), want[it])))
+        dist.barrier()
+        out["status"].append(comm.p2p_status())
+        comm.close()
 else:
     raise SystemExit(f"unknown case {case}")
 print(json.dumps(out), flush=True)

@@ -278,3 +278,44 @@ def test_exchange_schedule_rejects_bad_input():
         L.dist_exchange_schedule([0, 5, 3, 8, 9], 2, 2, 0)  # cuts not ascending
     with pytest.raises(L.LhpcError):
         L.dist_exchange_schedule([0, 1, 2, 3, 4], 2, 2, 2)  # rank out of range
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("K", [1, 2, 3, 4])
+@pytest.mark.parametrize("kind", ["uniform", "powerlaw", "empty"])
+@pytest.mark.parametrize("tile_width", [1, 7, 4096, 39063])
+def test_chain_parts_schedule(world, K, kind, tile_width):
+    """The cross-step overlap's schedule (lhpc_dist_chain_parts, the host rule
+    the chained stage of lhpc_dist_spmv_begin follows): tile t's gather
+    waits for exchange part[t].  Exchanges land in chunk order and chunk j
+    delivers rows [cuts[j·N], cuts[(j+1)·N]) of y = those columns of the next
+    x.  Every column a tile reads must have landed (it lies below
+    cuts[(part+1)·N]), the part is the earliest such chunk (the tile waits no
+    longer than it must), and the parts never decrease along x."""
+    import libhpc_amd as L
+    if kind == "powerlaw":
+        n = 30_011
+        rp, _, _ = L.gen_powerlaw_csr(n, n, lmax=2000, dtype=L.F32, dist=1, seed=0xD190)
+    elif kind == "uniform":
+        n = 4_096 * world * K + 13
+        rp, _, _ = L.gen_uniform_csr(n, n, 5, dtype=L.F32, dist=1, seed=0xD191)
+    else:
+        n = 5  # fewer rows than blocks: empty chunks
+        rp, _, _ = L.gen_uniform_csr(n, n, 2, dtype=L.F32, dist=1, seed=0xD192)
+    cuts = L.interleaved_cuts(rp, world, K)
+    part = L.dist_chain_parts(cuts, world, K, n, tile_width)
+    landed = [int(cuts[(j + 1) * world]) for j in range(K)]  # columns complete after exchange j
+    for t, j in enumerate(part):
+        last = min((t + 1) * tile_width, n)  # exclusive end of the tile's columns
+        assert 0 <= j < K and landed[j] >= last, (t, j)
+        assert j == 0 or landed[j - 1] < last, (t, j)
+    assert np.all(np.diff(part) >= 0)
+
+
+def test_chain_parts_rejects_bad_input():
+    import libhpc_amd as L
+    cuts = np.array([0, 5, 10], dtype=np.int64)
+    with pytest.raises(L.LhpcError):
+        L.dist_chain_parts(cuts, 2, 1, 11, 4)  # the chunks do not cover x
+    with pytest.raises(L.LhpcError):
+        L.dist_chain_parts(np.array([0, 6, 4, 10], dtype=np.int64), 1, 3, 10, 4)  # not ascending

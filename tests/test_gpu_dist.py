@@ -93,6 +93,50 @@ def test_dist_spmv_world1_rccl_exchange(lhpc, gpu, comm, mode, uniform):
         assert np.array_equal(y.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("K", [1, 2, 3, 4])
+@pytest.mark.parametrize("case", [(3_000_000, 6, "f32"), (2_500_000, 5, "f64"), (20_000, 7, "f64")],
+                         ids=["xtile-f32", "xtile-f64", "blocks-f64"])
+def test_dist_spmv_chained_world1(lhpc, gpu, comm, K, case):
+    """Cross-step overlap (lhpc_dist_spmv_begin / _end) at world 1 with the
+    RCCL exchange issued (options.dist_world1): five chained calls, y of call
+    n is x of call n+1 (ping-pong), no end between them — each chained stage
+    gathers x by column parts, part j waiting only for exchange j of the call
+    before (XTILE row-range plans; the per-block plans of the small matrix
+    wait for the whole exchange instead).  Every iterate equals the oracle's
+    bit for bit (dyadic values; snapshots of y(n) taken on the stream after
+    the chained stage of call n+1 has waited for it)."""
+    import torch
+    n, per_row, dts = case
+    dt = lhpc.F32 if dts == "f32" else lhpc.F64
+    rp, col, val = lhpc.gen_uniform_csr(n, n, per_row, dtype=dt, dist=1, seed=0xD400 + K)
+    x = lhpc.gen_values(dt, 1, n, 0xD401)
+    steps = 5
+    want, cur = [], x
+    for _ in range(steps):
+        _, cur, _ = S.spmv_oracle(rp, col, val, cur)
+        want.append(cur)
+    cuts = lhpc.interleaved_cuts(rp, 1, K)
+    s = torch.cuda.current_stream(gpu)
+    with lhpc.DistSpMVPlan(comm, n, n, K, cuts, *lhpc.interleaved_local_csr(rp, col, val, cuts, 1, K, 0),
+                           options={"dist_world1": 1}) as d:
+        bufs = [torch.from_numpy(x).to(gpu), torch.full((n,), float("nan"), dtype=torch.float32 if dts == "f32"
+                                                        else torch.float64, device=gpu)]
+        bufs.append(torch.full_like(bufs[1], float("nan")))
+        snaps = []
+        cur_x = bufs[0]
+        for it in range(steps):
+            y = bufs[1 + it % 2]
+            d.begin(cur_x, y, stream=s)
+            if it > 0:
+                snaps.append(cur_x.clone())  # y of call it-1: complete once call it's stage waited for it
+            cur_x = y
+        d.end(stream=s)
+        snaps.append(cur_x.clone())
+        torch.cuda.synchronize()
+    for it in range(steps):
+        assert np.array_equal(snaps[it].cpu().numpy(), want[it]), it
+
+
 def test_dist_spmv_rejects_aliased_xy(lhpc, gpu, comm):
     import torch
     n = 1000
@@ -119,7 +163,7 @@ def test_dist_stencil7_world1_matches_single_domain(lhpc, gpu, comm, nz, ny, nx)
     assert np.array_equal(od.cpu().numpy(), want)
 
 
-P2P_CASES = {"barrier": 6, "loop": 8, "pingpong": 8, "tiny": 8, "rollback": 4, "reset": 6}
+P2P_CASES = {"barrier": 6, "loop": 8, "pingpong": 8, "tiny": 8, "rollback": 4, "reset": 6, "chain": 10}
 
 
 @pytest.mark.parametrize("case", list(P2P_CASES))
@@ -135,8 +179,10 @@ def test_dist_spmv_p2p_two_ranks_one_gpu(lhpc, gpu, case):
     16-B phase; a setup whose import fails on one rank rolled back on both
     (then an AUTO call refused on both, and a fresh setup bit-exact); three
     rounds of setup / calls / collective reset (flag arrays re-allocated and
-    remapped by generation).  (On one GPU the pushes are device-local; over
-    xGMI they are the same stores.)"""
+    remapped by generation); chained calls (lhpc_dist_spmv_begin: the
+    stage's column part j waits for the previous call's per-chunk DONE(j)
+    flags, ping-pong windows, five calls, one end).  (On one GPU the pushes
+    are device-local; over xGMI they are the same stores.)"""
     import json
     import os
     import subprocess
