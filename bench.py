@@ -98,6 +98,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--chunks", type=int, default=2, help="N>1: row chunks per rank (all-gather overlap; DESIGN.md §6)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--spmv-options", default=None,
+                    help="JSON dict of lhpc_options fields for the 1-GPU SpMV plan (measured alternatives, DESIGN.md §4)")
     ap.add_argument("--dtype", default="auto", choices=["auto", "f32", "f64"],
                     help="SpMV value type (auto: the config's own — fp64 for c1/c3, fp32 for c2/c4; "
                          "SURVEY §8d also runs C4 in fp64)")
@@ -207,7 +209,8 @@ def main():
         xd = torch.from_numpy(x).to(dev)
         t0 = time.time()
         if world == 1 and not native_dist:
-            plans = [L.SpMVPlan(rp, col, val, n)]
+            plans = [L.SpMVPlan(rp, col, val, n,
+                                options=json.loads(args.spmv_options) if args.spmv_options else None)]
             local_nnz, local_rows = nnz, n
             y_local = torch.empty(n, dtype=xd.dtype, device=dev)
 

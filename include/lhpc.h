@@ -522,8 +522,13 @@ int lhpc_dist_comm_create(lhpc_dist_comm **out, const unsigned char *id, int nra
                           int device);
 int lhpc_dist_comm_info(const lhpc_dist_comm *comm, int *nranks, int *rank, int *device);
 int lhpc_dist_comm_destroy(lhpc_dist_comm *comm);
-/* in-place sum over ranks of `count` doubles (the CG dots), async on stream */
+/* in-place sum over ranks of `count` doubles (the CG dots), async on
+ * stream: ncclAllReduce, or over a P2P communicator (lhpc_dist_comm_create_local,
+ * after a window import) every rank's values gathered through the flag
+ * allocation's scalar slots and added in rank order (count ≤ 8).
+ * lhpc_dist_allgather_f64: out[r·count + i] = rank r's vals[i] (same paths)  */
 int lhpc_dist_allreduce_sum_f64(lhpc_dist_comm *comm, double *buf, int64_t count, void *stream);
+int lhpc_dist_allgather_f64(lhpc_dist_comm *comm, const double *vals, int64_t count, double *out, void *stream);
 /*
  * Distributed y = A·x.  The n_rows rows are cut into nranks·K blocks by
  * `cuts` (nranks·K + 1 ascending global rows, cuts[0] = 0; nnz-balanced:
@@ -577,6 +582,24 @@ int lhpc_dist_chain_parts(const int64_t *cuts, int nranks, int K, int64_t n_cols
 /* the exchange of a whole call alone (every chunk, no SpMV): y must already
  * hold this rank's blocks; for exchange-only timing (bench.py --gpus N)    */
 int lhpc_dist_exchange(lhpc_dist_spmv_plan *d, void *y, void *stream);
+/*
+ * Conjugate gradient over a distributed plan (SURVEY §8f rank 3 with the
+ * multi-GPU path; square SPD matrix).  b, x and p_work are full-length
+ * (n_rows) device vectors of the plan's dtype on this rank's device: b is
+ * read on this rank's rows, x is the initial guess (complete on every rank)
+ * and on return holds the whole solution on every rank, p_work is the search
+ * direction — register it as a P2P window (lhpc_dist_p2p_export/_import) to
+ * exchange it by peer stores, else the plan's RCCL exchange.  Per iteration:
+ * q = A·p on this rank's rows (a chained stage: part j of p is gathered as
+ * soon as exchange j of p has landed), the dots p·q and r·r as K block
+ * partials per rank all-gathered and added in global block order (so the
+ * solve is independent of how the same block split is spread over ranks),
+ * the fused x/r/p updates on this rank's rows, and the exchange of p's
+ * blocks.  K ≤ 8.  Stops as lhpc_cg_solve; LHPC_ERR_INTERNAL on breakdown or
+ * a timed-out P2P flag wait.  Synchronous (host checks every check_every).
+ */
+int lhpc_dist_cg_solve(lhpc_dist_spmv_plan *d, const void *b, void *x, void *p_work, double tol,
+                       int max_iter, int check_every, int *iters_out, double *resid_out, void *stream);
 int lhpc_dist_spmv_plan_destroy(lhpc_dist_spmv_plan *d);
 /*
  * The exchange schedule of lhpc_dist_spmv, as data (host only; the call

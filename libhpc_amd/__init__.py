@@ -68,7 +68,7 @@ ABI_SYMBOLS = (
     "lhpc_stencil7_f32_planes_opts", "lhpc_dist_spmv_plan_create_opts", "lhpc_dist_exchange",
     "lhpc_dist_exchange_schedule", "lhpc_dist_p2p_reset", "lhpc_dist_p2p_unmap", "lhpc_scratch_trim", "lhpc_scratch_poison",
     "lhpc_spmv_multi", "lhpc_spmv_plan_multi_info", "lhpc_dist_spmv_begin", "lhpc_dist_spmv_end",
-    "lhpc_dist_chain_parts",
+    "lhpc_dist_chain_parts", "lhpc_dist_allgather_f64", "lhpc_dist_cg_solve",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -219,6 +219,8 @@ _sig("lhpc_dist_comm_create", _i, C.POINTER(_p), _p, _i, _i, _i)
 _sig("lhpc_dist_comm_info", _i, _p, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i))
 _sig("lhpc_dist_comm_destroy", _i, _p)
 _sig("lhpc_dist_allreduce_sum_f64", _i, _p, _p, _i64, _p)
+_sig("lhpc_dist_allgather_f64", _i, _p, _p, _i64, _p, _p)
+_sig("lhpc_dist_cg_solve", _i, _p, _p, _p, _p, _d, _i, _i, C.POINTER(_i), C.POINTER(_d), _p)
 _sig("lhpc_dist_spmv_plan_create", _i, C.POINTER(_p), _p, _i, _i64, _i64, _i, _p, _p, _i, _p, _p, _u)
 _sig("lhpc_dist_spmv_plan_create_opts", _i, C.POINTER(_p), _p, _i, _i64, _i64, _i, _p, _p, _i, _p, _p, _u, _p)
 _sig("lhpc_dist_spmv", _i, _p, _p, _p, _p)
@@ -919,6 +921,11 @@ class DistComm:
         dist.broadcast(t, 0, group=group)
         return cls(t.cpu().numpy().tobytes(), world, rank, device)
 
+    def allgather_f64(self, t, out, stream=None):
+        _check(lib.lhpc_dist_allgather_f64(self._h, t.data_ptr(), t.numel(), out.data_ptr(), _stream_ptr(stream)),
+               "lhpc_dist_allgather_f64")
+        return out
+
     def allreduce_sum_f64(self, t, stream=None):
         _check(lib.lhpc_dist_allreduce_sum_f64(self._h, t.data_ptr(), t.numel(), _stream_ptr(stream)),
                "lhpc_dist_allreduce_sum_f64")
@@ -1055,6 +1062,20 @@ class DistSpMVPlan:
         if stream is None:
             stream = torch.cuda.current_stream()
         _check(lib.lhpc_dist_spmv_end(self._h, _stream_ptr(stream)), "lhpc_dist_spmv_end")
+
+    def cg(self, b, x, p_work, tol: float = 1e-8, max_iter: int = 1000, check_every: int = 1, stream=None):
+        """lhpc_dist_cg_solve: b, x (initial guess in, whole solution out on
+        every rank) and p_work full-length device tensors; p_work registered
+        as a P2P window gives peer-store exchanges.  Returns (x, iterations,
+        ‖r‖/‖b‖)."""
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream(b.device)
+        it, res = _i(), _d()
+        _check(lib.lhpc_dist_cg_solve(self._h, b.data_ptr(), x.data_ptr(), p_work.data_ptr(), float(tol),
+                                      int(max_iter), int(check_every), C.byref(it), C.byref(res),
+                                      _stream_ptr(stream)), "lhpc_dist_cg_solve")
+        return x, it.value, res.value
 
     def exchange(self, y, stream=None):
         """The call's y exchange alone (every chunk; lhpc_dist_exchange)."""

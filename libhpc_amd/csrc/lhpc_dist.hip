@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <cstdlib>
 #include <random>
 #include <cstring>
@@ -80,6 +81,7 @@ struct lhpc_dist_comm {
   bool flags_mapped = false;
   uint32_t *h_status = nullptr;  // host-mapped: bit 0 = a flag wait timed out
   uint32_t epoch = 0;
+  uint32_t red_epoch = 0;        // P2P all-gathers of scalars (RED flags)
   int cus = 256;  // compute units of the device (k_p2p_acquire_all grid)
   P2pWindow win[LHPC_DIST_P2P_MAX_WINDOWS];
   int n_win = 0;
@@ -108,6 +110,7 @@ struct lhpc_dist_spmv_plan {
   // x by column parts (part j = the columns exchange j delivers)
   const void *pending_y = nullptr;
   bool chain = false;
+  double *h_scalars = nullptr;  // lhpc_dist_cg_solve: 2 pinned host scalars (first solve; freed with the plan)
 };
 
 namespace {
@@ -181,6 +184,49 @@ __global__ void k_p2p_wait(const uint32_t *flags, int base, uint32_t e, int nran
 // call reads y as x) could be stale; one block per CU (dealt round-robin
 // over the XCDs) invalidates them all before the compute stream continues.
 __global__ void k_p2p_acquire_all() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+
+// The flag allocation (uncached, one IPC handle): READY [0, n) | DONE
+// [n, 2n) | RED [2n, 3n) uint32 flags (n ≤ 64) in the first kFlagBytes, then
+// the scalar slots of the P2P all-gather: double [2 parities][64 ranks][8]
+constexpr size_t kFlagBytes = 1024;
+constexpr int kRedMax = 8;
+constexpr size_t kFlagAlloc = kFlagBytes + 2 * 64 * kRedMax * sizeof(double);
+__device__ __forceinline__ double *red_slots(uint32_t *flags) {
+  return reinterpret_cast<double *>(reinterpret_cast<unsigned char *>(flags) + kFlagBytes);
+}
+// this rank's `count` values into slot [parity][self] of every rank (itself
+// included), then its RED flag (epoch e, release) into every peer
+__global__ void k_p2p_red_push(uint32_t *const *peer_flags, int nranks, int self, int parity, const double *vals,
+                               int count, uint32_t e, const uint32_t *status) {
+  const int p = threadIdx.x;
+  if (p >= nranks || p2p_failed(status)) return;
+  double *dst = red_slots(peer_flags[p]) + (parity * 64 + self) * kRedMax;
+  for (int i = 0; i < count; ++i)
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(dst + i),
+                       static_cast<unsigned long long>(__double_as_longlong(vals[i])), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (p != self)
+    __hip_atomic_store(peer_flags[p] + 2 * nranks + self, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+}
+// after every peer's RED flag: out[r·count + i] = rank r's value i
+__global__ void k_p2p_red_collect(uint32_t *flags, int nranks, int parity, int count, double *out) {
+  const int t = threadIdx.x;
+  if (t >= nranks * count) return;
+  const int r = t / count, i = t % count;
+  const double *src = red_slots(flags) + (parity * 64 + r) * kRedMax + i;
+  out[t] = __longlong_as_double(static_cast<long long>(__hip_atomic_load(
+      reinterpret_cast<const unsigned long long *>(src), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)));
+}
+// out[i] = Σ_r gathered[r·count + i] in rank order (identical on every rank)
+__global__ void k_sum_ranks(const double *gathered, int nranks, int count, double *out) {
+  const int i = threadIdx.x;
+  if (i >= count) return;
+  double acc = 0.0;
+  for (int r = 0; r < nranks; ++r) acc += gathered[r * count + i];
+  out[i] = acc;
+}
 // bytes [o0, o1) of this rank's y into the same bytes of every peer's y;
 // offsets are multiples of 4.  16-B stores on [a0, a1) (the 16-B aligned
 // interior) for peers whose y has our 16-B phase, head [o0, a0) and tail
@@ -302,6 +348,7 @@ void destroy_spmv(lhpc_dist_spmv_plan *d) {
   for (hipEvent_t e : d->ev_x)
     if (e) (void)hipEventDestroy(e);
   if (d->done) (void)hipEventDestroy(d->done);
+  if (d->h_scalars) (void)hipHostFree(d->h_scalars);
   if (d->ev_p2p) (void)hipEventDestroy(d->ev_p2p);
   delete d;
 }
@@ -489,9 +536,9 @@ extern "C" int lhpc_dist_p2p_export(lhpc_dist_comm *c, void *y, int64_t bytes, u
   LHPC_HIP_TRY(hipIpcGetMemHandle(&b.buf, base));
   if (!c->flags) {
     // flags: uncached, so a peer's store is seen by the next poll; zeroed
-    LHPC_HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void **>(&c->flags), 2 * 64 * sizeof(uint32_t),
-                                       hipDeviceMallocUncached));
-    LHPC_HIP_TRY(hipMemset(c->flags, 0, 2 * 64 * sizeof(uint32_t)));
+    LHPC_HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void **>(&c->flags), kFlagAlloc, hipDeviceMallocUncached));
+    LHPC_HIP_TRY(hipMemset(c->flags, 0, kFlagAlloc));
+    c->red_epoch = 0;
     LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_status), sizeof(uint32_t), hipHostMallocMapped));
     *c->h_status = 0;
     c->epoch = 0;
@@ -653,14 +700,65 @@ extern "C" int lhpc_dist_comm_info(const lhpc_dist_comm *c, int *nranks, int *ra
   return LHPC_OK;
 }
 
+namespace {
+// out[r·count + i] = rank r's vals[i], on `s`: RCCL all-gather, or over a
+// P2P communicator the scalar slots of the flag allocation (count ≤ 8;
+// double-buffered by parity: a rank overwrites parity p only after every
+// peer signalled the reduction after the one that last read it)
+int allgather_f64(lhpc_dist_comm *c, const double *vals, int count, double *out, hipStream_t s) {
+  if (c->nranks == 1) {
+    LHPC_HIP_TRY(hipMemcpyAsync(out, vals, static_cast<size_t>(count) * 8, hipMemcpyDeviceToDevice, s));
+    return LHPC_OK;
+  }
+  if (c->comm) {
+    LHPC_NCCL_TRY(ncclAllGather(vals, out, static_cast<size_t>(count), ncclFloat64, c->comm, s));
+    return LHPC_OK;
+  }
+  if (!c->flags_mapped || count > kRedMax) return LHPC_ERR_UNSUPPORTED;  // no window imported yet
+  if (*c->h_status) return LHPC_ERR_INTERNAL;
+  const uint32_t e = ++c->red_epoch;
+  const int parity = static_cast<int>(e & 1u);
+  hipLaunchKernelGGL(k_p2p_red_push, dim3(1), dim3(64), 0, s, c->d_peer_flags, c->nranks, c->rank, parity, vals, count,
+                     e, c->h_status);
+  LHPC_HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_p2p_wait, dim3(1), dim3(64), 0, s, c->flags, 2 * c->nranks, e, c->nranks, c->rank,
+                     c->h_status);
+  LHPC_HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_p2p_red_collect, dim3(1), dim3(512), 0, s, c->flags, c->nranks, parity, count, out);
+  return static_cast<int>(hipGetLastError());
+}
+}  // namespace
+
+extern "C" int lhpc_dist_allgather_f64(lhpc_dist_comm *c, const double *vals, int64_t count, double *out,
+                                       void *stream) {
+  if (!c || count < 0 || (count > 0 && (!vals || !out))) return LHPC_ERR_INVALID_ARG;
+  if (count == 0) return LHPC_OK;
+  LHPC_HIP_TRY(hipSetDevice(c->device));
+  if (!c->comm && c->nranks > 1 && count > kRedMax) return LHPC_ERR_UNSUPPORTED;
+  return allgather_f64(c, vals, static_cast<int>(count), out, static_cast<hipStream_t>(stream));
+}
+
 extern "C" int lhpc_dist_allreduce_sum_f64(lhpc_dist_comm *c, double *buf, int64_t count, void *stream) {
   if (!c || (count > 0 && !buf) || count < 0) return LHPC_ERR_INVALID_ARG;
   if (count == 0) return LHPC_OK;
-  if (!c->comm) return LHPC_ERR_UNSUPPORTED;  // local (P2P-only) communicator
   LHPC_HIP_TRY(hipSetDevice(c->device));
-  LHPC_NCCL_TRY(ncclAllReduce(buf, buf, static_cast<size_t>(count), ncclFloat64, ncclSum, c->comm,
-                              static_cast<hipStream_t>(stream)));
-  return LHPC_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (c->comm) {
+    LHPC_NCCL_TRY(ncclAllReduce(buf, buf, static_cast<size_t>(count), ncclFloat64, ncclSum, c->comm, s));
+    return LHPC_OK;
+  }
+  // P2P communicator: gather every rank's values, add them in rank order
+  if (c->nranks == 1) return LHPC_OK;
+  if (count > kRedMax) return LHPC_ERR_UNSUPPORTED;
+  double *g = nullptr;
+  LHPC_HIP_TRY(lhpc::scratch_alloc(reinterpret_cast<void **>(&g), static_cast<size_t>(c->nranks * count) * 8, s));
+  int st = allgather_f64(c, buf, static_cast<int>(count), g, s);
+  if (st == LHPC_OK) {
+    hipLaunchKernelGGL(k_sum_ranks, dim3(1), dim3(64), 0, s, g, c->nranks, static_cast<int>(count), buf);
+    st = static_cast<int>(hipGetLastError());
+  }
+  (void)hipFreeAsync(g, s);
+  return st;
 }
 
 extern "C" int lhpc_dist_spmv_plan_create_opts(lhpc_dist_spmv_plan **out, lhpc_dist_comm *comm, int dtype,
@@ -732,16 +830,18 @@ extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_c
                                          val, flags, nullptr);
 }
 
-extern "C" int lhpc_dist_spmv_begin(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream) {
+namespace {
+// lhpc_dist_spmv_begin; local_only: this rank's rows of y only (no exchange,
+// the CG solver's q = A·p)
+int spmv_begin(lhpc_dist_spmv_plan *d, const void *x, void *y, hipStream_t s, bool local_only) {
   if (!d || (d->n_cols > 0 && !x) || (d->n_rows > 0 && !y) || (x == y && d->n_rows > 0)) return LHPC_ERR_INVALID_ARG;
   lhpc_dist_comm *c = d->comm;
   lhpc::RocTxRange rx("lhpc_dist_spmv");
   LHPC_HIP_TRY(hipSetDevice(c->device));
-  hipStream_t s = static_cast<hipStream_t>(stream);
   const size_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
   // the y exchange: direct peer stores into a registered window, RCCL, or none
   const P2pWindow *win = nullptr;
-  const int xk = pick_exchange(d, y, &win);
+  const int xk = local_only ? LHPC_DIST_EXCHANGE_NONE : pick_exchange(d, y, &win);
   if (xk < 0) return xk;
   // x is the y of the begun call before (chained): its exchange is still in
   // flight; with column parts, part j of the stage waits only for exchange j
@@ -777,6 +877,27 @@ extern "C" int lhpc_dist_spmv_begin(lhpc_dist_spmv_plan *d, const void *x, void 
   return LHPC_OK;
 }
 
+// the exchange of y alone (y holds this rank's blocks), left in flight like
+// a begun call's, so a chained call's stage can wait per chunk
+int exchange_begin(lhpc_dist_spmv_plan *d, void *y, hipStream_t s) {
+  lhpc_dist_comm *c = d->comm;
+  LHPC_TRY(wait_pending(d, s));
+  const P2pWindow *win = nullptr;
+  const int xk = pick_exchange(d, y, &win);
+  if (xk < 0) return xk;
+  if (xk == LHPC_DIST_EXCHANGE_NONE) return LHPC_OK;
+  if (xk == LHPC_DIST_EXCHANGE_P2P) LHPC_TRY(p2p_exchange_begin(c, s, d->ev_p2p));
+  for (int k = 0; k < d->K; ++k) LHPC_TRY(exchange_chunk(d, xk, win, k, y, s));
+  LHPC_HIP_TRY(hipEventRecord(d->done, c->s_comm));
+  d->pending_y = y;
+  return LHPC_OK;
+}
+}  // namespace
+
+extern "C" int lhpc_dist_spmv_begin(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream) {
+  return spmv_begin(d, x, y, static_cast<hipStream_t>(stream), false);
+}
+
 extern "C" int lhpc_dist_spmv_end(lhpc_dist_spmv_plan *d, void *stream) {
   if (!d) return LHPC_ERR_INVALID_ARG;
   LHPC_HIP_TRY(hipSetDevice(d->comm->device));
@@ -790,20 +911,149 @@ extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, vo
 
 extern "C" int lhpc_dist_exchange(lhpc_dist_spmv_plan *d, void *y, void *stream) {
   if (!d || (d->n_rows > 0 && !y)) return LHPC_ERR_INVALID_ARG;
-  lhpc_dist_comm *c = d->comm;
   lhpc::RocTxRange rx("lhpc_dist_exchange");
+  LHPC_HIP_TRY(hipSetDevice(d->comm->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  LHPC_TRY(exchange_begin(d, y, s));
+  return wait_pending(d, s);
+}
+
+namespace {
+__global__ void k_set_scalars(double *p, double v, int n) {
+  if (static_cast<int>(threadIdx.x) < n) p[threadIdx.x] = v;
+}
+// out = Σ_b part[slot(b)] over the N·K global blocks in block order b = k·N + r
+// (gathered as [r][K]): the dot is independent of how the blocks are spread
+// over ranks, so an N-rank solve matches a one-rank solve of the same split
+__global__ void k_sum_blocks(const double *gathered, int nranks, int K, double *out) {
+  if (threadIdx.x != 0) return;
+  double acc = 0.0;
+  for (int k = 0; k < K; ++k)
+    for (int r = 0; r < nranks; ++r) acc += gathered[r * K + k];
+  *out = acc;
+}
+}  // namespace
+
+extern "C" int lhpc_dist_cg_solve(lhpc_dist_spmv_plan *d, const void *b, void *x, void *p_work, double tol,
+                                  int max_iter, int check_every, int *iters_out, double *resid_out, void *stream) {
+  if (!d || !b || !x || !p_work || max_iter < 0 || !(tol >= 0.0) || d->n_rows != d->n_cols || b == x ||
+      p_work == x || p_work == b)
+    return LHPC_ERR_INVALID_ARG;
+  lhpc_dist_comm *c = d->comm;
+  if (d->K > kRedMax) return LHPC_ERR_UNSUPPORTED;  // K dot partials per rank in one all-gather
+  lhpc::RocTxRange rx("lhpc_dist_cg_solve");
   LHPC_HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   LHPC_TRY(wait_pending(d, s));
-  const P2pWindow *win = nullptr;
-  const int xk = pick_exchange(d, y, &win);
-  if (xk < 0) return xk;
-  if (xk == LHPC_DIST_EXCHANGE_NONE) return LHPC_OK;
-  if (xk == LHPC_DIST_EXCHANGE_P2P) LHPC_TRY(p2p_exchange_begin(c, s, d->ev_p2p));
-  for (int k = 0; k < d->K; ++k) LHPC_TRY(exchange_chunk(d, xk, win, k, y, s));
-  LHPC_HIP_TRY(hipEventRecord(d->done, c->s_comm));
-  LHPC_HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
-  return LHPC_OK;
+  const int N = c->nranks, K = d->K, dt = d->dtype;
+  const int64_t n = d->n_rows;
+  const size_t ts = dt == LHPC_F32 ? 4 : 8;
+  if (check_every < 1) check_every = 1;
+  auto at = [&](const void *v, int64_t i) { return static_cast<unsigned char *>(const_cast<void *>(v)) + i * ts; };
+  // this rank's K blocks of rows
+  std::vector<int64_t> r0(static_cast<size_t>(K)), len(static_cast<size_t>(K));
+  for (int k = 0; k < K; ++k) {
+    const int64_t bi = static_cast<int64_t>(k) * N + c->rank;
+    r0[static_cast<size_t>(k)] = d->cuts[bi];
+    len[static_cast<size_t>(k)] = d->cuts[bi + 1] - d->cuts[bi];
+  }
+  // scratch: r and q (full length: the SpMV writes q at global rows), the
+  // scalars [rr0, rr1, pq, bb, one] and the dot partials / their all-gather
+  void *vec = nullptr;
+  double *sc = nullptr;
+  LHPC_HIP_TRY(lhpc::scratch_alloc(&vec, static_cast<size_t>(std::max<int64_t>(n, 1)) * ts * 2, s));
+  struct Free {
+    void *a;
+    hipStream_t s;
+    ~Free() { (void)hipFreeAsync(a, s); }
+  } fv{vec, s};
+  const int parts = 8 + K + N * K;
+  LHPC_HIP_TRY(lhpc::scratch_alloc(reinterpret_cast<void **>(&sc), static_cast<size_t>(parts) * 8, s));
+  Free fs{sc, s};
+  void *r = vec, *q = at(vec, n);
+  double *rr[2] = {sc, sc + 1}, *pq = sc + 2, *bb = sc + 3, *one = sc + 4, *part = sc + 8, *gath = sc + 8 + K;
+  hipLaunchKernelGGL(k_set_scalars, dim3(1), dim3(64), 0, s, one, 1.0, 1);
+  LHPC_HIP_TRY(hipGetLastError());
+  // global dot from this rank's K block partials: all-gather, block-order sum
+  auto global_dot = [&](double *out) -> int {
+    LHPC_TRY(allgather_f64(c, part, K, gath, s));
+    hipLaunchKernelGGL(k_sum_blocks, dim3(1), dim3(64), 0, s, gath, N, K, out);
+    return static_cast<int>(hipGetLastError());
+  };
+  auto dots = [&](const void *a, const void *bv, double *out) -> int {
+    for (int k = 0; k < K; ++k) LHPC_TRY(lhpc_vec_dot(dt, len[k], at(a, r0[k]), at(bv, r0[k]), part + k, s));
+    return global_dot(out);
+  };
+  if (!d->h_scalars)
+    LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&d->h_scalars), 2 * sizeof(double), hipHostMallocDefault));
+  double &h_rr = d->h_scalars[0], &h_bb = d->h_scalars[1];
+  h_rr = h_bb = 0.0;
+  // bb = b·b; q = A·x (x complete on every rank); r = b − q; p = r; rr = r·r
+  LHPC_TRY(dots(b, b, bb));
+  LHPC_TRY(spmv_begin(d, x, q, s, true));
+  for (int k = 0; k < K; ++k) {
+    if (!len[k]) {
+      LHPC_HIP_TRY(hipMemsetAsync(part + k, 0, 8, s));
+      continue;
+    }
+    LHPC_HIP_TRY(hipMemcpyAsync(at(r, r0[k]), at(b, r0[k]), len[k] * ts, hipMemcpyDeviceToDevice, s));
+    LHPC_TRY(lhpc_cg_step_r(dt, len[k], one, one, at(r, r0[k]), at(q, r0[k]), part + k, s));
+    LHPC_HIP_TRY(hipMemcpyAsync(at(p_work, r0[k]), at(r, r0[k]), len[k] * ts, hipMemcpyDeviceToDevice, s));
+  }
+  LHPC_TRY(global_dot(rr[0]));
+  LHPC_TRY(exchange_begin(d, p_work, s));  // p complete on every rank; the next stage waits per chunk
+  LHPC_HIP_TRY(hipMemcpyAsync(&h_bb, bb, 8, hipMemcpyDeviceToHost, s));  // pinned
+  LHPC_HIP_TRY(hipMemcpyAsync(&h_rr, rr[0], 8, hipMemcpyDeviceToHost, s));
+  LHPC_HIP_TRY(hipStreamSynchronize(s));
+  const double stop = tol * tol * (h_bb > 0.0 ? h_bb : 1.0);
+  int it = 0, cur = 0, status = LHPC_OK;
+  if (h_rr > stop) {
+    for (it = 1; it <= max_iter; ++it) {
+      // q = A·p: a chained stage (part j of p waits only for exchange j)
+      LHPC_TRY(spmv_begin(d, p_work, q, s, true));
+      LHPC_TRY(dots(p_work, q, pq));
+      for (int k = 0; k < K; ++k) {  // r −= α·q, partial r·r
+        if (len[k]) LHPC_TRY(lhpc_cg_step_r(dt, len[k], rr[cur], pq, at(r, r0[k]), at(q, r0[k]), part + k, s));
+        else LHPC_HIP_TRY(hipMemsetAsync(part + k, 0, 8, s));
+      }
+      LHPC_TRY(global_dot(rr[cur ^ 1]));
+      if (it % check_every == 0 || it == max_iter) {
+        LHPC_HIP_TRY(hipMemcpyAsync(&h_rr, rr[cur ^ 1], 8, hipMemcpyDeviceToHost, s));
+        LHPC_HIP_TRY(hipStreamSynchronize(s));
+        if (!std::isfinite(h_rr)) {
+          status = LHPC_ERR_INTERNAL;  // breakdown: the matrix is not SPD?
+          break;
+        }
+        if (h_rr <= stop) {
+          for (int k = 0; k < K; ++k)  // x += α·p
+            if (len[k])
+              LHPC_TRY(lhpc_cg_step_xp(dt, len[k], rr[cur], pq, nullptr, nullptr, at(x, r0[k]), at(p_work, r0[k]),
+                                       nullptr, s));
+          break;
+        }
+      }
+      for (int k = 0; k < K; ++k)  // x += α·p; p = r + β·p
+        if (len[k])
+          LHPC_TRY(lhpc_cg_step_xp(dt, len[k], rr[cur], pq, rr[cur ^ 1], rr[cur], at(x, r0[k]), at(p_work, r0[k]),
+                                   at(r, r0[k]), s));
+      LHPC_TRY(exchange_begin(d, p_work, s));
+      cur ^= 1;
+    }
+    if (it > max_iter) it = max_iter;
+  }
+  // every rank ends with the whole x: this rank's rows of x go out through
+  // p_work (the registered window when the exchange is P2P)
+  LHPC_TRY(wait_pending(d, s));
+  for (int k = 0; k < K; ++k)
+    if (len[k]) LHPC_HIP_TRY(hipMemcpyAsync(at(p_work, r0[k]), at(x, r0[k]), len[k] * ts, hipMemcpyDeviceToDevice, s));
+  LHPC_TRY(exchange_begin(d, p_work, s));
+  LHPC_TRY(wait_pending(d, s));
+  LHPC_HIP_TRY(hipMemcpyAsync(x, p_work, static_cast<size_t>(n) * ts, hipMemcpyDeviceToDevice, s));
+  LHPC_HIP_TRY(hipStreamSynchronize(s));
+  if (c->h_status && *c->h_status) status = LHPC_ERR_INTERNAL;  // a P2P flag wait timed out
+  if (iters_out) *iters_out = it;
+  if (resid_out) *resid_out = std::sqrt(std::max(h_rr, 0.0)) / std::sqrt(h_bb > 0.0 ? h_bb : 1.0);
+  return status;
 }
 
 extern "C" int lhpc_dist_spmv_plan_destroy(lhpc_dist_spmv_plan *d) {

@@ -20,6 +20,9 @@ Cases (argv[1]):
             windows up again: its P2P calls are bit-exact
   reset     P2P calls, a collective lhpc_dist_p2p_reset (new flag arrays),
             re-export / import (peers' flags remapped by generation), calls
+  cg        lhpc_dist_cg_solve over two ranks (K = 2, p_work a window, dots
+            through the P2P scalar all-gather) equals the world-1 solve with
+            K = 4 (the same four blocks) bit for bit; P2P all-reduce of [r+1]
   chain     cross-step overlap: five chained lhpc_dist_spmv_begin calls over
             two windows (y of call n is x of call n+1), no end in between —
             each stage's column part waits for the previous call's DONE(j)
@@ -226,6 +229,39 @@ elif case == "chain":
         dist.barrier()
         out["status"].append(comm.p2p_status())
         comm.close()
+elif case == "cg":
+    ny, nx = 90, 77
+    rp, col, val = S.laplacian_2d(ny, nx)
+    n = rp.size - 1
+    b = torch.from_numpy(np.random.default_rng(0xE700).uniform(-1, 1, n)).to(dev)
+    # the one-rank solve of the same four blocks (world-1 local communicator)
+    c1 = L.DistComm.local(1, 0, 0)
+    cuts1 = L.interleaved_cuts(rp, 1, 4)
+    with L.DistSpMVPlan(c1, n, n, 4, cuts1, *L.interleaved_local_csr(rp, col, val, cuts1, 1, 4, 0)) as d1:
+        x1, it1, _ = d1.cg(b, torch.zeros(n, dtype=torch.float64, device=dev), torch.empty(n, dtype=torch.float64,
+                                                                                          device=dev), tol=1e-10,
+                           max_iter=5000)
+        x1 = x1.cpu().numpy()
+    c1.close()
+    comm = L.DistComm.local(world, rank, 0)
+    pw = torch.full((n,), float("nan"), dtype=torch.float64, device=dev)
+    comm.p2p_setup_torch(pw)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([rank + 1.0, 2.0 * rank], dtype=torch.float64, device=dev)
+    comm.allreduce_sum_f64(t, stream=torch.cuda.current_stream(dev))
+    torch.cuda.synchronize()
+    out["ok"].append(t.cpu().tolist() == [3.0, 2.0])
+    cuts = L.interleaved_cuts(rp, world, 2)
+    assert np.array_equal(cuts, cuts1)
+    with L.DistSpMVPlan(comm, n, n, 2, cuts, *L.interleaved_local_csr(rp, col, val, cuts, world, 2, rank)) as d:
+        x2, it2, _ = d.cg(b, torch.zeros(n, dtype=torch.float64, device=dev), pw, tol=1e-10, max_iter=5000)
+        x2 = x2.cpu().numpy()
+    out["ok"].append(it1 == it2)
+    out["ok"].append(bool(np.array_equal(x1, x2)))
+    dist.barrier()
+    out["status"].append(comm.p2p_status())
+    comm.close()
 else:
     raise SystemExit(f"unknown case {case}")
 print(json.dumps(out), flush=True)

@@ -137,6 +137,36 @@ def test_dist_spmv_chained_world1(lhpc, gpu, comm, K, case):
         assert np.array_equal(snaps[it].cpu().numpy(), want[it]), it
 
 
+@pytest.mark.parametrize("K", [1, 2, 4])
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_dist_cg_world1(lhpc, gpu, comm, K, dtype):
+    """lhpc_dist_cg_solve at world 1 (RCCL communicator, K blocks of rows,
+    block-order dots, chained stages) on the 2-D Laplacian: fp64 — the fp64
+    CG restatement's iteration count ±1 and x within 1e-8·‖x‖; fp32 —
+    converged and within 1e-4·‖x‖ of the fp64 solution."""
+    import torch
+    ny, nx = 80, 70
+    dt = np.float64 if dtype == "f64" else np.float32
+    rp, col, val = S.laplacian_2d(ny, nx, dtype=dt, shift=0.0 if dtype == "f64" else 0.5)
+    n = rp.size - 1
+    b = np.random.default_rng(0xD500 + K).uniform(-1, 1, n)
+    want, it_o, _ = S.cg_oracle(rp, col, val.astype(np.float64), b, tol=1e-10, max_iter=5000)
+    cuts = lhpc.interleaved_cuts(rp, 1, K)
+    tol = 1e-10 if dtype == "f64" else 1e-5
+    with lhpc.DistSpMVPlan(comm, n, n, K, cuts, *lhpc.interleaved_local_csr(rp, col, val, cuts, 1, K, 0)) as d:
+        bd = torch.from_numpy(b.astype(dt)).to(gpu)
+        x = torch.zeros(n, dtype=bd.dtype, device=gpu)
+        p = torch.empty_like(x)
+        x, it, res = d.cg(bd, x, p, tol=tol, max_iter=5000, check_every=2)
+        x = x.cpu().numpy().astype(np.float64)
+    assert res <= tol
+    if dtype == "f64":
+        assert abs(it - it_o) <= 2  # checked every 2nd iteration
+        assert np.linalg.norm(x - want) <= 1e-8 * np.linalg.norm(want)
+    else:
+        assert np.linalg.norm(x - want) <= 1e-4 * np.linalg.norm(want)
+
+
 def test_dist_spmv_rejects_aliased_xy(lhpc, gpu, comm):
     import torch
     n = 1000
@@ -163,7 +193,7 @@ def test_dist_stencil7_world1_matches_single_domain(lhpc, gpu, comm, nz, ny, nx)
     assert np.array_equal(od.cpu().numpy(), want)
 
 
-P2P_CASES = {"barrier": 6, "loop": 8, "pingpong": 8, "tiny": 8, "rollback": 4, "reset": 6, "chain": 10}
+P2P_CASES = {"barrier": 6, "loop": 8, "pingpong": 8, "tiny": 8, "rollback": 4, "reset": 6, "chain": 10, "cg": 3}
 
 
 @pytest.mark.parametrize("case", list(P2P_CASES))
@@ -181,7 +211,10 @@ def test_dist_spmv_p2p_two_ranks_one_gpu(lhpc, gpu, case):
     rounds of setup / calls / collective reset (flag arrays re-allocated and
     remapped by generation); chained calls (lhpc_dist_spmv_begin: the
     stage's column part j waits for the previous call's per-chunk DONE(j)
-    flags, ping-pong windows, five calls, one end).  (On one GPU the pushes
+    flags, ping-pong windows, five calls, one end); the distributed CG
+    (lhpc_dist_cg_solve, p_work a window, dots all-gathered through the P2P
+    scalar slots) at world 2 × K 2 bit-identical to a world-1 × K 4 solve of
+    the same block split, and the P2P all-reduce.  (On one GPU the pushes
     are device-local; over xGMI they are the same stores.)"""
     import json
     import os
