@@ -96,7 +96,9 @@ def parse():
     ap.add_argument("--n", type=int, default=10_000_000)
     ap.add_argument("--per-row", type=int, default=15)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--chunks", type=int, default=2, help="N>1: row chunks per rank (all-gather overlap; DESIGN.md §6)")
+    ap.add_argument("--chunks", type=int, default=4,
+                    help="N>1: row chunks per rank K (exchange overlap; K = 4 is the step model's best for N = 2-8, "
+                         "tools/step_model.py, DESIGN.md §6)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spmv-options", default=None,
                     help="JSON dict of lhpc_options fields for the 1-GPU SpMV plan (measured alternatives, DESIGN.md §4)")
@@ -795,7 +797,7 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
             ts.append(time.perf_counter() - t0)
         out["_cpu"] = {"value": cells / min(ts) / 1e9, "unit": "Gcell/s", "cores": th, "kind": "port",
                        "sample": f"full 8192^2 grid, best of {len(ts)} passes, reference SSE loop restated",
-                       "host": host_info(used)}
+                       "host": host_info(th)}
     return out
 
 
@@ -805,17 +807,35 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
     rp, col, val = L.gen_laplacian_2d(nx, nx, L.F64)
     n, nnz = nx * nx, int(col.size)
     b = L.gen_values(L.F64, 0, n, L.SEED_X)
-    ib = InterleavedBlocks(n, world, 1)
-    r0, r1 = ib.rows(rank, 0)
-    plan = L.SpMVPlan(*ib.local_csr(rp, col, val, rank, 0), n)
-    bd = torch.zeros(ib.B, dtype=torch.float64, device=dev)
-    bd[:r1 - r0] = torch.from_numpy(b[r0:r1]).to(dev)
-    solver = DistCG(ib, rank, lambda pf, qb: plan(pf, qb, stream=stream), HipOps(stream), like=bd,
-                    local_spmv_dot=lambda pf, qb, wb, out: L.spmv_dot(plan, pf, qb, wb, out, stream=stream))
+    native = world > 1 and torch.distributed.get_backend() == "nccl" and os.environ.get("LHPC_DIST_TORCH", "0") != "1"
+    comm = dplan = None
+    if native:
+        # the native distributed CG (lhpc_dist_cg_solve): interleaved
+        # nnz-balanced blocks, K chunks per rank, p exchanged over RCCL with
+        # the next q = A·p's gather chained per chunk, dots as block partials
+        K = min(args.chunks, 8)
+        comm = L.DistComm.from_torch(dev.index)
+        cuts = L.interleaved_cuts(rp, world, K)
+        dplan = L.DistSpMVPlan(comm, n, n, K, cuts, *L.interleaved_local_csr(rp, col, val, cuts, world, K, rank))
+        plan = dplan
+        bfull = torch.from_numpy(b).to(dev)
+        pw = torch.empty(n, dtype=torch.float64, device=dev)
 
-    def run(iters):
-        x = torch.zeros_like(bd)
-        return solver.solve(bd, x, tol=0.0, max_iter=iters, check_every=iters)  # tol 0: exactly `iters` iterations
+        def run(iters):
+            x = torch.zeros(n, dtype=torch.float64, device=dev)
+            return dplan.cg(bfull, x, pw, tol=0.0, max_iter=iters, check_every=iters, stream=stream)
+    else:
+        ib = InterleavedBlocks(n, world, 1)
+        r0, r1 = ib.rows(rank, 0)
+        plan = L.SpMVPlan(*ib.local_csr(rp, col, val, rank, 0), n)
+        bd = torch.zeros(ib.B, dtype=torch.float64, device=dev)
+        bd[:r1 - r0] = torch.from_numpy(b[r0:r1]).to(dev)
+        solver = DistCG(ib, rank, lambda pf, qb: plan(pf, qb, stream=stream), HipOps(stream), like=bd,
+                        local_spmv_dot=lambda pf, qb, wb, out: L.spmv_dot(plan, pf, qb, wb, out, stream=stream))
+
+        def run(iters):
+            x = torch.zeros_like(bd)
+            return solver.solve(bd, x, tol=0.0, max_iter=iters, check_every=iters)  # tol 0: exactly `iters` iterations
 
     run(max(1, args.warmup))
     barrier()
@@ -838,7 +858,11 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
                higher_is_better=True, scaling="strong", vs_baseline=None, dtype="f64",
                data="synthetic: 5-point Laplacian, b = U[-1,1) (SEED_X)",
                config={"workload": f"CG, 2-D Laplacian {nx}^2 fp64, n={n}, nnz={nnz}, {world} GPU(s)",
-                       "iterations": it, "relres": res, "kernel": plan.info()["kernel"]},
+                       "iterations": it, "relres": res,
+                       "kernel": dplan.local_info()["kernel"] if native else plan.info()["kernel"],
+                       "solver": "lhpc_dist_cg_solve (native, RCCL, chained stages)" if native else
+                                 ("lhpc building blocks (libhpc_amd.dist.DistCG)" if world == 1 else
+                                  "DistCG over torch.distributed")},
                roofline={"bound": "hbm", "kernel": "spmv_dot + k_cg_r + k_cg_xp",
                          "achieved": alg / per / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": alg / per / 1e9 / HBM_PEAK_GBPS, "traffic": None,
@@ -859,8 +883,10 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
             ts.append((time.perf_counter() - t0) / max(k, 1))
         out["cpu_baseline"] = {"value": 1.0 / min(ts), "unit": "iter/s", "cores": 1, "kind": "port",
                                "sample": f"{k} iterations of the fp64 CG restatement (oracle.c), best of {len(ts)}",
-                               "host": host_info(used)}
+                               "host": host_info(1)}
     plan.close()
+    if comm is not None:
+        comm.close()
     return out
 
 
@@ -936,7 +962,7 @@ def cpu_sort_baseline(keys, src, seconds):
     return {"value": m / min(ts) / 1e9, "unit": "Gkeys/s", "cores": cpu_threads(), "kind": kind,
             "sample": f"50M of the same keys, best of {len(ts)} sorts"
                       + (" (reference radix_sort, OpenMP)" if kind == "reference" else " (C LSD restatement)"),
-            "host": host_info(used)}
+            "host": host_info(cpu_threads())}
 
 
 if __name__ == "__main__":

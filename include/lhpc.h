@@ -574,6 +574,9 @@ int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream)
  */
 int lhpc_dist_spmv_begin(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream);
 int lhpc_dist_spmv_end(lhpc_dist_spmv_plan *d, void *stream);
+/* the rank's local plan (the row-range plan over its K blocks, else its
+ * first block's plan) and whether chained calls gather by column part      */
+int lhpc_dist_spmv_plan_info(const lhpc_dist_spmv_plan *d, lhpc_spmv_plan_info *info, int *chained_stage);
 /* host only: part[t] for each of the n_tiles x tiles of tile_width columns =
  * the first exchange chunk j whose end row cuts[(j+1)·nranks] covers the
  * tile's last column (the order chunks land in) */

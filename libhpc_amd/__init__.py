@@ -68,7 +68,7 @@ ABI_SYMBOLS = (
     "lhpc_stencil7_f32_planes_opts", "lhpc_dist_spmv_plan_create_opts", "lhpc_dist_exchange",
     "lhpc_dist_exchange_schedule", "lhpc_dist_p2p_reset", "lhpc_dist_p2p_unmap", "lhpc_scratch_trim", "lhpc_scratch_poison",
     "lhpc_spmv_multi", "lhpc_spmv_plan_multi_info", "lhpc_dist_spmv_begin", "lhpc_dist_spmv_end",
-    "lhpc_dist_chain_parts", "lhpc_dist_allgather_f64", "lhpc_dist_cg_solve",
+    "lhpc_dist_chain_parts", "lhpc_dist_allgather_f64", "lhpc_dist_cg_solve", "lhpc_dist_spmv_plan_info",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -226,6 +226,7 @@ _sig("lhpc_dist_spmv_plan_create_opts", _i, C.POINTER(_p), _p, _i, _i64, _i64, _
 _sig("lhpc_dist_spmv", _i, _p, _p, _p, _p)
 _sig("lhpc_dist_spmv_begin", _i, _p, _p, _p, _p)
 _sig("lhpc_dist_spmv_end", _i, _p, _p)
+_sig("lhpc_dist_spmv_plan_info", _i, _p, C.POINTER(PlanInfo), C.POINTER(_i))
 _sig("lhpc_dist_chain_parts", _i, _p, _i, _i, _i64, _i64, _p, _i64)
 _sig("lhpc_dist_exchange", _i, _p, _p, _p)
 _sig("lhpc_dist_exchange_schedule", _i, _p, _i, _i, _i, _i, _i, _p, _i64, C.POINTER(_i64))
@@ -1062,6 +1063,16 @@ class DistSpMVPlan:
         if stream is None:
             stream = torch.cuda.current_stream()
         _check(lib.lhpc_dist_spmv_end(self._h, _stream_ptr(stream)), "lhpc_dist_spmv_end")
+
+    def local_info(self) -> dict:
+        """lhpc_dist_spmv_plan_info: the rank's local plan (kernel family,
+        tiles, chained column parts …)."""
+        inf = PlanInfo()
+        chain = _i()
+        _check(lib.lhpc_dist_spmv_plan_info(self._h, C.byref(inf), C.byref(chain)), "lhpc_dist_spmv_plan_info")
+        d = inf.as_dict()
+        d["chained_stage"] = bool(chain.value)
+        return d
 
     def cg(self, b, x, p_work, tol: float = 1e-8, max_iter: int = 1000, check_every: int = 1, stream=None):
         """lhpc_dist_cg_solve: b, x (initial guess in, whole solution out on

@@ -898,6 +898,22 @@ extern "C" int lhpc_dist_spmv_begin(lhpc_dist_spmv_plan *d, const void *x, void 
   return spmv_begin(d, x, y, static_cast<hipStream_t>(stream), false);
 }
 
+extern "C" int lhpc_dist_spmv_plan_info(const lhpc_dist_spmv_plan *d, lhpc_spmv_plan_info *info, int *chained_stage) {
+  if (!d || !info) return LHPC_ERR_INVALID_ARG;
+  const lhpc_spmv_plan *q = d->lp.split;
+  for (const lhpc_spmv_plan *b : d->lp.block_plan)
+    if (!q && b) q = b;
+  if (chained_stage) *chained_stage = d->chain ? 1 : 0;
+  if (!q) {  // no local rows
+    std::memset(info, 0, sizeof(*info));
+    info->dtype = d->dtype;
+    info->n_cols = d->n_cols;
+    info->device = d->comm->device;
+    return LHPC_OK;
+  }
+  return lhpc_spmv_plan_info_get(q, info);
+}
+
 extern "C" int lhpc_dist_spmv_end(lhpc_dist_spmv_plan *d, void *stream) {
   if (!d) return LHPC_ERR_INVALID_ARG;
   LHPC_HIP_TRY(hipSetDevice(d->comm->device));
