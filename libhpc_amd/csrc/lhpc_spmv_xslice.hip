@@ -31,14 +31,13 @@ constexpr int kLongRow = 48;  // in-slice rows longer than this are wave-reduced
 // lengths.  A chunk with more than NB·64 nonzeros loops over windows (rows
 // spanning windows keep accumulating in order, so the result is unchanged).
 template <typename T, typename P, typename LT, int NB>
-__global__ __launch_bounds__(kBlock) void k_spmv_xslice_stream(
+__device__ __forceinline__ void xslice_block(
     const LT *__restrict__ lens, const int64_t *__restrict__ cbase,
     const int32_t *__restrict__ col, const T *__restrict__ val, const T *__restrict__ x,
     P *__restrict__ partial, int64_t n_rows, int64_t n_rows_pad, int64_t n_chunks,
-    int64_t blocks_per_slice, int S) {
+    int64_t blocks_per_slice, int S, int64_t b, double (*prod)[NB * kWave]) {
   constexpr int CAP = NB * kWave;
-  __shared__ double prod[kBlock / kWave][CAP];
-  const int64_t b = blockIdx.x;
+  (void)CAP;
   int s;
   int64_t wb;
   if (S >= 8) {
@@ -52,7 +51,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_xslice_stream(
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = threadIdx.x / kWave;
   const int64_t chunk = wb * (kBlock / kWave) + wv;
-  if (s >= S || chunk >= n_chunks) return;  // wave-uniform
+  if (s >= S || chunk >= n_chunks) return;  // wave-uniform (this logical block only)
   const int64_t row = chunk * kWave + lane;
   const int len = lens[static_cast<int64_t>(s) * n_rows_pad + row];
   const int64_t base = cbase[static_cast<int64_t>(s) * n_chunks + chunk];
@@ -109,6 +108,21 @@ __global__ __launch_bounds__(kBlock) void k_spmv_xslice_stream(
     __builtin_nontemporal_store(static_cast<P>(acc), partial + static_cast<int64_t>(s) * n_rows_pad + row);
 }
 
+template <typename T, typename P, typename LT, int NB>
+__global__ __launch_bounds__(kBlock) void k_spmv_xslice_stream(
+    const LT *__restrict__ lens, const int64_t *__restrict__ cbase,
+    const int32_t *__restrict__ col, const T *__restrict__ val, const T *__restrict__ x,
+    P *__restrict__ partial, int64_t n_rows, int64_t n_rows_pad, int64_t n_chunks,
+    int64_t blocks_per_slice, int S, int64_t n_blocks) {
+  constexpr int CAP = NB * kWave;
+  __shared__ double prod[kBlock / kWave][CAP];
+  // grid-stride over the logical blocks: a dispatch holds < 2^32 work-items,
+  // and at n = 80M the slice grid alone is 20M blocks (5.1e9 work-items)
+  for (int64_t b = blockIdx.x; b < n_blocks; b += gridDim.x)
+    xslice_block<T, P, LT, NB>(lens, cbase, col, val, x, partial, n_rows, n_rows_pad, n_chunks, blocks_per_slice, S,
+                               b, prod);
+}
+
 // y[i] = Σ_{s=0}^{S-1} partial[s][i], fp64, fixed slice order; 4 rows/thread.
 template <typename T, typename P>
 __global__ __launch_bounds__(kBlock) void k_xslice_reduce(const P *__restrict__ partial,
@@ -136,7 +150,9 @@ template <typename T>
 int launch_xslice(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
   if (p->n_rows == 0) return LHPC_OK;
   const int64_t grid = p->S >= 8 ? 8 * (p->S / 8) * p->xs_bps : p->S * p->xs_bps;
-  const dim3 g(static_cast<unsigned>(grid)), blk(kBlock);
+  // ≤ 2^20 workgroups per dispatch (a multiple of 8, so each XCD keeps its
+  // slices); the kernel strides over the rest
+  const dim3 g(static_cast<unsigned>(std::min<int64_t>(grid, int64_t{1} << 20))), blk(kBlock);
   const T *xv = static_cast<const T *>(x);
   const T *vv = static_cast<const T *>(p->d_val);
 #define LHPC_XS_STREAM(P, NB)                                                                        \
@@ -144,12 +160,12 @@ int launch_xslice(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s
     hipLaunchKernelGGL((k_spmv_xslice_stream<T, P, uint16_t, NB>), g, blk, 0, s,                      \
                        static_cast<const uint16_t *>(p->d_lens), p->d_cbase, p->d_col, vv, xv,         \
                        static_cast<P *>(p->d_partial), p->n_rows, p->xs_rows_pad, p->xs_chunks,        \
-                       p->xs_bps, p->S);                                                              \
+                       p->xs_bps, p->S, grid);                                                        \
   else                                                                                               \
     hipLaunchKernelGGL((k_spmv_xslice_stream<T, P, uint8_t, NB>), g, blk, 0, s,                       \
                        static_cast<const uint8_t *>(p->d_lens), p->d_cbase, p->d_col, vv, xv,          \
                        static_cast<P *>(p->d_partial), p->n_rows, p->xs_rows_pad, p->xs_chunks,        \
-                       p->xs_bps, p->S)
+                       p->xs_bps, p->S, grid)
 #define LHPC_XS_NB(P)                     \
   switch (p->xs_nb) {                     \
     case 1: LHPC_XS_STREAM(P, 1); break;  \

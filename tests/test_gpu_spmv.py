@@ -586,3 +586,23 @@ def test_xtile_parts_150m_past_int32(lhpc, gpu):
         del xd, y1, y2
     rows, y64, _ = S.sampled_rows_fp64(rp, col, val, x, 100_000)
     assert np.array_equal(y[rows].astype(np.float64), y64)
+
+
+@pytest.mark.slow
+def test_xslice_dispatch_past_2p32_work_items(lhpc, gpu):
+    """A dispatch holds < 2^32 work-items: the XSLICE stream kernel's logical
+    grid (slices × 64-row chunks, 256 threads each) passes that at S · n >
+    2^32 (S = 256 slices, n = 17M rows here; C2 at n = 80M is 64 · 80M), and
+    the kernel strides over its logical blocks.  Before the stride the
+    truncated dispatch left rows unwritten (bench --n 80000000 with XSLICE
+    failed its sampled check).  Dyadic values: 10^5 sampled rows exact."""
+    import torch
+    n = 17_000_000
+    rp, col, val = lhpc.gen_uniform_csr(n, n, 2, dtype=lhpc.F32, dist=1, seed=0x17000)
+    x = lhpc.gen_values(lhpc.F32, 1, n, 0x17001)
+    with lhpc.SpMVPlan(rp, col, val, n, flags=FAMILIES["xslice"], options={"xslice_slices": 256}) as plan:
+        info = plan.info()
+        assert info["kernel"] == lhpc.KERNEL_XSLICE and info["slices"] * n > 2**32
+        y = plan(torch.from_numpy(x).to(gpu)).cpu().numpy()
+    rows, y64, _ = S.sampled_rows_fp64(rp, col, val, x, 100_000)
+    assert np.array_equal(y[rows].astype(np.float64), y64)
