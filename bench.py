@@ -416,6 +416,20 @@ def main():
                 dsp.step(xd)
         t_plan = time.time() - t0
         info = plans[0].info()
+        t_plan_dev = None
+        if world == 1 and not native_dist and info["kernel"] == L.KERNEL_XTILE and wl in ("c2", "c3", "c4"):
+            # the same plan from device-resident CSR (LHPC_PLAN_DEVICE_INPUT:
+            # the XTILE layout built on the GPU), timed beside the host build
+            drp, dcol, dval = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (rp, col, val))
+            torch.cuda.synchronize()
+            t0 = time.time()
+            pdev = L.SpMVPlan(drp, dcol, dval, n,
+                              options=json.loads(args.spmv_options) if args.spmv_options else None)
+            t_plan_dev = time.time() - t0
+            same = pdev.layout_digest() == plans[0].layout_digest()
+            pdev.close()
+            del drp, dcol, dval
+            torch.cuda.empty_cache()
 
         if step_end is None:
             step_end = lambda: None  # noqa: E731
@@ -498,7 +512,8 @@ def main():
                       "alg_bytes_per_call": local_alg, "call_us": call_s * 1e6},
             step_ms={"median": float(np.median(step_ms)), "p10": float(np.percentile(step_ms, 10)),
                      "p90": float(np.percentile(step_ms, 90)), "source": "rank 0 HIP events per step"},
-            setup_s={"generate": t_gen, "plan": t_plan},
+            setup_s={"generate": t_gen, "plan": t_plan,
+                     **({"plan_device_input": t_plan_dev, "device_layout_identical": same} if t_plan_dev else {})},
         )
         # correctness of the timed output, outside the timed region: y of the
         # last step on 10^5 sampled rows against an fp64 numpy evaluation,

@@ -64,7 +64,10 @@ enum lhpc_dtype { LHPC_F32 = 0, LHPC_F64 = 1 };
 enum lhpc_plan_flags {
   LHPC_PLAN_DEFAULT = 0,
   LHPC_PLAN_VALIDATE = 1u << 0,     /* check row_ptr monotone, cols in range  */
-  LHPC_PLAN_DEVICE_INPUT = 1u << 1, /* row_ptr/col_idx/val are device ptrs    */
+  LHPC_PLAN_DEVICE_INPUT = 1u << 1, /* row_ptr/col_idx/val are device ptrs on the
+                                       plan's device: validated there; XTILE
+                                       layouts are built on the GPU (others
+                                       copy A to the host first)              */
   /* force a kernel family instead of the heuristic (testing / benchmarks)   */
   LHPC_PLAN_FORCE_ROWGROUP = 1u << 4,
   LHPC_PLAN_FORCE_ADAPTIVE = 1u << 5,
@@ -245,6 +248,13 @@ int lhpc_spmv(lhpc_spmv_plan *plan, const void *x, void *y,
               int buffers_on_device, void *stream);
 int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *plan,
                             lhpc_spmv_plan_info *info);
+/* Test support: 64-bit FNV-1a digests (size folded in) of an XTILE plan's
+ * device layout arrays — row_ptr, col16, perm/iperm, val runs, chunk
+ * descriptors, cr, segment table lo/len and hi, gather pieces, cont — into
+ * out[0..9] (cap ≥ 10), *n_out = 10.  LHPC_ERR_UNSUPPORTED for other plans.
+ * A plan built from LHPC_PLAN_DEVICE_INPUT has the same digests as the host
+ * build of the same matrix and options.                                     */
+int lhpc_spmv_plan_layout_digest(const lhpc_spmv_plan *plan, uint64_t *out, int cap, int *n_out);
 /*
  * Multi-device plans: y = A·x with full replicas on every device.  x[d]
  * (n_cols) and y[d] (n_rows, not x[d]) are HBM pointers on device d; after

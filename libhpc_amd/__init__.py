@@ -39,6 +39,7 @@ LIB_PATH = os.environ.get("LHPC_LIB_PATH") or os.path.join(_HERE, "_lib", "liblh
 
 F32, F64 = 0, 1
 PLAN_VALIDATE = 1 << 0
+PLAN_DEVICE_INPUT = 1 << 1
 PLAN_FORCE_ROWGROUP = 1 << 4
 PLAN_FORCE_ADAPTIVE = 1 << 5
 PLAN_FORCE_XSLICE = 1 << 6
@@ -69,6 +70,7 @@ ABI_SYMBOLS = (
     "lhpc_dist_exchange_schedule", "lhpc_dist_p2p_reset", "lhpc_dist_p2p_unmap", "lhpc_scratch_trim", "lhpc_scratch_poison",
     "lhpc_spmv_multi", "lhpc_spmv_plan_multi_info", "lhpc_dist_spmv_begin", "lhpc_dist_spmv_end",
     "lhpc_dist_chain_parts", "lhpc_dist_allgather_f64", "lhpc_dist_cg_solve", "lhpc_dist_spmv_plan_info",
+    "lhpc_spmv_plan_layout_digest",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -175,6 +177,7 @@ _sig("lhpc_spmv_stage", _i, _p, _p, _p)
 _sig("lhpc_spmv_range", _i, _p, _i, _p, _p)
 _sig("lhpc_spmv_plan_info_get", _i, _p, C.POINTER(PlanInfo))
 _sig("lhpc_spmv_multi", _i, _p, _p, _p, _p)
+_sig("lhpc_spmv_plan_layout_digest", _i, _p, _p, _i, C.POINTER(_i))
 _sig("lhpc_spmv_plan_multi_info", _i, _p, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i), _p, _p)
 _sig("lhpc_spmv_plan_destroy", _i, _p)
 _sig("lhpc_csr_partition_rows", _i, _p, _i, _i64, _i, _p)
@@ -305,18 +308,40 @@ class SpMVPlan:
         ordinals for a single-process multi-device plan (a
         device may repeat: several shares of one GPU); ``plan(x, y)`` then
         takes x, y on devices[0] and ``plan.multi(xs, ys)`` full replicas."""
-        row_ptr = np.ascontiguousarray(row_ptr)
-        col_idx = np.ascontiguousarray(col_idx, dtype=np.int32)
-        val = np.ascontiguousarray(val)
-        if row_ptr.dtype not in (np.int32, np.int64):
-            raise TypeError("row_ptr must be int32 or int64")
-        if val.dtype == np.float32:
-            self.dtype = F32
-        elif val.dtype == np.float64:
-            self.dtype = F64
+        if _is_torch(row_ptr) and row_ptr.is_cuda:
+            # device-resident CSR (LHPC_PLAN_DEVICE_INPUT): validated and, for
+            # XTILE, laid out on the GPU; the tensors must live on the plan's device
+            import torch
+            if row_ptr.dtype not in (torch.int32, torch.int64) or col_idx.dtype != torch.int32:
+                raise TypeError("device row_ptr int32/int64 and col_idx int32")
+            if val.dtype not in (torch.float32, torch.float64):
+                raise TypeError("val must be float32 or float64")
+            for t in (row_ptr, col_idx, val):
+                if not (t.is_cuda and t.is_contiguous()):
+                    raise ValueError("device CSR arrays must be contiguous CUDA tensors")
+            flags |= PLAN_DEVICE_INPUT
+            self.dtype = F32 if val.dtype == torch.float32 else F64
+            self.np_dtype = np.dtype(np.float32 if self.dtype == F32 else np.float64)
+            if device is None and devices is None:
+                device = row_ptr.device.index
+            self._dev_arrays = (row_ptr, col_idx, val)
+            rp_ptr, rp_bits = row_ptr.data_ptr(), 64 if row_ptr.dtype == torch.int64 else 32
+            col_ptr, val_ptr = col_idx.data_ptr(), val.data_ptr()
         else:
-            raise TypeError("val must be float32 or float64")
-        self.np_dtype = val.dtype
+            row_ptr = np.ascontiguousarray(row_ptr)
+            col_idx = np.ascontiguousarray(col_idx, dtype=np.int32)
+            val = np.ascontiguousarray(val)
+            if row_ptr.dtype not in (np.int32, np.int64):
+                raise TypeError("row_ptr must be int32 or int64")
+            if val.dtype == np.float32:
+                self.dtype = F32
+            elif val.dtype == np.float64:
+                self.dtype = F64
+            else:
+                raise TypeError("val must be float32 or float64")
+            self.np_dtype = val.dtype
+            rp_ptr, rp_bits = row_ptr.ctypes.data, 64 if row_ptr.dtype == np.int64 else 32
+            col_ptr, val_ptr = col_idx.ctypes.data, val.ctypes.data
         self.n_rows = int(row_ptr.shape[0] - 1)
         self.n_cols = int(n_cols)
         self.nnz = int(col_idx.shape[0])
@@ -334,16 +359,13 @@ class SpMVPlan:
             self.splits = None
             _check(lib.lhpc_spmv_plan_create(
                 C.byref(self._h), self.dtype, self.n_rows, self.n_cols, self.nnz,
-                row_ptr.ctypes.data, 64 if row_ptr.dtype == np.int64 else 32,
-                col_idx.ctypes.data, val.ctypes.data, dev, ndev,
-                flags), "lhpc_spmv_plan_create")
+                rp_ptr, rp_bits, col_ptr, val_ptr, dev, ndev, flags), "lhpc_spmv_plan_create")
         else:
             sp = np.ascontiguousarray(splits if splits is not None else [], dtype=np.int64)
             self.splits = None if splits is None else [0] + [int(v) for v in sp] + [self.n_rows]
             _check(lib.lhpc_spmv_plan_create_opts(
                 C.byref(self._h), self.dtype, self.n_rows, self.n_cols, self.nnz,
-                row_ptr.ctypes.data, 64 if row_ptr.dtype == np.int64 else 32,
-                col_idx.ctypes.data, val.ctypes.data, dev, ndev,
+                rp_ptr, rp_bits, col_ptr, val_ptr, dev, ndev,
                 flags, int(sp.shape[0]), sp.ctypes.data if sp.shape[0] else None, _opts(self._opts)),
                 "lhpc_spmv_plan_create_opts")
 
@@ -351,6 +373,14 @@ class SpMVPlan:
         inf = PlanInfo()
         _check(lib.lhpc_spmv_plan_info_get(self._h, C.byref(inf)), "lhpc_spmv_plan_info_get")
         return inf.as_dict()
+
+    def layout_digest(self):
+        """lhpc_spmv_plan_layout_digest: FNV-1a digests of an XTILE plan's
+        device layout arrays (test support)."""
+        out = (C.c_uint64 * 10)()
+        n = _i()
+        _check(lib.lhpc_spmv_plan_layout_digest(self._h, out, 10, C.byref(n)), "lhpc_spmv_plan_layout_digest")
+        return [int(v) for v in out[:n.value]]
 
     def multi_info(self) -> dict:
         """lhpc_spmv_plan_multi_info: devices, chunks K, exchange, row cuts."""

@@ -128,9 +128,9 @@ int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, 
   return LHPC_OK;
 }
 
-int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
-                int64_t W, int M, int Rmax, int64_t piece_nnz, int slot_bytes,
-                const int64_t *splits, int n_splits, bool iperm, int cut_window, XtileHost &o, int unit) {
+int xtile_plan_chunks(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols, int64_t W,
+                      int M, int Rmax, int slot_bytes, const int64_t *splits, int n_splits, bool iperm,
+                      int cut_window, XtileHost &o, int unit) {
   const int64_t nnz = rp_at(rp, bits, n_rows) - rp_at(rp, bits, 0);
   if (W < 8 || M < 64 || M >= 65536 || M % 16 || Rmax < 1 || (slot_bytes != 4 && slot_bytes != 8) ||
       cut_window < 1 || cut_window > M || (unit != 1 && unit != 2 && unit != 4) || (unit > 1 && !iperm))
@@ -143,7 +143,6 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
   o.Rmax = Rmax;
   o.unit = unit;
   const int64_t U = unit;
-  auto pad = [U](int64_t len) { return (len + U - 1) / U * U; };
   auto RP = [&](int64_t i) { return rp_at(rp, bits, i); };
   // aligned segments: the longest window [e, e + len) whose padded length
   // Σ_s ⌈count_s / U⌉·U stays ≤ M (monotone in len, so any shorter cut fits)
@@ -237,17 +236,21 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
     const int64_t r0 = o.cr[c], r1 = o.cr[c + 1];
     if (r1 > r0 && RP(r1) > o.ce[c + 1]) o.cont.push_back(static_cast<int32_t>(c));
   }
-  // ---- per (chunk, tile) counts → segment offsets in (tile, chunk) order
+  o.iperm_mode = iperm;
+  o.slot_bytes = slot_bytes;
   o.segoff.assign(static_cast<size_t>((C + 1) * S), 0);
-  int32_t *cnt = o.segoff.data() + S;  // row c+1 temporarily holds count[c]
-#pragma omp parallel for schedule(dynamic, 64)
-  for (int64_t c = 0; c < C; ++c) {
-    int32_t *cc = cnt + c * S;
-    for (int64_t k = o.ce[c]; k < o.ce[c + 1]; ++k) ++cc[col[k] / W];
-    if (U > 1)  // aligned segments: padding at each segment's end
-      for (int64_t s = 0; s < S; ++s) cc[s] = static_cast<int32_t>(pad(cc[s]));
-  }
-  std::vector<int64_t> tbase(static_cast<size_t>(S) + 1, 0);
+  return LHPC_OK;
+}
+
+int xtile_plan_offsets(XtileHost &o, std::vector<int64_t> &tbase) {
+  const int64_t S = o.S, C = o.n_chunks, U = o.unit;
+  auto pad = [U](int64_t len) { return (len + U - 1) / U * U; };
+  int32_t *cnt = o.segoff.data() + S;  // row c+1 holds count[c] on entry
+  if (U > 1)  // aligned segments: padding at each segment's end
+#pragma omp parallel for schedule(static)
+    for (int64_t c = 0; c < C; ++c)
+      for (int64_t s = 0; s < S; ++s) cnt[c * S + s] = static_cast<int32_t>(pad(cnt[c * S + s]));
+  tbase.assign(static_cast<size_t>(S) + 1, 0);
   {
     std::vector<int64_t> tot(static_cast<size_t>(S), 0);
 #pragma omp parallel for schedule(static)
@@ -270,6 +273,13 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
       acc += n;
     }
   }
+  return LHPC_OK;
+}
+
+void xtile_plan_scatter_host(const int32_t *col, int64_t nnz, XtileHost &o) {
+  const int64_t S = o.S, C = o.n_chunks, W = o.W;
+  const bool iperm = o.iperm_mode;
+  const int slot_bytes = o.slot_bytes;
   // ---- scatter (stable: CSR order inside each segment)
   o.col16.reset(new uint16_t[o.total > 0 ? o.total : 1]());
   if (iperm)
@@ -301,6 +311,10 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
       }
     }
   }
+}
+
+void xtile_plan_pieces(XtileHost &o, const std::vector<int64_t> &tbase, int64_t piece_nnz) {
+  const int64_t S = o.S;
   // ---- gather workgroups: each non-empty tile split into pieces of ≈ piece_nnz.
   //      Order: tiles in runs of 8, and inside a run piece k of the 8 tiles
   //      before piece k + 1, so the pieces of one tile are 8 workgroups
@@ -329,6 +343,26 @@ int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, in
         o.pieces.push_back(static_cast<int32_t>(s));
       }
   }
+}
+
+int build_xtile(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
+                int64_t W, int M, int Rmax, int64_t piece_nnz, int slot_bytes,
+                const int64_t *splits, int n_splits, bool iperm, int cut_window, XtileHost &o, int unit) {
+  int st = xtile_plan_chunks(rp, bits, col, n_rows, n_cols, W, M, Rmax, slot_bytes, splits, n_splits, iperm,
+                             cut_window, o, unit);
+  if (st != LHPC_OK) return st;
+  const int64_t S = o.S, C = o.n_chunks;
+  // ---- per (chunk, tile) counts → segment offsets in (tile, chunk) order
+  int32_t *cnt = o.segoff.data() + S;  // row c+1 temporarily holds count[c]
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t c = 0; c < C; ++c) {
+    int32_t *cc = cnt + c * S;
+    for (int64_t k = o.ce[c]; k < o.ce[c + 1]; ++k) ++cc[col[k] / W];
+  }
+  std::vector<int64_t> tbase;
+  if ((st = xtile_plan_offsets(o, tbase)) != LHPC_OK) return st;
+  xtile_plan_scatter_host(col, rp_at(rp, bits, n_rows) - rp_at(rp, bits, 0), o);
+  xtile_plan_pieces(o, tbase, piece_nnz);
   return LHPC_OK;
 }
 

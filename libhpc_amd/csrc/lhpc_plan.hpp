@@ -78,6 +78,8 @@ struct XtileHost {
   // iperm mode: [nnz] in CSR order — for nonzero k of chunk c, iperm[k] is its
   // flat position in the chunk's segment concatenation (tiles ascending)
   std::unique_ptr<uint16_t[]> iperm;
+  bool iperm_mode = false;           // which reduce index stream the plan carries
+  int slot_bytes = 4;
 };
 
 // Device form of the segment table (the reduce reads one 4-B word per tile
@@ -106,6 +108,23 @@ int build_xtile(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_
                 int64_t n_cols, int64_t W, int M, int Rmax, int64_t piece_nnz, int slot_bytes,
                 const int64_t *splits, int n_splits, bool iperm, int cut_window, XtileHost &out,
                 int unit = 1);
+
+// The phases of build_xtile, so that the O(nnz) passes can also run on the
+// GPU from device-resident input (lhpc_xtile_device.hip) while everything that
+// decides the layout stays this one host code:
+//   xtile_plan_chunks      validation, chunk cuts (ce, cr), ranges, cont; needs
+//                          col only for unit > 1; zeroes segoff
+//   (counts)               segoff row c+1 = count of chunk c per tile
+//   xtile_plan_offsets     tile bases (tbase, each a multiple of 8), total,
+//                          segoff = segment starts
+//   xtile_plan_scatter_host  col16 + perm / iperm from host col
+//   xtile_plan_pieces      the gather workgroups from tbase
+int xtile_plan_chunks(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols, int64_t W,
+                      int M, int Rmax, int slot_bytes, const int64_t *splits, int n_splits, bool iperm,
+                      int cut_window, XtileHost &o, int unit);
+int xtile_plan_offsets(XtileHost &o, std::vector<int64_t> &tbase);
+void xtile_plan_scatter_host(const int32_t *col, int64_t nnz, XtileHost &o);
+void xtile_plan_pieces(XtileHost &o, const std::vector<int64_t> &tbase, int64_t piece_nnz);
 
 // Wave-transposed run layout of the XTILE reduce's per-position streams (val,
 // iperm): chunk position i belongs to thread t = i / run (run = 64 B of

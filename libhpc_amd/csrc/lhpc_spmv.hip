@@ -27,8 +27,10 @@ namespace {
 
 // Distinct 128-B x lines touched per nonzero, over up to 32 evenly spaced
 // chunks of 8192 consecutive rows (1.0 = no reuse within a chunk).
-template <typename RP>
-double gather_lines_per_nnz(const RP &rp, const int32_t *col, int64_t n_rows, size_t tsz) {
+// fetch(k0, k1, out): the columns of nonzeros [k0, k1) (host array or a copy
+// from device-resident input)
+template <typename RP, typename Fetch>
+double gather_lines_per_nnz(const RP &rp, Fetch fetch, int64_t n_rows, size_t tsz) {
   constexpr int64_t kChunk = 8192, kSamples = 32;
   const int shift = tsz == 8 ? 4 : 5;  // 16 doubles / 32 floats per line
   const int64_t chunks = (n_rows + kChunk - 1) / kChunk;
@@ -39,12 +41,31 @@ double gather_lines_per_nnz(const RP &rp, const int32_t *col, int64_t n_rows, si
     const int64_t r0 = c * kChunk, r1 = std::min(n_rows, r0 + kChunk);
     const int64_t k0 = rp[r0], k1 = rp[r1];
     buf.resize(static_cast<size_t>(k1 - k0));
-    for (int64_t k = k0; k < k1; ++k) buf[static_cast<size_t>(k - k0)] = col[k] >> shift;
+    if (k1 > k0 && fetch(k0, k1, buf.data()) != LHPC_OK) return 1.0;
+    for (auto &v : buf) v >>= shift;
     std::sort(buf.begin(), buf.end());
     lines += std::unique(buf.begin(), buf.end()) - buf.begin();
     nz += k1 - k0;
   }
   return nz ? static_cast<double>(lines) / static_cast<double>(nz) : 1.0;
+}
+
+// device CSR checks for LHPC_PLAN_DEVICE_INPUT (validate_csr on the GPU):
+// bit 0: row_ptr[0] != 0, decreasing, or row_ptr[n_rows] != nnz; bit 1: a
+// column outside [0, n_cols)
+__global__ void k_validate_device_csr(const void *rp, int bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
+                                      int64_t nnz, unsigned *flag) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x, T = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  auto at = [&](int64_t i) -> int64_t {
+    return bits == 64 ? static_cast<const int64_t *>(rp)[i] : static_cast<const int32_t *>(rp)[i];
+  };
+  unsigned bad = 0;
+  for (int64_t i = t; i < n_rows; i += T)
+    if (at(i + 1) < at(i)) bad |= 1u;
+  if (t == 0 && (at(0) != 0 || at(n_rows) != nnz)) bad |= 1u;
+  for (int64_t k = t; k < nnz; k += T)
+    if (col[k] < 0 || col[k] >= n_cols) bad |= 2u;
+  if (bad) atomicOr(flag, bad);
 }
 
 bool is_gfx950(int dev) {
@@ -117,6 +138,11 @@ int build_parts(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const 
   return LHPC_OK;
 }
 
+int plan_create_device_input(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
+                             const void *row_ptr, int row_ptr_bits, const int32_t *col_idx, const void *val,
+                             const int *device_ids, int n_devices, unsigned flags, int n_splits,
+                             const int64_t *split_rows, const lhpc_options *opts);
+
 int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
                      const void *row_ptr, int row_ptr_bits, const int32_t *col_idx, const void *val,
                      const int *device_ids, int n_devices, unsigned flags, int n_splits,
@@ -129,8 +155,10 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
       (nnz > 0 && (!col_idx || !val)))
     return LHPC_ERR_INVALID_ARG;
   if (n_devices < 0 || (n_devices > 1 && !device_ids)) return LHPC_ERR_INVALID_ARG;
-  if (flags & LHPC_PLAN_DEVICE_INPUT) return LHPC_ERR_UNSUPPORTED;
   if (row_ptr_bits == 32 && nnz > INT32_MAX) return LHPC_ERR_INVALID_ARG;
+  if (flags & LHPC_PLAN_DEVICE_INPUT)
+    return plan_create_device_input(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val, device_ids,
+                                    n_devices, flags, n_splits, split_rows, opts);
 
   const RowPtrView rp{row_ptr, row_ptr_bits};
   // always: every layout pass below indexes host arrays by row_ptr / col_idx,
@@ -211,7 +239,13 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
   const bool auto_ok = !(flags & (LHPC_PLAN_FORCE_ROWGROUP | LHPC_PLAN_FORCE_ADAPTIVE |
                                    LHPC_PLAN_FORCE_XSLICE | LHPC_PLAN_FORCE_XTILE));
   const bool nolocal =
-      auto_ok && x_bytes > 8.0e6 && gather_lines_per_nnz(rp, col_idx, n_rows, tsz) > locality_thr;
+      auto_ok && x_bytes > 8.0e6 && gather_lines_per_nnz(
+          rp,
+          [&](int64_t k0, int64_t k1, int32_t *out) {
+            std::memcpy(out, col_idx + k0, static_cast<size_t>(k1 - k0) * 4);
+            return LHPC_OK;
+          },
+          n_rows, tsz) > locality_thr;
   // XTILE (x tiles in LDS) is the default for gathers without locality;
   // options.spmv_no_xtile selects XSLICE instead.
   const bool want_xtile = (flags & LHPC_PLAN_FORCE_XTILE) || (nolocal && !o.spmv_no_xtile);
@@ -324,6 +358,100 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
   *out = p;
   return LHPC_OK;
 }
+// LHPC_PLAN_DEVICE_INPUT: row_ptr / col_idx / val in HBM of the plan's
+// device (e.g. straight from lhpc_coo_to_csr on the device).  Validated on
+// the GPU; row_ptr (n_rows + 1 words) and the 32 locality samples come back
+// to the host, which makes every layout decision.  The XTILE layout — the
+// default for gathers without locality — is then built on the GPU from the
+// device arrays (xtile_build_device: byte-identical to the host build); any
+// other family, row parts, aligned segments or several devices copy A to the
+// host and take the host path.
+int plan_create_device_input(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
+                             const void *row_ptr, int row_ptr_bits, const int32_t *col_idx, const void *val,
+                             const int *device_ids, int n_devices, unsigned flags, int n_splits,
+                             const int64_t *split_rows, const lhpc_options *opts) {
+  RocTxRange rx("lhpc_spmv_plan_create: device input");
+  const lhpc_options o = resolve_options(opts);
+  int dev = 0;
+  if (device_ids && n_devices >= 1) {
+    dev = device_ids[0];
+    LHPC_HIP_TRY(hipSetDevice(dev));
+  } else {
+    LHPC_HIP_TRY(hipGetDevice(&dev));
+  }
+  if (!is_gfx950(dev)) return LHPC_ERR_NO_DEVICE;
+  // the arrays may still be in flight on any stream of the caller (plan
+  // creation is synchronous anyway)
+  LHPC_HIP_TRY(hipDeviceSynchronize());
+  const size_t tsz = dtype == LHPC_F32 ? 4 : 8;
+  {
+    unsigned *flag = nullptr;
+    LHPC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&flag), 4));
+    hipError_t e = hipMemset(flag, 0, 4);
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(k_validate_device_csr, dim3(1024), dim3(256), 0, nullptr, row_ptr, row_ptr_bits, col_idx,
+                         n_rows, n_cols, nnz, flag);
+      e = hipGetLastError();
+    }
+    unsigned bad = 0;
+    if (e == hipSuccess) e = hipMemcpy(&bad, flag, 4, hipMemcpyDeviceToHost);
+    (void)hipFree(flag);
+    if (e != hipSuccess) return static_cast<int>(e);
+    if (bad) return LHPC_ERR_BAD_CSR;
+  }
+  const size_t rpb = static_cast<size_t>(n_rows + 1) * (row_ptr_bits / 8);
+  std::vector<unsigned char> hrp(rpb);
+  LHPC_HIP_TRY(hipMemcpy(hrp.data(), row_ptr, rpb, hipMemcpyDeviceToHost));
+  const RowPtrView rp{hrp.data(), row_ptr_bits};
+  // the host path's XTILE decision (plan_create_impl), on the copied row_ptr
+  // and device-fetched locality samples
+  const double x_bytes = static_cast<double>(n_cols) * static_cast<double>(tsz);
+  const double locality_thr = o.spmv_locality > 0 ? o.spmv_locality : 0.25;
+  const bool auto_ok = !(flags & (LHPC_PLAN_FORCE_ROWGROUP | LHPC_PLAN_FORCE_ADAPTIVE | LHPC_PLAN_FORCE_XSLICE |
+                                   LHPC_PLAN_FORCE_XTILE));
+  const int64_t tiles = (n_cols + (tsz == 4 ? 40960 : 20480) - 1) / (tsz == 4 ? 40960 : 20480);
+  int64_t cap = INT32_MAX - 8 * (tiles + 256) - (int64_t{1} << 16);
+  if (o.xtile_part_nnz > 0) cap = std::min<int64_t>(cap, o.xtile_part_nnz);
+  const bool single = n_devices <= 1 && !o.multi_force && nnz <= cap && tiles <= 4096 && n_rows > 0;
+  bool want_xtile = single && (flags & LHPC_PLAN_FORCE_XTILE);
+  if (single && auto_ok && !o.spmv_no_xtile && x_bytes > 8.0e6)
+    want_xtile = gather_lines_per_nnz(
+                     rp,
+                     [&](int64_t k0, int64_t k1, int32_t *dst) {
+                       return static_cast<int>(hipMemcpy(dst, col_idx + k0, static_cast<size_t>(k1 - k0) * 4,
+                                                         hipMemcpyDeviceToHost));
+                     },
+                     n_rows, tsz) > locality_thr;
+  if (want_xtile) {
+    auto *p = new (std::nothrow) lhpc_spmv_plan();
+    if (!p) return LHPC_ERR_ALLOC;
+    p->opt = o;
+    if (n_splits > 0) p->split_rows.assign(split_rows, split_rows + n_splits);
+    p->dtype = dtype;
+    p->device = dev;
+    p->n_rows = n_rows;
+    p->n_cols = n_cols;
+    p->nnz = nnz;
+    const int st = xtile_build_device(p, rp, col_idx, val, tsz);
+    if (st == LHPC_OK) {
+      *out = p;
+      return LHPC_OK;
+    }
+    lhpc_spmv_plan_destroy(p);
+    if (st != LHPC_ERR_UNSUPPORTED) return st;
+  }
+  // every other case: A to the host, the host path
+  std::vector<int32_t> hcol(static_cast<size_t>(nnz));
+  std::vector<unsigned char> hval(static_cast<size_t>(nnz) * tsz);
+  if (nnz) {
+    LHPC_HIP_TRY(hipMemcpy(hcol.data(), col_idx, static_cast<size_t>(nnz) * 4, hipMemcpyDeviceToHost));
+    LHPC_HIP_TRY(hipMemcpy(hval.data(), val, static_cast<size_t>(nnz) * tsz, hipMemcpyDeviceToHost));
+  }
+  return plan_create_impl(out, dtype, n_rows, n_cols, nnz, hrp.data(), row_ptr_bits, hcol.data(), hval.data(),
+                          device_ids, n_devices, flags & ~static_cast<unsigned>(LHPC_PLAN_DEVICE_INPUT), n_splits,
+                          split_rows, opts);
+}
+
 }  // namespace
 }  // namespace lhpc
 
@@ -489,5 +617,38 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
     if (q) (void)hipFree(q);
   if (p->h_scalars) (void)hipHostFree(p->h_scalars);
   delete p;
+  return LHPC_OK;
+}
+
+// Test support: FNV-1a digests of an XTILE plan's device layout, in the
+// order row_ptr, col16, perm/iperm, val runs, chunk descriptors, cr, segment
+// table (lo/len, hi), gather pieces, cont — so a test can byte-compare the
+// layout built on the GPU from device input with the host build's.
+extern "C" int lhpc_spmv_plan_layout_digest(const lhpc_spmv_plan *p, uint64_t *out, int cap, int *n_out) {
+  if (!p || !out || !n_out || cap < 10) return LHPC_ERR_INVALID_ARG;
+  if (p->kernel != LHPC_KERNEL_XTILE || !p->parts.empty() || p->multi) return LHPC_ERR_UNSUPPORTED;
+  LHPC_HIP_TRY(hipSetDevice(p->device));
+  const size_t tsz = p->dtype == LHPC_F32 ? 4 : 8;
+  const int64_t C = p->xt_C, S = p->S, H = (C + kXtSegHi - 1) / kXtSegHi;
+  const std::pair<const void *, size_t> arr[10] = {
+      {p->d_row_ptr, static_cast<size_t>(p->n_rows + 1) * 4},
+      {p->d_col16, static_cast<size_t>(p->xt_total) * 2},
+      {p->d_perm, static_cast<size_t>(p->xt_p == 3 ? p->xt_nrun : p->xt_total + 2) * 2},
+      {p->d_val, static_cast<size_t>(p->xt_nrun) * tsz},
+      {p->d_cdesc, static_cast<size_t>(8 * C + 8) * 4},
+      {p->d_cr, static_cast<size_t>(C + 1) * 4},
+      {p->d_seg, static_cast<size_t>(std::max<int64_t>(C, 1) * S) * 4},
+      {p->d_seghi, static_cast<size_t>(std::max<int64_t>(H, 1) * S) * 4},
+      {p->d_pieces, static_cast<size_t>(p->xt_pieces) * 12},
+      {p->d_cont, static_cast<size_t>(p->xt_cont) * 4}};
+  std::vector<unsigned char> h;
+  for (int i = 0; i < 10; ++i) {
+    h.resize(arr[i].second);
+    if (arr[i].second) LHPC_HIP_TRY(hipMemcpy(h.data(), arr[i].first, arr[i].second, hipMemcpyDeviceToHost));
+    uint64_t x = 0xcbf29ce484222325ull;
+    for (unsigned char b : h) x = (x ^ b) * 0x100000001b3ull;
+    out[i] = x ^ static_cast<uint64_t>(arr[i].second);
+  }
+  *n_out = 10;
   return LHPC_OK;
 }

@@ -40,7 +40,7 @@ struct lhpc_spmv_plan {
   int64_t *d_cbase = nullptr;
   void *d_partial = nullptr;
   // XTILE
-  int64_t xt_C = 0, xt_pieces = 0, xt_cont = 0, xt_total = 0;
+  int64_t xt_C = 0, xt_pieces = 0, xt_cont = 0, xt_total = 0, xt_nrun = 0;
   size_t xt_lds = 0;
   int xt_u = 8;  // gather steps in flight (lhpc_options.xtile_steps)
   int xt_nt = 0;  // gather: non-temporal xg stores (lhpc_options.xtile_store)
@@ -176,5 +176,8 @@ int xtile_part_of_tile(int64_t tile, int64_t tile_width, int64_t n_cols, const i
 int xtile_stage_part(const lhpc_spmv_plan *p, const void *x, int j, hipStream_t s);
 // LHPC_ERR_UNSUPPORTED: the layout does not fit its index types (caller falls back)
 int xtile_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz);
+// the same layout from device-resident col/val (rp: a host copy of row_ptr);
+// LHPC_ERR_UNSUPPORTED for options the device build lacks (aligned segments)
+int xtile_build_device(lhpc_spmv_plan *p, RowPtrView rp_host, const int32_t *d_col, const void *d_val, size_t tsz);
 
 }  // namespace lhpc

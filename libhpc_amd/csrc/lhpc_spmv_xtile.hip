@@ -731,8 +731,123 @@ int launch_reduce(const lhpc_spmv_plan *p, int64_t c0, int64_t c1, int64_t n0, i
   return LHPC_OK;
 }
 
+
+// ---------------------------------------------- device-side layout build
+// The O(nnz) passes of the XTILE layout from device-resident CSR
+// (LHPC_PLAN_DEVICE_INPUT); every decision (chunk cuts, segment offsets,
+// pieces, ranges) stays the host code of lhpc_plan.cpp, fed the counts this
+// pass produces, so the layout is byte-identical to the host build's
+// (tests/test_gpu_spmv.py::test_device_input_layout_matches_host).
+constexpr int kXtBuildMaxS = 4096;
+// lhpc_plan.hpp xtile_wave_pos, on the device
+__device__ __forceinline__ int64_t xtile_wave_pos_dev(int64_t i, int run, int vw) {
+  const int64_t t = i / run, j = i % run, w = t / 64, l = t % 64, q = j / vw, r = j % vw;
+  return w * 64 * run + (q * 64 + l) * vw + r;
+}
+
+// counts[c·S + s] = nonzeros of chunk c in tile s (LDS histogram per chunk)
+__global__ __launch_bounds__(256) void k_xt_counts(const int32_t *__restrict__ ce, const int32_t *__restrict__ col,
+                                                   int64_t W, int S, int32_t *__restrict__ counts) {
+  __shared__ int32_t h[kXtBuildMaxS];
+  const int64_t c = blockIdx.x;
+  for (int s = threadIdx.x; s < S; s += blockDim.x) h[s] = 0;
+  __syncthreads();
+  const int e0 = ce[c], e1 = ce[c + 1];
+  for (int k = e0 + static_cast<int>(threadIdx.x); k < e1; k += blockDim.x)
+    atomicAdd(&h[static_cast<int>(col[k] / W)], 1);
+  __syncthreads();
+  for (int s = threadIdx.x; s < S; s += blockDim.x) counts[c * S + s] = h[s];
+}
+
+// One wave per chunk, its nonzeros in CSR order 64 at a time: a nonzero's
+// slot in its (tile, chunk) segment is the segment's running count plus its
+// rank among the step's lanes with the same tile (lanes matched by one
+// ballot per tile-index bit) — the host scatter's stable order.  Writes
+// col16 at the stream slot, and either perm (the slot's LDS offset) or the
+// CSR-order iperm (flat position in the chunk's segment concatenation) in the
+// wave-transposed run layout, with val in the same layout.
+template <typename T, bool IP>
+__global__ __launch_bounds__(64) void k_xt_scatter(
+    const int32_t *__restrict__ ce, const int32_t *__restrict__ segoff, const int32_t *__restrict__ vbase,
+    const int32_t *__restrict__ col, const T *__restrict__ val, int64_t W, int S, int sbits,
+    uint16_t *__restrict__ col16, uint16_t *__restrict__ perm, uint16_t *__restrict__ ipt, T *__restrict__ valt) {
+  __shared__ int32_t base[kXtBuildMaxS];  // segment start of (s, c)
+  __shared__ int32_t cur[kXtBuildMaxS];   // entries placed so far
+  __shared__ int32_t flat[kXtBuildMaxS];  // flat offset of the segment in the chunk
+  const int64_t c = blockIdx.x;
+  const int lane = threadIdx.x;
+  constexpr int RUN = xt_run<T>(), VW = 16 / static_cast<int>(sizeof(T));
+  for (int s = lane; s < S; s += 64) {
+    base[s] = segoff[c * S + s];
+    cur[s] = 0;
+    flat[s] = segoff[(c + 1) * S + s] - segoff[c * S + s];  // length, scanned below
+  }
+  __syncthreads();
+  if (IP && lane == 0) {  // exclusive scan of the lengths over the tiles (≤ 4096)
+    int32_t f = 0;
+    for (int s = 0; s < S; ++s) {
+      const int32_t l = flat[s];
+      flat[s] = f;
+      f += l;
+    }
+  }
+  __syncthreads();
+  const int e0 = ce[c], e1 = ce[c + 1];
+  const int64_t vb = vbase[c];
+  for (int k0 = e0; k0 < e1; k0 += 64) {
+    const int k = k0 + lane;
+    const bool ok = k < e1;
+    const int32_t cv = ok ? col[k] : 0;
+    const int s = ok ? static_cast<int>(cv / W) : 0;
+    uint64_t m = __ballot(ok);
+    for (int b = 0; b < sbits; ++b) {
+      const uint64_t bal = __ballot(ok && ((s >> b) & 1));
+      m &= ((s >> b) & 1) ? bal : ~bal;
+    }
+    const uint64_t lt = (uint64_t{1} << lane) - 1;
+    const int rank = __popcll(m & lt);
+    const int before = ok ? cur[s] : 0;
+    __builtin_amdgcn_wave_barrier();
+    if (ok && rank == 0) cur[s] = before + __popcll(m);  // the lowest lane of each tile group
+    __builtin_amdgcn_wave_barrier();
+    if (ok) {
+      const int i = k - e0;  // chunk position
+      const int rel = before + rank;
+      const int64_t g = static_cast<int64_t>(base[s]) + rel;
+      col16[g] = static_cast<uint16_t>(cv - s * W);
+      if constexpr (IP) {
+        ipt[vb + xtile_wave_pos_dev(i, RUN, 8)] = static_cast<uint16_t>(flat[s] + rel);
+      } else {
+        perm[g] = static_cast<uint16_t>(xt_slot<T>(i));  // lhpc_plan.hpp xtile_slot(i, sizeof(T))
+      }
+      valt[vb + xtile_wave_pos_dev(i, RUN, VW)] = val[k];
+    }
+  }
+}
+
+// the gather's wave-coalesced store order (lhpc_plan.hpp xtile_gather_pos):
+// inside each piece, every full 512-entry block of col16 from the piece start
+// is permuted so that lane l's 8 entries are the stream positions its 16-B
+// stores cover.  One workgroup (64 lanes) per piece.
+__global__ __launch_bounds__(64) void k_xt_permute_blocks(const int32_t *__restrict__ pieces, int vw,
+                                                          uint16_t *__restrict__ col16) {
+  const int64_t g0 = pieces[3 * blockIdx.x], g1 = pieces[3 * blockIdx.x + 1];
+  const int l = threadIdx.x;
+  for (int64_t g = g0; g + 512 <= g1; g += 512) {
+    uint16_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = col16[g + (k / vw) * 64 * vw + vw * l + k % vw];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) col16[g + 8 * l + k] = v[k];
+    __syncthreads();
+  }
+}
+
+// dev: col_idx and val are device pointers (LHPC_PLAN_DEVICE_INPUT; rp is a
+// host copy of row_ptr): the O(nnz) passes run on the GPU
 template <typename T>
-int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val) {
+int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, bool dev) {
   constexpr size_t tsz = sizeof(T);
   constexpr int M = XtRed<T, xt_red_blk<T>()>::M, RMAX = XtRed<T, xt_red_blk<T>()>::Rmax, RUN = xt_run<T>();
   int cus = 256;
@@ -823,8 +938,36 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
     p->xt_mall = static_cast<int>(p->split_rows.size()) + 1;
   }
   XtileHost xt;
-  LHPC_TRY(build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, M, RMAX, piece, static_cast<int>(tsz),
-                       p->split_rows.data(), static_cast<int>(p->split_rows.size()), ip, cut, xt, al ? VW : 1));
+  // device-side O(nnz) buffers (dev only): chunk starts, segment starts, run bases
+  struct DevTmp {
+    void *a = nullptr;
+    ~DevTmp() {
+      if (a) (void)hipFree(a);
+    }
+  } d_ce, d_segoff, d_vbase, d_counts;
+  if (dev) {
+    if (al) return LHPC_ERR_UNSUPPORTED;  // aligned segments: host build only
+    LHPC_TRY(xtile_plan_chunks(rp.p, rp.bits, nullptr, p->n_rows, p->n_cols, W, M, RMAX, static_cast<int>(tsz),
+                               p->split_rows.data(), static_cast<int>(p->split_rows.size()), ip, cut, xt, 1));
+    const int64_t S = xt.S, C = xt.n_chunks;
+    if (S > kXtBuildMaxS) return LHPC_ERR_UNSUPPORTED;
+    LHPC_HIP_TRY(hipMalloc(&d_ce.a, xt.ce.size() * 4));
+    LHPC_HIP_TRY(hipMemcpy(d_ce.a, xt.ce.data(), xt.ce.size() * 4, hipMemcpyHostToDevice));
+    if (C > 0) {
+      LHPC_HIP_TRY(hipMalloc(&d_counts.a, static_cast<size_t>(C * S) * 4));
+      hipLaunchKernelGGL(k_xt_counts, dim3(static_cast<unsigned>(C)), dim3(256), 0, nullptr,
+                         static_cast<const int32_t *>(d_ce.a), col_idx, W, static_cast<int>(S),
+                         static_cast<int32_t *>(d_counts.a));
+      LHPC_HIP_TRY(hipGetLastError());
+      LHPC_HIP_TRY(hipMemcpy(xt.segoff.data() + S, d_counts.a, static_cast<size_t>(C * S) * 4, hipMemcpyDeviceToHost));
+    }
+    std::vector<int64_t> tbase;
+    LHPC_TRY(xtile_plan_offsets(xt, tbase));
+    xtile_plan_pieces(xt, tbase, piece);
+  } else {
+    LHPC_TRY(build_xtile(rp.p, rp.bits, col_idx, p->n_rows, p->n_cols, W, M, RMAX, piece, static_cast<int>(tsz),
+                         p->split_rows.data(), static_cast<int>(p->split_rows.size()), ip, cut, xt, al ? VW : 1));
+  }
   p->kernel = LHPC_KERNEL_XTILE;
   p->rp64 = 0;
   p->S = xt.S;
@@ -861,10 +1004,26 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   std::vector<int32_t> vbase;
   std::unique_ptr<unsigned char[]> valt;
   std::unique_ptr<uint16_t[]> ipt;
-  LHPC_TRY(xtile_transpose_runs(xt, val, tsz, RUN, 64 * RUN, vbase, valt, ipt));
-  const size_t nrun = static_cast<size_t>(vbase[C]) + 64 * RUN;
-  LHPC_TRY(up(&p->d_val, valt.get(), nrun * tsz));
-  valt.reset();
+  size_t nrun = 0;
+  if (dev) {
+    // run bases as xtile_transpose_runs; the runs themselves come from
+    // k_xt_scatter (val zero-padded, iperm padded with the zero slot M)
+    std::vector<int64_t> vb(static_cast<size_t>(C) + 1, 0);
+    const int64_t reg = 64 * RUN;
+    for (int64_t c = 0; c < C; ++c) vb[c + 1] = vb[c] + (xt.ce[c + 1] - xt.ce[c] + reg - 1) / reg * reg;
+    if (vb[C] + reg >= INT32_MAX) return LHPC_ERR_UNSUPPORTED;
+    vbase.assign(vb.begin(), vb.end());
+    nrun = static_cast<size_t>(vbase[C]) + 64 * RUN;
+    p->xt_nrun = static_cast<int64_t>(nrun);
+    LHPC_TRY(dmalloc(&p->d_val, nrun * tsz, p->bytes));
+    LHPC_HIP_TRY(hipMemset(p->d_val, 0, nrun * tsz));
+  } else {
+    LHPC_TRY(xtile_transpose_runs(xt, val, tsz, RUN, 64 * RUN, vbase, valt, ipt));
+    nrun = static_cast<size_t>(vbase[C]) + 64 * RUN;
+    p->xt_nrun = static_cast<int64_t>(nrun);
+    LHPC_TRY(up(&p->d_val, valt.get(), nrun * tsz));
+    valt.reset();
+  }
   {
     std::vector<int32_t> cd(static_cast<size_t>(8 * C + 8), 0);  // {e0, e1, r0, r1, vbase, 0, 0, 0}
     for (int64_t c = 0; c < C; ++c) {
@@ -887,8 +1046,51 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   }
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_pieces), xt.pieces.data(), xt.pieces.size() * 4));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cont), xt.cont.data(), xt.cont.size() * 4));
-  xtile_permute_gather_blocks(xt, static_cast<int>(16 / tsz));
-  LHPC_TRY(up(reinterpret_cast<void **>(&p->d_col16), xt.col16.get(), static_cast<size_t>(xt.total) * 2));
+  if (dev) {
+    // col16 and perm / iperm + val runs on the device, then the gather-store
+    // permutation of col16 inside every piece
+    const int64_t S = xt.S;
+    LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_col16), static_cast<size_t>(xt.total) * 2, p->bytes));
+    LHPC_HIP_TRY(hipMemset(p->d_col16, 0, static_cast<size_t>(std::max<int64_t>(xt.total, 1)) * 2));
+    if (ip) {
+      LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_perm), nrun * 2, p->bytes));
+      LHPC_HIP_TRY(hipMemsetD16(reinterpret_cast<hipDeviceptr_t>(p->d_perm), static_cast<unsigned short>(M), nrun));
+    } else {
+      LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_perm), static_cast<size_t>(xt.total + 2) * 2, p->bytes));
+      LHPC_HIP_TRY(hipMemset(p->d_perm, 0, static_cast<size_t>(xt.total + 2) * 2));
+      const uint16_t spare[2] = {static_cast<uint16_t>(M), static_cast<uint16_t>(M)};
+      LHPC_HIP_TRY(hipMemcpy(p->d_perm + xt.total, spare, 4, hipMemcpyHostToDevice));
+    }
+    if (C > 0) {
+      LHPC_HIP_TRY(hipMalloc(&d_segoff.a, xt.segoff.size() * 4));
+      LHPC_HIP_TRY(hipMemcpy(d_segoff.a, xt.segoff.data(), xt.segoff.size() * 4, hipMemcpyHostToDevice));
+      LHPC_HIP_TRY(hipMalloc(&d_vbase.a, vbase.size() * 4));
+      LHPC_HIP_TRY(hipMemcpy(d_vbase.a, vbase.data(), vbase.size() * 4, hipMemcpyHostToDevice));
+      int sbits = 0;
+      while ((int64_t{1} << sbits) < S) ++sbits;
+      if (ip)
+        hipLaunchKernelGGL((k_xt_scatter<T, true>), dim3(static_cast<unsigned>(C)), dim3(64), 0, nullptr,
+                           static_cast<const int32_t *>(d_ce.a), static_cast<const int32_t *>(d_segoff.a),
+                           static_cast<const int32_t *>(d_vbase.a), col_idx, static_cast<const T *>(val), W,
+                           static_cast<int>(S), sbits, p->d_col16, nullptr, p->d_perm, static_cast<T *>(p->d_val));
+      else
+        hipLaunchKernelGGL((k_xt_scatter<T, false>), dim3(static_cast<unsigned>(C)), dim3(64), 0, nullptr,
+                           static_cast<const int32_t *>(d_ce.a), static_cast<const int32_t *>(d_segoff.a),
+                           static_cast<const int32_t *>(d_vbase.a), col_idx, static_cast<const T *>(val), W,
+                           static_cast<int>(S), sbits, p->d_col16, p->d_perm, nullptr, static_cast<T *>(p->d_val));
+      LHPC_HIP_TRY(hipGetLastError());
+    }
+    const int64_t np = static_cast<int64_t>(xt.pieces.size() / 3);
+    if (np > 0) {
+      hipLaunchKernelGGL(k_xt_permute_blocks, dim3(static_cast<unsigned>(np)), dim3(64), 0, nullptr, p->d_pieces,
+                         static_cast<int>(16 / tsz), p->d_col16);
+      LHPC_HIP_TRY(hipGetLastError());
+    }
+    LHPC_HIP_TRY(hipDeviceSynchronize());
+  } else {
+    xtile_permute_gather_blocks(xt, static_cast<int>(16 / tsz));
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_col16), xt.col16.get(), static_cast<size_t>(xt.total) * 2));
+  }
   {
     std::vector<uint32_t> seg;
     std::vector<int32_t> seghi;
@@ -896,7 +1098,9 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_seg), seg.data(), seg.size() * 4));
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_seghi), seghi.data(), seghi.size() * 4));
   }
-  if (ip) {
+  if (dev) {
+    // built above
+  } else if (ip) {
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_perm), ipt.get(), nrun * 2));
   } else {
     // one sentinel entry past the stream: the reduce loads it for positions
@@ -1010,7 +1214,11 @@ int xtile_stage_part(const lhpc_spmv_plan *p, const void *x, int j, hipStream_t 
 }
 
 int xtile_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz) {
-  return tsz == 4 ? build_t<float>(p, rp, col_idx, val) : build_t<double>(p, rp, col_idx, val);
+  return tsz == 4 ? build_t<float>(p, rp, col_idx, val, false) : build_t<double>(p, rp, col_idx, val, false);
+}
+
+int xtile_build_device(lhpc_spmv_plan *p, RowPtrView rp_host, const int32_t *d_col, const void *d_val, size_t tsz) {
+  return tsz == 4 ? build_t<float>(p, rp_host, d_col, d_val, true) : build_t<double>(p, rp_host, d_col, d_val, true);
 }
 
 }  // namespace lhpc

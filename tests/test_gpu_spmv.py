@@ -554,21 +554,22 @@ def test_xtile_row_parts_row_past_cap(lhpc, gpu):
 
 
 @pytest.mark.slow
-def test_xtile_parts_150m_past_int32(lhpc, gpu):
-    """Past the int32 stream: n = 150M rows and columns, 15 uniform nonzeros
-    per row (nnz = 2.25e9 > 2^31, int64 row_ptr, fp32, dyadic values).
-    Before row parts this plan fell to XSLICE; now it stays XTILE (two row
-    parts).  10^5 sampled rows bit-exact against fp64 numpy (exact on
-    dyadic data), the whole y equal run to run, and GFLOP/s printed (C2
-    level expected: per part the same kernels as C2)."""
+def test_xtile_parts_past_int32(lhpc, gpu):
+    """Past the int32 tile stream: n = 20M rows and columns, 108 uniform
+    nonzeros per row (nnz = 2.16e9 > 2^31, int64 row_ptr, fp32, dyadic
+    values).  Before row parts this plan fell to XSLICE; now it stays XTILE
+    (two row parts over the same 512 tiles).  10^5 sampled rows bit-exact
+    against fp64 numpy (exact on dyadic data), the whole y equal run to run,
+    and GFLOP/s printed (per part the same kernels and segment lengths as
+    C2, so C2-level rates are expected)."""
     import torch
-    n = 150_000_000
-    rp, col, val = lhpc.gen_uniform_csr(n, n, 15, dtype=lhpc.F32, dist=1, seed=0x15000)
+    n, per_row = 20_000_000, 108
+    rp, col, val = lhpc.gen_uniform_csr(n, n, per_row, dtype=lhpc.F32, dist=1, seed=0x15000)
     assert rp.dtype == np.int64 and int(rp[-1]) > 2**31
     x = lhpc.gen_values(lhpc.F32, 1, n, 0x15001)
     with lhpc.SpMVPlan(rp, col, val, n) as plan:
         info = plan.info()
-        assert info["kernel"] == lhpc.KERNEL_XTILE and info["nnz"] == 15 * n
+        assert info["kernel"] == lhpc.KERNEL_XTILE and info["nnz"] == per_row * n
         xd = torch.from_numpy(x).to(gpu)
         y1 = plan(xd).clone()
         y2 = plan(xd)
@@ -581,7 +582,8 @@ def test_xtile_parts_150m_past_int32(lhpc, gpu):
         t1.record()
         torch.cuda.synchronize()
         ms = t0.elapsed_time(t1) / 5
-        print(f"\n150M XTILE parts: {ms:.3f} ms/call, {2 * 15 * n / ms / 1e6:.1f} GFLOP/s, launches {info['launches']}")
+        print(f"\nXTILE row parts, nnz {per_row * n}: {ms:.3f} ms/call, {2 * per_row * n / ms / 1e6:.1f} GFLOP/s, "
+              f"launches {info['launches']}")
         y = y1.cpu().numpy()
         del xd, y1, y2
     rows, y64, _ = S.sampled_rows_fp64(rp, col, val, x, 100_000)
@@ -606,3 +608,95 @@ def test_xslice_dispatch_past_2p32_work_items(lhpc, gpu):
         y = plan(torch.from_numpy(x).to(gpu)).cpu().numpy()
     rows, y64, _ = S.sampled_rows_fp64(rp, col, val, x, 100_000)
     assert np.array_equal(y[rows].astype(np.float64), y64)
+
+
+def _digests_host_vs_device(lhpc, gpu, rp, col, val, n_cols, flags=0, options=None, splits=None):
+    import torch
+    kw = dict(flags=flags, options=options, splits=splits)
+    with lhpc.SpMVPlan(rp, col, val, n_cols, **kw) as ph:
+        dh, ih = ph.layout_digest(), ph.info()
+    drp, dcol, dval = (torch.from_numpy(np.ascontiguousarray(a)).to(gpu) for a in (rp, col, val))
+    with lhpc.SpMVPlan(drp, dcol, dval, n_cols, **kw) as pd:
+        dd, idev = pd.layout_digest(), pd.info()
+        if splits is None:
+            x = (np.random.default_rng(5).integers(-8, 9, size=n_cols) / 8.0).astype(val.dtype)
+            y = pd(torch.from_numpy(x).to(gpu)).cpu().numpy()
+            assert np.array_equal(y, S.spmv_oracle(rp, col, val, x)[1])
+    assert ih == idev
+    return dh, dd
+
+
+@pytest.mark.parametrize("case", ["uniform_f32", "uniform_f64", "powerlaw_f32", "perm_f32", "ranges_f32",
+                                  "splits_f64", "rp64_f32"])
+def test_device_input_layout_matches_host(lhpc, gpu, case):
+    """LHPC_PLAN_DEVICE_INPUT: an XTILE plan built on the GPU from device
+    row_ptr / col_idx / val (k_xt_counts → host offsets → k_xt_scatter →
+    k_xt_permute_blocks) has the host build's layout byte for byte (FNV-1a
+    digests of row_ptr, col16, perm/iperm, val runs, chunk descriptors, cr,
+    the segment table, the gather pieces and cont), the same plan info, and
+    gives the oracle's y bit for bit (dyadic).  Cases: uniform fp32 / fp64
+    (iperm reduce), power-law rows crossing chunks (cont, fix-up), the perm
+    reduce, cache-sized ranges (per-range pieces), a row-range split plan
+    (fp64), and int64 row_ptr input."""
+    n = 3_000_000
+    dt = lhpc.F64 if "f64" in case else lhpc.F32
+    if case.startswith("powerlaw"):
+        rp, col, val = lhpc.gen_powerlaw_csr(n, n, lmax=5000, dtype=dt, dist=1, seed=0xDE00)
+    else:
+        rp, col, val = lhpc.gen_uniform_csr(n, n, 7, dtype=dt, dist=1, seed=0xDE01, narrow=case != "rp64_f32")
+    opts, splits = None, None
+    if case == "perm_f32":
+        opts = {"xtile_reduce": lhpc.XTILE_REDUCE_PERM}
+    elif case == "ranges_f32":
+        opts = {"xtile_ranges": 3}
+    elif case == "splits_f64":
+        splits = [n // 3, n // 2 + 7]
+    if case == "rp64_f32":
+        assert rp.dtype == np.int64
+    dh, dd = _digests_host_vs_device(lhpc, gpu, rp, col, val, n, options=opts, splits=splits)
+    assert dh == dd, [i for i, (a, b) in enumerate(zip(dh, dd)) if a != b]
+
+
+def test_device_input_checks_and_fallbacks(lhpc, gpu):
+    """Device input that does not select XTILE (x fits L2: ADAPTIVE) goes
+    through the host path and is exact; malformed device CSR is refused on
+    the GPU with LHPC_ERR_BAD_CSR (a column out of range, a decreasing
+    row_ptr)."""
+    import torch
+    n = 50_000
+    rp, col, val = lhpc.gen_uniform_csr(n, n, 5, dtype=lhpc.F32, dist=1, seed=0xDE10)
+    x = lhpc.gen_values(lhpc.F32, 1, n, 0xDE11)
+    dev = [torch.from_numpy(np.ascontiguousarray(a)).to(gpu) for a in (rp, col, val)]
+    with lhpc.SpMVPlan(*dev, n) as p:
+        assert p.info()["kernel"] == lhpc.KERNEL_ADAPTIVE
+        assert np.array_equal(p(torch.from_numpy(x).to(gpu)).cpu().numpy(), S.spmv_oracle(rp, col, val, x)[1])
+    bad_col = dev[1].clone()
+    bad_col[123] = n
+    with pytest.raises(lhpc.LhpcError) as e:
+        lhpc.SpMVPlan(dev[0], bad_col, dev[2], n)
+    assert e.value.status == -2
+    bad_rp = dev[0].clone()
+    bad_rp[7] = bad_rp[9] + 1
+    with pytest.raises(lhpc.LhpcError) as e:
+        lhpc.SpMVPlan(bad_rp, dev[1], dev[2], n)
+    assert e.value.status == -2
+
+
+def test_coo_to_csr_to_spmv_stays_on_device(lhpc, gpu):
+    """SURVEY §8f chain without a host round trip for A: COO triples on the
+    device → lhpc_coo_to_csr (GPU radix sort) → device CSR → an XTILE plan
+    built on the GPU from it (LHPC_PLAN_DEVICE_INPUT) → y = A·x, against the
+    oracle on the same triples (dyadic, duplicates summed)."""
+    import torch
+    n, m = 2_500_000, 12_000_000
+    rng = np.random.default_rng(0xDE20)
+    r = rng.integers(0, n, m).astype(np.int32)
+    c = rng.integers(0, n, m).astype(np.int32)
+    v = (rng.integers(-8, 9, m) / 8.0).astype(np.float32)
+    want_rp, want_col, want_val = S.coo_oracle(n, n, r, c, v)
+    rp, col, val = lhpc.coo_to_csr(n, n, *(torch.from_numpy(a).to(gpu) for a in (r, c, v)), row_ptr_bits=32)
+    with lhpc.SpMVPlan(rp, col, val, n) as p:
+        assert p.info()["kernel"] == lhpc.KERNEL_XTILE
+        x = lhpc.gen_values(lhpc.F32, 1, n, 0xDE21)
+        y = p(torch.from_numpy(x).to(gpu)).cpu().numpy()
+    assert np.array_equal(y, S.spmv_oracle(want_rp, want_col, want_val, x)[1])
