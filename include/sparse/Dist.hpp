@@ -151,6 +151,31 @@ void spmv(DistSpMVPlan<T> &plan, const T *d_x, T *d_y, void *stream = nullptr) {
   lhpc::checkLhpc(lhpc_dist_spmv(plan.native(), d_x, d_y, stream));
 }
 
+// Iterative use (y of call n is x of call n+1): begin leaves the exchange of y
+// in flight; a begin whose x is the previous begin's y gathers x by column
+// part as each exchange chunk lands (cross-step overlap); end waits for it
+template <typename T>
+void spmv_begin(DistSpMVPlan<T> &plan, const T *d_x, T *d_y, void *stream = nullptr) {
+  lhpc::checkLhpc(lhpc_dist_spmv_begin(plan.native(), d_x, d_y, stream));
+}
+template <typename T>
+void spmv_end(DistSpMVPlan<T> &plan, void *stream = nullptr) {
+  lhpc::checkLhpc(lhpc_dist_spmv_end(plan.native(), stream));
+}
+
+// Conjugate gradient over the distributed plan (lhpc_dist_cg_solve): b, x
+// (initial guess in, whole solution out on every rank) and p_work are
+// full-length device vectors; returns {iterations, ‖r‖/‖b‖}
+template <typename T>
+std::pair<int, double> cg(DistSpMVPlan<T> &plan, const T *d_b, T *d_x, T *d_p_work, double tol = 1e-8,
+                          int max_iter = 1000, int check_every = 1, void *stream = nullptr) {
+  int it = 0;
+  double res = 0.0;
+  lhpc::checkLhpc(lhpc_dist_cg_solve(plan.native(), d_b, d_x, d_p_work, tol, max_iter, check_every, &it, &res,
+                                     stream));
+  return {it, res};
+}
+
 // the y exchange of a call alone (every chunk; y holds this rank's blocks)
 template <typename T>
 void exchange(DistSpMVPlan<T> &plan, T *d_y, void *stream = nullptr) {

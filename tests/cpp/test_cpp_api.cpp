@@ -8,7 +8,9 @@
 // AlignedAlloc.hpp fails to link this way; ours must not.
 #include <HPCHighDimensionFlatArray.hpp>
 #include <Stencil.hpp>
+#include <sparse/DeviceCSR.hpp>
 #include <sparse/Dist.hpp>
+#include <sparse/SparseDS.hpp>
 #include <sparse/SpMV.hpp>
 
 #include <hip/hip_runtime.h>
@@ -180,13 +182,23 @@ int gpu_mode() {
       if (!hip_ok(hipMemcpy(yd.data(), dy, sizeof(float) * n, hipMemcpyDeviceToHost))) return fail("hipMemcpy");
       for (std::int64_t i = 0; i < n; ++i)
         if (yd[std::size_t(i)] != y(i)) return fail("local-comm dist spmv mismatch");
-      bool threw = false;
-      try {
-        lc.allreduce_sum(dd, 4);  // needs RCCL
-      } catch (const std::system_error &) {
-        threw = true;
-      }
-      if (!threw) return fail("allreduce on a local communicator must fail");
+      // the P2P scalar all-reduce of a local communicator (world 1: unchanged)
+      lc.allreduce_sum(dd, 4);
+      if (!hip_ok(hipMemcpy(b4, dd, sizeof(b4), hipMemcpyDeviceToHost))) return fail("hipMemcpy");
+      for (int i = 0; i < 4; ++i)
+        if (b4[i] != h4[i]) return fail("local-comm allreduce world 1");
+    }
+    // chained calls (cross-step overlap API) at world 1: x → y → x
+    {
+      float *dz = nullptr;
+      if (!hip_ok(hipMalloc(&dz, sizeof(float) * m))) return fail("hipMalloc");
+      sparse::spmv_begin(dplan, dx, dy);
+      sparse::spmv_end(dplan);
+      std::vector<float> y1(static_cast<std::size_t>(n));
+      if (!hip_ok(hipMemcpy(y1.data(), dy, sizeof(float) * n, hipMemcpyDeviceToHost))) return fail("hipMemcpy");
+      for (std::int64_t i = 0; i < n; ++i)
+        if (y1[std::size_t(i)] != y(i)) return fail("spmv_begin/end mismatch");
+      (void)hipFree(dz);
     }
     // explicit variant options: the RCCL exchange driven at world 1 (an
     // in-place no-op), then the exchange alone; the schedule as data
@@ -207,6 +219,48 @@ int gpu_mode() {
       if (rows != n) return fail("broadcast schedule covers every row once");
     }
     if (!hip_ok(hipFree(dx)) || !hip_ok(hipFree(dy)) || !hip_ok(hipFree(dd))) return fail("hipFree");
+  }
+  // ---- single-process multi-device plan: the device listed
+  //      twice (the box has one GPU) — host vectors, then full replicas
+  {
+    sparse::SpMVPlan<float> mplan(A, std::vector<int>{0, 0});
+    if (mplan.devices() != 2) return fail("multi plan devices");
+    hpc::HPCHighDimensionFlatArray<1, float> ym(n);
+    sparse::spmv(mplan, x, ym);
+    for (std::int64_t i = 0; i < n; ++i)
+      if (ym(i) != y(i)) return fail("multi-device spmv mismatch");
+    float *dx = nullptr, *dy0 = nullptr, *dy1 = nullptr;
+    if (hipMalloc(&dx, sizeof(float) * m) != hipSuccess || hipMalloc(&dy0, sizeof(float) * n) != hipSuccess ||
+        hipMalloc(&dy1, sizeof(float) * n) != hipSuccess)
+      return fail("hipMalloc");
+    if (hipMemcpy(dx, x.data(), sizeof(float) * m, hipMemcpyHostToDevice) != hipSuccess) return fail("hipMemcpy");
+    sparse::spmv_multi(mplan, {dx, dx}, {dy0, dy1});
+    if (hipDeviceSynchronize() != hipSuccess) return fail("sync");
+    std::vector<float> h0(static_cast<std::size_t>(n)), h1(static_cast<std::size_t>(n));
+    if (hipMemcpy(h0.data(), dy0, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(h1.data(), dy1, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess)
+      return fail("hipMemcpy");
+    for (std::int64_t i = 0; i < n; ++i)
+      if (h0[std::size_t(i)] != y(i) || h1[std::size_t(i)] != y(i)) return fail("multi-device replicas mismatch");
+    (void)hipFree(dx);
+    (void)hipFree(dy0);
+    (void)hipFree(dy1);
+  }
+  // ---- RootGrid → device CSR (GPU COO → CSR) → plan from device arrays
+  {
+    sparse::RootGrid<float, sparse::HashBlock<sparse::DenseBlock<16, float>>> grid;
+    for (std::int64_t i = 0; i < n; ++i)
+      for (auto k = A.row_ptr[i]; k < A.row_ptr[i + 1]; ++k) grid.write(i, A.col_idx[k], A.val[k] == 0.f ? 0.5f : A.val[k]);
+    auto dA = sparse::to_csr_device<float>(grid, 0, 0, n, m, 0);
+    sparse::SpMVPlan<float> dplan2(dA.view());
+    hpc::HPCHighDimensionFlatArray<1, float> yg(n);
+    sparse::spmv(dplan2, x, yg);
+    for (std::int64_t i = 0; i < n; ++i) {
+      double s = 0;
+      for (auto k = A.row_ptr[i]; k < A.row_ptr[i + 1]; ++k)
+        s += double(A.val[k] == 0.f ? 0.5f : A.val[k]) * double(x(A.col_idx[k]));
+      if (static_cast<float>(s) != yg(i)) return fail("grid → device CSR → spmv mismatch");
+    }
   }
   std::printf("cpp api gpu: ok (spmv kernel %d)\n", plan.info().kernel);
   return 0;
