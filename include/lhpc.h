@@ -199,7 +199,10 @@ typedef struct lhpc_options {
                                    stores, RCCL = ncclCommInitAll group
                                    all-gathers (distinct devices only)          */
   int32_t multi_force;          /* 1: the multi-device path even for one device */
-  int32_t reserved[3];
+  int32_t dist_reduce_streams;  /* lhpc_dist_spmv: chunk reduces alternate over this many
+                                   streams (1 or 2; 0: 2), so chunk k+1 fills the CUs
+                                   chunk k's tail leaves idle                        */
+  int32_t reserved[2];
 } lhpc_options;
 void lhpc_options_init(lhpc_options *opts);
 

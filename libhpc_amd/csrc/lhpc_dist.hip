@@ -110,6 +110,10 @@ struct lhpc_dist_spmv_plan {
   // x by column parts (part j = the columns exchange j delivers)
   const void *pending_y = nullptr;
   bool chain = false;
+  // chunk reduces alternate over the caller's stream and s_red2
+  // (options.dist_reduce_streams), joined by ev_fork / ev_join
+  hipStream_t s_red2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   double *h_scalars = nullptr;  // lhpc_dist_cg_solve: 2 pinned host scalars (first solve; freed with the plan)
 };
 
@@ -348,6 +352,12 @@ void destroy_spmv(lhpc_dist_spmv_plan *d) {
   for (hipEvent_t e : d->ev_x)
     if (e) (void)hipEventDestroy(e);
   if (d->done) (void)hipEventDestroy(d->done);
+  if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
+  if (d->ev_join) (void)hipEventDestroy(d->ev_join);
+  if (d->s_red2) {
+    (void)hipStreamSynchronize(d->s_red2);
+    (void)hipStreamDestroy(d->s_red2);
+  }
   if (d->h_scalars) (void)hipHostFree(d->h_scalars);
   if (d->ev_p2p) (void)hipEventDestroy(d->ev_p2p);
   delete d;
@@ -812,6 +822,12 @@ extern "C" int lhpc_dist_spmv_plan_create_opts(lhpc_dist_spmv_plan **out, lhpc_d
     for (auto &e : d->ev)
       if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->done, hipEventDisableTiming));
+    const int nstreams = o.dist_reduce_streams > 0 ? o.dist_reduce_streams : 2;
+    if (st == LHPC_OK && nstreams > 1 && K > 1) {
+      st = static_cast<int>(hipStreamCreateWithFlags(&d->s_red2, hipStreamNonBlocking));
+      if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
+      if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
+    }
     if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->ev_p2p, hipEventDisableTiming));
   }
   if (st != LHPC_OK) {
@@ -864,11 +880,24 @@ int spmv_begin(lhpc_dist_spmv_plan *d, const void *x, void *y, hipStream_t s, bo
     if (chained) LHPC_TRY(wait_pending(d, s));
     LHPC_TRY(lhpc::local_plans_stage(d->lp, x, s));
   }
+  // two reduce streams: chunk k on s (even k) or s_red2 (odd k), so the next
+  // chunk's workgroups take the CUs a chunk's last round leaves idle; range
+  // gathers (a range's first entries come from the range before) stay on one
+  const bool two = d->s_red2 && d->K > 1 && !d->lp.range_gather();
+  if (two) {
+    LHPC_HIP_TRY(hipEventRecord(d->ev_fork, s));
+    LHPC_HIP_TRY(hipStreamWaitEvent(d->s_red2, d->ev_fork, 0));
+  }
   for (int k = 0; k < d->K; ++k) {
+    hipStream_t sk = two && (k & 1) ? d->s_red2 : s;
     const int64_t b = static_cast<int64_t>(k) * c->nranks + c->rank;
     void *yk = static_cast<unsigned char *>(y) + d->cuts[b] * tsz;
-    LHPC_TRY(lhpc::local_plans_chunk(d->lp, x, k, yk, gathered, s));
-    if (xchg) LHPC_TRY(exchange_chunk(d, xk, win, k, y, s));
+    LHPC_TRY(lhpc::local_plans_chunk(d->lp, x, k, yk, gathered, sk));
+    if (xchg) LHPC_TRY(exchange_chunk(d, xk, win, k, y, sk));
+  }
+  if (two) {
+    LHPC_HIP_TRY(hipEventRecord(d->ev_join, d->s_red2));
+    LHPC_HIP_TRY(hipStreamWaitEvent(s, d->ev_join, 0));
   }
   if (xchg) {
     LHPC_HIP_TRY(hipEventRecord(d->done, c->s_comm));

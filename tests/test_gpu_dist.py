@@ -96,7 +96,8 @@ def test_dist_spmv_world1_rccl_exchange(lhpc, gpu, comm, mode, uniform):
 @pytest.mark.parametrize("K", [1, 2, 3, 4])
 @pytest.mark.parametrize("case", [(3_000_000, 6, "f32"), (2_500_000, 5, "f64"), (20_000, 7, "f64")],
                          ids=["xtile-f32", "xtile-f64", "blocks-f64"])
-def test_dist_spmv_chained_world1(lhpc, gpu, comm, K, case):
+@pytest.mark.parametrize("streams", [1, 2])
+def test_dist_spmv_chained_world1(lhpc, gpu, comm, K, case, streams):
     """Cross-step overlap (lhpc_dist_spmv_begin / _end) at world 1 with the
     RCCL exchange issued (options.dist_world1): five chained calls, y of call
     n is x of call n+1 (ping-pong), no end between them — each chained stage
@@ -104,7 +105,9 @@ def test_dist_spmv_chained_world1(lhpc, gpu, comm, K, case):
     before (XTILE row-range plans; the per-block plans of the small matrix
     wait for the whole exchange instead).  Every iterate equals the oracle's
     bit for bit (dyadic values; snapshots of y(n) taken on the stream after
-    the chained stage of call n+1 has waited for it)."""
+    the chained stage of call n+1 has waited for it).  streams: the chunk
+    reduces on the caller's stream only, or alternating with a second one
+    (options.dist_reduce_streams, default 2)."""
     import torch
     n, per_row, dts = case
     dt = lhpc.F32 if dts == "f32" else lhpc.F64
@@ -118,7 +121,7 @@ def test_dist_spmv_chained_world1(lhpc, gpu, comm, K, case):
     cuts = lhpc.interleaved_cuts(rp, 1, K)
     s = torch.cuda.current_stream(gpu)
     with lhpc.DistSpMVPlan(comm, n, n, K, cuts, *lhpc.interleaved_local_csr(rp, col, val, cuts, 1, K, 0),
-                           options={"dist_world1": 1}) as d:
+                           options={"dist_world1": 1, "dist_reduce_streams": streams}) as d:
         bufs = [torch.from_numpy(x).to(gpu), torch.full((n,), float("nan"), dtype=torch.float32 if dts == "f32"
                                                         else torch.float64, device=gpu)]
         bufs.append(torch.full_like(bufs[1], float("nan")))

@@ -48,6 +48,10 @@ for dts in (os.environ.get("DTYPES", "f32 f64")).split():
             with L.DistSpMVPlan(comm, n, n, K, cuts, lrp, lc, lv,
                                 options={"dist_exchange": L.DIST_EXCHANGE_NONE}) as d:
                 rec["local_ms"] = timed(lambda: d(x, y))
+            if K > 1:  # the chunk reduces on one stream (round 3's schedule)
+                with L.DistSpMVPlan(comm, n, n, K, cuts, lrp, lc, lv,
+                                    options={"dist_exchange": L.DIST_EXCHANGE_NONE, "dist_reduce_streams": 1}) as d:
+                    rec["local_ms_1stream"] = timed(lambda: d(x, y))
             comm.close()
             if K > 1:
                 splits = [int(v) for v in (lambda ls: ls[1:-1])(
