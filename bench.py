@@ -320,15 +320,17 @@ def main():
                 e2e = timed(lambda dp=dp, yb=yb: dp(xd, yb, stream=stream), args.steps, args.warmup)
                 xo = timed(lambda dp=dp, yb=yb: dp.exchange(yb, stream=stream), args.steps, args.warmup)
                 ch = timed_chain(dp, yb, ybuf_b[kx], args.steps, args.warmup)
-                # chained calls must give what two plain calls give (every rank agrees)
-                dp(xd, y_full, stream=stream)
-                dp(y_full, y_full_b, stream=stream)
-                ref2 = y_full_b.clone()
-                ybuf_b[kx].copy_(xd)
-                dp.begin(ybuf_b[kx], yb, stream=stream)
-                dp.begin(yb, ybuf_b[kx], stream=stream)
+                # chained calls must give what two plain calls give (every rank
+                # agrees); the plan's own y buffers (P2P plans need windows)
+                ybb = ybuf_b[kx]
+                dp(xd, yb, stream=stream)
+                dp(yb, ybb, stream=stream)
+                ref2 = ybb.clone()
+                ybb.copy_(xd)
+                dp.begin(ybb, yb, stream=stream)
+                dp.begin(yb, ybb, stream=stream)
                 dp.end(stream=stream)
-                same = torch.tensor([1 if torch.equal(ref2, ybuf_b[kx]) else 0], dtype=torch.int32, device=dev)
+                same = torch.tensor([1 if torch.equal(ref2, ybb) else 0], dtype=torch.int32, device=dev)
                 if world > 1:
                     dist.all_reduce(same, op=dist.ReduceOp.MIN)
                 xtimes[kx] = {"step_ms": e2e * 1e3, "exchange_only_ms": xo * 1e3,
