@@ -30,21 +30,28 @@ namespace {
 // fetch(k0, k1, out): the columns of nonzeros [k0, k1) (host array or a copy
 // from device-resident input)
 template <typename RP, typename Fetch>
-double gather_lines_per_nnz(const RP &rp, Fetch fetch, int64_t n_rows, size_t tsz) {
+double gather_lines_per_nnz(const RP &rp, Fetch fetch, int64_t n_rows, int64_t n_cols, size_t tsz) {
   constexpr int64_t kChunk = 8192, kSamples = 32;
   const int shift = tsz == 8 ? 4 : 5;  // 16 doubles / 32 floats per line
   const int64_t chunks = (n_rows + kChunk - 1) / kChunk;
   const int64_t step = std::max<int64_t>(1, chunks / kSamples);
   int64_t lines = 0, nz = 0;
   std::vector<int32_t> buf;
+  // distinct lines per sample with a bitmap over x's lines (set, count, then
+  // clear what was set): O(nonzeros) where a sort + unique cost ≈ 0.2 s for C2
+  std::vector<uint64_t> seen(static_cast<size_t>(((n_cols >> shift) + 64) / 64), 0);
   for (int64_t c = 0; c < chunks; c += step) {
     const int64_t r0 = c * kChunk, r1 = std::min(n_rows, r0 + kChunk);
     const int64_t k0 = rp[r0], k1 = rp[r1];
     buf.resize(static_cast<size_t>(k1 - k0));
     if (k1 > k0 && fetch(k0, k1, buf.data()) != LHPC_OK) return 1.0;
-    for (auto &v : buf) v >>= shift;
-    std::sort(buf.begin(), buf.end());
-    lines += std::unique(buf.begin(), buf.end()) - buf.begin();
+    for (const int32_t v : buf) {
+      const uint64_t l = static_cast<uint64_t>(v) >> shift, bit = uint64_t{1} << (l & 63);
+      uint64_t &w = seen[static_cast<size_t>(l >> 6)];
+      lines += (w & bit) ? 0 : 1;
+      w |= bit;
+    }
+    for (const int32_t v : buf) seen[static_cast<size_t>((static_cast<uint64_t>(v) >> shift) >> 6)] = 0;
     nz += k1 - k0;
   }
   return nz ? static_cast<double>(lines) / static_cast<double>(nz) : 1.0;
@@ -245,7 +252,7 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
             std::memcpy(out, col_idx + k0, static_cast<size_t>(k1 - k0) * 4);
             return LHPC_OK;
           },
-          n_rows, tsz) > locality_thr;
+          n_rows, n_cols, tsz) > locality_thr;
   // XTILE (x tiles in LDS) is the default for gathers without locality;
   // options.spmv_no_xtile selects XSLICE instead.
   const bool want_xtile = (flags & LHPC_PLAN_FORCE_XTILE) || (nolocal && !o.spmv_no_xtile);
@@ -421,7 +428,7 @@ int plan_create_device_input(lhpc_spmv_plan **out, int dtype, int64_t n_rows, in
                        return static_cast<int>(hipMemcpy(dst, col_idx + k0, static_cast<size_t>(k1 - k0) * 4,
                                                          hipMemcpyDeviceToHost));
                      },
-                     n_rows, tsz) > locality_thr;
+                     n_rows, n_cols, tsz) > locality_thr;
   if (want_xtile) {
     auto *p = new (std::nothrow) lhpc_spmv_plan();
     if (!p) return LHPC_ERR_ALLOC;
