@@ -101,6 +101,15 @@ hipError_t g_pool_err[kMaxDevices] = {};
 hipError_t scratch_pool(int dev, hipMemPool_t *out) {
   if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
   std::call_once(g_pool_once[dev], [dev] {
+#ifdef LHPC_SCRATCH_DEFAULT_POOL  // A/B build: the device's default pool
+    hipError_t e = hipDeviceGetDefaultMemPool(&g_pool[dev], dev);
+    if (e == hipSuccess) {
+      uint64_t thr = UINT64_MAX;
+      e = hipMemPoolSetAttribute(g_pool[dev], hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    g_pool_err[dev] = e;
+    return;
+#endif
     hipMemPoolProps props{};
     props.allocType = hipMemAllocationTypePinned;
     props.handleTypes = hipMemHandleTypeNone;
