@@ -21,6 +21,10 @@ import sys
 from collections import defaultdict
 
 
+# kernels of the device-input plan build (bench.py times it once per run)
+PLAN_BUILD = {"k_validate_device_csr", "k_xt_counts", "k_xt_scatter", "k_xt_permute_blocks"}
+
+
 def per_kernel(d, counter):
     vals = defaultdict(list)
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
@@ -73,6 +77,9 @@ def main():
                              "raw_fetch_bytes": fetch[k], "launches_per_call": per_call.get(k, 1)}
         if k.startswith("k_copyw"):  # bench.py's copy-ceiling probe, not part of the workload
             ent["kernels"][k]["probe"] = True
+            continue
+        if k in PLAN_BUILD:  # device-side plan build (once per plan, not per call)
+            ent["kernels"][k]["plan_build"] = True
             continue
         tot += (rb + wb) * per_call.get(k, 1)
     ent["bytes_per_call"] = tot
