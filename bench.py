@@ -96,9 +96,10 @@ def parse():
     ap.add_argument("--n", type=int, default=10_000_000)
     ap.add_argument("--per-row", type=int, default=15)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--chunks", type=int, default=4,
-                    help="N>1: row chunks per rank K (exchange overlap; K = 4 is the step model's best for N = 2-8, "
-                         "tools/step_model.py, DESIGN.md §6)")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="N>1: row chunks per rank K (exchange overlap).  0 (default): the native path measures "
+                         "K = 1, 2, 4 and reports the fastest (the step model, tools/step_model.py, puts K = 4 "
+                         "first at 64 GB/s per xGMI link, DESIGN.md §6.3); other paths use 4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spmv-options", default=None,
                     help="JSON dict of lhpc_options fields for the 1-GPU SpMV plan (measured alternatives, DESIGN.md §4)")
@@ -226,64 +227,29 @@ def main():
             # a plan option), each over the same local rows.
             has_rccl = dist.get_backend() == "nccl"
             comm = L.DistComm.from_torch(local) if has_rccl else L.DistComm.local(world, rank, local)
-            cuts = L.interleaved_cuts(rp, world, args.chunks)
-            lrp, lc, lv = L.interleaved_local_csr(rp, col, val, cuts, world, args.chunks, rank)
-            dplans, xnotes = {}, {}
-            if has_rccl:
-                dplans["rccl"] = L.DistSpMVPlan(comm, n, n, args.chunks, cuts, lrp, lc, lv,
-                                                options={"dist_exchange": L.DIST_EXCHANGE_RCCL,
-                                                         "dist_world1": 1 if world == 1 else 0})
+            xnotes = {}
             y_p2p = torch.empty(n, dtype=xd.dtype, device=dev)
             y_p2p_b = torch.empty(n, dtype=xd.dtype, device=dev)  # second window: chained ping-pong
+            y_full = torch.empty(n, dtype=xd.dtype, device=dev)
+            y_full_b = torch.empty(n, dtype=xd.dtype, device=dev)
+            ybuf = {"rccl": y_full, "p2p": y_p2p, "none": y_full}
+            ybuf_b = {"rccl": y_full_b, "p2p": y_p2p_b}
 
             def agree(ok):  # every rank takes the same branch (no half-set-up exchange)
                 f = torch.tensor([1 if ok else 0], dtype=torch.int32,
                                  device=dev if dist.get_backend() == "nccl" else "cpu")
                 dist.all_reduce(f, op=dist.ReduceOp.MIN)
                 return bool(f.item())
+            # the peer windows (y buffers registered on every rank) serve every K
+            p2p_ok = False
             if world > 1:
-                # the peer exchange is an optimisation: if its setup or a short
-                # probe fails on any rank (no IPC between the devices, a flag
-                # wait timing out), every rank drops it and the RCCL exchange
-                # is still measured.  The probe calls hold no collective, and
-                # every flag wait is bounded, so all ranks reach the agreement.
-                pp = None
                 try:
                     comm.p2p_setup_torch(y_p2p)  # collective-safe: raises on every rank or none
                     comm.p2p_setup_torch(y_p2p_b)
-                    pp = L.DistSpMVPlan(comm, n, n, args.chunks, cuts, lrp, lc, lv,
-                                        options={"dist_exchange": L.DIST_EXCHANGE_P2P})
+                    p2p_ok = True
                 except Exception as e:  # e.g. no IPC between the ranks' devices
                     xnotes["p2p"] = f"unavailable: {e}"
-                if agree(pp is not None):
-                    ok = True
-                    try:
-                        for _ in range(3):
-                            pp(xd, y_p2p, stream=stream)
-                        torch.cuda.synchronize()
-                        ok = comm.p2p_status() == 0
-                        if not ok:
-                            xnotes["p2p"] = "probe: a flag wait timed out"
-                    except Exception as e:
-                        ok, xnotes["p2p"] = False, f"probe failed: {e}"
-                    if agree(ok):
-                        dplans["p2p"] = pp
-                    else:
-                        xnotes.setdefault("p2p", "probe failed on another rank")
-                        torch.cuda.synchronize()
-                        pp.close()
-                elif pp is not None:
-                    xnotes.setdefault("p2p", "unavailable on another rank")
-                    pp.close()
-            dplans["none"] = L.DistSpMVPlan(comm, n, n, args.chunks, cuts, lrp, lc, lv,
-                                            options={"dist_exchange": L.DIST_EXCHANGE_NONE})
-            # the same local rows as one plan: the live kernel-only call timing below
-            plans = [L.SpMVPlan(lrp, lc, lv, n)]
-            local_nnz, local_rows = int(lc.shape[0]), int(lrp.shape[0] - 1)
-            y_full = torch.empty(n, dtype=xd.dtype, device=dev)
-            y_full_b = torch.empty(n, dtype=xd.dtype, device=dev)
-            ybuf = {"rccl": y_full, "p2p": y_p2p, "none": y_full}
-            ybuf_b = {"rccl": y_full_b, "p2p": y_p2p_b}
+                p2p_ok = agree(p2p_ok)
 
             def timed_chain(dp, ya, yb, steps, warmup):
                 """Iterative use (y of step n is x of step n+1, ping-pong
@@ -313,55 +279,134 @@ def main():
                     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
                     el = float(tt.item())
                 return el / steps
-            # per-exchange end-to-end (single and chained), exchange-only and SpMV-only steps
-            xtimes = {}
-            for kx in [k for k in ("rccl", "p2p") if k in dplans]:
-                dp, yb = dplans[kx], ybuf[kx]
-                e2e = timed(lambda dp=dp, yb=yb: dp(xd, yb, stream=stream), args.steps, args.warmup)
-                xo = timed(lambda dp=dp, yb=yb: dp.exchange(yb, stream=stream), args.steps, args.warmup)
-                ch = timed_chain(dp, yb, ybuf_b[kx], args.steps, args.warmup)
-                # chained calls must give what two plain calls give (every rank
-                # agrees); the plan's own y buffers (P2P plans need windows)
-                ybb = ybuf_b[kx]
-                dp(xd, yb, stream=stream)
-                dp(yb, ybb, stream=stream)
-                ref2 = ybb.clone()
-                ybb.copy_(xd)
-                dp.begin(ybb, yb, stream=stream)
-                dp.begin(yb, ybb, stream=stream)
-                dp.end(stream=stream)
-                same = torch.tensor([1 if torch.equal(ref2, ybb) else 0], dtype=torch.int32, device=dev)
-                if world > 1:
-                    dist.all_reduce(same, op=dist.ReduceOp.MIN)
-                xtimes[kx] = {"step_ms": e2e * 1e3, "exchange_only_ms": xo * 1e3,
+
+            def measure_k(K):
+                """Plans over K chunks per rank (one per exchange kind: the kind
+                is a plan option) and their times: end-to-end (plain and
+                chained), exchange-only, SpMV-only."""
+                cuts = L.interleaved_cuts(rp, world, K)
+                lrp, lc, lv = L.interleaved_local_csr(rp, col, val, cuts, world, K, rank)
+                dpl, notes = {}, {}
+                if has_rccl:
+                    dpl["rccl"] = L.DistSpMVPlan(comm, n, n, K, cuts, lrp, lc, lv,
+                                                 options={"dist_exchange": L.DIST_EXCHANGE_RCCL,
+                                                          "dist_world1": 1 if world == 1 else 0})
+                if p2p_ok:
+                    # the peer exchange is an optimisation: if a short probe fails
+                    # on any rank (a flag wait timing out), every rank drops it and
+                    # the RCCL exchange is still measured.  The probe calls hold no
+                    # collective, and every flag wait is bounded, so all ranks
+                    # reach the agreement.
+                    pp, ok = None, True
+                    try:
+                        pp = L.DistSpMVPlan(comm, n, n, K, cuts, lrp, lc, lv,
+                                            options={"dist_exchange": L.DIST_EXCHANGE_P2P})
+                        for _ in range(3):
+                            pp(xd, y_p2p, stream=stream)
+                        torch.cuda.synchronize()
+                        ok = comm.p2p_status() == 0
+                        if not ok:
+                            notes["p2p"] = "probe: a flag wait timed out"
+                    except Exception as e:
+                        ok, notes["p2p"] = False, f"probe failed: {e}"
+                    if agree(ok):
+                        dpl["p2p"] = pp
+                    else:
+                        notes.setdefault("p2p", "probe failed on another rank")
+                        torch.cuda.synchronize()
+                        if pp is not None:
+                            pp.close()
+                dpl["none"] = L.DistSpMVPlan(comm, n, n, K, cuts, lrp, lc, lv,
+                                             options={"dist_exchange": L.DIST_EXCHANGE_NONE})
+                xt = {}
+                for kx in [k for k in ("rccl", "p2p") if k in dpl]:
+                    dp, yb = dpl[kx], ybuf[kx]
+                    e2e = timed(lambda dp=dp, yb=yb: dp(xd, yb, stream=stream), args.steps, args.warmup)
+                    xo = timed(lambda dp=dp, yb=yb: dp.exchange(yb, stream=stream), args.steps, args.warmup)
+                    ch = timed_chain(dp, yb, ybuf_b[kx], args.steps, args.warmup)
+                    # chained calls must give what two plain calls give (every rank
+                    # agrees); the plan's own y buffers (P2P plans need windows)
+                    ybb = ybuf_b[kx]
+                    dp(xd, yb, stream=stream)
+                    dp(yb, ybb, stream=stream)
+                    ref2 = ybb.clone()
+                    ybb.copy_(xd)
+                    dp.begin(ybb, yb, stream=stream)
+                    dp.begin(yb, ybb, stream=stream)
+                    dp.end(stream=stream)
+                    same = torch.tensor([1 if torch.equal(ref2, ybb) else 0], dtype=torch.int32, device=dev)
+                    if world > 1:
+                        dist.all_reduce(same, op=dist.ReduceOp.MIN)
+                    xt[kx] = {"step_ms": e2e * 1e3, "exchange_only_ms": xo * 1e3,
                               "gflops": 2.0 * nnz / e2e / 1e9, "chained_step_ms": ch * 1e3,
                               "chained_gflops": 2.0 * nnz / ch / 1e9, "chained_same_y": bool(same.item())}
-            spmv_only = timed(lambda: dplans["none"](xd, y_full, stream=stream), args.steps, args.warmup)
-            # the peer exchange competes only with a y identical on every rank
-            # to the RCCL one (read on the device, through this GPU's caches)
-            if "p2p" in xtimes and "rccl" in xtimes:
-                dplans["rccl"](xd, y_full, stream=stream)
-                dplans["p2p"](xd, y_p2p, stream=stream)
-                same = torch.tensor([1 if torch.equal(y_full, y_p2p) else 0], dtype=torch.int32, device=dev)
-                dist.all_reduce(same, op=dist.ReduceOp.MIN)
-                xtimes["p2p"]["same_y_as_rccl"] = bool(same.item())
-                if not same.item():
-                    xtimes["p2p"]["excluded"] = "y differs from the RCCL exchange"
-            eligible = [k for k in xtimes if "excluded" not in xtimes[k]]
-            # the headline: the faster exchange, and for it the chained
-            # (iterative, cross-step overlapped) step when that is faster and
-            # gave the plain calls' y
-            chosen = min(eligible, key=lambda k: xtimes[k]["step_ms"]) if eligible else "none"
-            chained = chosen != "none" and xtimes[chosen]["chained_same_y"] and \
-                xtimes[chosen]["chained_step_ms"] < xtimes[chosen]["step_ms"]
+                so = timed(lambda: dpl["none"](xd, y_full, stream=stream), args.steps, args.warmup)
+                # the peer exchange competes only with a y identical on every rank
+                # to the RCCL one (read on the device, through this GPU's caches)
+                if "p2p" in xt and "rccl" in xt:
+                    dpl["rccl"](xd, y_full, stream=stream)
+                    dpl["p2p"](xd, y_p2p, stream=stream)
+                    same = torch.tensor([1 if torch.equal(y_full, y_p2p) else 0], dtype=torch.int32, device=dev)
+                    dist.all_reduce(same, op=dist.ReduceOp.MIN)
+                    xt["p2p"]["same_y_as_rccl"] = bool(same.item())
+                    if not same.item():
+                        xt["p2p"]["excluded"] = "y differs from the RCCL exchange"
+                # per exchange: the faster of plain and chained (chained only when
+                # it gave the plain calls' y)
+                best = None
+                for kx, r in xt.items():
+                    if "excluded" in r:
+                        continue
+                    for mode in ("plain", "chained"):
+                        if mode == "chained" and not r["chained_same_y"]:
+                            continue
+                        t = r["chained_step_ms" if mode == "chained" else "step_ms"]
+                        if best is None or t < best[2]:
+                            best = (kx, mode == "chained", t)
+                return {"K": K, "plans": dpl, "xtimes": xt, "notes": notes, "spmv_only_ms": so * 1e3,
+                        "best": best, "local": (lrp, lc, lv)}
+
+            # K (chunks per rank) is measured, not assumed: the exchange overlap
+            # it buys against the per-chunk launch cost depends on the link rate
+            # (tools/step_model.py, DESIGN.md §6.3); --chunks N fixes it
+            kcands = [args.chunks] if args.chunks > 0 else [1, 2, 4]
+
+            def strip(r):
+                return {k: v for k, v in r.items() if k not in ("plans", "local")}
+            top, others = None, []
+            for K in kcands:
+                r = measure_k(K)
+                torch.cuda.synchronize()
+                if top is None or (r["best"] is not None and (top["best"] is None or r["best"][2] < top["best"][2])):
+                    if top is not None:  # the new fastest K: the previous one's plans go
+                        for dp in top["plans"].values():
+                            dp.close()
+                        others.append(strip(top))
+                    top = r
+                else:
+                    for dp in r["plans"].values():
+                        dp.close()
+                    others.append(strip(r))
+            n_chunks = top["K"]
+            dplans, xtimes = top["plans"], top["xtimes"]
+            xnotes.update(top["notes"])
+            lrp, lc, lv = top["local"]
+            spmv_only = top["spmv_only_ms"] * 1e-3
+            chosen, chained = (top["best"][0], top["best"][1]) if top["best"] else ("none", False)
             dplan = dplans[chosen]
             y_out_buf = ybuf[chosen]
-            exchange_report = {"chosen": chosen, "chained": chained, "spmv_only_ms": spmv_only * 1e3, **xtimes,
-                               **xnotes,
+            # the same local rows as one plan: the live kernel-only call timing below
+            plans = [L.SpMVPlan(lrp, lc, lv, n)]
+            local_nnz, local_rows = int(lc.shape[0]), int(lrp.shape[0] - 1)
+            exchange_report = {"chosen": chosen, "chained": chained, "chunks_per_rank": n_chunks,
+                               "spmv_only_ms": spmv_only * 1e3, **xtimes, **xnotes,
+                               "other_chunk_counts": [{"K": r["K"], "spmv_only_ms": r["spmv_only_ms"],
+                                                       "best": r["best"], **r["xtimes"]} for r in others],
                                "note": "step = local SpMV + y exchange (lhpc_dist_spmv); chained = iterative use, "
                                        "y of step n is x of step n+1, lhpc_dist_spmv_begin (next step's gather by "
                                        "column part as each exchange lands); exchange_only = lhpc_dist_exchange "
-                                       "alone; spmv_only = exchange NONE; max over ranks"}
+                                       "alone; spmv_only = exchange NONE; max over ranks; chunks_per_rank = the "
+                                       "fastest of the measured K (other_chunk_counts)"}
 
             class _Native:
                 def step(self, xv):
@@ -385,9 +430,10 @@ def main():
             # torch.distributed form (gloo rehearsal, LHPC_DIST_TORCH=1):
             # interleaved nnz-balanced row blocks, K chunks per rank; chunk
             # k's all-gather overlaps the SpMV of chunk k+1 (libhpc_amd/dist.py)
-            ib = InterleavedBlocks(n, world, args.chunks, row_ptr=rp)
+            n_chunks = args.chunks if args.chunks > 0 else 4
+            ib = InterleavedBlocks(n, world, n_chunks, row_ptr=rp)
             plans, local_nnz, fns = [], 0, None
-            if args.chunks > 1:
+            if n_chunks > 1:
                 # one row-range plan over the rank's K chunks: x is staged once
                 # (one XTILE tile gather), then chunk k is reduced and its
                 # all-gather starts; falls back to a plan per chunk when the
@@ -404,14 +450,14 @@ def main():
                         pl.stage(xv, stream=stream)
                         pl.range(0, yv, stream=stream)
                     fns = [first] + [lambda xv, yv, k=k, pl=sp: pl.range(k, yv, stream=stream)
-                                     for k in range(1, args.chunks)]
+                                     for k in range(1, n_chunks)]
             if fns is None:
-                for k in range(args.chunks):
+                for k in range(n_chunks):
                     lrp, lc, lv = ib.local_csr(rp, col, val, rank, k)
                     plans.append(L.SpMVPlan(lrp, lc, lv, n))
                     local_nnz += int(lc.shape[0])
                 fns = [lambda xv, yv, pl=pl: pl(xv, yv, stream=stream) for pl in plans]
-            local_rows = ib.B * args.chunks
+            local_rows = ib.B * n_chunks
             dsp = DistSpMVOverlap(ib, fns, like=xd)
 
             def step():
@@ -502,14 +548,14 @@ def main():
                     + (f" (run in {dtag})" if dtag else ""),
                     "n_rows": n, "n_cols": n, "nnz": nnz, "kernel": kname, "slices": info["slices"],
                     "parallelism": f"row-block x{world}" + (
-                        f" (interleaved nnz-balanced, {args.chunks} chunks/rank) + "
+                        f" (interleaved nnz-balanced, {n_chunks} chunks/rank) + "
                         + ("direct xGMI peer stores of y chunks (lhpc_dist_p2p windows)" if chosen == "p2p" else
                            "native RCCL exchange of y chunks (in-place all-gather for equal blocks, else "
                            "broadcasts)" if chosen == "rccl" else "no exchange")
                         + (" (lhpc_dist_spmv_begin, chained: y of step n is x of step n+1, next gather by column "
                            "part under the exchange)" if chained else " (lhpc_dist_spmv)")
                         + " overlapped; faster of the measured exchanges" if native_dist else
-                        f" (interleaved nnz-balanced, {args.chunks} chunks/rank) + torch.distributed all_gather(y) "
+                        f" (interleaved nnz-balanced, {n_chunks} chunks/rank) + torch.distributed all_gather(y) "
                         "overlapped" if world > 1 else "")},
             achieved_GBps=alg_bytes / per_step / 1e9,
             roofline={"bound": "hbm", "kernel": kernels, "achieved": achieved, "peak": HBM_PEAK_GBPS,
@@ -833,7 +879,7 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
         # the native distributed CG (lhpc_dist_cg_solve): interleaved
         # nnz-balanced blocks, K chunks per rank, p exchanged over RCCL with
         # the next q = A·p's gather chained per chunk, dots as block partials
-        K = min(args.chunks, 8)
+        K = min(args.chunks if args.chunks > 0 else 4, 8)
         comm = L.DistComm.from_torch(dev.index)
         cuts = L.interleaved_cuts(rp, world, K)
         dplan = L.DistSpMVPlan(comm, n, n, K, cuts, *L.interleaved_local_csr(rp, col, val, cuts, world, K, rank))
