@@ -202,7 +202,13 @@ typedef struct lhpc_options {
   int32_t dist_reduce_streams;  /* lhpc_dist_spmv: chunk reduces alternate over this many
                                    streams (1 or 2; 0: 2), so chunk k+1 fills the CUs
                                    chunk k's tail leaves idle                        */
-  int32_t reserved[2];
+  /* XTILE column blocks: when x spans many tiles (n_cols past ≈ 30M fp32 /
+   * 15M fp64) each reduce chunk meets every tile in a few nonzeros, so the
+   * plan cuts the columns into B blocks, one XTILE plan each over x's column
+   * range, run in turn, every block after the first adding into y.  0: auto,
+   * 1: never, B ≥ 2: B blocks (tests: the path at small sizes)               */
+  int32_t xtile_col_blocks;
+  int32_t reserved;
 } lhpc_options;
 void lhpc_options_init(lhpc_options *opts);
 

@@ -31,6 +31,34 @@ int validate_csr(const void *rp, int bits, const int32_t *col, int64_t n_rows, i
   return bad ? LHPC_ERR_BAD_CSR : LHPC_OK;
 }
 
+void csr_column_block(const void *rp, int bits, const int32_t *col, const void *val, size_t tsz, int64_t r0,
+                      int64_t r1, int64_t c0, int64_t c1, std::vector<int64_t> &orp, std::vector<int32_t> &ocol,
+                      std::vector<unsigned char> &oval) {
+  const int64_t nr = r1 - r0;
+  orp.assign(static_cast<size_t>(nr) + 1, 0);
+#pragma omp parallel for schedule(static)
+  for (int64_t r = 0; r < nr; ++r) {
+    int64_t c = 0;
+    for (int64_t k = rp_at(rp, bits, r0 + r); k < rp_at(rp, bits, r0 + r + 1); ++k) c += col[k] >= c0 && col[k] < c1;
+    orp[static_cast<size_t>(r) + 1] = c;
+  }
+  for (int64_t r = 0; r < nr; ++r) orp[static_cast<size_t>(r) + 1] += orp[static_cast<size_t>(r)];
+  const int64_t m = orp[static_cast<size_t>(nr)];
+  ocol.resize(static_cast<size_t>(m));
+  oval.resize(static_cast<size_t>(m) * tsz);
+  const auto *vb = static_cast<const unsigned char *>(val);
+#pragma omp parallel for schedule(static)
+  for (int64_t r = 0; r < nr; ++r) {
+    int64_t o = orp[static_cast<size_t>(r)];
+    for (int64_t k = rp_at(rp, bits, r0 + r); k < rp_at(rp, bits, r0 + r + 1); ++k)
+      if (col[k] >= c0 && col[k] < c1) {
+        ocol[static_cast<size_t>(o)] = static_cast<int32_t>(col[k] - c0);
+        std::memcpy(oval.data() + static_cast<size_t>(o) * tsz, vb + static_cast<size_t>(k) * tsz, tsz);
+        ++o;
+      }
+  }
+}
+
 int build_xslice(const void *rp, int bits, const int32_t *col, const void *val, size_t tsz,
                  int64_t n_rows, int64_t n_cols, int S, XsliceHost &o) {
   if (S < 1 || S > 256) return LHPC_ERR_INVALID_ARG;

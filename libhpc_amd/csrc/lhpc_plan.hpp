@@ -16,6 +16,14 @@ namespace lhpc {
 int validate_csr(const void *row_ptr, int rp_bits, const int32_t *col, int64_t n_rows, int64_t n_cols,
                  int64_t nnz);
 
+// XTILE column blocks: rows [r0, r1) of A restricted to columns [c0, c1),
+// columns rebased to c0, each row's nonzeros in the caller's order.  out_rp
+// gets r1 − r0 + 1 offsets; out_col / out_val are resized to the block's
+// nonzeros (tsz bytes per value).  OpenMP: count per row, scan, fill.
+void csr_column_block(const void *row_ptr, int rp_bits, const int32_t *col, const void *val, size_t tsz,
+                      int64_t r0, int64_t r1, int64_t c0, int64_t c1, std::vector<int64_t> &out_rp,
+                      std::vector<int32_t> &out_col, std::vector<unsigned char> &out_val);
+
 // XSLICE: A split by column into S slices of `width` columns; inside a
 // slice, rows are grouped in 64-row chunks (one wave per chunk), and a
 // chunk's in-slice nonzeros are stored in CSR order (row by row; the wave

@@ -85,7 +85,8 @@ int launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
   if (!p->parts.empty()) {
     const size_t tsz = p->dtype == LHPC_F32 ? 4 : 8;
     for (size_t i = 0; i < p->parts.size(); ++i)
-      LHPC_TRY(xtile_launch(p->parts[i], x, static_cast<unsigned char *>(y) + p->part_row[i] * tsz, s));
+      LHPC_TRY(xtile_launch(p->parts[i], static_cast<const unsigned char *>(x) + p->part_col[i] * tsz,
+                            static_cast<unsigned char *>(y) + p->part_row[i] * tsz, s));
     return LHPC_OK;
   }
   if (p->kernel == LHPC_KERNEL_XTILE) return xtile_launch(p, x, y, s);
@@ -93,17 +94,38 @@ int launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
   return csr_launch(p, x, y, s);
 }
 
+// XTILE column blocks (lhpc_options.xtile_col_blocks).  A reduce chunk holds
+// M nonzeros and meets every one of the S tiles, so its segment per tile is
+// M/S nonzeros: 32 for C2 (S = 256), 4 at n = 80M (S = 2048), and the
+// reduce's cost per nonzero grows with S (DESIGN.md §4 "large n": 632 GFLOP/s
+// at S = 256, 533 at 768, 408 at 1024, 244 at 2048).  Cutting the columns into
+// B blocks gives each block's plan S/B tiles; the blocks run in turn on x's
+// column ranges, every block after the first adding into y.  A chunk also
+// holds ≤ M/8 rows, so once a block's rows average < 8 nonzeros the chunks
+// shrink with the blocks: B stays ≤ 1.2·mean/8 (2 at 15 per row).
+constexpr int64_t kColBlockTiles = 768;
+int xtile_col_blocks_for(int64_t n_rows, int64_t n_cols, int64_t nnz, size_t tsz, const lhpc_options &o) {
+  const int64_t most = std::max<int64_t>(1, n_cols / 64);  // ≥ 64 columns per block
+  if (o.xtile_col_blocks > 0) return static_cast<int>(std::min<int64_t>(o.xtile_col_blocks, most));
+  const int64_t W = tsz == 4 ? 40960 : 20480, S = (n_cols + W - 1) / W;
+  if (S <= kColBlockTiles || n_rows <= 0) return 1;
+  const double mean = static_cast<double>(nnz) / static_cast<double>(n_rows);
+  const int64_t bmax = std::max<int64_t>(1, static_cast<int64_t>(mean * 1.2 / 8.0));
+  return static_cast<int>(std::min({(S + kColBlockTiles - 1) / kColBlockTiles, bmax, most}));
+}
+
 // XTILE row parts: the tile stream of one plan is addressed with int32
 // offsets (nnz + 8 padding entries per tile < 2^31, lhpc_plan.cpp
 // build_xtile).  A larger matrix (n ≳ 143M rows at 15 nonzeros per row) is
 // cut into nnz-balanced row parts of ≤ cap nonzeros, each an ordinary XTILE
 // plan over its rows (row_ptr rebased, the caller's col/val at the part's
-// offset) run in turn on the same x, instead of dropping to XSLICE.
+// offset) run in turn on the same x, instead of dropping to XSLICE.  With
+// B > 1 column blocks every row part is further cut by column (above).
 // LHPC_ERR_UNSUPPORTED when some single row exceeds the cap.
 int build_parts(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz,
-                int64_t cap) {
+                int64_t cap, int B) {
   const int64_t n_rows = p->n_rows;
-  int64_t n_parts = (p->nnz + cap - 1) / cap;
+  int64_t n_parts = std::max<int64_t>(1, (p->nnz + cap - 1) / cap);
   std::vector<int64_t> cuts;
   for (;; ++n_parts) {  // nnz-balanced cuts; one more part until every part fits
     cuts.assign(static_cast<size_t>(n_parts) + 1, 0);
@@ -117,26 +139,49 @@ int build_parts(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const 
     if (fit) break;
     if (n_parts > n_rows) return LHPC_ERR_UNSUPPORTED;
   }
-  std::vector<int64_t> lrp;
-  for (int64_t i = 0; i < n_parts; ++i) {
-    const int64_t r0 = cuts[i], r1 = cuts[i + 1];
-    if (r1 == r0) continue;
+  // column block bounds, 64-column aligned (x + bound stays 256-B aligned)
+  std::vector<int64_t> cb(static_cast<size_t>(B) + 1, p->n_cols);
+  for (int b = 0; b < B; ++b) cb[b] = p->n_cols * b / B / 64 * 64;
+  auto add = [&](int64_t r0, int64_t r1, int64_t c0, int64_t c1, RowPtrView lrp, const int32_t *lc, const void *lv,
+                 int64_t lnnz, int acc) -> int {
     auto *q = new (std::nothrow) lhpc_spmv_plan();
     if (!q) return LHPC_ERR_ALLOC;
     p->parts.push_back(q);
     p->part_row.push_back(r0);
+    p->part_col.push_back(c0);
     q->opt = p->opt;
     q->dtype = p->dtype;
     q->device = p->device;
     q->n_rows = r1 - r0;
-    q->n_cols = p->n_cols;
-    const int64_t e0 = rp[r0];
-    q->nnz = rp[r1] - e0;
-    lrp.resize(static_cast<size_t>(r1 - r0 + 1));
-    for (int64_t r = r0; r <= r1; ++r) lrp[static_cast<size_t>(r - r0)] = rp[r] - e0;
-    LHPC_TRY(xtile_build(q, RowPtrView{lrp.data(), 64}, col_idx + e0,
-                         static_cast<const unsigned char *>(val) + e0 * static_cast<int64_t>(tsz), tsz));
+    q->n_cols = c1 - c0;
+    q->nnz = lnnz;
+    q->xt_acc = acc;
+    LHPC_TRY(xtile_build(q, lrp, lc, lv, tsz));
     p->bytes += q->bytes;
+    return LHPC_OK;
+  };
+  std::vector<int64_t> lrp;
+  std::vector<int32_t> lcol;
+  std::vector<unsigned char> lval;
+  for (int64_t i = 0; i < n_parts; ++i) {
+    const int64_t r0 = cuts[i], r1 = cuts[i + 1];
+    if (r1 == r0) continue;
+    const int64_t e0 = rp[r0];
+    if (B == 1 || rp[r1] == e0) {
+      lrp.resize(static_cast<size_t>(r1 - r0 + 1));
+      for (int64_t r = r0; r <= r1; ++r) lrp[static_cast<size_t>(r - r0)] = rp[r] - e0;
+      LHPC_TRY(add(r0, r1, 0, p->n_cols, RowPtrView{lrp.data(), 64}, col_idx + e0,
+                   static_cast<const unsigned char *>(val) + e0 * static_cast<int64_t>(tsz), rp[r1] - e0, 0));
+      continue;
+    }
+    bool first = true;  // the first non-empty block stores every row of the part
+    for (int b = 0; b < B; ++b) {
+      csr_column_block(rp.p, rp.bits, col_idx, val, tsz, r0, r1, cb[b], cb[b + 1], lrp, lcol, lval);
+      if (lcol.empty()) continue;  // adds nothing
+      LHPC_TRY(add(r0, r1, cb[b], cb[b + 1], RowPtrView{lrp.data(), 64}, lcol.data(), lval.data(),
+                   static_cast<int64_t>(lcol.size()), first ? 0 : 1));
+      first = false;
+    }
   }
   p->part_row.push_back(n_rows);
   p->kernel = LHPC_KERNEL_XTILE;
@@ -259,12 +304,14 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
   if (want_xtile && n_rows > 0) {
     // row parts when the tile stream outgrows its int32 offsets (or a lower
     // cap is asked for); user row splits keep a single plan
+    // and column blocks when x spans many tiles (xtile_col_blocks_for)
     const int64_t tiles = (n_cols + (tsz == 4 ? 40960 : 20480) - 1) / (tsz == 4 ? 40960 : 20480);
     int64_t cap = INT32_MAX - 8 * (tiles + 256) - (int64_t{1} << 16);
     if (o.xtile_part_nnz > 0) cap = std::min<int64_t>(cap, o.xtile_part_nnz);
+    const int B = n_splits == 0 ? xtile_col_blocks_for(n_rows, n_cols, nnz, tsz, o) : 1;
     int st;
-    if (nnz > cap && n_splits == 0 && tiles <= 4096)
-      st = build_parts(p, rp, col_idx, val, tsz, cap);
+    if ((nnz > cap || B > 1) && n_splits == 0 && (tiles + B - 1) / B <= 4096)
+      st = build_parts(p, rp, col_idx, val, tsz, cap, B);
     else
       st = xtile_build(p, rp, col_idx, val, tsz);
     if (st == LHPC_OK) {
@@ -278,6 +325,7 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
     for (auto *q : p->parts) lhpc_spmv_plan_destroy(q);
     p->parts.clear();
     p->part_row.clear();
+    p->part_col.clear();
     p->bytes = 0;
     // layout does not fit its index types: XSLICE / CSR kernels below
   }
@@ -371,8 +419,8 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
 // to the host, which makes every layout decision.  The XTILE layout — the
 // default for gathers without locality — is then built on the GPU from the
 // device arrays (xtile_build_device: byte-identical to the host build); any
-// other family, row parts, aligned segments or several devices copy A to the
-// host and take the host path.
+// other family, row parts, column blocks, aligned segments or several
+// devices copy A to the host and take the host path.
 int plan_create_device_input(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
                              const void *row_ptr, int row_ptr_bits, const int32_t *col_idx, const void *val,
                              const int *device_ids, int n_devices, unsigned flags, int n_splits,
@@ -419,7 +467,8 @@ int plan_create_device_input(lhpc_spmv_plan **out, int dtype, int64_t n_rows, in
   const int64_t tiles = (n_cols + (tsz == 4 ? 40960 : 20480) - 1) / (tsz == 4 ? 40960 : 20480);
   int64_t cap = INT32_MAX - 8 * (tiles + 256) - (int64_t{1} << 16);
   if (o.xtile_part_nnz > 0) cap = std::min<int64_t>(cap, o.xtile_part_nnz);
-  const bool single = n_devices <= 1 && !o.multi_force && nnz <= cap && tiles <= 4096 && n_rows > 0;
+  const bool single = n_devices <= 1 && !o.multi_force && nnz <= cap && tiles <= 4096 && n_rows > 0 &&
+                      (n_splits > 0 || xtile_col_blocks_for(n_rows, n_cols, nnz, tsz, o) == 1);
   bool want_xtile = single && (flags & LHPC_PLAN_FORCE_XTILE);
   if (single && auto_ok && !o.spmv_no_xtile && x_bytes > 8.0e6)
     want_xtile = gather_lines_per_nnz(

@@ -72,6 +72,12 @@ struct lhpc_spmv_plan {
   // the same x; this plan then holds no arrays of its own
   std::vector<lhpc_spmv_plan *> parts;
   std::vector<int64_t> part_row;
+  // XTILE column blocks (lhpc_options.xtile_col_blocks): parts may also cover a
+  // column range [part_col[i], …) of x; a part whose xt_acc is set adds its
+  // sums into y instead of storing them (every block of a row part after the
+  // first one, run after it on the same stream)
+  std::vector<int64_t> part_col;
+  int xt_acc = 0;
   // single-process multi-device plan (n_devices > 1; lhpc_multi.hip)
   struct lhpc_multi *multi = nullptr;
 };

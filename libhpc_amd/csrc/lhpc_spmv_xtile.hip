@@ -218,7 +218,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     int64_t c0, int64_t C,
     int64_t Cx, int total, const T *__restrict__ xg, const uint16_t *__restrict__ perm,
     const T *__restrict__ val, const int32_t *__restrict__ rp, T *__restrict__ y,
-    double *__restrict__ carry) {
+    double *__restrict__ carry, int y_add) {
   constexpr int RUN = xt_run<T>(), M = XtRed<T, BLK>::M, RMAX = XtRed<T, BLK>::Rmax;
   constexpr int RPT = (RMAX + 1 + BLK - 1) / BLK;  // row_ptr loads per thread
   constexpr int NB = M / BLK;                      // 64-position batches per wave (= RUN)
@@ -610,10 +610,15 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   LHPC_XT_STAMP(7, 0)
   // coalesced y store of the owned rows from their last positions (a row
   // continuing past the chunk is stored by k_xtile_fixup, later on the stream)
+  // (y_add: a column block after the first adds its sums; empty rows keep y)
   for (int j = tid; j < R; j += BLK) {
     const int a0 = rpl[j], a1 = rpl[j + 1];
-    if (a1 == a0) y[r0 + j] = T(0);
-    else if (a1 <= m) y[r0 + j] = xs[xt_slot<T>(a1 - 1)];
+    if (a1 == a0) {
+      if (!y_add) y[r0 + j] = T(0);
+    } else if (a1 <= m) {
+      const T v = xs[xt_slot<T>(a1 - 1)];
+      y[r0 + j] = y_add ? static_cast<T>(static_cast<double>(y[r0 + j]) + static_cast<double>(v)) : v;
+    }
   }
   LHPC_XT_STAMP(8, 0)
   LHPC_XT_STAMP(9, 1)
@@ -623,7 +628,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
 template <typename T>
 __global__ __launch_bounds__(kXtFixBlock) void k_xtile_fixup(
     const int32_t *__restrict__ cont, int64_t n_cont, const int32_t *__restrict__ cr, int64_t C,
-    const double *__restrict__ carry, T *__restrict__ y) {  // C: end of the chunk range (rows never cross it)
+    const double *__restrict__ carry, T *__restrict__ y, int acc) {  // C: end of the chunk range (rows never cross it)
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kXtFixBlock + threadIdx.x;
   if (i >= n_cont) return;
   const int64_t c = cont[i];
@@ -632,7 +637,8 @@ __global__ __launch_bounds__(kXtFixBlock) void k_xtile_fixup(
     s += carry[2 * d];
     if (cr[d + 1] > cr[d]) break;
   }
-  y[cr[c + 1] - 1] = static_cast<T>(s);
+  T *yr = y + (cr[c + 1] - 1);
+  *yr = acc ? static_cast<T>(static_cast<double>(*yr) + s) : static_cast<T>(s);
 }
 
 // ------------------------------------------------------------ launchers
@@ -719,13 +725,15 @@ int launch_reduce(const lhpc_spmv_plan *p, int64_t c0, int64_t c1, int64_t n0, i
     const T *xg = static_cast<const T *>(p->d_xg), *val = static_cast<const T *>(p->d_val);
     const uint16_t *perm = p->d_perm;
     double *carry = p->d_carry;
-    void *args[] = {&cd, &so, &sh, &S, &c0, &c1, const_cast<int64_t *>(&Cx), &total, &xg, &perm, &val, &rp, &y, &carry};
+    int acc = p->xt_acc;
+    void *args[] = {&cd, &so, &sh, &S, &c0, &c1, const_cast<int64_t *>(&Cx), &total, &xg, &perm, &val, &rp, &y, &carry,
+                    &acc};
     LHPC_HIP_TRY(hipLaunchKernel(fn, rg, rb, args, p->xt_lds, s));
     LHPC_TRY(check_launch(s));
   }
   if (n1 > n0) {
     hipLaunchKernelGGL((k_xtile_fixup<T>), dim3(static_cast<unsigned>((n1 - n0 + kXtFixBlock - 1) / kXtFixBlock)),
-                       dim3(kXtFixBlock), 0, s, p->d_cont + n0, n1 - n0, p->d_cr, c1, p->d_carry, y);
+                       dim3(kXtFixBlock), 0, s, p->d_cont + n0, n1 - n0, p->d_cr, c1, p->d_carry, y, p->xt_acc);
     LHPC_TRY(check_launch(s));
   }
   return LHPC_OK;

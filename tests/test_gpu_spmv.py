@@ -153,22 +153,25 @@ def test_full_size_c2_c3(lhpc, gpu, dtype):
 
 
 @pytest.mark.slow
-def test_xtile_large_n_80m(lhpc, gpu):
+@pytest.mark.parametrize("blocks", [0, 1])
+def test_xtile_large_n_80m(lhpc, gpu, blocks):
     """XTILE beyond C2: n = 80M rows and columns, 15 uniform nonzeros per row
-    (nnz = 1.2e9, 1954 x tiles, 146K chunks; fp32).  The dense segment table
-    of starts needed 2.9e8 entries and the plan fell to XSLICE; the two-level
-    table (lhpc_plan.hpp xtile_segment_table) keeps it XTILE.  Dyadic values:
-    10^5 sampled rows bit-exact against fp64 numpy (exact here), and run to
-    run determinism on the whole y."""
+    (nnz = 1.2e9, fp32).  blocks = 1: one plan over 2048 x tiles (146K chunks;
+    the dense segment table of starts needed 2.9e8 entries and the plan fell to
+    XSLICE until the two-level table, lhpc_plan.hpp xtile_segment_table);
+    blocks = 0 (auto): two column blocks of 1024 tiles each, the second adding
+    into y.  Dyadic values: 10^5 sampled rows bit-exact against fp64 numpy
+    (exact here), and run to run determinism on the whole y."""
     import torch
     n = 80_000_000
     rp, col, val = lhpc.gen_uniform_csr(n, n, 15, dtype=lhpc.F32, dist=1, seed=0x8000)
     x = lhpc.gen_values(lhpc.F32, 1, n, 0x8001)
-    with lhpc.SpMVPlan(rp, col, val, n) as plan:
+    with lhpc.SpMVPlan(rp, col, val, n, options={"xtile_col_blocks": blocks}) as plan:
         info = plan.info()
-        # tiles of ≤ 40960 columns (narrowed to a whole multiple of the CUs: 2048 x 39063)
+        # tiles of ≤ 40960 columns (narrowed to a whole multiple of the CUs: 2048 × 39063)
         assert info["kernel"] == lhpc.KERNEL_XTILE and info["slice_width"] <= 40960
-        assert info["slices"] == -(-n // info["slice_width"]) and info["slices"] >= -(-n // 40960)
+        cols = n if blocks == 1 else n // 2  # slices: the (first) block's tiles
+        assert info["slices"] == -(-cols // info["slice_width"]) and info["slices"] >= -(-cols // 40960)
         xd = torch.from_numpy(x).to(gpu)
         y1 = plan(xd).clone()
         y2 = plan(xd)
@@ -538,6 +541,79 @@ def test_xtile_row_parts(lhpc, gpu, dtype, cap, xt_layout):
     x = (np.random.default_rng(7).integers(-8, 9, size=200_000) / 8.0).astype(dtype)
     yh, _ = _run(lhpc, gpu, rp, col, val, x, 200_000, FAMILIES["xtile"], device_buffers=False, options=opts)
     assert np.array_equal(yh, S.spmv_oracle(rp, col, val, x)[1])
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("blocks", [2, 3, 5])
+def test_xtile_col_blocks(lhpc, gpu, dtype, blocks, xt_layout):
+    """XTILE column blocks (lhpc_options.xtile_col_blocks): the plan cuts the
+    columns into B blocks, one XTILE plan each over x's column range, run in
+    turn, every block after the first adding into y — the path a matrix takes
+    when x spans many tiles (lhpc_spmv.hip xtile_col_blocks_for), here forced
+    at small size.  Long rows cut by chunk ends (the fix-up adds under the
+    accumulation), empty rows, short rows with no entry in some blocks.
+    Dyadic: bit-exact; random: within the bound; with row parts on top; the
+    host-buffer path; a y full of NaN beforehand does not leak through."""
+    import torch
+    lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 3000 + [0, 0] + [30000] + [7] * 4000
+    opts = dict(xt_layout, xtile_col_blocks=blocks)
+    info = _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xAB00, opts=opts)
+    single = _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xAB00, opts=dict(xt_layout, xtile_col_blocks=1))
+    assert info["launches"] > single["launches"]
+    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xAB01, dyadic=False, opts=opts)
+    _check_xtile(lhpc, gpu, lengths, 200_000, dtype, 0xAB02, opts=dict(opts, xtile_part_nnz=40_000))
+    rp, col, val = _csr_from_lengths(lengths, 200_000, 0xAB03, True)
+    val = val.astype(dtype)
+    x = (np.random.default_rng(9).integers(-8, 9, size=200_000) / 8.0).astype(dtype)
+    yr = S.spmv_oracle(rp, col, val, x)[1]
+    yh, _ = _run(lhpc, gpu, rp, col, val, x, 200_000, FAMILIES["xtile"], device_buffers=False, options=opts)
+    assert np.array_equal(yh, yr)
+    with lhpc.SpMVPlan(rp, col, val, 200_000, flags=FAMILIES["xtile"], options=opts) as plan:
+        y = torch.full((len(lengths),), float("nan"), dtype=torch.from_numpy(x).dtype, device=gpu)
+        plan(torch.from_numpy(x).to(gpu), y)
+        assert np.array_equal(y.cpu().numpy(), yr)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("lo,hi", [(0, 60_000), (120_000, 200_000), (0, 200_000)])
+def test_xtile_col_blocks_empty_blocks(lhpc, gpu, dtype, lo, hi):
+    """Column blocks with no nonzeros are left out, and the first non-empty
+    block stores every row (columns only in the first 30% / the last 40% of
+    x, four blocks of 50000 columns; the full range as the control)."""
+    rng = np.random.default_rng(0xAC00 + lo)
+    lengths = rng.integers(0, 40, size=5000)
+    rp = np.zeros(lengths.size + 1, dtype=np.int32)
+    np.cumsum(lengths, out=rp[1:])
+    col = np.concatenate([np.sort(rng.choice(np.arange(lo, hi), size=int(n), replace=False)) for n in lengths])
+    col = col.astype(np.int32)
+    val = (rng.integers(-8, 9, size=col.size) / 8.0).astype(dtype)
+    x = (rng.integers(-8, 9, size=200_000) / 8.0).astype(dtype)
+    y, info = _run(lhpc, gpu, rp, col, val, x, 200_000, FAMILIES["xtile"], options={"xtile_col_blocks": 4})
+    assert info["kernel"] == lhpc.KERNEL_XTILE
+    assert np.array_equal(y, S.spmv_oracle(rp, col, val, x)[1])
+
+
+@pytest.mark.parametrize("dtype,blocks", [(np.float32, 2), (np.float64, 3)])
+def test_xtile_col_blocks_auto(lhpc, gpu, dtype, blocks):
+    """The automatic choice: x of 40M columns (977 fp32 / 1954 fp64 tiles,
+    past the 768 one block keeps) with 100 nonzeros per row gives 2 (fp32) /
+    3 (fp64) column blocks — as many launches as that many single plans, and
+    the same y as one block, bit for bit on dyadic values."""
+    import torch
+    n_cols, n_rows = 40_000_000, 300
+    rng = np.random.default_rng(0xAD00)
+    rp = np.arange(0, 100 * (n_rows + 1), 100, dtype=np.int32)
+    col = np.concatenate([np.sort(rng.choice(n_cols, size=100, replace=False)) for _ in range(n_rows)]).astype(np.int32)
+    val = (rng.integers(-8, 9, size=col.size) / 8.0).astype(dtype)
+    x = torch.from_numpy((rng.integers(-8, 9, size=n_cols) / 8.0).astype(dtype)).to(gpu)
+    with lhpc.SpMVPlan(rp, col, val, n_cols) as auto, \
+            lhpc.SpMVPlan(rp, col, val, n_cols, options={"xtile_col_blocks": 1}) as one:
+        ia, i1 = auto.info(), one.info()
+        assert ia["kernel"] == i1["kernel"] == lhpc.KERNEL_XTILE
+        assert ia["launches"] == blocks * i1["launches"]
+        ya, y1 = auto(x).cpu().numpy(), one(x).cpu().numpy()
+    assert np.array_equal(ya, y1)
+    assert np.array_equal(ya, S.spmv_oracle(rp, col, val, x.cpu().numpy())[1])
 
 
 def test_xtile_row_parts_row_past_cap(lhpc, gpu):
