@@ -101,8 +101,13 @@ int launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
 // at S = 256, 533 at 768, 408 at 1024, 244 at 2048).  Cutting the columns into
 // B blocks gives each block's plan S/B tiles; the blocks run in turn on x's
 // column ranges, every block after the first adding into y.  A chunk also
-// holds ≤ M/8 rows, so once a block's rows average < 8 nonzeros the chunks
-// shrink with the blocks: B stays ≤ 1.2·mean/8 (2 at 15 per row).
+// holds ≤ M/8 rows, so as a block's rows get shorter its chunks shrink with
+// the blocks.  Same box, fp32 15 per row, forced B (profiles/r04/col_blocks):
+// n = 10M (256 tiles) B = 1 / 2: 601 / 534 GFLOP/s; 40M (1024) B = 2 / 3 /
+// 4: 498 / 446 / 426; 80M (2048) B = 2 / 3 / 4 / 6: 378 / 417 / 365 / 314;
+// 150M (3840, two row parts) B = 2 / 3 / 4: 316 / 371 / 342.  fp64 10M (489)
+// B = 1 / 2: 318 / 304; 40M (1954) B = 2 / 3 / 4 / 6: 264 / 261 / 230 / 180.
+// Hence B = ⌈S / 768⌉, at most mean row length / 5.
 constexpr int64_t kColBlockTiles = 768;
 int xtile_col_blocks_for(int64_t n_rows, int64_t n_cols, int64_t nnz, size_t tsz, const lhpc_options &o) {
   const int64_t most = std::max<int64_t>(1, n_cols / 64);  // ≥ 64 columns per block
@@ -110,7 +115,7 @@ int xtile_col_blocks_for(int64_t n_rows, int64_t n_cols, int64_t nnz, size_t tsz
   const int64_t W = tsz == 4 ? 40960 : 20480, S = (n_cols + W - 1) / W;
   if (S <= kColBlockTiles || n_rows <= 0) return 1;
   const double mean = static_cast<double>(nnz) / static_cast<double>(n_rows);
-  const int64_t bmax = std::max<int64_t>(1, static_cast<int64_t>(mean * 1.2 / 8.0));
+  const int64_t bmax = std::max<int64_t>(1, static_cast<int64_t>(mean / 5.0));
   return static_cast<int>(std::min({(S + kColBlockTiles - 1) / kColBlockTiles, bmax, most}));
 }
 
