@@ -260,7 +260,8 @@ int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *plan,
 /* Test support: 64-bit FNV-1a digests (size folded in) of an XTILE plan's
  * device layout arrays — row_ptr, col16, perm/iperm, val runs, chunk
  * descriptors, cr, segment table lo/len and hi, gather pieces, cont — into
- * out[0..9] (cap ≥ 10), *n_out = 10.  LHPC_ERR_UNSUPPORTED for other plans.
+ * out[0..9] (cap ≥ 10), *n_out = 10; a plan of row parts / column blocks
+ * folds its parts' digests in order.  LHPC_ERR_UNSUPPORTED for other plans.
  * A plan built from LHPC_PLAN_DEVICE_INPUT has the same digests as the host
  * build of the same matrix and options.                                     */
 int lhpc_spmv_plan_layout_digest(const lhpc_spmv_plan *plan, uint64_t *out, int cap, int *n_out);

@@ -75,6 +75,80 @@ __global__ void k_validate_device_csr(const void *rp, int bits, const int32_t *c
   if (bad) atomicOr(flag, bad);
 }
 
+// XTILE column blocks from device-resident CSR (build_parts with d_rp):
+// rows [r0, r0 + nr) restricted to columns [c0, c1), rebased — the device
+// twin of lhpc_plan.cpp csr_column_block (count per row, host scan, scatter)
+__device__ __forceinline__ int64_t rp_dev(const void *rp, int bits, int64_t i) {
+  return bits == 64 ? static_cast<const int64_t *>(rp)[i] : static_cast<const int32_t *>(rp)[i];
+}
+__global__ void k_colblock_count(const void *rp, int bits, const int32_t *col, int64_t r0, int64_t nr, int32_t c0,
+                                 int32_t c1, int32_t *cnt) {
+  const int64_t T = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; r < nr; r += T) {
+    int32_t c = 0;
+    for (int64_t k = rp_dev(rp, bits, r0 + r), e = rp_dev(rp, bits, r0 + r + 1); k < e; ++k)
+      c += col[k] >= c0 && col[k] < c1;
+    cnt[r] = c;
+  }
+}
+template <typename T>
+__global__ void k_colblock_scatter(const void *rp, int bits, const int32_t *col, const T *val, int64_t r0, int64_t nr,
+                                   int32_t c0, int32_t c1, const int64_t *orp, int32_t *ocol, T *oval) {
+  const int64_t G = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; r < nr; r += G) {
+    int64_t o = orp[r];
+    for (int64_t k = rp_dev(rp, bits, r0 + r), e = rp_dev(rp, bits, r0 + r + 1); k < e; ++k)
+      if (col[k] >= c0 && col[k] < c1) {
+        ocol[o] = col[k] - c0;
+        oval[o] = val[k];
+        ++o;
+      }
+  }
+}
+
+// one column block on the device: host row offsets in orp, device col/val in
+// the returned buffers (freed by the caller)
+int colblock_device(const void *d_rp, int bits, const int32_t *d_col, const void *d_val, size_t tsz, int64_t r0,
+                    int64_t r1, int64_t c0, int64_t c1, std::vector<int64_t> &orp, void **d_ocol, void **d_oval) {
+  const int64_t nr = r1 - r0;
+  *d_ocol = *d_oval = nullptr;
+  orp.assign(static_cast<size_t>(nr) + 1, 0);
+  std::vector<int32_t> cnt(static_cast<size_t>(nr));
+  int32_t *d_cnt = nullptr;
+  int64_t *d_orp = nullptr;
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(&d_cnt), static_cast<size_t>(std::max<int64_t>(nr, 1)) * 4);
+  const unsigned grid = static_cast<unsigned>(std::min<int64_t>((nr + 255) / 256 + 1, 8192));
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_colblock_count, dim3(grid), dim3(256), 0, nullptr, d_rp, bits, d_col, r0, nr,
+                       static_cast<int32_t>(c0), static_cast<int32_t>(c1), d_cnt);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(cnt.data(), d_cnt, static_cast<size_t>(nr) * 4, hipMemcpyDeviceToHost);
+  (void)hipFree(d_cnt);
+  if (e != hipSuccess) return static_cast<int>(e);
+  for (int64_t r = 0; r < nr; ++r) orp[static_cast<size_t>(r) + 1] = orp[static_cast<size_t>(r)] + cnt[static_cast<size_t>(r)];
+  const int64_t m = orp[static_cast<size_t>(nr)];
+  if (m == 0) return LHPC_OK;
+  e = hipMalloc(&d_orp, static_cast<size_t>(nr + 1) * 8);
+  if (e == hipSuccess) e = hipMemcpy(d_orp, orp.data(), static_cast<size_t>(nr + 1) * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(d_ocol, static_cast<size_t>(m) * 4);
+  if (e == hipSuccess) e = hipMalloc(d_oval, static_cast<size_t>(m) * tsz);
+  if (e == hipSuccess) {
+    if (tsz == 4)
+      hipLaunchKernelGGL(k_colblock_scatter<float>, dim3(grid), dim3(256), 0, nullptr, d_rp, bits, d_col,
+                         static_cast<const float *>(d_val), r0, nr, static_cast<int32_t>(c0), static_cast<int32_t>(c1),
+                         d_orp, static_cast<int32_t *>(*d_ocol), static_cast<float *>(*d_oval));
+    else
+      hipLaunchKernelGGL(k_colblock_scatter<double>, dim3(grid), dim3(256), 0, nullptr, d_rp, bits, d_col,
+                         static_cast<const double *>(d_val), r0, nr, static_cast<int32_t>(c0), static_cast<int32_t>(c1),
+                         d_orp, static_cast<int32_t *>(*d_ocol), static_cast<double *>(*d_oval));
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  (void)hipFree(d_orp);
+  return static_cast<int>(e);
+}
+
 bool is_gfx950(int dev) {
   hipDeviceProp_t p;
   if (hipGetDeviceProperties(&p, dev) != hipSuccess) return false;
@@ -127,8 +201,10 @@ int xtile_col_blocks_for(int64_t n_rows, int64_t n_cols, int64_t nnz, size_t tsz
 // offset) run in turn on the same x, instead of dropping to XSLICE.  With
 // B > 1 column blocks every row part is further cut by column (above).
 // LHPC_ERR_UNSUPPORTED when some single row exceeds the cap.
+// d_rp non-null: device input (col_idx / val and d_rp in HBM, rp a host copy
+// of row_ptr): every part's layout is built on the GPU (xtile_build_device).
 int build_parts(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz,
-                int64_t cap, int B) {
+                int64_t cap, int B, const void *d_rp = nullptr) {
   const int64_t n_rows = p->n_rows;
   int64_t n_parts = std::max<int64_t>(1, (p->nnz + cap - 1) / cap);
   std::vector<int64_t> cuts;
@@ -161,7 +237,7 @@ int build_parts(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const 
     q->n_cols = c1 - c0;
     q->nnz = lnnz;
     q->xt_acc = acc;
-    LHPC_TRY(xtile_build(q, lrp, lc, lv, tsz));
+    LHPC_TRY(d_rp ? xtile_build_device(q, lrp, lc, lv, tsz) : xtile_build(q, lrp, lc, lv, tsz));
     p->bytes += q->bytes;
     return LHPC_OK;
   };
@@ -181,10 +257,25 @@ int build_parts(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const 
     }
     bool first = true;  // the first non-empty block stores every row of the part
     for (int b = 0; b < B; ++b) {
-      csr_column_block(rp.p, rp.bits, col_idx, val, tsz, r0, r1, cb[b], cb[b + 1], lrp, lcol, lval);
-      if (lcol.empty()) continue;  // adds nothing
-      LHPC_TRY(add(r0, r1, cb[b], cb[b + 1], RowPtrView{lrp.data(), 64}, lcol.data(), lval.data(),
-                   static_cast<int64_t>(lcol.size()), first ? 0 : 1));
+      if (d_rp) {
+        struct Tmp {
+          void *c = nullptr, *v = nullptr;
+          ~Tmp() {
+            if (c) (void)hipFree(c);
+            if (v) (void)hipFree(v);
+          }
+        } t;
+        LHPC_TRY(colblock_device(d_rp, rp.bits, col_idx, val, tsz, r0, r1, cb[b], cb[b + 1], lrp, &t.c, &t.v));
+        const int64_t m = lrp.back();
+        if (m == 0) continue;  // adds nothing
+        LHPC_TRY(add(r0, r1, cb[b], cb[b + 1], RowPtrView{lrp.data(), 64}, static_cast<const int32_t *>(t.c), t.v, m,
+                     first ? 0 : 1));
+      } else {
+        csr_column_block(rp.p, rp.bits, col_idx, val, tsz, r0, r1, cb[b], cb[b + 1], lrp, lcol, lval);
+        if (lcol.empty()) continue;  // adds nothing
+        LHPC_TRY(add(r0, r1, cb[b], cb[b + 1], RowPtrView{lrp.data(), 64}, lcol.data(), lval.data(),
+                     static_cast<int64_t>(lcol.size()), first ? 0 : 1));
+      }
       first = false;
     }
   }
@@ -424,8 +515,8 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
 // to the host, which makes every layout decision.  The XTILE layout — the
 // default for gathers without locality — is then built on the GPU from the
 // device arrays (xtile_build_device: byte-identical to the host build); any
-// other family, row parts, column blocks, aligned segments or several
-// devices copy A to the host and take the host path.
+// other family, aligned segments or several devices copy A to the host and
+// take the host path; row parts and column blocks are built on the GPU too.
 int plan_create_device_input(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
                              const void *row_ptr, int row_ptr_bits, const int32_t *col_idx, const void *val,
                              const int *device_ids, int n_devices, unsigned flags, int n_splits,
@@ -472,8 +563,11 @@ int plan_create_device_input(lhpc_spmv_plan **out, int dtype, int64_t n_rows, in
   const int64_t tiles = (n_cols + (tsz == 4 ? 40960 : 20480) - 1) / (tsz == 4 ? 40960 : 20480);
   int64_t cap = INT32_MAX - 8 * (tiles + 256) - (int64_t{1} << 16);
   if (o.xtile_part_nnz > 0) cap = std::min<int64_t>(cap, o.xtile_part_nnz);
-  const bool single = n_devices <= 1 && !o.multi_force && nnz <= cap && tiles <= 4096 && n_rows > 0 &&
-                      (n_splits > 0 || xtile_col_blocks_for(n_rows, n_cols, nnz, tsz, o) == 1);
+  // row parts and column blocks as plan_create_impl chooses them
+  const int B = n_splits == 0 ? xtile_col_blocks_for(n_rows, n_cols, nnz, tsz, o) : 1;
+  const bool parts = (nnz > cap || B > 1) && n_splits == 0;
+  const bool single = n_devices <= 1 && !o.multi_force && n_rows > 0 &&
+                      (parts ? (tiles + B - 1) / B <= 4096 : nnz <= cap && tiles <= 4096);
   bool want_xtile = single && (flags & LHPC_PLAN_FORCE_XTILE);
   if (single && auto_ok && !o.spmv_no_xtile && x_bytes > 8.0e6)
     want_xtile = gather_lines_per_nnz(
@@ -493,7 +587,8 @@ int plan_create_device_input(lhpc_spmv_plan **out, int dtype, int64_t n_rows, in
     p->n_rows = n_rows;
     p->n_cols = n_cols;
     p->nnz = nnz;
-    const int st = xtile_build_device(p, rp, col_idx, val, tsz);
+    const int st = parts ? build_parts(p, rp, col_idx, val, tsz, cap, B, row_ptr)
+                         : xtile_build_device(p, rp, col_idx, val, tsz);
     if (st == LHPC_OK) {
       *out = p;
       return LHPC_OK;
@@ -687,7 +782,20 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
 // layout built on the GPU from device input with the host build's.
 extern "C" int lhpc_spmv_plan_layout_digest(const lhpc_spmv_plan *p, uint64_t *out, int cap, int *n_out) {
   if (!p || !out || !n_out || cap < 10) return LHPC_ERR_INVALID_ARG;
-  if (p->kernel != LHPC_KERNEL_XTILE || !p->parts.empty() || p->multi) return LHPC_ERR_UNSUPPORTED;
+  if (p->kernel != LHPC_KERNEL_XTILE || p->multi) return LHPC_ERR_UNSUPPORTED;
+  if (!p->parts.empty()) {  // row parts / column blocks: the parts' digests folded in order
+    for (int i = 0; i < 10; ++i) out[i] = 0xcbf29ce484222325ull;
+    for (size_t j = 0; j < p->parts.size(); ++j) {
+      uint64_t d[10];
+      int n = 0;
+      LHPC_TRY(lhpc_spmv_plan_layout_digest(p->parts[j], d, 10, &n));
+      const uint64_t where = static_cast<uint64_t>(p->part_row[j]) * 0x9E3779B97F4A7C15ull ^
+                             static_cast<uint64_t>(p->part_col[j]) ^ static_cast<uint64_t>(p->parts[j]->xt_acc) << 63;
+      for (int i = 0; i < 10; ++i) out[i] = (out[i] ^ d[i] ^ where) * 0x100000001b3ull;
+    }
+    *n_out = 10;
+    return LHPC_OK;
+  }
   LHPC_HIP_TRY(hipSetDevice(p->device));
   const size_t tsz = p->dtype == LHPC_F32 ? 4 : 8;
   const int64_t C = p->xt_C, S = p->S, H = (C + kXtSegHi - 1) / kXtSegHi;

@@ -703,7 +703,8 @@ def _digests_host_vs_device(lhpc, gpu, rp, col, val, n_cols, flags=0, options=No
 
 
 @pytest.mark.parametrize("case", ["uniform_f32", "uniform_f64", "powerlaw_f32", "perm_f32", "ranges_f32",
-                                  "splits_f64", "rp64_f32"])
+                                  "splits_f64", "rp64_f32", "colblocks_f32", "powerlaw_colblocks_f64",
+                                  "parts_f32", "parts_colblocks_f32"])
 def test_device_input_layout_matches_host(lhpc, gpu, case):
     """LHPC_PLAN_DEVICE_INPUT: an XTILE plan built on the GPU from device
     row_ptr / col_idx / val (k_xt_counts → host offsets → k_xt_scatter →
@@ -713,7 +714,9 @@ def test_device_input_layout_matches_host(lhpc, gpu, case):
     gives the oracle's y bit for bit (dyadic).  Cases: uniform fp32 / fp64
     (iperm reduce), power-law rows crossing chunks (cont, fix-up), the perm
     reduce, cache-sized ranges (per-range pieces), a row-range split plan
-    (fp64), and int64 row_ptr input."""
+    (fp64), int64 row_ptr input, and plans of parts built part by part on the
+    GPU (column blocks cut by k_colblock_count / k_colblock_scatter, row
+    parts, both), whose digests fold the parts' in order."""
     n = 3_000_000
     dt = lhpc.F64 if "f64" in case else lhpc.F32
     if case.startswith("powerlaw"):
@@ -727,6 +730,14 @@ def test_device_input_layout_matches_host(lhpc, gpu, case):
         opts = {"xtile_ranges": 3}
     elif case == "splits_f64":
         splits = [n // 3, n // 2 + 7]
+    elif case == "colblocks_f32":
+        opts = {"xtile_col_blocks": 3}
+    elif case == "powerlaw_colblocks_f64":
+        opts = {"xtile_col_blocks": 2}
+    elif case == "parts_f32":
+        opts = {"xtile_part_nnz": 8_000_000}
+    elif case == "parts_colblocks_f32":
+        opts = {"xtile_part_nnz": 6_000_000, "xtile_col_blocks": 2}
     if case == "rp64_f32":
         assert rp.dtype == np.int64
     dh, dd = _digests_host_vs_device(lhpc, gpu, rp, col, val, n, options=opts, splits=splits)
