@@ -159,8 +159,8 @@ def test_xtile_large_n_80m(lhpc, gpu, blocks):
     (nnz = 1.2e9, fp32).  blocks = 1: one plan over 2048 x tiles (146K chunks;
     the dense segment table of starts needed 2.9e8 entries and the plan fell to
     XSLICE until the two-level table, lhpc_plan.hpp xtile_segment_table);
-    blocks = 0 (auto): two column blocks of 1024 tiles each, the second adding
-    into y.  Dyadic values: 10^5 sampled rows bit-exact against fp64 numpy
+    blocks = 0 (auto): three column blocks of ≈ 683 tiles each, the later ones
+    adding into y.  Dyadic values: 10^5 sampled rows bit-exact against fp64 numpy
     (exact here), and run to run determinism on the whole y."""
     import torch
     n = 80_000_000
@@ -170,8 +170,11 @@ def test_xtile_large_n_80m(lhpc, gpu, blocks):
         info = plan.info()
         # tiles of ≤ 40960 columns (narrowed to a whole multiple of the CUs: 2048 × 39063)
         assert info["kernel"] == lhpc.KERNEL_XTILE and info["slice_width"] <= 40960
-        cols = n if blocks == 1 else n // 2  # slices: the (first) block's tiles
-        assert info["slices"] == -(-cols // info["slice_width"]) and info["slices"] >= -(-cols // 40960)
+        if blocks == 1:
+            assert info["slices"] == -(-n // info["slice_width"]) and info["slices"] >= -(-n // 40960)
+        else:  # slices: the first block's tiles — B = ⌈2048 / 768⌉ = 3 blocks of ≤ 768
+            cols = n // 3 // 64 * 64
+            assert info["slices"] == -(-cols // info["slice_width"]) and info["slices"] <= 768
         xd = torch.from_numpy(x).to(gpu)
         y1 = plan(xd).clone()
         y2 = plan(xd)
