@@ -175,3 +175,32 @@ def test_multi_device_plan_argument_checks(lhpc):
     sp = np.array([1], dtype=np.int64)
     assert lhpc.lib.lhpc_spmv_plan_create_opts(*args, (C.c_int * 2)(0, 0), 2, 0, 1, sp.ctypes.data, None) == -5
     assert not h.value
+
+
+@pytest.mark.parametrize("py,c", [("Options", "lhpc_options"), ("PlanInfo", "lhpc_spmv_plan_info"),
+                                  ("DistXfer", "lhpc_dist_xfer")])
+def test_struct_mirrors_match_header(lhpc, tmp_path, py, c):
+    """Every ctypes mirror of an lhpc.h struct (libhpc_amd.Options, PlanInfo,
+    DistXfer) has the C struct's size and every field at the C offset: a
+    probe compiled against include/lhpc.h prints sizeof and offsetof for each
+    field the mirror names.  lhpc_options_init stamps struct_size = sizeof on
+    the Options mirror."""
+    import subprocess
+    cls = getattr(lhpc, py)
+    fields = [f[0] for f in cls._fields_]
+    src = tmp_path / "probe.c"
+    src.write_text("#include <stddef.h>\n#include <stdio.h>\n#include \"lhpc.h\"\nint main(void){\n"
+                   f"printf(\"size %zu\\n\", sizeof({c}));\n"
+                   + "".join(f"printf(\"{n} %zu\\n\", offsetof({c}, {n}));\n" for n in fields)
+                   + "return 0;}\n")
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                   check=True).stdout.splitlines())
+    assert int(got["size"]) == C.sizeof(cls)
+    for n in fields:
+        assert int(got[n]) == getattr(cls, n).offset, n
+    if py == "Options":
+        o = lhpc.Options()
+        lhpc.lib.lhpc_options_init(C.byref(o))
+        assert o.struct_size == C.sizeof(lhpc.Options)
