@@ -93,7 +93,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "blur_x", "blur_y", "sort", "cg"])
-    ap.add_argument("--n", type=int, default=10_000_000)
+    ap.add_argument("--n", "--n-rows", dest="n", type=int, default=10_000_000,
+                    help="rows = columns (--n-rows under torch.distributed.run, whose parser takes --n as a prefix)")
     ap.add_argument("--per-row", type=int, default=15)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--chunks", type=int, default=0,

@@ -186,13 +186,20 @@ __global__ void k_p2p_wait(const uint32_t *flags, int base, uint32_t e, int nran
 // stores reached this GPU's memory over xGMI without passing its L2s, so a
 // line of y that an XCD's L2 still holds from before (the gather of the next
 // call reads y as x) could be stale; one block per CU (dealt round-robin
-// over the XCDs) invalidates them all before the compute stream continues.
+// over the XCDs) invalidates them all before the stream continues.  (The wait
+// itself stays one block: a wait spread over every CU would hold a wave slot
+// on each while it spins, and the compute stream's reduce — 4 blocks of 8
+// waves per CU — would lose a block per CU for the duration.)
 __global__ void k_p2p_acquire_all() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
 
 // The flag allocation (uncached, one IPC handle): READY [0, n) | DONE
 // [n, 2n) | RED [2n, 3n) uint32 flags (n ≤ 64) in the first kFlagBytes, then
 // the scalar slots of the P2P all-gather: double [2 parities][64 ranks][8]
 constexpr size_t kFlagBytes = 1024;
+// uint32 index in the flag allocation of the push kernels' block counter
+// (this rank's only; past READY | DONE | RED at ≤ 3·64)
+constexpr int kPushCtr = 192;
+static_assert(kPushCtr * 4 < static_cast<int>(kFlagBytes), "push counter inside the flag words");
 constexpr int kRedMax = 8;
 constexpr size_t kFlagAlloc = kFlagBytes + 2 * 64 * kRedMax * sizeof(double);
 __device__ __forceinline__ double *red_slots(uint32_t *flags) {
@@ -236,23 +243,45 @@ __global__ void k_sum_ranks(const double *gathered, int nranks, int count, doubl
 // interior) for peers whose y has our 16-B phase, head [o0, a0) and tail
 // [a1, o1) as words; a peer with another phase (bit p of `narrow`) gets
 // words throughout.  blockIdx.y = peer
+// The chunk's DONE signal rides on the push: every block fences its stores at
+// system scope and counts itself in (kPushCtr, acq_rel); the last block resets
+// the counter and stores DONE = v (release, system scope) into every peer's
+// flag nranks + self.  A failed exchange still counts, so the counter stays
+// consistent, but stores nothing and signals nothing.
 __global__ __launch_bounds__(256) void k_p2p_push(void *const *peer_buf, const unsigned char *y, int64_t o0,
-                                                  int64_t o1, int self, uint64_t narrow, const uint32_t *status) {
-  if (p2p_failed(status)) return;
-  const int p = static_cast<int>(blockIdx.y) + (static_cast<int>(blockIdx.y) >= self ? 1 : 0);
-  unsigned char *dst = static_cast<unsigned char *>(peer_buf[p]);
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x, T = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  const uintptr_t yb = reinterpret_cast<uintptr_t>(y);
-  int64_t a0 = static_cast<int64_t>(((yb + o0 + 15) & ~uintptr_t{15}) - yb);
-  int64_t a1 = static_cast<int64_t>(((yb + o1) & ~uintptr_t{15}) - yb);
-  if ((narrow >> p) & 1u || a0 >= a1) a0 = a1 = o1;  // words only
-  for (int64_t i = o0 + 4 * t; i < a0; i += 4 * T)  // head words
-    *reinterpret_cast<uint32_t *>(dst + i) = *reinterpret_cast<const uint32_t *>(y + i);
-  for (int64_t i = a0 + 16 * t; i < a1; i += 16 * T)
-    *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(y + i);
-  for (int64_t i = a1 + 4 * t; i < o1; i += 4 * T)  // tail words
-    *reinterpret_cast<uint32_t *>(dst + i) = *reinterpret_cast<const uint32_t *>(y + i);
+                                                  int64_t o1, int self, uint64_t narrow, const uint32_t *status,
+                                                  uint32_t *flags, uint32_t *const *peer_flags, int nranks,
+                                                  uint32_t v) {
+  if (!p2p_failed(status)) {
+    const int p = static_cast<int>(blockIdx.y) + (static_cast<int>(blockIdx.y) >= self ? 1 : 0);
+    unsigned char *dst = static_cast<unsigned char *>(peer_buf[p]);
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
+                  T = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    const uintptr_t yb = reinterpret_cast<uintptr_t>(y);
+    int64_t a0 = static_cast<int64_t>(((yb + o0 + 15) & ~uintptr_t{15}) - yb);
+    int64_t a1 = static_cast<int64_t>(((yb + o1) & ~uintptr_t{15}) - yb);
+    if ((narrow >> p) & 1u || a0 >= a1) a0 = a1 = o1;  // words only
+    for (int64_t i = o0 + 4 * t; i < a0; i += 4 * T)  // head words
+      *reinterpret_cast<uint32_t *>(dst + i) = *reinterpret_cast<const uint32_t *>(y + i);
+    for (int64_t i = a0 + 16 * t; i < a1; i += 16 * T)
+      *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(y + i);
+    for (int64_t i = a1 + 4 * t; i < o1; i += 4 * T)  // tail words
+      *reinterpret_cast<uint32_t *>(dst + i) = *reinterpret_cast<const uint32_t *>(y + i);
+  }
   __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t *ctr = flags + kPushCtr;
+    const uint32_t total = gridDim.x * gridDim.y;
+    if (__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u == total) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      if (!p2p_failed(status))
+        for (int q = 0; q < nranks; ++q)
+          if (q != self)
+            __hip_atomic_store(peer_flags[q] + nranks + self, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 struct P2pBlob {  // LHPC_DIST_P2P_BLOB_BYTES per rank
@@ -317,25 +346,31 @@ int p2p_exchange_begin(lhpc_dist_comm *c, hipStream_t s, hipEvent_t ev) {
   return static_cast<int>(hipGetLastError());
 }
 
-int p2p_push(lhpc_dist_comm *c, const P2pWindow *w, int64_t o0, int64_t o1) {
-  if (o1 <= o0 || c->nranks < 2) return LHPC_OK;
+// chunk j's DONE value: epoch·64 + j + 1, so one slot per rank carries the
+// chunk progress of the call
+uint32_t p2p_done_value(const lhpc_dist_comm *c, int j) { return c->epoch * 64u + static_cast<uint32_t>(j) + 1u; }
+
+// bytes [o0, o1) of this rank's y to every peer, then DONE(j) (fused, see
+// k_p2p_push); a P2P chunk has at most one push (its own block)
+int p2p_push(lhpc_dist_comm *c, const P2pWindow *w, int64_t o0, int64_t o1, int j) {
   const int64_t vec = (o1 - o0) / 16 + 1;
   const unsigned bx = static_cast<unsigned>(std::min<int64_t>(64, (vec + 255) / 256));
   hipLaunchKernelGGL(k_p2p_push, dim3(bx, static_cast<unsigned>(c->nranks - 1)), dim3(256), 0, c->s_comm,
                      w->d_peer_buf, static_cast<const unsigned char *>(w->buf), o0, o1, c->rank, w->narrow,
-                     c->h_status);
+                     c->h_status, c->flags, c->d_peer_flags, c->nranks, p2p_done_value(c, j));
   return static_cast<int>(hipGetLastError());
 }
 
-// after this rank's pushes of chunk j: DONE(j) to every peer (value
-// epoch·64 + j + 1, so one slot per rank carries the chunk progress of the
-// call), then wait for every peer's DONE(j) and drop stale L2 lines of y —
-// from here chunk j of y is complete on this GPU
-int p2p_chunk_done(lhpc_dist_comm *c, int j) {
-  const uint32_t v = c->epoch * 64u + static_cast<uint32_t>(j) + 1u;
-  hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(64), 0, c->s_comm, c->d_peer_flags, c->nranks + c->rank, v, c->nranks,
-                     c->rank, c->h_status);
-  LHPC_HIP_TRY(hipGetLastError());
+// after this rank's push of chunk j (which signalled DONE(j); a chunk with
+// no rows here signals alone): wait for every peer's DONE(j) and drop stale
+// L2 lines of y — from here chunk j of y is complete on this GPU
+int p2p_chunk_done(lhpc_dist_comm *c, int j, bool pushed) {
+  const uint32_t v = p2p_done_value(c, j);
+  if (!pushed) {
+    hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(64), 0, c->s_comm, c->d_peer_flags, c->nranks + c->rank, v,
+                       c->nranks, c->rank, c->h_status);
+    LHPC_HIP_TRY(hipGetLastError());
+  }
   hipLaunchKernelGGL(k_p2p_wait, dim3(1), dim3(64), 0, c->s_comm, c->flags, c->nranks, v, c->nranks, c->rank,
                      c->h_status);
   LHPC_HIP_TRY(hipGetLastError());
@@ -419,11 +454,14 @@ int exchange_chunk(lhpc_dist_spmv_plan *d, int xk, const P2pWindow *w, int k, vo
   lhpc::RocTxRange rb("lhpc_dist_spmv: y chunk exchange");
   if (xk == LHPC_DIST_EXCHANGE_P2P) {
     const int64_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
-    for (int64_t e = d->first_p2p[k]; e < d->first_p2p[k + 1]; ++e) {
+    bool pushed = false;
+    for (int64_t e = d->first_p2p[k]; e < d->first_p2p[k + 1]; ++e) {  // ≤ 1 (build_schedule)
       const lhpc_dist_xfer &x = d->sched_p2p[e];
-      LHPC_TRY(p2p_push(c, w, x.offset * tsz, (x.offset + x.count) * tsz));
+      if (x.count <= 0 || c->nranks < 2) continue;
+      LHPC_TRY(p2p_push(c, w, x.offset * tsz, (x.offset + x.count) * tsz, k));
+      pushed = true;
     }
-    LHPC_TRY(p2p_chunk_done(c, k));
+    LHPC_TRY(p2p_chunk_done(c, k, pushed));
   } else {
     LHPC_TRY(issue_rccl_chunk(d, k, y, c->s_comm));
   }
