@@ -891,6 +891,20 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
         def run(iters):
             x = torch.zeros(n, dtype=torch.float64, device=dev)
             return dplan.cg(bfull, x, pw, tol=0.0, max_iter=iters, check_every=iters, stream=stream)
+    elif world == 1:
+        # lhpc_cg_solve: the native loop, whose check_every = 10 iterations
+        # between two convergence checks replay as one captured HIP graph
+        # (tol 0: exactly `iters` iterations; the warmup solve captures it)
+        plan = L.SpMVPlan(rp, col, val, n)
+        bfull = torch.from_numpy(b).to(dev)
+        cg_stream = torch.cuda.Stream(dev)
+
+        def run(iters):
+            x = torch.zeros(n, dtype=torch.float64, device=dev)
+            with torch.cuda.stream(cg_stream):
+                out = L.cg(plan, bfull, x, tol=0.0, max_iter=iters, check_every=10, stream=cg_stream)
+            cg_stream.synchronize()
+            return out
     else:
         ib = InterleavedBlocks(n, world, 1)
         r0, r1 = ib.rows(rank, 0)
@@ -904,7 +918,7 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
             x = torch.zeros_like(bd)
             return solver.solve(bd, x, tol=0.0, max_iter=iters, check_every=iters)  # tol 0: exactly `iters` iterations
 
-    run(max(1, args.warmup))
+    run(max(10, args.warmup))
     barrier()
     t0 = time.perf_counter()
     _, it, res = run(args.steps)
@@ -928,7 +942,7 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
                        "iterations": it, "relres": res,
                        "kernel": dplan.local_info()["kernel"] if native else plan.info()["kernel"],
                        "solver": "lhpc_dist_cg_solve (native, RCCL, chained stages)" if native else
-                                 ("lhpc building blocks (libhpc_amd.dist.DistCG)" if world == 1 else
+                                 ("lhpc_cg_solve (native loop, 10-iteration HIP graph blocks)" if world == 1 else
                                   "DistCG over torch.distributed")},
                roofline={"bound": "hbm", "kernel": "spmv_dot + k_cg_r + k_cg_xp",
                          "achieved": alg / per / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",

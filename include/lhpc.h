@@ -463,7 +463,11 @@ int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
  * every `check_every` iterations, the only host synchronisations) or after
  * max_iter iterations; reports the iterations run and ‖r‖/‖b‖ of the
  * recursively updated residual.  LHPC_ERR_INTERNAL on breakdown (non-finite
- * residual: the matrix is not SPD).  Dots are fp64, deterministic.
+ * residual: the matrix is not SPD).  Dots are fp64, deterministic.  The
+ * solve keeps its work (4 vectors + scalars) with the plan, and on a
+ * non-null stream with check_every ≥ 4 and an ADAPTIVE plan it replays the
+ * check_every iterations between two checks as a captured HIP graph, also
+ * kept with the plan (results bit-identical to the loop).
  * Building blocks for multi-GPU composition (all asynchronous on `stream`,
  * scalars are fp64 HBM pointers, read on the device):
  *   lhpc_vec_dot     *out = a·b

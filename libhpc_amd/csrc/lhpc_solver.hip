@@ -173,6 +173,21 @@ int dot_dev(const T *a, const T *b, int64_t n, double *out, double *part, hipStr
   return check_launch(s);
 }
 
+// r -= α·q, rr_out = r·r with the caller's partials buffer (no allocation:
+// the solver's iterations are captured into a graph)
+int cg_r_launch(int dtype, int64_t n, const double *num, const double *den, void *r, const void *q, double *rr_out,
+                double *part, hipStream_t s) {
+  const int g = vec_grid(n);
+  if (dtype == LHPC_F32)
+    hipLaunchKernelGGL((k_cg_r<float>), dim3(g), dim3(kVecThreads), 0, s, static_cast<float *>(r),
+                       static_cast<const float *>(q), n, num, den, part);
+  else
+    hipLaunchKernelGGL((k_cg_r<double>), dim3(g), dim3(kVecThreads), 0, s, static_cast<double *>(r),
+                       static_cast<const double *>(q), n, num, den, part);
+  hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(kVecThreads), 0, s, part, g, rr_out);
+  return check_launch(s);
+}
+
 }  // namespace
 }  // namespace lhpc
 
@@ -290,20 +305,20 @@ extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, doubl
   const size_t ts = dtype == LHPC_F32 ? 4 : 8;
   if (check_every < 1) check_every = 1;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // scratch: r, p, q vectors + scalars [rr0, rr1, pq, bb] + dot partials
-  void *vecs = nullptr;
-  Scratch sc;
-  sc.s = s;
-  LHPC_HIP_TRY(scratch_alloc(&vecs, static_cast<size_t>(std::max<int64_t>(n, 1)) * ts * 3, s));
-  struct VecFree {
-    void *p;
-    hipStream_t s;
-    ~VecFree() { (void)hipFreeAsync(p, s); }
-  } vf{vecs, s};
-  LHPC_HIP_TRY(scratch_alloc(reinterpret_cast<void **>(&sc.d), (8 + kDotBlocks) * sizeof(double), s));
-  char *vb = static_cast<char *>(vecs);
+  // work (kept with the plan, so a captured iteration block can be replayed
+  // by later solves): r, p, q, x vectors + scalars [rr0, rr1, pq, bb] + dot
+  // partials; the caller's x is copied in and out
+  if (!plan->cg_vecs) {
+    LHPC_HIP_TRY(hipMalloc(&plan->cg_vecs, static_cast<size_t>(std::max<int64_t>(n, 1)) * ts * 4));
+    LHPC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&plan->cg_scal), (8 + kDotBlocks) * sizeof(double)));
+  }
+  char *vb = static_cast<char *>(plan->cg_vecs);
   void *r = vb, *p = vb + static_cast<size_t>(n) * ts, *q = vb + 2 * static_cast<size_t>(n) * ts;
-  double *rr[2] = {sc.d, sc.d + 1}, *pq = sc.d + 2, *bb = sc.d + 3, *part = sc.d + 8;
+  void *x_user = x;
+  x = vb + 3 * static_cast<size_t>(n) * ts;
+  LHPC_HIP_TRY(hipMemcpyAsync(x, x_user, static_cast<size_t>(n) * ts, hipMemcpyDeviceToDevice, s));
+  double *rr[2] = {plan->cg_scal, plan->cg_scal + 1}, *pq = plan->cg_scal + 2, *bb = plan->cg_scal + 3,
+         *part = plan->cg_scal + 8;
   const int g = vec_grid(n);
   int it = 0;
   // the two scalars the host loop reads come back into pinned memory: no
@@ -335,10 +350,82 @@ extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, doubl
   const double stop = tol * tol * (h_bb > 0.0 ? h_bb : 1.0);
   int cur = 0;
   int status = LHPC_OK;
+  // one iteration's device work: q = A·p and p·q in one pass (ADAPTIVE), r -=
+  // α·q with rr' = r·r, and (full) x += α·p, p = r + β·p in one pass
+  auto body = [&](int c, bool full) -> int {
+    LHPC_TRY(lhpc_spmv_dot(plan, p, q, p, pq, s));
+    LHPC_TRY(cg_r_launch(dtype, n, rr[c], pq, r, q, rr[c ^ 1], part, s));
+    if (full) LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[c], pq, rr[c ^ 1], rr[c], x, p, r, s));
+    return LHPC_OK;
+  };
+  // Graph blocks: the C = check_every iterations between two convergence
+  // checks — C − 1 full iterations and the C-th up to rr' — captured once per
+  // starting parity of the rr pair and replayed (one launch instead of ≈ 5C;
+  // the same kernels in the same order, so x is bit-identical to the loop's).
+  // ADAPTIVE plans only (their fused dot allocates nothing after the first
+  // call, which the x·x warm-up below makes); not on the null stream, not
+  // for multi-device plans, not in the synchronous-check debug build.
+#ifdef LHPC_DEBUG_SYNC
+  bool graphs = false;
+#else
+  bool graphs = s != nullptr && check_every >= 4 && plan->kernel == LHPC_KERNEL_ADAPTIVE && !plan->multi &&
+                plan->parts.empty() && plan->n_blocks > 0;
+#endif
+  // kept with the plan: every pointer in them (the plan's arrays and work)
+  // outlives the solve, so later solves with the same check_every replay them
+  hipGraphExec_t *ge = plan->cg_graph;
+  for (int c = 0; c < 2; ++c)
+    if (ge[c] && plan->cg_graph_iters[c] != check_every) {
+      (void)hipGraphExecDestroy(ge[c]);
+      ge[c] = nullptr;
+    }
+  auto capture = [&](int c) -> bool {
+    hipGraph_t g = nullptr;
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) return false;
+    int st = LHPC_OK, cc = c;
+    for (int i = 0; i < check_every - 1 && st == LHPC_OK; ++i, cc ^= 1) st = body(cc, true);
+    if (st == LHPC_OK) st = body(cc, false);
+    const hipError_t e = hipStreamEndCapture(s, &g);
+    (void)hipGetLastError();
+    bool ok = st == LHPC_OK && e == hipSuccess && g &&
+              hipGraphInstantiate(&ge[c], g, nullptr, nullptr, 0) == hipSuccess;
+    plan->cg_graph_iters[c] = ok ? check_every : 0;
+    if (g) (void)hipGraphDestroy(g);
+    if (!ok && ge[c]) {
+      (void)hipGraphExecDestroy(ge[c]);
+      ge[c] = nullptr;
+    }
+    return ok;
+  };
+  if (graphs && !plan->d_dpart) {  // the fused dot's partials exist before any capture
+    LHPC_TRY(lhpc_spmv_dot(plan, x, q, x, pq, s));
+  }
   if (h_rr > stop) {
-    for (it = 1; it <= max_iter; ++it) {
-      LHPC_TRY(lhpc_spmv_dot(plan, p, q, p, pq, s));  // q = A·p and p·q in one pass (ADAPTIVE)
-      LHPC_TRY(lhpc_cg_step_r(dtype, n, rr[cur], pq, r, q, rr[cur ^ 1], s));
+    for (it = 0; it < max_iter;) {
+      if (graphs && it % check_every == 0 && it + check_every <= max_iter) {
+        if (!ge[cur] && !capture(cur)) {
+          graphs = false;  // capture refused: the plain loop below
+          continue;
+        }
+        LHPC_HIP_TRY(hipGraphLaunch(ge[cur], s));
+        it += check_every;
+        const int c = cur ^ ((check_every - 1) & 1);  // parity of the block's last iteration
+        LHPC_HIP_TRY(hipMemcpyAsync(&h_rr, rr[c ^ 1], 8, hipMemcpyDeviceToHost, s));
+        LHPC_HIP_TRY(hipStreamSynchronize(s));
+        if (!std::isfinite(h_rr)) {
+          status = LHPC_ERR_INTERNAL;
+          break;
+        }
+        if (h_rr <= stop) {
+          LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[c], pq, nullptr, nullptr, x, p, nullptr, s));  // x += α·p
+          break;
+        }
+        LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[c], pq, rr[c ^ 1], rr[c], x, p, r, s));
+        cur = c ^ 1;
+        continue;
+      }
+      ++it;
+      LHPC_TRY(body(cur, false));
       if (it % check_every == 0 || it == max_iter) {
         LHPC_HIP_TRY(hipMemcpyAsync(&h_rr, rr[cur ^ 1], 8, hipMemcpyDeviceToHost, s));
         LHPC_HIP_TRY(hipStreamSynchronize(s));
@@ -357,6 +444,7 @@ extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, doubl
     }
     if (it > max_iter) it = max_iter;
   }
+  LHPC_HIP_TRY(hipMemcpyAsync(x_user, x, static_cast<size_t>(n) * ts, hipMemcpyDeviceToDevice, s));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
   if (iters_out) *iters_out = it;
   if (resid_out) *resid_out = std::sqrt(std::max(h_rr, 0.0)) / std::sqrt(h_bb > 0.0 ? h_bb : 1.0);

@@ -772,6 +772,10 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
                   static_cast<void *>(p->d_carry)})
     if (q) (void)hipFree(q);
   if (p->h_scalars) (void)hipHostFree(p->h_scalars);
+  for (hipGraphExec_t g : p->cg_graph)
+    if (g) (void)hipGraphExecDestroy(g);
+  if (p->cg_vecs) (void)hipFree(p->cg_vecs);
+  if (p->cg_scal) (void)hipFree(p->cg_scal);
   delete p;
   return LHPC_OK;
 }

@@ -28,6 +28,13 @@ struct lhpc_spmv_plan {
   int64_t n_blocks = 0, n_long = 0;
   void *d_xstage = nullptr, *d_ystage = nullptr;
   double *h_scalars = nullptr;  // lhpc_cg_solve: 2 pinned host scalars, allocated on first use
+  // lhpc_cg_solve's work (first solve; freed with the plan): r, p, q and x
+  // vectors, device scalars + dot partials, and the captured iteration blocks
+  // (graph c starts at rr parity c and holds cg_graph_iters[c] iterations)
+  void *cg_vecs = nullptr;
+  double *cg_scal = nullptr;
+  hipGraphExec_t cg_graph[2] = {nullptr, nullptr};
+  int cg_graph_iters[2] = {0, 0};
   double *d_dpart = nullptr;  // lhpc_spmv_dot: per-block partials (ADAPTIVE), allocated on first use
   int kernel = LHPC_KERNEL_ROWGROUP;
   int L = 16, R = 4;

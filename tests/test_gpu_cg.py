@@ -44,6 +44,36 @@ def test_cg_fp32(lhpc, gpu):
     assert np.linalg.norm(x - want) <= 1e-4 * np.linalg.norm(want)
 
 
+@pytest.mark.parametrize("check_every,max_iter", [(4, 5000), (7, 5000), (6, 20), (5, 3)])
+def test_cg_graph_blocks_match_loop(lhpc, gpu, check_every, max_iter):
+    """On a non-null stream lhpc_cg_solve replays the check_every iterations
+    between two convergence checks as a captured HIP graph (ADAPTIVE plans);
+    on the null stream it runs the plain loop.  Both issue the same kernels in
+    the same order: x bit-identical, same iteration count and residual — for
+    even and odd check_every (both graph parities), a max_iter that ends in
+    the middle of a block (the tail runs the loop), and one too short for
+    any block; then the fp64 oracle's tolerance."""
+    import torch
+    rp, col, val = S.laplacian_2d(96, 80)
+    n = rp.size - 1
+    b = _dev(gpu, np.random.default_rng(17).uniform(-1, 1, n))
+    with lhpc.SpMVPlan(rp, col, val, n) as plan:
+        assert plan.info()["kernel"] == lhpc.KERNEL_ADAPTIVE
+        x0, it0, r0 = lhpc.cg(plan, b, tol=1e-10, max_iter=max_iter, check_every=check_every,
+                              stream=torch.cuda.default_stream(gpu))
+        s = torch.cuda.Stream(gpu)
+        with torch.cuda.stream(s):
+            x1, it1, r1 = lhpc.cg(plan, b, tol=1e-10, max_iter=max_iter, check_every=check_every, stream=s)
+            x2, it2, r2 = lhpc.cg(plan, b, tol=1e-10, max_iter=max_iter, check_every=check_every, stream=s)
+        s.synchronize()
+    assert (it0, r0) == (it1, r1) == (it2, r2)
+    assert torch.equal(x0, x1) and torch.equal(x1, x2)
+    if max_iter == 5000:
+        want, it_o, _ = S.cg_oracle(rp, col, val, b.cpu().numpy(), tol=1e-10, max_iter=5000)
+        assert it0 - check_every <= it_o <= it0 and it0 % check_every == 0
+        assert np.linalg.norm(x0.cpu().numpy() - want) <= 1e-8 * np.linalg.norm(want)
+
+
 def test_cg_warm_start_and_zero_rhs(lhpc, gpu):
     import torch
     rp, col, val = S.laplacian_2d(32, 32)
