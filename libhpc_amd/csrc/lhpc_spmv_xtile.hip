@@ -883,11 +883,13 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   const lhpc_options &o = p->opt;
   if (o.xtile_piece > 0) piece = std::max<int64_t>(8, o.xtile_piece);
   // reduce index stream: iperm (gather each CSR position's x from the flat
-  // segment concatenation in LDS) for ≥ 32 full chunks per CU, else perm
-  // (scatter into CSR slots): with fewer chunks (per-rank matrices at N ≥ 4)
-  // the perm reduce's shorter blocks win (W = 8 rank of C2: 0.088 against
-  // 0.093 ms; W = 1: 0.626 against 0.611 ms; profiles/r01/explore_scaling_*)
-  bool ip = p->nnz >= 32LL * cus * M;
+  // segment concatenation in LDS), else perm (scatter into CSR slots).  Round
+  // 1 kept perm below 32 full chunks per CU (per-rank matrices at N ≥ 4);
+  // with the reduce as it is now iperm is as fast or faster there too — same
+  // box, local work of rank 0 (tools/explore_rank_reduce.py,
+  // profiles/r04/rank_reduce.jsonl): fp32 W = 4 0.132 → 0.118 ms, W = 8
+  // 0.0656 → 0.0653; fp64 W = 4 0.263 → 0.245, W = 8 0.125 → 0.118
+  bool ip = true;
   if (o.xtile_reduce != LHPC_XTILE_REDUCE_AUTO) ip = o.xtile_reduce == LHPC_XTILE_REDUCE_IPERM;
   // the iperm reduce addresses xg with 32-bit buffer offsets: stream + tile
   // padding (≤ 8 per tile) + one piece of slack must stay below 2 GiB
