@@ -208,7 +208,10 @@ typedef struct lhpc_options {
    * range, run in turn, every block after the first adding into y.  0: auto,
    * 1: never, B ≥ 2: B blocks (tests: the path at small sizes)               */
   int32_t xtile_col_blocks;
-  int32_t reserved;
+  /* XTILE layout build for host-buffer CSR: 0 (auto) uploads A and builds on
+   * the GPU (byte-identical to the host build, several times faster), 1
+   * builds on the host (tests compare the two)                              */
+  int32_t xtile_host_build;
 } lhpc_options;
 void lhpc_options_init(lhpc_options *opts);
 

@@ -82,7 +82,7 @@ struct lhpc_dist_comm {
   uint32_t *h_status = nullptr;  // host-mapped: bit 0 = a flag wait timed out
   uint32_t epoch = 0;
   uint32_t red_epoch = 0;        // P2P all-gathers of scalars (RED flags)
-  int cus = 256;  // compute units of the device (k_p2p_acquire_all grid)
+  int cus = 256;  // compute units of the device
   P2pWindow win[LHPC_DIST_P2P_MAX_WINDOWS];
   int n_win = 0;
   // halo stencil: "u complete on the caller's stream" and "halo planes
@@ -110,6 +110,11 @@ struct lhpc_dist_spmv_plan {
   // x by column parts (part j = the columns exchange j delivers)
   const void *pending_y = nullptr;
   bool chain = false;
+  // a pending P2P exchange: its epoch (the peers' DONE values are
+  // epoch·64 + chunk + 1), waited for on the compute stream by the consumer
+  // (the chained stage per part, or wait_pending for the whole y)
+  bool pending_p2p = false;
+  uint32_t pending_epoch = 0;
   // chunk reduces alternate over the caller's stream and s_red2
   // (options.dist_reduce_streams), joined by ev_fork / ev_join
   hipStream_t s_red2 = nullptr;
@@ -182,15 +187,32 @@ __global__ void k_p2p_wait(const uint32_t *flags, int base, uint32_t e, int nran
     __builtin_amdgcn_s_sleep(127);
   }
 }
-// after every peer's DONE: a system-scope acquire on every XCD.  The peers'
-// stores reached this GPU's memory over xGMI without passing its L2s, so a
-// line of y that an XCD's L2 still holds from before (the gather of the next
-// call reads y as x) could be stale; one block per CU (dealt round-robin
-// over the XCDs) invalidates them all before the stream continues.  (The wait
-// itself stays one block: a wait spread over every CU would hold a wave slot
-// on each while it spins, and the compute stream's reduce — 4 blocks of 8
-// waves per CU — would lose a block per CU for the duration.)
-__global__ void k_p2p_acquire_all() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+// the consumer's side of a P2P chunk (compute stream, right before the first
+// read of it): every block waits for every peer's DONE at base + p ≥ e
+// (bounded as k_p2p_wait), then acquires at system scope.  The peers' stores
+// reached this GPU's memory over xGMI without passing its L2s, so a line of
+// y that an XCD's L2 still holds from before (the gather reads y as the next
+// x) could be stale: kP2pAcqBlocks blocks, dealt round-robin over the XCDs,
+// make every XCD drop them.  A handful of spinning waves, not one per CU (a
+// wave slot per CU would cost a concurrent reduce a block per CU).
+constexpr int kP2pAcqBlocks = 16;
+__global__ void k_p2p_wait_acquire(const uint32_t *flags, int base, uint32_t e, int nranks, int self,
+                                   uint32_t *status) {
+  const int p = threadIdx.x;
+  if (p < nranks && p != self) {
+    for (uint32_t spins = 0;; ++spins) {
+      const uint32_t f = __hip_atomic_load(flags + base + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (static_cast<int32_t>(f - e) >= 0) break;
+      if (spins > (1u << 21) || p2p_failed(status)) {
+        __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(127);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
 
 // The flag allocation (uncached, one IPC handle): READY [0, n) | DONE
 // [n, 2n) | RED [2n, 3n) uint32 flags (n ≤ 64) in the first kFlagBytes, then
@@ -361,20 +383,19 @@ int p2p_push(lhpc_dist_comm *c, const P2pWindow *w, int64_t o0, int64_t o1, int 
   return static_cast<int>(hipGetLastError());
 }
 
-// after this rank's push of chunk j (which signalled DONE(j); a chunk with
-// no rows here signals alone): wait for every peer's DONE(j) and drop stale
-// L2 lines of y — from here chunk j of y is complete on this GPU
-int p2p_chunk_done(lhpc_dist_comm *c, int j, bool pushed) {
-  const uint32_t v = p2p_done_value(c, j);
-  if (!pushed) {
-    hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(64), 0, c->s_comm, c->d_peer_flags, c->nranks + c->rank, v,
-                       c->nranks, c->rank, c->h_status);
-    LHPC_HIP_TRY(hipGetLastError());
-  }
-  hipLaunchKernelGGL(k_p2p_wait, dim3(1), dim3(64), 0, c->s_comm, c->flags, c->nranks, v, c->nranks, c->rank,
-                     c->h_status);
-  LHPC_HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_p2p_acquire_all, dim3(static_cast<unsigned>(c->cus)), dim3(64), 0, c->s_comm);
+// chunk j with no rows on this rank: DONE(j) alone (a push signals it)
+int p2p_signal_done(lhpc_dist_comm *c, int j) {
+  hipLaunchKernelGGL(k_p2p_signal, dim3(1), dim3(64), 0, c->s_comm, c->d_peer_flags, c->nranks + c->rank,
+                     p2p_done_value(c, j), c->nranks, c->rank, c->h_status);
+  return static_cast<int>(hipGetLastError());
+}
+
+// on the consumer's stream: every peer's chunk j of the exchange of `epoch`
+// has landed, and this GPU's caches hold no stale line of it
+int p2p_wait_chunk(lhpc_dist_comm *c, uint32_t epoch, int j, hipStream_t s) {
+  const uint32_t v = epoch * 64u + static_cast<uint32_t>(j) + 1u;
+  hipLaunchKernelGGL(k_p2p_wait_acquire, dim3(kP2pAcqBlocks), dim3(64), 0, s, c->flags, c->nranks, v, c->nranks,
+                     c->rank, c->h_status);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -446,7 +467,8 @@ int pick_exchange(const lhpc_dist_spmv_plan *d, const void *y, const P2pWindow *
 }
 
 // chunk k's exchange on the comm stream, after the compute stream's event;
-// ev_x[k] marks it landed on this rank
+// ev_x[k] marks this rank's part of it done (RCCL: the chunk landed; P2P: the
+// push issued — the peers' chunk is waited for by p2p_wait_chunk)
 int exchange_chunk(lhpc_dist_spmv_plan *d, int xk, const P2pWindow *w, int k, void *y, hipStream_t s) {
   lhpc_dist_comm *c = d->comm;
   LHPC_HIP_TRY(hipEventRecord(d->ev[k], s));
@@ -454,6 +476,9 @@ int exchange_chunk(lhpc_dist_spmv_plan *d, int xk, const P2pWindow *w, int k, vo
   lhpc::RocTxRange rb("lhpc_dist_spmv: y chunk exchange");
   if (xk == LHPC_DIST_EXCHANGE_P2P) {
     const int64_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
+    // the push signals DONE(k); the consumer waits for the peers' DONE(k) on
+    // its own stream (p2p_wait_chunk), so the comm stream carries one kernel
+    // per chunk
     bool pushed = false;
     for (int64_t e = d->first_p2p[k]; e < d->first_p2p[k + 1]; ++e) {  // ≤ 1 (build_schedule)
       const lhpc_dist_xfer &x = d->sched_p2p[e];
@@ -461,7 +486,7 @@ int exchange_chunk(lhpc_dist_spmv_plan *d, int xk, const P2pWindow *w, int k, vo
       LHPC_TRY(p2p_push(c, w, x.offset * tsz, (x.offset + x.count) * tsz, k));
       pushed = true;
     }
-    LHPC_TRY(p2p_chunk_done(c, k, pushed));
+    if (!pushed && c->nranks > 1) LHPC_TRY(p2p_signal_done(c, k));
   } else {
     LHPC_TRY(issue_rccl_chunk(d, k, y, c->s_comm));
   }
@@ -473,7 +498,11 @@ int exchange_chunk(lhpc_dist_spmv_plan *d, int xk, const P2pWindow *w, int k, vo
 int wait_pending(lhpc_dist_spmv_plan *d, hipStream_t s) {
   if (!d->pending_y) return LHPC_OK;
   d->pending_y = nullptr;
-  LHPC_HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
+  LHPC_HIP_TRY(hipStreamWaitEvent(s, d->done, 0));  // this rank's own exchange work
+  if (d->pending_p2p) {  // the peers' last chunk (DONE values are monotone: all chunks)
+    d->pending_p2p = false;
+    LHPC_TRY(p2p_wait_chunk(d->comm, d->pending_epoch, d->K - 1, s));
+  }
   return LHPC_OK;
 }
 
@@ -910,10 +939,14 @@ int spmv_begin(lhpc_dist_spmv_plan *d, const void *x, void *y, hipStream_t s, bo
   if (chained && d->chain) {
     lhpc::RocTxRange rc("lhpc_dist_spmv: chained stage");
     for (int j = 0; j < d->K; ++j) {
-      LHPC_HIP_TRY(hipStreamWaitEvent(s, d->ev_x[j], 0));
+      if (d->pending_p2p) LHPC_TRY(p2p_wait_chunk(c, d->pending_epoch, j, s));  // the peers' chunk j
+      else LHPC_HIP_TRY(hipStreamWaitEvent(s, d->ev_x[j], 0));
       LHPC_TRY(lhpc::local_plans_stage_part(d->lp, x, j, s));
     }
+    // this rank's own pushes of x end before anything here writes its rows
+    if (d->pending_p2p) LHPC_HIP_TRY(hipStreamWaitEvent(s, d->done, 0));
     d->pending_y = nullptr;
+    d->pending_p2p = false;
   } else {
     if (chained) LHPC_TRY(wait_pending(d, s));
     LHPC_TRY(lhpc::local_plans_stage(d->lp, x, s));
@@ -940,6 +973,8 @@ int spmv_begin(lhpc_dist_spmv_plan *d, const void *x, void *y, hipStream_t s, bo
   if (xchg) {
     LHPC_HIP_TRY(hipEventRecord(d->done, c->s_comm));
     d->pending_y = y;
+    d->pending_p2p = xk == LHPC_DIST_EXCHANGE_P2P;
+    d->pending_epoch = c->epoch;
   }
   return LHPC_OK;
 }
@@ -957,6 +992,8 @@ int exchange_begin(lhpc_dist_spmv_plan *d, void *y, hipStream_t s) {
   for (int k = 0; k < d->K; ++k) LHPC_TRY(exchange_chunk(d, xk, win, k, y, s));
   LHPC_HIP_TRY(hipEventRecord(d->done, c->s_comm));
   d->pending_y = y;
+  d->pending_p2p = xk == LHPC_DIST_EXCHANGE_P2P;
+  d->pending_epoch = c->epoch;
   return LHPC_OK;
 }
 }  // namespace

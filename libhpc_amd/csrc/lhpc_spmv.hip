@@ -291,6 +291,35 @@ int plan_create_device_input(lhpc_spmv_plan **out, int dtype, int64_t n_rows, in
                              const int *device_ids, int n_devices, unsigned flags, int n_splits,
                              const int64_t *split_rows, const lhpc_options *opts);
 
+// host A → HBM copies → the device layout build (xtile_build_device /
+// build_parts on the device); LHPC_ERR_UNSUPPORTED when the device build
+// does not apply (aligned segments) or the copies do not fit in HBM
+int xtile_build_uploaded(lhpc_spmv_plan *p, RowPtrView rp, const void *row_ptr, const int32_t *col_idx,
+                         const void *val, size_t tsz, bool parts, int64_t cap, int B) {
+  if (p->opt.xtile_host_build == 1 || p->opt.xtile_align == LHPC_XTILE_ALIGN_UNITS || p->nnz == 0)
+    return LHPC_ERR_UNSUPPORTED;
+  struct Tmp {
+    void *a = nullptr;
+    ~Tmp() {
+      if (a) (void)hipFree(a);
+    }
+  } d_rp, d_col, d_val;
+  const size_t rpb = static_cast<size_t>(p->n_rows + 1) * (rp.bits / 8);
+  const size_t nnz = static_cast<size_t>(p->nnz);
+  if (hipMalloc(&d_rp.a, rpb) != hipSuccess || hipMalloc(&d_col.a, std::max<size_t>(nnz, 1) * 4) != hipSuccess ||
+      hipMalloc(&d_val.a, std::max<size_t>(nnz, 1) * tsz) != hipSuccess) {
+    (void)hipGetLastError();
+    return LHPC_ERR_UNSUPPORTED;
+  }
+  LHPC_HIP_TRY(hipMemcpy(d_rp.a, row_ptr, rpb, hipMemcpyHostToDevice));
+  if (nnz) {
+    LHPC_HIP_TRY(hipMemcpy(d_col.a, col_idx, nnz * 4, hipMemcpyHostToDevice));
+    LHPC_HIP_TRY(hipMemcpy(d_val.a, val, nnz * tsz, hipMemcpyHostToDevice));
+  }
+  const int32_t *dc = static_cast<const int32_t *>(d_col.a);
+  return parts ? build_parts(p, rp, dc, d_val.a, tsz, cap, B, d_rp.a) : xtile_build_device(p, rp, dc, d_val.a, tsz);
+}
+
 int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
                      const void *row_ptr, int row_ptr_bits, const int32_t *col_idx, const void *val,
                      const int *device_ids, int n_devices, unsigned flags, int n_splits,
@@ -405,11 +434,21 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
     int64_t cap = INT32_MAX - 8 * (tiles + 256) - (int64_t{1} << 16);
     if (o.xtile_part_nnz > 0) cap = std::min<int64_t>(cap, o.xtile_part_nnz);
     const int B = n_splits == 0 ? xtile_col_blocks_for(n_rows, n_cols, nnz, tsz, o) : 1;
-    int st;
-    if ((nnz > cap || B > 1) && n_splits == 0 && (tiles + B - 1) / B <= 4096)
-      st = build_parts(p, rp, col_idx, val, tsz, cap, B);
-    else
-      st = xtile_build(p, rp, col_idx, val, tsz);
+    const bool parts = (nnz > cap || B > 1) && n_splits == 0 && (tiles + B - 1) / B <= 4096;
+    // the layout is built on the GPU from uploaded copies of A (byte-identical
+    // to the host build, DESIGN.md §4 device input; C2 0.57 → ≈ 0.15 s); the
+    // host build when the device cannot (aligned segments, no memory)
+    const std::vector<int64_t> splits_in = p->split_rows;  // a build may add cache-range cuts
+    int st = xtile_build_uploaded(p, rp, row_ptr, col_idx, val, tsz, parts, cap, B);
+    if (st == LHPC_ERR_UNSUPPORTED) {
+      p->split_rows = splits_in;
+      for (auto *q : p->parts) lhpc_spmv_plan_destroy(q);
+      p->parts.clear();
+      p->part_row.clear();
+      p->part_col.clear();
+      p->bytes = 0;
+      st = parts ? build_parts(p, rp, col_idx, val, tsz, cap, B) : xtile_build(p, rp, col_idx, val, tsz);
+    }
     if (st == LHPC_OK) {
       *out = p;
       return LHPC_OK;

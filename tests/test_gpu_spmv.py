@@ -692,8 +692,13 @@ def test_xslice_dispatch_past_2p32_work_items(lhpc, gpu):
 def _digests_host_vs_device(lhpc, gpu, rp, col, val, n_cols, flags=0, options=None, splits=None):
     import torch
     kw = dict(flags=flags, options=options, splits=splits)
-    with lhpc.SpMVPlan(rp, col, val, n_cols, **kw) as ph:
+    # the host build (options.xtile_host_build) against the device builds:
+    # from device arrays, and from host arrays uploaded by the library
+    with lhpc.SpMVPlan(rp, col, val, n_cols, flags=flags, splits=splits,
+                       options=dict(options or {}, xtile_host_build=1)) as ph:
         dh, ih = ph.layout_digest(), ph.info()
+    with lhpc.SpMVPlan(rp, col, val, n_cols, **kw) as pu:
+        assert pu.layout_digest() == dh and pu.info() == ih
     drp, dcol, dval = (torch.from_numpy(np.ascontiguousarray(a)).to(gpu) for a in (rp, col, val))
     with lhpc.SpMVPlan(drp, dcol, dval, n_cols, **kw) as pd:
         dd, idev = pd.layout_digest(), pd.info()
