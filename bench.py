@@ -788,12 +788,42 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
             u.view(nzl + 2, P, P)[1:-1, 1:-1, 1:-1] = torch.rand(nzl, n, n, device=dev) * 2 - 1
             o = torch.zeros_like(u)
             import torch.distributed as dist
-            if dist.get_backend() == "nccl" and os.environ.get("LHPC_DIST_TORCH", "0") != "1":
-                # native: lhpc_dist_stencil7_f32 (RCCL send/recv of the halo planes on
-                # the comm stream while the interior planes run)
-                comm = L.DistComm.from_torch(torch.cuda.current_device())
-                fn = lambda: comm.stencil7(u, o, nzl, n, n, 1, -6.0, 1.0, stream=stream)  # noqa: E731
-                how = "native RCCL halo (lhpc_dist_stencil7_f32)"
+            has_rccl = dist.get_backend() == "nccl" and os.environ.get("LHPC_DIST_TORCH", "0") != "1"
+            if has_rccl or os.environ.get("LHPC_DIST_P2P", "0") == "1":
+                # native (lhpc_dist_stencil7_f32_x): the halo planes over RCCL
+                # send/recv on the comm stream, or stored straight into the
+                # neighbours' ghost planes (u a registered P2P window), while
+                # the interior planes run — both timed, the faster reported
+                comm = L.DistComm.from_torch(torch.cuda.current_device()) if has_rccl else \
+                    L.DistComm.local(world, rank, torch.cuda.current_device())
+                kinds = {}
+                if has_rccl:
+                    kinds["rccl"] = L.DIST_EXCHANGE_RCCL
+                try:
+                    comm.p2p_setup_torch(u)
+                    kinds["p2p"] = L.DIST_EXCHANGE_P2P
+                except Exception:  # no IPC between the devices: RCCL only
+                    pass
+                halo_ms = {}
+                for kname, kx in kinds.items():
+                    f = lambda kx=kx: comm.stencil7(u, o, nzl, n, n, 1, -6.0, 1.0, stream=stream,  # noqa: E731
+                                                    exchange=kx)
+                    for _ in range(3):
+                        f()
+                    barrier()
+                    t0 = time.perf_counter()
+                    for _ in range(20):
+                        f()
+                    barrier()
+                    tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                                      device=dev if has_rccl else "cpu")
+                    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                    halo_ms[kname] = float(tt.item()) / 20 * 1e3
+                best = min(halo_ms, key=halo_ms.get)
+                fn = lambda: comm.stencil7(u, o, nzl, n, n, 1, -6.0, 1.0, stream=stream,  # noqa: E731
+                                           exchange=kinds[best])
+                how = (f"native {'RCCL send/recv' if best == 'rccl' else 'P2P peer-store'} halo "
+                       f"(lhpc_dist_stencil7_f32_x; measured ms/step {halo_ms})")
             else:
                 ds = DistStencil7(nzl, n, n, rank, world, lambda ut, ot, zb, ze: L.stencil7_planes(
                     ut, ot, nzl, n, n, 1, -6.0, 1.0, zb, ze, stream=stream))

@@ -714,6 +714,16 @@ int lhpc_dist_p2p_status(const lhpc_dist_comm *comm);
  */
 int lhpc_dist_stencil7_f32(lhpc_dist_comm *comm, float *u, float *out, int64_t nzl, int64_t ny,
                            int64_t nx, int64_t ghost, float c0, float c1, void *stream);
+/* The same step with the halo exchange chosen (enum lhpc_dist_exchange):
+ * RCCL (send/recv, as above) or P2P — u is a registered window on every rank
+ * (lhpc_dist_p2p_export/_import, windows may differ in size: slabs of
+ * different depth) and each rank stores its boundary planes straight into
+ * its neighbours' ghost planes over xGMI, under the READY/DONE flags of the
+ * SpMV windows (neighbours only); the boundary planes wait for the
+ * neighbours' DONE on `stream`.  AUTO: P2P when u is a window, else RCCL.
+ * In a time loop register both ping-pong buffers.                          */
+int lhpc_dist_stencil7_f32_x(lhpc_dist_comm *comm, float *u, float *out, int64_t nzl, int64_t ny,
+                             int64_t nx, int64_t ghost, float c0, float c1, int exchange, void *stream);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -195,10 +195,13 @@ inline std::vector<lhpc_dist_xfer> exchange_schedule(const std::vector<std::int6
 }
 
 // One 7-point step on this rank's z-slab (HPCHighDimensionFlatArray<3,float,ghost>
-// layout of logical (nzl, ny, nx), device buffers), halo planes over RCCL.
+// layout of logical (nzl, ny, nx), device buffers), halo planes over RCCL, or
+// stored into the neighbours' ghost planes when d_u is a registered P2P window
+// (exchange LHPC_DIST_EXCHANGE_AUTO / _RCCL / _P2P; lhpc_dist_stencil7_f32_x).
 inline void dist_stencil7(DistComm &comm, float *d_u, float *d_out, std::int64_t nzl, std::int64_t ny,
-                          std::int64_t nx, std::int64_t ghost, float c0, float c1, void *stream = nullptr) {
-  lhpc::checkLhpc(lhpc_dist_stencil7_f32(comm.native(), d_u, d_out, nzl, ny, nx, ghost, c0, c1, stream));
+                          std::int64_t nx, std::int64_t ghost, float c0, float c1, void *stream = nullptr,
+                          int exchange = LHPC_DIST_EXCHANGE_AUTO) {
+  lhpc::checkLhpc(lhpc_dist_stencil7_f32_x(comm.native(), d_u, d_out, nzl, ny, nx, ghost, c0, c1, exchange, stream));
 }
 
 }  // namespace sparse

@@ -63,7 +63,7 @@ ABI_SYMBOLS = (
     "lhpc_spmv_plan_create_split", "lhpc_spmv_stage", "lhpc_spmv_range",
     "lhpc_dist_get_unique_id", "lhpc_dist_comm_create", "lhpc_dist_comm_info", "lhpc_dist_comm_destroy",
     "lhpc_dist_allreduce_sum_f64", "lhpc_dist_spmv_plan_create", "lhpc_dist_spmv",
-    "lhpc_dist_spmv_plan_destroy", "lhpc_dist_stencil7_f32", "lhpc_dist_comm_create_local",
+    "lhpc_dist_spmv_plan_destroy", "lhpc_dist_stencil7_f32", "lhpc_dist_stencil7_f32_x", "lhpc_dist_comm_create_local",
     "lhpc_dist_p2p_export", "lhpc_dist_p2p_import", "lhpc_dist_p2p_status",
     "lhpc_options_init", "lhpc_spmv_plan_create_opts", "lhpc_blur_x_f32_opts", "lhpc_blur_y_f32_opts",
     "lhpc_stencil7_f32_planes_opts", "lhpc_dist_spmv_plan_create_opts", "lhpc_dist_exchange",
@@ -238,6 +238,7 @@ _sig("lhpc_dist_p2p_reset", _i, _p)
 _sig("lhpc_dist_p2p_unmap", _i, _p, _p)
 _sig("lhpc_dist_spmv_plan_destroy", _i, _p)
 _sig("lhpc_dist_stencil7_f32", _i, _p, _p, _p, _i64, _i64, _i64, _i64, _f, _f, _p)
+_sig("lhpc_dist_stencil7_f32_x", _i, _p, _p, _p, _i64, _i64, _i64, _i64, _f, _f, _i, _p)
 _sig("lhpc_dist_comm_create_local", _i, C.POINTER(_p), _i, _i, _i)
 _sig("lhpc_dist_p2p_export", _i, _p, _p, _i64, _p)
 _sig("lhpc_dist_p2p_import", _i, _p, _p)
@@ -963,13 +964,17 @@ class DistComm:
                "lhpc_dist_allreduce_sum_f64")
         return t
 
-    def stencil7(self, u, out, nzl, ny, nx, ghost=1, c0=-6.0, c1=1.0, stream=None):
-        """One 7-point step on this rank's z-slab, halo planes exchanged over RCCL."""
+    def stencil7(self, u, out, nzl, ny, nx, ghost=1, c0=-6.0, c1=1.0, stream=None, exchange=DIST_EXCHANGE_AUTO):
+        """One 7-point step on this rank's z-slab, halo planes exchanged over
+        RCCL, or stored straight into the neighbours' ghost planes when u is a
+        registered P2P window (lhpc_dist_stencil7_f32_x; exchange AUTO / RCCL /
+        P2P)."""
         if stream is None:
             import torch
             stream = torch.cuda.current_stream(u.device)
-        _check(lib.lhpc_dist_stencil7_f32(self._h, u.data_ptr(), out.data_ptr(), nzl, ny, nx, ghost,
-                                          float(c0), float(c1), _stream_ptr(stream)), "lhpc_dist_stencil7_f32")
+        _check(lib.lhpc_dist_stencil7_f32_x(self._h, u.data_ptr(), out.data_ptr(), nzl, ny, nx, ghost,
+                                            float(c0), float(c1), int(exchange), _stream_ptr(stream)),
+               "lhpc_dist_stencil7_f32_x")
         return out
 
     def close(self):

@@ -63,6 +63,9 @@ struct P2pWindow {
   bool ready = false;               // imported: every peer's copy is mapped
   std::vector<void *> peer_base;    // hipIpcOpenMemHandle results (closed on reset)
   void **d_peer_buf = nullptr;      // [nranks] device table of peer pointers (self: own)
+  std::vector<void *> peer_buf;     // the same pointers on the host
+  std::vector<int64_t> peer_bytes;  // every rank's window size (stencil slabs may differ)
+  int64_t min_bytes = 0;            // the smallest of them
   uint64_t narrow = 0;              // bit p: peer p's y has another 16-B phase → 4-B stores
 };
 
@@ -156,6 +159,16 @@ int build_schedule(const int64_t *cuts, int nranks, int K, int rank, int exchang
   return LHPC_OK;
 }
 
+// The flag allocation (uncached, one IPC handle): READY [0, n) | DONE
+// [n, 2n) | RED [2n, 3n) uint32 flags (n ≤ 64) in the first kFlagBytes, then
+// the scalar slots of the P2P all-gather: double [2 parities][64 ranks][8]
+constexpr size_t kFlagBytes = 1024;
+// uint32 index in the flag allocation of the push kernels' block counters
+// (this rank's only; past READY | DONE | RED at ≤ 3·64): y pushes at
+// kPushCtr, the stencil's two halo transfers at kPushCtr + 1 and + 2
+constexpr int kPushCtr = 192;
+static_assert((kPushCtr + 2) * 4 < static_cast<int>(kFlagBytes), "push counters inside the flag words");
+
 // ---- P2P window kernels.  Every kernel of a call reads the status word
 // first: once a wait has timed out, pushes and DONE flags are skipped (the
 // peers then time out as well), so no rank writes into a peer that never
@@ -187,6 +200,68 @@ __global__ void k_p2p_wait(const uint32_t *flags, int base, uint32_t e, int nran
     __builtin_amdgcn_s_sleep(127);
   }
 }
+// READY to the peers in `mask` only (the stencil's neighbours)
+__global__ void k_p2p_signal_mask(uint32_t *const *peer_flags, int slot, uint32_t e, int nranks, int self,
+                                  uint64_t mask, const uint32_t *status) {
+  const int p = threadIdx.x;
+  if (p2p_failed(status)) return;
+  if (p < nranks && p != self && ((mask >> p) & 1u))
+    __hip_atomic_store(peer_flags[p] + slot, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void k_p2p_wait_mask(const uint32_t *flags, int base, uint32_t e, int nranks, int self, uint64_t mask,
+                                uint32_t *status) {
+  const int p = threadIdx.x;
+  if (p >= nranks || p == self || !((mask >> p) & 1u)) return;
+  for (uint32_t spins = 0;; ++spins) {
+    const uint32_t f = __hip_atomic_load(flags + base + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (static_cast<int32_t>(f - e) >= 0) return;
+    if (spins > (1u << 21) || p2p_failed(status)) {
+      __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(127);
+  }
+}
+
+// Halo planes straight into the neighbours' ghost planes: transfer i =
+// blockIdx.y (≤ 2: down to rank − 1, up to rank + 1) copies bytes[i] from
+// src[i] to dst[i] (a peer's window), 16 B per lane when vec[i], else words;
+// then, as k_p2p_push, the transfer's last block signals DONE = v into that
+// peer's flag nranks + self (its own block counter kPushCtr + 1 + i)
+struct HaloPut {
+  const unsigned char *src[2];
+  unsigned char *dst[2];
+  int64_t bytes[2];
+  int peer[2];
+  int vec[2];
+};
+__global__ __launch_bounds__(256) void k_p2p_halo_put(HaloPut h, const uint32_t *status, uint32_t *flags,
+                                                      uint32_t *const *peer_flags, int nranks, int self, uint32_t v) {
+  const int i = blockIdx.y;
+  if (!p2p_failed(status)) {
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
+                  T = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    if (h.vec[i]) {
+      for (int64_t o = 16 * t; o < h.bytes[i]; o += 16 * T)
+        *reinterpret_cast<uint4 *>(h.dst[i] + o) = *reinterpret_cast<const uint4 *>(h.src[i] + o);
+    } else {
+      for (int64_t o = 4 * t; o < h.bytes[i]; o += 4 * T)
+        *reinterpret_cast<uint32_t *>(h.dst[i] + o) = *reinterpret_cast<const uint32_t *>(h.src[i] + o);
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t *ctr = flags + kPushCtr + 1 + i;
+    if (__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u == gridDim.x) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      if (!p2p_failed(status))
+        __hip_atomic_store(peer_flags[h.peer[i]] + nranks + self, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // the consumer's side of a P2P chunk (compute stream, right before the first
 // read of it): every block waits for every peer's DONE at base + p ≥ e
 // (bounded as k_p2p_wait), then acquires at system scope.  The peers' stores
@@ -197,9 +272,9 @@ __global__ void k_p2p_wait(const uint32_t *flags, int base, uint32_t e, int nran
 // wave slot per CU would cost a concurrent reduce a block per CU).
 constexpr int kP2pAcqBlocks = 16;
 __global__ void k_p2p_wait_acquire(const uint32_t *flags, int base, uint32_t e, int nranks, int self,
-                                   uint32_t *status) {
+                                   uint32_t *status, uint64_t mask) {
   const int p = threadIdx.x;
-  if (p < nranks && p != self) {
+  if (p < nranks && p != self && ((mask >> p) & 1u)) {
     for (uint32_t spins = 0;; ++spins) {
       const uint32_t f = __hip_atomic_load(flags + base + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
       if (static_cast<int32_t>(f - e) >= 0) break;
@@ -214,14 +289,6 @@ __global__ void k_p2p_wait_acquire(const uint32_t *flags, int base, uint32_t e, 
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
-// The flag allocation (uncached, one IPC handle): READY [0, n) | DONE
-// [n, 2n) | RED [2n, 3n) uint32 flags (n ≤ 64) in the first kFlagBytes, then
-// the scalar slots of the P2P all-gather: double [2 parities][64 ranks][8]
-constexpr size_t kFlagBytes = 1024;
-// uint32 index in the flag allocation of the push kernels' block counter
-// (this rank's only; past READY | DONE | RED at ≤ 3·64)
-constexpr int kPushCtr = 192;
-static_assert(kPushCtr * 4 < static_cast<int>(kFlagBytes), "push counter inside the flag words");
 constexpr int kRedMax = 8;
 constexpr size_t kFlagAlloc = kFlagBytes + 2 * 64 * kRedMax * sizeof(double);
 __device__ __forceinline__ double *red_slots(uint32_t *flags) {
@@ -346,7 +413,7 @@ void p2p_release(lhpc_dist_comm *c) {
 // the ready window whose buffer is y, or null
 const P2pWindow *find_window(const lhpc_dist_comm *c, const void *y, size_t need) {
   for (int i = 0; i < c->n_win; ++i)
-    if (c->win[i].ready && c->win[i].buf == y && c->win[i].bytes >= need) return &c->win[i];
+    if (c->win[i].ready && c->win[i].buf == y && c->win[i].min_bytes >= static_cast<int64_t>(need)) return &c->win[i];
   return nullptr;
 }
 
@@ -395,7 +462,7 @@ int p2p_signal_done(lhpc_dist_comm *c, int j) {
 int p2p_wait_chunk(lhpc_dist_comm *c, uint32_t epoch, int j, hipStream_t s) {
   const uint32_t v = epoch * 64u + static_cast<uint32_t>(j) + 1u;
   hipLaunchKernelGGL(k_p2p_wait_acquire, dim3(kP2pAcqBlocks), dim3(64), 0, s, c->flags, c->nranks, v, c->nranks,
-                     c->rank, c->h_status);
+                     c->rank, c->h_status, ~uint64_t{0});
   return static_cast<int>(hipGetLastError());
 }
 
@@ -651,7 +718,7 @@ extern "C" int lhpc_dist_p2p_import(lhpc_dist_comm *c, const unsigned char *blob
   P2pWindow &w = c->win[wi];
   if (w.ready) return LHPC_ERR_INVALID_ARG;  // imported already
   for (int r = 0; r < nr; ++r)
-    if (bl[r].magic != kP2pMagic || bl[r].window != wi || bl[r].nranks != nr || static_cast<size_t>(bl[r].bytes) != w.bytes)
+    if (bl[r].magic != kP2pMagic || bl[r].window != wi || bl[r].nranks != nr || bl[r].bytes <= 0)
       return LHPC_ERR_INVALID_ARG;  // every rank must export the same windows in the same order
   // open everything first; on any failure close what this call opened
   std::vector<void *> pb(static_cast<size_t>(nr), nullptr), pf(static_cast<size_t>(nr), nullptr);
@@ -704,6 +771,13 @@ extern "C" int lhpc_dist_p2p_import(lhpc_dist_comm *c, const unsigned char *blob
   // commit
   w.peer_base = pb;
   w.d_peer_buf = d_buf;
+  w.peer_buf = bufs;
+  w.peer_bytes.assign(static_cast<size_t>(nr), 0);
+  w.min_bytes = INT64_MAX;
+  for (int r = 0; r < nr; ++r) {
+    w.peer_bytes[static_cast<size_t>(r)] = bl[r].bytes;
+    w.min_bytes = std::min<int64_t>(w.min_bytes, bl[r].bytes);
+  }
   w.narrow = narrow;
   w.ready = true;
   if (remap) {
@@ -1181,10 +1255,11 @@ extern "C" int lhpc_dist_spmv_plan_destroy(lhpc_dist_spmv_plan *d) {
   return LHPC_OK;
 }
 
-extern "C" int lhpc_dist_stencil7_f32(lhpc_dist_comm *c, float *u, float *out, int64_t nzl, int64_t ny,
-                                      int64_t nx, int64_t ghost, float c0, float c1, void *stream) {
+extern "C" int lhpc_dist_stencil7_f32_x(lhpc_dist_comm *c, float *u, float *out, int64_t nzl, int64_t ny,
+                                        int64_t nx, int64_t ghost, float c0, float c1, int exchange, void *stream) {
   if (!c || !u || !out || nzl < 1 || ny < 0 || nx < 0 || ghost < 1) return LHPC_ERR_INVALID_ARG;
-  if (!c->comm && c->nranks > 1) return LHPC_ERR_UNSUPPORTED;  // halos travel over RCCL
+  if (exchange != LHPC_DIST_EXCHANGE_AUTO && exchange != LHPC_DIST_EXCHANGE_RCCL && exchange != LHPC_DIST_EXCHANGE_P2P)
+    return LHPC_ERR_INVALID_ARG;
   LHPC_HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t P = (ny + 2 * ghost) * (nx + 2 * ghost);  // padded plane
@@ -1192,10 +1267,67 @@ extern "C" int lhpc_dist_stencil7_f32(lhpc_dist_comm *c, float *u, float *out, i
   const bool lo = c->rank > 0, hi = c->rank < c->nranks - 1;
   lhpc::RocTxRange rx("lhpc_dist_stencil7_f32");
   const bool halo = lo || hi;
+  // the exchange: P2P when u is a registered window (AUTO) or asked for
+  const size_t ubytes = static_cast<size_t>(nzl + 2 * ghost) * static_cast<size_t>(P) * 4;
+  const P2pWindow *w = nullptr;
+  if (halo && exchange != LHPC_DIST_EXCHANGE_RCCL) {
+    for (int i = 0; i < c->n_win && !w; ++i)
+      if (c->win[i].ready && c->win[i].buf == u && c->win[i].bytes >= ubytes) w = &c->win[i];
+    if (!w && exchange == LHPC_DIST_EXCHANGE_P2P) return LHPC_ERR_INVALID_ARG;  // u is not a window
+  }
+  if (halo && !w && !c->comm) return LHPC_ERR_UNSUPPORTED;  // a local communicator has no RCCL
   if (halo) {
-    lhpc::RocTxRange rh("lhpc_dist_stencil7_f32: halo exchange");
     if (!c->ev_in) LHPC_HIP_TRY(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     if (!c->ev_halo) LHPC_HIP_TRY(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
+  }
+  uint64_t mask = 0;
+  if (w) {
+    // READY (epoch) to the neighbours on the compute stream: this rank has
+    // finished every earlier read of u's ghost planes
+    lhpc::RocTxRange rh("lhpc_dist_stencil7_f32: P2P halo");
+    if (*c->h_status) return LHPC_ERR_INTERNAL;  // an earlier flag wait timed out
+    const int64_t pb = P * 4;
+    int64_t nzl_lo = 0;  // the lower neighbour's slab depth, from its window size
+    if (lo) {
+      const int64_t wb = w->peer_bytes[static_cast<size_t>(c->rank - 1)];
+      if (wb % pb || wb / pb - 2 * ghost < 1) return LHPC_ERR_INVALID_ARG;
+      nzl_lo = wb / pb - 2 * ghost;
+    }
+    if (hi && w->peer_bytes[static_cast<size_t>(c->rank + 1)] < (2 * ghost + 1) * pb) return LHPC_ERR_INVALID_ARG;
+    if (lo) mask |= uint64_t{1} << (c->rank - 1);
+    if (hi) mask |= uint64_t{1} << (c->rank + 1);
+    ++c->epoch;
+    if (c->epoch == 0) c->epoch = 1;
+    hipLaunchKernelGGL(k_p2p_signal_mask, dim3(1), dim3(64), 0, s, c->d_peer_flags, c->rank, c->epoch, c->nranks,
+                       c->rank, mask, c->h_status);
+    LHPC_HIP_TRY(hipGetLastError());
+    LHPC_HIP_TRY(hipEventRecord(c->ev_in, s));  // u complete on the caller's stream
+    LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, c->ev_in, 0));
+    hipLaunchKernelGGL(k_p2p_wait_mask, dim3(1), dim3(64), 0, c->s_comm, c->flags, 0, c->epoch, c->nranks, c->rank,
+                       mask, c->h_status);
+    LHPC_HIP_TRY(hipGetLastError());
+    // plane 0 → the lower neighbour's plane nzl_lo (its upper ghost), plane
+    // nzl − 1 → the upper neighbour's plane −1 (its lower ghost)
+    HaloPut h{};
+    int nt = 0;
+    auto add = [&](int peer, const float *src, int64_t dst_off) {
+      h.src[nt] = reinterpret_cast<const unsigned char *>(src);
+      h.dst[nt] = static_cast<unsigned char *>(w->peer_buf[static_cast<size_t>(peer)]) + dst_off;
+      h.bytes[nt] = pb;
+      h.peer[nt] = peer;
+      h.vec[nt] = (reinterpret_cast<uintptr_t>(h.src[nt]) | reinterpret_cast<uintptr_t>(h.dst[nt]) |
+                   static_cast<uintptr_t>(pb)) % 16 == 0;
+      ++nt;
+    };
+    if (lo) add(c->rank - 1, plane(0), (nzl_lo + ghost) * pb);
+    if (hi) add(c->rank + 1, plane(nzl - 1), (ghost - 1) * pb);
+    const unsigned bx = static_cast<unsigned>(std::min<int64_t>(32, (pb / 16 + 255) / 256 + 1));
+    hipLaunchKernelGGL(k_p2p_halo_put, dim3(bx, static_cast<unsigned>(nt)), dim3(256), 0, c->s_comm, h, c->h_status,
+                       c->flags, c->d_peer_flags, c->nranks, c->rank, c->epoch * 64u + 1u);
+    LHPC_HIP_TRY(hipGetLastError());
+    LHPC_HIP_TRY(hipEventRecord(c->ev_halo, c->s_comm));  // this rank's puts issued (u read)
+  } else if (halo) {
+    lhpc::RocTxRange rh("lhpc_dist_stencil7_f32: halo exchange");
     LHPC_HIP_TRY(hipEventRecord(c->ev_in, s));  // u complete on the caller's stream
     LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, c->ev_in, 0));
     LHPC_NCCL_TRY(ncclGroupStart());
@@ -1213,9 +1345,23 @@ extern "C" int lhpc_dist_stencil7_f32(lhpc_dist_comm *c, float *u, float *out, i
   // interior planes need no halo: they run while the planes travel
   int st = LHPC_OK;
   if (nzl > 2) st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, 1, nzl - 1, stream);
-  if (st == LHPC_OK && halo) st = static_cast<int>(hipStreamWaitEvent(s, c->ev_halo, 0));
+  if (st == LHPC_OK && halo) {
+    if (w) {  // the neighbours' planes landed (DONE), stale L2 lines dropped
+      hipLaunchKernelGGL(k_p2p_wait_acquire, dim3(kP2pAcqBlocks), dim3(64), 0, s, c->flags, c->nranks,
+                         c->epoch * 64u + 1u, c->nranks, c->rank, c->h_status, mask);
+      st = static_cast<int>(hipGetLastError());
+    }
+    // RCCL: the received planes; P2P: this rank's own puts, which read u's
+    // boundary planes, end before the caller's next step writes them
+    if (st == LHPC_OK) st = static_cast<int>(hipStreamWaitEvent(s, c->ev_halo, 0));
+  }
   if (st == LHPC_OK) st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, 0, 1, stream);
   if (st == LHPC_OK && nzl > 1)
     st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, nzl - 1, nzl, stream);
   return st;
+}
+
+extern "C" int lhpc_dist_stencil7_f32(lhpc_dist_comm *c, float *u, float *out, int64_t nzl, int64_t ny,
+                                      int64_t nx, int64_t ghost, float c0, float c1, void *stream) {
+  return lhpc_dist_stencil7_f32_x(c, u, out, nzl, ny, nx, ghost, c0, c1, LHPC_DIST_EXCHANGE_AUTO, stream);
 }

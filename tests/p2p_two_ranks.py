@@ -26,6 +26,13 @@ Cases (argv[1]):
   chain     cross-step overlap: five chained lhpc_dist_spmv_begin calls over
             two windows (y of call n is x of call n+1), no end in between —
             each stage's column part waits for the previous call's DONE(j)
+  stencil   the 7-point stencil over z-slabs of uneven depth (37 planes over
+            WORLD_SIZE ranks, ragged 19 × 23 planes), both ping-pong buffers
+            registered windows of different size per rank: six steps of
+            lhpc_dist_stencil7_f32_x with the P2P halo (boundary planes stored
+            into the neighbours' ghost planes, READY/DONE with the neighbours
+            only), no host ordering between steps; each slab equals the
+            single-domain lhpc_stencil7_f32 result bit for bit
 """
 import json
 import os
@@ -259,6 +266,46 @@ elif case == "cg":
         x2 = x2.cpu().numpy()
     out["ok"].append(it1 == it2)
     out["ok"].append(bool(np.array_equal(x1, x2)))
+    dist.barrier()
+    out["status"].append(comm.p2p_status())
+    comm.close()
+elif case == "stencil":
+    from libhpc_amd.dist import slab_bounds
+    nz, ny, nx, steps = 37, 19, 23, 6
+    P = (ny + 2) * (nx + 2)
+    rng = np.random.default_rng(0xE800)
+    full = np.zeros((nz + 2, ny + 2, nx + 2), dtype=np.float32)
+    full[1:-1, 1:-1, 1:-1] = rng.uniform(-1, 1, (nz, ny, nx)).astype(np.float32)
+    # the single-domain reference: the same kernel family on the whole grid
+    ga, gb = torch.from_numpy(full.ravel().copy()).to(dev), torch.zeros(full.size, dtype=torch.float32, device=dev)
+    for _ in range(steps):
+        L.stencil7(ga, gb, nz, ny, nx, 1, -6.0, 1.0)
+        ga, gb = gb, ga
+    torch.cuda.synchronize()
+    want = ga.cpu().numpy().reshape(nz + 2, ny + 2, nx + 2)
+    z0, z1 = slab_bounds(nz, rank, world)
+    nzl = z1 - z0
+    comm = L.DistComm.local(world, rank, 0)
+    ua = torch.from_numpy(full[z0:z1 + 2].ravel().copy()).to(dev)  # slab + both z ghost planes
+    ub = torch.zeros((nzl + 2) * P, dtype=torch.float32, device=dev)
+    if rank > 0:
+        ua[:P] = float("nan")  # inner ghosts: only the neighbour's stores may fill them
+    if rank < world - 1:
+        ua[(nzl + 1) * P:] = float("nan")
+    comm.p2p_setup_torch(ua)
+    comm.p2p_setup_torch(ub)
+    torch.cuda.synchronize()
+    dist.barrier()
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        a, b = ua, ub
+        for _ in range(steps):
+            comm.stencil7(a, b, nzl, ny, nx, 1, -6.0, 1.0, stream=s, exchange=L.DIST_EXCHANGE_P2P)
+            a, b = b, a
+    s.synchronize()
+    got = a.cpu().numpy().reshape(nzl + 2, ny + 2, nx + 2)[1:-1]
+    out["ok"].append(bool(np.array_equal(got, want[z0 + 1:z1 + 1])))
+    out["ok"].append(nzl >= 1)
     dist.barrier()
     out["status"].append(comm.p2p_status())
     comm.close()

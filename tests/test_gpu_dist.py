@@ -196,7 +196,8 @@ def test_dist_stencil7_world1_matches_single_domain(lhpc, gpu, comm, nz, ny, nx)
     assert np.array_equal(od.cpu().numpy(), want)
 
 
-P2P_CASES = {"barrier": 6, "loop": 8, "pingpong": 8, "tiny": 8, "rollback": 4, "reset": 6, "chain": 10, "cg": 3}
+P2P_CASES = {"barrier": 6, "loop": 8, "pingpong": 8, "tiny": 8, "rollback": 4, "reset": 6, "chain": 10, "cg": 3,
+             "stencil": 2, "stencil/3": 2}
 
 
 @pytest.mark.parametrize("case", list(P2P_CASES))
@@ -217,18 +218,23 @@ def test_dist_spmv_p2p_two_ranks_one_gpu(lhpc, gpu, case):
     flags, ping-pong windows, five calls, one end); the distributed CG
     (lhpc_dist_cg_solve, p_work a window, dots all-gathered through the P2P
     scalar slots) at world 2 × K 2 bit-identical to a world-1 × K 4 solve of
-    the same block split, and the P2P all-reduce.  (On one GPU the pushes
-    are device-local; over xGMI they are the same stores.)"""
+    the same block split, and the P2P all-reduce; the stencil's P2P halo
+    over two and three ranks (slabs of different depth, so the middle rank
+    has both neighbours), six ping-pong steps bit-identical to the single
+    domain.  (On one GPU the pushes are device-local; over xGMI they are the
+    same stores.)"""
     import json
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     port = str(29631 + list(P2P_CASES).index(case))
-    env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-    procs = [subprocess.Popen([sys.executable, os.path.join(root, "tests", "p2p_two_ranks.py"), case],
+    name, _, w = case.partition("/")
+    world = int(w or 2)
+    env = dict(os.environ, WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    procs = [subprocess.Popen([sys.executable, os.path.join(root, "tests", "p2p_two_ranks.py"), name],
                               env=dict(env, RANK=str(r), LOCAL_RANK="0"), stdout=subprocess.PIPE,
-                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+                              stderr=subprocess.PIPE, text=True) for r in range(world)]
     outs = []
     try:
         for p in procs:
