@@ -262,6 +262,27 @@ int gpu_mode() {
       if (static_cast<float>(s) != yg(i)) return fail("grid → device CSR → spmv mismatch");
     }
   }
+  // ---- explicit XTILE column blocks through the options (more launches);
+  //      both plans within the 1e-6·Σ|a·x| bound of the fp64 row sums
+  {
+    auto o = sparse::default_options();
+    o.xtile_col_blocks = 3;
+    sparse::SpMVPlan<float> cb(A, -1, LHPC_PLAN_FORCE_XTILE, &o);
+    sparse::SpMVPlan<float> one(A, -1, LHPC_PLAN_FORCE_XTILE);
+    if (cb.info().launches <= one.info().launches) return fail("column blocks: more launches expected");
+    hpc::HPCHighDimensionFlatArray<1, float> y1(n), y3(n);
+    sparse::spmv(one, x, y1);
+    sparse::spmv(cb, x, y3);
+    for (std::int64_t i = 0; i < n; ++i) {
+      double s = 0, a = 0;
+      for (auto k = A.row_ptr[i]; k < A.row_ptr[i + 1]; ++k) {
+        s += double(A.val[k]) * double(x(A.col_idx[k]));
+        a += std::fabs(double(A.val[k]) * double(x(A.col_idx[k])));
+      }
+      if (std::fabs(double(y3(i)) - s) > 1e-6 * a + 1e-30 || std::fabs(double(y1(i)) - s) > 1e-6 * a + 1e-30)
+        return fail("column blocks spmv outside the bound");
+    }
+  }
   std::printf("cpp api gpu: ok (spmv kernel %d)\n", plan.info().kernel);
   return 0;
 }

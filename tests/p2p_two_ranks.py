@@ -20,9 +20,10 @@ Cases (argv[1]):
             windows up again: its P2P calls are bit-exact
   reset     P2P calls, a collective lhpc_dist_p2p_reset (new flag arrays),
             re-export / import (peers' flags remapped by generation), calls
-  cg        lhpc_dist_cg_solve over two ranks (K = 2, p_work a window, dots
-            through the P2P scalar all-gather) equals the world-1 solve with
-            K = 4 (the same four blocks) bit for bit; P2P all-reduce of [r+1]
+  cg        lhpc_dist_cg_solve over WORLD_SIZE ranks (K = 2, p_work a window,
+            dots through the P2P scalar all-gather) equals the world-1 solve
+            with K = 2·WORLD_SIZE (the same blocks) bit for bit; P2P all-reduce
+            of [r+1, 2r]
   chain     cross-step overlap: five chained lhpc_dist_spmv_begin calls over
             two windows (y of call n is x of call n+1), no end in between —
             each stage's column part waits for the previous call's DONE(j)
@@ -243,8 +244,9 @@ elif case == "cg":
     b = torch.from_numpy(np.random.default_rng(0xE700).uniform(-1, 1, n)).to(dev)
     # the one-rank solve of the same four blocks (world-1 local communicator)
     c1 = L.DistComm.local(1, 0, 0)
-    cuts1 = L.interleaved_cuts(rp, 1, 4)
-    with L.DistSpMVPlan(c1, n, n, 4, cuts1, *L.interleaved_local_csr(rp, col, val, cuts1, 1, 4, 0)) as d1:
+    K1 = 2 * world  # the same blocks on one rank
+    cuts1 = L.interleaved_cuts(rp, 1, K1)
+    with L.DistSpMVPlan(c1, n, n, K1, cuts1, *L.interleaved_local_csr(rp, col, val, cuts1, 1, K1, 0)) as d1:
         x1, it1, _ = d1.cg(b, torch.zeros(n, dtype=torch.float64, device=dev), torch.empty(n, dtype=torch.float64,
                                                                                           device=dev), tol=1e-10,
                            max_iter=5000)
@@ -258,7 +260,7 @@ elif case == "cg":
     t = torch.tensor([rank + 1.0, 2.0 * rank], dtype=torch.float64, device=dev)
     comm.allreduce_sum_f64(t, stream=torch.cuda.current_stream(dev))
     torch.cuda.synchronize()
-    out["ok"].append(t.cpu().tolist() == [3.0, 2.0])
+    out["ok"].append(t.cpu().tolist() == [world * (world + 1) / 2.0, world * (world - 1) * 1.0])
     cuts = L.interleaved_cuts(rp, world, 2)
     assert np.array_equal(cuts, cuts1)
     with L.DistSpMVPlan(comm, n, n, 2, cuts, *L.interleaved_local_csr(rp, col, val, cuts, world, 2, rank)) as d:

@@ -197,7 +197,7 @@ def test_dist_stencil7_world1_matches_single_domain(lhpc, gpu, comm, nz, ny, nx)
 
 
 P2P_CASES = {"barrier": 6, "loop": 8, "pingpong": 8, "tiny": 8, "rollback": 4, "reset": 6, "chain": 10, "cg": 3,
-             "stencil": 2, "stencil/3": 2}
+             "stencil": 2, "stencil/3": 2, "pingpong/3": 8, "chain/3": 10, "cg/3": 3}
 
 
 @pytest.mark.parametrize("case", list(P2P_CASES))
@@ -218,8 +218,9 @@ def test_dist_spmv_p2p_two_ranks_one_gpu(lhpc, gpu, case):
     flags, ping-pong windows, five calls, one end); the distributed CG
     (lhpc_dist_cg_solve, p_work a window, dots all-gathered through the P2P
     scalar slots) at world 2 × K 2 bit-identical to a world-1 × K 4 solve of
-    the same block split, and the P2P all-reduce; the stencil's P2P halo
-    over two and three ranks (slabs of different depth, so the middle rank
+    the same block split, and the P2P all-reduce; ping-pong, chained calls
+    and the CG again with three ranks (two peers per rank); the stencil's
+    P2P halo over two and three ranks (slabs of different depth, so the middle rank
     has both neighbours), six ping-pong steps bit-identical to the single
     domain.  (On one GPU the pushes are device-local; over xGMI they are the
     same stores.)"""
