@@ -208,6 +208,9 @@ __device__ uint64_t g_xt_stamps[1 << 22];
 #ifndef LHPC_XT_IP_WAVES
 #define LHPC_XT_IP_WAVES 8  // iperm reduce: 8 waves/SIMD (fp32 66 → 64 VGPRs: C2 593 → 580 µs)
 #endif
+// the reduce keeps the chunk's row offsets in registers (k_xtile_reduce)
+template <typename T> constexpr bool xt_rreg(int G) { return std::is_same<T, float>::value && G == 2; }
+
 // AL (iperm only): aligned segments (lhpc_plan.hpp build_xtile unit > 1) —
 // every segment starts on a 16-B boundary and spans whole 16-B units of VW
 // positions, so phase A ranks units instead of positions (M/VW ≤ 64 batches
@@ -231,7 +234,16 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   static_assert(!AL || NBU * (BLK / kWave) <= kWave, "AL: a chunk's unit batches fit one wave's lanes");
   // dynamic LDS (xtile_lds_bytes): xs[M + VW] T (slot M is the sentinel's
   // spare), bt[BLK/64][NB] u32x4, ws[BLK/64] f64, wsf[BLK/64] i32, bm[M/32]
-  // u32, sbm[M/32] u32, rpl[RMAX+1] u16 (padded to 4 B), base_ne[S] i32, wsum[8] i32
+  // u32, sbm[M/32] u32, rfirst[RPT][BLK/64] u16 (padded to 4 B), rlast i32,
+  // base_ne[S] i32, wsum[8] i32.  RREG (fp32 G = 2, 476–1024 tiles): the
+  // chunk's local row offsets stay in the threads' registers (rt[q] = row
+  // q·BLK + tid) and the y store takes row j+1's from lane + 1, or from
+  // rfirst for a wave's last lane — 56 B of LDS instead of rpl[RMAX+1] u16
+  // (2 KB), so the fp32 reduce keeps 4 blocks per CU up to ≈ 970 tiles
+  // instead of ≈ 470 (same box: n = 30M +1.1%, 80M +3.3%).  Only fp32 G = 2
+  // gains: G = 1 plans (C2) keep rpl in LDS (the register form cost C2
+  // 0.8%), and past 1024 tiles base_ne alone exceeds the 4-block budget.
+  constexpr bool RREG = xt_rreg<T>(G);
   extern __shared__ __align__(16) unsigned char smem[];
   T *xs = reinterpret_cast<T *>(smem);
   u32x4 *bt0 = reinterpret_cast<u32x4 *>(xs + M + VW);
@@ -239,8 +251,11 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   int *wsf = reinterpret_cast<int *>(ws + BLK / kWave);
   uint32_t *bm = reinterpret_cast<uint32_t *>(wsf + BLK / kWave);
   uint32_t *sbm = bm + M / 32;
-  uint16_t *rpl = reinterpret_cast<uint16_t *>(sbm + M / 32);
-  int32_t *base_ne = reinterpret_cast<int32_t *>(rpl + ((RMAX + 2) & ~1));
+  constexpr int NW = BLK / kWave;
+  uint16_t *rpl = reinterpret_cast<uint16_t *>(sbm + M / 32);  // !RREG: rpl[RMAX + 1]
+  uint16_t *rfirst = rpl;                                       // RREG: rfirst[RPT][NW]
+  int32_t *rlast = reinterpret_cast<int32_t *>(rfirst + ((RPT * NW + 1) & ~1));
+  int32_t *base_ne = RREG ? rlast + 1 : reinterpret_cast<int32_t *>(rpl + ((RMAX + 2) & ~1));
   int32_t *wsum = base_ne + S;
 
   const int tid = threadIdx.x;
@@ -504,12 +519,20 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     for (int u = 0; u < NB; ++u) xs[pv[u]] = xv[u];
   }
   LHPC_XT_STAMP(4, 0)
-  // row_ptr (round trip 2) → local row offsets and the row-start bitmap
+  // row_ptr (round trip 2) → local row offsets (registers; a wave's first in
+  // rfirst, row R's in rlast) and the row-start bitmap
+  int rt[RPT];
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
     const int j = q * BLK + tid;
     rv[q] -= e0;
-    if (j <= R) rpl[j] = static_cast<uint16_t>(rv[q] <= m ? rv[q] : m + 1);  // > m: continues
+    rt[q] = rv[q] <= m ? rv[q] : m + 1;  // > m: continues (rows past R repeat row R's)
+    if constexpr (RREG) {
+      if (lane == 0) rfirst[q * NW + wv] = static_cast<uint16_t>(rt[q]);
+      if (j == R) *rlast = rt[q];
+    } else {
+      if (j <= R) rpl[j] = static_cast<uint16_t>(rt[q]);
+    }
     if (j < R && rv[q] < m) atomicOr(bm + (rv[q] >> 5), 1u << (rv[q] & 31));  // empty rows share a bit
   }
   const int n = m - i0 < RUN ? (m - i0 > 0 ? m - i0 : 0) : RUN;  // valid entries in the run
@@ -565,7 +588,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
 #pragma unroll
   for (int q = 0; q < NV; ++q) xr[q ^ swz] = xq[q];
   const bool has_head = n > 0 && !(mask & 1u);
-  const bool cont = rpl[R] > m;  // the row active at m−1 runs past the chunk
+  const bool cont = (RREG ? *rlast : static_cast<int>(rpl[R])) > m;  // the row active at m−1 runs past the chunk
   // ---- rows that cross runs: segmented scan over threads (run order) of
   //      x(t) = tail piece if run t holds a row start, else its whole-run sum;
   //      the row open when run t begins is the exclusive value S(t−1)
@@ -589,7 +612,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   const double oin = dpp_f64_old<kShr1>(cw, sv);                                 // S(t−1)
   const int fin = __builtin_amdgcn_update_dpp(gw, fin_incl, kShr1, 0xF, 0xF, false);  // starts before run t
   const int tlast = m > 0 ? (m - 1) / RUN : -1;
-  if (tid == 0 && !(m > 0 && rpl[0] > 0)) carry[2 * c] = 0.0;  // no head piece
+  if (tid == 0 && !(m > 0 && (RREG ? rt[0] : static_cast<int>(rpl[0])) > 0)) carry[2 * c] = 0.0;  // no head piece
   if (has_head) {
     const int i1 = i0 + n;
     const bool end_i1 = i1 < m ? ((bm[i1 >> 5] >> (i1 & 31)) & 1u) != 0 : !cont;
@@ -611,13 +634,33 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   // coalesced y store of the owned rows from their last positions (a row
   // continuing past the chunk is stored by k_xtile_fixup, later on the stream)
   // (y_add: a column block after the first adds its sums; empty rows keep y)
-  for (int j = tid; j < R; j += BLK) {
-    const int a0 = rpl[j], a1 = rpl[j + 1];
-    if (a1 == a0) {
-      if (!y_add) y[r0 + j] = T(0);
-    } else if (a1 <= m) {
-      const T v = xs[xt_slot<T>(a1 - 1)];
-      y[r0 + j] = y_add ? static_cast<T>(static_cast<double>(y[r0 + j]) + static_cast<double>(v)) : v;
+  if constexpr (RREG) {
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int j = q * BLK + tid;
+      // row j + 1's offset: lane + 1's register (every lane shuffles), the
+      // next wave's first (rfirst) for a wave's last lane; j < R keeps q + 1 < RPT
+      int a1 = __shfl_down(rt[q], 1, kWave);
+      if (lane == kWave - 1) a1 = wv + 1 < NW ? rfirst[q * NW + wv + 1] : (q + 1 < RPT ? rfirst[(q + 1) * NW] : 0);
+      if (j < R) {
+        const int a0 = rt[q];
+        if (a1 == a0) {
+          if (!y_add) y[r0 + j] = T(0);
+        } else if (a1 <= m) {
+          const T v = xs[xt_slot<T>(a1 - 1)];
+          y[r0 + j] = y_add ? static_cast<T>(static_cast<double>(y[r0 + j]) + static_cast<double>(v)) : v;
+        }
+      }
+    }
+  } else {
+    for (int j = tid; j < R; j += BLK) {
+      const int a0 = rpl[j], a1 = rpl[j + 1];
+      if (a1 == a0) {
+        if (!y_add) y[r0 + j] = T(0);
+      } else if (a1 <= m) {
+        const T v = xs[xt_slot<T>(a1 - 1)];
+        y[r0 + j] = y_add ? static_cast<T>(static_cast<double>(y[r0 + j]) + static_cast<double>(v)) : v;
+      }
     }
   }
   LHPC_XT_STAMP(8, 0)
@@ -642,23 +685,34 @@ __global__ __launch_bounds__(kXtFixBlock) void k_xtile_fixup(
 }
 
 // ------------------------------------------------------------ launchers
-template <typename T>
-size_t xtile_lds_bytes(int S) {
-  constexpr int BLK = xt_red_blk<T>(), M = XtRed<T, BLK>::M, RMAX = XtRed<T, BLK>::Rmax, W = BLK / kWave;
-  return static_cast<size_t>(M + 16 / sizeof(T)) * sizeof(T) + W * xt_run<T>() * 16 + W * (sizeof(double) + 4) +
-         2 * M / 32 * sizeof(uint32_t) + ((RMAX + 2) & ~1) * sizeof(uint16_t) +
-         sizeof(int32_t) * (static_cast<size_t>(S) + 8);
-}
-
 // segment-table entries per reduce thread: G = ⌈S / BLK⌉ rounded up to a
 // power of two.  build_xtile caps S at kXtMaxTiles = 4096, so G ≤ 8 for fp32
 // (BLK 512) and ≤ 4 for fp64 (BLK 1024); only those are instantiated (a G = 16
 // form spilled and could never be selected)
 template <typename T> constexpr int xt_gmax() { return 4096 / xt_red_blk<T>(); }
 template <typename T>
+size_t xtile_lds_bytes_g(int S, int g) {
+  constexpr int BLK = xt_red_blk<T>(), M = XtRed<T, BLK>::M, RMAX = XtRed<T, BLK>::Rmax, W = BLK / kWave;
+  constexpr int RPT = (RMAX + 1 + BLK - 1) / BLK;
+  const size_t rows = xt_rreg<T>(g) ? ((RPT * W + 1) & ~1) * sizeof(uint16_t) + sizeof(int32_t)  // rfirst, rlast
+                                    : ((RMAX + 2) & ~1) * sizeof(uint16_t);                     // rpl
+  return static_cast<size_t>(M + 16 / sizeof(T)) * sizeof(T) + W * xt_run<T>() * 16 + W * (sizeof(double) + 4) +
+         2 * M / 32 * sizeof(uint32_t) + rows + sizeof(int32_t) * (static_cast<size_t>(S) + 8);
+}
+// a G = 1 plan whose rpl pushes the reduce past 4 blocks per CU (160 KB / 4
+// of LDS; fp32 S ≈ 476–512) takes the G = 2 form, whose row offsets live in
+// registers, when that one fits
+constexpr size_t kXtLds4 = 160 * 1024 / 4;
+template <typename T>
 int xtile_g(int S) {
   const int g = (S + xt_red_blk<T>() - 1) / xt_red_blk<T>();
-  return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : 8;
+  if (g <= 1)
+    return xt_rreg<T>(2) && xtile_lds_bytes_g<T>(S, 1) > kXtLds4 && xtile_lds_bytes_g<T>(S, 2) <= kXtLds4 ? 2 : 1;
+  return g <= 2 ? 2 : g <= 4 ? 4 : 8;
+}
+template <typename T>
+size_t xtile_lds_bytes(int S) {
+  return xtile_lds_bytes_g<T>(S, xtile_g<T>(S));
 }
 
 template <typename T, int G, bool IP, bool AL>

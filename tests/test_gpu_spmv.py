@@ -187,6 +187,32 @@ def test_xtile_large_n_80m(lhpc, gpu, blocks):
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("n,tiles", [(20_000_000, (476, 512)), (30_000_000, (513, 1024))])
+def test_xtile_register_row_offsets(lhpc, gpu, n, tiles):
+    """The fp32 reduce's G = 2 form keeps a chunk's row offsets in registers
+    (lhpc_spmv_xtile.hip xt_rreg): n = 30M runs it for its 733 tiles; n = 20M
+    (489 tiles, G = 1 by count) is moved onto it because the LDS row-offset
+    array would cost a block per CU (xtile_g).  15 uniform nonzeros per row,
+    dyadic values: 10^5 sampled rows bit-exact against fp64 numpy, and run to
+    run determinism on the whole y."""
+    import torch
+    rp, col, val = lhpc.gen_uniform_csr(n, n, 15, dtype=lhpc.F32, dist=1, seed=0x7000)
+    x = lhpc.gen_values(lhpc.F32, 1, n, 0x7001)
+    with lhpc.SpMVPlan(rp, col, val, n) as plan:
+        info = plan.info()
+        assert info["kernel"] == lhpc.KERNEL_XTILE and tiles[0] <= info["slices"] <= tiles[1]
+        xd = torch.from_numpy(x).to(gpu)
+        y1 = plan(xd).clone()
+        y2 = plan(xd)
+        torch.cuda.synchronize()
+        assert torch.equal(y1, y2)
+        y = y1.cpu().numpy()
+        del xd, y1, y2
+    rows, y64, _ = S.sampled_rows_fp64(rp, col, val, x, 100_000)
+    assert np.array_equal(y[rows].astype(np.float64), y64)
+
+
+@pytest.mark.slow
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
 def test_full_size_c4(lhpc, gpu, dtype):
     """BASELINE configs[3] (C4) at full size, as bench.py --workload c4 builds
