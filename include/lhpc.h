@@ -470,7 +470,8 @@ int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
  * solve keeps its work (4 vectors + scalars) with the plan, and on a
  * non-null stream with check_every ≥ 4 and an ADAPTIVE plan it replays the
  * check_every iterations between two checks as a captured HIP graph, also
- * kept with the plan (results bit-identical to the loop).
+ * kept with the plan (results bit-identical to the loop).  So one plan
+ * serves one solve at a time: concurrent solves need a plan each.
  * Building blocks for multi-GPU composition (all asynchronous on `stream`,
  * scalars are fp64 HBM pointers, read on the device):
  *   lhpc_vec_dot     *out = a·b
