@@ -171,6 +171,45 @@ def test_dist_cg_hip_ops_world1(lhpc, gpu):
     assert torch.linalg.norm(x[:n] - x1) <= 1e-8 * torch.linalg.norm(x1)
 
 
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+@pytest.mark.parametrize("maxlen", [0, 1, 5, 9])
+def test_adaptive_short_rows(lhpc, gpu, dt, maxlen):
+    """ADAPTIVE blocks of short rows (≤ 256 rows of ≤ 2048 nonzeros per
+    block, lhpc_spmv_csr.hip csr_build_blocks; 512-row blocks measured slower,
+    DESIGN.md §4): rows of 0..maxlen nonzeros (maxlen 0: an all-empty
+    matrix), dyadic values, y bit-exact against the oracle through lhpc_spmv
+    and lhpc_spmv_dot, and the fused dot within 1e-12·Σ|w·y| of numpy on the
+    stored y."""
+    import torch
+    n = 300_001
+    rng = np.random.default_rng(0xAD + maxlen)
+    lens = rng.integers(0, maxlen + 1, size=n)
+    rp = np.zeros(n + 1, dtype=np.int32)
+    np.cumsum(lens, out=rp[1:])
+    nnz = int(rp[-1])
+    col = rng.integers(0, n, size=nnz).astype(np.int32)
+    val = (rng.integers(-8, 9, size=nnz) / 8.0).astype(dt)
+    xh = (rng.integers(-8, 9, size=n) / 8.0).astype(dt)
+    wh = (rng.integers(-8, 9, size=n) / 4.0).astype(dt)
+    want = S.spmv_oracle(rp, col, val, xh)[1]
+    x, w = _dev(gpu, xh), _dev(gpu, wh)
+    with lhpc.SpMVPlan(rp, col, val, n, flags=lhpc.PLAN_FORCE_ADAPTIVE) as plan:
+        info = plan.info()
+        assert info["kernel"] == lhpc.KERNEL_ADAPTIVE
+        if maxlen and maxlen <= 5:  # ≤ 2048 / 256 nonzeros per row on average: 256-row blocks
+            assert info["n_blocks"] == -(-n // 256)
+        y0 = plan(x)
+        y = torch.full_like(y0, float("nan"))
+        out = torch.zeros(1, dtype=torch.float64, device=gpu)
+        lhpc.spmv_dot(plan, x, y, w, out)
+        torch.cuda.synchronize()
+        assert torch.equal(y, y0)
+        yh = y.cpu().numpy()
+        assert np.array_equal(yh, want)
+        yw = yh.astype(np.float64) * wh.astype(np.float64)
+        assert abs(out.item() - yw.sum()) <= 1e-12 * max(np.abs(yw).sum(), 1e-300)
+
+
 @pytest.mark.parametrize("flags", [0, 1 << 4, 1 << 6])
 @pytest.mark.parametrize("dt", [np.float64, np.float32])
 def test_spmv_dot(lhpc, gpu, flags, dt):
