@@ -2,7 +2,9 @@
 the code objects inside liblhpc.so (no GPU needed): no kernel spills to
 scratch, and the hot kernels keep the occupancy their design assumes
 (DESIGN.md §4).  The kernels' metadata come from the AMDHSA notes of each
-translation unit's offload bundle (llvm-readelf --notes)."""
+translation unit's offload bundle (llvm-readelf --notes).  The library is
+built with compressed bundles (hipcc --offload-compress: "CCOB" header, zstd),
+which clang-offload-bundler unpacks; plain bundles are read directly."""
 import os
 import re
 import struct
@@ -15,11 +17,35 @@ from tests._support import ROOT
 
 LIB = os.path.join(ROOT, "libhpc_amd", "_lib", "liblhpc.so")
 READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+BUNDLER = "/opt/rocm/lib/llvm/bin/clang-offload-bundler"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+CMAGIC = b"CCOB"
+TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
 
 
-def _gfx950_objects(path):
+def _compressed_objects(data, td):
+    """gfx950 code objects of the compressed bundles: header magic, u16
+    version, u16 method, then (version ≥ 3) u64 total size, u64 uncompressed
+    size, u64 hash; version 2 has u32 sizes"""
+    objs, i = [], data.find(CMAGIC)
+    while i >= 0:
+        ver = struct.unpack_from("<H", data, i + 4)[0]
+        tot = struct.unpack_from("<Q" if ver >= 3 else "<I", data, i + 8)[0]
+        src, dst = os.path.join(td, f"b{i}.bin"), os.path.join(td, f"b{i}.co")
+        open(src, "wb").write(data[i:i + tot])
+        if TARGET in subprocess.run([BUNDLER, "--list", "--type=o", f"--input={src}"], capture_output=True,
+                                    text=True, check=True).stdout:
+            subprocess.run([BUNDLER, "--unbundle", "--type=o", f"--targets={TARGET}", f"--input={src}",
+                            f"--output={dst}"], check=True)
+            objs.append(open(dst, "rb").read())
+        i = data.find(CMAGIC, i + tot)
+    return objs
+
+
+def _gfx950_objects(path, td):
     data = open(path, "rb").read()
+    if data.find(CMAGIC) >= 0 and data.find(MAGIC) < 0:
+        return _compressed_objects(data, td)
     objs, i = [], data.find(MAGIC)
     while i >= 0:
         n = struct.unpack_from("<Q", data, i + len(MAGIC))[0]
@@ -39,7 +65,7 @@ def kernels(path=LIB):
     """name → {vgpr_count, vgpr_spill_count, sgpr_spill_count, private_segment_fixed_size}"""
     out = {}
     with tempfile.TemporaryDirectory() as td:
-        for k, blob in enumerate(_gfx950_objects(path)):
+        for k, blob in enumerate(_gfx950_objects(path, td)):
             f = os.path.join(td, f"co{k}.elf")
             open(f, "wb").write(blob)
             notes = subprocess.run([READELF, "--notes", f], capture_output=True, text=True, check=True).stdout
@@ -57,8 +83,8 @@ def kernels(path=LIB):
 
 @pytest.fixture(scope="module")
 def ks():
-    if not os.path.exists(READELF) or not os.path.exists(LIB):
-        pytest.skip("llvm-readelf or the built library not available")
+    if not os.path.exists(READELF) or not os.path.exists(BUNDLER) or not os.path.exists(LIB):
+        pytest.skip("llvm-readelf / clang-offload-bundler or the built library not available")
     k = kernels()
     assert len(k) > 40, "expected the product kernels in the code objects"
     return k
