@@ -40,8 +40,11 @@ timed events); cpu_baseline = the reference's own CPU radix sort
 
 --workload cg: conjugate gradient on the 4096² 2-D
 Laplacian in fp64 (16.8M rows, 83.9M nnz); a step = one CG iteration
-(SpMV + 2 all-reduced dots + the fused vector updates); N>1 runs DistCG
-(row blocks, RCCL all-reduce of the dots, all-gather of p).
+(SpMV + 2 all-reduced dots + the fused vector updates).  N=1 runs the
+native lhpc_cg_solve (10-iteration blocks replayed as HIP graphs); N>1 over
+RCCL runs the native lhpc_dist_cg_solve (K chunks per rank, p's exchange
+chained into the next q = A·p), and the torch.distributed DistCG only under
+gloo or LHPC_DIST_TORCH=1.
 """
 import argparse
 import json
