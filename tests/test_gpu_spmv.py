@@ -189,21 +189,22 @@ def test_xtile_large_n_80m(lhpc, gpu, blocks):
 @pytest.mark.parametrize("n_cols,dtype,tiles", [(19_040_000, "f32", 465), (20_000_000, "f32", 512),
                                                 (30_000_000, "f32", 768), (45_000_000, "f32", 550),
                                                 (15_000_000, "f64", 733)])
-def test_xtile_reduce_forms_wide_x(lhpc, gpu, n_cols, dtype, tiles):
+def test_xtile_reduce_forms_wide_x(lhpc, gpu, n_cols, dtype, tiles, xt_layout):
     """The reduce forms picked by the tile count (lhpc_spmv_xtile.hip
     xtile_g): 200K rows × 15 uniform nonzeros over an x of n_cols columns.
     fp32: 465 tiles (G = 1, row offsets in LDS, 4 blocks per CU; too few to
     be widened to 512), 512 (20M columns widened to a multiple of the CUs;
     G = 1 by count, moved to the G = 2 register form by the LDS budget), 768
     (G = 2), 45M columns as two column blocks of 550 tiles (G = 2, the second
-    adding into y); fp64 733 tiles (G = 1, BLK 1024).  Small nnz, so the
-    whole y is checked: dyadic values, bit-exact against the oracle."""
+    adding into y); fp64 733 tiles (G = 1, BLK 1024) — each over the three
+    reduce layouts (perm, iperm, iperm over aligned segments).  Small nnz, so
+    the whole y is checked: dyadic values, bit-exact against the oracle."""
     import torch
     dt = lhpc.F32 if dtype == "f32" else lhpc.F64
     n = 200_000
     rp, col, val = lhpc.gen_uniform_csr(n, n_cols, 15, dtype=dt, dist=1, seed=0x7100 + n_cols % 977)
     x = lhpc.gen_values(dt, 1, n_cols, 0x7101)
-    with lhpc.SpMVPlan(rp, col, val, n_cols) as plan:
+    with lhpc.SpMVPlan(rp, col, val, n_cols, options=xt_layout) as plan:
         info = plan.info()
         assert info["kernel"] == lhpc.KERNEL_XTILE and info["slices"] == tiles, info
         y = plan(torch.from_numpy(x).to(gpu)).cpu().numpy()
