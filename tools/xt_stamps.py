@@ -1,6 +1,7 @@
 """Phase timing of the XTILE reduce from in-kernel stamps (diagnostic build:
-make EXTRA_HIPFLAGS=-DLHPC_XT_STAMPS into libhpc_amd/_ab/stamps/, loaded with
-LHPC_LIB_PATH).  One SpMV after warm-up; per block: s_memtime deltas between
+make -C libhpc_amd/csrc BUILD=../_build_stamps OUT=../_lib_stamps
+EXTRA_HIPFLAGS=-DLHPC_XT_STAMPS ../_lib_stamps/liblhpc.so — not under _ab/,
+which gpurun does not send — loaded with LHPC_LIB_PATH).  One SpMV after warm-up; per block: s_memtime deltas between
 the phase boundaries of k_xtile_reduce (thread 0 of each block), and the
 realtime span.  Prints JSON: median / mean / p90 per phase in cycles."""
 import ctypes as C
