@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 
@@ -305,20 +306,27 @@ struct HostStage {
   hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 16); }
 };
 
-// resident downsweep blocks on this device (CUs × blocks per CU), cached per kernel
+// resident downsweep blocks on the current device (CUs × blocks per CU),
+// cached per kernel and device (relaxed atomics: racing threads compute the
+// same value)
 template <typename K, bool HAS_V, int IPT, bool PF>
 int64_t sort_grid_cap() {
-  static int64_t cap = 0;
-  if (!cap) {
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT, PF>, kSortThreads, 0) !=
-            hipSuccess ||
-        cus <= 0 || per_cu <= 0)
-      return kSortMaxResident;
-    cap = std::min<int64_t>(kSortMaxResident, int64_t{cus} * per_cu);
+  static std::atomic<int64_t> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return kSortMaxResident;
+  std::atomic<int64_t> *slot = dev >= 0 && dev < 64 ? &cache[dev] : nullptr;
+  if (slot) {
+    const int64_t c = slot->load(std::memory_order_relaxed);
+    if (c > 0) return c;
   }
+  int cus = 0, per_cu = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT, PF>, kSortThreads, 0) !=
+          hipSuccess ||
+      cus <= 0 || per_cu <= 0)
+    return kSortMaxResident;
+  const int64_t cap = std::min<int64_t>(kSortMaxResident, int64_t{cus} * per_cu);
+  if (slot) slot->store(cap, std::memory_order_relaxed);
   return cap;
 }
 
