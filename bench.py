@@ -4,7 +4,10 @@
 
 N=1: BASELINE configs[1] — CSR SpMV, n=10M, nnz=150M (exactly 15 uniform
 distinct sorted columns per row), fp32 values/x/y, A and x resident in HBM.
-N>1 (launched by torch.distributed.run, one rank per GPU): the SAME matrix is
+N>1 (one rank per GPU; `python bench.py --gpus N` without a launcher starts
+torch.distributed.run with N ranks itself, as a child process, and refuses
+when N disagrees with the launcher's WORLD_SIZE or exceeds the visible GPUs
+outside the LHPC_DIST_BACKEND=gloo rehearsal — launch_decision): the SAME matrix is
 split into N·K nnz-balanced interleaved row blocks, K = --chunks per rank
 (strong scaling); a step is the rank's local SpMV plus the y exchange over
 xGMI that makes y the next x, chunk k's exchange overlapping chunk k+1's
@@ -105,6 +108,8 @@ def parse():
                          "K = 1, 2, 4 and reports the fastest (the step model, tools/step_model.py, puts K = 4 "
                          "first at 64 GB/s per xGMI link, DESIGN.md §6.3); other paths use 4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-alt-kernels", action="store_true",
+                    help="skip the other kernel families' C2-C4 times (alt_kernels: ADAPTIVE, ROWGROUP, XSLICE)")
     ap.add_argument("--spmv-options", default=None,
                     help="JSON dict of lhpc_options fields for the 1-GPU SpMV plan (measured alternatives, DESIGN.md §4)")
     ap.add_argument("--dtype", default="auto", choices=["auto", "f32", "f64"],
@@ -134,17 +139,59 @@ def load_traffic(kernel_tag):
         return None
 
 
+def launch_decision(gpus, env, visible, argv, port=0):
+    """What `bench.py --gpus N` does in this process, decided before any GPU
+    call:  ("run", None) — this process is a rank (or N = 1);
+    ("spawn", cmd) — N > 1 with no launcher: start torch.distributed.run with
+    N ranks as a CHILD process running the same arguments (never exec: the
+    parent has imported torch); ("refuse", message) — N disagrees with the
+    launcher's WORLD_SIZE, or N exceeds the visible GPUs outside the gloo
+    rehearsal (LHPC_DIST_BACKEND=gloo: ranks may share a GPU)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            return "refuse", f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={ws} ranks"
+        return "run", None
+    if gpus <= 1:
+        return "run", None
+    if gpus > visible and env.get("LHPC_DIST_BACKEND", "nccl") != "gloo":
+        return "refuse", (f"bench.py: --gpus {gpus} but {visible} GPU(s) visible; one rank per GPU "
+                          "(set LHPC_DIST_BACKEND=gloo to rehearse ranks sharing a GPU)")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py")] + list(argv)
+    return "spawn", cmd
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def main():
     args = parse()
     import torch
+    # N > 1 without a launcher: N ranks through torch.distributed.run, as a
+    # child process (device_count() does not initialise the GPU on this image)
+    action, what = launch_decision(args.gpus, os.environ, torch.cuda.device_count(), sys.argv[1:], free_port())
+    if action == "refuse":
+        print(what, file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    if action == "spawn":
+        import subprocess
+        env = dict(os.environ)
+        if env.get("LHPC_DIST_BACKEND") == "gloo":
+            env.setdefault("LHPC_DIST_P2P", "1")  # the native peer-store path, as on a node
+        print(f"bench.py: --gpus {args.gpus}: {' '.join(what)}", file=sys.stderr, flush=True)
+        rc = subprocess.run(what, env=env).returncode  # rank 0 prints the JSON line to our stdout
+        raise SystemExit(rc)
     import torch.distributed as dist
     import libhpc_amd as L
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # one rank per GPU; the modulo only matters for the 1-GPU rehearsal of the
     # N>1 path (LHPC_DIST_BACKEND=gloo, ranks sharing cuda:0) — identity on a full node
     local = local % max(1, torch.cuda.device_count())
@@ -594,6 +641,8 @@ def main():
             lay = result["roofline"].get("layout")
             moved = lay["stream_bytes_per_call"] if lay else local_alg
             result["roofline"]["copy"] = copy_ceiling(L, torch, dev, stream, int(moved), moved / call_s / 1e9)
+        if rank == 0 and world == 1 and not native_dist and not args.no_alt_kernels and wl in ("c2", "c3", "c4"):
+            result["alt_kernels"] = alt_kernels(L, torch, dev, stream, rp, col, val, xd, n, nnz, args)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_spmv_baseline(rp, col, val, x, nnz, args.cpu_seconds,
                                                        threads=1 if wl == "c1" else None)
@@ -619,6 +668,42 @@ def main():
         dist.destroy_process_group()
 
 
+def alt_kernels(L, torch, dev, stream, rp, col, val, xd, n, nnz, args):
+    """The same matrix through the other kernel families, each forced by its
+    plan flag and timed like the headline call (HIP events over 10 calls on
+    the bench stream): ADAPTIVE and ROWGROUP are the wavefront-per-row CSR
+    kernels BASELINE configs[1] names (report both), XSLICE the
+    column-sliced one.  Reported beside the default (XTILE), not as `value`."""
+    out = {}
+    flags = {"adaptive": L.PLAN_FORCE_ADAPTIVE, "rowgroup": L.PLAN_FORCE_ROWGROUP, "xslice": L.PLAN_FORCE_XSLICE}
+    y = torch.empty(n, dtype=xd.dtype, device=dev)
+    for name, fl in flags.items():
+        try:
+            t0 = time.time()
+            pl = L.SpMVPlan(rp, col, val, n, flags=fl)
+            t_plan = time.time() - t0
+        except L.LhpcError as e:
+            out[name] = {"error": str(e)}
+            continue
+        for _ in range(3):
+            pl(xd, y, stream=stream)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(10):
+            pl(xd, y, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) * 1e-3 / 10
+        kern = {L.KERNEL_XSLICE: "xslice", L.KERNEL_ROWGROUP: "rowgroup", L.KERNEL_ADAPTIVE: "adaptive",
+                L.KERNEL_XTILE: "xtile"}[pl.info()["kernel"]]
+        pl.close()
+        out[name] = {"gflops": 2.0 * nnz / t / 1e9, "call_us": t * 1e6, "kernel": kern, "plan_s": t_plan}
+    del y
+    torch.cuda.empty_cache()
+    return out
+
+
 def probe_lib_path(L):
     """liblhpc_probe.so (measurement kernels, not on the ABI): next to the
     loaded liblhpc.so, else the in-tree build (A/B builds ship only liblhpc.so)."""
@@ -627,38 +712,57 @@ def probe_lib_path(L):
 
 
 def copy_ceiling(L, torch, dev, stream, nbytes, achieved_gbps):
-    """Attainable read+write rate for the same bytes (report a
-    measured copy bandwidth beside the 8 TB/s peak), timed live on the bench
-    stream: grid-stride non-temporal copies moving nbytes/2 in and nbytes/2
-    out, at 8 B/lane (the best copy probe measured, tools/probe_copy.py) and
-    16 B/lane (SURVEY §8d's `stall_lg_coalesced_256_best` idiom,
-    cuda_tut_stall_lg.cu:63-71).  `copy` is the faster of the two; `frac`
-    puts achieved_gbps against it."""
+    """Attainable rates for the same bytes (a measured copy
+    bandwidth beside the 8 TB/s peak), timed live on the bench stream with the
+    probes of liblhpc_probe.so (not on the ABI):
+      copy  a 16-B/lane copy of nbytes/2 in and nbytes/2 out, non-temporal
+            loads and stores, one 16-KB tile per 1024-thread block (the
+            fastest of the round-5 calibration sweep, tools/probe_calib.py,
+            profiles/r05/probe_calib.jsonl: 6.38 TB/s at this size against
+            MI355X_MICROARCH.md's 6.29 TB/s float4 copy); 512-thread blocks
+            with 2 loads in flight are timed too and the faster is `copy`;
+      read  the same bytes read only (non-temporal, same tiling): the ceiling
+            of a read-dominated kernel such as the XTILE reduce;
+      copy_gridstride  the round-1..4 probe (grid-stride, 16384 blocks of
+            256), kept for continuity.
+    `frac` puts achieved_gbps against `copy`."""
     import ctypes as C
     P = C.CDLL(probe_lib_path(L))
     half = (nbytes // 2) // 16 * 16
     src = torch.empty(half // 4, dtype=torch.float32, device=dev).uniform_()
     dst = torch.empty_like(src)
-    rates = {}
-    for width in (8, 16):
-        def run():
-            P.lhpc_probe_copy_w(C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()), C.c_int64(half),
-                                C.c_int(16384), C.c_int(width), C.c_int(1), C.c_void_p(stream.cuda_stream))
+    n16 = half // 16
+    s = C.c_void_p(stream.cuda_stream)
+
+    def rate(fn, moved):
         for _ in range(3):
-            run()
+            fn()
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(10):
-            run()
+            fn()
         e1.record(stream)
         torch.cuda.synchronize()
-        rates[width] = 2 * half / (e0.elapsed_time(e1) * 1e-3 / 10) / 1e9
+        return moved / (e0.elapsed_time(e1) * 1e-3 / 10) / 1e9
+
+    def cu(buf_in, buf_out, block, unroll, mode):
+        grid = (n16 + block * unroll - 1) // (block * unroll)
+        rc = P.lhpc_probe_copy_u(C.c_void_p(buf_in.data_ptr()), C.c_void_p(buf_out.data_ptr()), C.c_int64(half),
+                                 C.c_int(grid), C.c_int(block), C.c_int(unroll), C.c_int(mode), s)
+        if rc != 0:
+            raise RuntimeError(f"lhpc_probe_copy_u: {rc}")
+    copies = {f"{b}x{u}": rate(lambda b=b, u=u: cu(src, dst, b, u, 3), 2 * half) for b, u in ((1024, 1), (512, 2))}
+    read = rate(lambda: (cu(src, dst, 1024, 1, 5), cu(dst, src, 1024, 1, 5)), 2 * half)
+    legacy = rate(lambda: P.lhpc_probe_copy_w(C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()),
+                                              C.c_int64(half), C.c_int(16384), C.c_int(16), C.c_int(1), s), 2 * half)
     del src, dst
-    gbps = max(rates.values())
-    return {"unit": "GB/s", "copy": gbps, "frac": achieved_gbps / gbps, "copy_8B_lane": rates[8],
-            "copy_16B_lane": rates[16], "bytes": 2 * half,
-            "note": "the same bytes copied by non-temporal grid-stride probes (8 and 16 B/lane); copy = the faster"}
+    gbps = max(copies.values())
+    return {"unit": "GB/s", "copy": gbps, "frac": achieved_gbps / gbps, "read": read,
+            "frac_of_read": achieved_gbps / read, "copy_tiles": copies, "copy_gridstride": legacy,
+            "bytes": 2 * half,
+            "note": "live 16-B/lane probes over the same bytes: copy (nt loads + stores, one 16-KB tile per "
+                    "block; the faster of 1024x1 / 512x2), read (nt, read only), copy_gridstride (rounds 1-4)"}
 
 
 def gather_ceiling(L, torch, dev, stream, nnz, call_s):
@@ -747,23 +851,32 @@ def host_info(threads=None):
 
 
 def cpu_spmv_baseline(rp, col, val, x, nnz, seconds, threads=None):
-    """C1 is quoted single-thread; C2-C4 on all host threads."""
+    """C1 is quoted single-thread.  C2-C4 run two legs on the
+    box's host: OMP_NUM_THREADS (the box sets 16: its CPU share per GPU) and
+    the process CPU set's size (`$(nproc)`, SURVEY §8d / BASELINE.md §3);
+    `value` is the faster leg and `cores` the thread count it used, `legs`
+    holds both.  Each leg gets half of `seconds`."""
     from tests import _support as S  # oracle/ is test infrastructure: baseline leg only
-    threads = threads or cpu_threads()
-    y, used = S.spmv_cpu_simd(rp, col, val, x, threads=threads)  # warm
-    times = []
-    t_end = time.perf_counter() + seconds
-    while len(times) < 3 or (time.perf_counter() < t_end and len(times) < 200_000):
-        t0 = time.perf_counter()
-        S.spmv_cpu_simd(rp, col, val, x, threads=threads)
-        times.append(time.perf_counter() - t0)
-    best = min(times)
-    return {"value": 2.0 * nnz / best / 1e9, "unit": "GFLOP/s", "cores": used, "kind": "port",
-            "sample": f"full matrix (nnz={nnz}), best of {len(times)} passes "
-                      f"({sum(times):.1f} s), AVX2 gather" + (" + OpenMP" if threads > 1 else ", 1 thread")
-                      + ", oracle/oracle.c cpu_spmv_simd",
+    counts = [threads] if threads else sorted({cpu_threads(), len(PROCESS_CPUS)})
+    legs = []
+    for th in counts:
+        y, used = S.spmv_cpu_simd(rp, col, val, x, threads=th)  # warm
+        times = []
+        t_end = time.perf_counter() + seconds / len(counts)
+        while len(times) < 3 or (time.perf_counter() < t_end and len(times) < 200_000):
+            t0 = time.perf_counter()
+            S.spmv_cpu_simd(rp, col, val, x, threads=th)
+            times.append(time.perf_counter() - t0)
+        legs.append({"threads": used, "value": 2.0 * nnz / min(times) / 1e9, "passes": len(times),
+                     "seconds": sum(times)})
+    best = max(legs, key=lambda g: g["value"])
+    return {"value": best["value"], "unit": "GFLOP/s", "cores": best["threads"], "kind": "port",
+            "legs": legs,
+            "sample": f"full matrix (nnz={nnz}), best pass per leg, AVX2 gather"
+                      + (" + OpenMP" if best["threads"] > 1 else ", 1 thread") + ", oracle/oracle.c cpu_spmv_simd; "
+                      "legs: OMP_NUM_THREADS and the process CPU set size",
             "omp": {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OMP_PROC_BIND", "OMP_PLACES")},
-            "host": host_info(used)}
+            "host": host_info(best["threads"])}
 
 
 def stencil_bench(args, L, torch, dev, stream, barrier):

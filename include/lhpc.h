@@ -52,7 +52,8 @@ enum lhpc_status {
   LHPC_ERR_ALLOC = -3,         /* device or host allocation failed          */
   LHPC_ERR_NO_DEVICE = -4,     /* no usable gfx950 device                   */
   LHPC_ERR_UNSUPPORTED = -5,   /* valid request the build does not support  */
-  LHPC_ERR_INTERNAL = -6
+  LHPC_ERR_INTERNAL = -6,
+  LHPC_ERR_BUSY = -7           /* plan-owned work already in use (CG solve) */
 };
 /* RCCL failures: LHPC_RCCL_STATUS_BASE + ncclResult_t (above any hipError_t) */
 #define LHPC_RCCL_STATUS_BASE 10000
@@ -471,7 +472,9 @@ int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
  * non-null stream with check_every ≥ 4 and an ADAPTIVE plan it replays the
  * check_every iterations between two checks as a captured HIP graph, also
  * kept with the plan (results bit-identical to the loop).  So one plan
- * serves one solve at a time: concurrent solves need a plan each.
+ * serves one solve at a time: a solve started while another one on the
+ * same plan is running returns LHPC_ERR_BUSY (concurrent solves need a plan
+ * each).  The work is allocated on the plan's device.
  * Building blocks for multi-GPU composition (all asynchronous on `stream`,
  * scalars are fp64 HBM pointers, read on the device):
  *   lhpc_vec_dot     *out = a·b
@@ -660,6 +663,37 @@ typedef struct lhpc_dist_xfer {
 } lhpc_dist_xfer;
 int lhpc_dist_exchange_schedule(const int64_t *cuts, int nranks, int K, int rank, int exchange,
                                 int broadcast, lhpc_dist_xfer *out, int64_t max_out, int64_t *n_out);
+/*
+ * The RCCL calls themselves, argument by argument, that the RCCL exchange
+ * issues for this rank (lhpc_dist_spmv, one process per rank) or device
+ * (the single-process multi-device plan, device index = rank): both device
+ * paths walk exactly this list (lhpc_rccl.hpp), the CPU tests check it for
+ * every rank against RCCL's contracts (matching collectives on every rank,
+ * the in-place all-gather's sendbuff == recvbuff + rank·count, broadcast
+ * roots) and emulate it.  One entry per call, chunk order:
+ *   op  LHPC_RCCL_ALLGATHER: ncclAllGather(y + send_byte_offset,
+ *       y + recv_byte_offset, count, datatype, comm, stream);
+ *       LHPC_RCCL_BROADCAST: ncclBroadcast(y + send_byte_offset,
+ *       y + recv_byte_offset, count, datatype, root, comm, stream)
+ *   group_begin / group_end: ncclGroupStart() before / ncclGroupEnd() after
+ *       the call (lhpc_dist_spmv; the multi-device plan brackets each chunk's
+ *       calls of all its devices in one group instead)
+ * datatype is the ncclDataType_t value (ncclFloat32 / ncclFloat64).
+ */
+enum lhpc_rccl_op { LHPC_RCCL_ALLGATHER = 1, LHPC_RCCL_BROADCAST = 2 };
+typedef struct lhpc_rccl_call {
+  int32_t chunk;
+  int32_t op;                   /* enum lhpc_rccl_op                              */
+  int32_t root;                 /* broadcast root (−1: all-gather)                */
+  int32_t datatype;             /* ncclDataType_t                                 */
+  int32_t group_begin;          /* ncclGroupStart() before this call              */
+  int32_t group_end;            /* ncclGroupEnd() after this call                 */
+  int64_t send_byte_offset;     /* sendbuff = (char *)y + send_byte_offset         */
+  int64_t recv_byte_offset;     /* recvbuff = (char *)y + recv_byte_offset         */
+  int64_t count;                /* elements (all-gather: per rank)                */
+} lhpc_rccl_call;
+int lhpc_dist_rccl_calls(const int64_t *cuts, int nranks, int K, int rank, int broadcast, int dtype,
+                         lhpc_rccl_call *out, int64_t max_out, int64_t *n_out);
 /*
  * Direct peer exchange of y (SURVEY §8e "Optimisation": every pair of
  * MI355X in a node is connected by xGMI).  Each rank exports a y buffer

@@ -70,7 +70,7 @@ ABI_SYMBOLS = (
     "lhpc_dist_exchange_schedule", "lhpc_dist_p2p_reset", "lhpc_dist_p2p_unmap", "lhpc_scratch_trim", "lhpc_scratch_poison",
     "lhpc_spmv_multi", "lhpc_spmv_plan_multi_info", "lhpc_dist_spmv_begin", "lhpc_dist_spmv_end",
     "lhpc_dist_chain_parts", "lhpc_dist_allgather_f64", "lhpc_dist_cg_solve", "lhpc_dist_spmv_plan_info",
-    "lhpc_spmv_plan_layout_digest",
+    "lhpc_spmv_plan_layout_digest", "lhpc_dist_rccl_calls",
 )
 
 if not os.path.exists(LIB_PATH):
@@ -143,6 +143,13 @@ XFER_ALLGATHER, XFER_BROADCAST, XFER_PUSH = 1, 2, 3
 class DistXfer(C.Structure):
     _fields_ = [("chunk", C.c_int32), ("kind", C.c_int32), ("root", C.c_int32), ("group", C.c_int32),
                 ("offset", C.c_int64), ("count", C.c_int64), ("send_offset", C.c_int64)]
+
+
+class RcclCall(C.Structure):
+    """include/lhpc.h lhpc_rccl_call: one RCCL call of the y exchange."""
+    _fields_ = [("chunk", C.c_int32), ("op", C.c_int32), ("root", C.c_int32), ("datatype", C.c_int32),
+                ("group_begin", C.c_int32), ("group_end", C.c_int32), ("send_byte_offset", C.c_int64),
+                ("recv_byte_offset", C.c_int64), ("count", C.c_int64)]
 
 
 class PlanInfo(C.Structure):
@@ -234,6 +241,7 @@ _sig("lhpc_dist_spmv_plan_info", _i, _p, C.POINTER(PlanInfo), C.POINTER(_i))
 _sig("lhpc_dist_chain_parts", _i, _p, _i, _i, _i64, _i64, _p, _i64)
 _sig("lhpc_dist_exchange", _i, _p, _p, _p)
 _sig("lhpc_dist_exchange_schedule", _i, _p, _i, _i, _i, _i, _i, _p, _i64, C.POINTER(_i64))
+_sig("lhpc_dist_rccl_calls", _i, _p, _i, _i, _i, _i, _i, _p, _i64, C.POINTER(_i64))
 _sig("lhpc_dist_p2p_reset", _i, _p)
 _sig("lhpc_dist_p2p_unmap", _i, _p, _p)
 _sig("lhpc_dist_spmv_plan_destroy", _i, _p)
@@ -1045,6 +1053,25 @@ def dist_exchange_schedule(cuts, nranks: int, K: int, rank: int, exchange: int =
     _check(lib.lhpc_dist_exchange_schedule(cuts.ctypes.data, nranks, K, rank, exchange, int(broadcast), buf, cap,
                                            C.byref(n)), "lhpc_dist_exchange_schedule")
     return [{f: getattr(buf[i], f) for f, _ in DistXfer._fields_} for i in range(n.value)]
+
+
+RCCL_ALLGATHER, RCCL_BROADCAST = 1, 2
+
+
+def dist_rccl_calls(cuts, nranks: int, K: int, rank: int, dtype: int = F32, broadcast: bool = False):
+    """The RCCL calls, argument by argument, that the device paths issue for
+    `rank` (include/lhpc.h lhpc_dist_rccl_calls): a list of dicts {chunk, op,
+    root, datatype, group_begin, group_end, send_byte_offset,
+    recv_byte_offset, count} in issue order."""
+    cuts = np.ascontiguousarray(cuts, dtype=np.int64)
+    if cuts.shape[0] != nranks * K + 1:
+        raise ValueError("cuts must hold nranks*K + 1 rows")
+    cap = nranks * K
+    buf = (RcclCall * max(cap, 1))()
+    n = _i64(0)
+    _check(lib.lhpc_dist_rccl_calls(cuts.ctypes.data, nranks, K, rank, int(broadcast), dtype, buf, cap, C.byref(n)),
+           "lhpc_dist_rccl_calls")
+    return [{f: getattr(buf[i], f) for f, _ in RcclCall._fields_} for i in range(n.value)]
 
 
 class DistSpMVPlan:

@@ -46,6 +46,7 @@
 #include <vector>
 
 #include "lhpc_common.hpp"
+#include "lhpc_rccl.hpp"
 #include "lhpc_spmv_impl.hpp"
 
 #define LHPC_NCCL_TRY(expr)                                                \
@@ -104,6 +105,9 @@ struct lhpc_dist_spmv_plan {
   // at [first[k], first[k+1])
   std::vector<lhpc_dist_xfer> sched_rccl, sched_p2p;
   std::vector<int64_t> first_rccl, first_p2p;
+  // the RCCL calls of sched_rccl, one per entry (lhpc_rccl.hpp; the records
+  // lhpc_dist_rccl_calls exports to the CPU tests)
+  std::vector<lhpc_rccl_call> calls_rccl;
   std::vector<hipEvent_t> ev;               // [K] chunk k reduced
   std::vector<hipEvent_t> ev_x;             // [K] chunk k's exchange landed (comm stream)
   hipEvent_t done = nullptr;                // last exchange issued on the comm stream
@@ -487,31 +491,11 @@ void destroy_spmv(lhpc_dist_spmv_plan *d) {
 }
 
 // chunk k's RCCL transfers from the schedule: one in-place all-gather, or
-// one group of in-place broadcasts (root r sends its block)
+// one group of in-place broadcasts (root r sends its block) — the records of
+// lhpc_rccl.hpp, with their group brackets
 int issue_rccl_chunk(const lhpc_dist_spmv_plan *d, int k, void *y, hipStream_t cs) {
-  const lhpc_dist_comm *c = d->comm;
-  const size_t tsz = d->dtype == LHPC_F64 ? 8 : 4;
-  unsigned char *yb = static_cast<unsigned char *>(y);
-  const int64_t e0 = d->first_rccl[k], e1 = d->first_rccl[k + 1];
-  if (e1 == e0) return LHPC_OK;
-  const bool group = d->sched_rccl[e0].group != 0;
-  if (group) LHPC_NCCL_TRY(ncclGroupStart());
-  for (int64_t e = e0; e < e1; ++e) {
-    const lhpc_dist_xfer &x = d->sched_rccl[e];
-    ncclResult_t st;
-    if (x.kind == LHPC_XFER_ALLGATHER)
-      st = ncclAllGather(yb + x.send_offset * tsz, yb + x.offset * tsz, static_cast<size_t>(x.count),
-                         nccl_dt(d->dtype), c->comm, cs);
-    else
-      st = ncclBroadcast(yb + x.offset * tsz, yb + x.offset * tsz, static_cast<size_t>(x.count), nccl_dt(d->dtype),
-                         x.root, c->comm, cs);
-    if (st != ncclSuccess) {
-      if (group) (void)ncclGroupEnd();
-      return LHPC_RCCL_STATUS_BASE + static_cast<int>(st);
-    }
-  }
-  if (group) LHPC_NCCL_TRY(ncclGroupEnd());
-  return LHPC_OK;
+  return lhpc::rccl_issue_list(d->calls_rccl.data(), d->first_rccl[k], d->first_rccl[k + 1], static_cast<unsigned char *>(y),
+                         d->comm->comm, cs);
 }
 
 // which exchange a call with this y runs (LHPC_DIST_EXCHANGE_NONE: none);
@@ -590,6 +574,23 @@ extern "C" int lhpc_dist_exchange_schedule(const int64_t *cuts, int nranks, int 
   *n_out = static_cast<int64_t>(v.size());
   if (static_cast<int64_t>(v.size()) > max_out) return LHPC_ERR_INVALID_ARG;
   if (!v.empty()) std::memcpy(out, v.data(), v.size() * sizeof(lhpc_dist_xfer));
+  return LHPC_OK;
+}
+
+extern "C" int lhpc_dist_rccl_calls(const int64_t *cuts, int nranks, int K, int rank, int broadcast, int dtype,
+                                    lhpc_rccl_call *out, int64_t max_out, int64_t *n_out) {
+  if (dtype != LHPC_F32 && dtype != LHPC_F64) return LHPC_ERR_INVALID_ARG;
+  if (!n_out || max_out < 0 || (max_out > 0 && !out)) return LHPC_ERR_INVALID_ARG;
+  int64_t ns = 0;  // the schedule's size (a too-small buffer still reports it)
+  const int q = lhpc_dist_exchange_schedule(cuts, nranks, K, rank, LHPC_DIST_EXCHANGE_RCCL, broadcast, nullptr, 0, &ns);
+  if (q != LHPC_OK && ns == 0) return q;  // bad cuts / ranks
+  std::vector<lhpc_dist_xfer> v(static_cast<size_t>(ns));
+  LHPC_TRY(lhpc_dist_exchange_schedule(cuts, nranks, K, rank, LHPC_DIST_EXCHANGE_RCCL, broadcast, v.data(), ns, &ns));
+  std::vector<lhpc_rccl_call> calls;
+  lhpc::rccl_calls_of(v.data(), ns, dtype, calls);
+  *n_out = static_cast<int64_t>(calls.size());
+  if (*n_out > max_out) return LHPC_ERR_INVALID_ARG;
+  if (!calls.empty()) std::memcpy(out, calls.data(), calls.size() * sizeof(lhpc_rccl_call));
   return LHPC_OK;
 }
 
@@ -782,8 +783,13 @@ extern "C" int lhpc_dist_p2p_import(lhpc_dist_comm *c, const unsigned char *blob
   w.ready = true;
   if (remap) {
     // close the replaced peer mappings (every window's kernels read peers'
-    // flags through d_peer_flags only, which is swapped here)
-    if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
+    // flags through d_peer_flags only, which is swapped here).  Kernels on the
+    // callers' compute streams (k_p2p_signal, k_p2p_signal_mask,
+    // k_p2p_red_push) dereference the old table too, and their streams are not
+    // known here: drain the whole device before the old mappings close
+    // (import is a setup call, not on the step path)
+    if (c->flags_mapped) (void)hipDeviceSynchronize();
+    else if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
     std::vector<void *> base(static_cast<size_t>(nr), nullptr);
     for (int r = 0; r < nr; ++r) {
       if (r == c->rank) continue;
@@ -939,6 +945,7 @@ extern "C" int lhpc_dist_spmv_plan_create_opts(lhpc_dist_spmv_plan **out, lhpc_d
   d->opt = o;
   d->cuts.assign(cuts, cuts + nb + 1);
   build_schedule(cuts, nr, K, rk, LHPC_DIST_EXCHANGE_RCCL, o.dist_broadcast, d->sched_rccl, d->first_rccl);
+  lhpc::rccl_calls_of(d->sched_rccl.data(), static_cast<int64_t>(d->sched_rccl.size()), dtype, d->calls_rccl);
   build_schedule(cuts, nr, K, rk, LHPC_DIST_EXCHANGE_P2P, 0, d->sched_p2p, d->first_p2p);
   // the local CSR: the rank's K blocks stacked in chunk order
   std::vector<int64_t> ls(static_cast<size_t>(K) + 1, 0);

@@ -42,6 +42,7 @@
 #include <vector>
 
 #include "lhpc_common.hpp"
+#include "lhpc_rccl.hpp"
 #include "lhpc_spmv_impl.hpp"
 
 // ------------------------------------------------------------ local plans
@@ -199,6 +200,10 @@ struct lhpc_multi {
   std::vector<int64_t> cuts;              // D·K + 1
   std::vector<lhpc_dist_xfer> sched;      // RCCL schedule of device 0's view (root/offsets are global)
   std::vector<std::vector<lhpc_dist_xfer>> sched_dev;  // per device (send offsets differ)
+  // their RCCL calls (lhpc_rccl.hpp; one per schedule entry, so first[] indexes
+  // both).  Each chunk's calls of all devices go in one outer group: one
+  // process drives every communicator
+  std::vector<std::vector<lhpc_rccl_call>> calls_dev;
   std::vector<int64_t> first;             // chunk k's entries [first[k], first[k+1])
   MultiDev dev[kMultiMaxDevices];
   hipEvent_t ev_start = nullptr;          // home calls: recorded on the caller's stream
@@ -320,16 +325,9 @@ int multi_chunks(lhpc_multi *m, const void *const *xs, void *const *ys, const hi
       for (int d = 0; d < D; ++d) {
         MultiDev &v = m->dev[d];
         unsigned char *yb = static_cast<unsigned char *>(ys[d]);
-        const auto &sd = m->sched_dev[static_cast<size_t>(d)];
+        const auto &cd = m->calls_dev[static_cast<size_t>(d)];  // lhpc_rccl.hpp records, as lhpc_dist_rccl_calls
         for (int64_t e = m->first[k]; e < m->first[k + 1]; ++e) {
-          const lhpc_dist_xfer &x = sd[static_cast<size_t>(e)];
-          ncclResult_t r;
-          if (x.kind == LHPC_XFER_ALLGATHER)
-            r = ncclAllGather(yb + x.send_offset * tsz, yb + x.offset * tsz, static_cast<size_t>(x.count),
-                              m->dtype == LHPC_F64 ? ncclFloat64 : ncclFloat32, v.comm, v.s_comm);
-          else
-            r = ncclBroadcast(yb + x.offset * tsz, yb + x.offset * tsz, static_cast<size_t>(x.count),
-                              m->dtype == LHPC_F64 ? ncclFloat64 : ncclFloat32, x.root, v.comm, v.s_comm);
+          const ncclResult_t r = rccl_issue(cd[static_cast<size_t>(e)], yb, v.comm, v.s_comm);
           if (r != ncclSuccess) {
             (void)ncclGroupEnd();
             return LHPC_RCCL_STATUS_BASE + static_cast<int>(r);
@@ -345,14 +343,23 @@ int multi_chunks(lhpc_multi *m, const void *const *xs, void *const *ys, const hi
   }
   if (D == 1 && !rccl) return LHPC_OK;
   // every device's stream waits for what was pushed into its y, then drops
-  // stale L2 lines of y (peer stores bypassed its L2s)
+  // stale L2 lines of y (peer stores bypassed its L2s).  It also waits for
+  // its OWN pushes (they read ys[d]): a write to ys[d] queued on ss[d] after
+  // the call — a user kernel, or the next call's reduce, which waits only on
+  // READY — must not race the push that copies ys[d]'s blocks to the peers
   for (int d = 0; d < D; ++d) {
-    if (home_only && d != 0) continue;
     MultiDev &v = m->dev[d];
     LHPC_HIP_TRY(hipSetDevice(v.device));
+    if (home_only && d != 0) {
+      if (!rccl) LHPC_HIP_TRY(hipStreamWaitEvent(ss[d], v.ev_push[m->K - 1], 0));  // s_comm is in order
+      continue;
+    }
     bool remote = rccl;
     for (int p = 0; p < D; ++p) {
-      if (p == d && !rccl) continue;
+      if (p == d && !rccl) {
+        LHPC_HIP_TRY(hipStreamWaitEvent(ss[d], v.ev_push[m->K - 1], 0));
+        continue;
+      }
       for (int k = 0; k < m->K; ++k) LHPC_HIP_TRY(hipStreamWaitEvent(ss[d], m->dev[p].ev_push[k], 0));
       if (m->dev[p].device != v.device) remote = true;
     }
@@ -409,6 +416,8 @@ int multi_create(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const
                                            v.data(), static_cast<int64_t>(v.size()), &n));
       v.resize(static_cast<size_t>(n));
       m->sched_dev[static_cast<size_t>(d)] = v;
+      m->calls_dev.emplace_back();
+      rccl_calls_of(v.data(), n, p->dtype, m->calls_dev.back());
     }
     m->first.assign(static_cast<size_t>(K) + 1, 0);
     const auto &s0 = m->sched_dev[0];

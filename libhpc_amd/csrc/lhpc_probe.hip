@@ -43,6 +43,48 @@ __global__ __launch_bounds__(256) void k_copyw(const T *__restrict__ s, T *__res
   }
 }
 
+// Unrolled 16-B/lane probes (round 5 calibration against MI355X_MICROARCH.md's
+// 6.29 TB/s float4 copy): a block moves a tile of U·BLK float4 per iteration
+// (U loads in flight per lane, each wave instruction 1 KB contiguous) and
+// strides over tiles by the grid.  MODE bit 0: non-temporal loads, bit 1:
+// non-temporal stores, bit 2: read only (sum kept alive), bit 3: write only.
+template <int BLK, int U, int MODE>
+__global__ __launch_bounds__(BLK) void k_copy_u(const f32x4 *__restrict__ s, f32x4 *__restrict__ d, int64_t n) {
+  constexpr bool NTL = MODE & 1, NTS = MODE & 2, RO = MODE & 4, WO = MODE & 8;
+  const int64_t tile = static_cast<int64_t>(BLK) * U;
+  const int64_t tiles = n / tile;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int64_t b = t * tile + threadIdx.x;
+    f32x4 v[U];
+    if constexpr (!WO) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = NTL ? __builtin_nontemporal_load(s + b + u * BLK) : s[b + u * BLK];
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = f32x4{static_cast<float>(t), 1.f, 2.f, static_cast<float>(u)};
+    }
+    if constexpr (RO) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += v[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if constexpr (NTS) __builtin_nontemporal_store(v[u], d + b + u * BLK);
+        else d[b + u * BLK] = v[u];
+      }
+    }
+  }
+  // the tail (n not a multiple of the tile): block 0, one float4 per lane
+  if (blockIdx.x == 0)
+    for (int64_t i = tiles * tile + threadIdx.x; i < n; i += BLK) {
+      if constexpr (RO) acc += s[i];
+      else d[i] = WO ? f32x4{0.f, 0.f, 0.f, 0.f} : s[i];
+    }
+  if constexpr (RO)
+    if (acc[0] + acc[1] + acc[2] + acc[3] == 12345.678f) d[0] = acc;  // keep the loads alive
+}
+
 __global__ __launch_bounds__(256) void k_read16(const f32x4 *__restrict__ s, float *__restrict__ sink,
                                                int64_t n) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
@@ -183,6 +225,43 @@ extern "C" int lhpc_probe_gather(const int32_t *idx, const float *table, float *
   hipLaunchKernelGGL((k_gather<U>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), idx, table, out, n);
   return static_cast<int>(hipGetLastError());
+}
+
+// k_copy_u: block ∈ {256, 512, 1024}, unroll ∈ {1, 2, 4, 8}, mode as k_copy_u's
+// MODE (0–15; read-only and write-only exclusive).  Returns hipErrorInvalidValue
+// for a combination not instantiated.
+template <int BLK, int U>
+static hipError_t launch_copy_u(const f32x4 *s, f32x4 *d, int64_t n, int grid, int mode, hipStream_t st) {
+  switch (mode) {
+#define LHPC_CU(M) \
+  case M: hipLaunchKernelGGL((k_copy_u<BLK, U, M>), dim3(grid), dim3(BLK), 0, st, s, d, n); break;
+    LHPC_CU(0) LHPC_CU(1) LHPC_CU(2) LHPC_CU(3) LHPC_CU(4) LHPC_CU(5) LHPC_CU(8) LHPC_CU(10)
+#undef LHPC_CU
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+template <int BLK>
+static hipError_t launch_copy_b(const f32x4 *s, f32x4 *d, int64_t n, int grid, int unroll, int mode, hipStream_t st) {
+  switch (unroll) {
+    case 1: return launch_copy_u<BLK, 1>(s, d, n, grid, mode, st);
+    case 2: return launch_copy_u<BLK, 2>(s, d, n, grid, mode, st);
+    case 4: return launch_copy_u<BLK, 4>(s, d, n, grid, mode, st);
+    case 8: return launch_copy_u<BLK, 8>(s, d, n, grid, mode, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+extern "C" int lhpc_probe_copy_u(const void *src, void *dst, int64_t bytes, int grid, int block, int unroll,
+                                 int mode, void *stream) {
+  const f32x4 *s = static_cast<const f32x4 *>(src);
+  f32x4 *d = static_cast<f32x4 *>(dst);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t n = bytes / 16;
+  hipError_t e = block == 256    ? launch_copy_b<256>(s, d, n, grid, unroll, mode, st)
+                 : block == 512  ? launch_copy_b<512>(s, d, n, grid, unroll, mode, st)
+                 : block == 1024 ? launch_copy_b<1024>(s, d, n, grid, unroll, mode, st)
+                                 : hipErrorInvalidValue;
+  return static_cast<int>(e);
 }
 
 // width ∈ {4, 8, 16} bytes per lane; mode bit 0 = non-temporal, bit 1 = chunked (see k_copyw)

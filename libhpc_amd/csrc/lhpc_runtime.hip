@@ -19,6 +19,7 @@ extern "C" const char *lhpc_strerror(int status) {
     case LHPC_ERR_NO_DEVICE: return "lhpc: no gfx950 (MI355X) device";
     case LHPC_ERR_UNSUPPORTED: return "lhpc: unsupported configuration";
     case LHPC_ERR_INTERNAL: return "lhpc: internal error";
+    case LHPC_ERR_BUSY: return "lhpc: plan work in use by another call (one CG solve per plan at a time)";
     default:
       if (status >= LHPC_RCCL_STATUS_BASE)
         return ncclGetErrorString(static_cast<ncclResult_t>(status - LHPC_RCCL_STATUS_BASE));
@@ -127,9 +128,19 @@ hipError_t scratch_pool(int dev, hipMemPool_t *out) {
 }
 }  // namespace
 
+// The pool of the stream's device (a caller whose current device differs
+// from its stream's still gets scratch where the stream runs); the current
+// device only for the null stream.
 hipError_t scratch_alloc(void **p, size_t bytes, hipStream_t s) {
   int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
+  hipError_t e;
+  if (s) {
+    hipDevice_t sd = 0;
+    e = hipStreamGetDevice(s, &sd);
+    dev = static_cast<int>(sd);
+  } else {
+    e = hipGetDevice(&dev);
+  }
   if (e != hipSuccess) return e;
   hipMemPool_t pool;
   if ((e = scratch_pool(dev, &pool)) != hipSuccess) return e;

@@ -293,10 +293,28 @@ extern "C" int lhpc_cg_step_xp(int dtype, int64_t n, const double *alpha_num, co
   return check_launch(s);
 }
 
+namespace {
+int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int max_iter, int check_every,
+                   int *iters_out, double *resid_out, void *stream);
+}
+
+// One solve per plan at a time: the work vectors, scalars and captured
+// graphs belong to the plan, so a second concurrent solve is
+// refused instead of racing on them.
 extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int max_iter,
                              int check_every, int *iters_out, double *resid_out, void *stream) {
-  lhpc_spmv_plan_info info{};
   if (!plan || !b || !x || max_iter < 0 || !(tol >= 0.0)) return LHPC_ERR_INVALID_ARG;
+  int idle = 0;
+  if (!plan->cg_busy.compare_exchange_strong(idle, 1)) return LHPC_ERR_BUSY;
+  const int st = cg_solve_owned(plan, b, x, tol, max_iter, check_every, iters_out, resid_out, stream);
+  plan->cg_busy.store(0);
+  return st;
+}
+
+namespace {
+int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int max_iter, int check_every,
+                   int *iters_out, double *resid_out, void *stream) {
+  lhpc_spmv_plan_info info{};
   LHPC_TRY(lhpc_spmv_plan_info_get(plan, &info));
   if (info.n_rows != info.n_cols) return LHPC_ERR_INVALID_ARG;  // CG needs a square (SPD) matrix
   RocTxRange rx("lhpc_cg_solve");
@@ -308,9 +326,14 @@ extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, doubl
   // work (kept with the plan, so a captured iteration block can be replayed
   // by later solves): r, p, q, x vectors + scalars [rr0, rr1, pq, bb] + dot
   // partials; the caller's x is copied in and out
-  if (!plan->cg_vecs) {
-    LHPC_HIP_TRY(hipMalloc(&plan->cg_vecs, static_cast<size_t>(std::max<int64_t>(n, 1)) * ts * 4));
-    LHPC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&plan->cg_scal), (8 + kDotBlocks) * sizeof(double)));
+  if (!plan->cg_vecs) {  // on the plan's device, whatever the caller's current device
+    int cur = 0;
+    LHPC_HIP_TRY(hipGetDevice(&cur));
+    LHPC_HIP_TRY(hipSetDevice(plan->device));
+    hipError_t e = hipMalloc(&plan->cg_vecs, static_cast<size_t>(std::max<int64_t>(n, 1)) * ts * 4);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&plan->cg_scal), (8 + kDotBlocks) * sizeof(double));
+    (void)hipSetDevice(cur);
+    LHPC_HIP_TRY(e);
   }
   char *vb = static_cast<char *>(plan->cg_vecs);
   void *r = vb, *p = vb + static_cast<size_t>(n) * ts, *q = vb + 2 * static_cast<size_t>(n) * ts;
@@ -450,3 +473,4 @@ extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, doubl
   if (resid_out) *resid_out = std::sqrt(std::max(h_rr, 0.0)) / std::sqrt(h_bb > 0.0 ? h_bb : 1.0);
   return status;
 }
+}  // namespace

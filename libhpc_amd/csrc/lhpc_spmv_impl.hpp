@@ -10,6 +10,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <vector>
 
@@ -35,6 +36,7 @@ struct lhpc_spmv_plan {
   double *cg_scal = nullptr;
   hipGraphExec_t cg_graph[2] = {nullptr, nullptr};
   int cg_graph_iters[2] = {0, 0};
+  std::atomic<int> cg_busy{0};  // a solve holds the work above (LHPC_ERR_BUSY for a second one)
   double *d_dpart = nullptr;  // lhpc_spmv_dot: per-block partials (ADAPTIVE), allocated on first use
   int kernel = LHPC_KERNEL_ROWGROUP;
   int L = 16, R = 4;

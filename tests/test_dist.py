@@ -319,3 +319,96 @@ def test_chain_parts_rejects_bad_input():
         L.dist_chain_parts(cuts, 2, 1, 11, 4)  # the chunks do not cover x
     with pytest.raises(L.LhpcError):
         L.dist_chain_parts(np.array([0, 6, 4, 10], dtype=np.int64), 1, 3, 10, 4)  # not ascending
+
+
+def _cuts_of(kind, world, K):
+    import libhpc_amd as L
+    if kind == "uniform":
+        rp = np.arange(0, 5 * (4096 * world * K) + 1, 5, dtype=np.int64)
+    elif kind == "powerlaw":
+        rp, _, _ = L.gen_powerlaw_csr(30_011, 30_011, lmax=2000, dtype=L.F32, dist=1, seed=0xD190)
+    else:  # fewer rows than blocks: empty blocks
+        rp = np.arange(0, 2 * 5 + 1, 2, dtype=np.int64)
+    return L.interleaved_cuts(rp, world, K), int(rp.shape[0] - 1)
+
+
+@pytest.mark.parametrize("world,K", [(8, 1), (8, 2), (8, 4), (2, 2), (3, 4)])
+@pytest.mark.parametrize("kind", ["uniform", "powerlaw", "empty"])
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+@pytest.mark.parametrize("broadcast", [False, True])
+def test_rccl_call_arguments(world, K, kind, dtype, broadcast):
+    """the exact RCCL argument lists the device paths
+    issue (lhpc_dist_rccl_calls = the records lhpc_dist.hip and lhpc_multi.hip
+    walk, lhpc_rccl.hpp), for every rank: matching collectives on every rank
+    (op, count, datatype, root, group brackets, recvbuff — a mismatch hangs
+    RCCL), the in-place all-gather contract sendbuff == recvbuff + rank·count,
+    in-place broadcasts of exactly the root's block, balanced group brackets,
+    buffers inside y; then the calls are executed on byte buffers with RCCL
+    semantics and every rank must end with the whole y."""
+    import libhpc_amd as L
+    dt = L.F32 if dtype == "f32" else L.F64
+    tsz, npdt, ncdt = (4, np.float32, 7) if dt == L.F32 else (8, np.float64, 8)
+    cuts, n = _cuts_of(kind, world, K)
+    calls = [L.dist_rccl_calls(cuts, world, K, r, dt, broadcast) for r in range(world)]
+    full = np.arange(n, dtype=npdt) + 1
+    ys = []
+    for r in range(world):
+        y = np.full(n, np.nan, dtype=npdt)
+        for k in range(K):
+            b = k * world + r
+            y[cuts[b]:cuts[b + 1]] = full[cuts[b]:cuts[b + 1]]
+        ys.append(y.view(np.uint8))
+    for k in range(K):
+        per = [[c for c in calls[r] if c["chunk"] == k] for r in range(world)]
+        sig = [[(c["op"], c["count"], c["datatype"], c["root"], c["group_begin"], c["group_end"],
+                 c["recv_byte_offset"]) for c in per[r]] for r in range(world)]
+        assert all(s == sig[0] for s in sig), f"chunk {k}: ranks issue different collectives"
+        b0 = k * world
+        blocks = [(int(cuts[b0 + q]), int(cuts[b0 + q + 1])) for q in range(world)]
+        nonempty = [q for q, (a, e) in enumerate(blocks) if e > a]
+        depth = 0
+        for j in range(len(per[0])):
+            c0 = per[0][j]
+            assert c0["datatype"] == ncdt and c0["count"] > 0
+            depth += c0["group_begin"]
+            assert depth in (0, 1), "nested or unbalanced group"
+            if c0["op"] == L.RCCL_ALLGATHER:
+                cnt, recv = c0["count"], c0["recv_byte_offset"]
+                assert not broadcast and c0["root"] == -1 and len(per[0]) == 1
+                assert all(e - a == cnt for a, e in blocks), "all-gather needs equal blocks"
+                assert recv == blocks[0][0] * tsz and recv + world * cnt * tsz == blocks[-1][1] * tsz <= n * tsz
+                parts = []
+                for r in range(world):
+                    send = per[r][j]["send_byte_offset"]
+                    assert send == recv + r * cnt * tsz, "in-place all-gather: sendbuff = recvbuff + rank*count"
+                    parts.append(ys[r][send:send + cnt * tsz].copy())
+                for r in range(world):
+                    for q in range(world):
+                        ys[r][recv + q * cnt * tsz:recv + (q + 1) * cnt * tsz] = parts[q]
+            else:
+                assert c0["op"] == L.RCCL_BROADCAST and 0 <= c0["root"] < world
+                root, cnt, recv = c0["root"], c0["count"], c0["recv_byte_offset"]
+                assert (recv, recv + cnt * tsz) == (blocks[root][0] * tsz, blocks[root][1] * tsz), "root's block"
+                for r in range(world):
+                    assert per[r][j]["send_byte_offset"] == recv, "in-place broadcast"
+                data = ys[root][recv:recv + cnt * tsz].copy()
+                for r in range(world):
+                    ys[r][recv:recv + cnt * tsz] = data
+            depth -= c0["group_end"]
+            assert depth in (0, 1)
+        assert depth == 0, "a group left open"
+        ops = {c["op"] for c in per[0]}
+        if ops == {L.RCCL_BROADCAST}:
+            assert sorted(c["root"] for c in per[0]) == nonempty, "one broadcast per non-empty block"
+        elif nonempty:
+            assert ops == {L.RCCL_ALLGATHER}
+    for r in range(world):
+        assert np.array_equal(ys[r].view(npdt), full), f"rank {r}"
+
+
+def test_rccl_calls_reject_bad_input():
+    import libhpc_amd as L
+    with pytest.raises(L.LhpcError):
+        L.dist_rccl_calls([0, 5, 3, 8, 9], 2, 2, 0)
+    with pytest.raises(L.LhpcError):
+        L.dist_rccl_calls([0, 1, 2, 3, 4], 2, 2, 0, dtype=7)

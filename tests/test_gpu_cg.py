@@ -230,3 +230,38 @@ def test_spmv_dot(lhpc, gpu, flags, dt):
         assert torch.equal(y, y0)
         yw = y.cpu().numpy().astype(np.float64) * w.cpu().numpy().astype(np.float64)
         assert abs(out.item() - yw.sum()) <= 1e-12 * np.abs(yw).sum()
+
+
+def test_cg_concurrent_solve_on_one_plan_is_refused(lhpc, gpu):
+    """the solve's work (vectors, scalars, captured graphs)
+    belongs to the plan, so a second solve on the same plan while one runs
+    returns LHPC_ERR_BUSY (-7) instead of racing on it; a solve after the
+    first one ended runs normally, and the first solve's x is unaffected."""
+    import threading
+    import time
+    import torch
+    ny = nx = 1024  # ≈ 0.2 ms per iteration: 3000 iterations keep the first solve busy for ≫ 0.1 s
+    rp, col, val = S.laplacian_2d(ny, nx)
+    b = np.random.default_rng(0xC6).uniform(-1, 1, ny * nx)
+    with lhpc.SpMVPlan(rp, col, val, ny * nx) as plan:
+        bd = _dev(gpu, b)
+        ref, it_ref, _ = lhpc.cg(plan, bd, tol=0.0, max_iter=300, check_every=10)
+        ref = ref.cpu().numpy()
+        out, started = {}, threading.Event()
+
+        def long_solve():
+            started.set()
+            out["long"] = lhpc.cg(plan, bd, tol=0.0, max_iter=3000, check_every=10)
+        t = threading.Thread(target=long_solve)
+        t.start()
+        started.wait()
+        time.sleep(0.1)
+        busy = None
+        try:
+            lhpc.cg(plan, bd, tol=0.0, max_iter=10, check_every=10)
+        except lhpc.LhpcError as e:
+            busy = e.status
+        t.join()
+        assert "long" in out and busy == -7, (busy, "long" in out)
+        x2, it2, _ = lhpc.cg(plan, bd, tol=0.0, max_iter=300, check_every=10)  # the plan is free again
+        assert it2 == it_ref and np.array_equal(x2.cpu().numpy(), ref)

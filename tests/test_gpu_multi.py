@@ -100,6 +100,32 @@ def test_multi_replicas_iterate(lhpc, gpu, devices, case):
             assert np.array_equal(snaps[it][d].cpu().numpy(), want[it]), (it, d)
 
 
+def test_multi_own_push_before_later_writes(lhpc, gpu):
+    """share d's stream passes lhpc_spmv_multi only after its
+    OWN push (which reads y[d] to copy d's blocks into the peers' replicas)
+    has finished, so a write to y[d] queued on that stream right after the
+    call cannot corrupt the peers' replicas."""
+    import torch
+    n, D = 3_000_000, 3
+    rp, col, val, x = _problem(lhpc, n, 6, lhpc.F32, 0xB250)
+    _, want, _ = S.spmv_oracle(rp, col, val, x)
+    with lhpc.SpMVPlan(rp, col, val, n, devices=[0] * D, options={"multi_chunks": 2}) as plan:
+        xd = torch.from_numpy(x).to(gpu)
+        a = [xd.clone() for _ in range(D)]
+        streams = [torch.cuda.Stream(gpu) for _ in range(D)]
+        for it in range(3):
+            src = it % D  # the share whose y is overwritten
+            b = [torch.full((n,), float("nan"), dtype=xd.dtype, device=gpu) for _ in range(D)]
+            torch.cuda.synchronize()
+            plan.multi(a, b, streams)
+            with torch.cuda.stream(streams[src]):
+                b[src].fill_(-1.0)  # right after the call, on that share's stream only
+            torch.cuda.synchronize()
+            for d in range(D):
+                if d != src:
+                    assert np.array_equal(b[d].cpu().numpy(), want), (src, d)
+
+
 @pytest.mark.parametrize("exchange", ["p2p", "rccl"])
 @pytest.mark.parametrize("K", [1, 2])
 def test_multi_one_device_forced(lhpc, gpu, exchange, K):
