@@ -96,7 +96,10 @@ struct XtileHost {
 // start(c, s) ≤ M; lo ≤ (kXtSegHi − 1)·M < 2^16 for M ≤ 8192.  Size ≈ 4.6 B
 // per (chunk, tile): 21 MB for C2, 1.3 GB at n = 80M (where a dense int32
 // table of starts hit the old 2.7e8-entry limit).
-constexpr int kXtSegHi = 7;
+#ifndef LHPC_XT_SEGHI
+#define LHPC_XT_SEGHI 7  // (kXtSegHi − 1)·M < 2^16: 7 for M = 8192, 4 for M = 16384
+#endif
+constexpr int kXtSegHi = LHPC_XT_SEGHI;
 void xtile_segment_table(const XtileHost &o, std::vector<uint32_t> &seg, std::vector<int32_t> &hi);
 
 // 0 on success; LHPC_ERR_UNSUPPORTED when the layout does not fit its

@@ -37,10 +37,17 @@ template <> struct XtTile<double> { static constexpr int W = 20480; };  // 160 K
 // col16 step does not depend on the tile, so it is issued under the tile load.
 // (A fused form that also streamed val in tile order and wrote val·x[col]
 // was slower: C2 603 → 621 µs, C3 1141 → 1736 µs)
+#ifdef LHPC_XT_PROBE_GVAL
+// timing-only probe (wrong results): the gather also streams one T per entry
+// (from the plan's val, index masked into range) and writes val·x
+#define LHPC_GVAL_PARAM , const T *__restrict__ vg, int64_t vmask
+#else
+#define LHPC_GVAL_PARAM
+#endif
 template <typename T, int U, bool NT = false>
 __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
     const int32_t *__restrict__ pieces, const uint16_t *__restrict__ col16,
-    const T *__restrict__ x, int64_t n_cols, int tw, T *__restrict__ xg) {
+    const T *__restrict__ x, int64_t n_cols, int tw, T *__restrict__ xg LHPC_GVAL_PARAM) {
   constexpr int W = XtTile<T>::W;  // LDS capacity; the plan's tile width tw ≤ W
   __shared__ T xt[W];
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
@@ -51,11 +58,21 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
   const int q0 = g0 >> 3, q1 = g1 >> 3;  // 8-entry groups
   const u32x4 *cv = reinterpret_cast<const u32x4 *>(col16);
   u32x4 w[U];
+#ifdef LHPC_XT_PROBE_GVAL
+  typedef T gv16 __attribute__((ext_vector_type(16 / sizeof(T))));
+  constexpr int GVN = 8 * sizeof(T) / 16;  // 16-B vectors per 8 entries
+  gv16 gv[U][GVN];
+#endif
   auto load_w = [&](int q) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int qq = q + u * kXtGatherBlock;
       w[u] = qq < q1 ? __builtin_nontemporal_load(cv + qq) : u32x4{0, 0, 0, 0};
+#ifdef LHPC_XT_PROBE_GVAL
+      const gv16 *vp = reinterpret_cast<const gv16 *>(vg + ((static_cast<int64_t>(qq) * 8) & vmask));
+#pragma unroll
+      for (int h = 0; h < GVN; ++h) gv[u][h] = __builtin_nontemporal_load(vp + h);
+#endif
     }
   };
   load_w(q0 + tid);
@@ -80,6 +97,10 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
         o[2 * h] = xt[w[u][h] & 0xFFFFu];
         o[2 * h + 1] = xt[w[u][h] >> 16];
       }
+#ifdef LHPC_XT_PROBE_GVAL
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] *= gv[u][k / (16 / sizeof(T))][k % (16 / sizeof(T))];
+#endif
       // a full 64-group block of the piece is stored wave-coalesced: the
       // plan permuted its col16 (xtile_gather_pos) so that the lane's 16-B
       // vector h lands at block + h·64·VW + VW·lane and every store
@@ -297,7 +318,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   {
     const tvec *vp = reinterpret_cast<const tvec *>(val + vreg) + lane;
 #pragma unroll
-#if defined(LHPC_XT_PROBE_VI)  // timing-only probe: no val / iperm loads
+#if defined(LHPC_XT_PROBE_VI) || defined(LHPC_XT_PROBE_NOVAL)  // timing-only probe: no val (/ iperm) loads
     for (int q = 0; q < NV; ++q) vv[q] = tvec{};
     (void)vp;
 #else
@@ -736,9 +757,23 @@ const void *xtile_reduce_fn(int g, bool ip, bool al) {
 
 template <typename T, int U, bool NT = false>
 void gather_u(const lhpc_spmv_plan *p, const int32_t *pieces, const void *x, int64_t q0, int64_t q1, hipStream_t s) {
+#ifdef LHPC_XT_PROBE_GVAL
+  int64_t vmask = 1;
+  while (vmask * 2 <= p->nnz) vmask *= 2;
+  vmask = (vmask - 1) & ~int64_t{7};
+  if constexpr (U > LHPC_XT_PROBE_GVAL) {
+    gather_u<T, LHPC_XT_PROBE_GVAL, NT>(p, pieces, x, q0, q1, s);
+    return;
+  } else
+    hipLaunchKernelGGL((k_xtile_gather<T, U, NT>), dim3(static_cast<unsigned>(q1 - q0)), dim3(kXtGatherBlock), 0, s,
+                       pieces + 3 * q0, p->d_col16, static_cast<const T *>(x), p->n_cols,
+                       static_cast<int>(p->xs_width), static_cast<T *>(p->d_xg), static_cast<const T *>(p->d_val),
+                       vmask);
+#else
   hipLaunchKernelGGL((k_xtile_gather<T, U, NT>), dim3(static_cast<unsigned>(q1 - q0)), dim3(kXtGatherBlock), 0, s,
                      pieces + 3 * q0, p->d_col16, static_cast<const T *>(x), p->n_cols,
                      static_cast<int>(p->xs_width), static_cast<T *>(p->d_xg));
+#endif
 }
 
 // gather pieces [q0, q1) (default: all) of `pieces` (default: the plan's)

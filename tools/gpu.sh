@@ -6,10 +6,14 @@
 # Output goes to gpurun_out/OUT/ (progress.log + one log per step).  Each STEP
 # is one quoted string; every GPU step runs under its own time limit and the
 # first failure ends the session (no retries):
-#   tests [PYTEST -k EXPR]          the -m gpu suite (-x, per-test 120 s timeout)
+#   tests [PYTEST ARGS]             the -m gpu suite (-x, per-test 120 s timeout); ARGS
+#                                   (test files, -k EXPR) replace the default `tests`
 #   smoke                           __graft_entry__.smoke()
 #   bench NAME [BENCH ARGS]         python bench.py ARGS > NAME.json (the JSON line) + NAME.log
+#   benv NAME K=V[,K=V] [BENCH ARGS]  the same with environment variables set (e.g.
+#                                   LHPC_LIB_PATH=libhpc_amd/_abx/X/liblhpc.so for an A/B build)
 #   stats NAME [BENCH ARGS]         the same under rocprofv3 --kernel-trace --stats (NAME/ dir)
+#   senv NAME K=PATH[,K=PATH] [BENCH ARGS]  stats with K=$REPO/PATH exported first (A/B library paths)
 #   pmc NAME COUNTERS [BENCH ARGS]  one rocprofv3 --pmc pass (COUNTERS comma-separated)
 #   py NAME SCRIPT [ARGS]           python SCRIPT ARGS > NAME.log (tools/*.py probes)
 #   dist NAME NPROC [BENCH ARGS]    bench.py under torch.distributed.run (env passed through)
@@ -32,16 +36,27 @@ for S in "$@"; do
   kind=${A[0]}
   case $kind in
     tests)
-      run pytest_gpu 1100 TERM python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
-        --timeout-method thread "${A[@]:1}" || exit 1 ;;
+      T=("${A[@]:1}"); [ ${#T[@]} -eq 0 ] && T=(tests)
+      run pytest_gpu 1100 TERM python -u -m pytest "${T[@]}" -m gpu -x -v -p no:cacheprovider --timeout 120 \
+        --timeout-method thread || exit 1 ;;
     smoke)
       run smoke 300 TERM python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench)
       run "${A[1]}" 600 TERM python bench.py "${A[@]:2}" || exit 1
       grep '^{' "$O/${A[1]}.log" | tail -1 > "$O/${A[1]}.json" ;;
+    benv)
+      IFS=',' read -ra KV <<< "${A[2]}"
+      run "${A[1]}" 600 TERM env "${KV[@]}" python bench.py "${A[@]:3}" || exit 1
+      grep '^{' "$O/${A[1]}.log" | tail -1 > "$O/${A[1]}.json" ;;
     stats)
       (cd /tmp && run "${A[1]}" 600 TERM rocprofv3 --kernel-trace --stats -d "$O/${A[1]}" -o run -f csv -- \
         python3 "$R/bench.py" "${A[@]:2}") || exit 1
+      grep '^{' "$O/${A[1]}.log" | tail -1 > "$O/${A[1]}.json" ;;
+    senv)
+      IFS=',' read -ra KV <<< "${A[2]}"
+      (for kv in "${KV[@]}"; do export "${kv%%=*}=$R/${kv#*=}"; done
+       cd /tmp && run "${A[1]}" 600 TERM rocprofv3 --kernel-trace --stats -d "$O/${A[1]}" -o run -f csv -- \
+        python3 "$R/bench.py" "${A[@]:3}") || exit 1
       grep '^{' "$O/${A[1]}.log" | tail -1 > "$O/${A[1]}.json" ;;
     pmc)
       (cd /tmp && run "${A[1]}" 240 KILL rocprofv3 --pmc ${A[2]//,/ } -d "$O/${A[1]}" -o run -f csv -- \
