@@ -786,8 +786,14 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
     // default tile: 2 rows × 8 blocks for the dword ring; 2 rows × 4 blocks (256 x) for the
     // x4 ring with LDS-shared halos (512^3, same box, three runs each: 2,8 200.9 µs, 2,4 195.6,
     // 1,8 196.0, 4,8 214.7; 384 / 512 blocks instead of 256: 232-234 µs)
+    // Round 5 (512^3, same box, five interleaved runs each, profiles/r05/stencil_ab.jsonl):
+    // 1 row × 8 blocks (a wave owns 512 consecutive x of one row) 188.4–190.2 µs against
+    // 192.2–195.0 for 2 × 4, so rows of ≥ 512 columns take 1 × 8.  More waves per block
+    // (one z front over 8 or 16 waves' rows) were slower: 196–236 µs.
     const bool x4_default = impl == LHPC_S7_AUTO || impl == LHPC_S7_RING_X4_LDS;
-    int ry = o.stencil7_ry > 0 ? o.stencil7_ry : 2, nj = o.stencil7_nj > 0 ? o.stencil7_nj : (x4_default ? 4 : 8);
+    const bool wide = x4_default && nx >= 512;
+    int ry = o.stencil7_ry > 0 ? o.stencil7_ry : (wide ? 1 : 2),
+        nj = o.stencil7_nj > 0 ? o.stencil7_nj : (x4_default && !wide ? 4 : 8);
     int zc = o.stencil7_zc, pf = o.stencil7_pf;
     // x4 ring by default when every x tile is full (nx % (64·NJ) == 0): 198-211 us against
     // 209-225 us for the dword ring on 512^3, same boxes; "buf" forces the dword ring

@@ -75,7 +75,8 @@ def test_blur_rejects_narrow_ghost(lhpc):
         lhpc.blur_x(a, np.zeros(16, dtype=np.float32), 4, 4, 2, 8)
 
 
-@pytest.mark.parametrize("nz,ny,nx", [(1, 1, 1), (2, 3, 5), (16, 17, 65), (33, 64, 64), (64, 96, 130)])
+@pytest.mark.parametrize("nz,ny,nx", [(1, 1, 1), (2, 3, 5), (16, 17, 65), (33, 64, 64), (64, 96, 130),
+                                      (4, 5, 512), (5, 9, 517), (3, 7, 1100)])  # ≥ 512: the 1 × 8 default tile
 def test_stencil7_vs_oracle(lhpc, gpu, nz, ny, nx):
     g = 1
     shape = (nz + 2, ny + 2, nx + 2)
@@ -149,7 +150,7 @@ def test_stencil7_every_impl(lhpc, gpu, impl, store):
         assert np.array_equal(got, want), (impl, store, nz, ny, nx, g)
 
 
-S7_BUF4 = ["2,8,0", "2,8,5", "1,8,16", "4,8,32", "2,4,7", "4,4,32"]
+S7_BUF4 = ["2,8,0", "2,8,5", "1,8,16", "1,8,0", "4,8,32", "2,4,7", "4,4,32"]
 
 
 @pytest.mark.parametrize("cfg", S7_BUF4)

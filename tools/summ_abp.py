@@ -1,4 +1,4 @@
-"""Summarise tools/gpu_ab_prof.sh output: bench ms/step and per-kernel totals per call."""
+"""Summarise A/B profile output (tools/gpu.sh senv steps): bench ms/step and per-kernel totals per call."""
 import csv
 import glob
 import json
