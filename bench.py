@@ -93,6 +93,14 @@ METRIC = "CSR SpMV GFLOP/s + achieved HBM GB/s, n=10M nnz=150M, at 1/2/4/8 MI355
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
+def parse_options(text):
+    """--spmv-options: a JSON dict, or k=v[,k=v] (integers) — the form that
+    survives shell quoting in tools/gpu.sh steps."""
+    if text is None or text.strip().startswith("{"):
+        return json.loads(text) if text else None
+    return {k.strip(): int(v) for k, v in (kv.split("=", 1) for kv in text.split(",") if kv.strip())}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,8 +118,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt-kernels", action="store_true",
                     help="skip the other kernel families' C2-C4 times (alt_kernels: ADAPTIVE, ROWGROUP, XSLICE)")
-    ap.add_argument("--spmv-options", default=None,
-                    help="JSON dict of lhpc_options fields for the 1-GPU SpMV plan (measured alternatives, DESIGN.md §4)")
+    ap.add_argument("--spmv-options", default=None, type=parse_options,
+                    help="lhpc_options fields for the 1-GPU SpMV plan (measured alternatives, DESIGN.md §4): a JSON "
+                         "dict or k=v[,k=v] with integer values")
     ap.add_argument("--dtype", default="auto", choices=["auto", "f32", "f64"],
                     help="SpMV value type (auto: the config's own — fp64 for c1/c3, fp32 for c2/c4; "
                          "SURVEY §8d also runs C4 in fp64)")
@@ -264,7 +273,7 @@ def main():
         t0 = time.time()
         if world == 1 and not native_dist:
             plans = [L.SpMVPlan(rp, col, val, n,
-                                options=json.loads(args.spmv_options) if args.spmv_options else None)]
+                                options=args.spmv_options)]
             local_nnz, local_rows = nnz, n
             y_local = torch.empty(n, dtype=xd.dtype, device=dev)
 
@@ -523,7 +532,7 @@ def main():
             torch.cuda.synchronize()
             t0 = time.time()
             pdev = L.SpMVPlan(drp, dcol, dval, n,
-                              options=json.loads(args.spmv_options) if args.spmv_options else None)
+                              options=args.spmv_options)
             t_plan_dev = time.time() - t0
             try:
                 same = pdev.layout_digest() == plans[0].layout_digest()

@@ -57,3 +57,9 @@ def test_refusal_exits_nonzero_before_any_gpu_call():
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
     assert "GPU(s) visible" in r.stderr and not r.stdout.strip()
+
+
+def test_spmv_options_forms():
+    assert bench.parse_options(None) is None
+    assert bench.parse_options('{"xtile_steps": 4}') == {"xtile_steps": 4}
+    assert bench.parse_options("xtile_steps=4,xtile_piece=150000") == {"xtile_steps": 4, "xtile_piece": 150000}
