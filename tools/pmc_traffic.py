@@ -75,7 +75,7 @@ def main():
         wb = write.get(k, 0.0)
         ent["kernels"][k] = {"read_bytes": rb, "write_bytes": wb, "dispatches": n[k],
                              "raw_fetch_bytes": fetch[k], "launches_per_call": per_call.get(k, 1)}
-        if k.startswith("k_copyw"):  # bench.py's copy-ceiling probe, not part of the workload
+        if k.startswith("k_copy"):  # bench.py copy / read ceiling probes, not part of the workload
             ent["kernels"][k]["probe"] = True
             continue
         if k in PLAN_BUILD:  # device-side plan build (once per plan, not per call)
