@@ -572,6 +572,7 @@ def main():
         step_ms = np.array([sev[i].elapsed_time(sev[i + 1]) for i in range(args.steps)])
         t_ev = ev0.elapsed_time(ev1) * 1e-3
         elapsed = max(t_wall, t_ev)
+        timing = {"wall_s": t_wall, "events_s": t_ev, "value_from": "wall" if t_wall >= t_ev else "events"}
         if world > 1:
             tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -627,6 +628,7 @@ def main():
             roofline={"bound": "hbm", "kernel": kernels, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                       "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                       "alg_bytes_per_call": local_alg, "call_us": call_s * 1e6},
+            timing=timing,
             step_ms={"median": float(np.median(step_ms)), "p10": float(np.percentile(step_ms, 10)),
                      "p90": float(np.percentile(step_ms, 90)),
                      "source": "rank 0 HIP events per step, in a second untimed pass of the same K steps"},

@@ -1076,6 +1076,9 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   p->xt_cont = static_cast<int64_t>(xt.cont.size());
   p->xt_total = xt.total;
   p->xt_lds = xtile_lds_bytes<T>(xt.S);
+#ifdef LHPC_XT_LDS_TOTAL  // A/B build only: reduce blocks padded to this many bytes of LDS (fewer per CU)
+  if (sizeof(T) == 4) p->xt_lds = std::max<size_t>(p->xt_lds, LHPC_XT_LDS_TOTAL);
+#endif
   if (o.xtile_steps > 0) {
     const int u = o.xtile_steps;
     p->xt_u = u <= 2 ? 2 : u < 8 ? 4 : u < 16 ? 8 : 16;
