@@ -116,6 +116,11 @@ def parse():
                          "K = 1, 2, 4 and reports the fastest (the step model, tools/step_model.py, puts K = 4 "
                          "first at 64 GB/s per xGMI link, DESIGN.md §6.3); other paths use 4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="N=1: run the step back to back for this long before the W warmup steps (0: off) — the "
+                         "device's clocks ramp over the first ~10-15 ms of sustained load after an idle gap "
+                         "(round 5: C2 call 479-483 -> 462-465 us on one box, 462 -> 435 on another, profiles/r05/ramp*.jsonl; 40 ms "
+                         "of settle left part of it, 100 ms all of it); reported as `settle`")
     ap.add_argument("--no-alt-kernels", action="store_true",
                     help="skip the other kernel families' C2-C4 times (alt_kernels: ADAPTIVE, ROWGROUP, XSLICE)")
     ap.add_argument("--spmv-options", default=None, type=parse_options,
@@ -146,6 +151,32 @@ def load_traffic(kernel_tag):
         return d.get(kernel_tag, {}).get("bytes_per_call")
     except Exception:
         return None
+
+
+def settle(fn, torch, ms, end=None):
+    """Keep the device busy with `fn` (one step) for `ms` milliseconds before
+    the warmup, so the timed steps do not straddle the clock ramp that
+    follows an idle gap (host-side setup: data generation, plan builds,
+    layout checks).  Untimed; the W warmup and K timed steps are unchanged.
+    N = 1 only (a time-based loop would give ranks different step counts);
+    the N > 1 paths time their exchange candidates just before the headline
+    loop, which keeps the devices under load."""
+    if ms <= 0:
+        return {"ms": 0.0, "steps": 0}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = 0
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        fn()
+        n += 1
+        if n % 16 == 0:
+            torch.cuda.synchronize()  # keep the host within a few steps of the device
+    if end is not None:
+        end()
+    torch.cuda.synchronize()
+    return {"ms": (time.perf_counter() - t0) * 1e3, "steps": n,
+            "why": "device clocks ramp over the first ~10-15 ms of sustained load after an idle gap "
+                   "(DESIGN.md §5, profiles/r05/ramp.jsonl); untimed, before the W warmup steps"}
 
 
 def launch_decision(gpus, env, visible, argv, port=0):
@@ -544,6 +575,7 @@ def main():
 
         if step_end is None:
             step_end = lambda: None  # noqa: E731
+        settled = settle(step, torch, args.settle_ms if world == 1 else 0.0, step_end)
         for _ in range(args.warmup):
             step()
         step_end()
@@ -592,7 +624,11 @@ def main():
                 pl(xd, ysc[:pl.n_rows], stream=stream)
         kev1.record(stream)
         torch.cuda.synchronize()
-        call_s = kev0.elapsed_time(kev1) * 1e-3 / reps
+        call_loop_s = kev0.elapsed_time(kev1) * 1e-3 / reps
+        # N = 1: the call time is the timed region's own (HIP events on the
+        # launch stream around exactly the K timed steps); N > 1 steps hold the
+        # exchange too, so there the kernel-only loop above gives the call
+        call_s = t_ev / args.steps if (world == 1 and not native_dist) else call_loop_s
         local_alg = local_nnz * (tsz + 4) + (local_rows + len(plans)) * 4 + (n + local_rows) * tsz
         achieved = local_alg / call_s / 1e9
         kname = {L.KERNEL_XSLICE: "xslice", L.KERNEL_ROWGROUP: "rowgroup",
@@ -627,8 +663,10 @@ def main():
             achieved_GBps=alg_bytes / per_step / 1e9,
             roofline={"bound": "hbm", "kernel": kernels, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                       "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                      "alg_bytes_per_call": local_alg, "call_us": call_s * 1e6},
-            timing=timing,
+                      "alg_bytes_per_call": local_alg, "call_us": call_s * 1e6,
+                      "call_us_source": "HIP events over the timed region" if (world == 1 and not native_dist)
+                      else "kernel-only loop of the rank's local calls", "call_us_kernel_loop": call_loop_s * 1e6},
+            timing=timing, settle=settled,
             step_ms={"median": float(np.median(step_ms)), "p10": float(np.percentile(step_ms, 10)),
                      "p90": float(np.percentile(step_ms, 90)),
                      "source": "rank 0 HIP events per step, in a second untimed pass of the same K steps"},
@@ -973,6 +1011,7 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
         cells = n * n
         name = "k_blur_x" if wl == "blur_x" else "k_blur_y"
         workload = f"reference BM_{wl} grid: 8192^2 fp32, ghost 8, 17 taps"
+    settled = settle(fn, torch, args.settle_ms if world == 1 else 0.0)
     for _ in range(args.warmup):
         fn()
     barrier()
@@ -994,6 +1033,7 @@ def stencil_bench(args, L, torch, dev, stream, barrier):
     out = dict(metric=f"{wl} Gcell/s (8 B/cell algorithmic)", value=cells / per / 1e9, unit="Gcell/s",
                n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=per * 1e3,
                higher_is_better=True, scaling="strong" if wl == "c5" else "weak", vs_baseline=None, dtype="f32",
+               settle=settled,
                data="synthetic U[-1,1)", config={"workload": workload},
                roofline={"bound": "hbm", "kernel": name, "achieved": ach, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,
@@ -1082,6 +1122,7 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
             x = torch.zeros_like(bd)
             return solver.solve(bd, x, tol=0.0, max_iter=iters, check_every=iters)  # tol 0: exactly `iters` iterations
 
+    settled = settle(lambda: run(10), torch, args.settle_ms if world == 1 else 0.0)
     run(max(10, args.warmup))
     barrier()
     t0 = time.perf_counter()
@@ -1100,7 +1141,7 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
     alg = (spmv_b + vec_b) / world
     out = dict(metric="CG iterations/s, 2-D Laplacian 4096^2 fp64 (SURVEY 8f rank 3)", value=1.0 / per,
                unit="iter/s", n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=per * 1e3,
-               higher_is_better=True, scaling="strong", vs_baseline=None, dtype="f64",
+               higher_is_better=True, scaling="strong", vs_baseline=None, dtype="f64", settle=settled,
                data="synthetic: 5-point Laplacian, b = U[-1,1) (SEED_X)",
                config={"workload": f"CG, 2-D Laplacian {nx}^2 fp64, n={n}, nnz={nnz}, {world} GPU(s)",
                        "iterations": it, "relres": res,
@@ -1145,9 +1186,13 @@ def sort_bench(args, L, torch, dev, stream, barrier, world, rank):
     g.manual_seed(0x5EED0006 + rank)
     src = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device=dev, generator=g)
     keys = torch.empty_like(src)
-    for _ in range(args.warmup):
+
+    def one_sort():
         keys.copy_(src)
         L.radix_sort(keys, stream=stream)
+    settled = settle(one_sort, torch, args.settle_ms if world == 1 else 0.0)
+    for _ in range(args.warmup):
+        one_sort()
     barrier()
     total = 0.0
     for _ in range(args.steps):
@@ -1172,6 +1217,7 @@ def sort_bench(args, L, torch, dev, stream, barrier, world, rank):
     out = dict(metric="radix sort G keys/s, 500M uint32 keys (reference README.md:52)", value=value,
                unit="Gkeys/s", n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=per * 1e3,
                higher_is_better=True, scaling="weak", vs_baseline=value / world / SORT_REF_GKEYS, dtype="u32",
+               settle=settled,
                data="synthetic uniform uint32 (torch generator)",
                config={"workload": "reference README radix-sort config: 500M uint32 keys, 1 GPU"
                        + (f" x{world} replicas" if world > 1 else ""), "sorted": ok},
