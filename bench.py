@@ -631,10 +631,10 @@ def main():
         call_s = t_ev / args.steps if (world == 1 and not native_dist) else call_loop_s
         local_alg = local_nnz * (tsz + 4) + (local_rows + len(plans)) * 4 + (n + local_rows) * tsz
         achieved = local_alg / call_s / 1e9
-        kname = {L.KERNEL_XSLICE: "xslice", L.KERNEL_ROWGROUP: "rowgroup",
-                 L.KERNEL_ADAPTIVE: "adaptive", L.KERNEL_XTILE: "xtile"}[info["kernel"]]
+        kname = {L.KERNEL_XSLICE: "xslice", L.KERNEL_ROWGROUP: "rowgroup", L.KERNEL_ADAPTIVE: "adaptive",
+                 L.KERNEL_XTILE: "xtile", L.KERNEL_SELL: "sell"}[info["kernel"]]
         kernels = {"xslice": "k_spmv_xslice+k_xslice_reduce", "rowgroup": "k_spmv_rowgroup",
-                   "adaptive": "k_spmv_adaptive",
+                   "adaptive": "k_spmv_adaptive", "sell": "k_spmv_sell",
                    "xtile": "k_xtile_gather+k_xtile_reduce" + ("+k_xtile_fixup" if info["n_long_rows"] else "")}[kname]
         traffic = load_traffic(f"{wl}{dtag}_{kname}") if world == 1 else None
         result.update(
@@ -752,7 +752,7 @@ def alt_kernels(L, torch, dev, stream, rp, col, val, xd, n, nnz, args):
         torch.cuda.synchronize()
         t = e0.elapsed_time(e1) * 1e-3 / 10
         kern = {L.KERNEL_XSLICE: "xslice", L.KERNEL_ROWGROUP: "rowgroup", L.KERNEL_ADAPTIVE: "adaptive",
-                L.KERNEL_XTILE: "xtile"}[pl.info()["kernel"]]
+                L.KERNEL_XTILE: "xtile", L.KERNEL_SELL: "sell"}[pl.info()["kernel"]]
         pl.close()
         out[name] = {"gflops": 2.0 * nnz / t / 1e9, "call_us": t * 1e6, "kernel": kern, "plan_s": t_plan}
     del y
@@ -1099,7 +1099,7 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
         # lhpc_cg_solve: the native loop, whose check_every = 10 iterations
         # between two convergence checks replay as one captured HIP graph
         # (tol 0: exactly `iters` iterations; the warmup solve captures it)
-        plan = L.SpMVPlan(rp, col, val, n)
+        plan = L.SpMVPlan(rp, col, val, n, options=args.spmv_options)  # SELL (spmv_no_sell=1: ADAPTIVE)
         bfull = torch.from_numpy(b).to(dev)
         cg_stream = torch.cuda.Stream(dev)
 
@@ -1139,17 +1139,20 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
     # x/p update (read x p r, write x p: 5n) — k_cg_r + k_cg_xp
     vec_b = 9 * n * 8
     alg = (spmv_b + vec_b) / world
+    kid = dplan.local_info()["kernel"] if native else plan.info()["kernel"]
+    kname = {L.KERNEL_ROWGROUP: "rowgroup", L.KERNEL_ADAPTIVE: "adaptive", L.KERNEL_XSLICE: "xslice",
+             L.KERNEL_XTILE: "xtile", L.KERNEL_SELL: "sell"}[kid]
     out = dict(metric="CG iterations/s, 2-D Laplacian 4096^2 fp64 (SURVEY 8f rank 3)", value=1.0 / per,
                unit="iter/s", n_gpus=world, steps=args.steps, warmup=args.warmup, ms_per_step=per * 1e3,
                higher_is_better=True, scaling="strong", vs_baseline=None, dtype="f64", settle=settled,
                data="synthetic: 5-point Laplacian, b = U[-1,1) (SEED_X)",
                config={"workload": f"CG, 2-D Laplacian {nx}^2 fp64, n={n}, nnz={nnz}, {world} GPU(s)",
                        "iterations": it, "relres": res,
-                       "kernel": dplan.local_info()["kernel"] if native else plan.info()["kernel"],
+                       "kernel": kid, "kernel_name": kname,
                        "solver": "lhpc_dist_cg_solve (native, RCCL, chained stages)" if native else
                                  ("lhpc_cg_solve (native loop, 10-iteration HIP graph blocks)" if world == 1 else
                                   "DistCG over torch.distributed")},
-               roofline={"bound": "hbm", "kernel": "spmv_dot + k_cg_r + k_cg_xp",
+               roofline={"bound": "hbm", "kernel": f"spmv_dot (k_spmv_{kname}) + k_cg_r + k_cg_xp",
                          "achieved": alg / per / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": alg / per / 1e9 / HBM_PEAK_GBPS, "traffic": None,
                          "alg_bytes_per_iter": alg})

@@ -82,7 +82,8 @@ enum lhpc_plan_flags {
    * kept as a flag for callers that name it.                               */
   LHPC_PLAN_FAST_PARTIALS = 1u << 7,
   LHPC_PLAN_EXACT_PARTIALS = 1u << 8,
-  LHPC_PLAN_FORCE_XTILE = 1u << 9
+  LHPC_PLAN_FORCE_XTILE = 1u << 9,
+  LHPC_PLAN_FORCE_SELL = 1u << 10  /* LHPC_ERR_UNSUPPORTED past 8 nonzeros per row */
 };
 
 /* kernel families a plan can select (lhpc_spmv_plan_info.kernel)          */
@@ -90,7 +91,8 @@ enum lhpc_spmv_kernel {
   LHPC_KERNEL_ROWGROUP = 0, /* L lanes per row, wave64 DPP reduction        */
   LHPC_KERNEL_ADAPTIVE = 1, /* nnz-balanced row blocks + long-row split     */
   LHPC_KERNEL_XSLICE = 2,   /* XCD-local column slices + partial reduce     */
-  LHPC_KERNEL_XTILE = 3     /* x tiles in LDS: tile gather + chunk reduce   */
+  LHPC_KERNEL_XTILE = 3,    /* x tiles in LDS: tile gather + chunk reduce   */
+  LHPC_KERNEL_SELL = 4      /* rows ≤ 8 nonzeros: lane per row, 64-row slices */
 };
 
 typedef struct lhpc_spmv_plan lhpc_spmv_plan;
@@ -101,7 +103,7 @@ typedef struct lhpc_spmv_plan_info {
   int lanes_per_row;   /* ROWGROUP: L in {4,8,16,32,64}                     */
   int rows_per_group;  /* ROWGROUP: rows per lane group per launch step     */
   int64_t n_rows, n_cols, nnz;
-  int64_t n_blocks;    /* ADAPTIVE: row blocks                              */
+  int64_t n_blocks;    /* ADAPTIVE / SELL: row blocks (SELL: 256 rows each)  */
   int64_t n_long_rows; /* ADAPTIVE: rows split across workgroups            */
   int64_t device_bytes;/* HBM held by the plan                              */
   int device;          /* HIP device ordinal                                */
@@ -213,6 +215,9 @@ typedef struct lhpc_options {
    * the GPU (byte-identical to the host build, several times faster), 1
    * builds on the host (tests compare the two)                              */
   int32_t xtile_host_build;
+  /* 1: short rows with x locality stay on ADAPTIVE instead of SELL (rows of
+   * ≤ 8 nonzeros whose padded slices stream no more bytes than CSR)        */
+  int32_t spmv_no_sell;
 } lhpc_options;
 void lhpc_options_init(lhpc_options *opts);
 

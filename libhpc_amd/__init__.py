@@ -29,7 +29,7 @@ __all__ = [
     "csr_partition_rows", "blur_x", "blur_y", "stencil7", "stencil7_planes",
     "gen_uniform_csr", "gen_powerlaw_csr", "gen_values", "padded_shape",
     "PLAN_VALIDATE", "PLAN_FORCE_ROWGROUP", "PLAN_FORCE_ADAPTIVE", "PLAN_FORCE_XSLICE", "PLAN_FAST_PARTIALS", "PLAN_EXACT_PARTIALS",
-    "PLAN_FORCE_XTILE", "KERNEL_XTILE",
+    "PLAN_FORCE_XTILE", "PLAN_FORCE_SELL", "KERNEL_XTILE", "KERNEL_SELL",
     "KERNEL_ROWGROUP", "KERNEL_ADAPTIVE", "KERNEL_XSLICE",
 ]
 
@@ -46,7 +46,8 @@ PLAN_FORCE_XSLICE = 1 << 6
 PLAN_FAST_PARTIALS = 1 << 7
 PLAN_EXACT_PARTIALS = 1 << 8
 PLAN_FORCE_XTILE = 1 << 9
-KERNEL_ROWGROUP, KERNEL_ADAPTIVE, KERNEL_XSLICE, KERNEL_XTILE = 0, 1, 2, 3
+PLAN_FORCE_SELL = 1 << 10
+KERNEL_ROWGROUP, KERNEL_ADAPTIVE, KERNEL_XSLICE, KERNEL_XTILE, KERNEL_SELL = 0, 1, 2, 3, 4
 
 # every symbol include/lhpc.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = (
@@ -112,7 +113,7 @@ class Options(C.Structure):
                 ("blur_y_rows", C.c_int32), ("dist_exchange", C.c_int32), ("dist_broadcast", C.c_int32),
                 ("dist_world1", C.c_int32), ("xtile_part_nnz", C.c_int32), ("multi_chunks", C.c_int32),
                 ("multi_exchange", C.c_int32), ("multi_force", C.c_int32), ("dist_reduce_streams", C.c_int32),
-                ("xtile_col_blocks", C.c_int32), ("xtile_host_build", C.c_int32)]
+                ("xtile_col_blocks", C.c_int32), ("xtile_host_build", C.c_int32), ("spmv_no_sell", C.c_int32)]
 
     def __init__(self, **kw):
         super().__init__()

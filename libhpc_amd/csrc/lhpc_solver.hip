@@ -385,13 +385,14 @@ int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int
   // checks — C − 1 full iterations and the C-th up to rr' — captured once per
   // starting parity of the rr pair and replayed (one launch instead of ≈ 5C;
   // the same kernels in the same order, so x is bit-identical to the loop's).
-  // ADAPTIVE plans only (their fused dot allocates nothing after the first
-  // call, which the x·x warm-up below makes); not on the null stream, not
+  // ADAPTIVE / SELL plans only (their fused dot allocates nothing after the
+  // first call, which the x·x warm-up below makes); not on the null stream, not
   // for multi-device plans, not in the synchronous-check debug build.
 #ifdef LHPC_DEBUG_SYNC
   bool graphs = false;
 #else
-  bool graphs = s != nullptr && check_every >= 4 && plan->kernel == LHPC_KERNEL_ADAPTIVE && !plan->multi &&
+  bool graphs = s != nullptr && check_every >= 4 &&
+                (plan->kernel == LHPC_KERNEL_ADAPTIVE || plan->kernel == LHPC_KERNEL_SELL) && !plan->multi &&
                 plan->parts.empty() && plan->n_blocks > 0;
 #endif
   // kept with the plan: every pointer in them (the plan's arrays and work)

@@ -414,7 +414,7 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
   // uniform columns, ≈0.03 for a 2-D Laplacian); ≤ 0.25 counts as local.
   const double locality_thr = o.spmv_locality > 0 ? o.spmv_locality : 0.25;
   const bool auto_ok = !(flags & (LHPC_PLAN_FORCE_ROWGROUP | LHPC_PLAN_FORCE_ADAPTIVE |
-                                   LHPC_PLAN_FORCE_XSLICE | LHPC_PLAN_FORCE_XTILE));
+                                   LHPC_PLAN_FORCE_XSLICE | LHPC_PLAN_FORCE_XTILE | LHPC_PLAN_FORCE_SELL));
   const bool nolocal =
       auto_ok && x_bytes > 8.0e6 && gather_lines_per_nnz(
           rp,
@@ -497,6 +497,27 @@ int plan_create_impl(lhpc_spmv_plan **out, int dtype, int64_t n_rows, int64_t n_
     }
     p->L = o.rowgroup_lanes;
     p->R = o.rowgroup_rows;
+  }
+
+  // SELL for short rows (≤ 8 nonzeros) whose padded slices stream no more
+  // bytes than CSR + row_ptr: bit-identical to ADAPTIVE, no row_ptr stream,
+  // LDS or barrier (the CG Laplacian: DESIGN.md §4)
+  const bool force_sell = (flags & LHPC_PLAN_FORCE_SELL) != 0;
+  if (p->kernel == LHPC_KERNEL_ADAPTIVE && (force_sell || (auto_ok && !o.spmv_no_sell)) && maxlen <= kSellMaxW &&
+      n_rows > 0) {
+    const int st = sell_build(p, rp, col_idx, val, tsz, force_sell);
+    if (st == LHPC_OK) {
+      *out = p;
+      return LHPC_OK;
+    }
+    if (st != LHPC_ERR_UNSUPPORTED) {
+      lhpc_spmv_plan_destroy(p);
+      return st;
+    }
+  }
+  if (force_sell) {
+    lhpc_spmv_plan_destroy(p);
+    return LHPC_ERR_UNSUPPORTED;  // a row longer than kSellMaxW (or no rows)
   }
 
   int st = LHPC_OK;
@@ -598,7 +619,7 @@ int plan_create_device_input(lhpc_spmv_plan **out, int dtype, int64_t n_rows, in
   const double x_bytes = static_cast<double>(n_cols) * static_cast<double>(tsz);
   const double locality_thr = o.spmv_locality > 0 ? o.spmv_locality : 0.25;
   const bool auto_ok = !(flags & (LHPC_PLAN_FORCE_ROWGROUP | LHPC_PLAN_FORCE_ADAPTIVE | LHPC_PLAN_FORCE_XSLICE |
-                                   LHPC_PLAN_FORCE_XTILE));
+                                   LHPC_PLAN_FORCE_XTILE | LHPC_PLAN_FORCE_SELL));
   const int64_t tiles = (n_cols + (tsz == 4 ? 40960 : 20480) - 1) / (tsz == 4 ? 40960 : 20480);
   int64_t cap = INT32_MAX - 8 * (tiles + 256) - (int64_t{1} << 16);
   if (o.xtile_part_nnz > 0) cap = std::min<int64_t>(cap, o.xtile_part_nnz);
@@ -751,7 +772,7 @@ extern "C" int lhpc_spmv_dot(lhpc_spmv_plan *p, const void *x, void *y, const vo
   if (!p || !dot_out || (p->n_cols > 0 && !x) || (p->n_rows > 0 && (!y || !w))) return LHPC_ERR_INVALID_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
   LHPC_HIP_TRY(hipSetDevice(p->device));
-  if (p->kernel == LHPC_KERNEL_ADAPTIVE && p->n_blocks > 0) {
+  if ((p->kernel == LHPC_KERNEL_ADAPTIVE || p->kernel == LHPC_KERNEL_SELL) && p->n_blocks > 0) {
     const int st = csr_launch_dot(p, x, y, w, dot_out, s);
     if (st != LHPC_ERR_UNSUPPORTED) return st;
   }
@@ -782,6 +803,10 @@ extern "C" int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *p, lhpc_spmv_plan_i
   }
   info->slices = p->S;
   info->slice_width = p->xs_width;
+  if (p->kernel == LHPC_KERNEL_SELL) {  // 64-row slices, widest slice in nonzeros
+    info->slices = static_cast<int>((p->n_rows + kWave - 1) / kWave);
+    info->slice_width = p->sell_w;
+  }
   if (!p->parts.empty()) {  // XTILE row parts: totals over the parts
     info->launches = 0;
     info->n_blocks = 0;

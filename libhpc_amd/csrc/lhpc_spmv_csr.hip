@@ -11,10 +11,22 @@
 //             in LDS, and reduces each row with L = 256/rows lanes; a row
 //             longer than kBlockNnz gets a workgroup to itself.  For skewed
 //             (power-law) row lengths.  Deterministic: fixed trees only.
-// Both read val/col_idx with non-temporal loads (streamed once) so the
+//   SELL      short rows (≤ kSellMaxW nonzeros) with x locality: rows in
+//             64-row slices, lane = row, entry j of every row of a slice
+//             stored together (64 cols, then 64 vals, per j; padding col −1),
+//             so the wave streams W coalesced col/val loads and keeps W
+//             gathers in flight with no row_ptr, LDS or barrier.  Bit-
+//             identical to ADAPTIVE on the same matrix: with ≤ 8 nonzeros per
+//             row ADAPTIVE's blocks are 256 rows with one lane per row, which
+//             adds the same products in the same order (a last block of ≤ 128
+//             rows uses L lanes per row: SELL then sums in that order), and
+//             the dot epilogue has the same tree.
+// All read val/col_idx with non-temporal loads (streamed once) so the
 // gathered x keeps its place in L2 / Infinity Cache.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "lhpc_spmv_impl.hpp"
@@ -193,6 +205,96 @@ __global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
   }
 }
 
+// ------------------------------------------------------------- SELL
+// The value ADAPTIVE computes for a row of ≤ 8 products p[] with L ≥ 2 lanes
+// per row: lane s sums p[s], p[s + L], … from 0.0, then group_sum<L> pairs the
+// lane sums as the tree (0+1)+(2+3)… (its butterfly steps are symmetric, so
+// every lane holds that tree).  Lanes ≥ 8 hold 0.0, which adds nothing.
+__device__ __forceinline__ double adaptive_lane_order(const double (&p)[kSellMaxW], int L) {
+#pragma clang fp contract(off)
+  if (L == 2) {
+    const double q0 = ((p[0] + p[2]) + p[4]) + p[6], q1 = ((p[1] + p[3]) + p[5]) + p[7];
+    return q0 + q1;
+  }
+  if (L == 4) return ((p[0] + p[4]) + (p[1] + p[5])) + ((p[2] + p[6]) + (p[3] + p[7]));
+  return ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+}
+
+// soff[s] = first entry of slice s (a multiple of 64); its width is
+// (soff[s + 1] − soff[s]) / 64 ≤ kSellMaxW.  One block = 4 slices = the
+// 256 rows of ADAPTIVE's block blockIdx.x.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_spmv_sell(const int32_t *__restrict__ col, const T *__restrict__ val,
+                                                      const int64_t *__restrict__ soff, const T *__restrict__ x,
+                                                      T *__restrict__ y, int64_t n_rows, const T *__restrict__ w,
+                                                      double *__restrict__ dpart) {
+#pragma clang fp contract(off)  // the product rounds before the add, as ADAPTIVE's LDS-staged products do
+  __shared__ double wsum[kBlock / kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t slice = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + threadIdx.x / kWave;
+  const int64_t row = slice * kWave + lane;
+  double a = 0.0;
+  T wv = T(0);
+  if (slice * kWave < n_rows) {  // wave-uniform
+    const int64_t o0 = soff[slice];
+    const int W = static_cast<int>((soff[slice + 1] - o0) / kWave);
+    if (w && row < n_rows) wv = w[row];
+    int32_t c[kSellMaxW];
+    T v[kSellMaxW];
+#pragma unroll
+    for (int j = 0; j < kSellMaxW; ++j) {
+      c[j] = -1;
+      v[j] = T(0);
+      if (j < W) {
+        c[j] = ld_stream(col + o0 + j * kWave + lane);
+        v[j] = ld_stream(val + o0 + j * kWave + lane);
+      }
+    }
+    T xv[kSellMaxW];
+#pragma unroll
+    for (int j = 0; j < kSellMaxW; ++j) xv[j] = c[j] >= 0 ? x[c[j]] : T(0);
+    double pr[kSellMaxW];  // padding: 0·0 = 0, which adds nothing
+#pragma unroll
+    for (int j = 0; j < kSellMaxW; ++j) pr[j] = static_cast<double>(v[j]) * static_cast<double>(xv[j]);
+    // ADAPTIVE's lanes per row in this block: 1 for every full block (256
+    // rows); a last block of ≤ 128 rows gives L = 2 … 64 — sum in its order
+    const int64_t nb = n_rows - static_cast<int64_t>(blockIdx.x) * kBlock;
+    int L = kWave;
+    while (L > 1 && nb * L > kBlock) L >>= 1;
+    if (L == 1) {
+#pragma unroll
+      for (int j = 0; j < kSellMaxW; ++j)
+        if (j < W) a += pr[j];
+    } else {
+      a = adaptive_lane_order(pr, L);
+    }
+  }
+  const T yv = static_cast<T>(a);
+  if (row < n_rows) y[row] = yv;
+  if (w) {  // block-uniform: ADAPTIVE's epilogue tree (one lane per row)
+    double d = row < n_rows ? static_cast<double>(yv) * static_cast<double>(wv) : 0.0;
+    d = group_sum<kWave>(d);
+    if (lane == 0) wsum[threadIdx.x / kWave] = d;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = wsum[0];
+#pragma unroll
+      for (int i = 1; i < kBlock / kWave; ++i) t += wsum[i];
+      dpart[blockIdx.x] = t;
+    }
+  }
+}
+
+template <typename T>
+int launch_sell(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s, const void *w = nullptr,
+                double *dpart = nullptr) {
+  if (p->n_blocks == 0) return LHPC_OK;
+  hipLaunchKernelGGL((k_spmv_sell<T>), dim3(static_cast<unsigned>(p->n_blocks)), dim3(kBlock), 0, s, p->d_col,
+                     static_cast<const T *>(p->d_val), p->d_blocks, static_cast<const T *>(x), static_cast<T *>(y),
+                     p->n_rows, static_cast<const T *>(w), dpart);
+  return check_launch(s);
+}
+
 template <typename T, typename I, int L, int R>
 int launch_rowgroup_t(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
   constexpr int WR = (kWave / L) * R;
@@ -293,8 +395,54 @@ std::vector<int64_t> csr_build_blocks(RowPtrView rp, int64_t n_rows, int64_t &n_
   return b;
 }
 
+// SELL layout (see k_spmv_sell): LHPC_ERR_UNSUPPORTED when a row has more
+// than kSellMaxW nonzeros, or (auto) when the padding would stream more
+// bytes than CSR with its row_ptr.  Sets kernel, n_blocks (256-row blocks,
+// ADAPTIVE's own for such rows) and d_blocks = the slice offsets.
+int sell_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz, bool forced) {
+  const int64_t n = p->n_rows, S = (n + kWave - 1) / kWave;
+  std::vector<int64_t> off(static_cast<size_t>(S) + 1, 0);
+  int wmax = 0;
+  for (int64_t s = 0; s < S; ++s) {
+    int64_t W = 0;
+    for (int64_t i = s * kWave; i < std::min(n, (s + 1) * kWave); ++i) W = std::max(W, rp[i + 1] - rp[i]);
+    if (W > kSellMaxW) return LHPC_ERR_UNSUPPORTED;
+    wmax = std::max(wmax, static_cast<int>(W));
+    off[static_cast<size_t>(s) + 1] = off[static_cast<size_t>(s)] + W * kWave;
+  }
+  const int64_t total = off[static_cast<size_t>(S)];
+  const double sell_b = static_cast<double>(total) * static_cast<double>(4 + tsz) + 8.0 * static_cast<double>(S);
+  const double csr_b = static_cast<double>(p->nnz) * static_cast<double>(4 + tsz) + 4.0 * static_cast<double>(n + 1);
+  if (!forced && sell_b > csr_b) return LHPC_ERR_UNSUPPORTED;
+  std::vector<int32_t> c(static_cast<size_t>(total), -1);
+  std::vector<unsigned char> v(static_cast<size_t>(total) * tsz, 0);
+  const unsigned char *vin = static_cast<const unsigned char *>(val);
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t b = off[static_cast<size_t>(i / kWave)] + (i % kWave), k0 = rp[i], len = rp[i + 1] - k0;
+    for (int64_t j = 0; j < len; ++j) {
+      c[static_cast<size_t>(b + j * kWave)] = col_idx[k0 + j];
+      std::memcpy(&v[static_cast<size_t>(b + j * kWave) * tsz], vin + static_cast<size_t>(k0 + j) * tsz, tsz);
+    }
+  }
+  LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_col), static_cast<size_t>(total) * 4, p->bytes));
+  LHPC_TRY(dmalloc(&p->d_val, static_cast<size_t>(total) * tsz, p->bytes));
+  LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_blocks), off.size() * 8, p->bytes));
+  if (total) {
+    LHPC_HIP_TRY(hipMemcpy(p->d_col, c.data(), c.size() * 4, hipMemcpyHostToDevice));
+    LHPC_HIP_TRY(hipMemcpy(p->d_val, v.data(), v.size(), hipMemcpyHostToDevice));
+  }
+  LHPC_HIP_TRY(hipMemcpy(p->d_blocks, off.data(), off.size() * 8, hipMemcpyHostToDevice));
+  p->kernel = LHPC_KERNEL_SELL;
+  p->n_blocks = (n + kBlock - 1) / kBlock;
+  p->n_long = 0;
+  p->sell_w = wmax;
+  p->sell_total = total;
+  return LHPC_OK;
+}
+
 int csr_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
   const bool f32 = p->dtype == LHPC_F32;
+  if (p->kernel == LHPC_KERNEL_SELL) return f32 ? launch_sell<float>(p, x, y, s) : launch_sell<double>(p, x, y, s);
   if (p->kernel == LHPC_KERNEL_ADAPTIVE)
     return f32 ? (p->rp64 ? launch_adaptive<float, int64_t>(p, x, y, s) : launch_adaptive<float, int32_t>(p, x, y, s))
                : (p->rp64 ? launch_adaptive<double, int64_t>(p, x, y, s) : launch_adaptive<double, int32_t>(p, x, y, s));
@@ -303,13 +451,17 @@ int csr_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s) {
 }
 
 int csr_launch_dot(lhpc_spmv_plan *p, const void *x, void *y, const void *w, double *dot_out, hipStream_t s) {
-  if (p->kernel != LHPC_KERNEL_ADAPTIVE || p->n_blocks == 0) return LHPC_ERR_UNSUPPORTED;
+  if ((p->kernel != LHPC_KERNEL_ADAPTIVE && p->kernel != LHPC_KERNEL_SELL) || p->n_blocks == 0)
+    return LHPC_ERR_UNSUPPORTED;
   const int64_t n1 = (p->n_blocks + kFinTile - 1) / kFinTile;  // stage-1 sums, after the partials
   if (n1 > kFinTile) return LHPC_ERR_UNSUPPORTED;                // > 4M blocks (> 8·10^9 nonzeros)
   if (!p->d_dpart)
     LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_dpart), (p->n_blocks + n1) * sizeof(double), p->bytes));
   int st;
-  if (p->dtype == LHPC_F32)
+  if (p->kernel == LHPC_KERNEL_SELL)
+    st = p->dtype == LHPC_F32 ? launch_sell<float>(p, x, y, s, w, p->d_dpart)
+                              : launch_sell<double>(p, x, y, s, w, p->d_dpart);
+  else if (p->dtype == LHPC_F32)
     st = p->rp64 ? launch_adaptive<float, int64_t>(p, x, y, s, w, p->d_dpart)
                  : launch_adaptive<float, int32_t>(p, x, y, s, w, p->d_dpart);
   else

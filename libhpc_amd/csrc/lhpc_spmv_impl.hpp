@@ -1,7 +1,7 @@
 // lhpc_spmv_impl.hpp — the SpMV plan object and the interface between the
 // kernel-family translation units:
 //   lhpc_spmv.hip         plan creation (kernel selection), the C ABI
-//   lhpc_spmv_csr.hip     ROWGROUP / ADAPTIVE (CSR kept as is)
+//   lhpc_spmv_csr.hip     ROWGROUP / ADAPTIVE (CSR kept as is), SELL (short rows)
 //   lhpc_spmv_xslice.hip  XSLICE (XCD-local column slices + partial reduce)
 //   lhpc_spmv_xtile.hip   XTILE (x tiles in LDS: tile gather + chunk reduce)
 // The reference has no SpMV: the operator is
@@ -25,8 +25,10 @@ struct lhpc_spmv_plan {
   void *d_row_ptr = nullptr;
   int32_t *d_col = nullptr;
   void *d_val = nullptr;
-  int64_t *d_blocks = nullptr;
+  int64_t *d_blocks = nullptr;  // ADAPTIVE: the block table; SELL: the slice offsets
   int64_t n_blocks = 0, n_long = 0;
+  int sell_w = 0;              // SELL: widest slice
+  int64_t sell_total = 0;      // SELL: entries stored (nonzeros + padding)
   void *d_xstage = nullptr, *d_ystage = nullptr;
   double *h_scalars = nullptr;  // lhpc_cg_solve: 2 pinned host scalars, allocated on first use
   // lhpc_cg_solve's work (first solve; freed with the plan): r, p, q and x
@@ -37,7 +39,7 @@ struct lhpc_spmv_plan {
   hipGraphExec_t cg_graph[2] = {nullptr, nullptr};
   int cg_graph_iters[2] = {0, 0};
   std::atomic<int> cg_busy{0};  // a solve holds the work above (LHPC_ERR_BUSY for a second one)
-  double *d_dpart = nullptr;  // lhpc_spmv_dot: per-block partials (ADAPTIVE), allocated on first use
+  double *d_dpart = nullptr;  // lhpc_spmv_dot: per-block partials (ADAPTIVE / SELL), allocated on first use
   int kernel = LHPC_KERNEL_ROWGROUP;
   int L = 16, R = 4;
   int64_t bytes = 0;
@@ -94,6 +96,7 @@ struct lhpc_spmv_plan {
 namespace lhpc {
 
 constexpr int kBlock = 256;
+constexpr int kSellMaxW = 8;  // SELL: nonzeros per row at most (ADAPTIVE's 2048 / 256)
 
 // Host view of row_ptr regardless of width.
 struct RowPtrView {
@@ -167,6 +170,8 @@ void local_csr_from_global(LocalCsr &out, RowPtrView rp, const int32_t *col_idx,
 int csr_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s);
 // ADAPTIVE with the fused y·w epilogue: *dot_out = Σ y[i]·w[i] (fixed order)
 int csr_launch_dot(lhpc_spmv_plan *p, const void *x, void *y, const void *w, double *dot_out, hipStream_t s);
+// SELL layout; LHPC_ERR_UNSUPPORTED when the rows do not suit it (caller falls back)
+int sell_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz, bool forced);
 // ADAPTIVE row blocks (≤ 2048 nonzeros and ≤ 256 rows, or one long row)
 std::vector<int64_t> csr_build_blocks(RowPtrView rp, int64_t n_rows, int64_t &n_long);
 

@@ -47,7 +47,7 @@ def test_cg_fp32(lhpc, gpu):
 @pytest.mark.parametrize("check_every,max_iter", [(4, 5000), (7, 5000), (6, 20), (5, 3)])
 def test_cg_graph_blocks_match_loop(lhpc, gpu, check_every, max_iter):
     """On a non-null stream lhpc_cg_solve replays the check_every iterations
-    between two convergence checks as a captured HIP graph (ADAPTIVE plans);
+    between two convergence checks as a captured HIP graph (ADAPTIVE / SELL plans);
     on the null stream it runs the plain loop.  Both issue the same kernels in
     the same order: x bit-identical, same iteration count and residual — for
     even and odd check_every (both graph parities), a max_iter that ends in
@@ -58,7 +58,7 @@ def test_cg_graph_blocks_match_loop(lhpc, gpu, check_every, max_iter):
     n = rp.size - 1
     b = _dev(gpu, np.random.default_rng(17).uniform(-1, 1, n))
     with lhpc.SpMVPlan(rp, col, val, n) as plan:
-        assert plan.info()["kernel"] == lhpc.KERNEL_ADAPTIVE
+        assert plan.info()["kernel"] == lhpc.KERNEL_SELL  # ≤ 5 nonzeros per row (test_gpu_sell.py)
         x0, it0, r0 = lhpc.cg(plan, b, tol=1e-10, max_iter=max_iter, check_every=check_every,
                               stream=torch.cuda.default_stream(gpu))
         s = torch.cuda.Stream(gpu)

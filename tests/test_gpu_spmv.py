@@ -804,7 +804,7 @@ def test_device_input_layout_matches_host(lhpc, gpu, case):
 
 
 def test_device_input_checks_and_fallbacks(lhpc, gpu):
-    """Device input that does not select XTILE (x fits L2: ADAPTIVE) goes
+    """Device input that does not select XTILE (x fits L2: SELL here) goes
     through the host path and is exact; malformed device CSR is refused on
     the GPU with LHPC_ERR_BAD_CSR (a column out of range, a decreasing
     row_ptr)."""
@@ -814,7 +814,7 @@ def test_device_input_checks_and_fallbacks(lhpc, gpu):
     x = lhpc.gen_values(lhpc.F32, 1, n, 0xDE11)
     dev = [torch.from_numpy(np.ascontiguousarray(a)).to(gpu) for a in (rp, col, val)]
     with lhpc.SpMVPlan(*dev, n) as p:
-        assert p.info()["kernel"] == lhpc.KERNEL_ADAPTIVE
+        assert p.info()["kernel"] == lhpc.KERNEL_SELL  # 5 nonzeros per row: SELL (test_gpu_sell.py)
         assert np.array_equal(p(torch.from_numpy(x).to(gpu)).cpu().numpy(), S.spmv_oracle(rp, col, val, x)[1])
     bad_col = dev[1].clone()
     bad_col[123] = n

@@ -101,11 +101,14 @@ def test_no_kernel_spills_to_memory(ks):
 def test_hot_kernel_register_budgets(ks):
     """The XTILE iperm reduce runs 8 waves per SIMD (≤ 64 VGPRs) in fp32 —
     the round-1 A/B that made it the default (DESIGN.md §4 iperm reduce);
+    the SELL kernel too (≤ 64, fp32 and fp64);
     the default stencil7 kernel (x4 ring, 2 rows × 4 blocks, LDS-shared
     halo) stays ≤ 128 VGPRs (4 waves per SIMD), under the dword ring's 150."""
     def pick(pat):
         return {n: r for n, r in ks.items() if re.search(pat, n)}
     red = pick(r"k_xtile_reduceIfLi[124]ELi512ELb1E")
     assert red and all(r["vgpr_count"] <= 64 for r in red.values()), red
+    sell = pick(r"k_spmv_sellI[fd]E")  # SELL: 8 waves per SIMD, every gather of a row in flight
+    assert len(sell) == 2 and all(r["vgpr_count"] <= 64 for r in sell.values()), sell
     s7 = pick(r"k_stencil7_buf4ILi2ELi4ELi[56]ELi2ELb[01]ELb1E")
     assert s7 and all(r["vgpr_count"] <= 128 for r in s7.values()), {n: r["vgpr_count"] for n, r in s7.items()}
