@@ -10,7 +10,9 @@
 //   β = rr'/rr; x += α·p;           k_cg_xp (reads x p r, writes x p)
 //   p = r + β·p
 // (k_cg_xr / k_cg_p, the x update beside the r update, stay as building
-// blocks of the C ABI.)
+// blocks of the C ABI.)  On SELL plans k_cg_xp is fused into the next
+// iteration's SpMV (lhpc_spmv_csr.hip k_spmv_sell_cg): two passes per
+// iteration, x bit-identical to the three-pass loop.
 // α and β are read on the device from fp64 scalars, so no host round trip is
 // needed between kernels; the host reads rr' only every `check_every`
 // iterations to test convergence.  Dots accumulate in fp64 with a fixed
@@ -133,6 +135,12 @@ __global__ __launch_bounds__(kVecThreads) void k_cg_xp(T *__restrict__ x, T *__r
     x[i] = x[i] + a * pi;
     if constexpr (P) p[i] = r[i] + beta * pi;
   }
+}
+
+// the fused loop's start: rr[1] = pq = 1 (any finite pair: they scale p_old = 0)
+__global__ void k_cg_scalar_ones(double *a, double *b) {
+  *a = 1.0;
+  *b = 1.0;
 }
 
 // r = b - q, p = r, part = block partials of r·r
@@ -330,7 +338,7 @@ int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int
     int cur = 0;
     LHPC_HIP_TRY(hipGetDevice(&cur));
     LHPC_HIP_TRY(hipSetDevice(plan->device));
-    hipError_t e = hipMalloc(&plan->cg_vecs, static_cast<size_t>(std::max<int64_t>(n, 1)) * ts * 4);
+    hipError_t e = hipMalloc(&plan->cg_vecs, static_cast<size_t>(std::max<int64_t>(n, 1)) * ts * 5);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&plan->cg_scal), (8 + kDotBlocks) * sizeof(double));
     (void)hipSetDevice(cur);
     LHPC_HIP_TRY(e);
@@ -339,6 +347,11 @@ int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int
   void *r = vb, *p = vb + static_cast<size_t>(n) * ts, *q = vb + 2 * static_cast<size_t>(n) * ts;
   void *x_user = x;
   x = vb + 3 * static_cast<size_t>(n) * ts;
+  // SELL plans fuse each iteration's x += α·p, p = r + β·p into the next
+  // iteration's SpMV (sell_cg_step), which reads p from one buffer and writes
+  // the other: the p of an iteration of parity c lives in pb[c]
+  const bool fused = plan->kernel == LHPC_KERNEL_SELL && !plan->multi && plan->parts.empty() && n > 0;
+  void *pb[2] = {p, vb + 4 * static_cast<size_t>(n) * ts};
   LHPC_HIP_TRY(hipMemcpyAsync(x, x_user, static_cast<size_t>(n) * ts, hipMemcpyDeviceToDevice, s));
   double *rr[2] = {plan->cg_scal, plan->cg_scal + 1}, *pq = plan->cg_scal + 2, *bb = plan->cg_scal + 3,
          *part = plan->cg_scal + 8;
@@ -374,12 +387,23 @@ int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int
   int cur = 0;
   int status = LHPC_OK;
   // one iteration's device work: q = A·p and p·q in one pass (ADAPTIVE), r -=
-  // α·q with rr' = r·r, and (full) x += α·p, p = r + β·p in one pass
+  // α·q with rr' = r·r, and (full) x += α·p, p = r + β·p in one pass.  Fused
+  // (SELL): the previous iteration's x / p update, q = A·p and p·q in one
+  // pass, then r -= α·q with rr' = r·r; nothing is left for after the block
+  // but the pending x += α·p, which the next iteration's first pass does
   auto body = [&](int c, bool full) -> int {
+    if (fused) {
+      LHPC_TRY(sell_cg_step(plan, r, pb[c ^ 1], pb[c], x, q, rr[c ^ 1], pq, rr[c], rr[c ^ 1], pq, s));
+      return cg_r_launch(dtype, n, rr[c], pq, r, q, rr[c ^ 1], part, s);
+    }
     LHPC_TRY(lhpc_spmv_dot(plan, p, q, p, pq, s));
     LHPC_TRY(cg_r_launch(dtype, n, rr[c], pq, r, q, rr[c ^ 1], part, s));
     if (full) LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[c], pq, rr[c ^ 1], rr[c], x, p, r, s));
     return LHPC_OK;
+  };
+  // the pending x += α·p of the last iteration (parity c), when the loop ends
+  auto finish_x = [&](int c) -> int {
+    return lhpc_cg_step_xp(dtype, n, rr[c], pq, nullptr, nullptr, x, fused ? pb[c] : p, nullptr, s);
   };
   // Graph blocks: the C = check_every iterations between two convergence
   // checks — C − 1 full iterations and the C-th up to rr' — captured once per
@@ -424,6 +448,16 @@ int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int
   if (graphs && !plan->d_dpart) {  // the fused dot's partials exist before any capture
     LHPC_TRY(lhpc_spmv_dot(plan, x, q, x, pq, s));
   }
+  int last = -1;  // parity of the last iteration whose x update is pending (fused)
+  if (fused && h_rr > stop) {
+    // the first iteration's "previous" step is x += 1·0, p = r + β·0 with
+    // p_old = pb[1] = 0 and rr[1] = pq = 1: x unchanged and p = r exactly, so
+    // every iteration (and every captured block) has the same form (after
+    // the warm-up above, which writes pq)
+    LHPC_HIP_TRY(hipMemsetAsync(pb[1], 0, static_cast<size_t>(n) * ts, s));
+    hipLaunchKernelGGL(k_cg_scalar_ones, dim3(1), dim3(1), 0, s, rr[1], pq);
+    LHPC_TRY(check_launch(s));
+  }
   if (h_rr > stop) {
     for (it = 0; it < max_iter;) {
       if (graphs && it % check_every == 0 && it + check_every <= max_iter) {
@@ -441,10 +475,12 @@ int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int
           break;
         }
         if (h_rr <= stop) {
-          LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[c], pq, nullptr, nullptr, x, p, nullptr, s));  // x += α·p
+          LHPC_TRY(finish_x(c));  // x += α·p
+          last = -1;
           break;
         }
-        LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[c], pq, rr[c ^ 1], rr[c], x, p, r, s));
+        if (!fused) LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[c], pq, rr[c ^ 1], rr[c], x, p, r, s));
+        last = c;
         cur = c ^ 1;
         continue;
       }
@@ -458,15 +494,18 @@ int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int
           break;
         }
         if (h_rr <= stop) {
-          LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[cur], pq, nullptr, nullptr, x, p, nullptr, s));  // x += α·p
+          LHPC_TRY(finish_x(cur));  // x += α·p
+          last = -1;
           break;
         }
       }
-      // x += α·p, then p = r + β·p (same pass)
-      LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[cur], pq, rr[cur ^ 1], rr[cur], x, p, r, s));
+      // x += α·p, then p = r + β·p (same pass; fused: in the next iteration's SpMV)
+      if (!fused) LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[cur], pq, rr[cur ^ 1], rr[cur], x, p, r, s));
+      last = cur;
       cur ^= 1;
     }
     if (it > max_iter) it = max_iter;
+    if (fused && last >= 0 && status == LHPC_OK) LHPC_TRY(finish_x(last));  // max_iter reached
   }
   LHPC_HIP_TRY(hipMemcpyAsync(x_user, x, static_cast<size_t>(n) * ts, hipMemcpyDeviceToDevice, s));
   LHPC_HIP_TRY(hipStreamSynchronize(s));

@@ -285,6 +285,78 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(const int32_t *__restrict_
   }
 }
 
+// CG step on a SELL plan (lhpc_cg_solve): the previous iteration's
+// x += α·p and p = r + β·p (k_cg_xp) fused into this iteration's q = A·p and
+// p·q.  Every gathered p[c] is formed as r[c] + β·p_old[c] — the value k_cg_xp
+// would have stored, so q, the dot and x are bit-identical to the unfused
+// loop — and each row stores its own p (p_new: the other buffer; blocks
+// still gather p_old) and x.  Saves k_cg_xp's pass over x, p, r (5n) for one
+// more gathered vector (r) and the x / p stores (3n).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_spmv_sell_cg(
+    const int32_t *__restrict__ col, const T *__restrict__ val, const int64_t *__restrict__ soff,
+    const T *__restrict__ r, const T *__restrict__ p_old, T *__restrict__ p_new, T *__restrict__ x,
+    T *__restrict__ q, int64_t n_rows, const double *__restrict__ anum, const double *__restrict__ aden,
+    const double *__restrict__ bnum, const double *__restrict__ bden, double *__restrict__ dpart) {
+  __shared__ double wsum[kBlock / kWave];
+  const T a = static_cast<T>(*anum / *aden);   // k_cg_xp's α and β
+  const T beta = static_cast<T>(*bnum / *bden);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t slice = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + threadIdx.x / kWave;
+  const int64_t row = slice * kWave + lane;
+  double acc = 0.0;
+  T pn = T(0);
+  if (slice * kWave < n_rows) {  // wave-uniform
+    const int64_t o0 = soff[slice];
+    const int W = static_cast<int>((soff[slice + 1] - o0) / kWave);
+    int32_t c[kSellMaxW];
+    T v[kSellMaxW];
+#pragma unroll
+    for (int j = 0; j < kSellMaxW; ++j) {
+      c[j] = -1;
+      v[j] = T(0);
+      if (j < W) {
+        c[j] = ld_stream(col + o0 + j * kWave + lane);
+        v[j] = ld_stream(val + o0 + j * kWave + lane);
+      }
+    }
+    T pv[kSellMaxW];
+#pragma unroll
+    for (int j = 0; j < kSellMaxW; ++j) pv[j] = c[j] >= 0 ? r[c[j]] + beta * p_old[c[j]] : T(0);
+    if (row < n_rows) {
+      const T po = p_old[row];
+      pn = r[row] + beta * po;
+      x[row] = x[row] + a * po;
+      p_new[row] = pn;
+    }
+    double pr[kSellMaxW];
+#pragma unroll
+    for (int j = 0; j < kSellMaxW; ++j) pr[j] = static_cast<double>(v[j]) * static_cast<double>(pv[j]);
+    const int64_t nb = n_rows - static_cast<int64_t>(blockIdx.x) * kBlock;
+    int L = kWave;
+    while (L > 1 && nb * L > kBlock) L >>= 1;
+    if (L == 1) {
+#pragma unroll
+      for (int j = 0; j < kSellMaxW; ++j)
+        if (j < W) acc += pr[j];
+    } else {
+      acc = adaptive_lane_order(pr, L);
+    }
+  }
+  const T yv = static_cast<T>(acc);
+  if (row < n_rows) q[row] = yv;
+  double d = row < n_rows ? static_cast<double>(yv) * static_cast<double>(pn) : 0.0;
+  d = group_sum<kWave>(d);
+  if (lane == 0) wsum[threadIdx.x / kWave] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = wsum[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / kWave; ++i) t += wsum[i];
+    dpart[blockIdx.x] = t;
+  }
+}
+
 template <typename T>
 int launch_sell(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s, const void *w = nullptr,
                 double *dpart = nullptr) {
@@ -368,6 +440,20 @@ __global__ __launch_bounds__(kBlock) void k_dpart_finish(const double *__restric
     for (int i = 1; i < kBlock / kWave; ++i) t += wsum[i];
     out[blockIdx.x] = t;
   }
+}
+
+// *dot_out = Σ of the plan's n_blocks dot partials (fixed order)
+int dpart_finish(const lhpc_spmv_plan *p, int64_t n1, double *dot_out, hipStream_t s) {
+  double *stage1 = p->d_dpart + p->n_blocks;
+  if (n1 == 1) {
+    hipLaunchKernelGGL(k_dpart_finish, dim3(1), dim3(kBlock), 0, s, p->d_dpart, p->n_blocks, dot_out);
+  } else {
+    hipLaunchKernelGGL(k_dpart_finish, dim3(static_cast<unsigned>(n1)), dim3(kBlock), 0, s, p->d_dpart,
+                       p->n_blocks, stage1);
+    LHPC_TRY(check_launch(s));
+    hipLaunchKernelGGL(k_dpart_finish, dim3(1), dim3(kBlock), 0, s, stage1, n1, dot_out);
+  }
+  return check_launch(s);
 }
 
 }  // namespace
@@ -468,16 +554,29 @@ int csr_launch_dot(lhpc_spmv_plan *p, const void *x, void *y, const void *w, dou
     st = p->rp64 ? launch_adaptive<double, int64_t>(p, x, y, s, w, p->d_dpart)
                  : launch_adaptive<double, int32_t>(p, x, y, s, w, p->d_dpart);
   LHPC_TRY(st);
-  double *stage1 = p->d_dpart + p->n_blocks;
-  if (n1 == 1) {
-    hipLaunchKernelGGL(k_dpart_finish, dim3(1), dim3(kBlock), 0, s, p->d_dpart, p->n_blocks, dot_out);
-  } else {
-    hipLaunchKernelGGL(k_dpart_finish, dim3(static_cast<unsigned>(n1)), dim3(kBlock), 0, s, p->d_dpart,
-                       p->n_blocks, stage1);
-    LHPC_TRY(check_launch(s));
-    hipLaunchKernelGGL(k_dpart_finish, dim3(1), dim3(kBlock), 0, s, stage1, n1, dot_out);
-  }
-  return check_launch(s);
+  return dpart_finish(p, n1, dot_out, s);
+}
+
+int sell_cg_step(lhpc_spmv_plan *p, const void *r, const void *p_old, void *p_new, void *x, void *q,
+                 const double *anum, const double *aden, const double *bnum, const double *bden, double *pq,
+                 hipStream_t s) {
+  if (p->kernel != LHPC_KERNEL_SELL || p->n_blocks == 0) return LHPC_ERR_UNSUPPORTED;
+  const int64_t n1 = (p->n_blocks + kFinTile - 1) / kFinTile;
+  if (n1 > kFinTile) return LHPC_ERR_UNSUPPORTED;
+  if (!p->d_dpart)
+    LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_dpart), (p->n_blocks + n1) * sizeof(double), p->bytes));
+  if (p->dtype == LHPC_F32)
+    hipLaunchKernelGGL((k_spmv_sell_cg<float>), dim3(static_cast<unsigned>(p->n_blocks)), dim3(kBlock), 0, s,
+                       p->d_col, static_cast<const float *>(p->d_val), p->d_blocks, static_cast<const float *>(r),
+                       static_cast<const float *>(p_old), static_cast<float *>(p_new), static_cast<float *>(x),
+                       static_cast<float *>(q), p->n_rows, anum, aden, bnum, bden, p->d_dpart);
+  else
+    hipLaunchKernelGGL((k_spmv_sell_cg<double>), dim3(static_cast<unsigned>(p->n_blocks)), dim3(kBlock), 0, s,
+                       p->d_col, static_cast<const double *>(p->d_val), p->d_blocks, static_cast<const double *>(r),
+                       static_cast<const double *>(p_old), static_cast<double *>(p_new), static_cast<double *>(x),
+                       static_cast<double *>(q), p->n_rows, anum, aden, bnum, bden, p->d_dpart);
+  LHPC_TRY(check_launch(s));
+  return dpart_finish(p, n1, pq, s);
 }
 
 }  // namespace lhpc

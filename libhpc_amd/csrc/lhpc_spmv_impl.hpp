@@ -170,6 +170,12 @@ void local_csr_from_global(LocalCsr &out, RowPtrView rp, const int32_t *col_idx,
 int csr_launch(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s);
 // ADAPTIVE with the fused y·w epilogue: *dot_out = Σ y[i]·w[i] (fixed order)
 int csr_launch_dot(lhpc_spmv_plan *p, const void *x, void *y, const void *w, double *dot_out, hipStream_t s);
+// lhpc_cg_solve on a SELL plan: x += α·p_old, p_new = r + β·p_old (α = *anum / *aden,
+// β = *bnum / *bden), q = A·p_new, *pq = p_new·q — k_cg_xp fused into the next
+// iteration's SpMV + dot, bit-identical to the unfused steps
+int sell_cg_step(lhpc_spmv_plan *p, const void *r, const void *p_old, void *p_new, void *x, void *q,
+                 const double *anum, const double *aden, const double *bnum, const double *bden, double *pq,
+                 hipStream_t s);
 // SELL layout; LHPC_ERR_UNSUPPORTED when the rows do not suit it (caller falls back)
 int sell_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz, bool forced);
 // ADAPTIVE row blocks (≤ 2048 nonzeros and ≤ 256 rows, or one long row)

@@ -138,11 +138,14 @@ def test_sell_host_buffers_and_device_input(lhpc, gpu):
     S.assert_spmv_close(yh, want[1], want[2])
 
 
+@pytest.mark.parametrize("max_iter,check_every", [(5000, 8), (5000, 1), (13, 4), (7, 1), (1, 1)])
 @pytest.mark.parametrize("dt", [np.float64, np.float32], ids=["f64", "f32"])
-def test_cg_sell_matches_adaptive(lhpc, gpu, dt):
-    """lhpc_cg_solve on a SELL plan (graph blocks on a side stream) and on an
-    ADAPTIVE plan of the same Laplacian: same iterations, residual and x bit
-    for bit."""
+def test_cg_sell_matches_adaptive(lhpc, gpu, dt, max_iter, check_every):
+    """lhpc_cg_solve on a SELL plan — each iteration's x / p update fused
+    into the next iteration's SpMV (sell_cg_step), graph blocks on a side
+    stream — and on an ADAPTIVE plan of the same Laplacian (the unfused
+    k_cg_xp loop): same iterations, residual and x bit for bit, converged or
+    stopped at max_iter (the pending x update of the last iteration)."""
     import torch
     rp, col, val = S.laplacian_2d(150, 130, dtype=dt, shift=0.0 if dt == np.float64 else 0.5)
     n = rp.size - 1
@@ -153,8 +156,8 @@ def test_cg_sell_matches_adaptive(lhpc, gpu, dt):
         with lhpc.SpMVPlan(rp, col, val, n, options=opts) as plan:
             s = torch.cuda.Stream(gpu)
             with torch.cuda.stream(s):
-                out.append((plan.info()["kernel"],) + tuple(lhpc.cg(plan, b, tol=tol, max_iter=5000, check_every=8,
-                                                                     stream=s)))
+                out.append((plan.info()["kernel"],) + tuple(lhpc.cg(plan, b, tol=tol, max_iter=max_iter,
+                                                                     check_every=check_every, stream=s)))
             s.synchronize()
     (k0, x0, it0, r0), (k1, x1, it1, r1) = out
     assert (k0, k1) == (lhpc.KERNEL_SELL, lhpc.KERNEL_ADAPTIVE)
