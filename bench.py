@@ -1152,9 +1152,13 @@ def cg_bench(args, L, torch, dev, stream, barrier, world, rank):
                        "solver": "lhpc_dist_cg_solve (native, RCCL, chained stages)" if native else
                                  ("lhpc_cg_solve (native loop, 10-iteration HIP graph blocks)" if world == 1 else
                                   "DistCG over torch.distributed")},
-               roofline={"bound": "hbm", "kernel": f"spmv_dot (k_spmv_{kname}) + k_cg_r + k_cg_xp",
+               roofline={"bound": "hbm",
+                         "kernel": "k_spmv_sell_cg + k_cg_r" if kname == "sell" and world == 1 else
+                                   f"spmv_dot (k_spmv_{kname}) + k_cg_r + k_cg_xp",
                          "achieved": alg / per / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": alg / per / 1e9 / HBM_PEAK_GBPS, "traffic": None,
+                         "frac": alg / per / 1e9 / HBM_PEAK_GBPS,
+                         # PMC bytes per iteration (profiles/traffic.json "cg_sell")
+                         "traffic": load_traffic("cg_sell") if kname == "sell" and world == 1 else None,
                          "alg_bytes_per_iter": alg})
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from tests import _support as S

@@ -5,7 +5,9 @@
 
 --per-call k_xtile_gather=3 says a call launches that kernel 3 times (XTILE
 cache-sized ranges): its per-dispatch average is multiplied by 3 in
-bytes_per_call.
+bytes_per_call.  --exclude k_a,k_b leaves set-up kernels (run once per solve,
+not per step) out of bytes_per_call; --fetch-factor F applies F instead of a
+calibration pass (the gfx950 factor the calibration passes measured: 2.0).
 
 Counters are in KiB per dispatch (FETCH_SIZE = TCC_EA0_RDREQ-based, so
 Infinity-Cache hits are included).  Per MI355X_MICROARCH.md §HBM, FETCH_SIZE
@@ -44,10 +46,17 @@ def main():
         out = sys.argv[sys.argv.index("--out") + 1]
         args = [a for a in args if a != out]
     per_call = {}
+    exclude, fixed_factor = set(), None
     for i, a in enumerate(sys.argv):
         if a == "--per-call":
             k, v = sys.argv[i + 1].split("=")
             per_call[k] = int(v)
+            args = [b for b in args if b != sys.argv[i + 1]]
+        if a == "--exclude":
+            exclude = set(sys.argv[i + 1].split(","))
+            args = [b for b in args if b != sys.argv[i + 1]]
+        if a == "--fetch-factor":
+            fixed_factor = float(sys.argv[i + 1])
             args = [b for b in args if b != sys.argv[i + 1]]
     tag, fdir, wdir = args[:3]
     cal = {"k_read16": 1 << 30, "k_read4": 1 << 30}
@@ -63,6 +72,8 @@ def main():
     fetch, n = per_kernel(fdir, "FETCH_SIZE")
     write, _ = per_kernel(wdir, "WRITE_SIZE")
     db = json.load(open(out)) if os.path.exists(out) else {}
+    if fixed_factor:
+        factor4 = factor16 = fixed_factor
     f4 = factor4 if factor4 else 1.0
     ent = {"kernels": {}, "fetch_factor_4B": factor4, "fetch_factor_16B": factor16,
            "note": "FETCH_SIZE*1024*fetch_factor_4B + WRITE_SIZE*1024, averaged over dispatches; "
@@ -80,6 +91,9 @@ def main():
             continue
         if k in PLAN_BUILD:  # device-side plan build (once per plan, not per call)
             ent["kernels"][k]["plan_build"] = True
+            continue
+        if k in exclude:  # set-up kernels of an iterative workload
+            ent["kernels"][k]["setup"] = True
             continue
         tot += (rb + wb) * per_call.get(k, 1)
     ent["bytes_per_call"] = tot
