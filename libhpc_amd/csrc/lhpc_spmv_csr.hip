@@ -522,7 +522,6 @@ int sell_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const v
   p->n_blocks = (n + kBlock - 1) / kBlock;
   p->n_long = 0;
   p->sell_w = wmax;
-  p->sell_total = total;
   return LHPC_OK;
 }
 

@@ -28,7 +28,6 @@ struct lhpc_spmv_plan {
   int64_t *d_blocks = nullptr;  // ADAPTIVE: the block table; SELL: the slice offsets
   int64_t n_blocks = 0, n_long = 0;
   int sell_w = 0;              // SELL: widest slice
-  int64_t sell_total = 0;      // SELL: entries stored (nonzeros + padding)
   void *d_xstage = nullptr, *d_ystage = nullptr;
   double *h_scalars = nullptr;  // lhpc_cg_solve: 2 pinned host scalars, allocated on first use
   // lhpc_cg_solve's work (first solve; freed with the plan): r, p, q and x
