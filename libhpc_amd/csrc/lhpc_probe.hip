@@ -43,6 +43,25 @@ __global__ __launch_bounds__(256) void k_copyw(const T *__restrict__ s, T *__res
   }
 }
 
+// Read:write mix probe (round 5): block t reads one 16-KB tile (16 B per lane,
+// non-temporal) and writes W 16-KB tiles (W stores per lane, plain or
+// non-temporal), so the stream moves W bytes written per byte read — the mix
+// of the XTILE gather (fp32: col16 2 B read per 4 B of xg written; fp64 per
+// 8 B) against the 1:1 copy.
+template <int W, bool NTS>
+__global__ __launch_bounds__(1024) void k_fan(const f32x4 *__restrict__ s, f32x4 *__restrict__ d, int64_t tiles) {
+  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const f32x4 v = __builtin_nontemporal_load(s + t * 1024 + threadIdx.x);
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      f32x4 o = v;
+      o.x += static_cast<float>(w);
+      if constexpr (NTS) __builtin_nontemporal_store(o, d + (t * W + w) * 1024 + threadIdx.x);
+      else d[(t * W + w) * 1024 + threadIdx.x] = o;
+    }
+  }
+}
+
 // Unrolled 16-B/lane probes (round 5 calibration against MI355X_MICROARCH.md's
 // 6.29 TB/s float4 copy): a block moves a tile of U·BLK float4 per iteration
 // (U loads in flight per lane, each wave instruction 1 KB contiguous) and
@@ -284,5 +303,24 @@ extern "C" int lhpc_probe_copy_w(const void *src, void *dst, int64_t bytes, int 
   else if (width == 8) LHPC_CW(f32x2, 8);
   else LHPC_CW(f32x4, 16);
 #undef LHPC_CW
+  return static_cast<int>(hipGetLastError());
+}
+
+// tiles 16-KB tiles read, tiles·w written (w ∈ {1, 2, 3, 4}); nt_store: non-temporal stores
+extern "C" int lhpc_probe_fan(const void *src, void *dst, int64_t tiles, int w, int nt_store, int grid,
+                              void *stream) {
+  const f32x4 *s = static_cast<const f32x4 *>(src);
+  f32x4 *d = static_cast<f32x4 *>(dst);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+#define LHPC_FAN(W)                                                                                     \
+  case W:                                                                                               \
+    if (nt_store) hipLaunchKernelGGL((k_fan<W, true>), dim3(grid), dim3(1024), 0, st, s, d, tiles);     \
+    else hipLaunchKernelGGL((k_fan<W, false>), dim3(grid), dim3(1024), 0, st, s, d, tiles);             \
+    break;
+  switch (w) {
+    LHPC_FAN(1) LHPC_FAN(2) LHPC_FAN(3) LHPC_FAN(4)
+    default: return static_cast<int>(hipErrorInvalidValue);
+  }
+#undef LHPC_FAN
   return static_cast<int>(hipGetLastError());
 }
