@@ -350,7 +350,8 @@ int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int
   // SELL plans fuse each iteration's x += α·p, p = r + β·p into the next
   // iteration's SpMV (sell_cg_step), which reads p from one buffer and writes
   // the other: the p of an iteration of parity c lives in pb[c]
-  const bool fused = plan->kernel == LHPC_KERNEL_SELL && !plan->multi && plan->parts.empty() && n > 0;
+  const bool fused = plan->kernel == LHPC_KERNEL_SELL && !plan->multi && plan->parts.empty() && n > 0 &&
+                     plan->n_blocks <= int64_t{2048} * 2048;  // sell_cg_step's two-stage dot (≤ 2^30 rows)
   void *pb[2] = {p, vb + 4 * static_cast<size_t>(n) * ts};
   LHPC_HIP_TRY(hipMemcpyAsync(x, x_user, static_cast<size_t>(n) * ts, hipMemcpyDeviceToDevice, s));
   double *rr[2] = {plan->cg_scal, plan->cg_scal + 1}, *pq = plan->cg_scal + 2, *bb = plan->cg_scal + 3,
