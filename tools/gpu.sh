@@ -16,6 +16,8 @@
 #   senv NAME K=PATH[,K=PATH] [BENCH ARGS]  stats with K=$REPO/PATH exported first (A/B library paths)
 #   pmc NAME COUNTERS [BENCH ARGS]  one rocprofv3 --pmc pass (COUNTERS comma-separated)
 #   py NAME SCRIPT [ARGS]           python SCRIPT ARGS > NAME.log (tools/*.py probes)
+#   spy NAME K=V[,K=V] SCRIPT [ARGS]  the same under rocprofv3 --kernel-trace --stats, with K=V
+#                                   exported (a V naming libhpc_amd/… is made absolute; - for none)
 #   dist NAME NPROC [BENCH ARGS]    bench.py under torch.distributed.run (env passed through)
 # Limits: tests 1100 s, stats/bench/py/dist 600 s, pmc 240 s (SIGKILL).
 set -o pipefail
@@ -63,6 +65,12 @@ for S in "$@"; do
         python3 "$R/bench.py" "${A[@]:3}") || exit 1 ;;
     py)
       run "${A[1]}" 600 TERM python -u "${A[@]:2}" || exit 1 ;;
+    spy)
+      IFS=',' read -ra KV <<< "${A[2]}"
+      (for kv in "${KV[@]}"; do [ "$kv" = "-" ] && continue; v=${kv#*=}; [[ $v == libhpc_amd/* ]] && v=$R/$v
+         export "${kv%%=*}=$v"; done
+       cd /tmp && run "${A[1]}" 600 TERM rocprofv3 --kernel-trace --stats -d "$O/${A[1]}" -o run -f csv -- \
+        python3 -u "$R/${A[3]}" "${A[@]:4}") || exit 1 ;;
     dist)
       run "${A[1]}" 600 TERM python -m torch.distributed.run --nnodes=1 --nproc-per-node "${A[2]}" \
         --master-addr 127.0.0.1 --master-port $((29500 + RANDOM % 400)) bench.py "${A[@]:3}" || exit 1 ;;
