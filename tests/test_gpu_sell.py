@@ -185,3 +185,34 @@ def test_sell_golden(lhpc, gpu, name):
         assert np.array_equal(y, g["y_exact"].astype(val.dtype))
     else:
         S.assert_spmv_close(y, g["y_exact"], S.spmv_oracle(rp, col, val, x)[2])
+
+
+def test_sell_full_size_cg_config(lhpc, gpu):
+    """The bench's CG configuration at full size (4096² 5-point Laplacian,
+    fp64, n = 16.8M): the SELL plan's y equals ADAPTIVE's bit for bit and
+    10⁵ sampled rows match fp64 numpy; 20 CG iterations (tol 0, graph blocks
+    of 10) through the fused SELL loop and the unfused ADAPTIVE loop give the
+    same x bit for bit."""
+    import torch
+    nx = 4096
+    rp, col, val = lhpc.gen_laplacian_2d(nx, nx, lhpc.F64)
+    n = nx * nx
+    xh = np.random.default_rng(0xC6).uniform(-1, 1, n)
+    x = _dev(gpu, xh)
+    b = _dev(gpu, np.random.default_rng(0xC7).uniform(-1, 1, n))
+    out = []
+    for opts in (None, {"spmv_no_sell": 1}):
+        with lhpc.SpMVPlan(rp, col, val, n, options=opts) as plan:
+            y = plan(x)
+            s = torch.cuda.Stream(gpu)
+            with torch.cuda.stream(s):
+                xs, it, res = lhpc.cg(plan, b, tol=0.0, max_iter=20, check_every=10, stream=s)
+            s.synchronize()
+            out.append((plan.info()["kernel"], y, xs, it, res))
+    (k0, y0, x0, it0, r0), (k1, y1, x1, it1, r1) = out
+    assert (k0, k1) == (lhpc.KERNEL_SELL, lhpc.KERNEL_ADAPTIVE)
+    assert torch.equal(y0, y1)
+    rows, y64, asum = S.sampled_rows_fp64(rp, col, val, xh, 100_000)
+    yr = y0.cpu().numpy()[rows]
+    assert np.all(np.abs(yr - y64) <= 1e-12 * asum + 1e-300)
+    assert (it0, r0) == (it1, r1) == (20, r0) and torch.equal(x0, x1)
