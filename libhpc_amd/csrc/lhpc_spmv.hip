@@ -629,14 +629,18 @@ int plan_create_device_input(lhpc_spmv_plan **out, int dtype, int64_t n_rows, in
   const bool single = n_devices <= 1 && !o.multi_force && n_rows > 0 &&
                       (parts ? (tiles + B - 1) / B <= 4096 : nnz <= cap && tiles <= 4096);
   bool want_xtile = single && (flags & LHPC_PLAN_FORCE_XTILE);
-  if (single && auto_ok && !o.spmv_no_xtile && x_bytes > 8.0e6)
-    want_xtile = gather_lines_per_nnz(
-                     rp,
-                     [&](int64_t k0, int64_t k1, int32_t *dst) {
-                       return static_cast<int>(hipMemcpy(dst, col_idx + k0, static_cast<size_t>(k1 - k0) * 4,
-                                                         hipMemcpyDeviceToHost));
-                     },
-                     n_rows, n_cols, tsz) > locality_thr;
+  // the host path's locality test (plan_create_impl's `nolocal`), on
+  // device-fetched samples: XTILE here, and the SELL decision below
+  bool nolocal = false;
+  if (auto_ok && x_bytes > 8.0e6)
+    nolocal = gather_lines_per_nnz(
+                  rp,
+                  [&](int64_t k0, int64_t k1, int32_t *dst) {
+                    return static_cast<int>(hipMemcpy(dst, col_idx + k0, static_cast<size_t>(k1 - k0) * 4,
+                                                      hipMemcpyDeviceToHost));
+                  },
+                  n_rows, n_cols, tsz) > locality_thr;
+  if (single && auto_ok && !o.spmv_no_xtile && x_bytes > 8.0e6) want_xtile = nolocal;
   if (want_xtile) {
     auto *p = new (std::nothrow) lhpc_spmv_plan();
     if (!p) return LHPC_ERR_ALLOC;
@@ -655,6 +659,32 @@ int plan_create_device_input(lhpc_spmv_plan **out, int dtype, int64_t n_rows, in
     }
     lhpc_spmv_plan_destroy(p);
     if (st != LHPC_ERR_UNSUPPORTED) return st;
+  }
+  // SELL (short rows with x locality, as plan_create_impl selects it) built
+  // on the GPU from the device arrays; when the padding rule refuses it, the
+  // host path below chooses again (ADAPTIVE)
+  const bool force_sell = (flags & LHPC_PLAN_FORCE_SELL) != 0;
+  if (n_devices <= 1 && !o.multi_force && n_splits == 0 && n_rows > 0 &&
+      (force_sell || (auto_ok && !o.spmv_no_sell && !nolocal))) {
+    int64_t maxlen = 0;
+    for (int64_t i = 0; i < n_rows; ++i) maxlen = std::max<int64_t>(maxlen, rp[i + 1] - rp[i]);
+    if (maxlen <= kSellMaxW) {
+      auto *p = new (std::nothrow) lhpc_spmv_plan();
+      if (!p) return LHPC_ERR_ALLOC;
+      p->opt = o;
+      p->dtype = dtype;
+      p->device = dev;
+      p->n_rows = n_rows;
+      p->n_cols = n_cols;
+      p->nnz = nnz;
+      const int st = sell_build_device(p, rp, row_ptr, col_idx, val, tsz, force_sell);
+      if (st == LHPC_OK) {
+        *out = p;
+        return LHPC_OK;
+      }
+      lhpc_spmv_plan_destroy(p);
+      if (st != LHPC_ERR_UNSUPPORTED) return st;
+    }
   }
   // every other case: A to the host, the host path
   std::vector<int32_t> hcol(static_cast<size_t>(nnz));

@@ -206,6 +206,26 @@ __global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
 }
 
 // ------------------------------------------------------------- SELL
+// Device build of the SELL layout from device CSR (sell_build_device): row i
+// (one thread) writes its entries to soff[i / 64] + 64·j + i % 64; padding
+// was set beforehand (col −1, val 0).  V: the value's bit pattern.
+template <typename V>
+__global__ __launch_bounds__(kBlock) void k_sell_scatter(const void *__restrict__ rp, int bits,
+                                                         const int32_t *__restrict__ col, const V *__restrict__ val,
+                                                         const int64_t *__restrict__ soff, int64_t n_rows,
+                                                         int32_t *__restrict__ ocol, V *__restrict__ oval) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n_rows;
+       i += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int64_t k0 = bits == 64 ? static_cast<const int64_t *>(rp)[i] : static_cast<const int32_t *>(rp)[i];
+    const int64_t k1 = bits == 64 ? static_cast<const int64_t *>(rp)[i + 1] : static_cast<const int32_t *>(rp)[i + 1];
+    const int64_t b = soff[i / kWave] + (i % kWave);
+    for (int64_t j = 0; j < k1 - k0; ++j) {
+      ocol[b + j * kWave] = col[k0 + j];
+      oval[b + j * kWave] = val[k0 + j];
+    }
+  }
+}
+
 // The value ADAPTIVE computes for a row of ≤ 8 products p[] with L ≥ 2 lanes
 // per row: lane s sums p[s], p[s + L], … from 0.0, then group_sum<L> pairs the
 // lane sums as the tree (0+1)+(2+3)… (its butterfly steps are symmetric, so
@@ -485,10 +505,15 @@ std::vector<int64_t> csr_build_blocks(RowPtrView rp, int64_t n_rows, int64_t &n_
 // than kSellMaxW nonzeros, or (auto) when the padding would stream more
 // bytes than CSR with its row_ptr.  Sets kernel, n_blocks (256-row blocks,
 // ADAPTIVE's own for such rows) and d_blocks = the slice offsets.
-int sell_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz, bool forced) {
-  const int64_t n = p->n_rows, S = (n + kWave - 1) / kWave;
-  std::vector<int64_t> off(static_cast<size_t>(S) + 1, 0);
-  int wmax = 0;
+// Slice offsets of the SELL layout (host): off[s] = first entry of slice s,
+// off[S] = entries stored; LHPC_ERR_UNSUPPORTED past kSellMaxW nonzeros in a
+// row, or (not forced) when the padded slices would stream more bytes than
+// CSR with its row_ptr.
+static int sell_offsets(RowPtrView rp, int64_t n, int64_t nnz, size_t tsz, bool forced, std::vector<int64_t> &off,
+                        int &wmax) {
+  const int64_t S = (n + kWave - 1) / kWave;
+  off.assign(static_cast<size_t>(S) + 1, 0);
+  wmax = 0;
   for (int64_t s = 0; s < S; ++s) {
     int64_t W = 0;
     for (int64_t i = s * kWave; i < std::min(n, (s + 1) * kWave); ++i) W = std::max(W, rp[i + 1] - rp[i]);
@@ -496,10 +521,27 @@ int sell_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const v
     wmax = std::max(wmax, static_cast<int>(W));
     off[static_cast<size_t>(s) + 1] = off[static_cast<size_t>(s)] + W * kWave;
   }
-  const int64_t total = off[static_cast<size_t>(S)];
-  const double sell_b = static_cast<double>(total) * static_cast<double>(4 + tsz) + 8.0 * static_cast<double>(S);
-  const double csr_b = static_cast<double>(p->nnz) * static_cast<double>(4 + tsz) + 4.0 * static_cast<double>(n + 1);
-  if (!forced && sell_b > csr_b) return LHPC_ERR_UNSUPPORTED;
+  const double sell_b = static_cast<double>(off[static_cast<size_t>(S)]) * static_cast<double>(4 + tsz) +
+                        8.0 * static_cast<double>(S);
+  const double csr_b = static_cast<double>(nnz) * static_cast<double>(4 + tsz) + 4.0 * static_cast<double>(n + 1);
+  return !forced && sell_b > csr_b ? LHPC_ERR_UNSUPPORTED : LHPC_OK;
+}
+
+static int sell_finish(lhpc_spmv_plan *p, const std::vector<int64_t> &off, int wmax) {
+  LHPC_HIP_TRY(hipMemcpy(p->d_blocks, off.data(), off.size() * 8, hipMemcpyHostToDevice));
+  p->kernel = LHPC_KERNEL_SELL;
+  p->n_blocks = (p->n_rows + kBlock - 1) / kBlock;
+  p->n_long = 0;
+  p->sell_w = wmax;
+  return LHPC_OK;
+}
+
+int sell_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz, bool forced) {
+  const int64_t n = p->n_rows;
+  std::vector<int64_t> off;
+  int wmax = 0;
+  LHPC_TRY(sell_offsets(rp, n, p->nnz, tsz, forced, off, wmax));
+  const int64_t total = off.back();
   std::vector<int32_t> c(static_cast<size_t>(total), -1);
   std::vector<unsigned char> v(static_cast<size_t>(total) * tsz, 0);
   const unsigned char *vin = static_cast<const unsigned char *>(val);
@@ -517,11 +559,35 @@ int sell_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const v
     LHPC_HIP_TRY(hipMemcpy(p->d_col, c.data(), c.size() * 4, hipMemcpyHostToDevice));
     LHPC_HIP_TRY(hipMemcpy(p->d_val, v.data(), v.size(), hipMemcpyHostToDevice));
   }
-  LHPC_HIP_TRY(hipMemcpy(p->d_blocks, off.data(), off.size() * 8, hipMemcpyHostToDevice));
-  p->kernel = LHPC_KERNEL_SELL;
-  p->n_blocks = (n + kBlock - 1) / kBlock;
-  p->n_long = 0;
-  p->sell_w = wmax;
+  return sell_finish(p, off, wmax);
+}
+
+int sell_build_device(lhpc_spmv_plan *p, RowPtrView rp_host, const void *d_rp, const int32_t *d_col,
+                      const void *d_val, size_t tsz, bool forced) {
+  const int64_t n = p->n_rows;
+  std::vector<int64_t> off;
+  int wmax = 0;
+  LHPC_TRY(sell_offsets(rp_host, n, p->nnz, tsz, forced, off, wmax));
+  const int64_t total = off.back();
+  LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_col), static_cast<size_t>(total) * 4, p->bytes));
+  LHPC_TRY(dmalloc(&p->d_val, static_cast<size_t>(total) * tsz, p->bytes));
+  LHPC_TRY(dmalloc(reinterpret_cast<void **>(&p->d_blocks), off.size() * 8, p->bytes));
+  LHPC_TRY(sell_finish(p, off, wmax));  // the slice offsets, which the scatter reads
+  if (total) {
+    LHPC_HIP_TRY(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(p->d_col), -1, static_cast<size_t>(total)));
+    LHPC_HIP_TRY(hipMemset(p->d_val, 0, static_cast<size_t>(total) * tsz));
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>((n + kBlock - 1) / kBlock, 65536));
+    if (tsz == 4)
+      hipLaunchKernelGGL((k_sell_scatter<uint32_t>), dim3(grid), dim3(kBlock), 0, nullptr, d_rp, rp_host.bits, d_col,
+                         static_cast<const uint32_t *>(d_val), p->d_blocks, n, p->d_col,
+                         static_cast<uint32_t *>(p->d_val));
+    else
+      hipLaunchKernelGGL((k_sell_scatter<uint64_t>), dim3(grid), dim3(kBlock), 0, nullptr, d_rp, rp_host.bits, d_col,
+                         static_cast<const uint64_t *>(d_val), p->d_blocks, n, p->d_col,
+                         static_cast<uint64_t *>(p->d_val));
+    LHPC_HIP_TRY(hipGetLastError());
+    LHPC_HIP_TRY(hipDeviceSynchronize());
+  }
   return LHPC_OK;
 }
 

@@ -177,6 +177,9 @@ int sell_cg_step(lhpc_spmv_plan *p, const void *r, const void *p_old, void *p_ne
                  hipStream_t s);
 // SELL layout; LHPC_ERR_UNSUPPORTED when the rows do not suit it (caller falls back)
 int sell_build(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void *val, size_t tsz, bool forced);
+// the same layout from device CSR (d_rp: row_ptr of rp_host.bits on the device; rp_host: its host copy)
+int sell_build_device(lhpc_spmv_plan *p, RowPtrView rp_host, const void *d_rp, const int32_t *d_col,
+                      const void *d_val, size_t tsz, bool forced);
 // ADAPTIVE row blocks (≤ 2048 nonzeros and ≤ 256 rows, or one long row)
 std::vector<int64_t> csr_build_blocks(RowPtrView rp, int64_t n_rows, int64_t &n_long);
 

@@ -121,6 +121,35 @@ def test_sell_selection_rules(lhpc, gpu):
         assert torch.count_nonzero(y).item() == 0
 
 
+@pytest.mark.parametrize("dt", [np.float64, np.float32], ids=["f64", "f32"])
+@pytest.mark.parametrize("rp64", [False, True], ids=["rp32", "rp64"])
+def test_sell_device_build_matches_host_build(lhpc, gpu, dt, rp64):
+    """A SELL plan built on the GPU from device-resident CSR
+    (LHPC_PLAN_DEVICE_INPUT: slice offsets from the host copy of row_ptr, a
+    scatter kernel for col / val) gives the host-built plan's y bit for bit:
+    the Laplacian (auto), random 0–8 rows (forced; padded slices), and a
+    matrix whose padding makes auto fall back to ADAPTIVE on both paths."""
+    import torch
+    cases = [(S.laplacian_2d(300, 77, dtype=dt), 0, lhpc.KERNEL_SELL)]
+    rpr, colr, valr = _random_short(70_001, 8, 0xD5, dt, False)
+    cases.append(((rpr, colr, valr), FORCE_SELL, lhpc.KERNEL_SELL))
+    cases.append(((rpr, colr, valr), 0, lhpc.KERNEL_ADAPTIVE))
+    for (rp, col, val), flags, kern in cases:
+        rp = rp.astype(np.int64 if rp64 else np.int32)
+        n = rp.size - 1
+        xh = np.random.default_rng(n).uniform(-1, 1, n).astype(dt)
+        x = _dev(gpu, xh)
+        with lhpc.SpMVPlan(rp, col, val, n, flags=flags) as ph, \
+                lhpc.SpMVPlan(_dev(gpu, rp), _dev(gpu, col), _dev(gpu, val), n, flags=flags) as pd:
+            assert ph.info()["kernel"] == pd.info()["kernel"] == kern
+            assert ph.info()["slice_width"] == pd.info()["slice_width"]
+            yh, yd = ph(x), pd(x)
+            torch.cuda.synchronize()
+            assert torch.equal(yh, yd)
+        _, y64, asum = S.spmv_oracle(rp, col, val, xh)
+        S.assert_spmv_close(yd.cpu().numpy(), y64, asum)
+
+
 def test_sell_host_buffers_and_device_input(lhpc, gpu):
     """Host x/y (staged) and device-resident CSR input build the same SELL plan."""
     import torch
