@@ -50,6 +50,8 @@ __global__ __launch_bounds__(256) void k_copyw(const T *__restrict__ s, T *__res
 // 8 B) against the 1:1 copy.
 template <int W, bool NTS>
 __global__ __launch_bounds__(1024) void k_fan(const f32x4 *__restrict__ s, f32x4 *__restrict__ d, int64_t tiles) {
+  extern __shared__ float fan_lds[];  // dynamic LDS: only to cap blocks per CU (occupancy study)
+  if (threadIdx.x == 0 && tiles < 0) fan_lds[0] = 0.f;
   for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
     const f32x4 v = __builtin_nontemporal_load(s + t * 1024 + threadIdx.x);
 #pragma unroll
@@ -306,16 +308,17 @@ extern "C" int lhpc_probe_copy_w(const void *src, void *dst, int64_t bytes, int 
   return static_cast<int>(hipGetLastError());
 }
 
-// tiles 16-KB tiles read, tiles·w written (w ∈ {1, 2, 3, 4}); nt_store: non-temporal stores
+// tiles 16-KB tiles read, tiles·w written (w ∈ {1, 2, 3, 4}); nt_store: non-temporal stores;
+// lds_bytes of dynamic LDS per block (0: none) caps the blocks per CU
 extern "C" int lhpc_probe_fan(const void *src, void *dst, int64_t tiles, int w, int nt_store, int grid,
-                              void *stream) {
+                              int lds_bytes, void *stream) {
   const f32x4 *s = static_cast<const f32x4 *>(src);
   f32x4 *d = static_cast<f32x4 *>(dst);
   hipStream_t st = static_cast<hipStream_t>(stream);
 #define LHPC_FAN(W)                                                                                     \
   case W:                                                                                               \
-    if (nt_store) hipLaunchKernelGGL((k_fan<W, true>), dim3(grid), dim3(1024), 0, st, s, d, tiles);     \
-    else hipLaunchKernelGGL((k_fan<W, false>), dim3(grid), dim3(1024), 0, st, s, d, tiles);             \
+    if (nt_store) hipLaunchKernelGGL((k_fan<W, true>), dim3(grid), dim3(1024), lds_bytes, st, s, d, tiles); \
+    else hipLaunchKernelGGL((k_fan<W, false>), dim3(grid), dim3(1024), lds_bytes, st, s, d, tiles);         \
     break;
   switch (w) {
     LHPC_FAN(1) LHPC_FAN(2) LHPC_FAN(3) LHPC_FAN(4)

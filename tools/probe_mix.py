@@ -2,8 +2,10 @@
 bytes per byte read, W = 1 … 4 — the XTILE gather's mix (fp32: ≈ 1 : 1.4
 with the x tiles; fp64: ≈ 1 : 2.6–3) against the 1:1 calibrated copy.
 lhpc_probe_fan: one 16-KB tile read (non-temporal) and W tiles written per
-1024-thread block, plain or non-temporal stores, ≈ 1.5 GB moved per launch.
-One JSON line per (W, store policy, repeat): µs, TB/s moved, TB/s written.
+1024-thread block, plain or non-temporal stores, ≈ 1.5 GB moved per launch; and with 96 KB of dynamic
+LDS per block and a grid of 256 blocks walking the tiles (one 1024-thread
+block per CU for the whole launch, as the XTILE gather runs).
+One JSON line per (W, store policy, LDS, repeat): µs, TB/s moved, TB/s written.
 """
 import ctypes as C
 import json
@@ -24,12 +26,13 @@ src = torch.empty(MOVED // 2 // 4 + TILE, device=dev).uniform_()
 dst = torch.empty(MOVED // 4 + TILE, device=dev)
 
 
-def run(w, nt, iters=20):
+def run(w, nt, lds=0, iters=20):
     tiles = MOVED // (TILE * (1 + w))
 
     def one():
         return P.lhpc_probe_fan(C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()), C.c_int64(tiles),
-                                C.c_int(w), C.c_int(nt), C.c_int(int(tiles)), C.c_void_p(st.cuda_stream))
+                                C.c_int(w), C.c_int(nt), C.c_int(256 if lds else int(tiles)), C.c_int(lds),
+                                C.c_void_p(st.cuda_stream))
     for _ in range(3):
         assert one() == 0
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -45,7 +48,7 @@ def run(w, nt, iters=20):
 
 for rep in range(2):
     for w in (1, 2, 3, 4):
-        for nt in (1, 0):
-            t, moved, written = run(w, nt)
-            print(json.dumps({"rep": rep, "write_per_read": w, "nt_store": nt, "us": t * 1e6,
+        for nt, lds in ((1, 0), (0, 0), (1, 96 * 1024)):
+            t, moved, written = run(w, nt, lds)
+            print(json.dumps({"rep": rep, "write_per_read": w, "nt_store": nt, "lds_bytes": lds, "us": t * 1e6,
                               "TBps": moved / t / 1e12, "write_TBps": written / t / 1e12}), flush=True)
