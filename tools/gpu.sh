@@ -13,7 +13,8 @@
 #   benv NAME K=V[,K=V] [BENCH ARGS]  the same with environment variables set (e.g.
 #                                   LHPC_LIB_PATH=libhpc_amd/_abx/X/liblhpc.so for an A/B build)
 #   stats NAME [BENCH ARGS]         the same under rocprofv3 --kernel-trace --stats (NAME/ dir)
-#   senv NAME K=PATH[,K=PATH] [BENCH ARGS]  stats with K=$REPO/PATH exported first (A/B library paths)
+#   senv NAME K=PATH[,K=PATH] [BENCH ARGS]  stats with K=$REPO/PATH exported first (A/B library paths;
+#                                   - for none: the same step on the default library)
 #   pmc NAME COUNTERS [BENCH ARGS]  one rocprofv3 --pmc pass (COUNTERS comma-separated)
 #   py NAME SCRIPT [ARGS]           python SCRIPT ARGS > NAME.log (tools/*.py probes)
 #   spy NAME K=V[,K=V] SCRIPT [ARGS]  the same under rocprofv3 --kernel-trace --stats, with K=V
@@ -56,7 +57,7 @@ for S in "$@"; do
       grep '^{' "$O/${A[1]}.log" | tail -1 > "$O/${A[1]}.json" ;;
     senv)
       IFS=',' read -ra KV <<< "${A[2]}"
-      (for kv in "${KV[@]}"; do export "${kv%%=*}=$R/${kv#*=}"; done
+      (for kv in "${KV[@]}"; do [ "$kv" = "-" ] && continue; export "${kv%%=*}=$R/${kv#*=}"; done
        cd /tmp && run "${A[1]}" 600 TERM rocprofv3 --kernel-trace --stats -d "$O/${A[1]}" -o run -f csv -- \
         python3 "$R/bench.py" "${A[@]:3}") || exit 1
       grep '^{' "$O/${A[1]}.log" | tail -1 > "$O/${A[1]}.json" ;;
