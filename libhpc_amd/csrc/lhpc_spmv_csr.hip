@@ -206,6 +206,24 @@ __global__ __launch_bounds__(kBlock) void k_spmv_adaptive(
 }
 
 // ------------------------------------------------------------- SELL
+// x[c] for one nonzero of a SELL wave whose rows start at base: a column in
+// [base, base + 64) comes from the lane holding x[base + lane] (`own`) by a
+// lane shuffle, any other column is gathered.  The diagonal band of a
+// row-local matrix then costs one coalesced load per wave instead of one
+// gather instruction per band diagonal; the values are the same.
+template <typename T>
+__device__ __forceinline__ T sell_x(const T *__restrict__ x, int32_t c, int64_t base, T own) {
+#ifdef LHPC_SELL_NO_SHFL
+  return c >= 0 ? x[c] : T(0);
+#else
+  const uint64_t d = static_cast<uint64_t>(static_cast<int64_t>(c) - base);
+  const bool loc = d < static_cast<uint64_t>(kWave);
+  T v = __shfl(own, loc ? static_cast<int>(d) : 0, kWave);
+  if (c >= 0 && !loc) v = x[c];
+  return c >= 0 ? v : T(0);
+#endif
+}
+
 // Device build of the SELL layout from device CSR (sell_build_device): row i
 // (one thread) writes its entries to soff[i / 64] + 64·j + i % 64; padding
 // was set beforehand (col −1, val 0).  V: the value's bit pattern.
@@ -246,8 +264,8 @@ __device__ __forceinline__ double adaptive_lane_order(const double (&p)[kSellMax
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_spmv_sell(const int32_t *__restrict__ col, const T *__restrict__ val,
                                                       const int64_t *__restrict__ soff, const T *__restrict__ x,
-                                                      T *__restrict__ y, int64_t n_rows, const T *__restrict__ w,
-                                                      double *__restrict__ dpart) {
+                                                      T *__restrict__ y, int64_t n_rows, int64_t n_cols,
+                                                      const T *__restrict__ w, double *__restrict__ dpart) {
 #pragma clang fp contract(off)  // the product rounds before the add, as ADAPTIVE's LDS-staged products do
   __shared__ double wsum[kBlock / kWave];
   const int lane = threadIdx.x & (kWave - 1);
@@ -270,9 +288,11 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(const int32_t *__restrict_
         v[j] = ld_stream(val + o0 + j * kWave + lane);
       }
     }
+    const int64_t base = slice * kWave;
+    const T own = base + lane < n_cols ? x[base + lane] : T(0);
     T xv[kSellMaxW];
 #pragma unroll
-    for (int j = 0; j < kSellMaxW; ++j) xv[j] = c[j] >= 0 ? x[c[j]] : T(0);
+    for (int j = 0; j < kSellMaxW; ++j) xv[j] = sell_x(x, c[j], base, own);
     double pr[kSellMaxW];  // padding: 0·0 = 0, which adds nothing
 #pragma unroll
     for (int j = 0; j < kSellMaxW; ++j) pr[j] = static_cast<double>(v[j]) * static_cast<double>(xv[j]);
@@ -340,14 +360,28 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell_cg(
         v[j] = ld_stream(val + o0 + j * kWave + lane);
       }
     }
-    T pv[kSellMaxW];
-#pragma unroll
-    for (int j = 0; j < kSellMaxW; ++j) pv[j] = c[j] >= 0 ? r[c[j]] + beta * p_old[c[j]] : T(0);
     if (row < n_rows) {
       const T po = p_old[row];
       pn = r[row] + beta * po;
       x[row] = x[row] + a * po;
       p_new[row] = pn;
+    }
+    // the gathered p[c] = r[c] + β·p_old[c]: from the lane of row c when c
+    // is one of this wave's rows (its pn: the same expression), else formed
+    // from two gathers
+    const int64_t base = slice * kWave;
+    T pv[kSellMaxW];
+#pragma unroll
+    for (int j = 0; j < kSellMaxW; ++j) {
+#ifdef LHPC_SELL_NO_SHFL
+      pv[j] = c[j] >= 0 ? r[c[j]] + beta * p_old[c[j]] : T(0);
+#else
+      const uint64_t d = static_cast<uint64_t>(static_cast<int64_t>(c[j]) - base);
+      const bool loc = d < static_cast<uint64_t>(kWave);
+      T v = __shfl(pn, loc ? static_cast<int>(d) : 0, kWave);
+      if (c[j] >= 0 && !loc) v = r[c[j]] + beta * p_old[c[j]];
+      pv[j] = c[j] >= 0 ? v : T(0);
+#endif
     }
     double pr[kSellMaxW];
 #pragma unroll
@@ -383,7 +417,7 @@ int launch_sell(const lhpc_spmv_plan *p, const void *x, void *y, hipStream_t s, 
   if (p->n_blocks == 0) return LHPC_OK;
   hipLaunchKernelGGL((k_spmv_sell<T>), dim3(static_cast<unsigned>(p->n_blocks)), dim3(kBlock), 0, s, p->d_col,
                      static_cast<const T *>(p->d_val), p->d_blocks, static_cast<const T *>(x), static_cast<T *>(y),
-                     p->n_rows, static_cast<const T *>(w), dpart);
+                     p->n_rows, p->n_cols, static_cast<const T *>(w), dpart);
   return check_launch(s);
 }
 
