@@ -13,6 +13,7 @@
 #include <cstdlib>
 
 #include "../../include/lhpc.h"
+#include "lhpc_abi.hpp"
 
 #define LHPC_HIP_TRY(expr)                                                     \
   do {                                                                         \

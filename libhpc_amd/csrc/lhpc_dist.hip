@@ -561,300 +561,326 @@ int wait_pending(lhpc_dist_spmv_plan *d, hipStream_t s) {
 
 extern "C" int lhpc_dist_exchange_schedule(const int64_t *cuts, int nranks, int K, int rank, int exchange,
                                            int broadcast, lhpc_dist_xfer *out, int64_t max_out, int64_t *n_out) {
-  if (!cuts || nranks < 1 || K < 1 || rank < 0 || rank >= nranks || !n_out || max_out < 0 || (max_out > 0 && !out) ||
-      (exchange != LHPC_DIST_EXCHANGE_RCCL && exchange != LHPC_DIST_EXCHANGE_P2P))
-    return LHPC_ERR_INVALID_ARG;
-  const int64_t nb = static_cast<int64_t>(nranks) * K;
-  if (cuts[0] != 0) return LHPC_ERR_INVALID_ARG;
-  for (int64_t b = 0; b < nb; ++b)
-    if (cuts[b + 1] < cuts[b]) return LHPC_ERR_INVALID_ARG;
-  std::vector<lhpc_dist_xfer> v;
-  std::vector<int64_t> first;
-  LHPC_TRY(build_schedule(cuts, nranks, K, rank, exchange, broadcast, v, first));
-  *n_out = static_cast<int64_t>(v.size());
-  if (static_cast<int64_t>(v.size()) > max_out) return LHPC_ERR_INVALID_ARG;
-  if (!v.empty()) std::memcpy(out, v.data(), v.size() * sizeof(lhpc_dist_xfer));
-  return LHPC_OK;
+  try {
+    if (!cuts || nranks < 1 || K < 1 || rank < 0 || rank >= nranks || !n_out || max_out < 0 || (max_out > 0 && !out) ||
+        (exchange != LHPC_DIST_EXCHANGE_RCCL && exchange != LHPC_DIST_EXCHANGE_P2P))
+      return LHPC_ERR_INVALID_ARG;
+    const int64_t nb = static_cast<int64_t>(nranks) * K;
+    if (cuts[0] != 0) return LHPC_ERR_INVALID_ARG;
+    for (int64_t b = 0; b < nb; ++b)
+      if (cuts[b + 1] < cuts[b]) return LHPC_ERR_INVALID_ARG;
+    std::vector<lhpc_dist_xfer> v;
+    std::vector<int64_t> first;
+    LHPC_TRY(build_schedule(cuts, nranks, K, rank, exchange, broadcast, v, first));
+    *n_out = static_cast<int64_t>(v.size());
+    if (static_cast<int64_t>(v.size()) > max_out) return LHPC_ERR_INVALID_ARG;
+    if (!v.empty()) std::memcpy(out, v.data(), v.size() * sizeof(lhpc_dist_xfer));
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_rccl_calls(const int64_t *cuts, int nranks, int K, int rank, int broadcast, int dtype,
                                     lhpc_rccl_call *out, int64_t max_out, int64_t *n_out) {
-  if (dtype != LHPC_F32 && dtype != LHPC_F64) return LHPC_ERR_INVALID_ARG;
-  if (!n_out || max_out < 0 || (max_out > 0 && !out)) return LHPC_ERR_INVALID_ARG;
-  int64_t ns = 0;  // the schedule's size (a too-small buffer still reports it)
-  const int q = lhpc_dist_exchange_schedule(cuts, nranks, K, rank, LHPC_DIST_EXCHANGE_RCCL, broadcast, nullptr, 0, &ns);
-  if (q != LHPC_OK && ns == 0) return q;  // bad cuts / ranks
-  std::vector<lhpc_dist_xfer> v(static_cast<size_t>(ns));
-  LHPC_TRY(lhpc_dist_exchange_schedule(cuts, nranks, K, rank, LHPC_DIST_EXCHANGE_RCCL, broadcast, v.data(), ns, &ns));
-  std::vector<lhpc_rccl_call> calls;
-  lhpc::rccl_calls_of(v.data(), ns, dtype, calls);
-  *n_out = static_cast<int64_t>(calls.size());
-  if (*n_out > max_out) return LHPC_ERR_INVALID_ARG;
-  if (!calls.empty()) std::memcpy(out, calls.data(), calls.size() * sizeof(lhpc_rccl_call));
-  return LHPC_OK;
+  try {
+    if (dtype != LHPC_F32 && dtype != LHPC_F64) return LHPC_ERR_INVALID_ARG;
+    if (!n_out || max_out < 0 || (max_out > 0 && !out)) return LHPC_ERR_INVALID_ARG;
+    int64_t ns = 0;  // the schedule's size (a too-small buffer still reports it)
+    const int q = lhpc_dist_exchange_schedule(cuts, nranks, K, rank, LHPC_DIST_EXCHANGE_RCCL, broadcast, nullptr, 0, &ns);
+    if (q != LHPC_OK && ns == 0) return q;  // bad cuts / ranks
+    std::vector<lhpc_dist_xfer> v(static_cast<size_t>(ns));
+    LHPC_TRY(lhpc_dist_exchange_schedule(cuts, nranks, K, rank, LHPC_DIST_EXCHANGE_RCCL, broadcast, v.data(), ns, &ns));
+    std::vector<lhpc_rccl_call> calls;
+    lhpc::rccl_calls_of(v.data(), ns, dtype, calls);
+    *n_out = static_cast<int64_t>(calls.size());
+    if (*n_out > max_out) return LHPC_ERR_INVALID_ARG;
+    if (!calls.empty()) std::memcpy(out, calls.data(), calls.size() * sizeof(lhpc_rccl_call));
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_chain_parts(const int64_t *cuts, int nranks, int K, int64_t n_cols, int64_t tile_width,
                                      int32_t *part, int64_t n_tiles) {
-  if (!cuts || nranks < 1 || K < 1 || n_cols < 0 || tile_width < 1 || !part ||
-      n_tiles < (n_cols + tile_width - 1) / tile_width)
-    return LHPC_ERR_INVALID_ARG;
-  std::vector<int64_t> col_end(static_cast<size_t>(K));
-  for (int j = 0; j < K; ++j) col_end[static_cast<size_t>(j)] = cuts[static_cast<int64_t>(j + 1) * nranks];
-  for (int j = 0; j < K; ++j)
-    if (j > 0 && col_end[j] < col_end[j - 1]) return LHPC_ERR_INVALID_ARG;
-  if (col_end[K - 1] < n_cols) return LHPC_ERR_INVALID_ARG;  // the chunks must cover x
-  for (int64_t t = 0; t < n_tiles; ++t)
-    part[t] = static_cast<int32_t>(lhpc::xtile_part_of_tile(t, tile_width, n_cols, col_end.data(), K));
-  return LHPC_OK;
+  try {
+    if (!cuts || nranks < 1 || K < 1 || n_cols < 0 || tile_width < 1 || !part ||
+        n_tiles < (n_cols + tile_width - 1) / tile_width)
+      return LHPC_ERR_INVALID_ARG;
+    std::vector<int64_t> col_end(static_cast<size_t>(K));
+    for (int j = 0; j < K; ++j) col_end[static_cast<size_t>(j)] = cuts[static_cast<int64_t>(j + 1) * nranks];
+    for (int j = 0; j < K; ++j)
+      if (j > 0 && col_end[j] < col_end[j - 1]) return LHPC_ERR_INVALID_ARG;
+    if (col_end[K - 1] < n_cols) return LHPC_ERR_INVALID_ARG;  // the chunks must cover x
+    for (int64_t t = 0; t < n_tiles; ++t)
+      part[t] = static_cast<int32_t>(lhpc::xtile_part_of_tile(t, tile_width, n_cols, col_end.data(), K));
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_get_unique_id(unsigned char *id_out) {
-  if (!id_out) return LHPC_ERR_INVALID_ARG;
-  ncclUniqueId id;
-  LHPC_NCCL_TRY(ncclGetUniqueId(&id));
-  std::memcpy(id_out, &id, sizeof(id));
-  return LHPC_OK;
+  try {
+    if (!id_out) return LHPC_ERR_INVALID_ARG;
+    ncclUniqueId id;
+    LHPC_NCCL_TRY(ncclGetUniqueId(&id));
+    std::memcpy(id_out, &id, sizeof(id));
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_comm_create(lhpc_dist_comm **out, const unsigned char *id, int nranks, int rank,
                                      int device) {
-  if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks || device < 0) return LHPC_ERR_INVALID_ARG;
-  *out = nullptr;
-  LHPC_HIP_TRY(hipSetDevice(device));
-  auto *c = new (std::nothrow) lhpc_dist_comm();
-  if (!c) return LHPC_ERR_ALLOC;
-  c->nranks = nranks;
-  c->rank = rank;
-  c->device = device;
-  (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
-  if (c->cus < 8) c->cus = 256;
-  ncclUniqueId uid;
-  std::memcpy(&uid, id, sizeof(uid));
-  const ncclResult_t st = ncclCommInitRank(&c->comm, nranks, uid, rank);
-  if (st != ncclSuccess) {
-    delete c;
-    return LHPC_RCCL_STATUS_BASE + static_cast<int>(st);
-  }
-  const hipError_t he = hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking);
-  if (he != hipSuccess) {
-    (void)ncclCommDestroy(c->comm);
-    delete c;
-    return static_cast<int>(he);
-  }
-  *out = c;
-  return LHPC_OK;
+  try {
+    if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks || device < 0) return LHPC_ERR_INVALID_ARG;
+    *out = nullptr;
+    LHPC_HIP_TRY(hipSetDevice(device));
+    auto *c = new (std::nothrow) lhpc_dist_comm();
+    if (!c) return LHPC_ERR_ALLOC;
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (c->cus < 8) c->cus = 256;
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    const ncclResult_t st = ncclCommInitRank(&c->comm, nranks, uid, rank);
+    if (st != ncclSuccess) {
+      delete c;
+      return LHPC_RCCL_STATUS_BASE + static_cast<int>(st);
+    }
+    const hipError_t he = hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking);
+    if (he != hipSuccess) {
+      (void)ncclCommDestroy(c->comm);
+      delete c;
+      return static_cast<int>(he);
+    }
+    *out = c;
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_comm_create_local(lhpc_dist_comm **out, int nranks, int rank, int device) {
-  if (!out || nranks < 1 || rank < 0 || rank >= nranks || device < 0 || nranks > 64) return LHPC_ERR_INVALID_ARG;
-  *out = nullptr;
-  LHPC_HIP_TRY(hipSetDevice(device));
-  auto *c = new (std::nothrow) lhpc_dist_comm();
-  if (!c) return LHPC_ERR_ALLOC;
-  c->nranks = nranks;
-  c->rank = rank;
-  c->device = device;
-  (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
-  if (c->cus < 8) c->cus = 256;
-  const hipError_t he = hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking);
-  if (he != hipSuccess) {
-    delete c;
-    return static_cast<int>(he);
-  }
-  *out = c;
-  return LHPC_OK;
+  try {
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks || device < 0 || nranks > 64) return LHPC_ERR_INVALID_ARG;
+    *out = nullptr;
+    LHPC_HIP_TRY(hipSetDevice(device));
+    auto *c = new (std::nothrow) lhpc_dist_comm();
+    if (!c) return LHPC_ERR_ALLOC;
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (c->cus < 8) c->cus = 256;
+    const hipError_t he = hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking);
+    if (he != hipSuccess) {
+      delete c;
+      return static_cast<int>(he);
+    }
+    *out = c;
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_p2p_export(lhpc_dist_comm *c, void *y, int64_t bytes, unsigned char *blob_out) {
-  if (!c || !y || bytes <= 0 || bytes % 4 || !blob_out || c->nranks > 64) return LHPC_ERR_INVALID_ARG;
-  if (c->n_win >= LHPC_DIST_P2P_MAX_WINDOWS) return LHPC_ERR_UNSUPPORTED;
-  for (int i = 0; i < c->n_win; ++i)
-    if (c->win[i].buf == y) return LHPC_ERR_INVALID_ARG;  // already a window
-  lhpc::RocTxRange rx("lhpc_dist_p2p_export");
-  LHPC_HIP_TRY(hipSetDevice(c->device));
-  P2pBlob b{};
-  void *base = nullptr;
-  size_t size = 0;
-  LHPC_HIP_TRY(hipMemGetAddressRange(reinterpret_cast<hipDeviceptr_t *>(&base), &size, y));
-  if (static_cast<unsigned char *>(y) + bytes > static_cast<unsigned char *>(base) + size) return LHPC_ERR_INVALID_ARG;
-  LHPC_HIP_TRY(hipIpcGetMemHandle(&b.buf, base));
-  if (!c->flags) {
-    // flags: uncached, so a peer's store is seen by the next poll; zeroed
-    LHPC_HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void **>(&c->flags), kFlagAlloc, hipDeviceMallocUncached));
-    LHPC_HIP_TRY(hipMemset(c->flags, 0, kFlagAlloc));
-    c->red_epoch = 0;
-    LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_status), sizeof(uint32_t), hipHostMallocMapped));
-    *c->h_status = 0;
-    c->epoch = 0;
-    static std::atomic<uint64_t> counter{0};
-    c->flags_gen = (std::random_device{}() * 0x9E3779B97F4A7C15ull) ^ (++counter << 1) ^ reinterpret_cast<uintptr_t>(c->flags);
-    if (c->flags_gen == 0) c->flags_gen = 1;
-  }
-  LHPC_HIP_TRY(hipIpcGetMemHandle(&b.flags, c->flags));
-  b.offset = static_cast<unsigned char *>(y) - static_cast<unsigned char *>(base);
-  b.bytes = bytes;
-  b.magic = kP2pMagic;
-  b.window = c->n_win;
-  b.nranks = c->nranks;
-  b.flags_gen = c->flags_gen;
-  P2pWindow &w = c->win[c->n_win++];
-  w = P2pWindow{};
-  w.buf = y;
-  w.bytes = static_cast<size_t>(bytes);
-  std::memset(blob_out, 0, LHPC_DIST_P2P_BLOB_BYTES);
-  std::memcpy(blob_out, &b, sizeof(b));
-  return LHPC_OK;
+  try {
+    if (!c || !y || bytes <= 0 || bytes % 4 || !blob_out || c->nranks > 64) return LHPC_ERR_INVALID_ARG;
+    if (c->n_win >= LHPC_DIST_P2P_MAX_WINDOWS) return LHPC_ERR_UNSUPPORTED;
+    for (int i = 0; i < c->n_win; ++i)
+      if (c->win[i].buf == y) return LHPC_ERR_INVALID_ARG;  // already a window
+    lhpc::RocTxRange rx("lhpc_dist_p2p_export");
+    LHPC_HIP_TRY(hipSetDevice(c->device));
+    P2pBlob b{};
+    void *base = nullptr;
+    size_t size = 0;
+    LHPC_HIP_TRY(hipMemGetAddressRange(reinterpret_cast<hipDeviceptr_t *>(&base), &size, y));
+    if (static_cast<unsigned char *>(y) + bytes > static_cast<unsigned char *>(base) + size) return LHPC_ERR_INVALID_ARG;
+    LHPC_HIP_TRY(hipIpcGetMemHandle(&b.buf, base));
+    if (!c->flags) {
+      // flags: uncached, so a peer's store is seen by the next poll; zeroed
+      LHPC_HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void **>(&c->flags), kFlagAlloc, hipDeviceMallocUncached));
+      LHPC_HIP_TRY(hipMemset(c->flags, 0, kFlagAlloc));
+      c->red_epoch = 0;
+      LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_status), sizeof(uint32_t), hipHostMallocMapped));
+      *c->h_status = 0;
+      c->epoch = 0;
+      static std::atomic<uint64_t> counter{0};
+      c->flags_gen = (std::random_device{}() * 0x9E3779B97F4A7C15ull) ^ (++counter << 1) ^ reinterpret_cast<uintptr_t>(c->flags);
+      if (c->flags_gen == 0) c->flags_gen = 1;
+    }
+    LHPC_HIP_TRY(hipIpcGetMemHandle(&b.flags, c->flags));
+    b.offset = static_cast<unsigned char *>(y) - static_cast<unsigned char *>(base);
+    b.bytes = bytes;
+    b.magic = kP2pMagic;
+    b.window = c->n_win;
+    b.nranks = c->nranks;
+    b.flags_gen = c->flags_gen;
+    P2pWindow &w = c->win[c->n_win++];
+    w = P2pWindow{};
+    w.buf = y;
+    w.bytes = static_cast<size_t>(bytes);
+    std::memset(blob_out, 0, LHPC_DIST_P2P_BLOB_BYTES);
+    std::memcpy(blob_out, &b, sizeof(b));
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_p2p_import(lhpc_dist_comm *c, const unsigned char *blobs) {
-  if (!c || !blobs || !c->flags) return LHPC_ERR_INVALID_ARG;
-  lhpc::RocTxRange rx("lhpc_dist_p2p_import");
-  LHPC_HIP_TRY(hipSetDevice(c->device));
-  const int nr = c->nranks;
-  std::vector<P2pBlob> bl(static_cast<size_t>(nr));
-  for (int r = 0; r < nr; ++r) std::memcpy(&bl[r], blobs + static_cast<size_t>(r) * LHPC_DIST_P2P_BLOB_BYTES, sizeof(P2pBlob));
-  const int wi = bl[c->rank].window;
-  if (wi < 0 || wi >= c->n_win) return LHPC_ERR_INVALID_ARG;
-  P2pWindow &w = c->win[wi];
-  if (w.ready) return LHPC_ERR_INVALID_ARG;  // imported already
-  for (int r = 0; r < nr; ++r)
-    if (bl[r].magic != kP2pMagic || bl[r].window != wi || bl[r].nranks != nr || bl[r].bytes <= 0)
-      return LHPC_ERR_INVALID_ARG;  // every rank must export the same windows in the same order
-  // open everything first; on any failure close what this call opened
-  std::vector<void *> pb(static_cast<size_t>(nr), nullptr), pf(static_cast<size_t>(nr), nullptr);
-  void **d_buf = nullptr;
-  uint32_t **d_flg = nullptr;
-  auto undo = [&](int st) {
+  try {
+    if (!c || !blobs || !c->flags) return LHPC_ERR_INVALID_ARG;
+    lhpc::RocTxRange rx("lhpc_dist_p2p_import");
+    LHPC_HIP_TRY(hipSetDevice(c->device));
+    const int nr = c->nranks;
+    std::vector<P2pBlob> bl(static_cast<size_t>(nr));
+    for (int r = 0; r < nr; ++r) std::memcpy(&bl[r], blobs + static_cast<size_t>(r) * LHPC_DIST_P2P_BLOB_BYTES, sizeof(P2pBlob));
+    const int wi = bl[c->rank].window;
+    if (wi < 0 || wi >= c->n_win) return LHPC_ERR_INVALID_ARG;
+    P2pWindow &w = c->win[wi];
+    if (w.ready) return LHPC_ERR_INVALID_ARG;  // imported already
+    for (int r = 0; r < nr; ++r)
+      if (bl[r].magic != kP2pMagic || bl[r].window != wi || bl[r].nranks != nr || bl[r].bytes <= 0)
+        return LHPC_ERR_INVALID_ARG;  // every rank must export the same windows in the same order
+    // open everything first; on any failure close what this call opened
+    std::vector<void *> pb(static_cast<size_t>(nr), nullptr), pf(static_cast<size_t>(nr), nullptr);
+    void **d_buf = nullptr;
+    uint32_t **d_flg = nullptr;
+    auto undo = [&](int st) {
+      for (int r = 0; r < nr; ++r) {
+        if (pb[r]) (void)hipIpcCloseMemHandle(pb[r]);
+        if (pf[r]) (void)hipIpcCloseMemHandle(pf[r]);
+      }
+      if (d_buf) (void)hipFree(d_buf);
+      if (d_flg) (void)hipFree(d_flg);
+      return st;
+    };
+    std::vector<void *> bufs(static_cast<size_t>(nr), nullptr), flg(static_cast<size_t>(nr), nullptr);
+    uint64_t narrow = 0;
+    const uintptr_t my_phase = reinterpret_cast<uintptr_t>(w.buf) & 15;
+    // the peers' flag arrays: mapped by the first import, and again whenever a
+    // peer's blob carries another flags generation (it reset and re-exported)
+    bool remap = !c->flags_mapped;
+    for (int r = 0; r < nr && !remap; ++r)
+      if (r != c->rank && c->peer_flags_gen[static_cast<size_t>(r)] != bl[r].flags_gen) remap = true;
     for (int r = 0; r < nr; ++r) {
-      if (pb[r]) (void)hipIpcCloseMemHandle(pb[r]);
-      if (pf[r]) (void)hipIpcCloseMemHandle(pf[r]);
-    }
-    if (d_buf) (void)hipFree(d_buf);
-    if (d_flg) (void)hipFree(d_flg);
-    return st;
-  };
-  std::vector<void *> bufs(static_cast<size_t>(nr), nullptr), flg(static_cast<size_t>(nr), nullptr);
-  uint64_t narrow = 0;
-  const uintptr_t my_phase = reinterpret_cast<uintptr_t>(w.buf) & 15;
-  // the peers' flag arrays: mapped by the first import, and again whenever a
-  // peer's blob carries another flags generation (it reset and re-exported)
-  bool remap = !c->flags_mapped;
-  for (int r = 0; r < nr && !remap; ++r)
-    if (r != c->rank && c->peer_flags_gen[static_cast<size_t>(r)] != bl[r].flags_gen) remap = true;
-  for (int r = 0; r < nr; ++r) {
-    if (r == c->rank) {
-      bufs[r] = w.buf;
-      flg[r] = c->flags;
-      continue;
-    }
-    hipError_t e = hipIpcOpenMemHandle(&pb[r], bl[r].buf, hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess) return undo(static_cast<int>(e));
-    bufs[r] = static_cast<unsigned char *>(pb[r]) + bl[r].offset;
-    if ((reinterpret_cast<uintptr_t>(bufs[r]) & 15) != my_phase) narrow |= uint64_t{1} << r;
-    if (remap) {
-      if (c->flags_mapped && c->peer_flags_gen[static_cast<size_t>(r)] == bl[r].flags_gen) {
-        flg[r] = c->peer_flags_base[static_cast<size_t>(r)];  // unchanged: keep the mapping
+      if (r == c->rank) {
+        bufs[r] = w.buf;
+        flg[r] = c->flags;
         continue;
       }
-      e = hipIpcOpenMemHandle(&pf[r], bl[r].flags, hipIpcMemLazyEnablePeerAccess);
+      hipError_t e = hipIpcOpenMemHandle(&pb[r], bl[r].buf, hipIpcMemLazyEnablePeerAccess);
       if (e != hipSuccess) return undo(static_cast<int>(e));
-      flg[r] = pf[r];
-    }
-  }
-  hipError_t e = hipMalloc(reinterpret_cast<void **>(&d_buf), nr * sizeof(void *));
-  if (e == hipSuccess) e = hipMemcpy(d_buf, bufs.data(), nr * sizeof(void *), hipMemcpyHostToDevice);
-  if (e == hipSuccess && remap) {
-    e = hipMalloc(reinterpret_cast<void **>(&d_flg), nr * sizeof(void *));
-    if (e == hipSuccess) e = hipMemcpy(d_flg, flg.data(), nr * sizeof(void *), hipMemcpyHostToDevice);
-  }
-  if (e != hipSuccess) return undo(static_cast<int>(e));
-  // commit
-  w.peer_base = pb;
-  w.d_peer_buf = d_buf;
-  w.peer_buf = bufs;
-  w.peer_bytes.assign(static_cast<size_t>(nr), 0);
-  w.min_bytes = INT64_MAX;
-  for (int r = 0; r < nr; ++r) {
-    w.peer_bytes[static_cast<size_t>(r)] = bl[r].bytes;
-    w.min_bytes = std::min<int64_t>(w.min_bytes, bl[r].bytes);
-  }
-  w.narrow = narrow;
-  w.ready = true;
-  if (remap) {
-    // close the replaced peer mappings (every window's kernels read peers'
-    // flags through d_peer_flags only, which is swapped here).  Kernels on the
-    // callers' compute streams (k_p2p_signal, k_p2p_signal_mask,
-    // k_p2p_red_push) dereference the old table too, and their streams are not
-    // known here: drain the whole device before the old mappings close
-    // (import is a setup call, not on the step path)
-    if (c->flags_mapped) (void)hipDeviceSynchronize();
-    else if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
-    std::vector<void *> base(static_cast<size_t>(nr), nullptr);
-    for (int r = 0; r < nr; ++r) {
-      if (r == c->rank) continue;
-      void *old = c->flags_mapped ? c->peer_flags_base[static_cast<size_t>(r)] : nullptr;
-      if (pf[r]) {
-        if (old) (void)hipIpcCloseMemHandle(old);
-        base[static_cast<size_t>(r)] = pf[r];
-      } else {
-        base[static_cast<size_t>(r)] = old;
+      bufs[r] = static_cast<unsigned char *>(pb[r]) + bl[r].offset;
+      if ((reinterpret_cast<uintptr_t>(bufs[r]) & 15) != my_phase) narrow |= uint64_t{1} << r;
+      if (remap) {
+        if (c->flags_mapped && c->peer_flags_gen[static_cast<size_t>(r)] == bl[r].flags_gen) {
+          flg[r] = c->peer_flags_base[static_cast<size_t>(r)];  // unchanged: keep the mapping
+          continue;
+        }
+        e = hipIpcOpenMemHandle(&pf[r], bl[r].flags, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) return undo(static_cast<int>(e));
+        flg[r] = pf[r];
       }
     }
-    if (c->d_peer_flags) (void)hipFree(c->d_peer_flags);
-    c->peer_flags_base = base;
-    c->peer_flags_gen.assign(static_cast<size_t>(nr), 0);
-    for (int r = 0; r < nr; ++r) c->peer_flags_gen[static_cast<size_t>(r)] = bl[r].flags_gen;
-    c->d_peer_flags = d_flg;
-    c->flags_mapped = true;
-  }
-  return LHPC_OK;
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&d_buf), nr * sizeof(void *));
+    if (e == hipSuccess) e = hipMemcpy(d_buf, bufs.data(), nr * sizeof(void *), hipMemcpyHostToDevice);
+    if (e == hipSuccess && remap) {
+      e = hipMalloc(reinterpret_cast<void **>(&d_flg), nr * sizeof(void *));
+      if (e == hipSuccess) e = hipMemcpy(d_flg, flg.data(), nr * sizeof(void *), hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) return undo(static_cast<int>(e));
+    // commit
+    w.peer_base = pb;
+    w.d_peer_buf = d_buf;
+    w.peer_buf = bufs;
+    w.peer_bytes.assign(static_cast<size_t>(nr), 0);
+    w.min_bytes = INT64_MAX;
+    for (int r = 0; r < nr; ++r) {
+      w.peer_bytes[static_cast<size_t>(r)] = bl[r].bytes;
+      w.min_bytes = std::min<int64_t>(w.min_bytes, bl[r].bytes);
+    }
+    w.narrow = narrow;
+    w.ready = true;
+    if (remap) {
+      // close the replaced peer mappings (every window's kernels read peers'
+      // flags through d_peer_flags only, which is swapped here).  Kernels on the
+      // callers' compute streams (k_p2p_signal, k_p2p_signal_mask,
+      // k_p2p_red_push) dereference the old table too, and their streams are not
+      // known here: drain the whole device before the old mappings close
+      // (import is a setup call, not on the step path)
+      if (c->flags_mapped) (void)hipDeviceSynchronize();
+      else if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
+      std::vector<void *> base(static_cast<size_t>(nr), nullptr);
+      for (int r = 0; r < nr; ++r) {
+        if (r == c->rank) continue;
+        void *old = c->flags_mapped ? c->peer_flags_base[static_cast<size_t>(r)] : nullptr;
+        if (pf[r]) {
+          if (old) (void)hipIpcCloseMemHandle(old);
+          base[static_cast<size_t>(r)] = pf[r];
+        } else {
+          base[static_cast<size_t>(r)] = old;
+        }
+      }
+      if (c->d_peer_flags) (void)hipFree(c->d_peer_flags);
+      c->peer_flags_base = base;
+      c->peer_flags_gen.assign(static_cast<size_t>(nr), 0);
+      for (int r = 0; r < nr; ++r) c->peer_flags_gen[static_cast<size_t>(r)] = bl[r].flags_gen;
+      c->d_peer_flags = d_flg;
+      c->flags_mapped = true;
+    }
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_p2p_unmap(lhpc_dist_comm *c, void *y) {
-  if (!c || !y || c->n_win == 0 || c->win[c->n_win - 1].buf != y) return LHPC_ERR_INVALID_ARG;
-  LHPC_HIP_TRY(hipSetDevice(c->device));
-  if (c->s_comm) LHPC_HIP_TRY(hipStreamSynchronize(c->s_comm));
-  window_release(c->win[--c->n_win]);
-  return LHPC_OK;
+  try {
+    if (!c || !y || c->n_win == 0 || c->win[c->n_win - 1].buf != y) return LHPC_ERR_INVALID_ARG;
+    LHPC_HIP_TRY(hipSetDevice(c->device));
+    if (c->s_comm) LHPC_HIP_TRY(hipStreamSynchronize(c->s_comm));
+    window_release(c->win[--c->n_win]);
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_p2p_reset(lhpc_dist_comm *c) {
-  if (!c) return LHPC_ERR_INVALID_ARG;
-  LHPC_HIP_TRY(hipSetDevice(c->device));
-  if (c->s_comm) LHPC_HIP_TRY(hipStreamSynchronize(c->s_comm));
-  p2p_release(c);
-  return LHPC_OK;
+  try {
+    if (!c) return LHPC_ERR_INVALID_ARG;
+    LHPC_HIP_TRY(hipSetDevice(c->device));
+    if (c->s_comm) LHPC_HIP_TRY(hipStreamSynchronize(c->s_comm));
+    p2p_release(c);
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_p2p_status(const lhpc_dist_comm *c) {
-  if (!c) return LHPC_ERR_INVALID_ARG;
-  return c->h_status && *c->h_status ? LHPC_ERR_INTERNAL : LHPC_OK;
+  try {
+    if (!c) return LHPC_ERR_INVALID_ARG;
+    return c->h_status && *c->h_status ? LHPC_ERR_INTERNAL : LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_comm_destroy(lhpc_dist_comm *c) {
-  if (!c) return LHPC_OK;
-  (void)hipSetDevice(c->device);
-  if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
-  p2p_release(c);
-  int st = LHPC_OK;
-  if (c->comm) {
-    const ncclResult_t r = ncclCommDestroy(c->comm);
-    if (r != ncclSuccess) st = LHPC_RCCL_STATUS_BASE + static_cast<int>(r);
-  }
-  if (c->s_comm) (void)hipStreamDestroy(c->s_comm);
-  if (c->ev_in) (void)hipEventDestroy(c->ev_in);
-  if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
-  delete c;
-  return st;
+  try {
+    if (!c) return LHPC_OK;
+    (void)hipSetDevice(c->device);
+    if (c->s_comm) (void)hipStreamSynchronize(c->s_comm);
+    p2p_release(c);
+    int st = LHPC_OK;
+    if (c->comm) {
+      const ncclResult_t r = ncclCommDestroy(c->comm);
+      if (r != ncclSuccess) st = LHPC_RCCL_STATUS_BASE + static_cast<int>(r);
+    }
+    if (c->s_comm) (void)hipStreamDestroy(c->s_comm);
+    if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+    if (c->ev_halo) (void)hipEventDestroy(c->ev_halo);
+    delete c;
+    return st;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_comm_info(const lhpc_dist_comm *c, int *nranks, int *rank, int *device) {
-  if (!c) return LHPC_ERR_INVALID_ARG;
-  if (nranks) *nranks = c->nranks;
-  if (rank) *rank = c->rank;
-  if (device) *device = c->device;
-  return LHPC_OK;
+  try {
+    if (!c) return LHPC_ERR_INVALID_ARG;
+    if (nranks) *nranks = c->nranks;
+    if (rank) *rank = c->rank;
+    if (device) *device = c->device;
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 namespace {
@@ -888,110 +914,118 @@ int allgather_f64(lhpc_dist_comm *c, const double *vals, int count, double *out,
 
 extern "C" int lhpc_dist_allgather_f64(lhpc_dist_comm *c, const double *vals, int64_t count, double *out,
                                        void *stream) {
-  if (!c || count < 0 || (count > 0 && (!vals || !out))) return LHPC_ERR_INVALID_ARG;
-  if (count == 0) return LHPC_OK;
-  LHPC_HIP_TRY(hipSetDevice(c->device));
-  if (!c->comm && c->nranks > 1 && count > kRedMax) return LHPC_ERR_UNSUPPORTED;
-  return allgather_f64(c, vals, static_cast<int>(count), out, static_cast<hipStream_t>(stream));
+  try {
+    if (!c || count < 0 || (count > 0 && (!vals || !out))) return LHPC_ERR_INVALID_ARG;
+    if (count == 0) return LHPC_OK;
+    LHPC_HIP_TRY(hipSetDevice(c->device));
+    if (!c->comm && c->nranks > 1 && count > kRedMax) return LHPC_ERR_UNSUPPORTED;
+    return allgather_f64(c, vals, static_cast<int>(count), out, static_cast<hipStream_t>(stream));
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_allreduce_sum_f64(lhpc_dist_comm *c, double *buf, int64_t count, void *stream) {
-  if (!c || (count > 0 && !buf) || count < 0) return LHPC_ERR_INVALID_ARG;
-  if (count == 0) return LHPC_OK;
-  LHPC_HIP_TRY(hipSetDevice(c->device));
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (c->comm) {
-    LHPC_NCCL_TRY(ncclAllReduce(buf, buf, static_cast<size_t>(count), ncclFloat64, ncclSum, c->comm, s));
-    return LHPC_OK;
-  }
-  // P2P communicator: gather every rank's values, add them in rank order
-  if (c->nranks == 1) return LHPC_OK;
-  if (count > kRedMax) return LHPC_ERR_UNSUPPORTED;
-  double *g = nullptr;
-  LHPC_HIP_TRY(lhpc::scratch_alloc(reinterpret_cast<void **>(&g), static_cast<size_t>(c->nranks * count) * 8, s));
-  int st = allgather_f64(c, buf, static_cast<int>(count), g, s);
-  if (st == LHPC_OK) {
-    hipLaunchKernelGGL(k_sum_ranks, dim3(1), dim3(64), 0, s, g, c->nranks, static_cast<int>(count), buf);
-    st = static_cast<int>(hipGetLastError());
-  }
-  (void)hipFreeAsync(g, s);
-  return st;
+  try {
+    if (!c || (count > 0 && !buf) || count < 0) return LHPC_ERR_INVALID_ARG;
+    if (count == 0) return LHPC_OK;
+    LHPC_HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (c->comm) {
+      LHPC_NCCL_TRY(ncclAllReduce(buf, buf, static_cast<size_t>(count), ncclFloat64, ncclSum, c->comm, s));
+      return LHPC_OK;
+    }
+    // P2P communicator: gather every rank's values, add them in rank order
+    if (c->nranks == 1) return LHPC_OK;
+    if (count > kRedMax) return LHPC_ERR_UNSUPPORTED;
+    double *g = nullptr;
+    LHPC_HIP_TRY(lhpc::scratch_alloc(reinterpret_cast<void **>(&g), static_cast<size_t>(c->nranks * count) * 8, s));
+    int st = allgather_f64(c, buf, static_cast<int>(count), g, s);
+    if (st == LHPC_OK) {
+      hipLaunchKernelGGL(k_sum_ranks, dim3(1), dim3(64), 0, s, g, c->nranks, static_cast<int>(count), buf);
+      st = static_cast<int>(hipGetLastError());
+    }
+    (void)hipFreeAsync(g, s);
+    return st;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_spmv_plan_create_opts(lhpc_dist_spmv_plan **out, lhpc_dist_comm *comm, int dtype,
                                                int64_t n_rows, int64_t n_cols, int K, const int64_t *cuts,
                                                const void *row_ptr, int row_ptr_bits, const int32_t *col_idx,
                                                const void *val, unsigned flags, const lhpc_options *opts) {
-  if (!out || !comm || !cuts || !row_ptr || K < 1 || n_rows < 0 || n_cols < 0 ||
-      (dtype != LHPC_F32 && dtype != LHPC_F64) || (row_ptr_bits != 32 && row_ptr_bits != 64))
-    return LHPC_ERR_INVALID_ARG;
-  *out = nullptr;
-  const int nr = comm->nranks, rk = comm->rank;
-  const int64_t nb = static_cast<int64_t>(nr) * K;
-  if (cuts[0] != 0 || cuts[nb] != n_rows) return LHPC_ERR_INVALID_ARG;
-  for (int64_t b = 0; b < nb; ++b)
-    if (cuts[b + 1] < cuts[b]) return LHPC_ERR_INVALID_ARG;
-  const lhpc_options o = lhpc::resolve_options(opts);
-  if (o.dist_exchange < LHPC_DIST_EXCHANGE_AUTO || o.dist_exchange > LHPC_DIST_EXCHANGE_NONE) return LHPC_ERR_INVALID_ARG;
-  if (K > 63) return LHPC_ERR_INVALID_ARG;  // the P2P DONE flag carries the chunk in 6 bits
-  LHPC_HIP_TRY(hipSetDevice(comm->device));
-  auto *d = new (std::nothrow) lhpc_dist_spmv_plan();
-  if (!d) return LHPC_ERR_ALLOC;
-  d->comm = comm;
-  d->dtype = dtype;
-  d->K = K;
-  d->n_rows = n_rows;
-  d->n_cols = n_cols;
-  d->opt = o;
-  d->cuts.assign(cuts, cuts + nb + 1);
-  build_schedule(cuts, nr, K, rk, LHPC_DIST_EXCHANGE_RCCL, o.dist_broadcast, d->sched_rccl, d->first_rccl);
-  lhpc::rccl_calls_of(d->sched_rccl.data(), static_cast<int64_t>(d->sched_rccl.size()), dtype, d->calls_rccl);
-  build_schedule(cuts, nr, K, rk, LHPC_DIST_EXCHANGE_P2P, 0, d->sched_p2p, d->first_p2p);
-  // the local CSR: the rank's K blocks stacked in chunk order
-  std::vector<int64_t> ls(static_cast<size_t>(K) + 1, 0);
-  for (int k = 0; k < K; ++k) {
-    const int64_t b = static_cast<int64_t>(k) * nr + rk;
-    ls[k + 1] = ls[k] + (cuts[b + 1] - cuts[b]);
-  }
-  int st = lhpc::local_plans_create(d->lp, dtype, n_cols, K, ls.data(), row_ptr, row_ptr_bits, col_idx, val,
-                                    comm->device, flags, o);
-  // column parts of the stage for chained calls (square matrices: chunk j's
-  // rows of y are columns [cuts[j·N], cuts[(j+1)·N]) of the next x)
-  if (st == LHPC_OK && n_rows == n_cols) {
-    std::vector<int64_t> col_end(static_cast<size_t>(K));
-    for (int j = 0; j < K; ++j) col_end[static_cast<size_t>(j)] = cuts[static_cast<int64_t>(j + 1) * nr];
-    d->chain = lhpc::local_plans_column_parts(d->lp, col_end.data(), K);
-  }
-  if (st == LHPC_OK) {
-    d->ev.assign(static_cast<size_t>(K), nullptr);
-    d->ev_x.assign(static_cast<size_t>(K), nullptr);
-    for (auto &e : d->ev_x)
-      if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (auto &e : d->ev)
-      if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->done, hipEventDisableTiming));
-    const int nstreams = o.dist_reduce_streams > 0 ? o.dist_reduce_streams : 2;
-    if (st == LHPC_OK && nstreams > 1 && K > 1) {
-      st = static_cast<int>(hipStreamCreateWithFlags(&d->s_red2, hipStreamNonBlocking));
-      if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
-      if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
+  try {
+    if (!out || !comm || !cuts || !row_ptr || K < 1 || n_rows < 0 || n_cols < 0 ||
+        (dtype != LHPC_F32 && dtype != LHPC_F64) || (row_ptr_bits != 32 && row_ptr_bits != 64))
+      return LHPC_ERR_INVALID_ARG;
+    *out = nullptr;
+    const int nr = comm->nranks, rk = comm->rank;
+    const int64_t nb = static_cast<int64_t>(nr) * K;
+    if (cuts[0] != 0 || cuts[nb] != n_rows) return LHPC_ERR_INVALID_ARG;
+    for (int64_t b = 0; b < nb; ++b)
+      if (cuts[b + 1] < cuts[b]) return LHPC_ERR_INVALID_ARG;
+    const lhpc_options o = lhpc::resolve_options(opts);
+    if (o.dist_exchange < LHPC_DIST_EXCHANGE_AUTO || o.dist_exchange > LHPC_DIST_EXCHANGE_NONE) return LHPC_ERR_INVALID_ARG;
+    if (K > 63) return LHPC_ERR_INVALID_ARG;  // the P2P DONE flag carries the chunk in 6 bits
+    LHPC_HIP_TRY(hipSetDevice(comm->device));
+    auto *d = new (std::nothrow) lhpc_dist_spmv_plan();
+    if (!d) return LHPC_ERR_ALLOC;
+    d->comm = comm;
+    d->dtype = dtype;
+    d->K = K;
+    d->n_rows = n_rows;
+    d->n_cols = n_cols;
+    d->opt = o;
+    d->cuts.assign(cuts, cuts + nb + 1);
+    build_schedule(cuts, nr, K, rk, LHPC_DIST_EXCHANGE_RCCL, o.dist_broadcast, d->sched_rccl, d->first_rccl);
+    lhpc::rccl_calls_of(d->sched_rccl.data(), static_cast<int64_t>(d->sched_rccl.size()), dtype, d->calls_rccl);
+    build_schedule(cuts, nr, K, rk, LHPC_DIST_EXCHANGE_P2P, 0, d->sched_p2p, d->first_p2p);
+    // the local CSR: the rank's K blocks stacked in chunk order
+    std::vector<int64_t> ls(static_cast<size_t>(K) + 1, 0);
+    for (int k = 0; k < K; ++k) {
+      const int64_t b = static_cast<int64_t>(k) * nr + rk;
+      ls[k + 1] = ls[k] + (cuts[b + 1] - cuts[b]);
     }
-    if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->ev_p2p, hipEventDisableTiming));
-  }
-  if (st != LHPC_OK) {
-    destroy_spmv(d);
-    return st;
-  }
-  *out = d;
-  return LHPC_OK;
+    int st = lhpc::local_plans_create(d->lp, dtype, n_cols, K, ls.data(), row_ptr, row_ptr_bits, col_idx, val,
+                                      comm->device, flags, o);
+    // column parts of the stage for chained calls (square matrices: chunk j's
+    // rows of y are columns [cuts[j·N], cuts[(j+1)·N]) of the next x)
+    if (st == LHPC_OK && n_rows == n_cols) {
+      std::vector<int64_t> col_end(static_cast<size_t>(K));
+      for (int j = 0; j < K; ++j) col_end[static_cast<size_t>(j)] = cuts[static_cast<int64_t>(j + 1) * nr];
+      d->chain = lhpc::local_plans_column_parts(d->lp, col_end.data(), K);
+    }
+    if (st == LHPC_OK) {
+      d->ev.assign(static_cast<size_t>(K), nullptr);
+      d->ev_x.assign(static_cast<size_t>(K), nullptr);
+      for (auto &e : d->ev_x)
+        if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      for (auto &e : d->ev)
+        if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->done, hipEventDisableTiming));
+      const int nstreams = o.dist_reduce_streams > 0 ? o.dist_reduce_streams : 2;
+      if (st == LHPC_OK && nstreams > 1 && K > 1) {
+        st = static_cast<int>(hipStreamCreateWithFlags(&d->s_red2, hipStreamNonBlocking));
+        if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
+        if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
+      }
+      if (st == LHPC_OK) st = static_cast<int>(hipEventCreateWithFlags(&d->ev_p2p, hipEventDisableTiming));
+    }
+    if (st != LHPC_OK) {
+      destroy_spmv(d);
+      return st;
+    }
+    *out = d;
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_spmv_plan_create(lhpc_dist_spmv_plan **out, lhpc_dist_comm *comm, int dtype,
                                           int64_t n_rows, int64_t n_cols, int K, const int64_t *cuts,
                                           const void *row_ptr, int row_ptr_bits, const int32_t *col_idx,
                                           const void *val, unsigned flags) {
-  return lhpc_dist_spmv_plan_create_opts(out, comm, dtype, n_rows, n_cols, K, cuts, row_ptr, row_ptr_bits, col_idx,
-                                         val, flags, nullptr);
+  try {
+    return lhpc_dist_spmv_plan_create_opts(out, comm, dtype, n_rows, n_cols, K, cuts, row_ptr, row_ptr_bits, col_idx,
+                                           val, flags, nullptr);
+  } LHPC_ABI_CATCH
 }
 
 namespace {
@@ -1080,43 +1114,53 @@ int exchange_begin(lhpc_dist_spmv_plan *d, void *y, hipStream_t s) {
 }  // namespace
 
 extern "C" int lhpc_dist_spmv_begin(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream) {
-  return spmv_begin(d, x, y, static_cast<hipStream_t>(stream), false);
+  try {
+    return spmv_begin(d, x, y, static_cast<hipStream_t>(stream), false);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_spmv_plan_info(const lhpc_dist_spmv_plan *d, lhpc_spmv_plan_info *info, int *chained_stage) {
-  if (!d || !info) return LHPC_ERR_INVALID_ARG;
-  const lhpc_spmv_plan *q = d->lp.split;
-  for (const lhpc_spmv_plan *b : d->lp.block_plan)
-    if (!q && b) q = b;
-  if (chained_stage) *chained_stage = d->chain ? 1 : 0;
-  if (!q) {  // no local rows
-    std::memset(info, 0, sizeof(*info));
-    info->dtype = d->dtype;
-    info->n_cols = d->n_cols;
-    info->device = d->comm->device;
-    return LHPC_OK;
-  }
-  return lhpc_spmv_plan_info_get(q, info);
+  try {
+    if (!d || !info) return LHPC_ERR_INVALID_ARG;
+    const lhpc_spmv_plan *q = d->lp.split;
+    for (const lhpc_spmv_plan *b : d->lp.block_plan)
+      if (!q && b) q = b;
+    if (chained_stage) *chained_stage = d->chain ? 1 : 0;
+    if (!q) {  // no local rows
+      std::memset(info, 0, sizeof(*info));
+      info->dtype = d->dtype;
+      info->n_cols = d->n_cols;
+      info->device = d->comm->device;
+      return LHPC_OK;
+    }
+    return lhpc_spmv_plan_info_get(q, info);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_spmv_end(lhpc_dist_spmv_plan *d, void *stream) {
-  if (!d) return LHPC_ERR_INVALID_ARG;
-  LHPC_HIP_TRY(hipSetDevice(d->comm->device));
-  return wait_pending(d, static_cast<hipStream_t>(stream));
+  try {
+    if (!d) return LHPC_ERR_INVALID_ARG;
+    LHPC_HIP_TRY(hipSetDevice(d->comm->device));
+    return wait_pending(d, static_cast<hipStream_t>(stream));
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_spmv(lhpc_dist_spmv_plan *d, const void *x, void *y, void *stream) {
-  LHPC_TRY(lhpc_dist_spmv_begin(d, x, y, stream));
-  return lhpc_dist_spmv_end(d, stream);
+  try {
+    LHPC_TRY(lhpc_dist_spmv_begin(d, x, y, stream));
+    return lhpc_dist_spmv_end(d, stream);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_exchange(lhpc_dist_spmv_plan *d, void *y, void *stream) {
-  if (!d || (d->n_rows > 0 && !y)) return LHPC_ERR_INVALID_ARG;
-  lhpc::RocTxRange rx("lhpc_dist_exchange");
-  LHPC_HIP_TRY(hipSetDevice(d->comm->device));
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  LHPC_TRY(exchange_begin(d, y, s));
-  return wait_pending(d, s);
+  try {
+    if (!d || (d->n_rows > 0 && !y)) return LHPC_ERR_INVALID_ARG;
+    lhpc::RocTxRange rx("lhpc_dist_exchange");
+    LHPC_HIP_TRY(hipSetDevice(d->comm->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    LHPC_TRY(exchange_begin(d, y, s));
+    return wait_pending(d, s);
+  } LHPC_ABI_CATCH
 }
 
 namespace {
@@ -1137,238 +1181,246 @@ __global__ void k_sum_blocks(const double *gathered, int nranks, int K, double *
 
 extern "C" int lhpc_dist_cg_solve(lhpc_dist_spmv_plan *d, const void *b, void *x, void *p_work, double tol,
                                   int max_iter, int check_every, int *iters_out, double *resid_out, void *stream) {
-  if (!d || !b || !x || !p_work || max_iter < 0 || !(tol >= 0.0) || d->n_rows != d->n_cols || b == x ||
-      p_work == x || p_work == b)
-    return LHPC_ERR_INVALID_ARG;
-  lhpc_dist_comm *c = d->comm;
-  if (d->K > kRedMax) return LHPC_ERR_UNSUPPORTED;  // K dot partials per rank in one all-gather
-  lhpc::RocTxRange rx("lhpc_dist_cg_solve");
-  LHPC_HIP_TRY(hipSetDevice(c->device));
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  LHPC_TRY(wait_pending(d, s));
-  const int N = c->nranks, K = d->K, dt = d->dtype;
-  const int64_t n = d->n_rows;
-  const size_t ts = dt == LHPC_F32 ? 4 : 8;
-  if (check_every < 1) check_every = 1;
-  auto at = [&](const void *v, int64_t i) { return static_cast<unsigned char *>(const_cast<void *>(v)) + i * ts; };
-  // this rank's K blocks of rows
-  std::vector<int64_t> r0(static_cast<size_t>(K)), len(static_cast<size_t>(K));
-  for (int k = 0; k < K; ++k) {
-    const int64_t bi = static_cast<int64_t>(k) * N + c->rank;
-    r0[static_cast<size_t>(k)] = d->cuts[bi];
-    len[static_cast<size_t>(k)] = d->cuts[bi + 1] - d->cuts[bi];
-  }
-  // scratch: r and q (full length: the SpMV writes q at global rows), the
-  // scalars [rr0, rr1, pq, bb, one] and the dot partials / their all-gather
-  void *vec = nullptr;
-  double *sc = nullptr;
-  LHPC_HIP_TRY(lhpc::scratch_alloc(&vec, static_cast<size_t>(std::max<int64_t>(n, 1)) * ts * 2, s));
-  struct Free {
-    void *a;
-    hipStream_t s;
-    ~Free() { (void)hipFreeAsync(a, s); }
-  } fv{vec, s};
-  const int parts = 8 + K + N * K;
-  LHPC_HIP_TRY(lhpc::scratch_alloc(reinterpret_cast<void **>(&sc), static_cast<size_t>(parts) * 8, s));
-  Free fs{sc, s};
-  void *r = vec, *q = at(vec, n);
-  double *rr[2] = {sc, sc + 1}, *pq = sc + 2, *bb = sc + 3, *one = sc + 4, *part = sc + 8, *gath = sc + 8 + K;
-  hipLaunchKernelGGL(k_set_scalars, dim3(1), dim3(64), 0, s, one, 1.0, 1);
-  LHPC_HIP_TRY(hipGetLastError());
-  // global dot from this rank's K block partials: all-gather, block-order sum
-  auto global_dot = [&](double *out) -> int {
-    LHPC_TRY(allgather_f64(c, part, K, gath, s));
-    hipLaunchKernelGGL(k_sum_blocks, dim3(1), dim3(64), 0, s, gath, N, K, out);
-    return static_cast<int>(hipGetLastError());
-  };
-  auto dots = [&](const void *a, const void *bv, double *out) -> int {
-    for (int k = 0; k < K; ++k) LHPC_TRY(lhpc_vec_dot(dt, len[k], at(a, r0[k]), at(bv, r0[k]), part + k, s));
-    return global_dot(out);
-  };
-  if (!d->h_scalars)
-    LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&d->h_scalars), 2 * sizeof(double), hipHostMallocDefault));
-  double &h_rr = d->h_scalars[0], &h_bb = d->h_scalars[1];
-  h_rr = h_bb = 0.0;
-  // bb = b·b; q = A·x (x complete on every rank); r = b − q; p = r; rr = r·r
-  LHPC_TRY(dots(b, b, bb));
-  LHPC_TRY(spmv_begin(d, x, q, s, true));
-  for (int k = 0; k < K; ++k) {
-    if (!len[k]) {
-      LHPC_HIP_TRY(hipMemsetAsync(part + k, 0, 8, s));
-      continue;
+  try {
+    if (!d || !b || !x || !p_work || max_iter < 0 || !(tol >= 0.0) || d->n_rows != d->n_cols || b == x ||
+        p_work == x || p_work == b)
+      return LHPC_ERR_INVALID_ARG;
+    lhpc_dist_comm *c = d->comm;
+    if (d->K > kRedMax) return LHPC_ERR_UNSUPPORTED;  // K dot partials per rank in one all-gather
+    lhpc::RocTxRange rx("lhpc_dist_cg_solve");
+    LHPC_HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    LHPC_TRY(wait_pending(d, s));
+    const int N = c->nranks, K = d->K, dt = d->dtype;
+    const int64_t n = d->n_rows;
+    const size_t ts = dt == LHPC_F32 ? 4 : 8;
+    if (check_every < 1) check_every = 1;
+    auto at = [&](const void *v, int64_t i) { return static_cast<unsigned char *>(const_cast<void *>(v)) + i * ts; };
+    // this rank's K blocks of rows
+    std::vector<int64_t> r0(static_cast<size_t>(K)), len(static_cast<size_t>(K));
+    for (int k = 0; k < K; ++k) {
+      const int64_t bi = static_cast<int64_t>(k) * N + c->rank;
+      r0[static_cast<size_t>(k)] = d->cuts[bi];
+      len[static_cast<size_t>(k)] = d->cuts[bi + 1] - d->cuts[bi];
     }
-    LHPC_HIP_TRY(hipMemcpyAsync(at(r, r0[k]), at(b, r0[k]), len[k] * ts, hipMemcpyDeviceToDevice, s));
-    LHPC_TRY(lhpc_cg_step_r(dt, len[k], one, one, at(r, r0[k]), at(q, r0[k]), part + k, s));
-    LHPC_HIP_TRY(hipMemcpyAsync(at(p_work, r0[k]), at(r, r0[k]), len[k] * ts, hipMemcpyDeviceToDevice, s));
-  }
-  LHPC_TRY(global_dot(rr[0]));
-  LHPC_TRY(exchange_begin(d, p_work, s));  // p complete on every rank; the next stage waits per chunk
-  LHPC_HIP_TRY(hipMemcpyAsync(&h_bb, bb, 8, hipMemcpyDeviceToHost, s));  // pinned
-  LHPC_HIP_TRY(hipMemcpyAsync(&h_rr, rr[0], 8, hipMemcpyDeviceToHost, s));
-  LHPC_HIP_TRY(hipStreamSynchronize(s));
-  const double stop = tol * tol * (h_bb > 0.0 ? h_bb : 1.0);
-  int it = 0, cur = 0, status = LHPC_OK;
-  if (h_rr > stop) {
-    for (it = 1; it <= max_iter; ++it) {
-      // q = A·p: a chained stage (part j of p waits only for exchange j)
-      LHPC_TRY(spmv_begin(d, p_work, q, s, true));
-      LHPC_TRY(dots(p_work, q, pq));
-      for (int k = 0; k < K; ++k) {  // r −= α·q, partial r·r
-        if (len[k]) LHPC_TRY(lhpc_cg_step_r(dt, len[k], rr[cur], pq, at(r, r0[k]), at(q, r0[k]), part + k, s));
-        else LHPC_HIP_TRY(hipMemsetAsync(part + k, 0, 8, s));
+    // scratch: r and q (full length: the SpMV writes q at global rows), the
+    // scalars [rr0, rr1, pq, bb, one] and the dot partials / their all-gather
+    void *vec = nullptr;
+    double *sc = nullptr;
+    LHPC_HIP_TRY(lhpc::scratch_alloc(&vec, static_cast<size_t>(std::max<int64_t>(n, 1)) * ts * 2, s));
+    struct Free {
+      void *a;
+      hipStream_t s;
+      ~Free() { (void)hipFreeAsync(a, s); }
+    } fv{vec, s};
+    const int parts = 8 + K + N * K;
+    LHPC_HIP_TRY(lhpc::scratch_alloc(reinterpret_cast<void **>(&sc), static_cast<size_t>(parts) * 8, s));
+    Free fs{sc, s};
+    void *r = vec, *q = at(vec, n);
+    double *rr[2] = {sc, sc + 1}, *pq = sc + 2, *bb = sc + 3, *one = sc + 4, *part = sc + 8, *gath = sc + 8 + K;
+    hipLaunchKernelGGL(k_set_scalars, dim3(1), dim3(64), 0, s, one, 1.0, 1);
+    LHPC_HIP_TRY(hipGetLastError());
+    // global dot from this rank's K block partials: all-gather, block-order sum
+    auto global_dot = [&](double *out) -> int {
+      LHPC_TRY(allgather_f64(c, part, K, gath, s));
+      hipLaunchKernelGGL(k_sum_blocks, dim3(1), dim3(64), 0, s, gath, N, K, out);
+      return static_cast<int>(hipGetLastError());
+    };
+    auto dots = [&](const void *a, const void *bv, double *out) -> int {
+      for (int k = 0; k < K; ++k) LHPC_TRY(lhpc_vec_dot(dt, len[k], at(a, r0[k]), at(bv, r0[k]), part + k, s));
+      return global_dot(out);
+    };
+    if (!d->h_scalars)
+      LHPC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&d->h_scalars), 2 * sizeof(double), hipHostMallocDefault));
+    double &h_rr = d->h_scalars[0], &h_bb = d->h_scalars[1];
+    h_rr = h_bb = 0.0;
+    // bb = b·b; q = A·x (x complete on every rank); r = b − q; p = r; rr = r·r
+    LHPC_TRY(dots(b, b, bb));
+    LHPC_TRY(spmv_begin(d, x, q, s, true));
+    for (int k = 0; k < K; ++k) {
+      if (!len[k]) {
+        LHPC_HIP_TRY(hipMemsetAsync(part + k, 0, 8, s));
+        continue;
       }
-      LHPC_TRY(global_dot(rr[cur ^ 1]));
-      if (it % check_every == 0 || it == max_iter) {
-        LHPC_HIP_TRY(hipMemcpyAsync(&h_rr, rr[cur ^ 1], 8, hipMemcpyDeviceToHost, s));
-        LHPC_HIP_TRY(hipStreamSynchronize(s));
-        if (!std::isfinite(h_rr)) {
-          status = LHPC_ERR_INTERNAL;  // breakdown: the matrix is not SPD?
-          break;
-        }
-        if (h_rr <= stop) {
-          for (int k = 0; k < K; ++k)  // x += α·p
-            if (len[k])
-              LHPC_TRY(lhpc_cg_step_xp(dt, len[k], rr[cur], pq, nullptr, nullptr, at(x, r0[k]), at(p_work, r0[k]),
-                                       nullptr, s));
-          break;
-        }
-      }
-      for (int k = 0; k < K; ++k)  // x += α·p; p = r + β·p
-        if (len[k])
-          LHPC_TRY(lhpc_cg_step_xp(dt, len[k], rr[cur], pq, rr[cur ^ 1], rr[cur], at(x, r0[k]), at(p_work, r0[k]),
-                                   at(r, r0[k]), s));
-      LHPC_TRY(exchange_begin(d, p_work, s));
-      cur ^= 1;
+      LHPC_HIP_TRY(hipMemcpyAsync(at(r, r0[k]), at(b, r0[k]), len[k] * ts, hipMemcpyDeviceToDevice, s));
+      LHPC_TRY(lhpc_cg_step_r(dt, len[k], one, one, at(r, r0[k]), at(q, r0[k]), part + k, s));
+      LHPC_HIP_TRY(hipMemcpyAsync(at(p_work, r0[k]), at(r, r0[k]), len[k] * ts, hipMemcpyDeviceToDevice, s));
     }
-    if (it > max_iter) it = max_iter;
-  }
-  // every rank ends with the whole x: this rank's rows of x go out through
-  // p_work (the registered window when the exchange is P2P)
-  LHPC_TRY(wait_pending(d, s));
-  for (int k = 0; k < K; ++k)
-    if (len[k]) LHPC_HIP_TRY(hipMemcpyAsync(at(p_work, r0[k]), at(x, r0[k]), len[k] * ts, hipMemcpyDeviceToDevice, s));
-  LHPC_TRY(exchange_begin(d, p_work, s));
-  LHPC_TRY(wait_pending(d, s));
-  LHPC_HIP_TRY(hipMemcpyAsync(x, p_work, static_cast<size_t>(n) * ts, hipMemcpyDeviceToDevice, s));
-  LHPC_HIP_TRY(hipStreamSynchronize(s));
-  if (c->h_status && *c->h_status) status = LHPC_ERR_INTERNAL;  // a P2P flag wait timed out
-  if (iters_out) *iters_out = it;
-  if (resid_out) *resid_out = std::sqrt(std::max(h_rr, 0.0)) / std::sqrt(h_bb > 0.0 ? h_bb : 1.0);
-  return status;
+    LHPC_TRY(global_dot(rr[0]));
+    LHPC_TRY(exchange_begin(d, p_work, s));  // p complete on every rank; the next stage waits per chunk
+    LHPC_HIP_TRY(hipMemcpyAsync(&h_bb, bb, 8, hipMemcpyDeviceToHost, s));  // pinned
+    LHPC_HIP_TRY(hipMemcpyAsync(&h_rr, rr[0], 8, hipMemcpyDeviceToHost, s));
+    LHPC_HIP_TRY(hipStreamSynchronize(s));
+    const double stop = tol * tol * (h_bb > 0.0 ? h_bb : 1.0);
+    int it = 0, cur = 0, status = LHPC_OK;
+    if (h_rr > stop) {
+      for (it = 1; it <= max_iter; ++it) {
+        // q = A·p: a chained stage (part j of p waits only for exchange j)
+        LHPC_TRY(spmv_begin(d, p_work, q, s, true));
+        LHPC_TRY(dots(p_work, q, pq));
+        for (int k = 0; k < K; ++k) {  // r −= α·q, partial r·r
+          if (len[k]) LHPC_TRY(lhpc_cg_step_r(dt, len[k], rr[cur], pq, at(r, r0[k]), at(q, r0[k]), part + k, s));
+          else LHPC_HIP_TRY(hipMemsetAsync(part + k, 0, 8, s));
+        }
+        LHPC_TRY(global_dot(rr[cur ^ 1]));
+        if (it % check_every == 0 || it == max_iter) {
+          LHPC_HIP_TRY(hipMemcpyAsync(&h_rr, rr[cur ^ 1], 8, hipMemcpyDeviceToHost, s));
+          LHPC_HIP_TRY(hipStreamSynchronize(s));
+          if (!std::isfinite(h_rr)) {
+            status = LHPC_ERR_INTERNAL;  // breakdown: the matrix is not SPD?
+            break;
+          }
+          if (h_rr <= stop) {
+            for (int k = 0; k < K; ++k)  // x += α·p
+              if (len[k])
+                LHPC_TRY(lhpc_cg_step_xp(dt, len[k], rr[cur], pq, nullptr, nullptr, at(x, r0[k]), at(p_work, r0[k]),
+                                         nullptr, s));
+            break;
+          }
+        }
+        for (int k = 0; k < K; ++k)  // x += α·p; p = r + β·p
+          if (len[k])
+            LHPC_TRY(lhpc_cg_step_xp(dt, len[k], rr[cur], pq, rr[cur ^ 1], rr[cur], at(x, r0[k]), at(p_work, r0[k]),
+                                     at(r, r0[k]), s));
+        LHPC_TRY(exchange_begin(d, p_work, s));
+        cur ^= 1;
+      }
+      if (it > max_iter) it = max_iter;
+    }
+    // every rank ends with the whole x: this rank's rows of x go out through
+    // p_work (the registered window when the exchange is P2P)
+    LHPC_TRY(wait_pending(d, s));
+    for (int k = 0; k < K; ++k)
+      if (len[k]) LHPC_HIP_TRY(hipMemcpyAsync(at(p_work, r0[k]), at(x, r0[k]), len[k] * ts, hipMemcpyDeviceToDevice, s));
+    LHPC_TRY(exchange_begin(d, p_work, s));
+    LHPC_TRY(wait_pending(d, s));
+    LHPC_HIP_TRY(hipMemcpyAsync(x, p_work, static_cast<size_t>(n) * ts, hipMemcpyDeviceToDevice, s));
+    LHPC_HIP_TRY(hipStreamSynchronize(s));
+    if (c->h_status && *c->h_status) status = LHPC_ERR_INTERNAL;  // a P2P flag wait timed out
+    if (iters_out) *iters_out = it;
+    if (resid_out) *resid_out = std::sqrt(std::max(h_rr, 0.0)) / std::sqrt(h_bb > 0.0 ? h_bb : 1.0);
+    return status;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_spmv_plan_destroy(lhpc_dist_spmv_plan *d) {
-  destroy_spmv(d);
-  return LHPC_OK;
+  try {
+    destroy_spmv(d);
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_stencil7_f32_x(lhpc_dist_comm *c, float *u, float *out, int64_t nzl, int64_t ny,
                                         int64_t nx, int64_t ghost, float c0, float c1, int exchange, void *stream) {
-  if (!c || !u || !out || nzl < 1 || ny < 0 || nx < 0 || ghost < 1) return LHPC_ERR_INVALID_ARG;
-  if (exchange != LHPC_DIST_EXCHANGE_AUTO && exchange != LHPC_DIST_EXCHANGE_RCCL && exchange != LHPC_DIST_EXCHANGE_P2P)
-    return LHPC_ERR_INVALID_ARG;
-  LHPC_HIP_TRY(hipSetDevice(c->device));
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t P = (ny + 2 * ghost) * (nx + 2 * ghost);  // padded plane
-  auto plane = [&](int64_t z) { return u + (z + ghost) * P; };  // logical plane z ∈ [−ghost, nzl + ghost)
-  const bool lo = c->rank > 0, hi = c->rank < c->nranks - 1;
-  lhpc::RocTxRange rx("lhpc_dist_stencil7_f32");
-  const bool halo = lo || hi;
-  // the exchange: P2P when u is a registered window (AUTO) or asked for
-  const size_t ubytes = static_cast<size_t>(nzl + 2 * ghost) * static_cast<size_t>(P) * 4;
-  const P2pWindow *w = nullptr;
-  if (halo && exchange != LHPC_DIST_EXCHANGE_RCCL) {
-    for (int i = 0; i < c->n_win && !w; ++i)
-      if (c->win[i].ready && c->win[i].buf == u && c->win[i].bytes >= ubytes) w = &c->win[i];
-    if (!w && exchange == LHPC_DIST_EXCHANGE_P2P) return LHPC_ERR_INVALID_ARG;  // u is not a window
-  }
-  if (halo && !w && !c->comm) return LHPC_ERR_UNSUPPORTED;  // a local communicator has no RCCL
-  if (halo) {
-    if (!c->ev_in) LHPC_HIP_TRY(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
-    if (!c->ev_halo) LHPC_HIP_TRY(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
-  }
-  uint64_t mask = 0;
-  if (w) {
-    // READY (epoch) to the neighbours on the compute stream: this rank has
-    // finished every earlier read of u's ghost planes
-    lhpc::RocTxRange rh("lhpc_dist_stencil7_f32: P2P halo");
-    if (*c->h_status) return LHPC_ERR_INTERNAL;  // an earlier flag wait timed out
-    const int64_t pb = P * 4;
-    int64_t nzl_lo = 0;  // the lower neighbour's slab depth, from its window size
-    if (lo) {
-      const int64_t wb = w->peer_bytes[static_cast<size_t>(c->rank - 1)];
-      if (wb % pb || wb / pb - 2 * ghost < 1) return LHPC_ERR_INVALID_ARG;
-      nzl_lo = wb / pb - 2 * ghost;
+  try {
+    if (!c || !u || !out || nzl < 1 || ny < 0 || nx < 0 || ghost < 1) return LHPC_ERR_INVALID_ARG;
+    if (exchange != LHPC_DIST_EXCHANGE_AUTO && exchange != LHPC_DIST_EXCHANGE_RCCL && exchange != LHPC_DIST_EXCHANGE_P2P)
+      return LHPC_ERR_INVALID_ARG;
+    LHPC_HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t P = (ny + 2 * ghost) * (nx + 2 * ghost);  // padded plane
+    auto plane = [&](int64_t z) { return u + (z + ghost) * P; };  // logical plane z ∈ [−ghost, nzl + ghost)
+    const bool lo = c->rank > 0, hi = c->rank < c->nranks - 1;
+    lhpc::RocTxRange rx("lhpc_dist_stencil7_f32");
+    const bool halo = lo || hi;
+    // the exchange: P2P when u is a registered window (AUTO) or asked for
+    const size_t ubytes = static_cast<size_t>(nzl + 2 * ghost) * static_cast<size_t>(P) * 4;
+    const P2pWindow *w = nullptr;
+    if (halo && exchange != LHPC_DIST_EXCHANGE_RCCL) {
+      for (int i = 0; i < c->n_win && !w; ++i)
+        if (c->win[i].ready && c->win[i].buf == u && c->win[i].bytes >= ubytes) w = &c->win[i];
+      if (!w && exchange == LHPC_DIST_EXCHANGE_P2P) return LHPC_ERR_INVALID_ARG;  // u is not a window
     }
-    if (hi && w->peer_bytes[static_cast<size_t>(c->rank + 1)] < (2 * ghost + 1) * pb) return LHPC_ERR_INVALID_ARG;
-    if (lo) mask |= uint64_t{1} << (c->rank - 1);
-    if (hi) mask |= uint64_t{1} << (c->rank + 1);
-    ++c->epoch;
-    if (c->epoch == 0) c->epoch = 1;
-    hipLaunchKernelGGL(k_p2p_signal_mask, dim3(1), dim3(64), 0, s, c->d_peer_flags, c->rank, c->epoch, c->nranks,
-                       c->rank, mask, c->h_status);
-    LHPC_HIP_TRY(hipGetLastError());
-    LHPC_HIP_TRY(hipEventRecord(c->ev_in, s));  // u complete on the caller's stream
-    LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, c->ev_in, 0));
-    hipLaunchKernelGGL(k_p2p_wait_mask, dim3(1), dim3(64), 0, c->s_comm, c->flags, 0, c->epoch, c->nranks, c->rank,
-                       mask, c->h_status);
-    LHPC_HIP_TRY(hipGetLastError());
-    // plane 0 → the lower neighbour's plane nzl_lo (its upper ghost), plane
-    // nzl − 1 → the upper neighbour's plane −1 (its lower ghost)
-    HaloPut h{};
-    int nt = 0;
-    auto add = [&](int peer, const float *src, int64_t dst_off) {
-      h.src[nt] = reinterpret_cast<const unsigned char *>(src);
-      h.dst[nt] = static_cast<unsigned char *>(w->peer_buf[static_cast<size_t>(peer)]) + dst_off;
-      h.bytes[nt] = pb;
-      h.peer[nt] = peer;
-      h.vec[nt] = (reinterpret_cast<uintptr_t>(h.src[nt]) | reinterpret_cast<uintptr_t>(h.dst[nt]) |
-                   static_cast<uintptr_t>(pb)) % 16 == 0;
-      ++nt;
-    };
-    if (lo) add(c->rank - 1, plane(0), (nzl_lo + ghost) * pb);
-    if (hi) add(c->rank + 1, plane(nzl - 1), (ghost - 1) * pb);
-    const unsigned bx = static_cast<unsigned>(std::min<int64_t>(32, (pb / 16 + 255) / 256 + 1));
-    hipLaunchKernelGGL(k_p2p_halo_put, dim3(bx, static_cast<unsigned>(nt)), dim3(256), 0, c->s_comm, h, c->h_status,
-                       c->flags, c->d_peer_flags, c->nranks, c->rank, c->epoch * 64u + 1u);
-    LHPC_HIP_TRY(hipGetLastError());
-    LHPC_HIP_TRY(hipEventRecord(c->ev_halo, c->s_comm));  // this rank's puts issued (u read)
-  } else if (halo) {
-    lhpc::RocTxRange rh("lhpc_dist_stencil7_f32: halo exchange");
-    LHPC_HIP_TRY(hipEventRecord(c->ev_in, s));  // u complete on the caller's stream
-    LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, c->ev_in, 0));
-    LHPC_NCCL_TRY(ncclGroupStart());
-    if (lo) {
-      LHPC_NCCL_TRY(ncclSend(plane(0), static_cast<size_t>(P), ncclFloat32, c->rank - 1, c->comm, c->s_comm));
-      LHPC_NCCL_TRY(ncclRecv(plane(-1), static_cast<size_t>(P), ncclFloat32, c->rank - 1, c->comm, c->s_comm));
+    if (halo && !w && !c->comm) return LHPC_ERR_UNSUPPORTED;  // a local communicator has no RCCL
+    if (halo) {
+      if (!c->ev_in) LHPC_HIP_TRY(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
+      if (!c->ev_halo) LHPC_HIP_TRY(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
     }
-    if (hi) {
-      LHPC_NCCL_TRY(ncclSend(plane(nzl - 1), static_cast<size_t>(P), ncclFloat32, c->rank + 1, c->comm, c->s_comm));
-      LHPC_NCCL_TRY(ncclRecv(plane(nzl), static_cast<size_t>(P), ncclFloat32, c->rank + 1, c->comm, c->s_comm));
+    uint64_t mask = 0;
+    if (w) {
+      // READY (epoch) to the neighbours on the compute stream: this rank has
+      // finished every earlier read of u's ghost planes
+      lhpc::RocTxRange rh("lhpc_dist_stencil7_f32: P2P halo");
+      if (*c->h_status) return LHPC_ERR_INTERNAL;  // an earlier flag wait timed out
+      const int64_t pb = P * 4;
+      int64_t nzl_lo = 0;  // the lower neighbour's slab depth, from its window size
+      if (lo) {
+        const int64_t wb = w->peer_bytes[static_cast<size_t>(c->rank - 1)];
+        if (wb % pb || wb / pb - 2 * ghost < 1) return LHPC_ERR_INVALID_ARG;
+        nzl_lo = wb / pb - 2 * ghost;
+      }
+      if (hi && w->peer_bytes[static_cast<size_t>(c->rank + 1)] < (2 * ghost + 1) * pb) return LHPC_ERR_INVALID_ARG;
+      if (lo) mask |= uint64_t{1} << (c->rank - 1);
+      if (hi) mask |= uint64_t{1} << (c->rank + 1);
+      ++c->epoch;
+      if (c->epoch == 0) c->epoch = 1;
+      hipLaunchKernelGGL(k_p2p_signal_mask, dim3(1), dim3(64), 0, s, c->d_peer_flags, c->rank, c->epoch, c->nranks,
+                         c->rank, mask, c->h_status);
+      LHPC_HIP_TRY(hipGetLastError());
+      LHPC_HIP_TRY(hipEventRecord(c->ev_in, s));  // u complete on the caller's stream
+      LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, c->ev_in, 0));
+      hipLaunchKernelGGL(k_p2p_wait_mask, dim3(1), dim3(64), 0, c->s_comm, c->flags, 0, c->epoch, c->nranks, c->rank,
+                         mask, c->h_status);
+      LHPC_HIP_TRY(hipGetLastError());
+      // plane 0 → the lower neighbour's plane nzl_lo (its upper ghost), plane
+      // nzl − 1 → the upper neighbour's plane −1 (its lower ghost)
+      HaloPut h{};
+      int nt = 0;
+      auto add = [&](int peer, const float *src, int64_t dst_off) {
+        h.src[nt] = reinterpret_cast<const unsigned char *>(src);
+        h.dst[nt] = static_cast<unsigned char *>(w->peer_buf[static_cast<size_t>(peer)]) + dst_off;
+        h.bytes[nt] = pb;
+        h.peer[nt] = peer;
+        h.vec[nt] = (reinterpret_cast<uintptr_t>(h.src[nt]) | reinterpret_cast<uintptr_t>(h.dst[nt]) |
+                     static_cast<uintptr_t>(pb)) % 16 == 0;
+        ++nt;
+      };
+      if (lo) add(c->rank - 1, plane(0), (nzl_lo + ghost) * pb);
+      if (hi) add(c->rank + 1, plane(nzl - 1), (ghost - 1) * pb);
+      const unsigned bx = static_cast<unsigned>(std::min<int64_t>(32, (pb / 16 + 255) / 256 + 1));
+      hipLaunchKernelGGL(k_p2p_halo_put, dim3(bx, static_cast<unsigned>(nt)), dim3(256), 0, c->s_comm, h, c->h_status,
+                         c->flags, c->d_peer_flags, c->nranks, c->rank, c->epoch * 64u + 1u);
+      LHPC_HIP_TRY(hipGetLastError());
+      LHPC_HIP_TRY(hipEventRecord(c->ev_halo, c->s_comm));  // this rank's puts issued (u read)
+    } else if (halo) {
+      lhpc::RocTxRange rh("lhpc_dist_stencil7_f32: halo exchange");
+      LHPC_HIP_TRY(hipEventRecord(c->ev_in, s));  // u complete on the caller's stream
+      LHPC_HIP_TRY(hipStreamWaitEvent(c->s_comm, c->ev_in, 0));
+      LHPC_NCCL_TRY(ncclGroupStart());
+      if (lo) {
+        LHPC_NCCL_TRY(ncclSend(plane(0), static_cast<size_t>(P), ncclFloat32, c->rank - 1, c->comm, c->s_comm));
+        LHPC_NCCL_TRY(ncclRecv(plane(-1), static_cast<size_t>(P), ncclFloat32, c->rank - 1, c->comm, c->s_comm));
+      }
+      if (hi) {
+        LHPC_NCCL_TRY(ncclSend(plane(nzl - 1), static_cast<size_t>(P), ncclFloat32, c->rank + 1, c->comm, c->s_comm));
+        LHPC_NCCL_TRY(ncclRecv(plane(nzl), static_cast<size_t>(P), ncclFloat32, c->rank + 1, c->comm, c->s_comm));
+      }
+      LHPC_NCCL_TRY(ncclGroupEnd());
+      LHPC_HIP_TRY(hipEventRecord(c->ev_halo, c->s_comm));
     }
-    LHPC_NCCL_TRY(ncclGroupEnd());
-    LHPC_HIP_TRY(hipEventRecord(c->ev_halo, c->s_comm));
-  }
-  // interior planes need no halo: they run while the planes travel
-  int st = LHPC_OK;
-  if (nzl > 2) st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, 1, nzl - 1, stream);
-  if (st == LHPC_OK && halo) {
-    if (w) {  // the neighbours' planes landed (DONE), stale L2 lines dropped
-      hipLaunchKernelGGL(k_p2p_wait_acquire, dim3(kP2pAcqBlocks), dim3(64), 0, s, c->flags, c->nranks,
-                         c->epoch * 64u + 1u, c->nranks, c->rank, c->h_status, mask);
-      st = static_cast<int>(hipGetLastError());
+    // interior planes need no halo: they run while the planes travel
+    int st = LHPC_OK;
+    if (nzl > 2) st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, 1, nzl - 1, stream);
+    if (st == LHPC_OK && halo) {
+      if (w) {  // the neighbours' planes landed (DONE), stale L2 lines dropped
+        hipLaunchKernelGGL(k_p2p_wait_acquire, dim3(kP2pAcqBlocks), dim3(64), 0, s, c->flags, c->nranks,
+                           c->epoch * 64u + 1u, c->nranks, c->rank, c->h_status, mask);
+        st = static_cast<int>(hipGetLastError());
+      }
+      // RCCL: the received planes; P2P: this rank's own puts, which read u's
+      // boundary planes, end before the caller's next step writes them
+      if (st == LHPC_OK) st = static_cast<int>(hipStreamWaitEvent(s, c->ev_halo, 0));
     }
-    // RCCL: the received planes; P2P: this rank's own puts, which read u's
-    // boundary planes, end before the caller's next step writes them
-    if (st == LHPC_OK) st = static_cast<int>(hipStreamWaitEvent(s, c->ev_halo, 0));
-  }
-  if (st == LHPC_OK) st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, 0, 1, stream);
-  if (st == LHPC_OK && nzl > 1)
-    st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, nzl - 1, nzl, stream);
-  return st;
+    if (st == LHPC_OK) st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, 0, 1, stream);
+    if (st == LHPC_OK && nzl > 1)
+      st = lhpc_stencil7_f32_planes(u, out, nzl, ny, nx, ghost, c0, c1, nzl - 1, nzl, stream);
+    return st;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_dist_stencil7_f32(lhpc_dist_comm *c, float *u, float *out, int64_t nzl, int64_t ny,
                                       int64_t nx, int64_t ghost, float c0, float c1, void *stream) {
-  return lhpc_dist_stencil7_f32_x(c, u, out, nzl, ny, nx, ghost, c0, c1, LHPC_DIST_EXCHANGE_AUTO, stream);
+  try {
+    return lhpc_dist_stencil7_f32_x(c, u, out, nzl, ny, nx, ghost, c0, c1, LHPC_DIST_EXCHANGE_AUTO, stream);
+  } LHPC_ABI_CATCH
 }

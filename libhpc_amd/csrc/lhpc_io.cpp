@@ -25,6 +25,7 @@
 #include <string>
 
 #include "../../include/lhpc.h"
+#include "lhpc_abi.hpp"
 
 namespace {
 
@@ -173,125 +174,135 @@ inline bool parse_f64(const char *&p, const char *e, double &v) {
 
 extern "C" int lhpc_csr_save(const char *path, int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz,
                              const void *row_ptr, int row_ptr_bits, const int32_t *col_idx, const void *val) {
-  if (!path || n_rows < 0 || n_cols < 0 || nnz < 0 || !row_ptr || (row_ptr_bits != 32 && row_ptr_bits != 64) ||
-      (nnz > 0 && (!col_idx || !val)) || (dtype != LHPC_F32 && dtype != LHPC_F64))
-    return LHPC_ERR_INVALID_ARG;
-  LcsrHeader h{};
-  std::memcpy(h.magic, kMagic, 8);
-  h.version = 1;
-  h.dtype = static_cast<uint32_t>(dtype);
-  h.n_rows = n_rows;
-  h.n_cols = n_cols;
-  h.nnz = nnz;
-  h.row_ptr_bits = static_cast<uint32_t>(row_ptr_bits);
-  h.index_bits = 32;
-  File f;
-  f.f = std::fopen(path, "wb");
-  if (!f.f) return LHPC_ERR_INVALID_ARG;
-  const int64_t rpb = (n_rows + 1) * (row_ptr_bits / 8), vb = dtype == LHPC_F32 ? 4 : 8;
-  const int64_t o_rp = 64, o_col = align64(o_rp + rpb), o_val = align64(o_col + nnz * 4);
-  if (!write_all(f.f, &h, 64) || !write_all(f.f, row_ptr, static_cast<size_t>(rpb)) || !pad_to(f.f, o_col) ||
-      !write_all(f.f, col_idx, static_cast<size_t>(nnz * 4)) || !pad_to(f.f, o_val) ||
-      !write_all(f.f, val, static_cast<size_t>(nnz * vb)))
-    return LHPC_ERR_INTERNAL;
-  if (std::fflush(f.f) != 0) return LHPC_ERR_INTERNAL;
-  return LHPC_OK;
+  try {
+    if (!path || n_rows < 0 || n_cols < 0 || nnz < 0 || !row_ptr || (row_ptr_bits != 32 && row_ptr_bits != 64) ||
+        (nnz > 0 && (!col_idx || !val)) || (dtype != LHPC_F32 && dtype != LHPC_F64))
+      return LHPC_ERR_INVALID_ARG;
+    LcsrHeader h{};
+    std::memcpy(h.magic, kMagic, 8);
+    h.version = 1;
+    h.dtype = static_cast<uint32_t>(dtype);
+    h.n_rows = n_rows;
+    h.n_cols = n_cols;
+    h.nnz = nnz;
+    h.row_ptr_bits = static_cast<uint32_t>(row_ptr_bits);
+    h.index_bits = 32;
+    File f;
+    f.f = std::fopen(path, "wb");
+    if (!f.f) return LHPC_ERR_INVALID_ARG;
+    const int64_t rpb = (n_rows + 1) * (row_ptr_bits / 8), vb = dtype == LHPC_F32 ? 4 : 8;
+    const int64_t o_rp = 64, o_col = align64(o_rp + rpb), o_val = align64(o_col + nnz * 4);
+    if (!write_all(f.f, &h, 64) || !write_all(f.f, row_ptr, static_cast<size_t>(rpb)) || !pad_to(f.f, o_col) ||
+        !write_all(f.f, col_idx, static_cast<size_t>(nnz * 4)) || !pad_to(f.f, o_val) ||
+        !write_all(f.f, val, static_cast<size_t>(nnz * vb)))
+      return LHPC_ERR_INTERNAL;
+    if (std::fflush(f.f) != 0) return LHPC_ERR_INTERNAL;
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_csr_load_header(const char *path, int *dtype, int64_t *n_rows, int64_t *n_cols, int64_t *nnz,
                                     int *row_ptr_bits) {
-  if (!path) return LHPC_ERR_INVALID_ARG;
-  File f;
-  f.f = std::fopen(path, "rb");
-  if (!f.f) return LHPC_ERR_INVALID_ARG;
-  LcsrHeader h{};
-  if (std::fread(&h, 1, 64, f.f) != 64 || std::memcmp(h.magic, kMagic, 8) != 0 || h.version != 1 ||
-      (h.dtype != LHPC_F32 && h.dtype != LHPC_F64) || (h.row_ptr_bits != 32 && h.row_ptr_bits != 64) ||
-      h.index_bits != 32 || h.n_rows < 0 || h.n_cols < 0 || h.nnz < 0)
-    return LHPC_ERR_BAD_CSR;
-  if (dtype) *dtype = static_cast<int>(h.dtype);
-  if (n_rows) *n_rows = h.n_rows;
-  if (n_cols) *n_cols = h.n_cols;
-  if (nnz) *nnz = h.nnz;
-  if (row_ptr_bits) *row_ptr_bits = static_cast<int>(h.row_ptr_bits);
-  return LHPC_OK;
+  try {
+    if (!path) return LHPC_ERR_INVALID_ARG;
+    File f;
+    f.f = std::fopen(path, "rb");
+    if (!f.f) return LHPC_ERR_INVALID_ARG;
+    LcsrHeader h{};
+    if (std::fread(&h, 1, 64, f.f) != 64 || std::memcmp(h.magic, kMagic, 8) != 0 || h.version != 1 ||
+        (h.dtype != LHPC_F32 && h.dtype != LHPC_F64) || (h.row_ptr_bits != 32 && h.row_ptr_bits != 64) ||
+        h.index_bits != 32 || h.n_rows < 0 || h.n_cols < 0 || h.nnz < 0)
+      return LHPC_ERR_BAD_CSR;
+    if (dtype) *dtype = static_cast<int>(h.dtype);
+    if (n_rows) *n_rows = h.n_rows;
+    if (n_cols) *n_cols = h.n_cols;
+    if (nnz) *nnz = h.nnz;
+    if (row_ptr_bits) *row_ptr_bits = static_cast<int>(h.row_ptr_bits);
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_csr_load(const char *path, void *row_ptr, int32_t *col_idx, void *val) {
-  int dtype = 0, rpbits = 0;
-  int64_t n_rows = 0, n_cols = 0, nnz = 0;
-  if (int st = lhpc_csr_load_header(path, &dtype, &n_rows, &n_cols, &nnz, &rpbits)) return st;
-  if (!row_ptr || (nnz > 0 && (!col_idx || !val))) return LHPC_ERR_INVALID_ARG;
-  Map m;
-  if (!m.open(path)) return LHPC_ERR_INVALID_ARG;
-  const int64_t rpb = (n_rows + 1) * (rpbits / 8), vb = dtype == LHPC_F32 ? 4 : 8;
-  const int64_t o_rp = 64, o_col = align64(o_rp + rpb), o_val = align64(o_col + nnz * 4);
-  if (static_cast<int64_t>(m.n) < o_val + nnz * vb) return LHPC_ERR_BAD_CSR;  // truncated
-  std::memcpy(row_ptr, m.p + o_rp, static_cast<size_t>(rpb));
-  if (nnz > 0) {
-    std::memcpy(col_idx, m.p + o_col, static_cast<size_t>(nnz * 4));
-    std::memcpy(val, m.p + o_val, static_cast<size_t>(nnz * vb));
-  }
-  return LHPC_OK;
+  try {
+    int dtype = 0, rpbits = 0;
+    int64_t n_rows = 0, n_cols = 0, nnz = 0;
+    if (int st = lhpc_csr_load_header(path, &dtype, &n_rows, &n_cols, &nnz, &rpbits)) return st;
+    if (!row_ptr || (nnz > 0 && (!col_idx || !val))) return LHPC_ERR_INVALID_ARG;
+    Map m;
+    if (!m.open(path)) return LHPC_ERR_INVALID_ARG;
+    const int64_t rpb = (n_rows + 1) * (rpbits / 8), vb = dtype == LHPC_F32 ? 4 : 8;
+    const int64_t o_rp = 64, o_col = align64(o_rp + rpb), o_val = align64(o_col + nnz * 4);
+    if (static_cast<int64_t>(m.n) < o_val + nnz * vb) return LHPC_ERR_BAD_CSR;  // truncated
+    std::memcpy(row_ptr, m.p + o_rp, static_cast<size_t>(rpb));
+    if (nnz > 0) {
+      std::memcpy(col_idx, m.p + o_col, static_cast<size_t>(nnz * 4));
+      std::memcpy(val, m.p + o_val, static_cast<size_t>(nnz * vb));
+    }
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_mm_read_header(const char *path, int64_t *n_rows, int64_t *n_cols, int64_t *nnz_max,
                                    int *symmetry, int *field) {
-  if (!path) return LHPC_ERR_INVALID_ARG;
-  Map m;
-  if (!m.open(path) || !m.p) return LHPC_ERR_INVALID_ARG;
-  MmInfo info{};
-  if (int st = mm_parse_header(m, info)) return st;
-  if (n_rows) *n_rows = info.n_rows;
-  if (n_cols) *n_cols = info.n_cols;
-  // symmetric / skew files store one triangle: off-diagonal entries expand to two
-  if (nnz_max) *nnz_max = info.sym == MM_GENERAL ? info.entries : 2 * info.entries;
-  if (symmetry) *symmetry = static_cast<int>(info.sym);
-  if (field) *field = static_cast<int>(info.field);
-  return LHPC_OK;
+  try {
+    if (!path) return LHPC_ERR_INVALID_ARG;
+    Map m;
+    if (!m.open(path) || !m.p) return LHPC_ERR_INVALID_ARG;
+    MmInfo info{};
+    if (int st = mm_parse_header(m, info)) return st;
+    if (n_rows) *n_rows = info.n_rows;
+    if (n_cols) *n_cols = info.n_cols;
+    // symmetric / skew files store one triangle: off-diagonal entries expand to two
+    if (nnz_max) *nnz_max = info.sym == MM_GENERAL ? info.entries : 2 * info.entries;
+    if (symmetry) *symmetry = static_cast<int>(info.sym);
+    if (field) *field = static_cast<int>(info.field);
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_mm_read_coo(const char *path, int32_t *rows, int32_t *cols, double *vals, int64_t *count) {
-  if (!path || !count) return LHPC_ERR_INVALID_ARG;
-  Map m;
-  if (!m.open(path) || !m.p) return LHPC_ERR_INVALID_ARG;
-  MmInfo info{};
-  if (int st = mm_parse_header(m, info)) return st;
-  if (info.n_rows > INT32_MAX || info.n_cols > INT32_MAX) return LHPC_ERR_UNSUPPORTED;
-  const char *p = m.p + info.data_off, *e = m.p + m.n;
-  int64_t k = 0;
-  for (int64_t i = 0; i < info.entries; ++i) {
-    p = skip_ws(p, e);
-    while (p < e && *p == '%') {  // stray comment lines
-      while (p < e && *p != '\n') ++p;
+  try {
+    if (!path || !count) return LHPC_ERR_INVALID_ARG;
+    Map m;
+    if (!m.open(path) || !m.p) return LHPC_ERR_INVALID_ARG;
+    MmInfo info{};
+    if (int st = mm_parse_header(m, info)) return st;
+    if (info.n_rows > INT32_MAX || info.n_cols > INT32_MAX) return LHPC_ERR_UNSUPPORTED;
+    const char *p = m.p + info.data_off, *e = m.p + m.n;
+    int64_t k = 0;
+    for (int64_t i = 0; i < info.entries; ++i) {
       p = skip_ws(p, e);
-    }
-    int64_t r, c;
-    double v = 1.0;
-    if (!parse_i64(p, e, r) || !parse_i64(p, e, c)) return LHPC_ERR_INVALID_ARG;
-    if (info.field == MM_INTEGER) {
-      int64_t iv;
-      if (!parse_i64(p, e, iv)) return LHPC_ERR_INVALID_ARG;
-      v = static_cast<double>(iv);
-    } else if (info.field == MM_REAL) {
-      if (!parse_f64(p, e, v)) return LHPC_ERR_INVALID_ARG;
-    }
-    if (r < 1 || r > info.n_rows || c < 1 || c > info.n_cols) return LHPC_ERR_INVALID_ARG;
-    if (rows) {
-      rows[k] = static_cast<int32_t>(r - 1);
-      cols[k] = static_cast<int32_t>(c - 1);
-      vals[k] = v;
-    }
-    ++k;
-    if (info.sym != MM_GENERAL && r != c) {
+      while (p < e && *p == '%') {  // stray comment lines
+        while (p < e && *p != '\n') ++p;
+        p = skip_ws(p, e);
+      }
+      int64_t r, c;
+      double v = 1.0;
+      if (!parse_i64(p, e, r) || !parse_i64(p, e, c)) return LHPC_ERR_INVALID_ARG;
+      if (info.field == MM_INTEGER) {
+        int64_t iv;
+        if (!parse_i64(p, e, iv)) return LHPC_ERR_INVALID_ARG;
+        v = static_cast<double>(iv);
+      } else if (info.field == MM_REAL) {
+        if (!parse_f64(p, e, v)) return LHPC_ERR_INVALID_ARG;
+      }
+      if (r < 1 || r > info.n_rows || c < 1 || c > info.n_cols) return LHPC_ERR_INVALID_ARG;
       if (rows) {
-        rows[k] = static_cast<int32_t>(c - 1);
-        cols[k] = static_cast<int32_t>(r - 1);
-        vals[k] = info.sym == MM_SKEW ? -v : v;
+        rows[k] = static_cast<int32_t>(r - 1);
+        cols[k] = static_cast<int32_t>(c - 1);
+        vals[k] = v;
       }
       ++k;
+      if (info.sym != MM_GENERAL && r != c) {
+        if (rows) {
+          rows[k] = static_cast<int32_t>(c - 1);
+          cols[k] = static_cast<int32_t>(r - 1);
+          vals[k] = info.sym == MM_SKEW ? -v : v;
+        }
+        ++k;
+      }
     }
-  }
-  *count = k;
-  return LHPC_OK;
+    *count = k;
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }

@@ -560,40 +560,44 @@ int multi_home(lhpc_spmv_plan *p, const void *x, void *y, int on_device, hipStre
 using namespace lhpc;
 
 extern "C" int lhpc_spmv_multi(lhpc_spmv_plan *p, const void *const *x, void *const *y, void *const *streams) {
-  if (!p || !p->multi || !x || !y) return LHPC_ERR_INVALID_ARG;
-  lhpc_multi *m = p->multi;
-  const int D = m->D;
-  std::vector<const void *> xs(static_cast<size_t>(D));
-  std::vector<void *> ys(static_cast<size_t>(D));
-  std::vector<hipStream_t> ss(static_cast<size_t>(D));
-  for (int d = 0; d < D; ++d) {
-    if ((m->n_cols > 0 && !x[d]) || (m->n_rows > 0 && !y[d]) || (x[d] == y[d] && m->n_rows > 0))
-      return LHPC_ERR_INVALID_ARG;
-    for (int e = 0; e < d; ++e)
-      if (y[e] == y[d] && m->n_rows > 0) return LHPC_ERR_INVALID_ARG;  // one y replica per device
-    xs[d] = x[d];
-    ys[d] = y[d];
-    ss[d] = streams ? static_cast<hipStream_t>(streams[d]) : m->dev[d].s;
-  }
-  RocTxRange rx("lhpc_spmv_multi");
-  const int st = multi_chunks(m, xs.data(), ys.data(), ss.data(), true, false);
-  (void)hipSetDevice(m->dev[0].device);
-  return st;
+  try {
+    if (!p || !p->multi || !x || !y) return LHPC_ERR_INVALID_ARG;
+    lhpc_multi *m = p->multi;
+    const int D = m->D;
+    std::vector<const void *> xs(static_cast<size_t>(D));
+    std::vector<void *> ys(static_cast<size_t>(D));
+    std::vector<hipStream_t> ss(static_cast<size_t>(D));
+    for (int d = 0; d < D; ++d) {
+      if ((m->n_cols > 0 && !x[d]) || (m->n_rows > 0 && !y[d]) || (x[d] == y[d] && m->n_rows > 0))
+        return LHPC_ERR_INVALID_ARG;
+      for (int e = 0; e < d; ++e)
+        if (y[e] == y[d] && m->n_rows > 0) return LHPC_ERR_INVALID_ARG;  // one y replica per device
+      xs[d] = x[d];
+      ys[d] = y[d];
+      ss[d] = streams ? static_cast<hipStream_t>(streams[d]) : m->dev[d].s;
+    }
+    RocTxRange rx("lhpc_spmv_multi");
+    const int st = multi_chunks(m, xs.data(), ys.data(), ss.data(), true, false);
+    (void)hipSetDevice(m->dev[0].device);
+    return st;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_spmv_plan_multi_info(const lhpc_spmv_plan *p, int *n_devices, int *chunks, int *exchange,
                                          int *device_ids, int64_t *cuts) {
-  if (!p) return LHPC_ERR_INVALID_ARG;
-  const lhpc_multi *m = p->multi;
-  const int D = m ? m->D : 1, K = m ? m->K : 1;
-  if (n_devices) *n_devices = D;
-  if (chunks) *chunks = K;
-  if (exchange) *exchange = m ? m->exchange : LHPC_DIST_EXCHANGE_NONE;
-  if (device_ids)
-    for (int d = 0; d < D; ++d) device_ids[d] = m ? m->dev[d].device : p->device;
-  if (cuts) {
-    if (m) std::copy(m->cuts.begin(), m->cuts.end(), cuts);
-    else cuts[0] = 0, cuts[1] = p->n_rows;
-  }
-  return LHPC_OK;
+  try {
+    if (!p) return LHPC_ERR_INVALID_ARG;
+    const lhpc_multi *m = p->multi;
+    const int D = m ? m->D : 1, K = m ? m->K : 1;
+    if (n_devices) *n_devices = D;
+    if (chunks) *chunks = K;
+    if (exchange) *exchange = m ? m->exchange : LHPC_DIST_EXCHANGE_NONE;
+    if (device_ids)
+      for (int d = 0; d < D; ++d) device_ids[d] = m ? m->dev[d].device : p->device;
+    if (cuts) {
+      if (m) std::copy(m->cuts.begin(), m->cuts.end(), cuts);
+      else cuts[0] = 0, cuts[1] = p->n_rows;
+    }
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }

@@ -28,18 +28,23 @@ extern "C" const char *lhpc_strerror(int status) {
   }
 }
 
-extern "C" int lhpc_abi_version(void) { return LHPC_ABI_VERSION; }
+extern "C" int lhpc_abi_version(void) {
+  try { return LHPC_ABI_VERSION;
+  } LHPC_ABI_CATCH
+}
 
 extern "C" int lhpc_device_count(void) {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
-  int good = 0;
-  for (int d = 0; d < n; ++d) {
-    hipDeviceProp_t p;
-    if (hipGetDeviceProperties(&p, d) == hipSuccess && std::strncmp(p.gcnArchName, "gfx950", 6) == 0)
-      ++good;
-  }
-  return good;
+  try {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int good = 0;
+    for (int d = 0; d < n; ++d) {
+      hipDeviceProp_t p;
+      if (hipGetDeviceProperties(&p, d) == hipSuccess && std::strncmp(p.gcnArchName, "gfx950", 6) == 0)
+        ++good;
+    }
+    return good;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" void lhpc_options_init(lhpc_options *o) {
@@ -166,23 +171,27 @@ lhpc_options resolve_options(const lhpc_options *in) {
 // Hands the current device's cached scratch back to the driver (the pool
 // keeps freed scratch between calls: GBs after a 500M-key sort).
 extern "C" int lhpc_scratch_trim(int device) {
-  hipMemPool_t pool;
-  LHPC_HIP_TRY(lhpc::scratch_pool(device, &pool));
-  LHPC_HIP_TRY(hipDeviceSynchronize());
-  LHPC_HIP_TRY(hipMemPoolTrimTo(pool, 0));
-  return LHPC_OK;
+  try {
+    hipMemPool_t pool;
+    LHPC_HIP_TRY(lhpc::scratch_pool(device, &pool));
+    LHPC_HIP_TRY(hipDeviceSynchronize());
+    LHPC_HIP_TRY(hipMemPoolTrimTo(pool, 0));
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 // Test support: leave `bytes` of the current device's scratch pool filled
 // with `value`, so the next scratch allocations on `stream` come back dirty
 // (tests/test_gpu_sort.py::test_coo_to_csr_poisoned_pool).
 extern "C" int lhpc_scratch_poison(int64_t bytes, int value, void *stream) {
-  if (bytes < 0) return LHPC_ERR_INVALID_ARG;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  void *p = nullptr;
-  LHPC_HIP_TRY(lhpc::scratch_alloc(&p, static_cast<size_t>(bytes), s));
-  LHPC_HIP_TRY(hipMemsetAsync(p, value, static_cast<size_t>(bytes), s));
-  LHPC_HIP_TRY(hipFreeAsync(p, s));
-  LHPC_HIP_TRY(hipStreamSynchronize(s));
-  return LHPC_OK;
+  try {
+    if (bytes < 0) return LHPC_ERR_INVALID_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    void *p = nullptr;
+    LHPC_HIP_TRY(lhpc::scratch_alloc(&p, static_cast<size_t>(bytes), s));
+    LHPC_HIP_TRY(hipMemsetAsync(p, value, static_cast<size_t>(bytes), s));
+    LHPC_HIP_TRY(hipFreeAsync(p, s));
+    LHPC_HIP_TRY(hipStreamSynchronize(s));
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }

@@ -206,99 +206,109 @@ int dtype_ok(int dtype) { return dtype == LHPC_F32 || dtype == LHPC_F64; }
 }  // namespace
 
 extern "C" int lhpc_vec_dot(int dtype, int64_t n, const void *a, const void *b, double *out, void *stream) {
-  if (!dtype_ok(dtype) || n < 0 || !out || (n > 0 && (!a || !b))) return LHPC_ERR_INVALID_ARG;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  Scratch part;
-  part.s = s;
-  LHPC_HIP_TRY(scratch_alloc(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
-  if (dtype == LHPC_F32)
-    return dot_dev(static_cast<const float *>(a), static_cast<const float *>(b), n, out, part.d, s);
-  return dot_dev(static_cast<const double *>(a), static_cast<const double *>(b), n, out, part.d, s);
+  try {
+    if (!dtype_ok(dtype) || n < 0 || !out || (n > 0 && (!a || !b))) return LHPC_ERR_INVALID_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    Scratch part;
+    part.s = s;
+    LHPC_HIP_TRY(scratch_alloc(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
+    if (dtype == LHPC_F32)
+      return dot_dev(static_cast<const float *>(a), static_cast<const float *>(b), n, out, part.d, s);
+    return dot_dev(static_cast<const double *>(a), static_cast<const double *>(b), n, out, part.d, s);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_cg_step_xr(int dtype, int64_t n, const double *alpha_num, const double *alpha_den, void *x,
                                const void *p, void *r, const void *q, double *rr_out, void *stream) {
-  if (!dtype_ok(dtype) || n < 0 || !alpha_num || !alpha_den || !rr_out || (n > 0 && (!x || !p || !r || !q)))
-    return LHPC_ERR_INVALID_ARG;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  Scratch part;
-  part.s = s;
-  LHPC_HIP_TRY(scratch_alloc(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
-  const int g = vec_grid(n);
-  if (dtype == LHPC_F32)
-    hipLaunchKernelGGL((k_cg_xr<float>), dim3(g), dim3(kVecThreads), 0, s, static_cast<float *>(x),
-                       static_cast<const float *>(p), static_cast<float *>(r), static_cast<const float *>(q), n,
-                       alpha_num, alpha_den, part.d);
-  else
-    hipLaunchKernelGGL((k_cg_xr<double>), dim3(g), dim3(kVecThreads), 0, s, static_cast<double *>(x),
-                       static_cast<const double *>(p), static_cast<double *>(r), static_cast<const double *>(q), n,
-                       alpha_num, alpha_den, part.d);
-  hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(kVecThreads), 0, s, part.d, g, rr_out);
-  return check_launch(s);
+  try {
+    if (!dtype_ok(dtype) || n < 0 || !alpha_num || !alpha_den || !rr_out || (n > 0 && (!x || !p || !r || !q)))
+      return LHPC_ERR_INVALID_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    Scratch part;
+    part.s = s;
+    LHPC_HIP_TRY(scratch_alloc(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
+    const int g = vec_grid(n);
+    if (dtype == LHPC_F32)
+      hipLaunchKernelGGL((k_cg_xr<float>), dim3(g), dim3(kVecThreads), 0, s, static_cast<float *>(x),
+                         static_cast<const float *>(p), static_cast<float *>(r), static_cast<const float *>(q), n,
+                         alpha_num, alpha_den, part.d);
+    else
+      hipLaunchKernelGGL((k_cg_xr<double>), dim3(g), dim3(kVecThreads), 0, s, static_cast<double *>(x),
+                         static_cast<const double *>(p), static_cast<double *>(r), static_cast<const double *>(q), n,
+                         alpha_num, alpha_den, part.d);
+    hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(kVecThreads), 0, s, part.d, g, rr_out);
+    return check_launch(s);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_cg_step_p(int dtype, int64_t n, const double *beta_num, const double *beta_den, const void *r,
                               void *p, void *stream) {
-  if (!dtype_ok(dtype) || n < 0 || !beta_num || !beta_den || (n > 0 && (!r || !p))) return LHPC_ERR_INVALID_ARG;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const int g = vec_grid(n);
-  if (dtype == LHPC_F32)
-    hipLaunchKernelGGL((k_cg_p<float>), dim3(g), dim3(kVecThreads), 0, s, static_cast<const float *>(r),
-                       static_cast<float *>(p), n, beta_num, beta_den);
-  else
-    hipLaunchKernelGGL((k_cg_p<double>), dim3(g), dim3(kVecThreads), 0, s, static_cast<const double *>(r),
-                       static_cast<double *>(p), n, beta_num, beta_den);
-  return check_launch(s);
+  try {
+    if (!dtype_ok(dtype) || n < 0 || !beta_num || !beta_den || (n > 0 && (!r || !p))) return LHPC_ERR_INVALID_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int g = vec_grid(n);
+    if (dtype == LHPC_F32)
+      hipLaunchKernelGGL((k_cg_p<float>), dim3(g), dim3(kVecThreads), 0, s, static_cast<const float *>(r),
+                         static_cast<float *>(p), n, beta_num, beta_den);
+    else
+      hipLaunchKernelGGL((k_cg_p<double>), dim3(g), dim3(kVecThreads), 0, s, static_cast<const double *>(r),
+                         static_cast<double *>(p), n, beta_num, beta_den);
+    return check_launch(s);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_cg_step_r(int dtype, int64_t n, const double *alpha_num, const double *alpha_den, void *r,
                               const void *q, double *rr_out, void *stream) {
-  if (!dtype_ok(dtype) || n < 0 || !alpha_num || !alpha_den || !rr_out || (n > 0 && (!r || !q)))
-    return LHPC_ERR_INVALID_ARG;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  Scratch part;
-  part.s = s;
-  LHPC_HIP_TRY(scratch_alloc(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
-  const int g = vec_grid(n);
-  if (dtype == LHPC_F32)
-    hipLaunchKernelGGL((k_cg_r<float>), dim3(g), dim3(kVecThreads), 0, s, static_cast<float *>(r),
-                       static_cast<const float *>(q), n, alpha_num, alpha_den, part.d);
-  else
-    hipLaunchKernelGGL((k_cg_r<double>), dim3(g), dim3(kVecThreads), 0, s, static_cast<double *>(r),
-                       static_cast<const double *>(q), n, alpha_num, alpha_den, part.d);
-  hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(kVecThreads), 0, s, part.d, g, rr_out);
-  return check_launch(s);
+  try {
+    if (!dtype_ok(dtype) || n < 0 || !alpha_num || !alpha_den || !rr_out || (n > 0 && (!r || !q)))
+      return LHPC_ERR_INVALID_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    Scratch part;
+    part.s = s;
+    LHPC_HIP_TRY(scratch_alloc(reinterpret_cast<void **>(&part.d), kDotBlocks * sizeof(double), s));
+    const int g = vec_grid(n);
+    if (dtype == LHPC_F32)
+      hipLaunchKernelGGL((k_cg_r<float>), dim3(g), dim3(kVecThreads), 0, s, static_cast<float *>(r),
+                         static_cast<const float *>(q), n, alpha_num, alpha_den, part.d);
+    else
+      hipLaunchKernelGGL((k_cg_r<double>), dim3(g), dim3(kVecThreads), 0, s, static_cast<double *>(r),
+                         static_cast<const double *>(q), n, alpha_num, alpha_den, part.d);
+    hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(kVecThreads), 0, s, part.d, g, rr_out);
+    return check_launch(s);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_cg_step_xp(int dtype, int64_t n, const double *alpha_num, const double *alpha_den,
                                const double *beta_num, const double *beta_den, void *x, void *p, const void *r,
                                void *stream) {
-  const bool up = beta_num != nullptr;
-  if (!dtype_ok(dtype) || n < 0 || !alpha_num || !alpha_den || (up && !beta_den) ||
-      (n > 0 && (!x || !p || (up && !r))))
-    return LHPC_ERR_INVALID_ARG;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const int g = vec_grid(n);
-  if (dtype == LHPC_F32) {
-    float *xf = static_cast<float *>(x), *pf = static_cast<float *>(p);
-    const float *rf = static_cast<const float *>(r);
-    if (up)
-      hipLaunchKernelGGL((k_cg_xp<float, true>), dim3(g), dim3(kVecThreads), 0, s, xf, pf, rf, n, alpha_num,
-                         alpha_den, beta_num, beta_den);
-    else
-      hipLaunchKernelGGL((k_cg_xp<float, false>), dim3(g), dim3(kVecThreads), 0, s, xf, pf, rf, n, alpha_num,
-                         alpha_den, beta_num, beta_den);
-  } else {
-    double *xd = static_cast<double *>(x), *pd = static_cast<double *>(p);
-    const double *rd = static_cast<const double *>(r);
-    if (up)
-      hipLaunchKernelGGL((k_cg_xp<double, true>), dim3(g), dim3(kVecThreads), 0, s, xd, pd, rd, n, alpha_num,
-                         alpha_den, beta_num, beta_den);
-    else
-      hipLaunchKernelGGL((k_cg_xp<double, false>), dim3(g), dim3(kVecThreads), 0, s, xd, pd, rd, n, alpha_num,
-                         alpha_den, beta_num, beta_den);
-  }
-  return check_launch(s);
+  try {
+    const bool up = beta_num != nullptr;
+    if (!dtype_ok(dtype) || n < 0 || !alpha_num || !alpha_den || (up && !beta_den) ||
+        (n > 0 && (!x || !p || (up && !r))))
+      return LHPC_ERR_INVALID_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int g = vec_grid(n);
+    if (dtype == LHPC_F32) {
+      float *xf = static_cast<float *>(x), *pf = static_cast<float *>(p);
+      const float *rf = static_cast<const float *>(r);
+      if (up)
+        hipLaunchKernelGGL((k_cg_xp<float, true>), dim3(g), dim3(kVecThreads), 0, s, xf, pf, rf, n, alpha_num,
+                           alpha_den, beta_num, beta_den);
+      else
+        hipLaunchKernelGGL((k_cg_xp<float, false>), dim3(g), dim3(kVecThreads), 0, s, xf, pf, rf, n, alpha_num,
+                           alpha_den, beta_num, beta_den);
+    } else {
+      double *xd = static_cast<double *>(x), *pd = static_cast<double *>(p);
+      const double *rd = static_cast<const double *>(r);
+      if (up)
+        hipLaunchKernelGGL((k_cg_xp<double, true>), dim3(g), dim3(kVecThreads), 0, s, xd, pd, rd, n, alpha_num,
+                           alpha_den, beta_num, beta_den);
+      else
+        hipLaunchKernelGGL((k_cg_xp<double, false>), dim3(g), dim3(kVecThreads), 0, s, xd, pd, rd, n, alpha_num,
+                           alpha_den, beta_num, beta_den);
+    }
+    return check_launch(s);
+  } LHPC_ABI_CATCH
 }
 
 namespace {
@@ -311,12 +321,20 @@ int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int
 // refused instead of racing on them.
 extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int max_iter,
                              int check_every, int *iters_out, double *resid_out, void *stream) {
-  if (!plan || !b || !x || max_iter < 0 || !(tol >= 0.0)) return LHPC_ERR_INVALID_ARG;
-  int idle = 0;
-  if (!plan->cg_busy.compare_exchange_strong(idle, 1)) return LHPC_ERR_BUSY;
-  const int st = cg_solve_owned(plan, b, x, tol, max_iter, check_every, iters_out, resid_out, stream);
-  plan->cg_busy.store(0);
-  return st;
+  try {
+    if (!plan || !b || !x || max_iter < 0 || !(tol >= 0.0)) return LHPC_ERR_INVALID_ARG;
+    int idle = 0;
+    if (!plan->cg_busy.compare_exchange_strong(idle, 1)) return LHPC_ERR_BUSY;
+    int st;
+    try {
+      st = cg_solve_owned(plan, b, x, tol, max_iter, check_every, iters_out, resid_out, stream);
+    } catch (...) {
+      plan->cg_busy.store(0);  // the plan's work is free again
+      throw;
+    }
+    plan->cg_busy.store(0);
+    return st;
+  } LHPC_ABI_CATCH
 }
 
 namespace {

@@ -635,59 +635,67 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
 // against 7.19 ms.)
 extern "C" int lhpc_radix_sort_u32(uint32_t *keys, int64_t n, int begin_bit, int end_bit, int on_device,
                                    void *stream) {
-  return sort_entry<uint32_t, false, 32>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
+  try {
+    return sort_entry<uint32_t, false, 32>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_radix_sort_pairs_u32(uint32_t *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit,
                                          int on_device, void *stream) {
-  return sort_entry<uint32_t, true, 32, false>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+  try {
+    return sort_entry<uint32_t, true, 32, false>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_radix_sort_pairs_u64(uint64_t *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit,
                                          int on_device, void *stream) {
-  return sort_entry<uint64_t, true, 32, false>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+  try {
+    return sort_entry<uint64_t, true, 32, false>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_coo_to_csr(int dtype, int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *rows,
                                const int32_t *cols, const void *vals, void *row_ptr, int row_ptr_bits,
                                int32_t *col_out, void *val_out, int64_t *nnz_out, int on_device, void *stream) {
-  if (n_rows < 0 || n_cols < 0 || nnz < 0 || !row_ptr || (row_ptr_bits != 32 && row_ptr_bits != 64) ||
-      (nnz > 0 && (!rows || !cols || !vals || !col_out || !val_out)) || (dtype != LHPC_F32 && dtype != LHPC_F64))
-    return LHPC_ERR_INVALID_ARG;
-  if (nnz >= (int64_t{1} << 32) || (row_ptr_bits == 32 && nnz >= (int64_t{1} << 31))) return LHPC_ERR_UNSUPPORTED;
-  RocTxRange rx("lhpc_coo_to_csr");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const size_t vb = dtype == LHPC_F32 ? 4 : 8;
-  auto run = [&](const int32_t *r, const int32_t *c, const void *v, void *rp, int32_t *co, void *vo,
-                 int64_t *un) -> int {
-    if (dtype == LHPC_F32)
-      return coo_to_csr_dev<float>(n_rows, n_cols, nnz, r, c, static_cast<const float *>(v), rp, row_ptr_bits, co,
-                                   static_cast<float *>(vo), un, s);
-    return coo_to_csr_dev<double>(n_rows, n_cols, nnz, r, c, static_cast<const double *>(v), rp, row_ptr_bits, co,
-                                  static_cast<double *>(vo), un, s);
-  };
-  if (on_device) return run(rows, cols, vals, row_ptr, col_out, val_out, nnz_out);
-  const size_t rpb = static_cast<size_t>(n_rows + 1) * (row_ptr_bits / 8);
-  HostStage dr, dc, dv, drp, dco, dvo;
-  LHPC_HIP_TRY(dr.alloc(static_cast<size_t>(nnz) * 4));
-  LHPC_HIP_TRY(dc.alloc(static_cast<size_t>(nnz) * 4));
-  LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(nnz) * vb));
-  LHPC_HIP_TRY(drp.alloc(rpb));
-  LHPC_HIP_TRY(dco.alloc(static_cast<size_t>(nnz) * 4));
-  LHPC_HIP_TRY(dvo.alloc(static_cast<size_t>(nnz) * vb));
-  if (nnz > 0) {
-    LHPC_HIP_TRY(hipMemcpy(dr.p, rows, static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice));
-    LHPC_HIP_TRY(hipMemcpy(dc.p, cols, static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice));
-    LHPC_HIP_TRY(hipMemcpy(dv.p, vals, static_cast<size_t>(nnz) * vb, hipMemcpyHostToDevice));
-  }
-  int64_t un = 0;
-  LHPC_TRY(run(static_cast<int32_t *>(dr.p), static_cast<int32_t *>(dc.p), dv.p, drp.p,
-               static_cast<int32_t *>(dco.p), dvo.p, &un));  // ends with a stream synchronize
-  LHPC_HIP_TRY(hipMemcpy(row_ptr, drp.p, rpb, hipMemcpyDeviceToHost));
-  if (un > 0) {
-    LHPC_HIP_TRY(hipMemcpy(col_out, dco.p, static_cast<size_t>(un) * 4, hipMemcpyDeviceToHost));
-    LHPC_HIP_TRY(hipMemcpy(val_out, dvo.p, static_cast<size_t>(un) * vb, hipMemcpyDeviceToHost));
-  }
-  if (nnz_out) *nnz_out = un;
-  return LHPC_OK;
+  try {
+    if (n_rows < 0 || n_cols < 0 || nnz < 0 || !row_ptr || (row_ptr_bits != 32 && row_ptr_bits != 64) ||
+        (nnz > 0 && (!rows || !cols || !vals || !col_out || !val_out)) || (dtype != LHPC_F32 && dtype != LHPC_F64))
+      return LHPC_ERR_INVALID_ARG;
+    if (nnz >= (int64_t{1} << 32) || (row_ptr_bits == 32 && nnz >= (int64_t{1} << 31))) return LHPC_ERR_UNSUPPORTED;
+    RocTxRange rx("lhpc_coo_to_csr");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t vb = dtype == LHPC_F32 ? 4 : 8;
+    auto run = [&](const int32_t *r, const int32_t *c, const void *v, void *rp, int32_t *co, void *vo,
+                   int64_t *un) -> int {
+      if (dtype == LHPC_F32)
+        return coo_to_csr_dev<float>(n_rows, n_cols, nnz, r, c, static_cast<const float *>(v), rp, row_ptr_bits, co,
+                                     static_cast<float *>(vo), un, s);
+      return coo_to_csr_dev<double>(n_rows, n_cols, nnz, r, c, static_cast<const double *>(v), rp, row_ptr_bits, co,
+                                    static_cast<double *>(vo), un, s);
+    };
+    if (on_device) return run(rows, cols, vals, row_ptr, col_out, val_out, nnz_out);
+    const size_t rpb = static_cast<size_t>(n_rows + 1) * (row_ptr_bits / 8);
+    HostStage dr, dc, dv, drp, dco, dvo;
+    LHPC_HIP_TRY(dr.alloc(static_cast<size_t>(nnz) * 4));
+    LHPC_HIP_TRY(dc.alloc(static_cast<size_t>(nnz) * 4));
+    LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(nnz) * vb));
+    LHPC_HIP_TRY(drp.alloc(rpb));
+    LHPC_HIP_TRY(dco.alloc(static_cast<size_t>(nnz) * 4));
+    LHPC_HIP_TRY(dvo.alloc(static_cast<size_t>(nnz) * vb));
+    if (nnz > 0) {
+      LHPC_HIP_TRY(hipMemcpy(dr.p, rows, static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice));
+      LHPC_HIP_TRY(hipMemcpy(dc.p, cols, static_cast<size_t>(nnz) * 4, hipMemcpyHostToDevice));
+      LHPC_HIP_TRY(hipMemcpy(dv.p, vals, static_cast<size_t>(nnz) * vb, hipMemcpyHostToDevice));
+    }
+    int64_t un = 0;
+    LHPC_TRY(run(static_cast<int32_t *>(dr.p), static_cast<int32_t *>(dc.p), dv.p, drp.p,
+                 static_cast<int32_t *>(dco.p), dvo.p, &un));  // ends with a stream synchronize
+    LHPC_HIP_TRY(hipMemcpy(row_ptr, drp.p, rpb, hipMemcpyDeviceToHost));
+    if (un > 0) {
+      LHPC_HIP_TRY(hipMemcpy(col_out, dco.p, static_cast<size_t>(un) * 4, hipMemcpyDeviceToHost));
+      LHPC_HIP_TRY(hipMemcpy(val_out, dvo.p, static_cast<size_t>(un) * vb, hipMemcpyDeviceToHost));
+    }
+    if (nnz_out) *nnz_out = un;
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }

@@ -708,9 +708,11 @@ extern "C" int lhpc_spmv_plan_create(lhpc_spmv_plan **out, int dtype, int64_t n_
                                      int row_ptr_bits, const int32_t *col_idx,
                                      const void *val, const int *device_ids,
                                      int n_devices, unsigned flags) {
-  RocTxRange rx("lhpc_spmv_plan_create");
-  return plan_create_impl(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
-                          device_ids, n_devices, flags, 0, nullptr, nullptr);
+  try {
+    RocTxRange rx("lhpc_spmv_plan_create");
+    return plan_create_impl(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
+                            device_ids, n_devices, flags, 0, nullptr, nullptr);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_spmv_plan_create_opts(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
@@ -719,21 +721,23 @@ extern "C" int lhpc_spmv_plan_create_opts(lhpc_spmv_plan **out, int dtype, int64
                                           const void *val, const int *device_ids, int n_devices,
                                           unsigned flags, int n_splits, const int64_t *split_rows,
                                           const lhpc_options *opts) {
-  if (!out || n_splits < 0 || (n_splits > 0 && !split_rows)) return LHPC_ERR_INVALID_ARG;
-  for (int i = 0; i < n_splits; ++i)
-    if (split_rows[i] <= 0 || split_rows[i] >= n_rows || (i > 0 && split_rows[i] <= split_rows[i - 1]))
-      return LHPC_ERR_INVALID_ARG;
-  RocTxRange rx("lhpc_spmv_plan_create");
-  const int st = plan_create_impl(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
-                                  device_ids, n_devices, flags, n_splits, split_rows, opts);
-  if (st != LHPC_OK || n_splits == 0) return st;
-  const lhpc_spmv_plan *p = *out;
-  if (p->kernel != LHPC_KERNEL_XTILE || p->xt_srow.size() != static_cast<size_t>(n_splits) + 2) {
-    lhpc_spmv_plan_destroy(*out);  // ranges exist only in the XTILE tile-stream layout
-    *out = nullptr;
-    return LHPC_ERR_UNSUPPORTED;
-  }
-  return LHPC_OK;
+  try {
+    if (!out || n_splits < 0 || (n_splits > 0 && !split_rows)) return LHPC_ERR_INVALID_ARG;
+    for (int i = 0; i < n_splits; ++i)
+      if (split_rows[i] <= 0 || split_rows[i] >= n_rows || (i > 0 && split_rows[i] <= split_rows[i - 1]))
+        return LHPC_ERR_INVALID_ARG;
+    RocTxRange rx("lhpc_spmv_plan_create");
+    const int st = plan_create_impl(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
+                                    device_ids, n_devices, flags, n_splits, split_rows, opts);
+    if (st != LHPC_OK || n_splits == 0) return st;
+    const lhpc_spmv_plan *p = *out;
+    if (p->kernel != LHPC_KERNEL_XTILE || p->xt_srow.size() != static_cast<size_t>(n_splits) + 2) {
+      lhpc_spmv_plan_destroy(*out);  // ranges exist only in the XTILE tile-stream layout
+      *out = nullptr;
+      return LHPC_ERR_UNSUPPORTED;
+    }
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_spmv_plan_create_split(lhpc_spmv_plan **out, int dtype, int64_t n_rows,
@@ -741,137 +745,151 @@ extern "C" int lhpc_spmv_plan_create_split(lhpc_spmv_plan **out, int dtype, int6
                                            int row_ptr_bits, const int32_t *col_idx,
                                            const void *val, const int *device_ids, int n_devices,
                                            unsigned flags, int n_splits, const int64_t *split_rows) {
-  if (n_splits < 1) return LHPC_ERR_INVALID_ARG;
-  return lhpc_spmv_plan_create_opts(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
-                                    device_ids, n_devices, flags, n_splits, split_rows, nullptr);
+  try {
+    if (n_splits < 1) return LHPC_ERR_INVALID_ARG;
+    return lhpc_spmv_plan_create_opts(out, dtype, n_rows, n_cols, nnz, row_ptr, row_ptr_bits, col_idx, val,
+                                      device_ids, n_devices, flags, n_splits, split_rows, nullptr);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_spmv_stage(const lhpc_spmv_plan *p, const void *x, void *stream) {
-  if (!p || (p->n_cols > 0 && !x)) return LHPC_ERR_INVALID_ARG;
-  if (p->xt_srow.empty()) return LHPC_ERR_UNSUPPORTED;
-  RocTxRange rx("lhpc_spmv_stage");
-  LHPC_HIP_TRY(hipSetDevice(p->device));
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  return xtile_stage(p, x, s);
+  try {
+    if (!p || (p->n_cols > 0 && !x)) return LHPC_ERR_INVALID_ARG;
+    if (p->xt_srow.empty()) return LHPC_ERR_UNSUPPORTED;
+    RocTxRange rx("lhpc_spmv_stage");
+    LHPC_HIP_TRY(hipSetDevice(p->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    return xtile_stage(p, x, s);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_spmv_range(const lhpc_spmv_plan *p, int k, void *y_range, void *stream) {
-  if (!p || p->xt_srow.empty() || k < 0 || k + 2 > static_cast<int>(p->xt_srow.size()))
-    return LHPC_ERR_INVALID_ARG;
-  if (p->xt_srow[k + 1] > p->xt_srow[k] && !y_range) return LHPC_ERR_INVALID_ARG;
-  RocTxRange rx("lhpc_spmv_range");
-  LHPC_HIP_TRY(hipSetDevice(p->device));
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  return xtile_range(p, k, y_range, s);
+  try {
+    if (!p || p->xt_srow.empty() || k < 0 || k + 2 > static_cast<int>(p->xt_srow.size()))
+      return LHPC_ERR_INVALID_ARG;
+    if (p->xt_srow[k + 1] > p->xt_srow[k] && !y_range) return LHPC_ERR_INVALID_ARG;
+    RocTxRange rx("lhpc_spmv_range");
+    LHPC_HIP_TRY(hipSetDevice(p->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    return xtile_range(p, k, y_range, s);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_spmv(lhpc_spmv_plan *p, const void *x, void *y, int on_device,
                          void *stream) {
-  if (!p || (p->n_cols > 0 && !x) || (p->n_rows > 0 && !y)) return LHPC_ERR_INVALID_ARG;
-  RocTxRange rx("lhpc_spmv");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (p->multi) return multi_home(p, x, y, on_device, s);
-  LHPC_HIP_TRY(hipSetDevice(p->device));
-  const size_t tsz = p->dtype == LHPC_F32 ? 4 : 8;
-  const void *dx = x;
-  void *dy = y;
-  if (!on_device) {
-    if (!p->d_xstage) {
-      LHPC_TRY(dmalloc(&p->d_xstage, static_cast<size_t>(p->n_cols) * tsz, p->bytes));
-      LHPC_TRY(dmalloc(&p->d_ystage, static_cast<size_t>(p->n_rows) * tsz, p->bytes));
+  try {
+    if (!p || (p->n_cols > 0 && !x) || (p->n_rows > 0 && !y)) return LHPC_ERR_INVALID_ARG;
+    RocTxRange rx("lhpc_spmv");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (p->multi) return multi_home(p, x, y, on_device, s);
+    LHPC_HIP_TRY(hipSetDevice(p->device));
+    const size_t tsz = p->dtype == LHPC_F32 ? 4 : 8;
+    const void *dx = x;
+    void *dy = y;
+    if (!on_device) {
+      if (!p->d_xstage) {
+        LHPC_TRY(dmalloc(&p->d_xstage, static_cast<size_t>(p->n_cols) * tsz, p->bytes));
+        LHPC_TRY(dmalloc(&p->d_ystage, static_cast<size_t>(p->n_rows) * tsz, p->bytes));
+      }
+      // host buffers: synchronous copies (see lhpc_sort.hip HostStage); the
+      // staging buffers are only touched by host-buffer calls, which end synced
+      LHPC_HIP_TRY(hipMemcpy(p->d_xstage, x, static_cast<size_t>(p->n_cols) * tsz, hipMemcpyHostToDevice));
+      dx = p->d_xstage;
+      dy = p->d_ystage;
     }
-    // host buffers: synchronous copies (see lhpc_sort.hip HostStage); the
-    // staging buffers are only touched by host-buffer calls, which end synced
-    LHPC_HIP_TRY(hipMemcpy(p->d_xstage, x, static_cast<size_t>(p->n_cols) * tsz, hipMemcpyHostToDevice));
-    dx = p->d_xstage;
-    dy = p->d_ystage;
-  }
-  const int st = launch(p, dx, dy, s);
-  if (st != LHPC_OK) return st;
-  if (!on_device) {
-    LHPC_HIP_TRY(hipStreamSynchronize(s));
-    LHPC_HIP_TRY(hipMemcpy(y, p->d_ystage, static_cast<size_t>(p->n_rows) * tsz, hipMemcpyDeviceToHost));
-  }
-  return LHPC_OK;
+    const int st = launch(p, dx, dy, s);
+    if (st != LHPC_OK) return st;
+    if (!on_device) {
+      LHPC_HIP_TRY(hipStreamSynchronize(s));
+      LHPC_HIP_TRY(hipMemcpy(y, p->d_ystage, static_cast<size_t>(p->n_rows) * tsz, hipMemcpyDeviceToHost));
+    }
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_vec_dot(int dtype, int64_t n, const void *a, const void *b, double *out, void *stream);
 
 extern "C" int lhpc_spmv_dot(lhpc_spmv_plan *p, const void *x, void *y, const void *w, double *dot_out,
                              void *stream) {
-  if (!p || !dot_out || (p->n_cols > 0 && !x) || (p->n_rows > 0 && (!y || !w))) return LHPC_ERR_INVALID_ARG;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  LHPC_HIP_TRY(hipSetDevice(p->device));
-  if ((p->kernel == LHPC_KERNEL_ADAPTIVE || p->kernel == LHPC_KERNEL_SELL) && p->n_blocks > 0) {
-    const int st = csr_launch_dot(p, x, y, w, dot_out, s);
-    if (st != LHPC_ERR_UNSUPPORTED) return st;
-  }
-  // other kernel families: SpMV, then a separate dot pass
-  LHPC_TRY(lhpc_spmv(p, x, y, 1, stream));
-  return lhpc_vec_dot(p->dtype, p->n_rows, w, y, dot_out, stream);
+  try {
+    if (!p || !dot_out || (p->n_cols > 0 && !x) || (p->n_rows > 0 && (!y || !w))) return LHPC_ERR_INVALID_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    LHPC_HIP_TRY(hipSetDevice(p->device));
+    if ((p->kernel == LHPC_KERNEL_ADAPTIVE || p->kernel == LHPC_KERNEL_SELL) && p->n_blocks > 0) {
+      const int st = csr_launch_dot(p, x, y, w, dot_out, s);
+      if (st != LHPC_ERR_UNSUPPORTED) return st;
+    }
+    // other kernel families: SpMV, then a separate dot pass
+    LHPC_TRY(lhpc_spmv(p, x, y, 1, stream));
+    return lhpc_vec_dot(p->dtype, p->n_rows, w, y, dot_out, stream);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_spmv_plan_info_get(const lhpc_spmv_plan *p, lhpc_spmv_plan_info *info) {
-  if (!p || !info) return LHPC_ERR_INVALID_ARG;
-  info->dtype = p->dtype;
-  info->kernel = p->kernel;
-  info->lanes_per_row = p->kernel == LHPC_KERNEL_ROWGROUP ? p->L : 0;
-  info->rows_per_group = p->kernel == LHPC_KERNEL_ROWGROUP ? p->R : 0;
-  info->n_rows = p->n_rows;
-  info->n_cols = p->n_cols;
-  info->nnz = p->nnz;
-  info->n_blocks = p->n_blocks;
-  info->n_long_rows = p->n_long;
-  info->device_bytes = p->bytes;
-  info->device = p->device;
-  info->launches = p->kernel == LHPC_KERNEL_XSLICE ? 2 : 1;
-  if (p->kernel == LHPC_KERNEL_XTILE) {
-    info->launches = p->xt_mall > 1 ? 2 * p->xt_mall + (p->xt_cont > 0 ? 1 : 0)
-                                    : (p->xt_pieces > 0 ? 1 : 0) + 1 + (p->xt_cont > 0 ? 1 : 0);
-    info->n_blocks = p->xt_C;
-    info->n_long_rows = p->xt_cont;
-  }
-  info->slices = p->S;
-  info->slice_width = p->xs_width;
-  if (p->kernel == LHPC_KERNEL_SELL) {  // 64-row slices, widest slice in nonzeros
-    info->slices = static_cast<int>((p->n_rows + kWave - 1) / kWave);
-    info->slice_width = p->sell_w;
-  }
-  if (!p->parts.empty()) {  // XTILE row parts: totals over the parts
-    info->launches = 0;
-    info->n_blocks = 0;
-    info->n_long_rows = 0;
-    for (const auto *q : p->parts) {
-      lhpc_spmv_plan_info qi{};
-      LHPC_TRY(lhpc_spmv_plan_info_get(q, &qi));
-      info->launches += qi.launches;
-      info->n_blocks += qi.n_blocks;
-      info->n_long_rows += qi.n_long_rows;
+  try {
+    if (!p || !info) return LHPC_ERR_INVALID_ARG;
+    info->dtype = p->dtype;
+    info->kernel = p->kernel;
+    info->lanes_per_row = p->kernel == LHPC_KERNEL_ROWGROUP ? p->L : 0;
+    info->rows_per_group = p->kernel == LHPC_KERNEL_ROWGROUP ? p->R : 0;
+    info->n_rows = p->n_rows;
+    info->n_cols = p->n_cols;
+    info->nnz = p->nnz;
+    info->n_blocks = p->n_blocks;
+    info->n_long_rows = p->n_long;
+    info->device_bytes = p->bytes;
+    info->device = p->device;
+    info->launches = p->kernel == LHPC_KERNEL_XSLICE ? 2 : 1;
+    if (p->kernel == LHPC_KERNEL_XTILE) {
+      info->launches = p->xt_mall > 1 ? 2 * p->xt_mall + (p->xt_cont > 0 ? 1 : 0)
+                                      : (p->xt_pieces > 0 ? 1 : 0) + 1 + (p->xt_cont > 0 ? 1 : 0);
+      info->n_blocks = p->xt_C;
+      info->n_long_rows = p->xt_cont;
     }
-  }
-  return LHPC_OK;
+    info->slices = p->S;
+    info->slice_width = p->xs_width;
+    if (p->kernel == LHPC_KERNEL_SELL) {  // 64-row slices, widest slice in nonzeros
+      info->slices = static_cast<int>((p->n_rows + kWave - 1) / kWave);
+      info->slice_width = p->sell_w;
+    }
+    if (!p->parts.empty()) {  // XTILE row parts: totals over the parts
+      info->launches = 0;
+      info->n_blocks = 0;
+      info->n_long_rows = 0;
+      for (const auto *q : p->parts) {
+        lhpc_spmv_plan_info qi{};
+        LHPC_TRY(lhpc_spmv_plan_info_get(q, &qi));
+        info->launches += qi.launches;
+        info->n_blocks += qi.n_blocks;
+        info->n_long_rows += qi.n_long_rows;
+      }
+    }
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
-  if (!p) return LHPC_OK;
-  if (p->multi) multi_free(p);
-  for (auto *q : p->parts) lhpc_spmv_plan_destroy(q);
-  (void)hipSetDevice(p->device);
-  for (void *q : {p->d_row_ptr, static_cast<void *>(p->d_col), p->d_val, static_cast<void *>(p->d_blocks),
-                  p->d_xstage, p->d_ystage, p->d_lens, static_cast<void *>(p->d_cbase), p->d_partial,
-                  static_cast<void *>(p->d_dpart), static_cast<void *>(p->d_cdesc), static_cast<void *>(p->d_cr),
-                  static_cast<void *>(p->d_seghi), static_cast<void *>(p->d_seg), static_cast<void *>(p->d_pieces), static_cast<void *>(p->d_cont),
-                  static_cast<void *>(p->d_col16), static_cast<void *>(p->d_perm), p->d_xg,
-                  static_cast<void *>(p->d_pieces_cp),
-                  static_cast<void *>(p->d_carry)})
-    if (q) (void)hipFree(q);
-  if (p->h_scalars) (void)hipHostFree(p->h_scalars);
-  for (hipGraphExec_t g : p->cg_graph)
-    if (g) (void)hipGraphExecDestroy(g);
-  if (p->cg_vecs) (void)hipFree(p->cg_vecs);
-  if (p->cg_scal) (void)hipFree(p->cg_scal);
-  delete p;
-  return LHPC_OK;
+  try {
+    if (!p) return LHPC_OK;
+    if (p->multi) multi_free(p);
+    for (auto *q : p->parts) lhpc_spmv_plan_destroy(q);
+    (void)hipSetDevice(p->device);
+    for (void *q : {p->d_row_ptr, static_cast<void *>(p->d_col), p->d_val, static_cast<void *>(p->d_blocks),
+                    p->d_xstage, p->d_ystage, p->d_lens, static_cast<void *>(p->d_cbase), p->d_partial,
+                    static_cast<void *>(p->d_dpart), static_cast<void *>(p->d_cdesc), static_cast<void *>(p->d_cr),
+                    static_cast<void *>(p->d_seghi), static_cast<void *>(p->d_seg), static_cast<void *>(p->d_pieces), static_cast<void *>(p->d_cont),
+                    static_cast<void *>(p->d_col16), static_cast<void *>(p->d_perm), p->d_xg,
+                    static_cast<void *>(p->d_pieces_cp),
+                    static_cast<void *>(p->d_carry)})
+      if (q) (void)hipFree(q);
+    if (p->h_scalars) (void)hipHostFree(p->h_scalars);
+    for (hipGraphExec_t g : p->cg_graph)
+      if (g) (void)hipGraphExecDestroy(g);
+    if (p->cg_vecs) (void)hipFree(p->cg_vecs);
+    if (p->cg_scal) (void)hipFree(p->cg_scal);
+    delete p;
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 
 // Test support: FNV-1a digests of an XTILE plan's device layout, in the
@@ -879,43 +897,45 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
 // table (lo/len, hi), gather pieces, cont — so a test can byte-compare the
 // layout built on the GPU from device input with the host build's.
 extern "C" int lhpc_spmv_plan_layout_digest(const lhpc_spmv_plan *p, uint64_t *out, int cap, int *n_out) {
-  if (!p || !out || !n_out || cap < 10) return LHPC_ERR_INVALID_ARG;
-  if (p->kernel != LHPC_KERNEL_XTILE || p->multi) return LHPC_ERR_UNSUPPORTED;
-  if (!p->parts.empty()) {  // row parts / column blocks: the parts' digests folded in order
-    for (int i = 0; i < 10; ++i) out[i] = 0xcbf29ce484222325ull;
-    for (size_t j = 0; j < p->parts.size(); ++j) {
-      uint64_t d[10];
-      int n = 0;
-      LHPC_TRY(lhpc_spmv_plan_layout_digest(p->parts[j], d, 10, &n));
-      const uint64_t where = static_cast<uint64_t>(p->part_row[j]) * 0x9E3779B97F4A7C15ull ^
-                             static_cast<uint64_t>(p->part_col[j]) ^ static_cast<uint64_t>(p->parts[j]->xt_acc) << 63;
-      for (int i = 0; i < 10; ++i) out[i] = (out[i] ^ d[i] ^ where) * 0x100000001b3ull;
+  try {
+    if (!p || !out || !n_out || cap < 10) return LHPC_ERR_INVALID_ARG;
+    if (p->kernel != LHPC_KERNEL_XTILE || p->multi) return LHPC_ERR_UNSUPPORTED;
+    if (!p->parts.empty()) {  // row parts / column blocks: the parts' digests folded in order
+      for (int i = 0; i < 10; ++i) out[i] = 0xcbf29ce484222325ull;
+      for (size_t j = 0; j < p->parts.size(); ++j) {
+        uint64_t d[10];
+        int n = 0;
+        LHPC_TRY(lhpc_spmv_plan_layout_digest(p->parts[j], d, 10, &n));
+        const uint64_t where = static_cast<uint64_t>(p->part_row[j]) * 0x9E3779B97F4A7C15ull ^
+                               static_cast<uint64_t>(p->part_col[j]) ^ static_cast<uint64_t>(p->parts[j]->xt_acc) << 63;
+        for (int i = 0; i < 10; ++i) out[i] = (out[i] ^ d[i] ^ where) * 0x100000001b3ull;
+      }
+      *n_out = 10;
+      return LHPC_OK;
+    }
+    LHPC_HIP_TRY(hipSetDevice(p->device));
+    const size_t tsz = p->dtype == LHPC_F32 ? 4 : 8;
+    const int64_t C = p->xt_C, S = p->S, H = (C + kXtSegHi - 1) / kXtSegHi;
+    const std::pair<const void *, size_t> arr[10] = {
+        {p->d_row_ptr, static_cast<size_t>(p->n_rows + 1) * 4},
+        {p->d_col16, static_cast<size_t>(p->xt_total) * 2},
+        {p->d_perm, static_cast<size_t>(p->xt_p == 3 ? p->xt_nrun : p->xt_total + 2) * 2},
+        {p->d_val, static_cast<size_t>(p->xt_nrun) * tsz},
+        {p->d_cdesc, static_cast<size_t>(8 * C + 8) * 4},
+        {p->d_cr, static_cast<size_t>(C + 1) * 4},
+        {p->d_seg, static_cast<size_t>(std::max<int64_t>(C, 1) * S) * 4},
+        {p->d_seghi, static_cast<size_t>(std::max<int64_t>(H, 1) * S) * 4},
+        {p->d_pieces, static_cast<size_t>(p->xt_pieces) * 12},
+        {p->d_cont, static_cast<size_t>(p->xt_cont) * 4}};
+    std::vector<unsigned char> h;
+    for (int i = 0; i < 10; ++i) {
+      h.resize(arr[i].second);
+      if (arr[i].second) LHPC_HIP_TRY(hipMemcpy(h.data(), arr[i].first, arr[i].second, hipMemcpyDeviceToHost));
+      uint64_t x = 0xcbf29ce484222325ull;
+      for (unsigned char b : h) x = (x ^ b) * 0x100000001b3ull;
+      out[i] = x ^ static_cast<uint64_t>(arr[i].second);
     }
     *n_out = 10;
     return LHPC_OK;
-  }
-  LHPC_HIP_TRY(hipSetDevice(p->device));
-  const size_t tsz = p->dtype == LHPC_F32 ? 4 : 8;
-  const int64_t C = p->xt_C, S = p->S, H = (C + kXtSegHi - 1) / kXtSegHi;
-  const std::pair<const void *, size_t> arr[10] = {
-      {p->d_row_ptr, static_cast<size_t>(p->n_rows + 1) * 4},
-      {p->d_col16, static_cast<size_t>(p->xt_total) * 2},
-      {p->d_perm, static_cast<size_t>(p->xt_p == 3 ? p->xt_nrun : p->xt_total + 2) * 2},
-      {p->d_val, static_cast<size_t>(p->xt_nrun) * tsz},
-      {p->d_cdesc, static_cast<size_t>(8 * C + 8) * 4},
-      {p->d_cr, static_cast<size_t>(C + 1) * 4},
-      {p->d_seg, static_cast<size_t>(std::max<int64_t>(C, 1) * S) * 4},
-      {p->d_seghi, static_cast<size_t>(std::max<int64_t>(H, 1) * S) * 4},
-      {p->d_pieces, static_cast<size_t>(p->xt_pieces) * 12},
-      {p->d_cont, static_cast<size_t>(p->xt_cont) * 4}};
-  std::vector<unsigned char> h;
-  for (int i = 0; i < 10; ++i) {
-    h.resize(arr[i].second);
-    if (arr[i].second) LHPC_HIP_TRY(hipMemcpy(h.data(), arr[i].first, arr[i].second, hipMemcpyDeviceToHost));
-    uint64_t x = 0xcbf29ce484222325ull;
-    for (unsigned char b : h) x = (x ^ b) * 0x100000001b3ull;
-    out[i] = x ^ static_cast<uint64_t>(arr[i].second);
-  }
-  *n_out = 10;
-  return LHPC_OK;
+  } LHPC_ABI_CATCH
 }

@@ -1328,16 +1328,20 @@ int xtile_build_device(lhpc_spmv_plan *p, RowPtrView rp_host, const int32_t *d_c
 #ifdef LHPC_XT_STAMPS
 // diagnostic build: copy the reduce's phase stamps (uint64 [blocks][10]) to host
 extern "C" int lhpc_probe_xtile_stamps(void *out, int64_t n) {
-  if (n > (1 << 22)) n = 1 << 22;
-  LHPC_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(lhpc::g_xt_stamps), static_cast<size_t>(n) * 8, 0,
-                                   hipMemcpyDeviceToHost));
-  return LHPC_OK;
+  try {
+    if (n > (1 << 22)) n = 1 << 22;
+    LHPC_HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(lhpc::g_xt_stamps), static_cast<size_t>(n) * 8, 0,
+                                     hipMemcpyDeviceToHost));
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 extern "C" int lhpc_probe_xtile_stamps_clear(void) {
-  static uint64_t zero[1 << 16];
-  for (int64_t o = 0; o < (1 << 22); o += 1 << 16)
-    LHPC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(lhpc::g_xt_stamps), zero, sizeof(zero), static_cast<size_t>(o) * 8,
-                                   hipMemcpyHostToDevice));
-  return LHPC_OK;
+  try {
+    static uint64_t zero[1 << 16];
+    for (int64_t o = 0; o < (1 << 22); o += 1 << 16)
+      LHPC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(lhpc::g_xt_stamps), zero, sizeof(zero), static_cast<size_t>(o) * 8,
+                                     hipMemcpyHostToDevice));
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }
 #endif

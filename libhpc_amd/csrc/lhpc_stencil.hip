@@ -894,56 +894,70 @@ using namespace lhpc;
 
 extern "C" int lhpc_blur_x_f32(const float *a, float *b, int64_t ny, int64_t nx, int64_t ghost,
                                int nblur, int on_device, void *stream) {
-  return blur_entry(false, a, b, ny, nx, ghost, nblur, on_device, stream, nullptr);
+  try {
+    return blur_entry(false, a, b, ny, nx, ghost, nblur, on_device, stream, nullptr);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_blur_y_f32(const float *a, float *b, int64_t ny, int64_t nx, int64_t ghost,
                                int nblur, int on_device, void *stream) {
-  return blur_entry(true, a, b, ny, nx, ghost, nblur, on_device, stream, nullptr);
+  try {
+    return blur_entry(true, a, b, ny, nx, ghost, nblur, on_device, stream, nullptr);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_blur_x_f32_opts(const float *a, float *b, int64_t ny, int64_t nx, int64_t ghost, int nblur,
                                     int on_device, void *stream, const lhpc_options *opts) {
-  return blur_entry(false, a, b, ny, nx, ghost, nblur, on_device, stream, opts);
+  try {
+    return blur_entry(false, a, b, ny, nx, ghost, nblur, on_device, stream, opts);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_blur_y_f32_opts(const float *a, float *b, int64_t ny, int64_t nx, int64_t ghost, int nblur,
                                     int on_device, void *stream, const lhpc_options *opts) {
-  return blur_entry(true, a, b, ny, nx, ghost, nblur, on_device, stream, opts);
+  try {
+    return blur_entry(true, a, b, ny, nx, ghost, nblur, on_device, stream, opts);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_stencil7_f32_planes_opts(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx,
                                              int64_t ghost, float c0, float c1, int64_t z_begin, int64_t z_end,
                                              void *stream, const lhpc_options *opts) {
-  if (!u || !out || nz < 0 || ny < 0 || nx < 0 || ghost < 1 || z_begin < 0 || z_end > nz)
-    return LHPC_ERR_INVALID_ARG;
-  return s7_launch(u, out, nz, ny, nx, ghost, c0, c1, z_begin, z_end, static_cast<hipStream_t>(stream),
-                   resolve_options(opts));
+  try {
+    if (!u || !out || nz < 0 || ny < 0 || nx < 0 || ghost < 1 || z_begin < 0 || z_end > nz)
+      return LHPC_ERR_INVALID_ARG;
+    return s7_launch(u, out, nz, ny, nx, ghost, c0, c1, z_begin, z_end, static_cast<hipStream_t>(stream),
+                     resolve_options(opts));
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_stencil7_f32_planes(const float *u, float *out, int64_t nz, int64_t ny,
                                         int64_t nx, int64_t ghost, float c0, float c1,
                                         int64_t z_begin, int64_t z_end, void *stream) {
-  return lhpc_stencil7_f32_planes_opts(u, out, nz, ny, nx, ghost, c0, c1, z_begin, z_end, stream, nullptr);
+  try {
+    return lhpc_stencil7_f32_planes_opts(u, out, nz, ny, nx, ghost, c0, c1, z_begin, z_end, stream, nullptr);
+  } LHPC_ABI_CATCH
 }
 
 extern "C" int lhpc_stencil7_f32(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx,
                                  int64_t ghost, float c0, float c1, int on_device, void *stream) {
-  if (!u || !out || nz < 0 || ny < 0 || nx < 0 || ghost < 1) return LHPC_ERR_INVALID_ARG;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const lhpc_options o = resolve_options(nullptr);
-  if (on_device) return s7_launch(u, out, nz, ny, nx, ghost, c0, c1, 0, nz, s, o);
-  const size_t bytes =
-      static_cast<size_t>((nz + 2 * ghost) * (ny + 2 * ghost) * (nx + 2 * ghost)) * 4;
-  HostStage du, dout;
-  LHPC_HIP_TRY(hipMalloc(&du.d, bytes));
-  LHPC_HIP_TRY(hipMalloc(&dout.d, bytes));
-  LHPC_HIP_TRY(hipMemcpy(du.d, u, bytes, hipMemcpyHostToDevice));  // host buffers: synchronous copies
-  // ghost cells of `out` keep the caller's values
-  LHPC_HIP_TRY(hipMemcpy(dout.d, out, bytes, hipMemcpyHostToDevice));
-  LHPC_TRY(s7_launch(static_cast<float *>(du.d), static_cast<float *>(dout.d), nz, ny, nx, ghost, c0,
-                     c1, 0, nz, s, o));
-  LHPC_HIP_TRY(hipStreamSynchronize(s));
-  LHPC_HIP_TRY(hipMemcpy(out, dout.d, bytes, hipMemcpyDeviceToHost));
-  return LHPC_OK;
+  try {
+    if (!u || !out || nz < 0 || ny < 0 || nx < 0 || ghost < 1) return LHPC_ERR_INVALID_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const lhpc_options o = resolve_options(nullptr);
+    if (on_device) return s7_launch(u, out, nz, ny, nx, ghost, c0, c1, 0, nz, s, o);
+    const size_t bytes =
+        static_cast<size_t>((nz + 2 * ghost) * (ny + 2 * ghost) * (nx + 2 * ghost)) * 4;
+    HostStage du, dout;
+    LHPC_HIP_TRY(hipMalloc(&du.d, bytes));
+    LHPC_HIP_TRY(hipMalloc(&dout.d, bytes));
+    LHPC_HIP_TRY(hipMemcpy(du.d, u, bytes, hipMemcpyHostToDevice));  // host buffers: synchronous copies
+    // ghost cells of `out` keep the caller's values
+    LHPC_HIP_TRY(hipMemcpy(dout.d, out, bytes, hipMemcpyHostToDevice));
+    LHPC_TRY(s7_launch(static_cast<float *>(du.d), static_cast<float *>(dout.d), nz, ny, nx, ghost, c0,
+                       c1, 0, nz, s, o));
+    LHPC_HIP_TRY(hipStreamSynchronize(s));
+    LHPC_HIP_TRY(hipMemcpy(out, dout.d, bytes, hipMemcpyDeviceToHost));
+    return LHPC_OK;
+  } LHPC_ABI_CATCH
 }

@@ -204,3 +204,17 @@ def test_struct_mirrors_match_header(lhpc, tmp_path, py, c):
         o = lhpc.Options()
         lhpc.lib.lhpc_options_init(C.byref(o))
         assert o.struct_size == C.sizeof(lhpc.Options)
+
+
+def test_host_allocation_failure_is_a_status_not_an_exception(lhpc):
+    """No C++ exception crosses the C ABI (int status only): an
+    entry point whose host work cannot allocate returns LHPC_ERR_ALLOC (-3)
+    instead of terminating the caller's process.  The power-law generator
+    asked for an 8-TiB length table (l_max = 2^40) fails that way before it
+    writes anything."""
+    import numpy as np
+    rp = np.full(11, -7, dtype=np.int64)
+    nnz = C.c_int64(0)
+    st = lhpc.lib.lhpc_gen_powerlaw_row_ptr(10, 1 << 41, 1.8, 1, 1 << 40, 1, rp.ctypes.data, C.byref(nnz))
+    assert st == -3, st
+    assert (rp == -7).all()
