@@ -88,6 +88,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import step_model  # noqa: E402  (tools/step_model.py: the N > 1 step model, pure Python)
 
 METRIC = "CSR SpMV GFLOP/s + achieved HBM GB/s, n=10M nnz=150M, at 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
@@ -498,6 +500,27 @@ def main():
                                        "column part as each exchange lands); exchange_only = lhpc_dist_exchange "
                                        "alone; spmv_only = exchange NONE; max over ranks; chunks_per_rank = the "
                                        "fastest of the measured K (other_chunk_counts)"}
+            if world > 1 and chosen in xtimes:
+                # the step model (tools/step_model.py) at this run's own numbers:
+                # measured receive / per-link rate from the exchange-only time, and
+                # the step it predicts beside the measured one.
+                # The stage (the x tile gather) alone, from a two-range plan of
+                # the same local rows; 0.45 of the local call when that plan
+                # cannot be built (not XTILE)
+                stage_ms, stage_src = 0.45 * spmv_only * 1e3, "0.45 of spmv_only (no split plan)"
+                if local_rows >= 2:
+                    try:
+                        with L.SpMVPlan(lrp, lc, lv, n, splits=[local_rows // 2]) as sp:
+                            stage_ms = timed(lambda: sp.stage(xd, stream=stream), args.steps, args.warmup) * 1e3
+                            stage_src = "measured (lhpc_spmv_stage of the rank's rows)"
+                    except L.LhpcError:
+                        pass
+                xr = xtimes[chosen]
+                exchange_report["model"] = dict(
+                    step_model.exchange_model(world, n_chunks, chained, n, tsz, stage_ms, spmv_only * 1e3,
+                                              xr["exchange_only_ms"],
+                                              xr["chained_step_ms" if chained else "step_ms"]),
+                    stage_source=stage_src, exchange=chosen)
 
             class _Native:
                 def step(self, xv):
@@ -718,6 +741,8 @@ def main():
             result["cpu_baseline"] = result.pop("_cpu", None)
         result.pop("_cpu", None)
     if rank == 0:
+        # which library ran: the product build has flags 0 (lhpc_build_flags)
+        result["library"] = {"path": os.path.relpath(L.LIB_PATH, ROOT), "build_flags": L.BUILD_FLAGS}
         print(json.dumps(result), flush=True)
     if world > 1 or force_native:
         dist.barrier()

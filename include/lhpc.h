@@ -224,6 +224,14 @@ void lhpc_options_init(lhpc_options *opts);
 /* ------------------------------------------------------------- runtime   */
 const char *lhpc_strerror(int status);
 int lhpc_abi_version(void);
+/* Build tag of this library, bit flags; 0 for the product build.  Loaders
+ * (libhpc_amd/__init__.py with LHPC_LIB_PATH) refuse LHPC_BUILD_PROBE, a
+ * timing-only build that skips work and computes wrong results.           */
+#define LHPC_BUILD_TUNING 1 /* reads LHPC_* tuning variables (tools/ A/B)     */
+#define LHPC_BUILD_DEBUG 2  /* device bounds traps, synchronous launch checks */
+#define LHPC_BUILD_PROBE 4  /* timing-only probe: wrong results               */
+#define LHPC_BUILD_AB 8     /* an A/B variant of the product kernels          */
+int lhpc_build_flags(void);
 /* number of visible gfx950 devices (0 when none; never an error)          */
 int lhpc_device_count(void);
 

@@ -51,7 +51,7 @@ KERNEL_ROWGROUP, KERNEL_ADAPTIVE, KERNEL_XSLICE, KERNEL_XTILE, KERNEL_SELL = 0, 
 
 # every symbol include/lhpc.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = (
-    "lhpc_strerror", "lhpc_abi_version", "lhpc_device_count",
+    "lhpc_strerror", "lhpc_abi_version", "lhpc_build_flags", "lhpc_device_count",
     "lhpc_spmv_plan_create", "lhpc_spmv", "lhpc_spmv_plan_info_get",
     "lhpc_spmv_plan_destroy", "lhpc_csr_partition_rows",
     "lhpc_blur_x_f32", "lhpc_blur_y_f32", "lhpc_stencil7_f32",
@@ -93,6 +93,13 @@ def _bind_single_hip_runtime():
 
 _bind_single_hip_runtime()
 lib = C.CDLL(LIB_PATH)
+BUILD_TUNING, BUILD_DEBUG, BUILD_PROBE, BUILD_AB = 1, 2, 4, 8
+BUILD_FLAGS = lib.lhpc_build_flags()
+if BUILD_FLAGS & BUILD_PROBE and os.environ.get("LHPC_ALLOW_PROBE_BUILD") != "1":
+    # a timing-only probe build skips work and computes wrong results: only
+    # an explicit opt-in (the tools/ A/B scripts) may load it
+    raise ImportError(f"{LIB_PATH} is a timing-only probe build (lhpc_build_flags = {BUILD_FLAGS}); "
+                      "set LHPC_ALLOW_PROBE_BUILD=1 to time it")
 _p, _i, _i64, _u, _u64, _f, _d = (C.c_void_p, C.c_int, C.c_int64, C.c_uint,
                                   C.c_uint64, C.c_float, C.c_double)
 
@@ -173,6 +180,7 @@ def _sig(name, res, *args):
 
 _sig("lhpc_strerror", C.c_char_p, _i)
 _sig("lhpc_abi_version", _i)
+_sig("lhpc_build_flags", _i)
 _sig("lhpc_device_count", _i)
 _sig("lhpc_spmv_plan_create", _i, C.POINTER(_p), _i, _i64, _i64, _i64, _p, _i, _p,
      _p, _p, _i, _u)

@@ -182,7 +182,130 @@ __global__ __launch_bounds__(256) void k_gather_sliced(const int32_t *__restrict
   }
 }
 
+// Fragment probe (round 6): the XTILE reduce's memory access shape and
+// occupancy without its compute (scan, rank, segmented scan).  One block per
+// chunk of M = BLK·RUN positions, chunks walked as the reduce walks them
+// (c = C − 1 − ((b % 8)·Cx + b / 8)); per chunk:
+//   round trip 1  the chunk's row of the segment table: S u32 starts;
+//   stream        RUN values of T + RUN u16 per thread, wave-transposed (each
+//                 load instruction 1 KB contiguous, non-temporal) — the
+//                 reduce's val + iperm;
+//   round trip 2  the chunk's S fragments of xg (segment j = flat positions
+//                 [⌊j·M/S⌋, ⌊(j+1)·M/S⌋), in the tile-major stream at
+//                 C·⌊j·M/S⌋ + c·len_j) into LDS in flat order: fp32 by 4-B
+//                 LDS-DMA (as the reduce); fp64 (F64 = 0) as 8-B buffer loads
+//                 + ds_write_b64 (as the reduce), (F64 = 1) as two 4-B LDS-DMA
+//                 per 64 lanes (32 positions per instruction);
+// then one barrier and a trivial read of the run (kept alive through sink).
+template <typename T, int BLK, int F64>
+__global__ __launch_bounds__(BLK) void k_frag(const uint32_t *__restrict__ seg, const T *__restrict__ xg,
+                                             int xg_bytes, const T *__restrict__ val,
+                                             const uint16_t *__restrict__ ip, int S, int64_t C, int64_t Cx,
+                                             double *__restrict__ sink) {
+  constexpr int RUN = 64 / static_cast<int>(sizeof(T)), M = BLK * RUN, NB = M / BLK;
+  constexpr int VW = 16 / static_cast<int>(sizeof(T)), NV = RUN / VW, REG = lhpc::kWave * RUN, NIP = RUN * 2 / 16;
+  typedef T tvec __attribute__((ext_vector_type(VW)));
+  extern __shared__ __align__(16) unsigned char frag_lds[];
+  T *xs = reinterpret_cast<T *>(frag_lds);
+  int *base = reinterpret_cast<int *>(xs + M + VW);
+  const int tid = threadIdx.x, lane = tid & (lhpc::kWave - 1);
+  const int wv = __builtin_amdgcn_readfirstlane(tid / lhpc::kWave);
+  const int64_t c = C - 1 - (static_cast<int64_t>(blockIdx.x % 8) * Cx + blockIdx.x / 8);
+  if (c < 0) return;
+  for (int j = tid; j < S; j += BLK)
+    base[j] = static_cast<int>(seg[c * S + j]) - static_cast<int>(static_cast<int64_t>(j) * M / S);
+  tvec vv[NV];
+  {
+    const tvec *vp = reinterpret_cast<const tvec *>(val + c * M + wv * REG) + lane;
+#pragma unroll
+    for (int q = 0; q < NV; ++q) vv[q] = __builtin_nontemporal_load(vp + q * lhpc::kWave);
+  }
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(xg), 0, xg_bytes, 0x00020000);
+  auto src_of = [&](int f) {  // stream index of flat position f of chunk c
+    const int j = static_cast<int>((static_cast<int64_t>(f + 1) * S + M - 1) / M) - 1;
+    return base[j] + f;
+  };
+  if constexpr (sizeof(T) == 4) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void *)(xs + (wv * NB + u) * lhpc::kWave), 4,
+          src_of((wv * NB + u) * lhpc::kWave + lane) * 4, 0, 0, 0);
+#endif
+  } else if constexpr (F64 == 1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int u = 0; u < 2 * NB; ++u)  // 32 positions (64 dwords) per instruction
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void *)(xs + (wv * NB * 2 + u) * 32), 4,
+          src_of((wv * NB * 2 + u) * 32 + lane / 2) * 8 + (lane & 1) * 4, 0, 0, 0);
+#endif
+  } else {
+    T xv[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      xv[u] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(
+                                        rs, src_of((wv * NB + u) * lhpc::kWave + lane) * 8, 0, 0));
+#pragma unroll
+    for (int u = 0; u < NB; ++u) xs[(wv * NB + u) * lhpc::kWave + lane] = xv[u];
+  }
+  lhpc::u32x4 ipv[NIP];
+  {
+    const lhpc::u32x4 *p = reinterpret_cast<const lhpc::u32x4 *>(ip + c * M + wv * REG) + lane;
+#pragma unroll
+    for (int q = 0; q < NIP; ++q) ipv[q] = __builtin_nontemporal_load(p + q * lhpc::kWave);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  double acc = 0.0;
+#pragma unroll
+  for (int j = 0; j < RUN; ++j)
+    acc += static_cast<double>(vv[j / VW][j % VW]) * static_cast<double>(xs[tid * RUN + j]) +
+           static_cast<double>(ipv[j / 8][(j % 8) / 2] & 1u);
+  if (acc == 1234.5678) sink[0] = acc;  // keep every load alive
+}
+
 }  // namespace
+
+// k_frag: t = 4 (fp32, 512 threads) or 8 (fp64, 1024 threads); f64_dma picks
+// the fp64 fragment load (0: b64 + ds_write, 1: 4-B LDS-DMA); lds_bytes of
+// dynamic LDS (≥ M·t + 16 + 4·S) sets the blocks per CU as the reduce's does.
+// seg[c·S + j] = stream start of chunk c's segment j; val: C·M of t, ip: C·M u16.
+extern "C" int lhpc_probe_frag(const uint32_t *seg, const void *xg, int64_t xg_bytes, const void *val,
+                               const uint16_t *ip, int S, int64_t C, int t, int f64_dma, int lds_bytes,
+                               double *sink, void *stream) {
+  if (C <= 0 || S <= 0 || xg_bytes <= 0 || xg_bytes >= (int64_t{1} << 31)) return static_cast<int>(hipErrorInvalidValue);
+  const int64_t Cx = (C + 7) / 8;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<unsigned>(8 * Cx));
+  if (t == 4) {
+    const int M = 512 * 16;
+    if (lds_bytes < M * 4 + 16 + 4 * S) return static_cast<int>(hipErrorInvalidValue);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_frag<float, 512, 0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    hipLaunchKernelGGL((k_frag<float, 512, 0>), grid, dim3(512), lds_bytes, st, seg, static_cast<const float *>(xg),
+                       static_cast<int>(xg_bytes), static_cast<const float *>(val), ip, S, C, Cx, sink);
+  } else if (t == 8) {
+    const int M = 1024 * 8;
+    if (lds_bytes < M * 8 + 16 + 4 * S) return static_cast<int>(hipErrorInvalidValue);
+    const void *fn = f64_dma ? reinterpret_cast<const void *>(k_frag<double, 1024, 1>)
+                             : reinterpret_cast<const void *>(k_frag<double, 1024, 0>);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    if (f64_dma)
+      hipLaunchKernelGGL((k_frag<double, 1024, 1>), grid, dim3(1024), lds_bytes, st, seg,
+                         static_cast<const double *>(xg), static_cast<int>(xg_bytes),
+                         static_cast<const double *>(val), ip, S, C, Cx, sink);
+    else
+      hipLaunchKernelGGL((k_frag<double, 1024, 0>), grid, dim3(1024), lds_bytes, st, seg,
+                         static_cast<const double *>(xg), static_cast<int>(xg_bytes),
+                         static_cast<const double *>(val), ip, S, C, Cx, sink);
+  } else {
+    return static_cast<int>(hipErrorInvalidValue);
+  }
+  return static_cast<int>(hipGetLastError());
+}
 
 // Check of lhpc::wave_incl_scan (DPP) against a shuffle scan, per wave.
 __global__ __launch_bounds__(256) void k_wave_scan(const int *__restrict__ in, int *__restrict__ dpp,

@@ -1,4 +1,17 @@
-// lhpc_runtime.hip — status strings and device discovery for the C ABI.
+// lhpc_runtime.hip — status strings, build tag and device discovery for the C ABI.
+
+// Build tag (lhpc_build_flags), read before any header sets a default, so
+// only command-line -D flags count: timing-only probes that skip work and
+// compute wrong results, and A/B variants of the product kernels.
+#if defined(LHPC_XT_PROBE_GVAL) || defined(LHPC_XT_PROBE_NOVAL) || defined(LHPC_XT_PROBE_VI) || \
+    defined(LHPC_XT_PROBE_XG) || defined(LHPC_XT_PROBE_GROUPED) || defined(LHPC_SORT_PROBE)
+#define LHPC_TAG_PROBE 1
+#endif
+#if defined(LHPC_XT_RBLK32) || defined(LHPC_XT_RBLK64) || defined(LHPC_XT_IP_WAVES) || defined(LHPC_XT_LDS_TOTAL) || \
+    defined(LHPC_XT_XG_CPOL) || defined(LHPC_XT_SEGHI) || defined(LHPC_XT_F64DMA) || defined(LHPC_XT_STAMPS) ||   \
+    defined(LHPC_SELL_NO_SHFL) || defined(LHPC_SCRATCH_DEFAULT_POOL)
+#define LHPC_TAG_AB 1
+#endif
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -31,6 +44,23 @@ extern "C" const char *lhpc_strerror(int status) {
 extern "C" int lhpc_abi_version(void) {
   try { return LHPC_ABI_VERSION;
   } LHPC_ABI_CATCH
+}
+
+extern "C" int lhpc_build_flags(void) {
+  int f = 0;
+#ifdef LHPC_TUNING_ENV
+  f |= LHPC_BUILD_TUNING;
+#endif
+#if defined(LHPC_DEBUG_BOUNDS) || defined(LHPC_DEBUG_SYNC)
+  f |= LHPC_BUILD_DEBUG;
+#endif
+#ifdef LHPC_TAG_PROBE
+  f |= LHPC_BUILD_PROBE;
+#endif
+#ifdef LHPC_TAG_AB
+  f |= LHPC_BUILD_AB;
+#endif
+  return f;
 }
 
 extern "C" int lhpc_device_count(void) {

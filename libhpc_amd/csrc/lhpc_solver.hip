@@ -22,6 +22,8 @@
 // between the dot and its use, and an all-gather of p after k_cg_p.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -316,24 +318,46 @@ int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int
                    int *iters_out, double *resid_out, void *stream);
 }
 
+#ifdef LHPC_DEBUG_BOUNDS
+// Debug build only (tests/debug_build_check.py): iteration body number k
+// (0-based, counted over the next solves) returns LHPC_ERR_INTERNAL after
+// enqueueing its work — lhpc_cg_solve's error path with work on the stream.
+namespace {
+std::atomic<int> g_cg_fail_at{-1};
+bool cg_fault_now() {
+  const int v = g_cg_fail_at.load();
+  if (v < 0) return false;
+  g_cg_fail_at.store(v - 1);
+  return v == 0;
+}
+}  // namespace
+extern "C" int lhpc_debug_cg_fail_at(int k) {
+  g_cg_fail_at.store(k);
+  return LHPC_OK;
+}
+#endif
+
 // One solve per plan at a time: the work vectors, scalars and captured
 // graphs belong to the plan, so a second concurrent solve is
-// refused instead of racing on them.
+// refused instead of racing on them.  The flag is released only once the
+// solve's stream has drained: an error return after the first enqueue
+//  leaves kernels in flight that still use the plan's work, and
+// the next solve (on any stream) may reuse it as soon as the flag is free.
 extern "C" int lhpc_cg_solve(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int max_iter,
                              int check_every, int *iters_out, double *resid_out, void *stream) {
   try {
     if (!plan || !b || !x || max_iter < 0 || !(tol >= 0.0)) return LHPC_ERR_INVALID_ARG;
     int idle = 0;
     if (!plan->cg_busy.compare_exchange_strong(idle, 1)) return LHPC_ERR_BUSY;
-    int st;
-    try {
-      st = cg_solve_owned(plan, b, x, tol, max_iter, check_every, iters_out, resid_out, stream);
-    } catch (...) {
-      plan->cg_busy.store(0);  // the plan's work is free again
-      throw;
-    }
-    plan->cg_busy.store(0);
-    return st;
+    struct Release {  // on every exit, the exception path included
+      lhpc_spmv_plan *p;
+      hipStream_t s;
+      ~Release() {
+        (void)hipStreamSynchronize(s);  // a no-op wait on the success path (already drained)
+        p->cg_busy.store(0);
+      }
+    } release{plan, static_cast<hipStream_t>(stream)};
+    return cg_solve_owned(plan, b, x, tol, max_iter, check_every, iters_out, resid_out, stream);
   } LHPC_ABI_CATCH
 }
 
@@ -413,11 +437,15 @@ int cg_solve_owned(lhpc_spmv_plan *plan, const void *b, void *x, double tol, int
   auto body = [&](int c, bool full) -> int {
     if (fused) {
       LHPC_TRY(sell_cg_step(plan, r, pb[c ^ 1], pb[c], x, q, rr[c ^ 1], pq, rr[c], rr[c ^ 1], pq, s));
-      return cg_r_launch(dtype, n, rr[c], pq, r, q, rr[c ^ 1], part, s);
+      LHPC_TRY(cg_r_launch(dtype, n, rr[c], pq, r, q, rr[c ^ 1], part, s));
+    } else {
+      LHPC_TRY(lhpc_spmv_dot(plan, p, q, p, pq, s));
+      LHPC_TRY(cg_r_launch(dtype, n, rr[c], pq, r, q, rr[c ^ 1], part, s));
+      if (full) LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[c], pq, rr[c ^ 1], rr[c], x, p, r, s));
     }
-    LHPC_TRY(lhpc_spmv_dot(plan, p, q, p, pq, s));
-    LHPC_TRY(cg_r_launch(dtype, n, rr[c], pq, r, q, rr[c ^ 1], part, s));
-    if (full) LHPC_TRY(lhpc_cg_step_xp(dtype, n, rr[c], pq, rr[c ^ 1], rr[c], x, p, r, s));
+#ifdef LHPC_DEBUG_BOUNDS
+    if (cg_fault_now()) return LHPC_ERR_INTERNAL;
+#endif
     return LHPC_OK;
   };
   // the pending x += α·p of the last iteration (parity c), when the loop ends

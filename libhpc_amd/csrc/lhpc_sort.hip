@@ -62,7 +62,7 @@ __device__ __forceinline__ uint32_t digit_of(K k, int shift, uint32_t mask) {
 template <typename K, int TILE>
 __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const K *__restrict__ keys, int64_t n,
                                                                 int shift, uint32_t mask, int64_t per_block,
-                                                                uint32_t *__restrict__ counts) {
+                                                                uint32_t *__restrict__ counts, int vec16) {
   __shared__ uint32_t hist[4][256];
   const int t = threadIdx.x, w = t / kWave;
   for (int i = t; i < 4 * 256; i += kSortThreads) (&hist[0][0])[i] = 0;
@@ -73,7 +73,10 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const K *__restr
   if constexpr (sizeof(K) == 4) {
     typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
     constexpr int STEP = 16 * kSortThreads;
-    for (; i + STEP <= b1; i += STEP) {  // b0 is a multiple of TILE, so 16-B aligned
+    // vec16 (host: keys 16-B aligned; a caller's key pointer may be 4-B
+    // aligned only, e.g. a slice t[1:]): b0 is a multiple of TILE, so every
+    // 16-B load is aligned; otherwise the scalar loop below takes every key
+    for (; vec16 && i + STEP <= b1; i += STEP) {
       const u32x4v *p = reinterpret_cast<const u32x4v *>(keys + i) + t;
       u32x4v v[4];
 #pragma unroll
@@ -378,8 +381,9 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
   for (int shift = begin_bit; shift < end_bit; shift += 8, ++passes) {
     const int bits = std::min(8, end_bit - shift);
     const uint32_t mask = (1u << bits) - 1u;
+    const int vec16 = (reinterpret_cast<uintptr_t>(kin) & 15u) == 0 ? 1 : 0;
     hipLaunchKernelGGL((k_radix_upsweep<K, TILE>), dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0, s, kin,
-                       n, shift, mask, per, cnt);
+                       n, shift, mask, per, cnt, vec16);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(kSortThreads), 0, s, cnt, static_cast<int>(nb), db);
     hipLaunchKernelGGL((k_radix_downsweep<K, HAS_V, IPT, PF>), dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0,
                        s, kin, kout, vin, vout, n, shift, mask, per, cnt, db);

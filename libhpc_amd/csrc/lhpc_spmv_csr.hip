@@ -258,6 +258,35 @@ __device__ __forceinline__ double adaptive_lane_order(const double (&p)[kSellMax
   return ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
 }
 
+// The block's y·w partial in ADAPTIVE's order (k_spmv_adaptive's epilogue):
+// thread t holds row t's product d (0 past n_rows).  A full block has one
+// ADAPTIVE lane per row — the same lanes, one wave tree per 64 rows, the
+// four wave sums folded left.  A last block of nb ≤ 128 rows has L ≥ 2 lanes
+// per row: ADAPTIVE's row r sits at lane r·L with zeros between, so its
+// waves hold 64/L rows each; the products are moved to those lanes through
+// LDS and summed the same way ((A0 + A1) + A2) + A3 (SELL's own waves would
+// give (A0 + A1) + (A2 + A3)).
+__device__ __forceinline__ void sell_dot_partial(double d, int64_t nb, double *wsum, double *dl, double *dpart) {
+  int L = kWave;
+  while (L > 1 && nb * L > kBlock) L >>= 1;  // block-uniform
+  if (L > 1) {
+    dl[threadIdx.x] = 0.0;
+    __syncthreads();
+    if (threadIdx.x < nb) dl[threadIdx.x * L] = d;
+    __syncthreads();
+    d = dl[threadIdx.x];
+  }
+  d = group_sum<kWave>(d);
+  if ((threadIdx.x & (kWave - 1)) == 0) wsum[threadIdx.x / kWave] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = wsum[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / kWave; ++i) t += wsum[i];
+    dpart[blockIdx.x] = t;
+  }
+}
+
 // soff[s] = first entry of slice s (a multiple of 64); its width is
 // (soff[s + 1] − soff[s]) / 64 ≤ kSellMaxW.  One block = 4 slices = the
 // 256 rows of ADAPTIVE's block blockIdx.x.
@@ -268,6 +297,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(const int32_t *__restrict_
                                                       const T *__restrict__ w, double *__restrict__ dpart) {
 #pragma clang fp contract(off)  // the product rounds before the add, as ADAPTIVE's LDS-staged products do
   __shared__ double wsum[kBlock / kWave];
+  __shared__ double dl[kBlock];
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t slice = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + threadIdx.x / kWave;
   const int64_t row = slice * kWave + lane;
@@ -311,18 +341,9 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell(const int32_t *__restrict_
   }
   const T yv = static_cast<T>(a);
   if (row < n_rows) y[row] = yv;
-  if (w) {  // block-uniform: ADAPTIVE's epilogue tree (one lane per row)
-    double d = row < n_rows ? static_cast<double>(yv) * static_cast<double>(wv) : 0.0;
-    d = group_sum<kWave>(d);
-    if (lane == 0) wsum[threadIdx.x / kWave] = d;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double t = wsum[0];
-#pragma unroll
-      for (int i = 1; i < kBlock / kWave; ++i) t += wsum[i];
-      dpart[blockIdx.x] = t;
-    }
-  }
+  if (w)  // block-uniform: ADAPTIVE's epilogue tree
+    sell_dot_partial(row < n_rows ? static_cast<double>(yv) * static_cast<double>(wv) : 0.0,
+                     n_rows - static_cast<int64_t>(blockIdx.x) * kBlock, wsum, dl, dpart);
 }
 
 // CG step on a SELL plan (lhpc_cg_solve): the previous iteration's
@@ -339,6 +360,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell_cg(
     T *__restrict__ q, int64_t n_rows, const double *__restrict__ anum, const double *__restrict__ aden,
     const double *__restrict__ bnum, const double *__restrict__ bden, double *__restrict__ dpart) {
   __shared__ double wsum[kBlock / kWave];
+  __shared__ double dl[kBlock];
   const T a = static_cast<T>(*anum / *aden);   // k_cg_xp's α and β
   const T beta = static_cast<T>(*bnum / *bden);
   const int lane = threadIdx.x & (kWave - 1);
@@ -399,16 +421,8 @@ __global__ __launch_bounds__(kBlock) void k_spmv_sell_cg(
   }
   const T yv = static_cast<T>(acc);
   if (row < n_rows) q[row] = yv;
-  double d = row < n_rows ? static_cast<double>(yv) * static_cast<double>(pn) : 0.0;
-  d = group_sum<kWave>(d);
-  if (lane == 0) wsum[threadIdx.x / kWave] = d;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = wsum[0];
-#pragma unroll
-    for (int i = 1; i < kBlock / kWave; ++i) t += wsum[i];
-    dpart[blockIdx.x] = t;
-  }
+  sell_dot_partial(row < n_rows ? static_cast<double>(yv) * static_cast<double>(pn) : 0.0,
+                   n_rows - static_cast<int64_t>(blockIdx.x) * kBlock, wsum, dl, dpart);
 }
 
 template <typename T>

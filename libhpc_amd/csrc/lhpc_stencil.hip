@@ -760,6 +760,68 @@ int blur_entry(bool ydir, const float *a, float *b, int64_t ny, int64_t nx, int6
   return LHPC_OK;
 }
 
+#ifdef LHPC_TUNING_ENV
+constexpr bool kS7AllTiles = true;
+#else
+constexpr bool kS7AllTiles = false;
+#endif
+struct S7Args {
+  const float *u;
+  float *out;
+  int64_t nz, ny, nx, g;
+  float c0, c1;
+  int64_t zb, ze, zc;
+  hipStream_t s;
+};
+// x4 ring, one tile shape: LDS-shared halos (prefetch 2) or the private ring
+// at prefetch depth 1–3.  Product build: the 2-row tile only with shared halos
+template <int RY, int NJ, int M, bool P>
+int s74_launch(const S7Args &a, bool share, int pf) {
+  const int64_t ntx = (a.nx + NJ * kWave - 1) / (NJ * kWave), nty = (a.ny + 4 * RY - 1) / (4 * RY),
+                ntz = (a.ze - a.zb + a.zc - 1) / a.zc;
+  const dim3 grid(static_cast<unsigned>(ntx * nty * ntz)), blk(256);
+#define LHPC_S74_GO(PFV, SH)                                                                               \
+  hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, PFV, P, SH>), grid, blk, 0, a.s, a.u, a.out, a.nz, a.ny, a.nx, \
+                     a.g, a.c0, a.c1, a.zb, a.ze, ntx, nty, ntz, a.zc)
+  if (share) {
+    LHPC_S74_GO(2, true);
+  } else if constexpr (kS7AllTiles || RY == 1) {
+    if (pf == 2) LHPC_S74_GO(2, false);
+    else if (pf == 3) LHPC_S74_GO(3, false);
+    else LHPC_S74_GO(1, false);
+  } else {
+    return LHPC_ERR_UNSUPPORTED;
+  }
+#undef LHPC_S74_GO
+  return LHPC_OK;
+}
+template <int RY, int NJ>
+int s74_store(const S7Args &a, bool m5, bool part, bool share, int pf) {
+  if (m5) return part ? s74_launch<RY, NJ, 5, true>(a, share, pf) : s74_launch<RY, NJ, 5, false>(a, share, pf);
+  return part ? s74_launch<RY, NJ, 6, true>(a, share, pf) : s74_launch<RY, NJ, 6, false>(a, share, pf);
+}
+// dword ring, one tile shape and store mode, prefetch depth 1–3
+template <int RY, int NJ, int M>
+int s7b_launch(const S7Args &a, int pf) {
+  const int64_t ntx = (a.nx + NJ * kWave - 1) / (NJ * kWave), nty = (a.ny + 4 * RY - 1) / (4 * RY),
+                ntz = (a.ze - a.zb + a.zc - 1) / a.zc;
+  const dim3 grid(static_cast<unsigned>(ntx * nty * ntz)), blk(256);
+#define LHPC_S7B_GO(PFV)                                                                                   \
+  hipLaunchKernelGGL((k_stencil7_buf<RY, NJ, M, PFV>), grid, blk, 0, a.s, a.u, a.out, a.nz, a.ny, a.nx, a.g,  \
+                     a.c0, a.c1, a.zb, a.ze, ntx, nty, ntz, a.zc)
+  if (pf == 2) LHPC_S7B_GO(2);
+  else if (pf == 3) LHPC_S7B_GO(3);
+  else LHPC_S7B_GO(1);
+#undef LHPC_S7B_GO
+  return LHPC_OK;
+}
+template <int RY, int NJ>
+int s7b_store(const S7Args &a, int store_mode, int pf) {
+  if (store_mode == 1) return s7b_launch<RY, NJ, 1>(a, pf);
+  if (store_mode == 4) return s7b_launch<RY, NJ, 4>(a, pf);
+  return s7b_launch<RY, NJ, 0>(a, pf);
+}
+
 int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, int64_t g, float c0,
               float c1, int64_t zb, int64_t ze, hipStream_t s, const lhpc_options &o) {
   if (zb >= ze || ny == 0 || nx == 0) return LHPC_OK;
@@ -792,7 +854,9 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
     // (one z front over 8 or 16 waves' rows) were slower: 196–236 µs.
     const bool x4_default = impl == LHPC_S7_AUTO || impl == LHPC_S7_RING_X4_LDS;
     const bool wide = x4_default && nx >= 512;
-    int ry = o.stencil7_ry > 0 ? o.stencil7_ry : (wide ? 1 : 2),
+    // (the dword ring — opt-in, S7_RING — takes 1 row × 8 blocks: its 2-row
+    // tiles spill SGPRs and are tuning-build only since round 6)
+    int ry = o.stencil7_ry > 0 ? o.stencil7_ry : (x4_default && !wide ? 2 : 1),
         nj = o.stencil7_nj > 0 ? o.stencil7_nj : (x4_default && !wide ? 4 : 8);
     int zc = o.stencil7_zc, pf = o.stencil7_pf;
     // x4 ring by default when every x tile is full (nx % (64·NJ) == 0): 198-211 us against
@@ -811,74 +875,33 @@ int s7_launch(const float *u, float *out, int64_t nz, int64_t ny, int64_t nx, in
       const int64_t nchunks = std::max<int64_t>(1, (target + xy - 1) / xy);
       zc = static_cast<int>(std::max<int64_t>(4, (ze - zb + nchunks - 1) / nchunks));
     }
+    // product build: only the tiles whose kernels keep every register in
+    // registers (1 row per wave, or the x4 ring's LDS-shared 2 × 4 default;
+    // tests/test_kernel_resources.py) — any other tile is LHPC_ERR_UNSUPPORTED.
+    // The tuning build (-DLHPC_TUNING_ENV) compiles every measured tile.
+    const S7Args a{u, out, nz, ny, nx, g, c0, c1, zb, ze, zc, s};
+    int st = LHPC_ERR_UNSUPPORTED;
     if (buf4) {  // x4 ring: non-temporal dwordx4 stores ("plain": plain)
-      const int m4 = stm == LHPC_STORE_PLAIN ? 5 : 6;
-#define LHPC_S74_P(RY, NJ, M, P)                                                                        \
-  do {                                                                                                  \
-    const int64_t ntx = (nx + NJ * kWave - 1) / (NJ * kWave), nty = (ny + 4 * RY - 1) / (4 * RY),          \
-                  ntz = (ze - zb + zc - 1) / zc;                                                        \
-    if (share)                                                                                          \
-      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 2, P, true>), dim3(static_cast<unsigned>(ntx * nty * ntz)), \
-                         dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
-    else if (pf == 2)                                                                                   \
-      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 2, P>), dim3(static_cast<unsigned>(ntx * nty * ntz)), \
-                         dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
-    else if (pf == 3)                                                                                   \
-      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 3, P>), dim3(static_cast<unsigned>(ntx * nty * ntz)), \
-                         dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
-    else                                                                                                \
-      hipLaunchKernelGGL((k_stencil7_buf4<RY, NJ, M, 1, P>), dim3(static_cast<unsigned>(ntx * nty * ntz)), \
-                         dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
-  } while (0)
-#define LHPC_S74_M(RY, NJ, M)              \
-  do {                                     \
-    if (part) LHPC_S74_P(RY, NJ, M, true); \
-    else LHPC_S74_P(RY, NJ, M, false);     \
-  } while (0)
-#define LHPC_S74(RY, NJ)                            \
-  do {                                              \
-    if (m4 == 5) LHPC_S74_M(RY, NJ, 5);             \
-    else LHPC_S74_M(RY, NJ, 6);                     \
-  } while (0)
-      if (ry == 1 && nj == 8) LHPC_S74(1, 8);
-      else if (ry == 4 && nj == 8) LHPC_S74(4, 8);
-      else if (ry == 2 && nj == 4) LHPC_S74(2, 4);
-      else if (ry == 1 && nj == 4) LHPC_S74(1, 4);
-      else if (ry == 4 && nj == 4) LHPC_S74(4, 4);
-      else LHPC_S74(2, 8);
-#undef LHPC_S74
-#undef LHPC_S74_M
-#undef LHPC_S74_P
-      return check_launch(s);
+      const bool m5 = stm == LHPC_STORE_PLAIN;
+      if (ry == 1 && nj == 8) st = s74_store<1, 8>(a, m5, part, share, pf);
+      else if (ry == 1 && nj == 4) st = s74_store<1, 4>(a, m5, part, share, pf);
+      else if (ry == 2 && nj == 4) st = s74_store<2, 4>(a, m5, part, share, pf);
+#ifdef LHPC_TUNING_ENV
+      else if (ry == 4 && nj == 8) st = s74_store<4, 8>(a, m5, part, share, pf);
+      else if (ry == 4 && nj == 4) st = s74_store<4, 4>(a, m5, part, share, pf);
+      else st = s74_store<2, 8>(a, m5, part, share, pf);
+#endif
+    } else {
+      if (ry == 1 && nj == 8) st = s7b_store<1, 8>(a, store_mode, pf);
+      else if (ry == 1 && nj == 4) st = s7b_store<1, 4>(a, store_mode, pf);
+#ifdef LHPC_TUNING_ENV
+      else if (ry == 4 && nj == 8) st = s7b_store<4, 8>(a, store_mode, pf);
+      else if (ry == 2 && nj == 4) st = s7b_store<2, 4>(a, store_mode, pf);
+      else if (ry == 4 && nj == 4) st = s7b_store<4, 4>(a, store_mode, pf);
+      else st = s7b_store<2, 8>(a, store_mode, pf);
+#endif
     }
-#define LHPC_S7B_M(RY, NJ, M)                                                                         \
-  do {                                                                                                \
-    const int64_t ntx = (nx + NJ * kWave - 1) / (NJ * kWave), nty = (ny + 4 * RY - 1) / (4 * RY),        \
-                  ntz = (ze - zb + zc - 1) / zc;                                                      \
-    if (pf == 2)                                                                                      \
-      hipLaunchKernelGGL((k_stencil7_buf<RY, NJ, M, 2>), dim3(static_cast<unsigned>(ntx * nty * ntz)),  \
-                         dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
-    else if (pf == 3)                                                                                 \
-      hipLaunchKernelGGL((k_stencil7_buf<RY, NJ, M, 3>), dim3(static_cast<unsigned>(ntx * nty * ntz)),  \
-                         dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
-    else                                                                                              \
-    hipLaunchKernelGGL((k_stencil7_buf<RY, NJ, M>), dim3(static_cast<unsigned>(ntx * nty * ntz)),       \
-                       dim3(256), 0, s, u, out, nz, ny, nx, g, c0, c1, zb, ze, ntx, nty, ntz, int64_t{zc}); \
-  } while (0)
-#define LHPC_S7B(RY, NJ)                                 \
-  do {                                                   \
-    if (store_mode == 1) LHPC_S7B_M(RY, NJ, 1);          \
-    else if (store_mode == 4) LHPC_S7B_M(RY, NJ, 4);     \
-    else LHPC_S7B_M(RY, NJ, 0);                          \
-  } while (0)
-    if (ry == 1 && nj == 8) LHPC_S7B(1, 8);
-    else if (ry == 4 && nj == 8) LHPC_S7B(4, 8);
-    else if (ry == 1 && nj == 4) LHPC_S7B(1, 4);
-    else if (ry == 2 && nj == 4) LHPC_S7B(2, 4);
-    else if (ry == 4 && nj == 4) LHPC_S7B(4, 4);
-    else LHPC_S7B(2, 8);
-#undef LHPC_S7B
-#undef LHPC_S7B_M
+    if (st != LHPC_OK) return st;
     return check_launch(s);
   }
   const int64_t ntx = (nx + kS7X - 1) / kS7X, nty = (ny + kS7Y - 1) / kS7Y, ntz = (ze - zb + kS7Z - 1) / kS7Z;

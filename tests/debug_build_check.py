@@ -44,5 +44,26 @@ for name in ("adaptive", "rowgroup", "xslice"):
     with L.SpMVPlan(g["row_ptr"], g["col_idx"], g["val"], int(g["n_cols"]), flags=FAMILIES[name]) as plan:
         y = plan(torch.from_numpy(g["x"]).to(dev)).cpu().numpy()
     assert np.array_equal(y, g["y_exact"].astype(np.float32)), name
+# CG error path: a solve whose 4th iteration body fails after
+# enqueueing its work returns LHPC_ERR_INTERNAL and frees the plan only once
+# its stream has drained; a second solve on another stream then equals a
+# clean solve bit for bit (SELL: fused loop; spmv_no_sell: ADAPTIVE loop)
+rp, col, val = S.laplacian_2d(150, 130, dtype=np.float64)
+n = rp.size - 1
+b = torch.from_numpy(np.random.default_rng(21).uniform(-1, 1, n)).to(dev)
+for opts in (None, {"spmv_no_sell": 1}):
+    with L.SpMVPlan(rp, col, val, n, options=opts) as plan:
+        s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        x_ref, it_ref, r_ref = L.cg(plan, b, tol=1e-10, max_iter=200, check_every=8, stream=s1)
+        s1.synchronize()
+        L.lib.lhpc_debug_cg_fail_at(3)
+        try:
+            L.cg(plan, b, tol=1e-10, max_iter=200, check_every=8, stream=s1)
+            raise AssertionError("the injected CG fault did not surface")
+        except L.LhpcError as e:
+            assert e.status == -6, e.status
+        x2, it2, r2 = L.cg(plan, b, tol=1e-10, max_iter=200, check_every=8, stream=s2)
+        s2.synchronize()
+        assert torch.equal(x2, x_ref) and (it2, r2) == (it_ref, r_ref), (opts, it2, it_ref)
 torch.cuda.synchronize()
 print("DEBUG BUILD OK")

@@ -63,3 +63,28 @@ def test_spmv_options_forms():
     assert bench.parse_options(None) is None
     assert bench.parse_options('{"xtile_steps": 4}') == {"xtile_steps": 4}
     assert bench.parse_options("xtile_steps=4,xtile_piece=150000") == {"xtile_steps": 4, "xtile_piece": 150000}
+
+
+def test_exchange_model_arithmetic():
+    """bench.py's `exchange.model` (tools/step_model.exchange_model): the
+    measured receive / per-link rate from the exchange-only time, and the
+    step the model predicts at that rate beside the measured step."""
+    import step_model as M
+    # W = 2, fp32 n = 10M: 20 MB into each rank; exchange alone 0.5 ms → 40 GB/s over one link
+    r = M.exchange_model(2, 1, False, 10_000_000, 4, 0.2, 0.3, 0.5, 0.9)
+    assert r["bytes_in_per_step"] == 20e6
+    assert abs(r["recv_GBps"] - 40.0) < 1e-9 and abs(r["link_GBps"] - 40.0) < 1e-9
+    # K = 1 plain: stage + reduce, then the whole exchange, serial → 0.2 + 0.1 + 0.5
+    assert abs(r["predicted_step_ms"] - 0.8) < 1e-9
+    assert abs(r["measured_over_predicted"] - 0.9 / 0.8) < 1e-9
+    # at 50 GB/s per link the exchange takes 0.4 ms
+    r = M.exchange_model(2, 1, False, 10_000_000, 4, 0.2, 0.3, 0.5, 0.9, assumed_link_GBps=(50.0,))
+    assert abs(r["at_assumed_link_rates"][0]["step_ms"] - 0.7) < 1e-9
+    # W = 8: 7/8 of y arrives over 7 links; K = 4 chained overlaps the exchange with the next stage
+    r = M.exchange_model(8, 4, True, 10_000_000, 8, 0.05, 0.15, 0.2, 0.2)
+    assert abs(r["bytes_in_per_step"] - 70e6) < 1e-3
+    assert abs(r["link_GBps"] - 70e6 / 0.2e-3 / 1e9 / 7) < 1e-9
+    assert r["mode"] == "chained" and 0.15 <= r["predicted_step_ms"] <= 0.05 + 0.15 + 0.2
+    assert abs(r["predicted_step_ms"] - M.simulate(0.05, 0.10, 0.2, 4, True)) < 1e-12
+    # one rank: no exchange, no rate
+    assert "link_GBps" not in M.exchange_model(1, 1, False, 100, 4, 0.1, 0.2, 0.0, 0.2)

@@ -49,6 +49,11 @@ def _run(lhpc, gpu, rp, col, val, n_cols, x, w, flags=0, options=None):
 CASES = [  # (name, n, maxlen, minlen)
     ("n1", 1, 3, 1), ("n63", 63, 8, 0), ("n65", 65, 8, 8), ("n257", 257, 5, 0),
     ("n300001_len0to8", 300_001, 8, 0), ("n100000_len8", 100_000, 8, 8), ("empty_rows", 1000, 2, 0),
+    # a last block of ≤ 128 rows whose 4th ADAPTIVE wave holds rows (n % 256 in
+    # {4, 7-8, 13-16, 25-32, 49-64, 97-128}): the fused dot must still fold the
+    # waves as ADAPTIVE does
+    ("n8", 8, 8, 0), ("n50", 50, 8, 0), ("n64", 64, 8, 0), ("n100", 100, 8, 0), ("n120", 120, 8, 0),
+    ("n2098", 2098, 8, 0),
 ]
 
 
@@ -169,14 +174,16 @@ def test_sell_host_buffers_and_device_input(lhpc, gpu):
 
 @pytest.mark.parametrize("max_iter,check_every", [(5000, 8), (5000, 1), (13, 4), (7, 1), (1, 1)])
 @pytest.mark.parametrize("dt", [np.float64, np.float32], ids=["f64", "f32"])
-def test_cg_sell_matches_adaptive(lhpc, gpu, dt, max_iter, check_every):
+@pytest.mark.parametrize("grid", [(150, 130), (72, 271)], ids=["n19500", "n19512"])  # n % 256 = 44 / 56
+def test_cg_sell_matches_adaptive(lhpc, gpu, dt, max_iter, check_every, grid):
     """lhpc_cg_solve on a SELL plan — each iteration's x / p update fused
     into the next iteration's SpMV (sell_cg_step), graph blocks on a side
     stream — and on an ADAPTIVE plan of the same Laplacian (the unfused
     k_cg_xp loop): same iterations, residual and x bit for bit, converged or
-    stopped at max_iter (the pending x update of the last iteration)."""
+    stopped at max_iter (the pending x update of the last iteration).  n % 256
+    = 56 puts rows in the last block's 4th ADAPTIVE wave."""
     import torch
-    rp, col, val = S.laplacian_2d(150, 130, dtype=dt, shift=0.0 if dt == np.float64 else 0.5)
+    rp, col, val = S.laplacian_2d(*grid, dtype=dt, shift=0.0 if dt == np.float64 else 0.5)
     n = rp.size - 1
     b = _dev(gpu, np.random.default_rng(21).uniform(-1, 1, n).astype(dt))
     tol = 1e-10 if dt == np.float64 else 1e-5

@@ -52,6 +52,28 @@ def test_sort_u32_distributions(lhpc, gpu, kind):
     assert np.array_equal(_u32_view(t), S.sort_oracle(keys))
 
 
+@pytest.mark.parametrize("off", [1, 2, 3])
+@pytest.mark.parametrize("n", [100_003, (1 << 20) + 7])
+def test_sort_u32_offset_pointer(lhpc, gpu, n, off):
+    """Keys whose device pointer is 4-B but not 16-B aligned (a slice t[off:]):
+    the upsweep's 16-B loads are used only on 16-B aligned keys (ADVICE r5);
+    the keys around the slice stay untouched."""
+    import torch
+    keys = _keys(n + off + 5, "uniform", n + off)
+    t = _dev(gpu, keys.view(np.int32))
+    sl = t[off:off + n]
+    assert sl.data_ptr() % 16 != 0
+    vals = torch.arange(n, dtype=torch.int32, device=gpu)
+    lhpc.radix_sort_pairs(sl, vals, 0, 32)
+    wk, wv = S.sort_oracle(keys[off:off + n], np.arange(n, dtype=np.uint32), 0, 32)
+    got = _u32_view(t)
+    assert np.array_equal(got[off:off + n], wk) and np.array_equal(_u32_view(vals), wv)
+    assert np.array_equal(got[:off], keys[:off]) and np.array_equal(got[off + n:], keys[off + n:])
+    t2 = _dev(gpu, keys.view(np.int32))
+    lhpc.radix_sort(t2[off:off + n])
+    assert np.array_equal(_u32_view(t2)[off:off + n], np.sort(keys[off:off + n]))
+
+
 def test_sort_u32_host_path(lhpc, gpu):
     keys = _keys(77_777, "uniform", 5)
     got = lhpc.radix_sort(keys.copy())

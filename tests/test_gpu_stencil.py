@@ -115,8 +115,19 @@ def test_stencil7_c5_size(lhpc, gpu):
     assert np.array_equal(got, want)
 
 
-S7_IMPLS = ["buf", "buf:2,8,0,2", "buf:4,4,128,3", "buf:2,8,5,3", "buf:2,8,32", "buf:1,8,16", "buf:1,8,32", "buf:2,4,32", "buf:4,4,32", "buf:1,4,32", "buf:4,8,32",
-            "buf:2,8,4", "simple"]
+S7_IMPLS = ["buf", "buf:1,8,0,2", "buf:1,4,128,3", "buf:1,8,5,3", "buf:1,8,16", "buf:1,8,32", "buf:1,4,32",
+            "buf:1,8,4", "simple",
+            # tuning-build tiles (their kernels spill SGPRs): LHPC_ERR_UNSUPPORTED in the product library
+            "buf:2,8,0,2", "buf:4,4,128,3", "buf:2,8,32", "buf:2,4,32", "buf:4,8,32"]
+
+
+def _s7_in_product(name, cfg):
+    """The tiles the product library compiles (lhpc_stencil.hip s7_launch):
+    one row per wave, or the x4 ring's LDS-shared 2 rows × 4 blocks."""
+    if name == "simple" or not cfg:
+        return True
+    ry, nj = (int(v) for v in cfg.split(",")[:2])
+    return nj in (4, 8) and (ry == 1 or (name == "buf4lds" and ry == 2 and nj == 4))
 
 
 def _s7_options(lhpc, name, cfg, store):
@@ -141,6 +152,12 @@ def test_stencil7_every_impl(lhpc, gpu, impl, store):
     multiples of the row / z-chunk tiles, ghost widths 1 and 2."""
     name, _, cfg = impl.partition(":")
     opts = _s7_options(lhpc, name, cfg, store)
+    if not _s7_in_product(name, cfg):
+        with pytest.raises(lhpc.LhpcError) as e:
+            u = np.zeros(5 * 6 * 7, np.float32)
+            lhpc.stencil7(_dev(gpu, u), _dev(gpu, u.copy()), 3, 4, 5, 1, -6.0, 1.0, options=opts)
+        assert e.value.status == -5
+        return
     for (nz, ny, nx, g) in ((37, 45, 1100, 1), (9, 19, 130, 2), (3, 2, 1, 1)):
         shape = (nz + 2 * g, ny + 2 * g, nx + 2 * g)
         u = S.random_padded(shape, seed=nz * 7 + nx + g, zero_ghost=False).reshape(-1)
@@ -150,7 +167,7 @@ def test_stencil7_every_impl(lhpc, gpu, impl, store):
         assert np.array_equal(got, want), (impl, store, nz, ny, nx, g)
 
 
-S7_BUF4 = ["2,8,0", "2,8,5", "1,8,16", "1,8,0", "4,8,32", "2,4,7", "4,4,32"]
+S7_BUF4 = ["1,8,16", "1,8,0", "1,4,0", "1,8,0,3", "1,4,7,1", "2,4,7", "2,4,0", "2,8,0", "4,8,32", "4,4,32"]
 
 
 @pytest.mark.parametrize("cfg", S7_BUF4)
@@ -165,6 +182,12 @@ def test_stencil7_buf4(lhpc, gpu, cfg, store, impl):
     last x tile is partial (dword loads and stores past nx, every lane phase
     of the last x4: nx % 4 = 0..3, nx < 4)."""
     opts = _s7_options(lhpc, impl, cfg, store)
+    if not _s7_in_product(impl, cfg):  # tuning-build tile: refused by the product library
+        with pytest.raises(lhpc.LhpcError) as e:
+            u = np.zeros(5 * 6 * 7, np.float32)
+            lhpc.stencil7(_dev(gpu, u), _dev(gpu, u.copy()), 3, 4, 5, 1, -6.0, 1.0, options=opts)
+        assert e.value.status == -5
+        return
     for (nz, ny, nx, g) in ((37, 45, 1024, 1), (9, 19, 512, 2), (3, 2, 1536, 3), (5, 9, 512, 1),
                             (37, 45, 1100, 1), (9, 19, 130, 2), (3, 2, 1, 1), (5, 7, 517, 3), (2, 3, 1541, 1),
                             (4, 5, 768, 2), (3, 4, 258, 1), (6, 3, 3, 2)):

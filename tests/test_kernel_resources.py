@@ -9,6 +9,7 @@ import os
 import re
 import struct
 import subprocess
+import sys
 import tempfile
 
 import pytest
@@ -112,3 +113,64 @@ def test_hot_kernel_register_budgets(ks):
     assert len(sell) == 2 and all(r["vgpr_count"] <= 64 for r in sell.values()), sell
     s7 = pick(r"k_stencil7_buf4ILi2ELi4ELi[56]ELi2ELb[01]ELb1E")
     assert s7 and all(r["vgpr_count"] <= 128 for r in s7.values()), {n: r["vgpr_count"] for n, r in s7.items()}
+
+
+def test_no_sgpr_spills_in_product(ks):
+    """Round 6: the product library holds only kernels
+    that keep every register in registers — the stencil tiles whose kernels
+    spilled SGPRs (2- and 4-row dword rings, 4-row and private-ring 2-row x4
+    tiles, prefetch depth 3 at 2 rows) are compiled in the tuning build only
+    (-DLHPC_TUNING_ENV); the product refuses them with LHPC_ERR_UNSUPPORTED."""
+    bad = {n: r["sgpr_spill_count"] for n, r in ks.items() if r["sgpr_spill_count"]}
+    assert not bad, f"{len(bad)} kernels spill SGPRs: {sorted(bad)[:4]}"
+    s7 = [n for n in ks if "k_stencil7" in n]
+    assert 0 < len(s7) <= 64, len(s7)
+
+
+def test_product_build_tag():
+    """lhpc_build_flags() is 0 for the product library and has the debug bit
+    for the debug build."""
+    import ctypes
+    prod = ctypes.CDLL(LIB)
+    assert prod.lhpc_build_flags() == 0
+    dbg = os.path.join(ROOT, "libhpc_amd", "_lib_debug", "liblhpc.so")
+    if os.path.exists(dbg):
+        assert ctypes.CDLL(dbg).lhpc_build_flags() & 2
+
+
+def _gpurun_ignored(rel, patterns):
+    rel = "./" + rel
+    return any(rel == p or rel.startswith(p.rstrip("/") + "/") for p in patterns if p.startswith("./"))
+
+
+def test_no_probe_build_travels():
+    """Of the lhpc libraries in the tree, none that goes to the GPU box is a
+    timing-only probe build (lhpc_build_flags & LHPC_BUILD_PROBE), and the
+    only one with flags 0 is the product library.
+    Tuning and probe build directories are listed in .gpurunignore."""
+    import ctypes
+    pats = [ln.strip() for ln in open(os.path.join(ROOT, ".gpurunignore")) if ln.strip() and not ln.startswith("#")]
+    travel = {}
+    for d, _, files in os.walk(os.path.join(ROOT, "libhpc_amd")):
+        for f in files:
+            if f.startswith("liblhpc") and f.endswith(".so") and "probe" not in f:
+                rel = os.path.relpath(os.path.join(d, f), ROOT)
+                if not _gpurun_ignored(rel, pats):
+                    travel[rel] = ctypes.CDLL(os.path.join(ROOT, rel)).lhpc_build_flags()
+    assert not {r: f for r, f in travel.items() if f & 4}, travel
+    assert [r for r, f in travel.items() if f == 0] == ["libhpc_amd/_lib/liblhpc.so"], travel
+    assert _gpurun_ignored("libhpc_amd/_lib_tuning/liblhpc.so", pats)
+
+
+def test_loader_refuses_probe_build(tmp_path):
+    """LHPC_LIB_PATH naming a timing-only probe build (lhpc_build_flags has
+    LHPC_BUILD_PROBE) fails the import unless LHPC_ALLOW_PROBE_BUILD=1."""
+    src = tmp_path / "probe.c"
+    src.write_text("int lhpc_build_flags(void) { return 4; }\n")
+    so = tmp_path / "liblhpc.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", str(src), "-o", str(so)], check=True)
+    code = "import libhpc_amd"
+    env = dict(os.environ, LHPC_LIB_PATH=str(so))
+    env.pop("LHPC_ALLOW_PROBE_BUILD", None)
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "timing-only probe build" in r.stderr, r.stderr[-2000:]

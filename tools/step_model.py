@@ -56,6 +56,31 @@ def simulate(Ts, Tr, Tx, K, chained, steps=30):
     return sum(tail) / len(tail)
 
 
+def exchange_model(world, K, chained, n, tsz, stage_ms, local_ms, exchange_only_ms, measured_step_ms,
+                   assumed_link_GBps=(48.0, 64.0, 76.5)):
+    """The model above evaluated at a bench run's own measurements (bench.py
+    --gpus N > 1, the `exchange.model` object): the exchange-only time gives
+    the measured receive rate, and per link (the model's direct-peer form:
+    the W − 1 peers' blocks arrive over W − 1 links at once); the step that
+    rate predicts (stage_ms, local_ms − stage_ms and exchange_only_ms as T_s,
+    T_r and T_x) stands beside the measured step, with the steps the assumed
+    link rates of DESIGN.md §6 would give."""
+    bytes_in = (world - 1) / world * n * tsz
+    Tr = max(local_ms - stage_ms, 0.0)
+    out = {"world": world, "K": K, "mode": "chained" if chained else "plain", "bytes_in_per_step": bytes_in,
+           "stage_ms": stage_ms, "reduce_ms": Tr, "exchange_only_ms": exchange_only_ms}
+    if world < 2 or exchange_only_ms <= 0.0:
+        return out
+    recv = bytes_in / (exchange_only_ms * 1e-3) / 1e9
+    pred = simulate(stage_ms, Tr, exchange_only_ms, K, chained)
+    out.update({"recv_GBps": recv, "link_GBps": recv / (world - 1), "predicted_step_ms": pred,
+                "measured_step_ms": measured_step_ms, "measured_over_predicted": measured_step_ms / pred,
+                "at_assumed_link_rates": [
+                    {"link_GBps": b, "step_ms": simulate(stage_ms, Tr, bytes_in / ((world - 1) * b * 1e9) * 1e3, K,
+                                                         chained)} for b in assumed_link_GBps]})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--data", default=os.path.join(ROOT, "profiles", "r04", "rank_model.jsonl"))
