@@ -218,6 +218,12 @@ typedef struct lhpc_options {
   /* 1: short rows with x locality stay on ADAPTIVE instead of SELL (rows of
    * ≤ 8 nonzeros whose padded slices stream no more bytes than CSR)        */
   int32_t spmv_no_sell;
+  /* XTILE cache-sized ranges (no user splits, iperm reduce): 0 (auto) one
+   * range-sized xg ring reused by every range, so a range's gather overwrites
+   * lines still in the Infinity Cache instead of evicting dirty ones to HBM;
+   * 1: one xg slot per stream entry (the round-5 layout).  Ring plans refuse
+   * lhpc_spmv_stage / lhpc_spmv_range (LHPC_ERR_UNSUPPORTED).               */
+  int32_t xtile_ring;
 } lhpc_options;
 void lhpc_options_init(lhpc_options *opts);
 

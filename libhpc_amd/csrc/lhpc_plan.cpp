@@ -422,16 +422,91 @@ int xtile_transpose_runs(const XtileHost &o, const void *val, size_t tsz, int ru
 }
 
 void xtile_segment_table(const XtileHost &o, std::vector<uint32_t> &seg, std::vector<int32_t> &hi) {
-  const int64_t S = o.S, C = o.n_chunks, H = (C + kXtSegHi - 1) / kXtSegHi;
+  const int64_t S = o.S, C = o.n_chunks;
+  if (o.rdelta.empty()) {
+    const int64_t H = (C + kXtSegHi - 1) / kXtSegHi;
+    seg.assign(static_cast<size_t>(std::max<int64_t>(C, 1) * S), 0u);
+    hi.assign(static_cast<size_t>(std::max<int64_t>(H, 1) * S), 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t c = 0; c < C; ++c) {
+      const int32_t *a = o.segoff.data() + c * S, *b = a + S, *h = o.segoff.data() + (c / kXtSegHi) * kXtSegHi * S;
+      if (c % kXtSegHi == 0) std::memcpy(hi.data() + (c / kXtSegHi) * S, a, sizeof(int32_t) * static_cast<size_t>(S));
+      for (int64_t s = 0; s < S; ++s)
+        seg[static_cast<size_t>(c * S + s)] =
+            static_cast<uint32_t>(a[s] - h[s]) | (static_cast<uint32_t>(b[s] - a[s]) << 16);
+    }
+    return;
+  }
+  // ring plans: starts in ring positions (stream position + rdelta of the
+  // chunk's range), hi groups of kXtSegHi chunks restarting at every range
+  // (a group straddling two ranges would mix two rings' positions)
+  const int64_t K = static_cast<int64_t>(o.rchunk.size()) - 1;
+  std::vector<int64_t> g0;  // first chunk of each hi group, then C (group g of range k: row hrow[k] + …)
+  std::vector<int32_t> gk;  // its range
+  for (int64_t k = 0; k < K; ++k) {
+    for (int64_t c = o.rchunk[k]; c < o.rchunk[k + 1]; c += kXtSegHi) {
+      g0.push_back(c);
+      gk.push_back(static_cast<int32_t>(k));
+    }
+  }
+  g0.push_back(C);
+  const int64_t H = static_cast<int64_t>(g0.size()) - 1;
   seg.assign(static_cast<size_t>(std::max<int64_t>(C, 1) * S), 0u);
   hi.assign(static_cast<size_t>(std::max<int64_t>(H, 1) * S), 0);
 #pragma omp parallel for schedule(static)
-  for (int64_t c = 0; c < C; ++c) {
-    const int32_t *a = o.segoff.data() + c * S, *b = a + S, *h = o.segoff.data() + (c / kXtSegHi) * kXtSegHi * S;
-    if (c % kXtSegHi == 0) std::memcpy(hi.data() + (c / kXtSegHi) * S, a, sizeof(int32_t) * static_cast<size_t>(S));
-    for (int64_t s = 0; s < S; ++s)
-      seg[static_cast<size_t>(c * S + s)] =
-          static_cast<uint32_t>(a[s] - h[s]) | (static_cast<uint32_t>(b[s] - a[s]) << 16);
+  for (int64_t g = 0; g < H; ++g) {
+    const int32_t *d = o.rdelta.data() + static_cast<int64_t>(gk[g]) * S;
+    const int32_t *h = o.segoff.data() + g0[g] * S;
+    for (int64_t s = 0; s < S; ++s) hi[static_cast<size_t>(g * S + s)] = h[s] + d[s];
+    const int64_t c1 = std::min(g0[g] + kXtSegHi, o.rchunk[gk[g] + 1]);
+    for (int64_t c = g0[g]; c < c1; ++c) {
+      const int32_t *a = o.segoff.data() + c * S, *b = a + S;
+      for (int64_t s = 0; s < S; ++s)
+        seg[static_cast<size_t>(c * S + s)] =
+            static_cast<uint32_t>(a[s] - h[s]) | (static_cast<uint32_t>(b[s] - a[s]) << 16);
+    }
+  }
+}
+
+void xtile_ring_pieces(XtileHost &o, int64_t piece_nnz, std::vector<int64_t> &rpc) {
+  const int64_t S = o.S, K = static_cast<int64_t>(o.rchunk.size()) - 1;
+  const int64_t pn = std::max<int64_t>(8, (piece_nnz + 7) / 8 * 8);
+  auto up8 = [](int64_t v) { return (v + 7) / 8 * 8; };
+  auto dn8 = [](int64_t v) { return v / 8 * 8; };
+  o.pieces.clear();
+  o.pext.clear();
+  o.rdelta.assign(static_cast<size_t>(K * S), 0);
+  o.ring_len = 0;
+  o.hrow.assign(1, 0);  // hi groups of kXtSegHi chunks per range (xtile_segment_table)
+  for (int64_t k = 0; k + 1 < K; ++k)
+    o.hrow.push_back(o.hrow.back() + (o.rchunk[k + 1] - o.rchunk[k] + kXtSegHi - 1) / kXtSegHi);
+  rpc.assign(1, 0);
+  for (int64_t k = 0; k < K; ++k) {
+    int64_t cur = 0;  // ring cursor (a multiple of 8)
+    for (int64_t s = 0; s < S; ++s) {
+      const int64_t a = o.segoff[o.rchunk[k] * S + s], b = o.segoff[o.rchunk[k + 1] * S + s];
+      if (b <= a) continue;
+      const int64_t d = cur - dn8(a);  // ring position of stream position g: g + d
+      o.rdelta[static_cast<size_t>(k * S + s)] = static_cast<int32_t>(d);
+      cur += up8(b) - dn8(a);
+      // whole groups [ia, ib) in ≈ piece_nnz pieces; the partial groups at a
+      // and b ride on the first / last piece as flagged extra groups
+      const int64_t ia = up8(a), ib = dn8(b);
+      const bool pre = a % 8 != 0, suf = b % 8 != 0 && ib >= ia;
+      if (ib <= ia) {  // no whole group: one piece holding the group(s) around a (and b)
+        o.pieces.insert(o.pieces.end(), {static_cast<int32_t>(ia), static_cast<int32_t>(ia), static_cast<int32_t>(s)});
+        o.pext.insert(o.pext.end(), {static_cast<int32_t>(d), (pre ? 1 : 0) | (suf ? 2 : 0)});
+        continue;
+      }
+      const int64_t P = (ib - ia + pn - 1) / pn, step = up8((ib - ia + P - 1) / P);
+      for (int64_t g = ia; g < ib; g += step) {
+        const int64_t e = std::min(ib, g + step);
+        o.pieces.insert(o.pieces.end(), {static_cast<int32_t>(g), static_cast<int32_t>(e), static_cast<int32_t>(s)});
+        o.pext.insert(o.pext.end(), {static_cast<int32_t>(d), (g == ia && pre ? 1 : 0) | (e == ib && suf ? 2 : 0)});
+      }
+    }
+    o.ring_len = std::max(o.ring_len, cur);
+    rpc.push_back(static_cast<int64_t>(o.pieces.size() / 3));
   }
 }
 

@@ -88,11 +88,23 @@ struct XtileHost {
   std::unique_ptr<uint16_t[]> iperm;
   bool iperm_mode = false;           // which reduce index stream the plan carries
   int slot_bytes = 4;
+  // xg ring (xtile_ring_pieces; cache-sized ranges): one range-sized xg buffer
+  // reused by every range.  Range k's part of tile s (sub-run (k, s) =
+  // [segoff[rchunk[k]][s], segoff[rchunk[k+1]][s]) of the tile-major stream)
+  // lives at stream position + rdelta[k·S + s] in the ring (a multiple of 8);
+  // ring_len = the longest range's ring.  pext: 2 int32 per piece {delta,
+  // flags}: bit 0 also gathers the 8-entry group before the piece, bit 1 the
+  // group at its end (the groups two ranges share, unpermuted).  hrow[k]:
+  // range k's first segment-table hi row (hi groups restart at each range).
+  std::vector<int32_t> rdelta, pext;
+  std::vector<int64_t> hrow;
+  int64_t ring_len = 0;
 };
 
 // Device form of the segment table (the reduce reads one 4-B word per tile
 // and chunk instead of two starts): seg[c·S + s] = lo | len << 16 with
-// start(c, s) = hi[⌊c / kXtSegHi⌋·S + s] + lo and len = start(c+1, s) −
+// start(c, s) = hi[⌊c / kXtSegHi⌋·S + s] + lo (ring plans: ring starts,
+// hi row hrow[k] + ⌊(c − rchunk[k]) / kXtSegHi⌋ for c in range k) and len = start(c+1, s) −
 // start(c, s) ≤ M; lo ≤ (kXtSegHi − 1)·M < 2^16 for M ≤ 8192.  Size ≈ 4.6 B
 // per (chunk, tile): 21 MB for C2, 1.3 GB at n = 80M (where a dense int32
 // table of starts hit the old 2.7e8-entry limit).
@@ -173,6 +185,13 @@ void xtile_permute_gather_blocks(XtileHost &o, int vw);
 // gathered entry depends only on its position), cut into ≈ piece_nnz pieces;
 // rpc[k] = first piece of range k.
 void xtile_range_pieces(XtileHost &o, int64_t piece_nnz, std::vector<int64_t> &rpc);
+// The same for an xg ring (round 6): sub-run (k, s) of [a, b) gets pieces
+// over the whole groups [⌈a⌉₈, ⌊b⌋₈) and, when a (b) is not a multiple of 8,
+// the group around it as a flagged prefix (suffix) of its first (last) piece
+// — so each range gathers every entry it reads into its own ring, and no
+// col16 group is permuted by two pieces.  Ring layout: sub-runs (k, s) in
+// tile order, [⌊a⌋₈, ⌈b⌉₈) at an 8-aligned cursor; rdelta, pext, ring_len.
+void xtile_ring_pieces(XtileHost &o, int64_t piece_nnz, std::vector<int64_t> &rpc);
 
 // LDS slot of chunk position i in the XTILE reduce (lhpc_spmv_xtile.hip
 // xt_slot): run t = i/run holds run = 64/elem_bytes elements (64 B) at

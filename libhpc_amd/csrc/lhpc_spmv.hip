@@ -755,7 +755,7 @@ extern "C" int lhpc_spmv_plan_create_split(lhpc_spmv_plan **out, int dtype, int6
 extern "C" int lhpc_spmv_stage(const lhpc_spmv_plan *p, const void *x, void *stream) {
   try {
     if (!p || (p->n_cols > 0 && !x)) return LHPC_ERR_INVALID_ARG;
-    if (p->xt_srow.empty()) return LHPC_ERR_UNSUPPORTED;
+    if (p->xt_srow.empty() || p->xt_ring) return LHPC_ERR_UNSUPPORTED;  // a ring holds one range's xg
     RocTxRange rx("lhpc_spmv_stage");
     LHPC_HIP_TRY(hipSetDevice(p->device));
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -767,6 +767,7 @@ extern "C" int lhpc_spmv_range(const lhpc_spmv_plan *p, int k, void *y_range, vo
   try {
     if (!p || p->xt_srow.empty() || k < 0 || k + 2 > static_cast<int>(p->xt_srow.size()))
       return LHPC_ERR_INVALID_ARG;
+    if (p->xt_ring) return LHPC_ERR_UNSUPPORTED;
     if (p->xt_srow[k + 1] > p->xt_srow[k] && !y_range) return LHPC_ERR_INVALID_ARG;
     RocTxRange rx("lhpc_spmv_range");
     LHPC_HIP_TRY(hipSetDevice(p->device));
@@ -879,7 +880,7 @@ extern "C" int lhpc_spmv_plan_destroy(lhpc_spmv_plan *p) {
                     static_cast<void *>(p->d_dpart), static_cast<void *>(p->d_cdesc), static_cast<void *>(p->d_cr),
                     static_cast<void *>(p->d_seghi), static_cast<void *>(p->d_seg), static_cast<void *>(p->d_pieces), static_cast<void *>(p->d_cont),
                     static_cast<void *>(p->d_col16), static_cast<void *>(p->d_perm), p->d_xg,
-                    static_cast<void *>(p->d_pieces_cp),
+                    static_cast<void *>(p->d_pieces_cp), static_cast<void *>(p->d_pext),
                     static_cast<void *>(p->d_carry)})
       if (q) (void)hipFree(q);
     if (p->h_scalars) (void)hipHostFree(p->h_scalars);

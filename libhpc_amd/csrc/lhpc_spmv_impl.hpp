@@ -69,6 +69,14 @@ struct lhpc_spmv_plan {
   int xt_p = 1;  // reduce: 1 perm scatter, 3 iperm gather (DESIGN.md §4 XTILE)
   int xt_al = 0;  // aligned segments: 16-B units (lhpc_options.xtile_align)
   void *d_xg = nullptr;
+  // xg ring (cache-sized ranges without user splits, lhpc_plan.hpp
+  // xtile_ring_pieces): d_xg holds xt_ring_len + 2 entries reused by every
+  // range; per piece {ring delta, flags} in d_pext; range k's segment-table hi
+  // rows start at xt_hrow[k]
+  int xt_ring = 0;
+  int64_t xt_ring_len = 0;
+  int32_t *d_pext = nullptr;
+  std::vector<int64_t> xt_hrow;
   double *d_carry = nullptr;
   // column parts (xtile_column_parts): the gather pieces reordered so that
   // part j = pieces [xt_cpf[j], xt_cpf[j+1]) of d_pieces_cp reads x only

@@ -44,10 +44,16 @@ template <> struct XtTile<double> { static constexpr int W = 20480; };  // 160 K
 #else
 #define LHPC_GVAL_PARAM
 #endif
+// pext (xg ring plans, lhpc_plan.hpp xtile_ring_pieces): {delta, flags} per
+// piece — every xg store lands at stream position + delta, and thread 0 /
+// thread 1 also gather the group before the piece / at its end (flags bit 0
+// / 1: an 8-entry group two ranges share, col16 unpermuted, stored as 8
+// contiguous entries); nullptr: delta 0, no extra groups.
 template <typename T, int U, bool NT = false>
 __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
     const int32_t *__restrict__ pieces, const uint16_t *__restrict__ col16,
-    const T *__restrict__ x, int64_t n_cols, int tw, T *__restrict__ xg LHPC_GVAL_PARAM) {
+    const T *__restrict__ x, int64_t n_cols, int tw, T *__restrict__ xg,
+    const int32_t *__restrict__ pext LHPC_GVAL_PARAM) {
   constexpr int W = XtTile<T>::W;  // LDS capacity; the plan's tile width tw ≤ W
   __shared__ T xt[W];
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
@@ -85,6 +91,30 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
 #pragma unroll
   for (int i = 0; i < PT; ++i) xt[i * kXtGatherBlock + tid] = tvv[i];
   __syncthreads();
+  typedef T tv16 __attribute__((ext_vector_type(16 / sizeof(T))));
+  constexpr int VW = 16 / sizeof(T);
+  if (pext) {
+    const int delta = pext[2 * blockIdx.x], flags = pext[2 * blockIdx.x + 1];
+    xg += delta;  // a multiple of 8: the 16-B store alignment holds
+    if (tid < 2 && ((flags >> tid) & 1)) {
+      const int gq = tid == 0 ? q0 - 1 : q1;  // the shared group before / at the end of the piece
+      const u32x4 wq = cv[gq];
+      T o[8];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        LHPC_DEVICE_CHECK((wq[h] & 0xFFFFu) < static_cast<uint32_t>(W) && (wq[h] >> 16) < static_cast<uint32_t>(W));
+        o[2 * h] = xt[wq[h] & 0xFFFFu];
+        o[2 * h + 1] = xt[wq[h] >> 16];
+      }
+#pragma unroll
+      for (int h = 0; h < 8 / VW; ++h) {
+        tv16 v;
+#pragma unroll
+        for (int k = 0; k < VW; ++k) v[k] = o[h * VW + k];
+        *reinterpret_cast<tv16 *>(xg + static_cast<int64_t>(gq) * 8 + h * VW) = v;
+      }
+    }
+  }
   for (int q = q0 + tid; q < q1; q += U * kXtGatherBlock) {
     if (q != q0 + tid) load_w(q);
 #pragma unroll
@@ -106,8 +136,6 @@ __global__ __launch_bounds__(kXtGatherBlock) void k_xtile_gather(
       // vector h lands at block + h·64·VW + VW·lane and every store
       // instruction writes 1 KB contiguous; a partial last block keeps the
       // lane's 8 entries contiguous
-      typedef T tv16 __attribute__((ext_vector_type(16 / sizeof(T))));
-      constexpr int VW = 16 / sizeof(T);
       const int qb = qq - lane;  // the wave's block (wave-uniform)
       T *blk = xg + static_cast<int64_t>(qb) * 8;
       if (qb + kWave <= q1) {
@@ -245,7 +273,7 @@ template <typename T> constexpr bool xt_rreg(int G) { return std::is_same<T, flo
 template <typename T, int G, int BLK, bool IP, bool AL>
 __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce(
     const int32_t *__restrict__ cdesc, const uint32_t *__restrict__ seg, const int32_t *__restrict__ seghi, int S,
-    int64_t c0, int64_t C,
+    int64_t hc0, int64_t hrow0, int64_t c0, int64_t C,
     int64_t Cx, int total, const T *__restrict__ xg, const uint16_t *__restrict__ perm,
     const T *__restrict__ val, const int32_t *__restrict__ rp, T *__restrict__ y,
     double *__restrict__ carry, int y_add) {
@@ -305,7 +333,8 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     const int sc = sI < S ? sI : S - 1;
     // segment table (lhpc_plan.hpp xtile_segment_table): start = hi + lo, end = start + len
     const uint32_t w = seg[c * S + sc];
-    sa[q] = seghi[(c / kXtSegHi) * S + sc] + static_cast<int>(w & 0xFFFFu);
+    // hi row: ⌊c / kXtSegHi⌋, or per range in ring plans (hrow0 + ⌊(c − hc0) / kXtSegHi⌋)
+    sa[q] = seghi[(hrow0 + (c - hc0) / kXtSegHi) * S + sc] + static_cast<int>(w & 0xFFFFu);
     sb[q] = sa[q] + static_cast<int>(w >> 16);
   }
   const u32x4 d = *reinterpret_cast<const u32x4 *>(cdesc + 8 * c);
@@ -785,23 +814,24 @@ const void *xtile_reduce_fn(int g, bool ip, bool al) {
 }
 
 template <typename T, int U, bool NT = false>
-void gather_u(const lhpc_spmv_plan *p, const int32_t *pieces, const void *x, int64_t q0, int64_t q1, hipStream_t s) {
+void gather_u(const lhpc_spmv_plan *p, const int32_t *pieces, const void *x, int64_t q0, int64_t q1, hipStream_t s,
+              const int32_t *pext) {
 #ifdef LHPC_XT_PROBE_GVAL
   int64_t vmask = 1;
   while (vmask * 2 <= p->nnz) vmask *= 2;
   vmask = (vmask - 1) & ~int64_t{7};
   if constexpr (U > LHPC_XT_PROBE_GVAL) {
-    gather_u<T, LHPC_XT_PROBE_GVAL, NT>(p, pieces, x, q0, q1, s);
+    gather_u<T, LHPC_XT_PROBE_GVAL, NT>(p, pieces, x, q0, q1, s, pext);
     return;
   } else
     hipLaunchKernelGGL((k_xtile_gather<T, U, NT>), dim3(static_cast<unsigned>(q1 - q0)), dim3(kXtGatherBlock), 0, s,
                        pieces + 3 * q0, p->d_col16, static_cast<const T *>(x), p->n_cols,
-                       static_cast<int>(p->xs_width), static_cast<T *>(p->d_xg), static_cast<const T *>(p->d_val),
-                       vmask);
+                       static_cast<int>(p->xs_width), static_cast<T *>(p->d_xg), pext ? pext + 2 * q0 : nullptr,
+                       static_cast<const T *>(p->d_val), vmask);
 #else
   hipLaunchKernelGGL((k_xtile_gather<T, U, NT>), dim3(static_cast<unsigned>(q1 - q0)), dim3(kXtGatherBlock), 0, s,
                      pieces + 3 * q0, p->d_col16, static_cast<const T *>(x), p->n_cols,
-                     static_cast<int>(p->xs_width), static_cast<T *>(p->d_xg));
+                     static_cast<int>(p->xs_width), static_cast<T *>(p->d_xg), pext ? pext + 2 * q0 : nullptr);
 #endif
 }
 
@@ -811,41 +841,46 @@ int launch_gather(const lhpc_spmv_plan *p, const void *x, hipStream_t s, int64_t
                   const int32_t *pieces = nullptr) {
   if (q1 < 0) q1 = p->xt_pieces;
   if (q1 <= q0) return LHPC_OK;
+  // the ring's per-piece deltas belong to the plan's own pieces
+  const int32_t *pext = !pieces && p->xt_ring ? p->d_pext : nullptr;
   if (!pieces) pieces = p->d_pieces;
   if (p->xt_nt) {
-    gather_u<T, 8, true>(p, pieces, x, q0, q1, s);
+    gather_u<T, 8, true>(p, pieces, x, q0, q1, s, pext);
     return check_launch(s);
   }
   switch (p->xt_u) {
-    case 2: gather_u<T, 2>(p, pieces, x, q0, q1, s); break;
-    case 4: gather_u<T, 4>(p, pieces, x, q0, q1, s); break;
+    case 2: gather_u<T, 2>(p, pieces, x, q0, q1, s, pext); break;
+    case 4: gather_u<T, 4>(p, pieces, x, q0, q1, s, pext); break;
     case 16:  // fp64 at 16 steps needs > 128 VGPRs (it spilled 22): capped at 8
-      if constexpr (sizeof(T) == 8) gather_u<T, 8>(p, pieces, x, q0, q1, s);
-      else gather_u<T, 16>(p, pieces, x, q0, q1, s);
+      if constexpr (sizeof(T) == 8) gather_u<T, 8>(p, pieces, x, q0, q1, s, pext);
+      else gather_u<T, 16>(p, pieces, x, q0, q1, s, pext);
       break;
-    default: gather_u<T, 8>(p, pieces, x, q0, q1, s); break;
+    default: gather_u<T, 8>(p, pieces, x, q0, q1, s, pext); break;
   }
   return check_launch(s);
 }
 
 // reduce of chunks [c0, c1) into y (rows at their plan index), then the fix-up
 // of the rows cut inside the range: cont entries [n0, n1)
+// ring: range k of a ring plan (ring-sized xg, range k's hi rows); −1: the
+// plan's whole stream
 template <typename T>
 int launch_reduce(const lhpc_spmv_plan *p, int64_t c0, int64_t c1, int64_t n0, int64_t n1, T *y,
-                  hipStream_t s) {
+                  hipStream_t s, int ring = -1) {
   if (c1 > c0) {
     const int64_t Cx = (c1 - c0 + 7) / 8;
     const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(xt_red_blk<T>());
     const void *fn = xtile_reduce_fn<T>(xtile_g<T>(p->S), p->xt_p == 3, p->xt_al != 0);
     const int32_t *cd = p->d_cdesc, *sh = p->d_seghi, *rp = static_cast<const int32_t *>(p->d_row_ptr);
     const uint32_t *so = p->d_seg;
-    int S = p->S, total = static_cast<int>(p->xt_total);
+    int S = p->S, total = static_cast<int>(ring >= 0 ? p->xt_ring_len : p->xt_total);
+    int64_t hc0 = ring >= 0 ? c0 : 0, hrow0 = ring >= 0 ? p->xt_hrow[static_cast<size_t>(ring)] : 0;
     const T *xg = static_cast<const T *>(p->d_xg), *val = static_cast<const T *>(p->d_val);
     const uint16_t *perm = p->d_perm;
     double *carry = p->d_carry;
     int acc = p->xt_acc;
-    void *args[] = {&cd, &so, &sh, &S, &c0, &c1, const_cast<int64_t *>(&Cx), &total, &xg, &perm, &val, &rp, &y, &carry,
-                    &acc};
+    void *args[] = {&cd, &so, &sh, &S, &hc0, &hrow0, &c0, &c1, const_cast<int64_t *>(&Cx), &total, &xg, &perm, &val,
+                    &rp, &y, &carry, &acc};
     LHPC_HIP_TRY(hipLaunchKernel(fn, rg, rb, args, p->xt_lds, s));
     LHPC_TRY(check_launch(s));
   }
@@ -1056,6 +1091,7 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   if (o.xtile_ranges > 0) mall = o.xtile_ranges;
   // a row-range plan (user splits) whose xg exceeds the cache gets per-range
   // gather pieces for its own ranges (stage still gathers them all)
+  const bool user_splits = !p->split_rows.empty();
   if (!p->split_rows.empty() && mall > 1) p->xt_mall = static_cast<int>(p->split_rows.size()) + 1;
   if (p->split_rows.empty() && mall > 1 && p->n_rows >= 2LL * mall) {
     std::vector<int64_t> cuts(static_cast<size_t>(mall) + 1);
@@ -1172,10 +1208,20 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
     // range loads every tile once (only one 160-KB gather block fits a CU)
     int64_t rpn = std::max<int64_t>(min_piece, p->nnz / p->xt_mall / static_cast<int64_t>(cus) * 5 / 4 + 1);
     if (o.xtile_range_piece > 0) rpn = std::max<int64_t>(8, o.xtile_range_piece);
-    xtile_range_pieces(xt, rpn, p->xt_rpc);
+    // the xg ring (options.xtile_ring): the plan's own cache
+    // ranges only — user row ranges are staged all at once (lhpc_spmv_stage)
+    p->xt_ring = !user_splits && ip && !al && o.xtile_ring != 1 ? 1 : 0;
+    if (p->xt_ring) {
+      xtile_ring_pieces(xt, rpn, p->xt_rpc);
+      p->xt_ring_len = xt.ring_len;
+      p->xt_hrow = xt.hrow;
+    } else {
+      xtile_range_pieces(xt, rpn, p->xt_rpc);
+    }
     p->xt_pieces = static_cast<int64_t>(xt.pieces.size() / 3);
   }
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_pieces), xt.pieces.data(), xt.pieces.size() * 4));
+  if (p->xt_ring) LHPC_TRY(up(reinterpret_cast<void **>(&p->d_pext), xt.pext.data(), xt.pext.size() * 4));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_cont), xt.cont.data(), xt.cont.size() * 4));
   if (dev) {
     // col16 and perm / iperm + val runs on the device, then the gather-store
@@ -1241,7 +1287,7 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
     const uint16_t spare[2] = {static_cast<uint16_t>(M), static_cast<uint16_t>(M)};
     LHPC_HIP_TRY(hipMemcpy(p->d_perm + xt.total, spare, 4, hipMemcpyHostToDevice));
   }
-  LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>(xt.total + 2) * tsz));
+  LHPC_TRY(up(&p->d_xg, nullptr, static_cast<size_t>((p->xt_ring ? xt.ring_len : xt.total) + 2) * tsz));
   LHPC_TRY(up(reinterpret_cast<void **>(&p->d_carry), nullptr, static_cast<size_t>(2 * C + 2) * 8));
   LHPC_HIP_TRY(hipMemset(p->d_carry, 0, static_cast<size_t>(2 * C + 2) * 8));
   if (!p->split_rows.empty()) {
@@ -1264,7 +1310,7 @@ template <typename T>
 int launch_mall(const lhpc_spmv_plan *p, const void *x, T *y, hipStream_t s) {
   for (int k = 0; k < p->xt_mall; ++k) {
     LHPC_TRY(launch_gather<T>(p, x, s, p->xt_rpc[k], p->xt_rpc[k + 1]));
-    LHPC_TRY(launch_reduce<T>(p, p->xt_src[k], p->xt_src[k + 1], 0, 0, y, s));
+    LHPC_TRY(launch_reduce<T>(p, p->xt_src[k], p->xt_src[k + 1], 0, 0, y, s, p->xt_ring ? k : -1));
   }
   // one fix-up for every range's cut rows (their carries stay in place)
   return launch_reduce<T>(p, p->xt_C, p->xt_C, 0, p->xt_cont, y, s);

@@ -129,6 +129,50 @@ void check_xtile(const Csr &a, bool iperm, const std::vector<int64_t> &splits, i
         for (int64_t g = xt.segoff[xt.rchunk[k] * S + s]; g < xt.segoff[xt.rchunk[k + 1] * S + s]; ++g)
           CHECK(by[static_cast<size_t>(g)] >= 0 && by[static_cast<size_t>(g)] <= k);
   }
+  // the xg ring (xtile_ring_pieces): per range, emulate the gather (every
+  // piece writes stream entry g at ring position g + delta, plus its flagged
+  // shared groups) on a ring wiped before the range, then the reduce's reads
+  // through the segment table (hi row hrow[k] + ⌊(c − rchunk[k]) / 7⌋):
+  // every segment must read back exactly its own stream entries
+  if (iperm && unit == 1 && xt.rchunk.size() > 2) {
+    std::vector<int64_t> rpc;
+    lhpc::xtile_ring_pieces(xt, 700, rpc);
+    std::vector<uint32_t> seg;
+    std::vector<int32_t> hi;
+    lhpc::xtile_segment_table(xt, seg, hi);
+    const int64_t K = static_cast<int64_t>(xt.rchunk.size()) - 1, L = xt.ring_len;
+    CHECK(L > 0 && L <= xt.total + 16 * S && static_cast<int64_t>(xt.hrow.size()) == K);
+    CHECK(xt.pext.size() == xt.pieces.size() / 3 * 2);
+    std::vector<int64_t> ring(static_cast<size_t>(L));
+    for (int64_t k = 0; k < K; ++k) {
+      std::fill(ring.begin(), ring.end(), -1);
+      for (int64_t q = rpc[k]; q < rpc[k + 1]; ++q) {
+        const int64_t g0 = xt.pieces[3 * q], g1 = xt.pieces[3 * q + 1], d = xt.pext[2 * q], fl = xt.pext[2 * q + 1];
+        CHECK(g0 % 8 == 0 && g1 % 8 == 0 && g0 <= g1 && d % 8 == 0);
+        auto put = [&](int64_t g) {
+          CHECK(g >= 0 && g < xt.total && g + d >= 0 && g + d < L);
+          if (g + d >= 0 && g + d < L) {
+            CHECK(ring[static_cast<size_t>(g + d)] < 0);  // no two writers in one range
+            ring[static_cast<size_t>(g + d)] = g;
+          }
+        };
+        for (int64_t g = g0; g < g1; ++g) put(g);
+        if (fl & 1)
+          for (int64_t g = g0 - 8; g < g0; ++g) put(g);
+        if (fl & 2)
+          for (int64_t g = g1; g < g1 + 8; ++g) put(g);
+      }
+      for (int64_t c = xt.rchunk[k]; c < xt.rchunk[k + 1]; ++c)
+        for (int64_t s = 0; s < S; ++s) {
+          const uint32_t w = seg[static_cast<size_t>(c * S + s)];
+          const int64_t h = xt.hrow[k] + (c - xt.rchunk[k]) / lhpc::kXtSegHi;
+          const int64_t start = hi[static_cast<size_t>(h * S + s)] + static_cast<int64_t>(w & 0xFFFFu), len = w >> 16;
+          CHECK(len == xt.segoff[(c + 1) * S + s] - xt.segoff[c * S + s]);
+          for (int64_t j = 0; j < len; ++j)
+            CHECK(start + j >= 0 && start + j < L && ring[static_cast<size_t>(start + j)] == xt.segoff[c * S + s] + j);
+        }
+    }
+  }
   // the transposed val/iperm streams and the gather-block permutation
   std::vector<int32_t> vbase;
   std::unique_ptr<unsigned char[]> valt;
@@ -203,6 +247,7 @@ int main() {
     check_xtile(u, ip, {});
     check_xtile(p, ip, {});
     check_xtile(p, ip, {1, 5000, 19999});
+    check_xtile(u, ip, {5000, 10000, 15000});
     check_xtile(p, ip, {}, 32);
     check_xtile(p, ip, {77}, 1024);
     check_xtile(e, ip, {});

@@ -536,6 +536,50 @@ def test_xtile_cache_ranges(lhpc, gpu, dtype, ranges, xt_layout):
                 assert np.array_equal(y, yr)
 
 
+@pytest.mark.parametrize("ranges", [2, 3, 5])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_xtile_xg_ring(lhpc, gpu, dtype, ranges):
+    """The xg ring of cache-sized ranges (round 6, options.xtile_ring auto):
+    one range-sized xg buffer that every range's gather rewrites, each
+    range's part of each tile at its own ring offset, the 8-entry groups two
+    ranges share gathered by both.  Bit-identical to the one-slot-per-entry
+    layout (xtile_ring = 1) and to the oracle — dyadic and uniform values,
+    tiny gather pieces (many pieces per (range, tile)), two calls in a row —
+    with less HBM held; a ring plan refuses lhpc_spmv_stage."""
+    import torch
+    lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 30000 + [0, 0] + [30000]
+    n_cols = 200_000
+    for dyadic in (True, False):
+        rp, col, val = _csr_from_lengths(lengths, n_cols, 0xB100 + ranges, dyadic=dyadic)
+        val = val.astype(dtype)
+        rng = np.random.default_rng(0xB1F0 + ranges)
+        x = ((rng.integers(-8, 9, size=n_cols) / 8.0) if dyadic else rng.uniform(-1, 1, n_cols)).astype(dtype)
+        xd = torch.from_numpy(x).to(gpu)
+        _, yr, asum = S.spmv_oracle(rp, col, val, x)
+        for piece in (0, 200):
+            ys, nbytes = [], []
+            for ring_off in (0, 1):
+                opts = {"xtile_reduce": 2, "xtile_ranges": ranges, "xtile_range_piece": piece, "xtile_ring": ring_off}
+                with lhpc.SpMVPlan(rp, col, val, n_cols, flags=FAMILIES["xtile"], options=opts) as plan:
+                    info = plan.info()
+                    assert info["kernel"] == lhpc.KERNEL_XTILE
+                    nbytes.append(info["device_bytes"])
+                    for _ in range(2):
+                        y = plan(xd)
+                    ys.append(y.cpu().numpy())
+                    if ring_off == 0:
+                        with pytest.raises(lhpc.LhpcError) as e:
+                            plan.stage(xd)
+                        assert e.value.status == -5
+            assert np.array_equal(ys[0], ys[1]), (dyadic, piece)
+            if dyadic:
+                assert np.array_equal(ys[0], yr)
+            else:
+                S.assert_spmv_close(ys[0], yr, asum)
+            nnz = int(col.size)
+            assert nbytes[0] < nbytes[1] - (ranges - 1) / ranges * 0.9 * nnz * val.itemsize
+
+
 def test_split_plan_unsupported_without_xtile(lhpc, gpu):
     """A matrix that does not select XTILE (small x) refuses a row-range plan."""
     rp, col, val = _csr_from_lengths([5] * 1000, 1000, 0xA800, dyadic=True)
