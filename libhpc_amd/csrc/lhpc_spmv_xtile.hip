@@ -1074,18 +1074,24 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   // Cache when its reduce reads it back.  fp32 only: each extra range re-reads
   // x (n_cols·T) in its gather.  Same box: C2 reduce 352 → 295
   // µs, gather 163 → 179 µs, call 523.5 → 483.8 µs at K = 3 (K = 4: 506.7);
-  // C3 (fp64, K = 6: 200 MB ranges) 928 → 944 µs, so not for fp64
-  // Only while each range still streams ≥ min_piece nonzeros per tile and
-  // K ≤ 8: every range re-loads all S tiles of x, so a wide x (n = 80M:
-  // 1954 tiles; n = 150M: 3662) would spend more on tile loads than the
-  // cache saves — such plans keep one range (the n = 150M plan took 23.6 ms
-  // with 8 ranges per part)
+  // C3 (fp64, K = 6: 200 MB ranges) 928 → 944 µs, so not for fp64 — until
+  // the xg ring (round 6, same box, xtile_ranges = 1 / 3 / 4 / 6 / 8: C3
+  // 0.908 / 0.943 / 0.995 / 0.868 / 0.902 ms): fp64 takes the ranges when its
+  // plan can hold the ring (no user row splits, iperm reduce).
+  // Only while each range still streams ≥ min_piece nonzeros per tile (fp64:
+  // min_piece / 2 — its ring saves the 8-B xg write-back) and K ≤ 8: every
+  // range re-loads all S tiles of x, so a wide x (n = 80M: 1954 tiles; n =
+  // 150M: 3662) would spend more on tile loads than the cache saves — such
+  // plans keep one range (the n = 150M plan took 23.6 ms with 8 ranges per part)
   int mall = 0;
   {
     const int64_t xg_bytes = p->nnz * static_cast<int64_t>(tsz);
     const int64_t k = (xg_bytes + (int64_t{200} << 20) - 1) / (int64_t{200} << 20);
     const int64_t tiles = (p->n_cols + W - 1) / W;
-    if (tsz == 4 && xg_bytes > (int64_t{256} << 20) && k <= 8 && p->nnz / k / std::max<int64_t>(1, tiles) >= min_piece)
+    const bool ring_ok = p->split_rows.empty() && ip && !al && o.xtile_ring != 1;
+    const int64_t need = tsz == 4 ? min_piece : min_piece / 2;
+    if ((tsz == 4 || ring_ok) && xg_bytes > (int64_t{256} << 20) && k <= 8 &&
+        p->nnz / k / std::max<int64_t>(1, tiles) >= need)
       mall = static_cast<int>(k);
   }
   if (o.xtile_ranges > 0) mall = o.xtile_ranges;
