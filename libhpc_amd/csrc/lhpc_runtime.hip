@@ -8,7 +8,7 @@
 #define LHPC_TAG_PROBE 1
 #endif
 #if defined(LHPC_XT_RBLK32) || defined(LHPC_XT_RBLK64) || defined(LHPC_XT_IP_WAVES) || defined(LHPC_XT_LDS_TOTAL) || \
-    defined(LHPC_XT_XG_CPOL) || defined(LHPC_XT_SEGHI) || defined(LHPC_XT_F64DMA) || defined(LHPC_XT_STAMPS) ||   \
+    defined(LHPC_XT_XG_CPOL) || defined(LHPC_XT_SEGHI) || defined(LHPC_XT_STAMPS) ||   \
     defined(LHPC_SELL_NO_SHFL) || defined(LHPC_SCRATCH_DEFAULT_POOL)
 #define LHPC_TAG_AB 1
 #endif

@@ -257,12 +257,6 @@ __device__ uint64_t g_xt_stamps[1 << 22];
 #ifndef LHPC_XT_IP_WAVES
 #define LHPC_XT_IP_WAVES 8  // iperm reduce: 8 waves/SIMD (fp32 66 → 64 VGPRs: C2 593 → 580 µs)
 #endif
-#ifndef LHPC_XT_F64DMA
-#define LHPC_XT_F64DMA 0
-#endif
-// fp64 iperm reduce: phase A's xg by 4-B LDS-DMA (two instructions per 64
-// positions) instead of b64 loads + ds_write_b64
-template <typename T, bool IP> constexpr bool kXtF64Dma = LHPC_XT_F64DMA && IP && sizeof(T) == 8;
 // the reduce keeps the chunk's row offsets in registers (k_xtile_reduce)
 template <typename T> constexpr bool xt_rreg(int G) { return std::is_same<T, float>::value && G == 2; }
 
@@ -417,7 +411,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
 
   // ---- phase A: src = base_ne[rank] + f, xg loads (round trip 3);
   //      positions past m load the sentinel entry `total` (perm: spare slot M)
-  int src[kXtF64Dma<T, IP> && !AL ? 2 * NB : NB];
+  int src[NB];
   if constexpr (AL) {
     // unit u of batch j covers flat positions VW·((wv·NBU + j)·64 + lane) …;
     // lane q holds unit batch q's bitmap word (≤ 64 batches: one pass)
@@ -462,19 +456,6 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
       const u32x4 t = bt[u];  // uniform address: broadcast
-      if constexpr (kXtF64Dma<T, IP>) {
-        // fp64 by 4-B LDS-DMA: instruction h of batch u moves positions
-        // 32·h … 32·h + 31 of the batch, lane l dword l & 1 of position 32·h + l/2
-        // (rank from the batch word: the starts at bits 1 … k of w)
-        const uint64_t w1 = static_cast<uint64_t>(t[0]) | (static_cast<uint64_t>(t[1]) << 32);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int k = 32 * h + (lane >> 1);
-          const int rk = static_cast<int>(t[2]) + __popcll(w1 & ((uint64_t{1} << k) - 1));
-          src[2 * u + h] = base_ne[rk] + (wv * NB + u) * kWave + k;
-        }
-        continue;
-      }
       const int rk = __builtin_amdgcn_mbcnt_hi(t[1], __builtin_amdgcn_mbcnt_lo(t[0], t[2]));
       const int f = (wv * NB + u) * kWave + lane;
       const int sv = base_ne[rk] + f;  // m > 0 ⇒ 0 ≤ rk < S; m = 0: base_ne[−1] (in LDS), unused
@@ -567,22 +548,14 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
       }
       (void)src;
 #else
-      if constexpr (kXtF64Dma<T, IP>) {
-#if defined(__HIP_DEVICE_COMPILE__)
+      // (a 4-B LDS-DMA form, two instructions per 64 positions, was 2%
+      // slower: DESIGN.md §4.1 round 6)
+      T xv[NB];
 #pragma unroll
-        for (int v = 0; v < 2 * NB; ++v)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              xr_rs, (__attribute__((address_space(3))) void *)(xs + (wv * NB * 2 + v) * (kWave / 2)), 4,
-              src[v] * 8 + (lane & 1) * 4, 0, 0, LHPC_XT_XG_CPOL);
-#endif
-      } else {
-        T xv[NB];
+      for (int u = 0; u < NB; ++u)
+        xv[u] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(xr_rs, src[u] * 8, 0, 0));
 #pragma unroll
-        for (int u = 0; u < NB; ++u)
-          xv[u] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(xr_rs, src[u] * 8, 0, 0));
-#pragma unroll
-        for (int u = 0; u < NB; ++u) xs[(wv * NB + u) * kWave + lane] = xv[u];
-      }
+      for (int u = 0; u < NB; ++u) xs[(wv * NB + u) * kWave + lane] = xv[u];
 #endif
       load_ipv();
     }
@@ -625,7 +598,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     if (tid == 0) xs[M] = T(0);  // the zero slot that iperm padding points at
   // the LDS-DMA of phase A is counted by vmcnt, which the barrier does not
   // wait for: drain it before any wave reads another wave's flat slots
-  if constexpr (IP && (sizeof(T) == 4 || AL || kXtF64Dma<T, IP>)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (IP && (sizeof(T) == 4 || AL)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   LHPC_XT_STAMP(5, 0)
 
