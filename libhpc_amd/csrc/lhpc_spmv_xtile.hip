@@ -284,7 +284,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   // dynamic LDS (xtile_lds_bytes): xs[M + VW] T (slot M is the sentinel's
   // spare), bt[BLK/64][NB] u32x4, ws[BLK/64] f64, wsf[BLK/64] i32, bm[M/32]
   // u32, sbm[M/32] u32, rfirst[RPT][BLK/64] u16 (padded to 4 B), rlast i32,
-  // base_ne[S] i32, wsum[8] i32.  RREG (fp32 G = 2, 476–1024 tiles): the
+  // base_ne[S] i32, wsum[16] i32 (one per wave: fp64 blocks have 16).  RREG (fp32 G = 2, 476–1024 tiles): the
   // chunk's local row offsets stay in the threads' registers (rt[q] = row
   // q·BLK + tid) and the y store takes row j+1's from lane + 1, or from
   // rfirst for a wave's last lane — 56 B of LDS instead of rpl[RMAX+1] u16
@@ -749,7 +749,7 @@ size_t xtile_lds_bytes_g(int S, int g) {
   const size_t rows = xt_rreg<T>(g) ? ((RPT * W + 1) & ~1) * sizeof(uint16_t) + sizeof(int32_t)  // rfirst, rlast
                                     : ((RMAX + 2) & ~1) * sizeof(uint16_t);                     // rpl
   return static_cast<size_t>(M + 16 / sizeof(T)) * sizeof(T) + W * xt_run<T>() * 16 + W * (sizeof(double) + 4) +
-         2 * M / 32 * sizeof(uint32_t) + rows + sizeof(int32_t) * (static_cast<size_t>(S) + 8);
+         2 * M / 32 * sizeof(uint32_t) + rows + sizeof(int32_t) * (static_cast<size_t>(S) + 16);  // base_ne, wsum[BLK/64 ≤ 16]
 }
 // a G = 1 plan whose rpl pushes the reduce past 4 blocks per CU (160 KB / 4
 // of LDS; fp32 S ≈ 476–512) takes the G = 2 form, whose row offsets live in
