@@ -224,6 +224,10 @@ typedef struct lhpc_options {
    * 1: one xg slot per stream entry (the round-5 layout).  Ring plans refuse
    * lhpc_spmv_stage / lhpc_spmv_range (LHPC_ERR_UNSUPPORTED).               */
   int32_t xtile_ring;
+  /* XTILE iperm reduce (≤ 512 fp32 / 1024 fp64 tiles): 1 the segment scan
+   * per chunk; 2 the plan's per-chunk phase-A tables (batch rank terms and
+   * segment bases, copied to LDS by LDS-DMA); 0 (auto): 2 for fp64, 1 fp32 */
+  int32_t xtile_pretable;
 } lhpc_options;
 void lhpc_options_init(lhpc_options *opts);
 

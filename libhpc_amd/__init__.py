@@ -121,7 +121,7 @@ class Options(C.Structure):
                 ("dist_world1", C.c_int32), ("xtile_part_nnz", C.c_int32), ("multi_chunks", C.c_int32),
                 ("multi_exchange", C.c_int32), ("multi_force", C.c_int32), ("dist_reduce_streams", C.c_int32),
                 ("xtile_col_blocks", C.c_int32), ("xtile_host_build", C.c_int32), ("spmv_no_sell", C.c_int32),
-                ("xtile_ring", C.c_int32)]
+                ("xtile_ring", C.c_int32), ("xtile_pretable", C.c_int32)]
 
     def __init__(self, **kw):
         super().__init__()

@@ -468,6 +468,44 @@ void xtile_segment_table(const XtileHost &o, std::vector<uint32_t> &seg, std::ve
   }
 }
 
+void xtile_phase_tables(const XtileHost &o, std::vector<uint32_t> &bt, std::vector<int32_t> &base_ne) {
+  const int64_t S = o.S, C = o.n_chunks, M = o.M, NBT = M / 64;
+  bt.assign(static_cast<size_t>(std::max<int64_t>(C, 1) * NBT * 4), 0u);
+  base_ne.assign(static_cast<size_t>(std::max<int64_t>(C, 1) * S), 0);
+  const int64_t K = static_cast<int64_t>(o.rchunk.size()) - 1;
+#pragma omp parallel
+  {
+    std::vector<uint64_t> starts(static_cast<size_t>(NBT));
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t c = 0; c < C; ++c) {
+      int64_t k = 0;  // c's range (for the ring deltas)
+      if (!o.rdelta.empty())
+        while (k + 1 < K && o.rchunk[k + 1] <= c) ++k;
+      std::fill(starts.begin(), starts.end(), uint64_t{0});
+      int32_t *bn = base_ne.data() + c * S;
+      int64_t flat = 0, nne = 0;
+      for (int64_t s = 0; s < S; ++s) {
+        const int64_t a = o.segoff[c * S + s], len = o.segoff[(c + 1) * S + s] - a;
+        if (len <= 0) continue;
+        const int64_t start = a + (o.rdelta.empty() ? 0 : o.rdelta[static_cast<size_t>(k * S + s)]);
+        bn[nne++] = static_cast<int32_t>(start - flat);
+        starts[static_cast<size_t>(flat / 64)] |= uint64_t{1} << (flat % 64);
+        flat += len;
+      }
+      for (int64_t r = nne; r < S; ++r) bn[r] = nne > 0 ? bn[nne - 1] : 0;
+      int64_t before = 0;
+      uint32_t *b4 = bt.data() + c * NBT * 4;
+      for (int64_t b = 0; b < NBT; ++b) {
+        const uint64_t w = starts[static_cast<size_t>(b)], w1 = w >> 1;
+        b4[4 * b] = static_cast<uint32_t>(w1);
+        b4[4 * b + 1] = static_cast<uint32_t>(w1 >> 32);
+        b4[4 * b + 2] = static_cast<uint32_t>(before - 1 + static_cast<int64_t>(w & 1u));
+        before += __builtin_popcountll(w);
+      }
+    }
+  }
+}
+
 void xtile_ring_pieces(XtileHost &o, int64_t piece_nnz, std::vector<int64_t> &rpc) {
   const int64_t S = o.S, K = static_cast<int64_t>(o.rchunk.size()) - 1;
   const int64_t pn = std::max<int64_t>(8, (piece_nnz + 7) / 8 * 8);

@@ -192,6 +192,13 @@ void xtile_range_pieces(XtileHost &o, int64_t piece_nnz, std::vector<int64_t> &r
 // col16 group is permuted by two pieces.  Ring layout: sub-runs (k, s) in
 // tile order, [⌊a⌋₈, ⌈b⌉₈) at an 8-aligned cursor; rdelta, pext, ring_len.
 void xtile_ring_pieces(XtileHost &o, int64_t piece_nnz, std::vector<int64_t> &rpc);
+// Phase-A tables of the iperm reduce (round 6, k_xtile_reduce PRE): per chunk
+// c, base_ne[c·S + r] = start of its r-th non-empty segment (stream position,
+// or ring position when o.rdelta is set) − that segment's flat offset (unused
+// entries repeat the last one), and for each of its M/64 batches b of flat
+// positions the rank terms bt[(c·M/64 + b)·4 …] = {w >> 1 (low, high word),
+// starts before the batch − 1 + (w & 1), 0}, w = the batch's 64 start bits.
+void xtile_phase_tables(const XtileHost &o, std::vector<uint32_t> &bt, std::vector<int32_t> &base_ne);
 
 // LDS slot of chunk position i in the XTILE reduce (lhpc_spmv_xtile.hip
 // xt_slot): run t = i/run holds run = 64/elem_bytes elements (64 B) at

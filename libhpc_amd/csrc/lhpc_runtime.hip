@@ -102,6 +102,7 @@ void env_overlay(lhpc_options &o) {
     o.xtile_reduce = std::atoi(e) ? LHPC_XTILE_REDUCE_IPERM : LHPC_XTILE_REDUCE_PERM;
   if (const char *e = tuning_env("LHPC_XTILE_MALL")) o.xtile_ranges = std::max(1, std::atoi(e));
   i32("LHPC_XTILE_RING", o.xtile_ring);
+  i32("LHPC_XTILE_PRETABLE", o.xtile_pretable);
   i32("LHPC_XTILE_U", o.xtile_steps);
   if (const char *e = tuning_env("LHPC_XTILE_NTSTORE")) o.xtile_store = std::atoi(e) ? LHPC_STORE_NT : LHPC_STORE_PLAIN;
   i32("LHPC_XTILE_CUT", o.xtile_cut);

@@ -916,7 +916,7 @@ extern "C" int lhpc_spmv_plan_layout_digest(const lhpc_spmv_plan *p, uint64_t *o
     }
     LHPC_HIP_TRY(hipSetDevice(p->device));
     const size_t tsz = p->dtype == LHPC_F32 ? 4 : 8;
-    const int64_t C = p->xt_C, S = p->S, H = (C + kXtSegHi - 1) / kXtSegHi;
+    const int64_t C = p->xt_C;
     const std::pair<const void *, size_t> arr[10] = {
         {p->d_row_ptr, static_cast<size_t>(p->n_rows + 1) * 4},
         {p->d_col16, static_cast<size_t>(p->xt_total) * 2},
@@ -924,8 +924,8 @@ extern "C" int lhpc_spmv_plan_layout_digest(const lhpc_spmv_plan *p, uint64_t *o
         {p->d_val, static_cast<size_t>(p->xt_nrun) * tsz},
         {p->d_cdesc, static_cast<size_t>(8 * C + 8) * 4},
         {p->d_cr, static_cast<size_t>(C + 1) * 4},
-        {p->d_seg, static_cast<size_t>(std::max<int64_t>(C, 1) * S) * 4},
-        {p->d_seghi, static_cast<size_t>(std::max<int64_t>(H, 1) * S) * 4},
+        {p->d_seg, static_cast<size_t>(p->xt_seg_n) * 4},  // segment table (or PRE: batch rank terms)
+        {p->d_seghi, static_cast<size_t>(p->xt_seghi_n) * 4},
         {p->d_pieces, static_cast<size_t>(p->xt_pieces) * 12},
         {p->d_cont, static_cast<size_t>(p->xt_cont) * 4}};
     std::vector<unsigned char> h;

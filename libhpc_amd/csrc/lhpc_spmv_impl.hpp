@@ -74,6 +74,8 @@ struct lhpc_spmv_plan {
   // range; per piece {ring delta, flags} in d_pext; range k's segment-table hi
   // rows start at xt_hrow[k]
   int xt_ring = 0;
+  int xt_pre = 0;
+  int64_t xt_seg_n = 0, xt_seghi_n = 0;  // entries of d_seg / d_seghi  // the reduce reads the plan's phase-A tables (d_seg = bt, d_seghi = base_ne)
   int64_t xt_ring_len = 0;
   int32_t *d_pext = nullptr;
   std::vector<int64_t> xt_hrow;

@@ -264,7 +264,13 @@ template <typename T> constexpr bool xt_rreg(int G) { return std::is_same<T, flo
 // every segment starts on a 16-B boundary and spans whole 16-B units of VW
 // positions, so phase A ranks units instead of positions (M/VW ≤ 64 batches
 // of 64 units) and each lane moves one 16-B unit by LDS-DMA, fp64 included.
-template <typename T, int G, int BLK, bool IP, bool AL>
+// PRE (iperm, no aligned segments; round 6): the plan holds each chunk's
+// phase-A tables — the rank terms of its M/64 batches (bt, u32x4: start mask
+// w >> 1 and the starts before the batch) and the bases of its non-empty
+// segments (base_ne, S i32, ring positions) — and the reduce copies them
+// into LDS by LDS-DMA in round trip 1 instead of the segment scan.
+// seg = pbt (u32x4 per batch, as u32), seghi = pbne in that mode.
+template <typename T, int G, int BLK, bool IP, bool AL, bool PRE = false>
 __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce(
     const int32_t *__restrict__ cdesc, const uint32_t *__restrict__ seg, const int32_t *__restrict__ seghi, int S,
     int64_t hc0, int64_t hrow0, int64_t c0, int64_t C,
@@ -320,16 +326,36 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
   //      trip 2 (val run and row_ptr, addressed by the descriptor).  The
   //      segment scan and phase A need only the table, so phase A's xg loads
   //      go out while val and row_ptr are still in flight.
+  static_assert(!PRE || (IP && !AL), "PRE: the iperm reduce without aligned segments");
   int sa[G], sb[G];
+  if constexpr (PRE) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the chunk's phase-A tables into LDS: bt (M/64 u32x4 = M/16 dwords,
+    // 64 per wave instruction) and base_ne (S dwords, padded to 64 in LDS)
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t *>(seg + c * (M / 16)), 0, (M / 16) * 4, 0x00020000);
+    for (int k = wv; k < M / 16 / kWave; k += NW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void *)(reinterpret_cast<uint32_t *>(bt0) + k * kWave),
+                                               4, (k * kWave + lane) * 4, 0, 0, 0);
+    const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<int32_t *>(seghi + c * S), 0, S * 4, 0x00020000);
+    for (int k = wv; k * kWave < S; k += NW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (__attribute__((address_space(3))) void *)(base_ne + k * kWave), 4,
+                                               (k * kWave + lane) * 4, 0, 0, 0);
+#endif
+    (void)sa;
+    (void)sb;
+  } else {
 #pragma unroll
-  for (int q = 0; q < G; ++q) {
-    const int sI = tid * G + q;
-    const int sc = sI < S ? sI : S - 1;
-    // segment table (lhpc_plan.hpp xtile_segment_table): start = hi + lo, end = start + len
-    const uint32_t w = seg[c * S + sc];
-    // hi row: ⌊c / kXtSegHi⌋, or per range in ring plans (hrow0 + ⌊(c − hc0) / kXtSegHi⌋)
-    sa[q] = seghi[(hrow0 + (c - hc0) / kXtSegHi) * S + sc] + static_cast<int>(w & 0xFFFFu);
-    sb[q] = sa[q] + static_cast<int>(w >> 16);
+    for (int q = 0; q < G; ++q) {
+      const int sI = tid * G + q;
+      const int sc = sI < S ? sI : S - 1;
+      // segment table (lhpc_plan.hpp xtile_segment_table): start = hi + lo, end = start + len
+      const uint32_t w = seg[c * S + sc];
+      // hi row: ⌊c / kXtSegHi⌋, or per range in ring plans (hrow0 + ⌊(c − hc0) / kXtSegHi⌋)
+      sa[q] = seghi[(hrow0 + (c - hc0) / kXtSegHi) * S + sc] + static_cast<int>(w & 0xFFFFu);
+      sb[q] = sa[q] + static_cast<int>(w >> 16);
+    }
   }
   const u32x4 d = *reinterpret_cast<const u32x4 *>(cdesc + 8 * c);
   const u32x4 d2 = *reinterpret_cast<const u32x4 *>(cdesc + 8 * c + 4);
@@ -374,11 +400,16 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     const int j = q * BLK + tid;
     rv[q] = rp[r0 + (j <= R ? j : R)];
   }
-  // ---- scan: segment ranks / bases and the segment-start bitmap
+  // ---- scan: segment ranks / bases and the segment-start bitmap (PRE:
+  //      the plan's tables, once their LDS-DMA has landed)
   if (tid < M / 32) {
     bm[tid] = 0u;
     sbm[tid] = 0u;
   }
+  if constexpr (PRE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
   int lsum = 0;  // (length | non-empty count << 16) of this thread's segments
 #pragma unroll
   for (int q = 0; q < G; ++q) {
@@ -407,6 +438,7 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     }
   }
   __syncthreads();
+  }  // !PRE
   LHPC_XT_STAMP(3, 0)
 
   // ---- phase A: src = base_ne[rank] + f, xg loads (round trip 3);
@@ -437,22 +469,24 @@ __global__ __launch_bounds__(BLK, IP ? LHPC_XT_IP_WAVES : 1) void k_xtile_reduce
     // broadcast:  rank = starts before the batch − 1 + (w & 1) + mbcnt(w >> 1)
     // (lanes hold batch words q and q + 64 … when M > 4096); wave w owns
     // batches [NB·w, NB·w + NB)
-    const int grp = (wv * NB) >> 6;  // this wave's batches lie in 64-batch group grp
-    uint64_t wl = 0;
-    int cnt = 0, incl = 0, below = 0;
-    for (int g2 = 0; g2 <= grp; ++g2) {  // wave-uniform
-      wl = static_cast<uint64_t>(sbm[128 * g2 + 2 * lane]) | (static_cast<uint64_t>(sbm[128 * g2 + 2 * lane + 1]) << 32);
-      cnt = __popcll(wl);
-      incl = wave_incl_scan(cnt) + below;  // starts in batches ≤ 64·g2 + lane
-      below = __builtin_amdgcn_readlane(incl, kWave - 1);
-    }
     u32x4 *bt = bt0 + wv * NB;
-    if (lane / NB == wv % (kWave / NB)) {  // lanes holding this wave's batches
-      const uint64_t w1 = wl >> 1;
-      bt[lane & (NB - 1)] = u32x4{static_cast<uint32_t>(w1), static_cast<uint32_t>(w1 >> 32),
-                                  static_cast<uint32_t>(incl - cnt - 1 + static_cast<int>(wl & 1u)), 0u};
+    if constexpr (!PRE) {
+      const int grp = (wv * NB) >> 6;  // this wave's batches lie in 64-batch group grp
+      uint64_t wl = 0;
+      int cnt = 0, incl = 0, below = 0;
+      for (int g2 = 0; g2 <= grp; ++g2) {  // wave-uniform
+        wl = static_cast<uint64_t>(sbm[128 * g2 + 2 * lane]) | (static_cast<uint64_t>(sbm[128 * g2 + 2 * lane + 1]) << 32);
+        cnt = __popcll(wl);
+        incl = wave_incl_scan(cnt) + below;  // starts in batches ≤ 64·g2 + lane
+        below = __builtin_amdgcn_readlane(incl, kWave - 1);
+      }
+      if (lane / NB == wv % (kWave / NB)) {  // lanes holding this wave's batches
+        const uint64_t w1 = wl >> 1;
+        bt[lane & (NB - 1)] = u32x4{static_cast<uint32_t>(w1), static_cast<uint32_t>(w1 >> 32),
+                                    static_cast<uint32_t>(incl - cnt - 1 + static_cast<int>(wl & 1u)), 0u};
+      }
+      __builtin_amdgcn_wave_barrier();  // LDS is in order within a wave: no block barrier needed
     }
-    __builtin_amdgcn_wave_barrier();  // LDS is in order within a wave: no block barrier needed
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
       const u32x4 t = bt[u];  // uniform address: broadcast
@@ -743,13 +777,14 @@ __global__ __launch_bounds__(kXtFixBlock) void k_xtile_fixup(
 // form spilled and could never be selected)
 template <typename T> constexpr int xt_gmax() { return 4096 / xt_red_blk<T>(); }
 template <typename T>
-size_t xtile_lds_bytes_g(int S, int g) {
+size_t xtile_lds_bytes_g(int S, int g, bool pre = false) {
   constexpr int BLK = xt_red_blk<T>(), M = XtRed<T, BLK>::M, RMAX = XtRed<T, BLK>::Rmax, W = BLK / kWave;
   constexpr int RPT = (RMAX + 1 + BLK - 1) / BLK;
   const size_t rows = xt_rreg<T>(g) ? ((RPT * W + 1) & ~1) * sizeof(uint16_t) + sizeof(int32_t)  // rfirst, rlast
                                     : ((RMAX + 2) & ~1) * sizeof(uint16_t);                     // rpl
   return static_cast<size_t>(M + 16 / sizeof(T)) * sizeof(T) + W * xt_run<T>() * 16 + W * (sizeof(double) + 4) +
-         2 * M / 32 * sizeof(uint32_t) + rows + sizeof(int32_t) * (static_cast<size_t>(S) + 16);  // base_ne, wsum[BLK/64 ≤ 16]
+         2 * M / 32 * sizeof(uint32_t) + rows + sizeof(int32_t) * (static_cast<size_t>(S) + 16) +  // base_ne, wsum[BLK/64 ≤ 16]
+         (pre ? 256 : 0);  // PRE: base_ne's LDS-DMA writes whole 64-entry rows
 }
 // a G = 1 plan whose rpl pushes the reduce past 4 blocks per CU (160 KB / 4
 // of LDS; fp32 S ≈ 476–512) takes the G = 2 form, whose row offsets live in
@@ -767,21 +802,23 @@ size_t xtile_lds_bytes(int S) {
   return xtile_lds_bytes_g<T>(S, xtile_g<T>(S));
 }
 
-template <typename T, int G, bool IP, bool AL>
+template <typename T, int G, bool IP, bool AL, bool PRE = false>
 const void *xtile_reduce_fn() {
-  if constexpr (G > xt_gmax<T>() || (AL && !IP) || (AL && G > 4))  // AL at G = 8 spilled (build_t avoids it)
+  if constexpr (G > xt_gmax<T>() || (AL && !IP) || (AL && G > 4) || (PRE && (!IP || AL)))  // AL at G = 8 spilled
     return nullptr;
   else
-    return reinterpret_cast<const void *>(k_xtile_reduce<T, G, xt_red_blk<T>(), IP, AL>);
+    return reinterpret_cast<const void *>(k_xtile_reduce<T, G, xt_red_blk<T>(), IP, AL, PRE>);
 }
-template <typename T, bool IP, bool AL>
+template <typename T, bool IP, bool AL, bool PRE = false>
 const void *xtile_reduce_fn(int g) {
-  return g == 1 ? xtile_reduce_fn<T, 1, IP, AL>() : g == 2 ? xtile_reduce_fn<T, 2, IP, AL>()
-         : g == 4 ? xtile_reduce_fn<T, 4, IP, AL>() : xtile_reduce_fn<T, 8, IP, AL>();
+  return g == 1 ? xtile_reduce_fn<T, 1, IP, AL, PRE>() : g == 2 ? xtile_reduce_fn<T, 2, IP, AL, PRE>()
+         : g == 4 ? xtile_reduce_fn<T, 4, IP, AL, PRE>() : xtile_reduce_fn<T, 8, IP, AL, PRE>();
 }
-// ip: iperm reduce; al: aligned segments (iperm only, else nullptr)
+// ip: iperm reduce; al: aligned segments (iperm only, else nullptr); pre:
+// the plan's phase-A tables instead of the segment scan (iperm, not aligned)
 template <typename T>
-const void *xtile_reduce_fn(int g, bool ip, bool al) {
+const void *xtile_reduce_fn(int g, bool ip, bool al, bool pre = false) {
+  if (pre) return ip && !al && g == 1 ? xtile_reduce_fn<T, 1, true, false, true>() : nullptr;  // G = 2 spilled
   if (al) return ip ? xtile_reduce_fn<T, true, true>(g) : nullptr;
   return ip ? xtile_reduce_fn<T, true, false>(g) : xtile_reduce_fn<T, false, false>(g);
 }
@@ -843,7 +880,7 @@ int launch_reduce(const lhpc_spmv_plan *p, int64_t c0, int64_t c1, int64_t n0, i
   if (c1 > c0) {
     const int64_t Cx = (c1 - c0 + 7) / 8;
     const dim3 rg(static_cast<unsigned>(8 * Cx)), rb(xt_red_blk<T>());
-    const void *fn = xtile_reduce_fn<T>(xtile_g<T>(p->S), p->xt_p == 3, p->xt_al != 0);
+    const void *fn = xtile_reduce_fn<T>(xtile_g<T>(p->S), p->xt_p == 3, p->xt_al != 0, p->xt_pre != 0);
     const int32_t *cd = p->d_cdesc, *sh = p->d_seghi, *rp = static_cast<const int32_t *>(p->d_row_ptr);
     const uint32_t *so = p->d_seg;
     int S = p->S, total = static_cast<int>(ring >= 0 ? p->xt_ring_len : p->xt_total);
@@ -1119,7 +1156,15 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   p->xt_pieces = static_cast<int64_t>(xt.pieces.size() / 3);
   p->xt_cont = static_cast<int64_t>(xt.cont.size());
   p->xt_total = xt.total;
-  p->xt_lds = xtile_lds_bytes<T>(xt.S);
+  // phase-A tables (options.xtile_pretable): iperm
+  // plans without aligned segments, G = 1.  Default for fp64 only — same box,
+  // two runs each: C3 reduce 89.9 → 85.3 µs per range (its 16-wave scan was
+  // 2.3K of 27.8K cycles per chunk), C2 88.1 → 89.4 µs (the tables' extra
+  // 1 KB per chunk outweighs an 8-wave scan)
+  const bool pre = ip && !al && xtile_g<T>(xt.S) == 1 &&
+                   (o.xtile_pretable == 2 || (o.xtile_pretable == 0 && sizeof(T) == 8));
+  p->xt_pre = pre ? 1 : 0;
+  p->xt_lds = xtile_lds_bytes_g<T>(xt.S, xtile_g<T>(xt.S), pre);
 #ifdef LHPC_XT_LDS_TOTAL  // A/B build only: reduce blocks padded to this many bytes of LDS (fewer per CU)
   if (sizeof(T) == 4) p->xt_lds = std::max<size_t>(p->xt_lds, LHPC_XT_LDS_TOTAL);
 #endif
@@ -1133,7 +1178,7 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   // non-temporal: 473 → 536 µs)
   p->xt_nt = p->xt_mall <= 1 && p->nnz * static_cast<int64_t>(tsz) > (int64_t{256} << 20) ? 1 : 0;
   if (o.xtile_store != LHPC_STORE_AUTO) p->xt_nt = o.xtile_store == LHPC_STORE_NT ? 1 : 0;
-  const void *rfn = xtile_reduce_fn<T>(xtile_g<T>(xt.S), ip, al);
+  const void *rfn = xtile_reduce_fn<T>(xtile_g<T>(xt.S), ip, al, pre);
   if (!rfn) return LHPC_ERR_UNSUPPORTED;  // more tiles than the reduce's segment table holds
   LHPC_HIP_TRY(hipFuncSetAttribute(rfn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(p->xt_lds)));
   const int64_t n_rows = p->n_rows, C = xt.n_chunks;
@@ -1247,12 +1292,22 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
     xtile_permute_gather_blocks(xt, static_cast<int>(16 / tsz));
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_col16), xt.col16.get(), static_cast<size_t>(xt.total) * 2));
   }
-  {
+  if (pre) {  // the reduce's phase-A tables in place of the segment table (seg = bt, seghi = base_ne)
+    std::vector<uint32_t> pbt;
+    std::vector<int32_t> pbne;
+    xtile_phase_tables(xt, pbt, pbne);
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_seg), pbt.data(), pbt.size() * 4));
+    LHPC_TRY(up(reinterpret_cast<void **>(&p->d_seghi), pbne.data(), pbne.size() * 4));
+    p->xt_seg_n = static_cast<int64_t>(pbt.size());
+    p->xt_seghi_n = static_cast<int64_t>(pbne.size());
+  } else {
     std::vector<uint32_t> seg;
     std::vector<int32_t> seghi;
     xtile_segment_table(xt, seg, seghi);
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_seg), seg.data(), seg.size() * 4));
     LHPC_TRY(up(reinterpret_cast<void **>(&p->d_seghi), seghi.data(), seghi.size() * 4));
+    p->xt_seg_n = static_cast<int64_t>(seg.size());
+    p->xt_seghi_n = static_cast<int64_t>(seghi.size());
   }
   if (dev) {
     // built above

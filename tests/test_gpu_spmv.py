@@ -892,3 +892,37 @@ def test_coo_to_csr_to_spmv_stays_on_device(lhpc, gpu):
         x = lhpc.gen_values(lhpc.F32, 1, n, 0xDE21)
         y = p(torch.from_numpy(x).to(gpu)).cpu().numpy()
     assert np.array_equal(y, S.spmv_oracle(want_rp, want_col, want_val, x)[1])
+
+
+@pytest.mark.parametrize("ranges", [1, 3])
+@pytest.mark.parametrize("tiles", [3, 256])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_xtile_phase_tables(lhpc, gpu, dtype, ranges, tiles):
+    """The iperm reduce from the plan's per-chunk phase-A tables
+    (options.xtile_pretable = 2: batch rank terms and segment bases copied to
+    LDS by LDS-DMA instead of the segment scan) gives the scanning reduce's y
+    bit for bit and the oracle's on dyadic data — one range and three ring
+    ranges, long rows across chunks and empty rows, 3 and 256 tiles."""
+    import torch
+    lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 30000 + [0, 0] + [30000]
+    n_cols = (40960 if dtype == np.float32 else 20480) * tiles - 7
+    for dyadic in (True, False):
+        rp, col, val = _csr_from_lengths(lengths, n_cols, 0xB500 + tiles, dyadic=dyadic)
+        val = val.astype(dtype)
+        rng = np.random.default_rng(0xB5F0)
+        x = ((rng.integers(-8, 9, size=n_cols) / 8.0) if dyadic else rng.uniform(-1, 1, n_cols)).astype(dtype)
+        xd = torch.from_numpy(x).to(gpu)
+        ys = []
+        for pre in (2, 1):
+            opts = {"xtile_reduce": 2, "xtile_ranges": ranges, "xtile_pretable": pre}
+            with lhpc.SpMVPlan(rp, col, val, n_cols, flags=FAMILIES["xtile"], options=opts) as plan:
+                assert plan.info()["kernel"] == lhpc.KERNEL_XTILE
+                for _ in range(2):
+                    y = plan(xd)
+                ys.append(y.cpu().numpy())
+        assert np.array_equal(ys[0], ys[1]), dyadic
+        _, yr, asum = S.spmv_oracle(rp, col, val, x)
+        if dyadic:
+            assert np.array_equal(ys[0], yr)
+        else:
+            S.assert_spmv_close(ys[0], yr, asum)
