@@ -221,8 +221,10 @@ typedef struct lhpc_options {
   /* XTILE cache-sized ranges (no user splits, iperm reduce): 0 (auto) one
    * range-sized xg ring reused by every range, so a range's gather overwrites
    * lines still in the Infinity Cache instead of evicting dirty ones to HBM;
-   * 1: one xg slot per stream entry (the round-5 layout).  Ring plans refuse
-   * lhpc_spmv_stage / lhpc_spmv_range (LHPC_ERR_UNSUPPORTED).               */
+   * 1: one xg slot per stream entry (the round-5 layout); 2: the ring for
+   * user row ranges too (whole calls only; the per-rank plans of
+   * lhpc_dist_spmv ask for it).  Ring plans refuse lhpc_spmv_stage /
+   * lhpc_spmv_range (LHPC_ERR_UNSUPPORTED).                                 */
   int32_t xtile_ring;
   /* XTILE iperm reduce (≤ 512 fp32 / 1024 fp64 tiles): 1 the segment scan
    * per chunk; 2 the plan's per-chunk phase-A tables (batch rank terms and

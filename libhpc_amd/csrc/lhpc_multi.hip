@@ -55,6 +55,9 @@ int local_plans_create(LocalPlans &lp, int dtype, int64_t n_cols, int K, const i
   lp.K = K;
   lhpc_options lo = o;
   lo.multi_force = 0;  // the local plans are single-device plans
+  // ranges are gathered and reduced one after the other (local_plans_chunk),
+  // so cache-sized ranges can share one xg ring
+  if (lo.xtile_ring == 0) lo.xtile_ring = 2;
   lp.ls.assign(ls, ls + K + 1);
   const RowPtrView rp{row_ptr, row_ptr_bits};
   const int64_t n_local = ls[K];

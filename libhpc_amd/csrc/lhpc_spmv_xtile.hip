@@ -1098,7 +1098,10 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
     const int64_t xg_bytes = p->nnz * static_cast<int64_t>(tsz);
     const int64_t k = (xg_bytes + (int64_t{200} << 20) - 1) / (int64_t{200} << 20);
     const int64_t tiles = (p->n_cols + W - 1) / W;
-    const bool ring_ok = p->split_rows.empty() && ip && !al && o.xtile_ring != 1;
+    // the xg ring: the plan's own cache ranges by default; user row ranges
+    // only when asked for (xtile_ring = 2: the library's per-rank plans,
+    // which gather and reduce range by range in order)
+    const bool ring_ok = ip && !al && (p->split_rows.empty() ? o.xtile_ring != 1 : o.xtile_ring == 2);
     const int64_t need = tsz == 4 ? min_piece : min_piece / 2;
     if ((tsz == 4 || ring_ok) && xg_bytes > (int64_t{256} << 20) && k <= 8 &&
         p->nnz / k / std::max<int64_t>(1, tiles) >= need)
@@ -1233,8 +1236,9 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
     int64_t rpn = std::max<int64_t>(min_piece, p->nnz / p->xt_mall / static_cast<int64_t>(cus) * 5 / 4 + 1);
     if (o.xtile_range_piece > 0) rpn = std::max<int64_t>(8, o.xtile_range_piece);
     // the xg ring (options.xtile_ring): the plan's own cache
-    // ranges only — user row ranges are staged all at once (lhpc_spmv_stage)
-    p->xt_ring = !user_splits && ip && !al && o.xtile_ring != 1 ? 1 : 0;
+    // ranges; user row ranges only with xtile_ring = 2 (lhpc_spmv_stage would
+    // gather every range into the one ring: a ring plan refuses it)
+    p->xt_ring = ip && !al && (user_splits ? o.xtile_ring == 2 : o.xtile_ring != 1) ? 1 : 0;
     if (p->xt_ring) {
       xtile_ring_pieces(xt, rpn, p->xt_rpc);
       p->xt_ring_len = xt.ring_len;
@@ -1379,9 +1383,10 @@ int xtile_range_gather(const lhpc_spmv_plan *p, const void *x, int k, hipStream_
 
 int xtile_range(const lhpc_spmv_plan *p, int k, void *yk, hipStream_t s) {
   const int64_t c0 = p->xt_src[k], c1 = p->xt_src[k + 1], n0 = p->xt_sco[k], n1 = p->xt_sco[k + 1];
+  const int ring = p->xt_ring ? k : -1;  // a ring plan: range k was the last one gathered
   if (p->dtype == LHPC_F32)
-    return launch_reduce<float>(p, c0, c1, n0, n1, static_cast<float *>(yk) - p->xt_srow[k], s);
-  return launch_reduce<double>(p, c0, c1, n0, n1, static_cast<double *>(yk) - p->xt_srow[k], s);
+    return launch_reduce<float>(p, c0, c1, n0, n1, static_cast<float *>(yk) - p->xt_srow[k], s, ring);
+  return launch_reduce<double>(p, c0, c1, n0, n1, static_cast<double *>(yk) - p->xt_srow[k], s, ring);
 }
 
 int xtile_part_of_tile(int64_t tile, int64_t tile_width, int64_t n_cols, const int64_t *col_end, int n_parts) {

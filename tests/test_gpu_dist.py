@@ -43,9 +43,10 @@ def test_dist_spmv_world1_matches_single_plan(lhpc, gpu, comm, n, per_row, K, dt
     one plan per block for the small one), twice in a row, y != x.
     range_gather: the row-range plan gets per-range gather pieces (as a plan
     whose xg exceeds the Infinity Cache does) and each chunk's range is
-    gathered right before its reduce instead of one stage."""
+    gathered right before its reduce instead of one stage — into one
+    range-sized xg ring (the local plans' default, options.xtile_ring = 2),
+    or with one slot per entry (xtile_ring = 1): same y, less device memory."""
     import torch
-    opts = {"xtile_ranges": 2} if range_gather else None
     dt = lhpc.F32 if dtype == "f32" else lhpc.F64
     rp, col, val = lhpc.gen_uniform_csr(n, n, per_row, dtype=dt, dist=1, seed=0xD200 + K)
     x = lhpc.gen_values(dt, 1, n, 0xD201)
@@ -53,12 +54,20 @@ def test_dist_spmv_world1_matches_single_plan(lhpc, gpu, comm, n, per_row, K, dt
     _, want, _ = S.spmv_oracle(rp, col, val, x)
     cuts = lhpc.interleaved_cuts(rp, 1, K)
     lrp, lc, lv = lhpc.interleaved_local_csr(rp, col, val, cuts, 1, K, 0)
-    with lhpc.DistSpMVPlan(comm, n, n, K, cuts, lrp, lc, lv, options=opts) as d:
-        for _ in range(2):
-            y = torch.full((n,), float("nan"), dtype=xd.dtype, device=gpu)
-            d(xd, y)
-            torch.cuda.synchronize()
-            assert np.array_equal(y.cpu().numpy(), want)
+    infos = []
+    for ring in ((0, 1) if range_gather else (0,)):
+        opts = {"xtile_ranges": 2, "xtile_ring": ring} if range_gather else None
+        with lhpc.DistSpMVPlan(comm, n, n, K, cuts, lrp, lc, lv, options=opts) as d:
+            infos.append(d.local_info())
+            for _ in range(2):
+                y = torch.full((n,), float("nan"), dtype=xd.dtype, device=gpu)
+                d(xd, y)
+                torch.cuda.synchronize()
+                assert np.array_equal(y.cpu().numpy(), want), ring
+    if range_gather and K > 1 and infos[0]["kernel"] == lhpc.KERNEL_XTILE:
+        # the ring holds the largest range's xg instead of every entry's
+        nnz = int(lc.size)
+        assert infos[0]["device_bytes"] < infos[1]["device_bytes"] - 0.3 * nnz * val.itemsize, infos
 
 
 @pytest.mark.parametrize("mode", ["allgather", "broadcast"])

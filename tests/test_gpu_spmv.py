@@ -582,6 +582,42 @@ def test_xtile_xg_ring(lhpc, gpu, dtype, ranges):
             assert nbytes[0] < nbytes[1] - (ranges - 1) / ranges * 0.9 * nnz * val.itemsize
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_xtile_xg_ring_user_ranges(lhpc, gpu, dtype):
+    """options.xtile_ring = 2: a plan with user row ranges whose ranges are
+    gathered one by one (forced here by xtile_ranges) shares one xg ring
+    across them, as the per-rank plans of lhpc_dist_spmv do.  A whole call is
+    bit-identical to the one-slot-per-entry plan (xtile_ring = 1) and to the
+    oracle, twice in a row, user ranges without nonzeros included; the ring plan
+    refuses lhpc_spmv_stage and lhpc_spmv_range."""
+    import torch
+    lengths = [20000] + [3] * 50 + [5000, 4096, 4095, 1, 0, 9000] + [15] * 30000 + [0, 0] + [30000]
+    n_cols = 200_000
+    rp, col, val = _csr_from_lengths(lengths, n_cols, 0xB300, dyadic=True)
+    val = val.astype(dtype)
+    x = (np.random.default_rng(0xB301).integers(-8, 9, size=n_cols) / 8.0).astype(dtype)
+    xd = torch.from_numpy(x).to(gpu)
+    _, yr, _ = S.spmv_oracle(rp, col, val, x)
+    splits = [55, 56, 9000, 30057, 30059]  # rows 55 and 30057-30058: ranges with no nonzeros
+    ys, nbytes = [], []
+    for ring in (2, 1):
+        opts = {"xtile_reduce": 2, "xtile_ranges": 2, "xtile_ring": ring}
+        with lhpc.SpMVPlan(rp, col, val, n_cols, flags=FAMILIES["xtile"], options=opts, splits=splits) as plan:
+            info = plan.info()
+            assert info["kernel"] == lhpc.KERNEL_XTILE
+            nbytes.append(info["device_bytes"])
+            for _ in range(2):
+                y = plan(xd)
+            ys.append(y.cpu().numpy())
+            if ring == 2:
+                with pytest.raises(lhpc.LhpcError) as e:
+                    plan.stage(xd)
+                assert e.value.status == -5
+    assert np.array_equal(ys[0], ys[1])
+    assert np.array_equal(ys[0], yr)
+    assert nbytes[0] < nbytes[1] - 0.3 * int(col.size) * val.itemsize, nbytes
+
+
 def test_split_plan_unsupported_without_xtile(lhpc, gpu):
     """A matrix that does not select XTILE (small x) refuses a row-range plan."""
     rp, col, val = _csr_from_lengths([5] * 1000, 1000, 0xA800, dyadic=True)
