@@ -101,20 +101,29 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const K *__restr
   counts[static_cast<int64_t>(blockIdx.x) * 256 + t] = hist[0][t] + hist[1][t] + hist[2][t] + hist[3][t];
 }
 
-// Block-wide exclusive scan of one value per thread (256 threads = 4 waves);
-// returns the total.  DPP scan inside each wave, the four wave totals through
+// Block-wide exclusive scan of one value per thread (NW waves: 256 threads =
+// 4); returns the total.  DPP scan inside each wave, the wave totals through
 // LDS: two barriers (the Hillis-Steele form took 16 per call, and the
 // downsweep runs two scans per 4096-key sub-tile).
-__device__ __forceinline__ uint32_t block_exscan256(uint32_t v, uint32_t *tmp /*[≥4]*/, uint32_t &total) {
+template <int NW = 4>
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *tmp /*[≥NW]*/, uint32_t &total) {
   const int t = threadIdx.x, w = t / kWave;
   const uint32_t inc = static_cast<uint32_t>(wave_incl_scan(static_cast<int>(v)));  // modular add: same bits
   if ((t & (kWave - 1)) == kWave - 1) tmp[w] = inc;
   __syncthreads();
-  const uint32_t t0 = tmp[0], t1 = tmp[1], t2 = tmp[2], t3 = tmp[3];
-  total = t0 + t1 + t2 + t3;
-  const uint32_t off = (w > 0 ? t0 : 0u) + (w > 1 ? t1 : 0u) + (w > 2 ? t2 : 0u);
+  uint32_t off = 0, all = 0;
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const uint32_t tj = tmp[j];
+    off += j < w ? tj : 0u;
+    all += tj;
+  }
+  total = all;
   __syncthreads();  // tmp is reused by the caller's next scan
   return off + inc - v;
+}
+__device__ __forceinline__ uint32_t block_exscan256(uint32_t v, uint32_t *tmp, uint32_t &total) {
+  return block_exscan<4>(v, tmp, total);
 }
 
 // Scan: one workgroup per digit d.  counts[b][d] → exclusive prefix over
@@ -182,24 +191,32 @@ __device__ __forceinline__ uint64_t match_any8(uint32_t d) {
 // base of digit t lives in thread t's register; full sub-tiles load and store
 // without bounds checks; one barrier fewer per sub-tile than reading two
 // offset tables (C2-sized sort, same box, three runs each: 9.04 → 8.91 ms).
-template <typename K, bool HAS_V, int IPT, bool PF = true>
-__global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
+// BT threads per block (NW = BT / 64 waves); threads t < 256 own digit t.
+#ifndef LHPC_SORT_DS_WAVES  // A/B builds: waves per SIMD the downsweep's registers must allow
+#define LHPC_SORT_DS_WAVES 1
+#endif
+template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads>
+__global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(LHPC_SORT_DS_WAVES))) void k_radix_downsweep(
     const K *__restrict__ kin, K *__restrict__ kout, const uint32_t *__restrict__ vin, uint32_t *__restrict__ vout,
     int64_t n, int shift, uint32_t mask, int64_t per_block, const uint32_t *__restrict__ counts,
     const uint32_t *__restrict__ totals) {
-  constexpr int TILE = IPT * kSortThreads;
+  constexpr int TILE = IPT * BT;
   constexpr int WSEG = IPT * kWave;
+  constexpr int NW = BT / kWave;
+  static_assert(BT % 256 == 0, "threads t < 256 own the digits");
   __shared__ K sk[TILE];
   __shared__ uint32_t sv[HAS_V ? TILE : 1];
-  __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t wcnt[NW][256];
   __shared__ uint32_t gofs[256];
-  __shared__ uint32_t tmp[256];
+  __shared__ uint32_t tmp[NW];
   const int t = threadIdx.x, w = t / kWave, lane = t & (kWave - 1);
+  const bool own = BT == 256 || t < 256;  // thread t owns digit t
   const uint64_t lt_mask = (uint64_t{1} << lane) - 1;
   uint32_t gb;  // thread t: global output position of digit t's next key
   {
     uint32_t all;
-    gb = block_exscan256(totals[t], tmp, all) + counts[static_cast<int64_t>(blockIdx.x) * 256 + t];
+    gb = block_exscan<NW>(own ? totals[t] : 0u, tmp, all) +
+         (own ? counts[static_cast<int64_t>(blockIdx.x) * 256 + t] : 0u);
   }
   const int64_t first = static_cast<int64_t>(blockIdx.x) * per_block;
   const int64_t ntiles = (n + TILE - 1) / TILE;
@@ -253,16 +270,24 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     __syncthreads();
     // per digit t: wave prefix + sub-tile start into the wave counters, and
     // global base − sub-tile start into gofs
-    const uint32_t c0 = wcnt[0][t], c1 = wcnt[1][t], c2 = wcnt[2][t], c3 = wcnt[3][t];
-    const uint32_t tot = c0 + c1 + c2 + c3;
+    uint32_t c[NW], tot = 0;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      c[j] = own ? wcnt[j][t] : 0u;
+      tot += c[j];
+    }
     uint32_t all;
-    const uint32_t ts = block_exscan256(tot, tmp, all);
-    wcnt[0][t] = ts;
-    wcnt[1][t] = ts + c0;
-    wcnt[2][t] = ts + c0 + c1;
-    wcnt[3][t] = ts + c0 + c1 + c2;
-    gofs[t] = gb - ts;
-    gb += tot;
+    const uint32_t ts = block_exscan<NW>(tot, tmp, all);
+    if (own) {
+      uint32_t run = ts;
+#pragma unroll
+      for (int j = 0; j < NW; ++j) {
+        wcnt[j][t] = run;
+        run += c[j];
+      }
+      gofs[t] = gb - ts;
+      gb += tot;
+    }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
@@ -278,7 +303,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_downsweep(
     const int valid = full ? TILE : static_cast<int>(n - base);
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
-      const int p = t + kSortThreads * k;
+      const int p = t + BT * k;
       if (full || p < valid) {
         const K kk = sk[p];
         const uint32_t g = gofs[digit_of(kk, shift, mask)] + static_cast<uint32_t>(p);
@@ -332,7 +357,7 @@ struct HostStage {
 // resident downsweep blocks on the current device (CUs × blocks per CU),
 // cached per kernel and device (relaxed atomics: racing threads compute the
 // same value)
-template <typename K, bool HAS_V, int IPT, bool PF>
+template <typename K, bool HAS_V, int IPT, bool PF, int BT>
 int64_t sort_grid_cap() {
   static std::atomic<int64_t> cache[64];
   int dev = 0;
@@ -344,7 +369,7 @@ int64_t sort_grid_cap() {
   }
   int cus = 0, per_cu = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT, PF>, kSortThreads, 0) !=
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT, PF, BT>, BT, 0) !=
           hipSuccess ||
       cus <= 0 || per_cu <= 0)
     return kSortMaxResident;
@@ -353,15 +378,15 @@ int64_t sort_grid_cap() {
   return cap;
 }
 
-template <typename K, bool HAS_V, int IPT, bool PF = true>
+template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads>
 int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, hipStream_t s) {
   if (n <= 1 || begin_bit >= end_bit) return LHPC_OK;
-  constexpr int TILE = IPT * kSortThreads;
+  constexpr int TILE = IPT * BT;
   const int64_t ntiles = (n + TILE - 1) / TILE;
   // Grid: up to 8 waves of resident blocks, but at least ~3 tiles per block. More, shorter blocks even out
   // the tail of the even-share split (500M keys: 768 blocks 8.94 ms, 6144 blocks 8.16 ms); below ~3 tiles
   // per block the per-block digit-count rows outweigh the gain (100M keys: 8192 blocks 1.89 ms, 30000 2.19).
-  const int64_t res = sort_grid_cap<K, HAS_V, IPT, PF>();
+  const int64_t res = sort_grid_cap<K, HAS_V, IPT, PF, BT>();
   // grid sweep knobs of the tuning build only (tools/explore_sort.py; lhpc_common.hpp tuning_env)
   static const int64_t waves = tuning_env("LHPC_SORT_WAVES") ? std::max(1, std::atoi(tuning_env("LHPC_SORT_WAVES"))) : 8;
   int64_t cap = std::min<int64_t>(waves * res, std::max<int64_t>(res, ntiles / 3));
@@ -385,7 +410,7 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
     hipLaunchKernelGGL((k_radix_upsweep<K, TILE>), dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0, s, kin,
                        n, shift, mask, per, cnt, vec16);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(kSortThreads), 0, s, cnt, static_cast<int>(nb), db);
-    hipLaunchKernelGGL((k_radix_downsweep<K, HAS_V, IPT, PF>), dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0,
+    hipLaunchKernelGGL((k_radix_downsweep<K, HAS_V, IPT, PF, BT>), dim3(static_cast<unsigned>(nb)), dim3(BT), 0,
                        s, kin, kout, vin, vout, n, shift, mask, per, cnt, db);
     std::swap(kin, kout);
     if (HAS_V) std::swap(vin, vout);
@@ -603,7 +628,7 @@ int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *r
 using namespace lhpc;
 
 namespace {
-template <typename K, bool HAS_V, int IPT, bool PF = true>
+template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads>
 int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, int on_device, void *stream) {
   constexpr int KB = static_cast<int>(sizeof(K) * 8);
   if (n < 0 || (!keys && n > 0) || (HAS_V && !vals && n > 0) || begin_bit < 0 || end_bit > KB ||
@@ -612,13 +637,13 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
   if (n >= (int64_t{1} << 32)) return LHPC_ERR_UNSUPPORTED;  // 32-bit ranks
   RocTxRange rx("lhpc_radix_sort");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (on_device) return radix_sort_dev<K, HAS_V, IPT, PF>(keys, vals, n, begin_bit, end_bit, s);
+  if (on_device) return radix_sort_dev<K, HAS_V, IPT, PF, BT>(keys, vals, n, begin_bit, end_bit, s);
   HostStage dk, dv;
   LHPC_HIP_TRY(dk.alloc(static_cast<size_t>(n) * sizeof(K)));
   if (HAS_V) LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(n) * 4));
   LHPC_HIP_TRY(hipMemcpy(dk.p, keys, static_cast<size_t>(n) * sizeof(K), hipMemcpyHostToDevice));
   if (HAS_V) LHPC_HIP_TRY(hipMemcpy(dv.p, vals, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice));
-  LHPC_TRY((radix_sort_dev<K, HAS_V, IPT, PF>(static_cast<K *>(dk.p), static_cast<uint32_t *>(dv.p), n, begin_bit,
+  LHPC_TRY((radix_sort_dev<K, HAS_V, IPT, PF, BT>(static_cast<K *>(dk.p), static_cast<uint32_t *>(dv.p), n, begin_bit,
                                           end_bit, s)));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
   LHPC_HIP_TRY(hipMemcpy(keys, dk.p, static_cast<size_t>(n) * sizeof(K), hipMemcpyDeviceToHost));
@@ -640,7 +665,11 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
 extern "C" int lhpc_radix_sort_u32(uint32_t *keys, int64_t n, int begin_bit, int end_bit, int on_device,
                                    void *stream) {
   try {
+#ifdef LHPC_SORT_KEYS_VARIANT  // A/B builds: IPT, PF, BT of the keys-only downsweep
+    return sort_entry<uint32_t, false, LHPC_SORT_KEYS_VARIANT>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
+#else
     return sort_entry<uint32_t, false, 32>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
+#endif
   } LHPC_ABI_CATCH
 }
 

@@ -14,6 +14,9 @@ and the val + iperm stream (wave-transposed, non-temporal).
               ic   xg written (plain stores, as the gather) right before: the
                    fragments come from the Infinity Cache
               hbm  xg written, then 1 GB of other data written: from HBM
+  c3r       fp64, S = 489, 25M positions (one of C3's six ring ranges: xg 200 MB
+            written right before, from the Infinity Cache), 1024-thread
+            blocks at the reduce's LDS (2 per CU)
   ring      C2 call shape: three 200-MB xg writes each followed by its probe,
             into three distinct buffers (the plan's xg[total]) or one reused
             buffer; the writes and the probes timed apart (does the dirty-line
@@ -116,6 +119,15 @@ for rep in range(2):
                 out(case="c3", rep=rep, f64_dma=f64_dma, blocks_per_cu=blocks, lds=lds, us=us, us_median=med,
                     moved=c3.moved, TBps=c3.moved / us * 1e-6)
         del c3, junk
+        torch.cuda.empty_cache()
+    if "c3r" in which:
+        c3r = Case(8, 489, 25_000_000)
+        for blocks in (2, 1):
+            lds = lds_bytes(8, 489) if blocks == 2 else 96 * 1024
+            us, med = timed(lambda: write(c3r.xg), lambda: c3r.launch(0, lds))
+            out(case="c3r", rep=rep, xg_from="ic", blocks_per_cu=blocks, lds=lds, us=us, us_median=med,
+                moved=c3r.moved, TBps=c3r.moved / us * 1e-6)
+        del c3r
         torch.cuda.empty_cache()
     if "c2" in which:
         c2 = Case(4, 256, 50_000_000)
