@@ -270,11 +270,12 @@ __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(LHPC_SORT_DS
     __syncthreads();
     // per digit t: wave prefix + sub-tile start into the wave counters, and
     // global base − sub-tile start into gofs
-    uint32_t c[NW], tot = 0;
+    // (the NW wave counts are read again after the scan instead of being
+    // held across it: 16 registers at NW = 16)
+    uint32_t tot = 0;
+    if (own) {
 #pragma unroll
-    for (int j = 0; j < NW; ++j) {
-      c[j] = own ? wcnt[j][t] : 0u;
-      tot += c[j];
+      for (int j = 0; j < NW; ++j) tot += wcnt[j][t];
     }
     uint32_t all;
     const uint32_t ts = block_exscan<NW>(tot, tmp, all);
@@ -282,8 +283,9 @@ __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(LHPC_SORT_DS
       uint32_t run = ts;
 #pragma unroll
       for (int j = 0; j < NW; ++j) {
+        const uint32_t cj = wcnt[j][t];
         wcnt[j][t] = run;
-        run += c[j];
+        run += cj;
       }
       gofs[t] = gb - ts;
       gb += tot;
