@@ -192,11 +192,12 @@ __device__ __forceinline__ uint64_t match_any8(uint32_t d) {
 // without bounds checks; one barrier fewer per sub-tile than reading two
 // offset tables (C2-sized sort, same box, three runs each: 9.04 → 8.91 ms).
 // BT threads per block (NW = BT / 64 waves); threads t < 256 own digit t.
-#ifndef LHPC_SORT_DS_WAVES  // A/B builds: waves per SIMD the downsweep's registers must allow
-#define LHPC_SORT_DS_WAVES 1
-#endif
-template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads>
-__global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(LHPC_SORT_DS_WAVES))) void k_radix_downsweep(
+// RL: the keys are not held across the digit scan — the rank loads them,
+// the reorder loads them again (L2 hits: the block read them one scan
+// earlier) together with the values, so IPT keys per thread fit the 128
+// VGPRs a 1024-thread block allows.
+template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads, bool RL = false>
+__global__ __launch_bounds__(BT) void k_radix_downsweep(
     const K *__restrict__ kin, K *__restrict__ kout, const uint32_t *__restrict__ vin, uint32_t *__restrict__ vout,
     int64_t n, int shift, uint32_t mask, int64_t per_block, const uint32_t *__restrict__ counts,
     const uint32_t *__restrict__ totals) {
@@ -204,6 +205,8 @@ __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(LHPC_SORT_DS
   constexpr int WSEG = IPT * kWave;
   constexpr int NW = BT / kWave;
   static_assert(BT % 256 == 0, "threads t < 256 own the digits");
+  static_assert(!(RL && PF), "a reloading downsweep prefetches nothing");
+  static_assert(TILE <= 65536, "16-bit ranks");
   __shared__ K sk[TILE];
   __shared__ uint32_t sv[HAS_V ? TILE : 1];
   __shared__ uint32_t wcnt[NW][256];
@@ -223,22 +226,28 @@ __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(LHPC_SORT_DS
   const int64_t last = std::min<int64_t>(ntiles, first + per_block);
   K key[IPT];
   uint32_t val[IPT];
-  auto load_tile = [&](int64_t tile, K(&kr)[IPT], uint32_t(&vr)[IPT]) {
+  auto load_tile = [&](int64_t tile, K(&kr)[IPT], uint32_t(&vr)[IPT], bool with_v = true, bool again = false) {
     const int64_t base = tile * TILE;
-    const K *ks = kin + base + w * WSEG + lane;
+    const K *kb = kin;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (again) asm volatile("" : "+s"(kb));  // a real second load, not the first one's registers
+#endif
+    const K *ks = kb + base + w * WSEG + lane;
     const uint32_t *vs = HAS_V ? vin + base + w * WSEG + lane : nullptr;
     if (base + TILE <= n) {
 #pragma unroll
       for (int i = 0; i < IPT; ++i) {
         kr[i] = ks[i * kWave];
-        if constexpr (HAS_V) vr[i] = vs[i * kWave];
+        if constexpr (HAS_V)
+          if (with_v) vr[i] = vs[i * kWave];
       }
     } else {
       const int valid = static_cast<int>(n - base) - (w * WSEG + lane);
 #pragma unroll
       for (int i = 0; i < IPT; ++i) {
         kr[i] = i * kWave < valid ? ks[i * kWave] : ~K(0);  // pad: max digit, ranked after every real key
-        if constexpr (HAS_V) vr[i] = i * kWave < valid ? vs[i * kWave] : 0u;
+        if constexpr (HAS_V)
+          if (with_v) vr[i] = i * kWave < valid ? vs[i * kWave] : 0u;
       }
     }
   };
@@ -255,16 +264,18 @@ __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(LHPC_SORT_DS
     if constexpr (PF) {
       if (tile + 1 < last) load_tile(tile + 1, nkey, nval);
     } else {
-      load_tile(tile, key, val);
+      load_tile(tile, key, val, !RL);
     }
-    uint32_t loc[IPT];
+    // ranks inside the sub-tile (< 65536) two per register
+    uint32_t loc[(IPT + 1) / 2];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const uint32_t d = digit_of(key[i], shift, mask);
       const uint64_t peers = match_any8(d);
       const uint64_t below = peers & lt_mask;
       const uint32_t before = wcnt[w][d];
-      loc[i] = before + static_cast<uint32_t>(__popcll(below));
+      const uint32_t r = before + static_cast<uint32_t>(__popcll(below));
+      loc[i / 2] = i & 1 ? loc[i / 2] | r << 16 : r;
       if (below == 0) wcnt[w][d] = before + static_cast<uint32_t>(__popcll(peers));
     }
     __syncthreads();
@@ -291,9 +302,10 @@ __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(LHPC_SORT_DS
       gb += tot;
     }
     __syncthreads();
+    if constexpr (RL) load_tile(tile, key, val, true, true);
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
-      const uint32_t p = wcnt[w][digit_of(key[i], shift, mask)] + loc[i];
+      const uint32_t p = wcnt[w][digit_of(key[i], shift, mask)] + (i & 1 ? loc[i / 2] >> 16 : loc[i / 2] & 0xFFFFu);
       sk[p] = key[i];
       if constexpr (HAS_V) sv[p] = val[i];
     }
@@ -303,7 +315,7 @@ __global__ __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(LHPC_SORT_DS
     // passes once its scatter is done; each wave clears only its own counter
     // row, which only it reads before that barrier)
     const int valid = full ? TILE : static_cast<int>(n - base);
-#pragma unroll
+#pragma unroll 8  // (a full unroll holds IPT 64-bit store addresses)
     for (int k = 0; k < IPT; ++k) {
       const int p = t + BT * k;
       if (full || p < valid) {
@@ -359,7 +371,7 @@ struct HostStage {
 // resident downsweep blocks on the current device (CUs × blocks per CU),
 // cached per kernel and device (relaxed atomics: racing threads compute the
 // same value)
-template <typename K, bool HAS_V, int IPT, bool PF, int BT>
+template <typename K, bool HAS_V, int IPT, bool PF, int BT, bool RL>
 int64_t sort_grid_cap() {
   static std::atomic<int64_t> cache[64];
   int dev = 0;
@@ -371,7 +383,7 @@ int64_t sort_grid_cap() {
   }
   int cus = 0, per_cu = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT, PF, BT>, BT, 0) !=
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT, PF, BT, RL>, BT, 0) !=
           hipSuccess ||
       cus <= 0 || per_cu <= 0)
     return kSortMaxResident;
@@ -380,7 +392,7 @@ int64_t sort_grid_cap() {
   return cap;
 }
 
-template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads>
+template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads, bool RL = false>
 int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, hipStream_t s) {
   if (n <= 1 || begin_bit >= end_bit) return LHPC_OK;
   constexpr int TILE = IPT * BT;
@@ -388,9 +400,14 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
   // Grid: up to 8 waves of resident blocks, but at least ~3 tiles per block. More, shorter blocks even out
   // the tail of the even-share split (500M keys: 768 blocks 8.94 ms, 6144 blocks 8.16 ms); below ~3 tiles
   // per block the per-block digit-count rows outweigh the gain (100M keys: 8192 blocks 1.89 ms, 30000 2.19).
-  const int64_t res = sort_grid_cap<K, HAS_V, IPT, PF, BT>();
+  const int64_t res = sort_grid_cap<K, HAS_V, IPT, PF, BT, RL>();
   // grid sweep knobs of the tuning build only (tools/explore_sort.py; lhpc_common.hpp tuning_env)
-  static const int64_t waves = tuning_env("LHPC_SORT_WAVES") ? std::max(1, std::atoi(tuning_env("LHPC_SORT_WAVES"))) : 8;
+  // (1024-thread downsweeps hold one block per CU: twice the waves, the same
+  // block count as two 256-thread blocks per CU at 8; 500M keys, same box:
+  // 74.3 / 74.9 / 75.0 G keys/s at 4 / 8 / 16)
+  constexpr int kWavesDefault = BT >= 1024 ? 16 : 8;
+  static const int64_t waves =
+      tuning_env("LHPC_SORT_WAVES") ? std::max(1, std::atoi(tuning_env("LHPC_SORT_WAVES"))) : kWavesDefault;
   int64_t cap = std::min<int64_t>(waves * res, std::max<int64_t>(res, ntiles / 3));
   if (const char *e = tuning_env("LHPC_SORT_BLOCKS")) cap = std::max<int64_t>(1, std::atoll(e));
   int64_t nb = std::min<int64_t>(cap, ntiles);
@@ -412,7 +429,7 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
     hipLaunchKernelGGL((k_radix_upsweep<K, TILE>), dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0, s, kin,
                        n, shift, mask, per, cnt, vec16);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(kSortThreads), 0, s, cnt, static_cast<int>(nb), db);
-    hipLaunchKernelGGL((k_radix_downsweep<K, HAS_V, IPT, PF, BT>), dim3(static_cast<unsigned>(nb)), dim3(BT), 0,
+    hipLaunchKernelGGL((k_radix_downsweep<K, HAS_V, IPT, PF, BT, RL>), dim3(static_cast<unsigned>(nb)), dim3(BT), 0,
                        s, kin, kout, vin, vout, n, shift, mask, per, cnt, db);
     std::swap(kin, kout);
     if (HAS_V) std::swap(vin, vout);
@@ -630,7 +647,7 @@ int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *r
 using namespace lhpc;
 
 namespace {
-template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads>
+template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads, bool RL = false>
 int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, int on_device, void *stream) {
   constexpr int KB = static_cast<int>(sizeof(K) * 8);
   if (n < 0 || (!keys && n > 0) || (HAS_V && !vals && n > 0) || begin_bit < 0 || end_bit > KB ||
@@ -639,13 +656,13 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
   if (n >= (int64_t{1} << 32)) return LHPC_ERR_UNSUPPORTED;  // 32-bit ranks
   RocTxRange rx("lhpc_radix_sort");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (on_device) return radix_sort_dev<K, HAS_V, IPT, PF, BT>(keys, vals, n, begin_bit, end_bit, s);
+  if (on_device) return radix_sort_dev<K, HAS_V, IPT, PF, BT, RL>(keys, vals, n, begin_bit, end_bit, s);
   HostStage dk, dv;
   LHPC_HIP_TRY(dk.alloc(static_cast<size_t>(n) * sizeof(K)));
   if (HAS_V) LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(n) * 4));
   LHPC_HIP_TRY(hipMemcpy(dk.p, keys, static_cast<size_t>(n) * sizeof(K), hipMemcpyHostToDevice));
   if (HAS_V) LHPC_HIP_TRY(hipMemcpy(dv.p, vals, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice));
-  LHPC_TRY((radix_sort_dev<K, HAS_V, IPT, PF, BT>(static_cast<K *>(dk.p), static_cast<uint32_t *>(dv.p), n, begin_bit,
+  LHPC_TRY((radix_sort_dev<K, HAS_V, IPT, PF, BT, RL>(static_cast<K *>(dk.p), static_cast<uint32_t *>(dv.p), n, begin_bit,
                                           end_bit, s)));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
   LHPC_HIP_TRY(hipMemcpy(keys, dk.p, static_cast<size_t>(n) * sizeof(K), hipMemcpyDeviceToHost));
@@ -678,7 +695,11 @@ extern "C" int lhpc_radix_sort_u32(uint32_t *keys, int64_t n, int begin_bit, int
 extern "C" int lhpc_radix_sort_pairs_u32(uint32_t *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit,
                                          int on_device, void *stream) {
   try {
+#ifdef LHPC_SORT_P32_VARIANT  // A/B builds
+    return sort_entry<uint32_t, true, LHPC_SORT_P32_VARIANT>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+#else
     return sort_entry<uint32_t, true, 32, false>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+#endif
   } LHPC_ABI_CATCH
 }
 
