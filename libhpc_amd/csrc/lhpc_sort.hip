@@ -13,10 +13,10 @@
 //  * per 8-bit pass: upsweep (per-block digit histogram, block-major counts),
 //    scan (one workgroup per digit: per-block exclusive prefixes + digit
 //    totals), downsweep;
-//  * even-share grid sized to the resident downsweep blocks (CUs × blocks per
-//    CU, ≤ 2048): each block walks its own run of TILE-key sub-tiles (8192
-//    keys) in order (keys-only: the next sub-tile's keys load under the
-//    current one's work), so the per-block histogram table stays ≤ 2 MB;
+//  * even-share grid of 8–16 × the resident downsweep blocks: each block
+//    walks its own run of TILE-key sub-tiles in order (u32 keys and pairs:
+//    16384 keys per 1024-thread block, one block per CU; u64 pairs: 8192 per
+//    256 threads), so the per-block histogram table stays small;
 //  * downsweep ranks stably inside a sub-tile with a wave64 match-any
 //    (8 ballots per key → peer mask; rank = popcount(peers & lanes below)),
 //    per-wave running digit counters in LDS, then reorders the sub-tile in
@@ -192,11 +192,7 @@ __device__ __forceinline__ uint64_t match_any8(uint32_t d) {
 // without bounds checks; one barrier fewer per sub-tile than reading two
 // offset tables (C2-sized sort, same box, three runs each: 9.04 → 8.91 ms).
 // BT threads per block (NW = BT / 64 waves); threads t < 256 own digit t.
-// RL: the keys are not held across the digit scan — the rank loads them,
-// the reorder loads them again (L2 hits: the block read them one scan
-// earlier) together with the values, so IPT keys per thread fit the 128
-// VGPRs a 1024-thread block allows.
-template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads, bool RL = false>
+template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads>
 __global__ __launch_bounds__(BT) void k_radix_downsweep(
     const K *__restrict__ kin, K *__restrict__ kout, const uint32_t *__restrict__ vin, uint32_t *__restrict__ vout,
     int64_t n, int shift, uint32_t mask, int64_t per_block, const uint32_t *__restrict__ counts,
@@ -205,7 +201,6 @@ __global__ __launch_bounds__(BT) void k_radix_downsweep(
   constexpr int WSEG = IPT * kWave;
   constexpr int NW = BT / kWave;
   static_assert(BT % 256 == 0, "threads t < 256 own the digits");
-  static_assert(!(RL && PF), "a reloading downsweep prefetches nothing");
   static_assert(TILE <= 65536, "16-bit ranks");
   __shared__ K sk[TILE];
   __shared__ uint32_t sv[HAS_V ? TILE : 1];
@@ -226,28 +221,22 @@ __global__ __launch_bounds__(BT) void k_radix_downsweep(
   const int64_t last = std::min<int64_t>(ntiles, first + per_block);
   K key[IPT];
   uint32_t val[IPT];
-  auto load_tile = [&](int64_t tile, K(&kr)[IPT], uint32_t(&vr)[IPT], bool with_v = true, bool again = false) {
+  auto load_tile = [&](int64_t tile, K(&kr)[IPT], uint32_t(&vr)[IPT]) {
     const int64_t base = tile * TILE;
-    const K *kb = kin;
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (again) asm volatile("" : "+s"(kb));  // a real second load, not the first one's registers
-#endif
-    const K *ks = kb + base + w * WSEG + lane;
+    const K *ks = kin + base + w * WSEG + lane;
     const uint32_t *vs = HAS_V ? vin + base + w * WSEG + lane : nullptr;
     if (base + TILE <= n) {
 #pragma unroll
       for (int i = 0; i < IPT; ++i) {
         kr[i] = ks[i * kWave];
-        if constexpr (HAS_V)
-          if (with_v) vr[i] = vs[i * kWave];
+        if constexpr (HAS_V) vr[i] = vs[i * kWave];
       }
     } else {
       const int valid = static_cast<int>(n - base) - (w * WSEG + lane);
 #pragma unroll
       for (int i = 0; i < IPT; ++i) {
         kr[i] = i * kWave < valid ? ks[i * kWave] : ~K(0);  // pad: max digit, ranked after every real key
-        if constexpr (HAS_V)
-          if (with_v) vr[i] = i * kWave < valid ? vs[i * kWave] : 0u;
+        if constexpr (HAS_V) vr[i] = i * kWave < valid ? vs[i * kWave] : 0u;
       }
     }
   };
@@ -264,7 +253,7 @@ __global__ __launch_bounds__(BT) void k_radix_downsweep(
     if constexpr (PF) {
       if (tile + 1 < last) load_tile(tile + 1, nkey, nval);
     } else {
-      load_tile(tile, key, val, !RL);
+      load_tile(tile, key, val);
     }
     // ranks inside the sub-tile (< 65536) two per register
     uint32_t loc[(IPT + 1) / 2];
@@ -302,7 +291,6 @@ __global__ __launch_bounds__(BT) void k_radix_downsweep(
       gb += tot;
     }
     __syncthreads();
-    if constexpr (RL) load_tile(tile, key, val, true, true);
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const uint32_t p = wcnt[w][digit_of(key[i], shift, mask)] + (i & 1 ? loc[i / 2] >> 16 : loc[i / 2] & 0xFFFFu);
@@ -371,7 +359,7 @@ struct HostStage {
 // resident downsweep blocks on the current device (CUs × blocks per CU),
 // cached per kernel and device (relaxed atomics: racing threads compute the
 // same value)
-template <typename K, bool HAS_V, int IPT, bool PF, int BT, bool RL>
+template <typename K, bool HAS_V, int IPT, bool PF, int BT>
 int64_t sort_grid_cap() {
   static std::atomic<int64_t> cache[64];
   int dev = 0;
@@ -383,7 +371,7 @@ int64_t sort_grid_cap() {
   }
   int cus = 0, per_cu = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT, PF, BT, RL>, BT, 0) !=
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT, PF, BT>, BT, 0) !=
           hipSuccess ||
       cus <= 0 || per_cu <= 0)
     return kSortMaxResident;
@@ -392,7 +380,7 @@ int64_t sort_grid_cap() {
   return cap;
 }
 
-template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads, bool RL = false>
+template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads>
 int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, hipStream_t s) {
   if (n <= 1 || begin_bit >= end_bit) return LHPC_OK;
   constexpr int TILE = IPT * BT;
@@ -400,7 +388,7 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
   // Grid: up to 8 waves of resident blocks, but at least ~3 tiles per block. More, shorter blocks even out
   // the tail of the even-share split (500M keys: 768 blocks 8.94 ms, 6144 blocks 8.16 ms); below ~3 tiles
   // per block the per-block digit-count rows outweigh the gain (100M keys: 8192 blocks 1.89 ms, 30000 2.19).
-  const int64_t res = sort_grid_cap<K, HAS_V, IPT, PF, BT, RL>();
+  const int64_t res = sort_grid_cap<K, HAS_V, IPT, PF, BT>();
   // grid sweep knobs of the tuning build only (tools/explore_sort.py; lhpc_common.hpp tuning_env)
   // (1024-thread downsweeps hold one block per CU: twice the waves, the same
   // block count as two 256-thread blocks per CU at 8; 500M keys, same box:
@@ -429,7 +417,7 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
     hipLaunchKernelGGL((k_radix_upsweep<K, TILE>), dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0, s, kin,
                        n, shift, mask, per, cnt, vec16);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(kSortThreads), 0, s, cnt, static_cast<int>(nb), db);
-    hipLaunchKernelGGL((k_radix_downsweep<K, HAS_V, IPT, PF, BT, RL>), dim3(static_cast<unsigned>(nb)), dim3(BT), 0,
+    hipLaunchKernelGGL((k_radix_downsweep<K, HAS_V, IPT, PF, BT>), dim3(static_cast<unsigned>(nb)), dim3(BT), 0,
                        s, kin, kout, vin, vout, n, shift, mask, per, cnt, db);
     std::swap(kin, kout);
     if (HAS_V) std::swap(vin, vout);
@@ -614,7 +602,11 @@ int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *r
   if (nnz > 0) {
     hipLaunchKernelGGL((k_coo_keys<kBits>), dim3(g), dim3(256), 0, s, rows, cols,
                        reinterpret_cast<const uint32_t *>(vals), nnz, n_rows, n_cols, cb, kp, ip, bad);
+#ifdef LHPC_SORT_P64_VARIANT  // A/B builds
+    LHPC_TRY((radix_sort_dev<uint64_t, true, LHPC_SORT_P64_VARIANT>(kp, ip, nnz, 0, cb + rb, s)));
+#else
     LHPC_TRY((radix_sort_dev<uint64_t, true, 32, false>(kp, ip, nnz, 0, cb + rb, s)));
+#endif
     hipLaunchKernelGGL(k_coo_heads, dim3(g), dim3(256), 0, s, kp, nnz, hp);
     LHPC_TRY(exclusive_scan_u32(hp, pp, nnz, gp, s));
     hipLaunchKernelGGL((k_coo_emit<T, kBits>), dim3(g), dim3(256), 0, s, kp, ip, hp, pp, nnz, cb, vals, col_out,
@@ -647,7 +639,7 @@ int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *r
 using namespace lhpc;
 
 namespace {
-template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads, bool RL = false>
+template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads>
 int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, int on_device, void *stream) {
   constexpr int KB = static_cast<int>(sizeof(K) * 8);
   if (n < 0 || (!keys && n > 0) || (HAS_V && !vals && n > 0) || begin_bit < 0 || end_bit > KB ||
@@ -656,13 +648,13 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
   if (n >= (int64_t{1} << 32)) return LHPC_ERR_UNSUPPORTED;  // 32-bit ranks
   RocTxRange rx("lhpc_radix_sort");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (on_device) return radix_sort_dev<K, HAS_V, IPT, PF, BT, RL>(keys, vals, n, begin_bit, end_bit, s);
+  if (on_device) return radix_sort_dev<K, HAS_V, IPT, PF, BT>(keys, vals, n, begin_bit, end_bit, s);
   HostStage dk, dv;
   LHPC_HIP_TRY(dk.alloc(static_cast<size_t>(n) * sizeof(K)));
   if (HAS_V) LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(n) * 4));
   LHPC_HIP_TRY(hipMemcpy(dk.p, keys, static_cast<size_t>(n) * sizeof(K), hipMemcpyHostToDevice));
   if (HAS_V) LHPC_HIP_TRY(hipMemcpy(dv.p, vals, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice));
-  LHPC_TRY((radix_sort_dev<K, HAS_V, IPT, PF, BT, RL>(static_cast<K *>(dk.p), static_cast<uint32_t *>(dv.p), n, begin_bit,
+  LHPC_TRY((radix_sort_dev<K, HAS_V, IPT, PF, BT>(static_cast<K *>(dk.p), static_cast<uint32_t *>(dv.p), n, begin_bit,
                                           end_bit, s)));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
   LHPC_HIP_TRY(hipMemcpy(keys, dk.p, static_cast<size_t>(n) * sizeof(K), hipMemcpyDeviceToHost));
@@ -671,7 +663,17 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
 }
 }  // namespace
 
-// keys-only: 8192-key sub-tiles (32 keys per thread, 246 VGPRs, 2 waves per
+// keys-only and 32-bit pairs (round 6): 16384-key sub-tiles as 1024-thread
+// blocks of 16 keys per thread without the prefetch (126 VGPRs: 4 waves per
+// SIMD, one block per CU) — digit runs of ≈ 64 keys and twice the waves of
+// the 256-thread 8192-key kernel (246 VGPRs, 2 per SIMD).  Same box, two runs
+// each (profiles/r06/ab_sort2): 500M keys 65.9 → 74.9 G keys/s (75.0 with 16
+// grid waves, the default here); 12288 / 20480-key sub-tiles 70.7 / 74.9;
+// 16384 keys as 512 threads × 32 (2 per SIMD) 68.7; keys reloaded after the
+// digit scan instead of held (24576-key sub-tiles) 74.9, 32768 spilled: 59.5.
+// 150M 32-bit pairs 4.17 → 3.50 ms; 64-bit pairs as 1024 × 8 unchanged
+// (8.71 → 8.71 ms), so they keep the kernel below.
+// Round 3: 8192-key sub-tiles (32 keys per thread, 246 VGPRs, 2 waves per
 // SIMD): digit runs twice as long, so the scatter writes whole 128-B lines,
 // and half the per-sub-tile scans and barriers per key — same box, three runs
 // each, 500M keys 8.92 → 7.68 ms against 4096-key sub-tiles (16384-key
@@ -687,7 +689,7 @@ extern "C" int lhpc_radix_sort_u32(uint32_t *keys, int64_t n, int begin_bit, int
 #ifdef LHPC_SORT_KEYS_VARIANT  // A/B builds: IPT, PF, BT of the keys-only downsweep
     return sort_entry<uint32_t, false, LHPC_SORT_KEYS_VARIANT>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
 #else
-    return sort_entry<uint32_t, false, 32>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
+    return sort_entry<uint32_t, false, 16, false, 1024>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
 #endif
   } LHPC_ABI_CATCH
 }
@@ -698,7 +700,7 @@ extern "C" int lhpc_radix_sort_pairs_u32(uint32_t *keys, uint32_t *vals, int64_t
 #ifdef LHPC_SORT_P32_VARIANT  // A/B builds
     return sort_entry<uint32_t, true, LHPC_SORT_P32_VARIANT>(keys, vals, n, begin_bit, end_bit, on_device, stream);
 #else
-    return sort_entry<uint32_t, true, 32, false>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+    return sort_entry<uint32_t, true, 16, false, 1024>(keys, vals, n, begin_bit, end_bit, on_device, stream);
 #endif
   } LHPC_ABI_CATCH
 }
@@ -706,7 +708,11 @@ extern "C" int lhpc_radix_sort_pairs_u32(uint32_t *keys, uint32_t *vals, int64_t
 extern "C" int lhpc_radix_sort_pairs_u64(uint64_t *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit,
                                          int on_device, void *stream) {
   try {
+#ifdef LHPC_SORT_P64_VARIANT  // A/B builds
+    return sort_entry<uint64_t, true, LHPC_SORT_P64_VARIANT>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+#else
     return sort_entry<uint64_t, true, 32, false>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+#endif
   } LHPC_ABI_CATCH
 }
 

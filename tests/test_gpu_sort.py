@@ -8,7 +8,8 @@ from tests import _support as S
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [0, 1, 2, 63, 64, 65, 4095, 4096, 4097, 8191, 8192, 8193, 100_003, (1 << 20) + 7]
+SIZES = [0, 1, 2, 63, 64, 65, 4095, 4096, 4097, 8191, 8192, 8193, 16383, 16384, 16385, 3 * 16384 + 5, 100_003,
+         (1 << 20) + 7]  # sub-tiles: 16384 keys (u32 keys / pairs), 8192 (u64 pairs)
 
 
 def _dev(gpu, a):
@@ -95,6 +96,20 @@ def test_sort_u32_bit_range(lhpc, gpu, begin, end):
     kt, vt = _dev(gpu, keys.view(np.int32)), _dev(gpu, vals.view(np.int32))
     lhpc.radix_sort_pairs(kt, vt, begin, end)
     wk, wv = S.sort_oracle(keys, vals, begin, end)
+    assert np.array_equal(_u32_view(kt), wk) and np.array_equal(_u32_view(vt), wv)
+
+
+@pytest.mark.parametrize("n", [1, 65, 16383, 16384, 16385, 3 * 16384 + 5, 300_001])
+def test_sort_pairs_u32_stable(lhpc, gpu, n):
+    """32-bit pairs across the 16384-key sub-tile boundaries, a third of the
+    keys equal (stability is observable through the values)."""
+    rng = np.random.default_rng(0x9A1 + n)
+    keys = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    keys[::3] = keys[0]
+    vals = np.arange(n, dtype=np.uint32)
+    kt, vt = _dev(gpu, keys.view(np.int32)), _dev(gpu, vals.view(np.int32))
+    lhpc.radix_sort_pairs(kt, vt, 0, 32)
+    wk, wv = S.sort_oracle(keys, vals, 0, 32)
     assert np.array_equal(_u32_view(kt), wk) and np.array_equal(_u32_view(vt), wv)
 
 
