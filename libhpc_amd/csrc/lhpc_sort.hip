@@ -192,7 +192,10 @@ __device__ __forceinline__ uint64_t match_any8(uint32_t d) {
 // without bounds checks; one barrier fewer per sub-tile than reading two
 // offset tables (C2-sized sort, same box, three runs each: 9.04 → 8.91 ms).
 // BT threads per block (NW = BT / 64 waves); threads t < 256 own digit t.
-template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads>
+// SR (pairs): keys and values reordered one after the other through the one
+// LDS buffer (the keys' global positions kept in registers), so a sub-tile
+// of 8-B keys needs TILE × 8 B of LDS instead of TILE × 12.
+template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads, bool SR = false>
 __global__ __launch_bounds__(BT) void k_radix_downsweep(
     const K *__restrict__ kin, K *__restrict__ kout, const uint32_t *__restrict__ vin, uint32_t *__restrict__ vout,
     int64_t n, int shift, uint32_t mask, int64_t per_block, const uint32_t *__restrict__ counts,
@@ -203,7 +206,8 @@ __global__ __launch_bounds__(BT) void k_radix_downsweep(
   static_assert(BT % 256 == 0, "threads t < 256 own the digits");
   static_assert(TILE <= 65536, "16-bit ranks");
   __shared__ K sk[TILE];
-  __shared__ uint32_t sv[HAS_V ? TILE : 1];
+  static_assert(!SR || (HAS_V && !PF), "SR: pairs without the prefetch");
+  __shared__ uint32_t sv[HAS_V && !SR ? TILE : 1];
   __shared__ uint32_t wcnt[NW][256];
   __shared__ uint32_t gofs[256];
   __shared__ uint32_t tmp[NW];
@@ -295,7 +299,7 @@ __global__ __launch_bounds__(BT) void k_radix_downsweep(
     for (int i = 0; i < IPT; ++i) {
       const uint32_t p = wcnt[w][digit_of(key[i], shift, mask)] + (i & 1 ? loc[i / 2] >> 16 : loc[i / 2] & 0xFFFFu);
       sk[p] = key[i];
-      if constexpr (HAS_V) sv[p] = val[i];
+      if constexpr (HAS_V && !SR) sv[p] = val[i];
     }
     __syncthreads();
     // (no barrier after the scatter: the next sub-tile writes sk, the wcnt
@@ -303,6 +307,28 @@ __global__ __launch_bounds__(BT) void k_radix_downsweep(
     // passes once its scatter is done; each wave clears only its own counter
     // row, which only it reads before that barrier)
     const int valid = full ? TILE : static_cast<int>(n - base);
+    if constexpr (SR) {
+      uint32_t gk[IPT];
+#pragma unroll
+      for (int k = 0; k < IPT; ++k) {
+        const int p = t + BT * k;
+        const K kk = sk[p];
+        gk[k] = gofs[digit_of(kk, shift, mask)] + static_cast<uint32_t>(p);
+        if (full || p < valid) kout[gk[k]] = kk;
+      }
+      __syncthreads();  // every key is out of sk: the values take its place
+      uint32_t *svr = reinterpret_cast<uint32_t *>(sk);
+#pragma unroll
+      for (int i = 0; i < IPT; ++i)
+        svr[wcnt[w][digit_of(key[i], shift, mask)] + (i & 1 ? loc[i / 2] >> 16 : loc[i / 2] & 0xFFFFu)] = val[i];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < IPT; ++k) {
+        const int p = t + BT * k;
+        if (full || p < valid) vout[gk[k]] = svr[p];
+      }
+      continue;
+    }
 #pragma unroll 8  // (a full unroll holds IPT 64-bit store addresses)
     for (int k = 0; k < IPT; ++k) {
       const int p = t + BT * k;
@@ -359,7 +385,7 @@ struct HostStage {
 // resident downsweep blocks on the current device (CUs × blocks per CU),
 // cached per kernel and device (relaxed atomics: racing threads compute the
 // same value)
-template <typename K, bool HAS_V, int IPT, bool PF, int BT>
+template <typename K, bool HAS_V, int IPT, bool PF, int BT, bool SR>
 int64_t sort_grid_cap() {
   static std::atomic<int64_t> cache[64];
   int dev = 0;
@@ -371,7 +397,7 @@ int64_t sort_grid_cap() {
   }
   int cus = 0, per_cu = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT, PF, BT>, BT, 0) !=
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_radix_downsweep<K, HAS_V, IPT, PF, BT, SR>, BT, 0) !=
           hipSuccess ||
       cus <= 0 || per_cu <= 0)
     return kSortMaxResident;
@@ -380,7 +406,7 @@ int64_t sort_grid_cap() {
   return cap;
 }
 
-template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads>
+template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads, bool SR = false>
 int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, hipStream_t s) {
   if (n <= 1 || begin_bit >= end_bit) return LHPC_OK;
   constexpr int TILE = IPT * BT;
@@ -388,7 +414,7 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
   // Grid: up to 8 waves of resident blocks, but at least ~3 tiles per block. More, shorter blocks even out
   // the tail of the even-share split (500M keys: 768 blocks 8.94 ms, 6144 blocks 8.16 ms); below ~3 tiles
   // per block the per-block digit-count rows outweigh the gain (100M keys: 8192 blocks 1.89 ms, 30000 2.19).
-  const int64_t res = sort_grid_cap<K, HAS_V, IPT, PF, BT>();
+  const int64_t res = sort_grid_cap<K, HAS_V, IPT, PF, BT, SR>();
   // grid sweep knobs of the tuning build only (tools/explore_sort.py; lhpc_common.hpp tuning_env)
   // (1024-thread downsweeps hold one block per CU: twice the waves, the same
   // block count as two 256-thread blocks per CU at 8; 500M keys, same box:
@@ -417,7 +443,7 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
     hipLaunchKernelGGL((k_radix_upsweep<K, TILE>), dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0, s, kin,
                        n, shift, mask, per, cnt, vec16);
     hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(kSortThreads), 0, s, cnt, static_cast<int>(nb), db);
-    hipLaunchKernelGGL((k_radix_downsweep<K, HAS_V, IPT, PF, BT>), dim3(static_cast<unsigned>(nb)), dim3(BT), 0,
+    hipLaunchKernelGGL((k_radix_downsweep<K, HAS_V, IPT, PF, BT, SR>), dim3(static_cast<unsigned>(nb)), dim3(BT), 0,
                        s, kin, kout, vin, vout, n, shift, mask, per, cnt, db);
     std::swap(kin, kout);
     if (HAS_V) std::swap(vin, vout);
@@ -639,7 +665,7 @@ int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *r
 using namespace lhpc;
 
 namespace {
-template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads>
+template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads, bool SR = false>
 int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, int on_device, void *stream) {
   constexpr int KB = static_cast<int>(sizeof(K) * 8);
   if (n < 0 || (!keys && n > 0) || (HAS_V && !vals && n > 0) || begin_bit < 0 || end_bit > KB ||
@@ -648,13 +674,13 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
   if (n >= (int64_t{1} << 32)) return LHPC_ERR_UNSUPPORTED;  // 32-bit ranks
   RocTxRange rx("lhpc_radix_sort");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (on_device) return radix_sort_dev<K, HAS_V, IPT, PF, BT>(keys, vals, n, begin_bit, end_bit, s);
+  if (on_device) return radix_sort_dev<K, HAS_V, IPT, PF, BT, SR>(keys, vals, n, begin_bit, end_bit, s);
   HostStage dk, dv;
   LHPC_HIP_TRY(dk.alloc(static_cast<size_t>(n) * sizeof(K)));
   if (HAS_V) LHPC_HIP_TRY(dv.alloc(static_cast<size_t>(n) * 4));
   LHPC_HIP_TRY(hipMemcpy(dk.p, keys, static_cast<size_t>(n) * sizeof(K), hipMemcpyHostToDevice));
   if (HAS_V) LHPC_HIP_TRY(hipMemcpy(dv.p, vals, static_cast<size_t>(n) * 4, hipMemcpyHostToDevice));
-  LHPC_TRY((radix_sort_dev<K, HAS_V, IPT, PF, BT>(static_cast<K *>(dk.p), static_cast<uint32_t *>(dv.p), n, begin_bit,
+  LHPC_TRY((radix_sort_dev<K, HAS_V, IPT, PF, BT, SR>(static_cast<K *>(dk.p), static_cast<uint32_t *>(dv.p), n, begin_bit,
                                           end_bit, s)));
   LHPC_HIP_TRY(hipStreamSynchronize(s));
   LHPC_HIP_TRY(hipMemcpy(keys, dk.p, static_cast<size_t>(n) * sizeof(K), hipMemcpyDeviceToHost));
