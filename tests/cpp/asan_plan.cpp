@@ -129,6 +129,36 @@ void check_xtile(const Csr &a, bool iperm, const std::vector<int64_t> &splits, i
         for (int64_t g = xt.segoff[xt.rchunk[k] * S + s]; g < xt.segoff[xt.rchunk[k + 1] * S + s]; ++g)
           CHECK(by[static_cast<size_t>(g)] >= 0 && by[static_cast<size_t>(g)] <= k);
   }
+  // phase-A tables (xtile_phase_tables): position f of chunk c's segment
+  // concatenation lies in non-empty segment rank = term + popcount(w1 &
+  // lanes below f % 64) of its 64-position batch, and its xg entry is at
+  // base_ne[rank] + f — the stream (or, after xtile_ring_pieces, the ring)
+  // position of that entry
+  auto check_phase_tables = [&]() {
+    std::vector<uint32_t> bt;
+    std::vector<int32_t> bne;
+    lhpc::xtile_phase_tables(xt, bt, bne);
+    const int64_t NBT = xt.M / 64, K = static_cast<int64_t>(xt.rchunk.size()) - 1;
+    CHECK(static_cast<int64_t>(bt.size()) == std::max<int64_t>(C, 1) * NBT * 4);
+    for (int64_t c = 0; c < C; ++c) {
+      int64_t k = 0;
+      while (k + 1 < K && xt.rchunk[k + 1] <= c) ++k;
+      int64_t flat = 0;
+      for (int64_t s = 0; s < S; ++s) {
+        const int64_t a = xt.segoff[c * S + s], len = xt.segoff[(c + 1) * S + s] - a;
+        const int64_t d = xt.rdelta.empty() ? 0 : xt.rdelta[static_cast<size_t>(k * S + s)];
+        for (int64_t j = 0; j < len; ++j, ++flat) {
+          const int64_t b = flat / 64, l = flat % 64;
+          const uint32_t *t4 = bt.data() + (c * NBT + b) * 4;
+          const uint64_t w1 = (static_cast<uint64_t>(t4[1]) << 32) | t4[0];
+          const int64_t rank = static_cast<int32_t>(t4[2]) + __builtin_popcountll(w1 & ((uint64_t{1} << l) - 1));
+          CHECK(rank >= 0 && rank < S);
+          if (rank >= 0 && rank < S) CHECK(bne[static_cast<size_t>(c * S + rank)] + flat == a + j + d);
+        }
+      }
+    }
+  };
+  if (iperm && unit == 1) check_phase_tables();
   // the xg ring (xtile_ring_pieces): per range, emulate the gather (every
   // piece writes stream entry g at ring position g + delta, plus its flagged
   // shared groups) on a ring wiped before the range, then the reduce's reads
@@ -172,6 +202,7 @@ void check_xtile(const Csr &a, bool iperm, const std::vector<int64_t> &splits, i
             CHECK(start + j >= 0 && start + j < L && ring[static_cast<size_t>(start + j)] == xt.segoff[c * S + s] + j);
         }
     }
+    check_phase_tables();  // with the ring deltas
   }
   // the transposed val/iperm streams and the gather-block permutation
   std::vector<int32_t> vbase;
