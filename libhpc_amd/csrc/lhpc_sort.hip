@@ -28,6 +28,7 @@
 #include <atomic>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "lhpc_common.hpp"
 
@@ -193,10 +194,17 @@ __device__ __forceinline__ uint64_t match_any8(uint32_t d) {
 // offset tables (C2-sized sort, same box, three runs each: 9.04 → 8.91 ms).
 // BT threads per block (NW = BT / 64 waves); threads t < 256 own digit t.
 // SR (pairs): keys and values reordered one after the other through the one
-// LDS buffer (the keys' global positions kept in registers), so a sub-tile
-// of 8-B keys needs TILE × 8 B of LDS instead of TILE × 12.
+// LDS buffer, so a sub-tile of 8-B keys needs TILE × 8 B of LDS instead of
+// TILE × 12; each sorted position's digit is kept as a byte (dg) for the
+// values' scatter, and the wave counters are 16-bit (< TILE ≤ 65536) to make
+// room for it.
+#ifdef LHPC_SORT_WPE  // A/B builds: waves per SIMD the downsweep's registers must allow
+#define LHPC_SORT_DS_ATTR __attribute__((amdgpu_waves_per_eu(LHPC_SORT_WPE)))
+#else
+#define LHPC_SORT_DS_ATTR
+#endif
 template <typename K, bool HAS_V, int IPT, bool PF = true, int BT = kSortThreads, bool SR = false>
-__global__ __launch_bounds__(BT) void k_radix_downsweep(
+__global__ __launch_bounds__(BT) LHPC_SORT_DS_ATTR void k_radix_downsweep(
     const K *__restrict__ kin, K *__restrict__ kout, const uint32_t *__restrict__ vin, uint32_t *__restrict__ vout,
     int64_t n, int shift, uint32_t mask, int64_t per_block, const uint32_t *__restrict__ counts,
     const uint32_t *__restrict__ totals) {
@@ -208,12 +216,12 @@ __global__ __launch_bounds__(BT) void k_radix_downsweep(
   __shared__ K sk[TILE];
   static_assert(!SR || (HAS_V && !PF), "SR: pairs without the prefetch");
   __shared__ uint32_t sv[HAS_V && !SR ? TILE : 1];
-  __shared__ uint32_t wcnt[NW][256];
+  __shared__ std::conditional_t<SR, uint16_t, uint32_t> wcnt[NW][256];
+  __shared__ uint8_t dg[SR ? TILE : 1];
   __shared__ uint32_t gofs[256];
   __shared__ uint32_t tmp[NW];
   const int t = threadIdx.x, w = t / kWave, lane = t & (kWave - 1);
   const bool own = BT == 256 || t < 256;  // thread t owns digit t
-  const uint64_t lt_mask = (uint64_t{1} << lane) - 1;
   uint32_t gb;  // thread t: global output position of digit t's next key
   {
     uint32_t all;
@@ -225,22 +233,26 @@ __global__ __launch_bounds__(BT) void k_radix_downsweep(
   const int64_t last = std::min<int64_t>(ntiles, first + per_block);
   K key[IPT];
   uint32_t val[IPT];
-  auto load_tile = [&](int64_t tile, K(&kr)[IPT], uint32_t(&vr)[IPT]) {
+  // SR loads the values only after the keys' reorder (they are not live
+  // through the rank and the scan)
+  auto load_tile = [&](int64_t tile, K(&kr)[IPT], uint32_t(&vr)[IPT], bool keys = true, bool vals = !SR) {
     const int64_t base = tile * TILE;
     const K *ks = kin + base + w * WSEG + lane;
     const uint32_t *vs = HAS_V ? vin + base + w * WSEG + lane : nullptr;
     if (base + TILE <= n) {
 #pragma unroll
       for (int i = 0; i < IPT; ++i) {
-        kr[i] = ks[i * kWave];
-        if constexpr (HAS_V) vr[i] = vs[i * kWave];
+        if (keys) kr[i] = ks[i * kWave];
+        if constexpr (HAS_V)
+          if (vals) vr[i] = vs[i * kWave];
       }
     } else {
       const int valid = static_cast<int>(n - base) - (w * WSEG + lane);
 #pragma unroll
       for (int i = 0; i < IPT; ++i) {
-        kr[i] = i * kWave < valid ? ks[i * kWave] : ~K(0);  // pad: max digit, ranked after every real key
-        if constexpr (HAS_V) vr[i] = i * kWave < valid ? vs[i * kWave] : 0u;
+        if (keys) kr[i] = i * kWave < valid ? ks[i * kWave] : ~K(0);  // pad: max digit, ranked after every real key
+        if constexpr (HAS_V)
+          if (vals) vr[i] = i * kWave < valid ? vs[i * kWave] : 0u;
       }
     }
   };
@@ -265,11 +277,14 @@ __global__ __launch_bounds__(BT) void k_radix_downsweep(
     for (int i = 0; i < IPT; ++i) {
       const uint32_t d = digit_of(key[i], shift, mask);
       const uint64_t peers = match_any8(d);
-      const uint64_t below = peers & lt_mask;
+      // peers in lanes below mine: mbcnt against the hardware lane mask (no
+      // per-lane mask register)
+      const uint32_t nbelow = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(peers >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(peers), 0u));
       const uint32_t before = wcnt[w][d];
-      const uint32_t r = before + static_cast<uint32_t>(__popcll(below));
+      const uint32_t r = before + nbelow;
       loc[i / 2] = i & 1 ? loc[i / 2] | r << 16 : r;
-      if (below == 0) wcnt[w][d] = before + static_cast<uint32_t>(__popcll(peers));
+      if (nbelow == 0) wcnt[w][d] = before + static_cast<uint32_t>(__popcll(peers));
     }
     __syncthreads();
     // per digit t: wave prefix + sub-tile start into the wave counters, and
@@ -300,6 +315,10 @@ __global__ __launch_bounds__(BT) void k_radix_downsweep(
       const uint32_t p = wcnt[w][digit_of(key[i], shift, mask)] + (i & 1 ? loc[i / 2] >> 16 : loc[i / 2] & 0xFFFFu);
       sk[p] = key[i];
       if constexpr (HAS_V && !SR) sv[p] = val[i];
+      if constexpr (SR) {
+        loc[i / 2] = i & 1 ? (loc[i / 2] & 0xFFFFu) | p << 16 : (loc[i / 2] & 0xFFFF0000u) | p;
+        dg[p] = static_cast<uint8_t>(digit_of(key[i], shift, mask));
+      }
     }
     __syncthreads();
     // (no barrier after the scatter: the next sub-tile writes sk, the wcnt
@@ -308,24 +327,21 @@ __global__ __launch_bounds__(BT) void k_radix_downsweep(
     // row, which only it reads before that barrier)
     const int valid = full ? TILE : static_cast<int>(n - base);
     if constexpr (SR) {
-      uint32_t gk[IPT];
-#pragma unroll
+#pragma unroll 8
       for (int k = 0; k < IPT; ++k) {
         const int p = t + BT * k;
-        const K kk = sk[p];
-        gk[k] = gofs[digit_of(kk, shift, mask)] + static_cast<uint32_t>(p);
-        if (full || p < valid) kout[gk[k]] = kk;
+        if (full || p < valid) kout[gofs[dg[p]] + static_cast<uint32_t>(p)] = sk[p];
       }
+      load_tile(tile, key, val, false, true);  // (L2 hits: under the barrier)
       __syncthreads();  // every key is out of sk: the values take its place
       uint32_t *svr = reinterpret_cast<uint32_t *>(sk);
 #pragma unroll
-      for (int i = 0; i < IPT; ++i)
-        svr[wcnt[w][digit_of(key[i], shift, mask)] + (i & 1 ? loc[i / 2] >> 16 : loc[i / 2] & 0xFFFFu)] = val[i];
+      for (int i = 0; i < IPT; ++i) svr[i & 1 ? loc[i / 2] >> 16 : loc[i / 2] & 0xFFFFu] = val[i];
       __syncthreads();
-#pragma unroll
+#pragma unroll 8
       for (int k = 0; k < IPT; ++k) {
         const int p = t + BT * k;
-        if (full || p < valid) vout[gk[k]] = svr[p];
+        if (full || p < valid) vout[gofs[dg[p]] + static_cast<uint32_t>(p)] = svr[p];
       }
       continue;
     }
