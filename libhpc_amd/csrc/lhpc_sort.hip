@@ -13,10 +13,10 @@
 //  * per 8-bit pass: upsweep (per-block digit histogram, block-major counts),
 //    scan (one workgroup per digit: per-block exclusive prefixes + digit
 //    totals), downsweep;
-//  * even-share grid of 8–16 × the resident downsweep blocks: each block
-//    walks its own run of TILE-key sub-tiles in order (u32 keys and pairs:
-//    16384 keys per 1024-thread block, one block per CU; u64 pairs: 8192 per
-//    256 threads), so the per-block histogram table stays small;
+//  * even-share grid of 16 × the resident downsweep blocks: each block walks
+//    its own run of TILE-key sub-tiles in order (1024-thread blocks, one per
+//    CU: 24576 u32 keys, 16384 u32 or u64 pairs), so the per-block histogram
+//    table stays small;
 //  * downsweep ranks stably inside a sub-tile with a wave64 match-any
 //    (8 ballots per key → peer mask; rank = popcount(peers & lanes below)),
 //    per-wave running digit counters in LDS, then reorders the sub-tile in
@@ -647,7 +647,7 @@ int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *r
 #ifdef LHPC_SORT_P64_VARIANT  // A/B builds
     LHPC_TRY((radix_sort_dev<uint64_t, true, LHPC_SORT_P64_VARIANT>(kp, ip, nnz, 0, cb + rb, s)));
 #else
-    LHPC_TRY((radix_sort_dev<uint64_t, true, 32, false>(kp, ip, nnz, 0, cb + rb, s)));
+    LHPC_TRY((radix_sort_dev<uint64_t, true, 16, false, 1024, true>(kp, ip, nnz, 0, cb + rb, s)));
 #endif
     hipLaunchKernelGGL(k_coo_heads, dim3(g), dim3(256), 0, s, kp, nnz, hp);
     LHPC_TRY(exclusive_scan_u32(hp, pp, nnz, gp, s));
@@ -705,16 +705,17 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
 }
 }  // namespace
 
-// keys-only and 32-bit pairs (round 6): 16384-key sub-tiles as 1024-thread
-// blocks of 16 keys per thread without the prefetch (126 VGPRs: 4 waves per
-// SIMD, one block per CU) — digit runs of ≈ 64 keys and twice the waves of
-// the 256-thread 8192-key kernel (246 VGPRs, 2 per SIMD).  Same box, two runs
-// each (profiles/r06/ab_sort2): 500M keys 65.9 → 74.9 G keys/s (75.0 with 16
-// grid waves, the default here); 12288 / 20480-key sub-tiles 70.7 / 74.9;
-// 16384 keys as 512 threads × 32 (2 per SIMD) 68.7; keys reloaded after the
-// digit scan instead of held (24576-key sub-tiles) 74.9, 32768 spilled: 59.5.
-// 150M 32-bit pairs 4.17 → 3.50 ms; 64-bit pairs as 1024 × 8 unchanged
-// (8.71 → 8.71 ms), so they keep the kernel below.
+// Round 6 (profiles/r06/ab_sort2): 1024-thread blocks without the prefetch,
+// one block per CU at 4 waves per SIMD (≤ 128 VGPRs) — twice the waves of
+// the 256-thread 8192-key kernel (246 VGPRs, 2 per SIMD) and longer digit
+// runs.  Keys only: 24576-key sub-tiles (24 keys per thread, 126 VGPRs once
+// the lanes-below count is an mbcnt; 28 / 32 keys spill), 500M keys 65.9 →
+// 75.0 (16384) → 78.6 G keys/s; 12288 keys 70.7; 16384 as 512 × 32 at 2 per
+// SIMD 68.7; 12288 as 512 × 24, two blocks per CU, 71.3.  32-bit pairs:
+// 16384 (values in their own LDS array), 150M pairs 4.17 → 3.53 ms.  64-bit
+// pairs: 16384 with the split reorder (SR: keys, then values, through one
+// 128 KB buffer; 127 VGPRs), 150M pairs over 47 bits 8.70 → 7.77 ms, COO→CSR
+// 12.0 → 11.8 ms; 12288 with SR 8.07; 8192 as 1024 × 8 8.75 (no gain).
 // Round 3: 8192-key sub-tiles (32 keys per thread, 246 VGPRs, 2 waves per
 // SIMD): digit runs twice as long, so the scatter writes whole 128-B lines,
 // and half the per-sub-tile scans and barriers per key — same box, three runs
@@ -731,7 +732,7 @@ extern "C" int lhpc_radix_sort_u32(uint32_t *keys, int64_t n, int begin_bit, int
 #ifdef LHPC_SORT_KEYS_VARIANT  // A/B builds: IPT, PF, BT of the keys-only downsweep
     return sort_entry<uint32_t, false, LHPC_SORT_KEYS_VARIANT>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
 #else
-    return sort_entry<uint32_t, false, 16, false, 1024>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
+    return sort_entry<uint32_t, false, 24, false, 1024>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
 #endif
   } LHPC_ABI_CATCH
 }
@@ -753,7 +754,7 @@ extern "C" int lhpc_radix_sort_pairs_u64(uint64_t *keys, uint32_t *vals, int64_t
 #ifdef LHPC_SORT_P64_VARIANT  // A/B builds
     return sort_entry<uint64_t, true, LHPC_SORT_P64_VARIANT>(keys, vals, n, begin_bit, end_bit, on_device, stream);
 #else
-    return sort_entry<uint64_t, true, 32, false>(keys, vals, n, begin_bit, end_bit, on_device, stream);
+    return sort_entry<uint64_t, true, 16, false, 1024, true>(keys, vals, n, begin_bit, end_bit, on_device, stream);
 #endif
   } LHPC_ABI_CATCH
 }

@@ -8,8 +8,8 @@ from tests import _support as S
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [0, 1, 2, 63, 64, 65, 4095, 4096, 4097, 8191, 8192, 8193, 16383, 16384, 16385, 3 * 16384 + 5, 100_003,
-         (1 << 20) + 7]  # sub-tiles: 16384 keys (u32 keys / pairs), 8192 (u64 pairs)
+SIZES = [0, 1, 2, 63, 64, 65, 4095, 4096, 4097, 8191, 8192, 8193, 16383, 16384, 16385, 24575, 24576, 24577,
+         3 * 24576 + 5, 100_003, (1 << 20) + 7]  # sub-tiles: 24576 u32 keys, 16384 u32 / u64 pairs
 
 
 def _dev(gpu, a):
@@ -113,7 +113,7 @@ def test_sort_pairs_u32_stable(lhpc, gpu, n):
     assert np.array_equal(_u32_view(kt), wk) and np.array_equal(_u32_view(vt), wv)
 
 
-@pytest.mark.parametrize("n", [1, 65, 4097, 70_001, 1 << 20])
+@pytest.mark.parametrize("n", [1, 65, 4097, 16383, 16384, 16385, 3 * 16384 + 5, 70_001, 1 << 20])
 @pytest.mark.parametrize("bits", [64, 47, 20])
 def test_sort_pairs_u64_stable(lhpc, gpu, n, bits):
     import torch
