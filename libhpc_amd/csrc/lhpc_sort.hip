@@ -73,17 +73,23 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const K *__restr
   int64_t i = b0;
   if constexpr (sizeof(K) == 4) {
     typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-    constexpr int STEP = 16 * kSortThreads;
+// (eight 16-B loads per thread and step: 366 → 363 µs per 500M-key pass,
+// two : 375; profiles/r06/ab_sort2/upsweep)
+#ifndef LHPC_SORT_UP_Q  // A/B builds: 16-B loads per thread and step
+#define LHPC_SORT_UP_Q 8
+#endif
+    constexpr int UQ = LHPC_SORT_UP_Q;
+    constexpr int STEP = 4 * UQ * kSortThreads;
     // vec16 (host: keys 16-B aligned; a caller's key pointer may be 4-B
     // aligned only, e.g. a slice t[1:]): b0 is a multiple of TILE, so every
     // 16-B load is aligned; otherwise the scalar loop below takes every key
     for (; vec16 && i + STEP <= b1; i += STEP) {
       const u32x4v *p = reinterpret_cast<const u32x4v *>(keys + i) + t;
-      u32x4v v[4];
+      u32x4v v[UQ];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = __builtin_nontemporal_load(p + q * kSortThreads);
+      for (int q = 0; q < UQ; ++q) v[q] = __builtin_nontemporal_load(p + q * kSortThreads);
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < UQ; ++q)
 #pragma unroll
         for (int e = 0; e < 4; ++e) atomicAdd(&hist[w][digit_of(static_cast<K>(v[q][e]), shift, mask)], 1u);
     }
