@@ -55,8 +55,8 @@ __device__ __forceinline__ uint32_t digit_of(K k, int shift, uint32_t mask) {
 }
 
 // Upsweep: digit histogram of the block's sub-tiles → counts[b·256 + d].
-// 32-bit keys stream as four 16-B non-temporal loads per thread and step (64
-// B per lane in flight; round 5, same box: 350.6 → 327.6 µs per 500M-key
+// 32-bit keys stream as LHPC_SORT_UP_Q 16-B non-temporal loads per thread and
+// step (round 5, four: same box, 350.6 → 327.6 µs per 500M-key
 // pass — 16 sub-histograms per block against LDS-atomic conflicts, and no
 // atomics at all (timing only), both left it at 342–350 µs, so the key
 // stream, not the atomics, bounds it); 64-bit keys four 8-B loads.
