@@ -11,7 +11,7 @@
     defined(LHPC_XT_XG_CPOL) || defined(LHPC_XT_SEGHI) || defined(LHPC_XT_STAMPS) ||   \
     defined(LHPC_SELL_NO_SHFL) || defined(LHPC_SCRATCH_DEFAULT_POOL) || defined(LHPC_SORT_KEYS_VARIANT) || \
     defined(LHPC_SORT_P32_VARIANT) || defined(LHPC_SORT_P64_VARIANT) || defined(LHPC_SORT_WPE) || \
-    defined(LHPC_SORT_UP_Q) || defined(LHPC_AB_BUILD)
+    defined(LHPC_SORT_UP_Q) || defined(LHPC_SORT_SCAN_TRAIL) || defined(LHPC_AB_BUILD)
 #define LHPC_TAG_AB 1
 #endif
 #include <hip/hip_runtime.h>
