@@ -1163,7 +1163,7 @@ int build_t(lhpc_spmv_plan *p, RowPtrView rp, const int32_t *col_idx, const void
   // plans without aligned segments, G = 1.  Default for fp64 only — same box,
   // two runs each: C3 reduce 89.9 → 85.3 µs per range (its 16-wave scan was
   // 2.3K of 27.8K cycles per chunk), C2 88.1 → 89.4 µs (the tables' extra
-  // 1 KB per chunk outweighs an 8-wave scan)
+  // 2 KB per chunk outweigh an 8-wave scan)
   const bool pre = ip && !al && xtile_g<T>(xt.S) == 1 &&
                    (o.xtile_pretable == 2 || (o.xtile_pretable == 0 && sizeof(T) == 8));
   p->xt_pre = pre ? 1 : 0;
