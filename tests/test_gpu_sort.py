@@ -223,6 +223,32 @@ def test_sort_u32_reference_100m(lhpc, gpu):
     assert np.array_equal(got, keys)
 
 
+def test_sort_u32_past_2_31(lhpc, gpu):
+    """2^31 + 4099 keys (8.6 GB): sub-tile bases and output positions past
+    2^31 (int64 tile offsets, u32 positions up to 2^32).  Checked on the
+    device: sorted as unsigned, the same 65536-bin histogram of the top 16
+    bits and the same sum as the input (a permutation), and the last partial
+    sub-tile's keys in place."""
+    import torch
+    n = (1 << 31) + 4099
+    g = torch.Generator(device=gpu)
+    g.manual_seed(0x2E31)
+    t = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device=gpu, generator=g)
+    t[-3:] = torch.tensor([-1, 0, 12345], dtype=torch.int32, device=gpu)  # max, min, a marker in the tail sub-tile
+
+    def summary(x):
+        u = x.to(torch.int64) & 0xFFFFFFFF
+        return torch.bincount(u >> 16, minlength=65536), int(u.sum().item())
+    h0, s0 = summary(t)
+    lhpc.radix_sort(t)
+    torch.cuda.synchronize()
+    h1, s1 = summary(t)
+    assert torch.equal(h0, h1) and s0 == s1
+    u = t.to(torch.int64) & 0xFFFFFFFF
+    assert bool((u[1:] >= u[:-1]).all())
+    assert int(u[0]) == 0 and int(u[-1]) == 0xFFFFFFFF
+
+
 @pytest.mark.parametrize("poison", [0x00, 0xA5, 0xFF])
 def test_coo_to_csr_poisoned_pool(lhpc, gpu, poison):
     """Regression for the round-2 host-path race: the on-device
