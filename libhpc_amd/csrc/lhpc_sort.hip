@@ -486,23 +486,8 @@ int radix_sort_dev(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bi
   return check_launch(s);
 }
 
-// ---------------------------------------------------------------- scan (uint32 → uint32 exclusive)
-constexpr int kScanTile = 4096;  // 256 threads × 16
-
-__global__ __launch_bounds__(kSortThreads) void k_scan_reduce(const uint32_t *__restrict__ in, int64_t n,
-                                                              uint32_t *__restrict__ sums) {
-  __shared__ uint32_t tmp[256];
-  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kScanTile;
-  uint32_t s = 0;
-  for (int k = 0; k < kScanTile / kSortThreads; ++k) {
-    const int64_t i = b0 + k * kSortThreads + threadIdx.x;
-    if (i < n) s += in[i];
-  }
-  uint32_t total;
-  (void)block_exscan256(s, tmp, total);
-  if (threadIdx.x == 0) sums[blockIdx.x] = total;
-}
-
+// ---------------------------------------------------------------- tile-sum scan
+// per-tile sums → exclusive prefix in place (one workgroup), total to *grand
 __global__ __launch_bounds__(kSortThreads) void k_scan_sums(uint32_t *__restrict__ sums, int64_t nb,
                                                             uint32_t *__restrict__ grand) {
   __shared__ uint32_t tmp[256];
@@ -516,55 +501,6 @@ __global__ __launch_bounds__(kSortThreads) void k_scan_sums(uint32_t *__restrict
     carry += total;
   }
   if (threadIdx.x == 0 && grand) *grand = carry;
-}
-
-__global__ __launch_bounds__(kSortThreads) void k_scan_apply(const uint32_t *__restrict__ in, int64_t n,
-                                                             const uint32_t *__restrict__ sums,
-                                                             uint32_t *__restrict__ out) {
-  __shared__ uint32_t tmp[256];
-  __shared__ uint32_t tile[kScanTile + kScanTile / 32];  // +1 word per 32: conflict-free row reads
-  constexpr int E = kScanTile / kSortThreads;            // each thread scans 16 consecutive elements
-  const int t = threadIdx.x;
-  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kScanTile;
-  auto at = [](int i) { return i + (i >> 5); };
-#pragma unroll
-  for (int k = 0; k < E; ++k) {  // coalesced load
-    const int i = k * kSortThreads + t;
-    tile[at(i)] = b0 + i < n ? in[b0 + i] : 0u;
-  }
-  __syncthreads();
-  uint32_t v[E], s = 0;
-#pragma unroll
-  for (int k = 0; k < E; ++k) {
-    v[k] = tile[at(t * E + k)];
-    s += v[k];
-  }
-  uint32_t total;
-  uint32_t run = sums[blockIdx.x] + block_exscan256(s, tmp, total);
-#pragma unroll
-  for (int k = 0; k < E; ++k) {
-    tile[at(t * E + k)] = run;
-    run += v[k];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < E; ++k) {  // coalesced store
-    const int i = k * kSortThreads + t;
-    if (b0 + i < n) out[b0 + i] = tile[at(i)];
-  }
-}
-
-// exclusive scan in → out (may alias), grand total to *grand (device) if non-null
-int exclusive_scan_u32(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *grand, hipStream_t s) {
-  if (n <= 0) return LHPC_OK;
-  const int64_t nb = (n + kScanTile - 1) / kScanTile;
-  DevBuf sums;
-  LHPC_HIP_TRY(sums.alloc(static_cast<size_t>(nb) * 4, s));
-  uint32_t *sp = static_cast<uint32_t *>(sums.p);
-  hipLaunchKernelGGL(k_scan_reduce, dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0, s, in, n, sp);
-  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kSortThreads), 0, s, sp, nb, grand);
-  hipLaunchKernelGGL(k_scan_apply, dim3(static_cast<unsigned>(nb)), dim3(kSortThreads), 0, s, in, n, sp, out);
-  return check_launch(s);
 }
 
 // ---------------------------------------------------------------- COO → CSR
@@ -587,45 +523,92 @@ __global__ void k_coo_keys(const int32_t *__restrict__ rows, const int32_t *__re
   pay[i] = PAY_BITS ? vbits[i] : static_cast<uint32_t>(i);
 }
 
-__global__ void k_coo_heads(const uint64_t *__restrict__ keys, int64_t nnz, uint32_t *__restrict__ head) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < nnz) head[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+// Fused merge (round 6): after the sort, one pass counts the run heads per
+// 4096-entry tile (head = key differs from the previous entry's), the tile
+// counts are scanned, and one pass per tile recomputes its heads, gives each
+// its merged position, sums its run in input order, writes col / val and
+// fills the row_ptr entries of the rows that start there — instead of
+// heads → scan (reduce, apply) → emit → row_ptr as five passes over the keys.
+// Entries are striped over the block (entry b0 + e·256 + t, every load
+// coalesced); a head's position within its 64-entry wave row is an mbcnt of
+// the row's head ballot, the 64 row counts of the tile are scanned in LDS.
+constexpr int kCooTile = 4096;  // 16 rows of 256 entries
+constexpr int kCooE = kCooTile / kSortThreads;
+
+__global__ __launch_bounds__(kSortThreads) void k_coo_count(const uint64_t *__restrict__ keys, int64_t nnz,
+                                                            uint32_t *__restrict__ sums) {
+  __shared__ uint32_t tmp[256];
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kCooTile;
+  uint32_t c = 0;
+#pragma unroll
+  for (int e = 0; e < kCooE; ++e) {
+    const int64_t i = b0 + e * kSortThreads + threadIdx.x;
+    if (i < nnz) c += (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+  }
+  uint32_t total;
+  (void)block_exscan256(c, tmp, total);
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
 
-// one thread per run head: col, and the run's values summed in input order
-template <typename T, bool PAY_BITS>
-__global__ void k_coo_emit(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ pay,
-                           const uint32_t *__restrict__ head, const uint32_t *__restrict__ pos, int64_t nnz,
-                           int col_bits, const T *__restrict__ vals, int32_t *__restrict__ col_out,
-                           T *__restrict__ val_out) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= nnz || !head[i]) return;
+template <typename T, bool PAY_BITS, typename O>
+__global__ __launch_bounds__(kSortThreads) void k_coo_finish(const uint64_t *__restrict__ keys,
+                                                             const uint32_t *__restrict__ pay, int64_t nnz,
+                                                             int64_t n_rows, int col_bits,
+                                                             const uint32_t *__restrict__ sums,
+                                                             const uint32_t *__restrict__ grand, const T *__restrict__ vals,
+                                                             int32_t *__restrict__ col_out, T *__restrict__ val_out,
+                                                             O *__restrict__ row_ptr) {
+  __shared__ uint32_t rc[kCooE * 4];  // head count of each 64-entry wave row, then its exclusive prefix
   auto value = [&](int64_t j) -> T {
     if constexpr (PAY_BITS) return __builtin_bit_cast(T, pay[j]);
     else return vals[pay[j]];
   };
-  const uint64_t k = keys[i];
-  T s = value(i);
-  for (int64_t j = i + 1; j < nnz && keys[j] == k; ++j) s = s + value(j);
-  const uint32_t p = pos[i];
-  col_out[p] = static_cast<int32_t>(k & ((uint64_t{1} << col_bits) - 1));
-  val_out[p] = s;
-}
-
-// row_ptr from the merged entries: thread per sorted index i that starts a new
-// row (a run head whose row differs from the previous entry's) fills
-// row_ptr[prev_row+1 .. row] = pos[i]; the last one also fills the tail.
-template <typename O>
-__global__ void k_coo_rowptr(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ pos,
-                             const uint32_t *__restrict__ grand, int64_t nnz, int64_t n_rows, int col_bits,
-                             O *__restrict__ row_ptr) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i > nnz) return;
-  const int64_t row = i < nnz ? static_cast<int64_t>(keys[i] >> col_bits) : n_rows;
-  const int64_t prev = i > 0 ? static_cast<int64_t>(keys[i - 1] >> col_bits) : -1;
-  if (row == prev) return;
-  const O p = static_cast<O>(i < nnz ? pos[i] : *grand);
-  for (int64_t r = prev + 1; r <= row; ++r) row_ptr[r] = p;
+  const int t = threadIdx.x, w = t / kWave, lane = t & (kWave - 1);
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kCooTile;
+  uint64_t k[kCooE];
+  uint32_t hm = 0, mb[kCooE / 4] = {};  // head bits; the mbcnt of each row, one byte per row
+#pragma unroll
+  for (int e = 0; e < kCooE; ++e) {
+    const int64_t i = b0 + e * kSortThreads + t;
+    const bool ok = i < nnz;
+    k[e] = ok ? keys[i] : 0;
+    const bool h = ok && (i == 0 || k[e] != keys[i - 1]);
+    const uint64_t bal = __ballot(h);
+    const uint32_t m = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bal >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bal), 0u));
+    mb[e / 4] |= m << (8 * (e % 4));
+    hm |= (h ? 1u : 0u) << e;
+    if (lane == 0) rc[e * 4 + w] = static_cast<uint32_t>(__popcll(bal));
+  }
+  __syncthreads();
+  if (w == 0) {  // the 64 row counts in entry order (row e, wave w) → exclusive prefix
+    const uint32_t v = rc[lane];
+    const uint32_t inc = static_cast<uint32_t>(wave_incl_scan(static_cast<int>(v)));
+    rc[lane] = inc - v;
+  }
+  __syncthreads();
+  const uint32_t base = sums[blockIdx.x];
+  const uint64_t cmask = (uint64_t{1} << col_bits) - 1;
+#pragma unroll
+  for (int e = 0; e < kCooE; ++e) {
+    const int64_t i = b0 + e * kSortThreads + t;
+    if (i >= nnz) break;
+    if (hm >> e & 1u) {
+      const uint32_t pos = base + rc[e * 4 + w] + (mb[e / 4] >> (8 * (e % 4)) & 0xFFu);
+      T sv = value(i);
+      for (int64_t j = i + 1; j < nnz && keys[j] == k[e]; ++j) sv = sv + value(j);
+      col_out[pos] = static_cast<int32_t>(k[e] & cmask);
+      val_out[pos] = sv;
+      // rows (previous entry's row, this row] start at this merged entry
+      const int64_t row = static_cast<int64_t>(k[e] >> col_bits);
+      const int64_t prow = i > 0 ? static_cast<int64_t>(keys[i - 1] >> col_bits) : -1;
+      for (int64_t r = prow + 1; r <= row; ++r) row_ptr[r] = static_cast<O>(pos);
+    }
+    if (i == nnz - 1) {  // the rows after the last entry's
+      const O g = static_cast<O>(*grand);
+      for (int64_t r = static_cast<int64_t>(k[e] >> col_bits) + 1; r <= n_rows; ++r) row_ptr[r] = g;
+    }
+  }
 }
 
 int bits_for(int64_t v) {  // bits to hold values in [0, v)
@@ -640,16 +623,15 @@ int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *r
                    int64_t *nnz_out, hipStream_t s) {
   const int cb = std::max(1, bits_for(n_cols)), rb = std::max(1, bits_for(n_rows));
   if (cb + rb > 64) return LHPC_ERR_UNSUPPORTED;
-  DevBuf keys, idx, head, pos, flag, grand;
+  const int64_t nt = (nnz + kCooTile - 1) / kCooTile;  // merge tiles
+  DevBuf keys, idx, tsum, flag, grand;
   LHPC_HIP_TRY(keys.alloc(static_cast<size_t>(nnz) * 8, s));
   LHPC_HIP_TRY(idx.alloc(static_cast<size_t>(nnz) * 4, s));
-  LHPC_HIP_TRY(head.alloc(static_cast<size_t>(nnz) * 4, s));
-  LHPC_HIP_TRY(pos.alloc(static_cast<size_t>(nnz) * 4, s));
+  LHPC_HIP_TRY(tsum.alloc(static_cast<size_t>(std::max<int64_t>(nt, 1)) * 4, s));
   LHPC_HIP_TRY(flag.alloc(8, s));
   LHPC_HIP_TRY(grand.alloc(8, s));
   uint64_t *kp = static_cast<uint64_t *>(keys.p);
-  uint32_t *ip = static_cast<uint32_t *>(idx.p), *hp = static_cast<uint32_t *>(head.p),
-           *pp = static_cast<uint32_t *>(pos.p);
+  uint32_t *ip = static_cast<uint32_t *>(idx.p), *tp = static_cast<uint32_t *>(tsum.p);
   int *bad = static_cast<int *>(flag.p);
   uint32_t *gp = static_cast<uint32_t *>(grand.p);
   LHPC_HIP_TRY(hipMemsetAsync(bad, 0, 8, s));
@@ -664,18 +646,18 @@ int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *r
 #else
     LHPC_TRY((radix_sort_dev<uint64_t, true, 16, false, 1024, true>(kp, ip, nnz, 0, cb + rb, s)));
 #endif
-    hipLaunchKernelGGL(k_coo_heads, dim3(g), dim3(256), 0, s, kp, nnz, hp);
-    LHPC_TRY(exclusive_scan_u32(hp, pp, nnz, gp, s));
-    hipLaunchKernelGGL((k_coo_emit<T, kBits>), dim3(g), dim3(256), 0, s, kp, ip, hp, pp, nnz, cb, vals, col_out,
-                       val_out);
+    const dim3 tg(static_cast<unsigned>(nt));
+    hipLaunchKernelGGL(k_coo_count, tg, dim3(kSortThreads), 0, s, kp, nnz, tp);
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kSortThreads), 0, s, tp, nt, gp);
+    if (row_ptr_bits == 64)
+      hipLaunchKernelGGL((k_coo_finish<T, kBits, int64_t>), tg, dim3(kSortThreads), 0, s, kp, ip, nnz, n_rows, cb, tp,
+                         gp, vals, col_out, val_out, static_cast<int64_t *>(row_ptr));
+    else
+      hipLaunchKernelGGL((k_coo_finish<T, kBits, int32_t>), tg, dim3(kSortThreads), 0, s, kp, ip, nnz, n_rows, cb, tp,
+                         gp, vals, col_out, val_out, static_cast<int32_t *>(row_ptr));
+  } else {  // no entries: row_ptr all zeros
+    LHPC_HIP_TRY(hipMemsetAsync(row_ptr, 0, static_cast<size_t>(n_rows + 1) * (row_ptr_bits / 8), s));
   }
-  const unsigned gr = static_cast<unsigned>((nnz + 1 + 255) / 256);
-  if (row_ptr_bits == 64)
-    hipLaunchKernelGGL((k_coo_rowptr<int64_t>), dim3(gr), dim3(256), 0, s, kp, pp, gp, nnz, n_rows, cb,
-                       static_cast<int64_t *>(row_ptr));
-  else
-    hipLaunchKernelGGL((k_coo_rowptr<int32_t>), dim3(gr), dim3(256), 0, s, kp, pp, gp, nnz, n_rows, cb,
-                       static_cast<int32_t *>(row_ptr));
   LHPC_TRY(check_launch(s));
   // the two status words are read after the stream has drained, with
   // synchronous copies: no asynchronous copy touches pageable host memory
