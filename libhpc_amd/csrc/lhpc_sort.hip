@@ -519,21 +519,48 @@ __global__ __launch_bounds__(kSortThreads) void k_scan_sums(uint32_t *__restrict
 // ---------------------------------------------------------------- COO → CSR
 // key = row << col_bits | col; payload = the f32 value's bits (carried through the sort, so no
 // permutation gather) or, for f64 values, the input index.
-template <bool PAY_BITS>
+// VEC (rows, cols and values 16-B aligned): four entries per thread, 16-B
+// loads and stores (150M entries: 817 → 611 µs against one entry per thread)
+template <bool PAY_BITS, bool VEC>
 __global__ void k_coo_keys(const int32_t *__restrict__ rows, const int32_t *__restrict__ cols,
                            const uint32_t *__restrict__ vbits, int64_t nnz, int64_t n_rows, int64_t n_cols,
                            int col_bits, uint64_t *__restrict__ keys, uint32_t *__restrict__ pay,
                            int *__restrict__ bad) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= nnz) return;
-  const int32_t r = rows[i], c = cols[i];
-  if (r < 0 || r >= n_rows || c < 0 || c >= n_cols) {
-    atomicOr(bad, 1);
-    keys[i] = 0;
+  auto key_of = [&](int32_t r, int32_t c) -> uint64_t {
+    if (r < 0 || r >= n_rows || c < 0 || c >= n_cols) {
+      atomicOr(bad, 1);
+      return 0;
+    }
+    return (static_cast<uint64_t>(r) << col_bits) | static_cast<uint64_t>(c);
+  };
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if constexpr (VEC) {
+    typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    const int64_t i = 4 * t;
+    if (i + 4 <= nnz) {
+      const i32x4 r = __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(rows) + t);
+      const i32x4 c = __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(cols) + t);
+      u64x2 k0 = {key_of(r.x, c.x), key_of(r.y, c.y)}, k1 = {key_of(r.z, c.z), key_of(r.w, c.w)};
+      reinterpret_cast<u64x2 *>(keys)[2 * t] = k0;
+      reinterpret_cast<u64x2 *>(keys)[2 * t + 1] = k1;
+      u32x4 pv;
+      if constexpr (PAY_BITS) pv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(vbits) + t);
+      else pv = u32x4{static_cast<uint32_t>(i), static_cast<uint32_t>(i + 1), static_cast<uint32_t>(i + 2),
+                      static_cast<uint32_t>(i + 3)};
+      reinterpret_cast<u32x4 *>(pay)[t] = pv;
+    } else {
+      for (int64_t j = i; j < nnz; ++j) {
+        keys[j] = key_of(rows[j], cols[j]);
+        pay[j] = PAY_BITS ? vbits[j] : static_cast<uint32_t>(j);
+      }
+    }
   } else {
-    keys[i] = (static_cast<uint64_t>(r) << col_bits) | static_cast<uint64_t>(c);
+    if (t >= nnz) return;
+    keys[t] = key_of(rows[t], cols[t]);
+    pay[t] = PAY_BITS ? vbits[t] : static_cast<uint32_t>(t);
   }
-  pay[i] = PAY_BITS ? vbits[i] : static_cast<uint32_t>(i);
 }
 
 // Fused merge (round 6): after the sort, one pass counts the run heads per
@@ -652,8 +679,14 @@ int coo_to_csr_dev(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *r
   const unsigned g = static_cast<unsigned>((std::max<int64_t>(nnz, 1) + 255) / 256);
   constexpr bool kBits = sizeof(T) == 4;
   if (nnz > 0) {
-    hipLaunchKernelGGL((k_coo_keys<kBits>), dim3(g), dim3(256), 0, s, rows, cols,
-                       reinterpret_cast<const uint32_t *>(vals), nnz, n_rows, n_cols, cb, kp, ip, bad);
+    const bool vec = ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(cols) |
+                       (kBits ? reinterpret_cast<uintptr_t>(vals) : 0)) & 15u) == 0;
+    if (vec)
+      hipLaunchKernelGGL((k_coo_keys<kBits, true>), dim3(static_cast<unsigned>((nnz + 1023) / 1024)), dim3(256), 0,
+                         s, rows, cols, reinterpret_cast<const uint32_t *>(vals), nnz, n_rows, n_cols, cb, kp, ip, bad);
+    else
+      hipLaunchKernelGGL((k_coo_keys<kBits, false>), dim3(g), dim3(256), 0, s, rows, cols,
+                         reinterpret_cast<const uint32_t *>(vals), nnz, n_rows, n_cols, cb, kp, ip, bad);
 #ifdef LHPC_SORT_P64_VARIANT  // A/B builds
     LHPC_TRY((radix_sort_dev<uint64_t, true, LHPC_SORT_P64_VARIANT>(kp, ip, nnz, 0, cb + rb, s)));
 #else

@@ -192,6 +192,24 @@ def test_coo_to_csr_vs_oracle(lhpc, gpu, dt, shape):
     assert np.array_equal(d[1].cpu().numpy(), want[1]) and np.array_equal(d[2].cpu().numpy(), want[2])
 
 
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("off", [0, 1, 2])
+def test_coo_to_csr_device_offsets(lhpc, gpu, dt, off):
+    """Device COO arrays starting 0 / 4 / 8 B past a 16-B boundary (slices
+    t[off:]): the key pass takes four entries per thread with 16-B loads only
+    when rows, cols and (fp32) values are all 16-B aligned, one per thread
+    otherwise; the same CSR either way, nnz not a multiple of 4."""
+    n_rows, n_cols, nnz = 3000, 5000, 40_003
+    rows, cols, vals = _coo(n_rows, n_cols, nnz, 0xC00 + off, dt)
+    want = S.coo_oracle(n_rows, n_cols, rows, cols, vals)
+
+    def pad(a):
+        return _dev(gpu, np.concatenate([np.zeros(off, a.dtype), a]))[off:]
+    d = lhpc.coo_to_csr(n_rows, n_cols, pad(rows), pad(cols), pad(vals))
+    assert np.array_equal(d[0].cpu().numpy(), want[0])
+    assert np.array_equal(d[1].cpu().numpy(), want[1]) and np.array_equal(d[2].cpu().numpy(), want[2])
+
+
 def test_coo_to_csr_feeds_spmv(lhpc, gpu):
     """Round trip: a generated CSR → COO (shuffled) → coo_to_csr gives back the
     same CSR, and the SpMV plan built from it reproduces y."""
