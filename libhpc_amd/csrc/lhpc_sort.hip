@@ -94,6 +94,21 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_upsweep(const K *__restr
         for (int e = 0; e < 4; ++e) atomicAdd(&hist[w][digit_of(static_cast<K>(v[q][e]), shift, mask)], 1u);
     }
   } else {
+    // 64-bit keys: four 16-B non-temporal loads (two keys each) per thread
+    // and step on 16-B aligned keys (round 6: 150M-pair COO sort, 240 → 212
+    // µs per pass against four 8-B loads)
+    typedef uint64_t u64x2v __attribute__((ext_vector_type(2)));
+    constexpr int STEP8 = 8 * kSortThreads;
+    for (; vec16 && i + STEP8 <= b1; i += STEP8) {
+      const u64x2v *p = reinterpret_cast<const u64x2v *>(keys + i) + t;
+      u64x2v v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = __builtin_nontemporal_load(p + q * kSortThreads);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) atomicAdd(&hist[w][digit_of(static_cast<K>(v[q][e]), shift, mask)], 1u);
+    }
     for (; i + 4 * kSortThreads <= b1; i += 4 * kSortThreads) {
       const K k0 = keys[i + t], k1 = keys[i + kSortThreads + t], k2 = keys[i + 2 * kSortThreads + t],
               k3 = keys[i + 3 * kSortThreads + t];

@@ -131,6 +131,24 @@ def test_sort_pairs_u64_stable(lhpc, gpu, n, bits):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("off", [0, 1])
+def test_sort_pairs_u64_offset_pointer(lhpc, gpu, off):
+    """64-bit keys 8 B past a 16-B boundary (a slice t[1:]): the upsweep's
+    16-B loads are used only on 16-B aligned keys, one key per load
+    otherwise; the same stable order either way."""
+    rng = np.random.default_rng(0x64 + off)
+    n = 3 * 16384 + 77
+    keys = rng.integers(0, 1 << 40, size=n, dtype=np.uint64)
+    keys[::5] = keys[1]
+    vals = np.arange(n, dtype=np.uint32)
+    kt = _dev(gpu, np.concatenate([np.zeros(off, np.uint64), keys]).view(np.int64))[off:]
+    vt = _dev(gpu, np.concatenate([np.zeros(off, np.uint32), vals]).view(np.int32))[off:]
+    lhpc.radix_sort_pairs(kt, vt, 0, 40)
+    wk, wv = S.sort_oracle(keys, vals, 0, 40)
+    assert np.array_equal(kt.cpu().numpy().view(np.uint64), wk)
+    assert np.array_equal(vt.cpu().numpy().view(np.uint32), wv)
+
+
 def test_sort_pairs_u64_host_path(lhpc, gpu):
     rng = np.random.default_rng(9)
     keys = rng.integers(0, 1 << 40, size=33_333, dtype=np.uint64)
