@@ -15,7 +15,7 @@
 //    totals), downsweep;
 //  * even-share grid of 16 × the resident downsweep blocks: each block walks
 //    its own run of TILE-key sub-tiles in order (1024-thread blocks, one per
-//    CU: 24576 u32 keys, 16384 u32 or u64 pairs), so the per-block histogram
+//    CU: 20480 u32 keys, 16384 u32 or u64 pairs), so the per-block histogram
 //    table stays small;
 //  * downsweep ranks stably inside a sub-tile with a wave64 match-any
 //    (8 ballots per key → peer mask; rank = popcount(peers & lanes below)),
@@ -766,10 +766,12 @@ int sort_entry(K *keys, uint32_t *vals, int64_t n, int begin_bit, int end_bit, i
 // Round 6 (profiles/r06/ab_sort2): 1024-thread blocks without the prefetch,
 // one block per CU at 4 waves per SIMD (≤ 128 VGPRs) — twice the waves of
 // the 256-thread 8192-key kernel (246 VGPRs, 2 per SIMD) and longer digit
-// runs.  Keys only: 24576-key sub-tiles (24 keys per thread, 126 VGPRs once
-// the lanes-below count is an mbcnt; 28 / 32 keys spill), 500M keys 65.9 →
-// 75.0 (16384) → 78.6 G keys/s; 12288 keys 70.7; 16384 as 512 × 32 at 2 per
-// SIMD 68.7; 12288 as 512 × 24, two blocks per CU, 71.3.  32-bit pairs:
+// runs.  Keys only: 20480-key sub-tiles with the next sub-tile's keys
+// prefetched into registers (20 + 20 keys per thread, 127 VGPRs once the
+// lanes-below count is an mbcnt), 500M keys 65.9 → 75.0 (16384, no
+// prefetch) → 78.6 (24576, no prefetch; 28 / 32 keys spill) → 81.1 G keys/s;
+// 12288 keys 70.7; 16384 as 512 × 32 at 2 per SIMD 68.7; 12288 as 512 × 24,
+// two blocks per CU, 71.3.  32-bit pairs:
 // 16384 (values in their own LDS array), 150M pairs 4.17 → 3.53 ms.  64-bit
 // pairs: 16384 with the split reorder (SR: keys, then values, through one
 // 128 KB buffer; 127 VGPRs), 150M pairs over 47 bits 8.70 → 7.77 ms, COO→CSR
@@ -790,7 +792,7 @@ extern "C" int lhpc_radix_sort_u32(uint32_t *keys, int64_t n, int begin_bit, int
 #ifdef LHPC_SORT_KEYS_VARIANT  // A/B builds: IPT, PF, BT of the keys-only downsweep
     return sort_entry<uint32_t, false, LHPC_SORT_KEYS_VARIANT>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
 #else
-    return sort_entry<uint32_t, false, 24, false, 1024>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
+    return sort_entry<uint32_t, false, 20, true, 1024>(keys, nullptr, n, begin_bit, end_bit, on_device, stream);
 #endif
   } LHPC_ABI_CATCH
 }

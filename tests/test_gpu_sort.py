@@ -8,8 +8,9 @@ from tests import _support as S
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [0, 1, 2, 63, 64, 65, 4095, 4096, 4097, 8191, 8192, 8193, 16383, 16384, 16385, 24575, 24576, 24577,
-         3 * 24576 + 5, 100_003, (1 << 20) + 7]  # sub-tiles: 24576 u32 keys, 16384 u32 / u64 pairs
+SIZES = [0, 1, 2, 63, 64, 65, 4095, 4096, 4097, 8191, 8192, 8193, 16383, 16384, 16385, 20479, 20480, 20481,
+         2 * 20480 + 3, 3 * 20480 + 5, 24575, 24576, 24577, 100_003, (1 << 20) + 7]  # sub-tiles: 20480 u32 keys
+                                                                                   # (prefetched), 16384 pairs
 
 
 def _dev(gpu, a):
